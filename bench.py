@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): in-pod bf16 matmul TFLOPS at 1/2/4/8 MI355X
+(+ notebook cold-start p50 from the native control plane when requested).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
+``torch.distributed.run`` with one rank per GPU (RCCL). Each rank is one notebook pod's GPU running
+the K1 readiness op: a bf16 GEMM C = A @ B^T (8192^3 by default) on the hand-written gfx950 MFMA
+kernel. A "step" = one such GEMM on every GPU. W untimed warmup steps, then exactly K timed steps
+bracketed by barrier + device sync on both sides; the slowest rank's time is used. ``value`` is
+the whole-job aggregate TFLOPS (N x per-GEMM FLOPs / max-rank time). Weak scaling: per-GPU work
+is fixed as N grows. Data: synthetic uniform [-1, 1) bf16 operands (random data, not zeros:
+zero operands inflate MFMA clocks — cdna_hip_programming.md §5.4 rule 25).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+METRIC = "notebook pod cold-start p50 (s) + in-pod bf16 matmul TFLOPS at 1/2/4/8 MI355X"
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--m", type=int, default=8192)
+    p.add_argument("--n", type=int, default=8192)
+    p.add_argument("--k", type=int, default=8192)
+    p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "0")),
+                   help="notebook cold-start runs through the native control plane (rank 0)")
+    p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from kubeflow_rm_amd import ops
+
+    M, N, K = args.m, args.n, args.k
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    a = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    b = (torch.rand(N, K, generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+    # correctness spot-check of this very configuration against a fp32 reference (a few rows)
+    ops.gemm_nt(a, b, out=c)
+    ref = a[:64].float() @ b.float().t()
+    err = (c[:64].float() - ref).abs().max().item()
+    ok = err <= 1e-2 * ref.abs().max().item() + 1e-2
+
+    def step():
+        ops.gemm_nt(a, b, out=c)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = t.item()
+    ms_per_step = dt_max / args.steps * 1e3
+    flops = ops.flops(M, N, K)
+    per_gpu_tflops = flops / (ms_per_step * 1e-3) / 1e12
+    value = per_gpu_tflops * world
+
+    extra = {}
+    if args.compare_torch and rank == 0:
+        for _ in range(5):
+            torch.matmul(a, b.t())
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            torch.matmul(a, b.t())
+        torch.cuda.synchronize(dev)
+        extra["torch_matmul_tflops_per_gpu"] = round(flops * args.steps / (time.perf_counter() - t1) / 1e12, 1)
+
+    if args.coldstart_runs > 0 and rank == 0:
+        try:
+            from kubeflow_rm_amd.bench_coldstart import measure_cold_start
+            cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=1)
+            extra["cold_start_p50_s"] = cs["p50_s"]
+            extra["cold_start_p90_s"] = cs["p90_s"]
+            extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
+        except Exception as e:  # reported, never fatal for the GEMM number
+            extra["cold_start_error"] = f"{type(e).__name__}: {e}"
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "TFLOPS (bf16 GEMM, aggregate over GPUs)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uniform [-1,1) bf16 operands, random-init)",
+            "config": {
+                "model": f"in-pod bf16 matmul HIP smoke (K1 readiness op), C=A@B^T {M}x{N}x{K}",
+                "global_batch": world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+            },
+            "per_gpu_tflops": round(per_gpu_tflops, 2),
+            "kernel": "kfamd gemm_nt_256 (MFMA 16x16x32 bf16, 256x256x64, glds, XCD remap)",
+            "correct": bool(ok),
+            "max_abs_err_vs_fp32": err,
+            **extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,74 @@
+// kfamd_kernels.h — C ABI of the hand-written CDNA4 (gfx950) kernel library.
+//
+// This library is the MI355X compute path of the framework (SURVEY.md §2.7.2, K1–K3):
+//   K1  bf16 GEMM on MFMA (v_mfma_f32_16x16x32_bf16), LDS-tiled, global_load_lds staging
+//   K2  LayerNorm / RMSNorm forward+backward (bf16 I/O, fp32 statistics)
+//   K3  (collectives live in RCCL; see kfamd_readiness.cpp / kubeflow_rm_amd.parallel)
+//
+// It is consumed three ways, all in-tree:
+//   * Python (kubeflow_rm_amd.ops) through ctypes — one HIP runtime shared with torch;
+//   * the native in-pod readiness op (native/readiness) linked directly;
+//   * the bench harness (bench.py) through the Python ops.
+//
+// Every launcher is asynchronous on the given stream and never allocates, syncs or copies,
+// so callers may capture it into a hipGraph (cdna_hip_programming.md §6 G9).
+// Return value: 0 on success, otherwise a negative kfamd_status code (shape/alignment
+// contract violated) or a positive hipError_t from the launch.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum kfamd_status {
+  KFAMD_OK = 0,
+  KFAMD_EINVAL = -1,     // bad shape / null pointer
+  KFAMD_EALIGN = -2,     // pointer or leading dimension not 16-byte aligned for the fast path
+};
+
+// Epilogue activation codes for the fused GEMM epilogue.
+enum kfamd_act { KFAMD_ACT_NONE = 0, KFAMD_ACT_RELU = 1, KFAMD_ACT_GELU_TANH = 2, KFAMD_ACT_SILU = 3 };
+
+// C[b][m][n] = act(alpha * sum_k A[b][m][k] * B[b][n][k] + bias[n]) (+ R[b][m][n])
+//   A: [batch][M][K] row-major (lda, stride_a in elements), K contiguous
+//   B: [batch][N][K] row-major (ldb, stride_b), K contiguous   -> "NT" (== torch F.linear)
+//   C: [batch][M][N] row-major (ldc, stride_c)
+//   bias: optional [N] bf16 (nullptr = none); R: optional residual, same layout as C (ldr/stride_r)
+// Dispatch: the 256x256x64 MFMA tile kernel when M%256==0, N%256==0, K%64==0 and all
+// pointers/leading dims are 16-byte aligned; otherwise the bounds-checked 128x128 kernel.
+int kfamd_gemm_nt_bf16(const void* A, const void* B, void* C, const void* bias, const void* R,
+                       int M, int N, int K, int batch,
+                       long long lda, long long ldb, long long ldc, long long ldr,
+                       long long stride_a, long long stride_b, long long stride_c, long long stride_r,
+                       float alpha, int act, void* stream);
+
+// Force a specific kernel (for tests/bench): variant 0 = auto, 1 = 256x256 fast path, 2 = generic.
+int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* C, const void* bias,
+                               const void* R, int M, int N, int K, int batch,
+                               long long lda, long long ldb, long long ldc, long long ldr,
+                               long long stride_a, long long stride_b, long long stride_c,
+                               long long stride_r, float alpha, int act, void* stream);
+
+// LayerNorm forward over the last dim (hidden). x,y: [rows][hidden] bf16 (row stride = hidden).
+// gamma/beta: [hidden] bf16 (beta may be null). mean/rstd: optional fp32 [rows] (saved for bwd).
+int kfamd_layernorm_fwd_bf16(const void* x, const void* gamma, const void* beta, void* y,
+                             float* mean, float* rstd, int rows, int hidden, float eps, void* stream);
+
+// RMSNorm forward: y = x * rsqrt(mean(x^2)+eps) * gamma. rstd optional.
+int kfamd_rmsnorm_fwd_bf16(const void* x, const void* gamma, void* y, float* rstd,
+                           int rows, int hidden, float eps, void* stream);
+
+// LayerNorm backward. dx: [rows][hidden] bf16. dgamma/dbeta: fp32 [hidden] (fully written).
+// workspace: fp32 scratch of kfamd_layernorm_bwd_workspace(rows, hidden) bytes.
+long long kfamd_layernorm_bwd_workspace(int rows, int hidden);
+int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, const float* mean,
+                             const float* rstd, void* dx, float* dgamma, float* dbeta,
+                             float* workspace, int rows, int hidden, void* stream);
+
+// Library identity (for the loud "native code loaded" check).
+const char* kfamd_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif

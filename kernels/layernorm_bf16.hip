@@ -1,0 +1,340 @@
+// layernorm_bf16.hip — K2: LayerNorm / RMSNorm (bf16 I/O, fp32 statistics) for MI355X (gfx950).
+//
+// SURVEY.md §2.7.2 K2. Memory-bound: the target is the HBM3E roof (~6.3 TB/s achievable).
+//  * Fast path: one 64-lane wave per row, the whole row resident in VGPRs (hidden = 512*VPL,
+//    VPL in {1,2,4,8,16} -> hidden 512..8192), 16-byte bf16x8 loads/stores (Guideline 13),
+//    exact two-pass mean/variance from registers (no re-read of HBM), wave-only reductions
+//    (no LDS, no barriers), 4 rows per 256-thread workgroup -> rows/4 workgroups (>>256 CUs).
+//  * Generic path: one workgroup per row, any hidden size, LDS block reduction.
+//  * Backward: dx per row (same wave-per-row structure), dgamma/dbeta by a column-strip
+//    partial-sum kernel + a finalize kernel (deterministic, no float atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kfamd_kernels.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block reduction for the generic (one workgroup per row) kernels. 256 threads = 4 waves.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t += red[i];
+  return t;
+}
+
+template <int VPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ x,
+                                                    const __bf16* __restrict__ gamma,
+                                                    const __bf16* __restrict__ beta,
+                                                    __bf16* __restrict__ y, float* __restrict__ mean_out,
+                                                    float* __restrict__ rstd_out, int rows, float eps) {
+  constexpr int H = VPL * 512;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;  // wave-uniform; no barriers below
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)row * H);
+  float v[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const bf16x8 t = xr[j * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[j][e] = (float)t[e];
+  }
+  float mean = 0.f;
+  if (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[j][e];
+    mean = wave_sum(s) * (1.f / H);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[j][e] - mean;
+      ss += d * d;
+    }
+  const float rstd = rsqrtf(wave_sum(ss) * (1.f / H) + eps);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+  const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
+  const bf16x8* b8 = reinterpret_cast<const bf16x8*>(beta);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + (long long)row * H);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const bf16x8 g = g8[j * 64 + lane];
+    bf16x8 b;
+    if (!RMS && beta) b = b8[j * 64 + lane];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float r = (v[j][e] - mean) * rstd * (float)g[e];
+      if (!RMS && beta) r += (float)b[e];
+      o[e] = (__bf16)r;
+    }
+    yr[j * 64 + lane] = o;
+  }
+}
+
+template <bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_block(const __bf16* __restrict__ x,
+                                                     const __bf16* __restrict__ gamma,
+                                                     const __bf16* __restrict__ beta,
+                                                     __bf16* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int hidden, float eps) {
+  __shared__ float red[4];
+  const long long row = blockIdx.x;
+  const __bf16* xr = x + row * hidden;
+  float mean = 0.f;
+  if (!RMS) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < hidden; i += 256) s += (float)xr[i];
+    mean = block_sum(s, red) / hidden;
+  }
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < hidden; i += 256) {
+    const float d = (float)xr[i] - mean;
+    ss += d * d;
+  }
+  const float rstd = rsqrtf(block_sum(ss, red) / hidden + eps);
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+  __bf16* yr = y + row * hidden;
+  for (int i = threadIdx.x; i < hidden; i += 256) {
+    float r = ((float)xr[i] - mean) * rstd * (float)gamma[i];
+    if (!RMS && beta) r += (float)beta[i];
+    yr[i] = (__bf16)r;
+  }
+}
+
+// ---- backward: dx ---------------------------------------------------------------------------
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__ dy,
+                                                     const __bf16* __restrict__ x,
+                                                     const __bf16* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     __bf16* __restrict__ dx, int rows) {
+  constexpr int H = VPL * 512;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)row * H);
+  const bf16x8* dyr = reinterpret_cast<const bf16x8*>(dy + (long long)row * H);
+  const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
+  const float mu = mean[row], rs = rstd[row];
+  float xh[VPL][8], gd[VPL][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const bf16x8 xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[j][e] = ((float)xv[e] - mu) * rs;
+      gd[j][e] = (float)dv[e] * (float)gv[e];
+      s1 += gd[j][e] * xh[j][e];
+      s2 += gd[j][e];
+    }
+  }
+  const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
+  bf16x8* dxr = reinterpret_cast<bf16x8*>(dx + (long long)row * H);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
+    dxr[j * 64 + lane] = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_dx_block(const __bf16* __restrict__ dy,
+                                                      const __bf16* __restrict__ x,
+                                                      const __bf16* __restrict__ gamma,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd,
+                                                      __bf16* __restrict__ dx, int hidden) {
+  __shared__ float red[4];
+  const long long row = blockIdx.x;
+  const float mu = mean[row], rs = rstd[row];
+  const __bf16* xr = x + row * hidden;
+  const __bf16* dyr = dy + row * hidden;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < hidden; i += 256) {
+    const float xh = ((float)xr[i] - mu) * rs, g = (float)dyr[i] * (float)gamma[i];
+    s1 += g * xh;
+    s2 += g;
+  }
+  const float c1 = block_sum(s1, red) / hidden;
+  const float c2 = block_sum(s2, red) / hidden;
+  __bf16* dxr = dx + row * hidden;
+  for (int i = threadIdx.x; i < hidden; i += 256) {
+    const float xh = ((float)xr[i] - mu) * rs, g = (float)dyr[i] * (float)gamma[i];
+    dxr[i] = (__bf16)(rs * (g - xh * c1 - c2));
+  }
+}
+
+// ---- backward: dgamma / dbeta partials over row chunks ---------------------------------------
+// Block: 64 column lanes x 4 row lanes; each column lane owns one column of the strip, so a
+// wave reads 64 consecutive bf16 (128 B) of one row per step; partials land in ws[chunk][col].
+constexpr int kColsPerBlock = 64, kRowLanes = 4, kRowsPerChunk = 64;
+
+__global__ __launch_bounds__(256) void ln_bwd_dgb_partial(const __bf16* __restrict__ dy,
+                                                         const __bf16* __restrict__ x,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         float* __restrict__ ws, int rows, int hidden) {
+  __shared__ float sg[kRowLanes][kColsPerBlock], sb[kRowLanes][kColsPerBlock];
+  const int c = blockIdx.x * kColsPerBlock + (threadIdx.x & (kColsPerBlock - 1));
+  const int rl = threadIdx.x / kColsPerBlock;
+  const int chunk = blockIdx.y;
+  const int r0 = chunk * kRowsPerChunk, r1 = min(rows, r0 + kRowsPerChunk);
+  float dg = 0.f, db = 0.f;
+  if (c < hidden) {
+    for (int r = r0 + rl; r < r1; r += kRowLanes) {
+      const float d = (float)dy[(long long)r * hidden + c];
+      const float xh = ((float)x[(long long)r * hidden + c] - mean[r]) * rstd[r];
+      dg += d * xh;
+      db += d;
+    }
+  }
+  sg[rl][threadIdx.x & (kColsPerBlock - 1)] = dg;
+  sb[rl][threadIdx.x & (kColsPerBlock - 1)] = db;
+  __syncthreads();
+  if (rl == 0 && c < hidden) {
+    float tg = 0.f, tb = 0.f;
+#pragma unroll
+    for (int i = 0; i < kRowLanes; ++i) {
+      tg += sg[i][threadIdx.x];
+      tb += sb[i][threadIdx.x];
+    }
+    const long long nch = gridDim.y;
+    ws[(long long)chunk * hidden + c] = tg;
+    ws[(nch + chunk) * (long long)hidden + c] = tb;
+  }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restrict__ ws, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, int nchunks, int hidden) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= hidden) return;
+  float tg = 0.f, tb = 0.f;
+  for (int k = 0; k < nchunks; ++k) {
+    tg += ws[(long long)k * hidden + c];
+    tb += ws[(long long)(nchunks + k) * hidden + c];
+  }
+  if (dgamma) dgamma[c] = tg;
+  if (dbeta) dbeta[c] = tb;
+}
+
+inline bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+inline int vpl_for(int hidden) {
+  switch (hidden) {
+    case 512: return 1;
+    case 1024: return 2;
+    case 2048: return 4;
+    case 4096: return 8;
+    case 8192: return 16;
+    default: return 0;
+  }
+}
+
+template <bool RMS>
+int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
+             int rows, int hidden, float eps, void* stream) {
+  if (!x || !gamma || !y || rows <= 0 || hidden <= 0) return KFAMD_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* xp = static_cast<const __bf16*>(x);
+  const __bf16* gp = static_cast<const __bf16*>(gamma);
+  const __bf16* bp = static_cast<const __bf16*>(beta);
+  __bf16* yp = static_cast<__bf16*>(y);
+  const int vpl = vpl_for(hidden);
+  const bool vec = vpl && a16(x) && a16(gamma) && a16(y) && (!beta || a16(beta));
+  if (vec) {
+    dim3 grid((rows + 3) / 4), block(256);
+    switch (vpl) {
+      case 1: hipLaunchKernelGGL((norm_fwd_wave<1, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 2: hipLaunchKernelGGL((norm_fwd_wave<2, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 4: hipLaunchKernelGGL((norm_fwd_wave<4, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 8: hipLaunchKernelGGL((norm_fwd_wave<8, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 16: hipLaunchKernelGGL((norm_fwd_wave<16, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+    }
+  } else {
+    hipLaunchKernelGGL((norm_fwd_block<RMS>), dim3(rows), dim3(256), 0, s, xp, gp, bp, yp, mean, rstd, hidden, eps);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+}  // namespace
+
+extern "C" int kfamd_layernorm_fwd_bf16(const void* x, const void* gamma, const void* beta, void* y,
+                                        float* mean, float* rstd, int rows, int hidden, float eps,
+                                        void* stream) {
+  return norm_fwd<false>(x, gamma, beta, y, mean, rstd, rows, hidden, eps, stream);
+}
+
+extern "C" int kfamd_rmsnorm_fwd_bf16(const void* x, const void* gamma, void* y, float* rstd,
+                                      int rows, int hidden, float eps, void* stream) {
+  return norm_fwd<true>(x, gamma, nullptr, y, nullptr, rstd, rows, hidden, eps, stream);
+}
+
+extern "C" long long kfamd_layernorm_bwd_workspace(int rows, int hidden) {
+  const long long nch = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
+  return 2LL * nch * hidden * (long long)sizeof(float);
+}
+
+extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma,
+                                        const float* mean, const float* rstd, void* dx,
+                                        float* dgamma, float* dbeta, float* workspace, int rows,
+                                        int hidden, void* stream) {
+  if (!dy || !x || !gamma || !mean || !rstd || !dx || rows <= 0 || hidden <= 0) return KFAMD_EINVAL;
+  if ((dgamma || dbeta) && !workspace) return KFAMD_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* dyp = static_cast<const __bf16*>(dy);
+  const __bf16* xp = static_cast<const __bf16*>(x);
+  const __bf16* gp = static_cast<const __bf16*>(gamma);
+  __bf16* dxp = static_cast<__bf16*>(dx);
+  const int vpl = vpl_for(hidden);
+  const bool vec = vpl && a16(dy) && a16(x) && a16(gamma) && a16(dx);
+  if (vec) {
+    dim3 grid((rows + 3) / 4), block(256);
+    switch (vpl) {
+      case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 2: hipLaunchKernelGGL((ln_bwd_dx_wave<2>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 4: hipLaunchKernelGGL((ln_bwd_dx_wave<4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 8: hipLaunchKernelGGL((ln_bwd_dx_wave<8>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 16: hipLaunchKernelGGL((ln_bwd_dx_wave<16>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+    }
+  } else {
+    hipLaunchKernelGGL(ln_bwd_dx_block, dim3(rows), dim3(256), 0, s, dyp, xp, gp, mean, rstd, dxp, hidden);
+  }
+  if (dgamma || dbeta) {
+    const int nch = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
+    dim3 grid((hidden + kColsPerBlock - 1) / kColsPerBlock, nch);
+    hipLaunchKernelGGL(ln_bwd_dgb_partial, grid, dim3(256), 0, s, dyp, xp, mean, rstd, workspace, rows, hidden);
+    hipLaunchKernelGGL(ln_bwd_dgb_finalize, dim3((hidden + 255) / 256), dim3(256), 0, s, workspace, dgamma, dbeta, nch, hidden);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}

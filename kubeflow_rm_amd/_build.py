@@ -1,0 +1,113 @@
+"""In-tree build of every native artefact of the framework.
+
+* ``libkfamd_kernels.so`` — the hand-written gfx950 HIP kernels (``kernels/*.hip``), compiled with
+  ``hipcc --offload-arch=gfx950`` and loaded by :mod:`kubeflow_rm_amd.ops` through ctypes (one HIP
+  runtime shared with torch: both resolve the ``libamdhip64.so.7`` SONAME).
+* ``native/`` — the C++17 control plane (API server, controllers, admission, KFAM, kubelet, GPU
+  topology/allocator) and the in-pod readiness op, built with CMake + Ninja into ``build/native``
+  and installed into ``kubeflow_rm_amd/bin``.
+
+Everything is built in-tree so that the artefacts travel with a ``gpurun`` snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+KERNEL_DIR = ROOT / "kernels"
+PKG_DIR = ROOT / "kubeflow_rm_amd"
+LIB_DIR = PKG_DIR / "lib"
+BIN_DIR = PKG_DIR / "bin"
+BUILD_DIR = ROOT / "build"
+KERNEL_LIB = LIB_DIR / "libkfamd_kernels.so"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KFAMD_OFFLOAD_ARCH", "gfx950")
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-mcode-object-version=5",
+    "-Wall",
+    "-Wno-unused-variable",
+    "-Wno-unused-function",
+]
+
+
+def _run(cmd: list[str], cwd: Path | None = None) -> None:
+    proc = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(
+            f"command failed ({proc.returncode}): {' '.join(cmd)}\n{proc.stdout}\n{proc.stderr}"
+        )
+
+
+def _newer(target: Path, sources: list[Path]) -> bool:
+    if not target.exists():
+        return False
+    t = target.stat().st_mtime
+    return all(s.stat().st_mtime <= t for s in sources)
+
+
+def build_kernels(force: bool = False, jobs: int = 8) -> Path:
+    """Compile kernels/*.hip for gfx950 and link libkfamd_kernels.so (incremental)."""
+    srcs = sorted(KERNEL_DIR.glob("*.hip"))
+    headers = sorted(KERNEL_DIR.glob("*.h"))
+    obj_dir = BUILD_DIR / "kernels"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+
+    def compile_one(src: Path) -> Path:
+        obj = obj_dir / (src.stem + ".o")
+        if force or not _newer(obj, [src, *headers]):
+            _run([HIPCC, *HIP_FLAGS, "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    if force or not _newer(KERNEL_LIB, objs):
+        tmp = KERNEL_LIB.with_suffix(".so.tmp")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)])
+        os.replace(tmp, KERNEL_LIB)
+    return KERNEL_LIB
+
+
+def build_native(force: bool = False, jobs: int = 8, build_type: str = "Release",
+                 sanitize: str = "") -> Path:
+    """Configure + build the C++ control plane with CMake/Ninja; install binaries into bin/."""
+    src = ROOT / "native"
+    if not (src / "CMakeLists.txt").exists():
+        return BIN_DIR
+    bdir = BUILD_DIR / ("native" if not sanitize else f"native-{sanitize}")
+    if force and bdir.exists():
+        shutil.rmtree(bdir)
+    bdir.mkdir(parents=True, exist_ok=True)
+    gen = ["-G", "Ninja"] if shutil.which("ninja") else []
+    cfg = ["cmake", *gen, str(src), f"-DCMAKE_BUILD_TYPE={build_type}",
+           f"-DKFAMD_SANITIZE={sanitize}", f"-DKFAMD_BIN_DIR={BIN_DIR if not sanitize else bdir / 'bin'}",
+           f"-DKFAMD_KERNEL_DIR={KERNEL_DIR}", f"-DKFAMD_OFFLOAD_ARCH={ARCH}"]
+    if not (bdir / "CMakeCache.txt").exists():
+        _run(cfg, cwd=bdir)
+    _run(["cmake", "--build", str(bdir), "-j", str(jobs)], cwd=bdir)
+    return BIN_DIR if not sanitize else bdir / "bin"
+
+
+def build_all(force: bool = False) -> None:
+    build_kernels(force=force)
+    build_native(force=force)
+
+
+if __name__ == "__main__":  # python -m kubeflow_rm_amd._build [--force] [kernels|native]
+    args = sys.argv[1:]
+    force = "--force" in args
+    what = [a for a in args if not a.startswith("--")] or ["kernels", "native"]
+    if "kernels" in what:
+        print(build_kernels(force=force))
+    if "native" in what:
+        print(build_native(force=force))

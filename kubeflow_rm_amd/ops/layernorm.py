@@ -1,0 +1,74 @@
+"""LayerNorm / RMSNorm on the hand-written gfx950 kernels (kernels/layernorm_bf16.hip)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .gemm import _check_operand, _stream_ptr
+
+
+def layer_norm_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, eps: float = 1e-5,
+                   save_stats: bool = False):
+    _check_operand(x, "x")
+    _check_operand(weight, "weight")
+    H = x.shape[-1]
+    x2 = x.reshape(-1, H).contiguous()
+    rows = x2.shape[0]
+    y = torch.empty_like(x2)
+    mean = rstd = None
+    if save_stats:
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rc = _lib.lib().kfamd_layernorm_fwd_bf16(
+        x2.data_ptr(), weight.contiguous().data_ptr(),
+        bias.contiguous().data_ptr() if bias is not None else None, y.data_ptr(),
+        mean.data_ptr() if mean is not None else None, rstd.data_ptr() if rstd is not None else None,
+        rows, H, float(eps), _stream_ptr(x))
+    _lib.check(rc, f"layernorm_fwd[{rows}x{H}]")
+    return y.view(x.shape), mean, rstd
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    _check_operand(x, "x")
+    H = x.shape[-1]
+    x2 = x.reshape(-1, H).contiguous()
+    y = torch.empty_like(x2)
+    rc = _lib.lib().kfamd_rmsnorm_fwd_bf16(x2.data_ptr(), weight.contiguous().data_ptr(), y.data_ptr(),
+                                           None, x2.shape[0], H, float(eps), _stream_ptr(x))
+    _lib.check(rc, f"rmsnorm_fwd[{x2.shape[0]}x{H}]")
+    return y.view(x.shape)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        y, mean, rstd = layer_norm_fwd(x, weight, bias, eps, save_stats=True)
+        ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, mean, rstd = ctx.saved_tensors
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous()
+        gy2 = gy.reshape(-1, H).contiguous().to(torch.bfloat16)
+        rows = x2.shape[0]
+        dx = torch.empty_like(x2)
+        dgamma = torch.empty(H, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(H, dtype=torch.float32, device=x.device)
+        ws_bytes = _lib.lib().kfamd_layernorm_bwd_workspace(rows, H)
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device)
+        rc = _lib.lib().kfamd_layernorm_bwd_bf16(
+            gy2.data_ptr(), x2.data_ptr(), weight.contiguous().data_ptr(), mean.data_ptr(),
+            rstd.data_ptr(), dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), ws.data_ptr(),
+            rows, H, _stream_ptr(x))
+        _lib.check(rc, f"layernorm_bwd[{rows}x{H}]")
+        return (dx.view(x.shape), dgamma.to(weight.dtype),
+                dbeta.to(weight.dtype) if ctx.has_bias else None, None)
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
+               eps: float = 1e-5) -> torch.Tensor:
+    """Autograd-aware LayerNorm over the last dim (bf16 I/O, fp32 statistics)."""
+    return _LayerNorm.apply(x, weight, bias, eps)
