@@ -17,6 +17,7 @@
 //   for any M/N/K/alignment (small or ragged shapes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "kfamd_kernels.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -203,6 +204,213 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_256(
 }
 
 // -------------------------------------------------------------------------------------------
+// Fast path v2 (pipelined): the fragments of the NEXT k-substep are read from LDS while the
+// MFMAs of the current one run (two register sets F0/F1), one barrier per K-tile, and the
+// LDS-DMA of tile kt+2 is issued right after that barrier beside the MFMAs of substep 1.
+//   per K-tile:  [ds_read F1(kt) || MFMA F0(kt)] -> lgkm(0), vmcnt(0) (tile kt+1 landed)
+//                -> s_barrier -> [glds kt+2 -> buf(kt) || ds_read F0(kt+1) || MFMA F1(kt)]
+// SCHED = 1 additionally pins a fine ds_read/glds : MFMA interleave with sched_group_barrier.
+// -------------------------------------------------------------------------------------------
+template <int ACT, bool HAS_BIAS, bool HAS_RES, int SCHED>
+__global__ __launch_bounds__(kThreads, 2) void gemm_nt_256p(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
+    const __bf16* __restrict__ bias, const __bf16* __restrict__ R, int M, int N, int K,
+    long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
+    long long sc, long long sr, float alpha) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+
+  const int tiles_m = M / kBM, tiles_n = N / kBN, nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  constexpr int kGroupM = 4;
+  const int per_group = kGroupM * tiles_n;
+  const int g = wg / per_group, first_m = g * kGroupM;
+  const int gm = min(tiles_m - first_m, kGroupM);
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const int m0 = tm * kBM, n0 = tn * kBN;
+
+  const long long bz = blockIdx.y;
+  A += bz * sa;
+  B += bz * sb;
+  C += bz * sc;
+  if (HAS_RES) R += bz * sr;
+
+  const char* a_src[4];
+  const char* b_src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = wid * 4 + j;
+    const int row = p * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    a_src[j] = reinterpret_cast<const char*>(A + (long long)(m0 + row) * lda + chunk * 8);
+    b_src[j] = reinterpret_cast<const char*>(B + (long long)(n0 + row) * ldb + chunk * 8);
+  }
+  auto stage = [&](int kt, int buf) {
+    char* base = smem + buf * kStageBytes;
+    const long long koff = (long long)kt * kBK * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = wid * 4 + j;
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[j] + koff), LDS_PTR(base + p * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[j] + koff), LDS_PTR(base + kTileBytes + p * 1024), 16, 0, 0);
+    }
+  };
+
+  const int lr = lane & 15, lh = lane >> 4;
+  const int sw = lh ^ (lr >> 1);
+  const int off0 = lr * 128 + (sw << 4);
+  const int off1 = lr * 128 + ((sw ^ 4) << 4);
+  const int a_base = (wm * 128) * 128;
+  const int b_base = kTileBytes + (wn * 64) * 128;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  auto read_frags = [&](const char* sbuf, int off, bf16x8(&af)[8], bf16x8(&bf)[4]) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bf[n] = *reinterpret_cast<const bf16x8*>(sbuf + b_base + n * 2048 + off);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8*>(sbuf + a_base + i * 2048 + off);
+  };
+  // SCHED: no s_setprio inside the cluster (it is a scheduling-region boundary that would keep
+  // sched_group_barrier from interleaving the loads into the MFMA stream); one static raise.
+  if (SCHED) __builtin_amdgcn_s_setprio(1);
+  auto mfmas = [&](bf16x8(&af)[8], bf16x8(&bf)[4]) {
+    if (!SCHED) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[n], af[i], acc[i][n], 0, 0, 0);
+    if (!SCHED) __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = K / kBK;
+  stage(0, 0);
+  if (nk > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  COMPILER_FENCE();
+  __builtin_amdgcn_s_barrier();
+  COMPILER_FENCE();
+  read_frags(smem, off0, a0, b0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): nothing pending at the loop head
+
+  // One K-tile of the steady state. STAGE: issue the LDS-DMA of tile kt+2; NEXT: read F0(kt+1).
+  // sched_barrier(0) pins the s_barrier section so hipcc cannot hoist an MFMA cluster across it.
+  auto body = [&](int kt, auto do_stage, auto do_next) {
+    constexpr bool kStage = decltype(do_stage)::value;
+    constexpr bool kNext = decltype(do_next)::value;
+    const char* cur = smem + (kt & 1) * kStageBytes;
+    const char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+    read_frags(cur, off1, a1, b1);
+    mfmas(a0, b0);
+    if (SCHED) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // vmcnt(0) (tile kt+1 landed) + lgkmcnt(0) (F1 in registers, cur fully read). The builtin
+    // form is visible to hipcc's waitcnt pass, so it will not re-wait for F1 behind F0(kt+1).
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    COMPILER_FENCE();
+    __builtin_amdgcn_s_barrier();
+    COMPILER_FENCE();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kStage) stage(kt + 2, kt & 1);
+    if (kNext) read_frags(nxt, off0, a0, b0);
+    mfmas(a1, b1);
+    if (SCHED == 2 && kStage && kNext) {
+      // 12 ds_reads first (they feed the NEXT tile's first cluster), then glds spread 1 per 2 MFMAs
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+    } else if (SCHED) {
+      if (kStage) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);  // 1 glds (VMEM read)
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // 1 MFMA
+        }
+      }
+      if (kNext) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // retire F0(kt+1) here (it had the whole F1 MFMA cluster to land) so the waitcnt pass does
+    // not emit lgkmcnt(0) at the loop head, behind the freshly issued F1 reads
+    if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+  };
+  using T = std::integral_constant<bool, true>;
+  using F = std::integral_constant<bool, false>;
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
+  if (kt + 1 < nk) {
+    body(kt, F{}, T{});
+    ++kt;
+  }
+  if (kt < nk) body(kt, F{}, F{});
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + lr;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = n0 + wn * 64 + n * 16 + lh * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
+      if (HAS_BIAS) {
+        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+      }
+      if (ACT != KFAMD_ACT_NONE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], ACT);
+      }
+      if (HAS_RES) {
+        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+      *reinterpret_cast<bf16x4*>(C + (long long)m * ldc + col) = o;
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // Generic path: 128 x 128 x 32, 4 waves (2x2, 64x64 each), register staging, full bounds checks.
 // -------------------------------------------------------------------------------------------
 constexpr int gBM = 128, gBN = 128, gBK = 32, gThreads = 256;
@@ -307,27 +515,28 @@ __global__ __launch_bounds__(gThreads, 2) void gemm_nt_128(
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 
-#define KFAMD_DISPATCH_EPI(KERNEL, GRID, BLOCK, STREAM, ...)                                      \
+#define KFAMD_COMMA ,
+#define KFAMD_DISPATCH_EPI(KERNEL, EXTRA, GRID, BLOCK, STREAM, ...)                                      \
   do {                                                                                           \
     const bool hb = bias != nullptr, hr = R != nullptr;                                          \
     switch (act) {                                                                               \
       case KFAMD_ACT_NONE:                                                                       \
-        if (hb && hr) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, true, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else if (hr) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, false, true>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
+        if (hb && hr) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, true, true EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, true, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else if (hr) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, false, true EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_NONE, false, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
         break;                                                                                   \
       case KFAMD_ACT_RELU:                                                                       \
-        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_RELU, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);       \
-        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_RELU, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
+        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_RELU, true, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);       \
+        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_RELU, false, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
         break;                                                                                   \
       case KFAMD_ACT_GELU_TANH:                                                                  \
-        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_GELU_TANH, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_GELU_TANH, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
+        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_GELU_TANH, true, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_GELU_TANH, false, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);    \
         break;                                                                                   \
       case KFAMD_ACT_SILU:                                                                       \
-        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_SILU, true, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);       \
-        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_SILU, false, false>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
+        if (hb) hipLaunchKernelGGL((KERNEL<KFAMD_ACT_SILU, true, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);       \
+        else hipLaunchKernelGGL((KERNEL<KFAMD_ACT_SILU, false, false EXTRA>), GRID, BLOCK, 0, STREAM, __VA_ARGS__);         \
         break;                                                                                   \
     }                                                                                            \
   } while (0)
@@ -355,7 +564,7 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
                         (!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0) &&
                         (!R || ((reinterpret_cast<uintptr_t>(R) & 7) == 0 && ldr % 4 == 0 && stride_r % 4 == 0));
   bool fast = shapes_ok && align_ok;
-  if (variant == 1) {
+  if (variant == 1 || variant >= 3) {
     if (!shapes_ok) return KFAMD_EINVAL;
     if (!align_ok) return KFAMD_EALIGN;
     fast = true;
@@ -370,13 +579,24 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   const __bf16* r = static_cast<const __bf16*>(R);
   if (fast) {
     dim3 grid((M / kBM) * (N / kBN), batch), block(kThreads);
-    KFAMD_DISPATCH_EPI(gemm_nt_256, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr,
-                       stride_a, stride_b, stride_c, stride_r, alpha);
+    if (variant == 0 || variant == 4) {  // default fast path: pipelined + pinned interleave
+      KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 1, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
+                         ldr, stride_a, stride_b, stride_c, stride_r, alpha);
+    } else if (variant == 3) {
+      KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 0, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
+                         ldr, stride_a, stride_b, stride_c, stride_r, alpha);
+    } else if (variant == 5) {
+      KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 2, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
+                         ldr, stride_a, stride_b, stride_c, stride_r, alpha);
+    } else {
+      KFAMD_DISPATCH_EPI(gemm_nt_256, , grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr,
+                         stride_a, stride_b, stride_c, stride_r, alpha);
+    }
   } else {
     const int vec_a = aligned16(A) && (lda % 8 == 0) && (stride_a % 8 == 0);
     const int vec_b = aligned16(B) && (ldb % 8 == 0) && (stride_b % 8 == 0);
     dim3 grid((M + gBM - 1) / gBM, batch, (N + gBN - 1) / gBN), block(gThreads);
-    KFAMD_DISPATCH_EPI(gemm_nt_128, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr,
+    KFAMD_DISPATCH_EPI(gemm_nt_128, , grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr,
                        stride_a, stride_b, stride_c, stride_r, alpha, vec_a, vec_b);
   }
   const hipError_t e = hipGetLastError();

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default="")
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--variants", default="auto")
     args = ap.parse_args()
     import torch
     from kubeflow_rm_amd import ops
@@ -45,19 +46,23 @@ def main():
         b = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
         c = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
         iters = max(3, min(200, int(2e12 / (2 * s ** 3)) + 1))
-        ours, theirs = [], []
+        variants = args.variants.split(",")
+        ours, theirs = {v: [] for v in variants}, []
         for _ in range(3):
-            ops.gemm_nt(a, b, out=c)
+            for v in variants:
+                ops.gemm_nt(a, b, out=c, variant=v)
             if not args.no_torch:
                 torch.matmul(a, b.t())
         for _ in range(args.rounds):
-            ours.append(timeit(lambda: ops.gemm_nt(a, b, out=c), iters, dev))
+            for v in variants:
+                ours[v].append(timeit(lambda: ops.gemm_nt(a, b, out=c, variant=v), iters, dev))
             if not args.no_torch:
                 theirs.append(timeit(lambda: torch.matmul(a, b.t()), iters, dev))
         fl = 2.0 * s ** 3
-        d = {"kind": "gemm_nt_bf16", "M": s, "N": s, "K": s,
-             "ours_tflops": round(fl / min(ours) / 1e12, 1),
-             "ours_tflops_median": round(fl / sorted(ours)[len(ours) // 2] / 1e12, 1)}
+        d = {"kind": "gemm_nt_bf16", "M": s, "N": s, "K": s}
+        for v in variants:
+            d[f"{v}_tflops"] = round(fl / min(ours[v]) / 1e12, 1)
+            d[f"{v}_tflops_median"] = round(fl / sorted(ours[v])[len(ours[v]) // 2] / 1e12, 1)
         if theirs:
             d["torch_tflops"] = round(fl / min(theirs) / 1e12, 1)
         emit(d)
