@@ -1,0 +1,61 @@
+// components.h — wiring of every control-plane component onto a Manager (shared by kflite and
+// the split per-component binaries).
+#pragma once
+
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "apiserver/apiserver.h"
+#include "core/util.h"
+#include "runtime/runtime.h"
+
+namespace kf {
+
+struct ComponentFlags {
+  // kubelet / node
+  std::string node_name = "mi355x-node-0";
+  int64_t gpus = -1;  // -1 = discover from KFD sysfs (or KFAMD_FAKE_GPUS)
+  std::string repo_root;  // where kubeflow_rm_amd lives (pod "image" recipes run from here)
+  std::string python = "python3";
+  double restart_backoff = 10.0;
+  std::string pod_cidr_prefix = "127.20";
+  // gateway (Istio ingress equivalent)
+  std::string gateway_addr = "127.0.0.1";
+  int64_t gateway_port = 0;
+  std::string gateway_name = "kubeflow/kubeflow-gateway";
+  // KFAM
+  int64_t kfam_port = -1;  // -1 = disabled unless "kfam" is enabled (then ephemeral)
+  std::string userid_header = "kubeflow-userid";
+  std::string userid_prefix = "";
+  std::string cluster_admin = "";
+  // profile controller
+  std::string namespace_labels_path;
+  bool workload_identity = false;
+  // odh
+  std::string oauth_proxy_image = "registry.redhat.io/openshift4/ose-oauth-proxy:latest";
+  std::string controller_namespace = "opendatahub";
+  // admission webhooks as HTTP services (split mode); in kflite they run in-process
+  int64_t webhook_port = -1;
+
+  void register_flags(Flags& f);
+};
+
+class Components {
+ public:
+  Components(ComponentFlags f, std::shared_ptr<Client> c, ApiServer* local_api, std::string api_url, std::string data_dir);
+  ~Components();
+  bool setup(Manager& mgr, const std::set<std::string>& enabled, int workers, std::string* err);
+  void start();
+  void stop();
+  int gateway_port() const;
+  int kfam_port() const;
+
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
+
+}  // namespace kf

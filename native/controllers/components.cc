@@ -1,0 +1,83 @@
+// components.cc — see cmd/components.h.
+#include "cmd/components.h"
+
+#include <unistd.h>
+
+#include "controllers/notebook.h"
+#include "core/util.h"
+
+namespace kf {
+
+void ComponentFlags::register_flags(Flags& f) {
+  f.add_string("node-name", &node_name, "mi355x-node-0", "kubelet node name");
+  f.add_int("gpus", &gpus, -1, "GPUs advertised by the device plugin (-1 = discover from KFD sysfs / KFAMD_FAKE_GPUS)");
+  f.add_string("repo-root", &repo_root, "", "framework root used by pod image recipes (default: derived from the binary path)");
+  f.add_string("python", &python, "python3", "python interpreter for pod image recipes");
+  f.add_double("restart-backoff", &restart_backoff, 10.0, "base container restart back-off in seconds");
+  f.add_string("pod-cidr-prefix", &pod_cidr_prefix, "127.20", "pod IPs are allocated as <prefix>.x.y (loopback)");
+  f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
+  f.add_int("gateway-port", &gateway_port, 0, "ingress gateway port (0 = ephemeral)");
+  f.add_string("gateway-name", &gateway_name, "kubeflow/kubeflow-gateway", "VirtualService gateway served by the ingress");
+  f.add_int("kfam-port", &kfam_port, -1, "KFAM port (-1 = ephemeral when kfam is enabled)");
+  f.add_string("userid-header", &userid_header, "kubeflow-userid", "user id header (KFAM / profile controller)");
+  f.add_string("userid-prefix", &userid_prefix, "", "user id prefix (KFAM / profile controller)");
+  f.add_string("cluster-admin", &cluster_admin, "", "KFAM cluster admin user");
+  f.add_string("namespace-labels-path", &namespace_labels_path, "", "profile controller namespace labels file");
+  f.add_bool("workload-identity", &workload_identity, false, "enable the GCP workload identity plugin");
+  f.add_string("oauth-proxy-image", &oauth_proxy_image, "registry.redhat.io/openshift4/ose-oauth-proxy:latest", "ODH oauth proxy image");
+  f.add_string("controller-namespace", &controller_namespace, "opendatahub", "ODH controller namespace");
+  f.add_int("webhook-port", &webhook_port, -1, "serve admission webhooks over HTTP on this port (-1 = in-process only)");
+}
+
+struct Components::Impl {
+  ComponentFlags f;
+  std::shared_ptr<Client> c;
+  ApiServer* api;
+  std::string api_url, data_dir;
+  std::shared_ptr<NotebookMetrics> nb_metrics;
+  std::unique_ptr<NotebookReconciler> notebook;
+  std::unique_ptr<CullingReconciler> culler;
+  std::vector<std::function<void()>> starters, stoppers;
+};
+
+Components::Components(ComponentFlags f, std::shared_ptr<Client> c, ApiServer* local_api, std::string api_url,
+                       std::string data_dir)
+    : impl_(std::make_unique<Impl>()) {
+  impl_->f = std::move(f);
+  impl_->c = std::move(c);
+  impl_->api = local_api;
+  impl_->api_url = std::move(api_url);
+  impl_->data_dir = std::move(data_dir);
+}
+
+Components::~Components() { stop(); }
+
+bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int workers, std::string* err) {
+  Impl& I = *impl_;
+  I.nb_metrics = NotebookMetrics::install(I.c);
+  if (enabled.count("notebook")) {
+    I.notebook = std::make_unique<NotebookReconciler>(I.c, NotebookOptions::from_env(), I.nb_metrics);
+    I.notebook->setup(mgr, workers);
+  }
+  if (enabled.count("culler") && getenv_or("ENABLE_CULLING", "false") == "true") {
+    I.culler = std::make_unique<CullingReconciler>(I.c, CullingOptions::from_env(), I.nb_metrics);
+    I.culler->setup(mgr);
+  }
+  (void)err;
+  return true;
+}
+
+void Components::start() {
+  for (auto& s : impl_->starters) s();
+}
+
+void Components::stop() {
+  if (!impl_) return;
+  for (auto it = impl_->stoppers.rbegin(); it != impl_->stoppers.rend(); ++it) (*it)();
+  impl_->stoppers.clear();
+}
+
+int Components::gateway_port() const { return 0; }
+int Components::kfam_port() const { return 0; }
+
+}  // namespace kf

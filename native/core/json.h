@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <initializer_list>
 #include <map>
 #include <stdexcept>
@@ -28,9 +29,11 @@ class JsonError : public std::runtime_error {
 class Json {
  public:
   enum class Type : uint8_t { Null, Bool, Int, Double, String, Array, Object };
-  using Array = std::vector<Json>;
+  // std::deque: appending a member/element never invalidates references to existing children,
+  // so `Json& md = obj["metadata"]; obj["status"] = ...; md["x"] = 1;` is safe.
+  using Array = std::deque<Json>;
   using Member = std::pair<std::string, Json>;
-  using Object = std::vector<Member>;
+  using Object = std::deque<Member>;
 
   Json() = default;
   Json(std::nullptr_t) {}
