@@ -1,0 +1,114 @@
+"""Start / stop an embedded kflite control plane (the envtest equivalent).
+
+    with LocalCluster(env={"USE_ISTIO": "true"}) as c:
+        c.client.create(notebook)
+
+The process is started in its own session; stop() terminates exactly that process group
+(never by pattern), and the kubelet inside tears down every pod process it started.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import tempfile
+import time
+from pathlib import Path
+
+from .client import KubeClient
+
+ROOT = Path(__file__).resolve().parent.parent
+BIN = Path(__file__).resolve().parent / "bin"
+
+
+def kflite_binary() -> Path:
+    p = Path(os.environ.get("KFAMD_KFLITE", BIN / "kflite"))
+    if not p.exists():
+        raise FileNotFoundError(f"{p} missing: build with `python -m kubeflow_rm_amd._build native`")
+    return p
+
+
+class LocalCluster:
+    def __init__(self, data_dir: str | None = None, env: dict | None = None, args: list[str] | None = None,
+                 controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0):
+        self._tmp = None
+        if data_dir is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="kflite-")
+            data_dir = self._tmp.name
+        self.data_dir = data_dir
+        self.env = dict(os.environ)
+        self.env.update(env or {})
+        self.args = list(args or [])
+        self.controllers = controllers
+        self.gpus = gpus
+        self.startup_timeout = startup_timeout
+        self.proc: subprocess.Popen | None = None
+        self.url = ""
+        self.gateway = ""
+        self.kfam = ""
+        self.client: KubeClient | None = None
+
+    def start(self) -> "LocalCluster":
+        info = Path(self.data_dir) / "kflite.json"
+        if info.exists():
+            info.unlink()
+        cmd = [str(kflite_binary()), "--data-dir", self.data_dir, "--controllers", self.controllers,
+               "--restart-backoff", self.env.get("KFAMD_RESTART_BACKOFF", "1")]
+        if self.gpus is not None:
+            cmd += ["--gpus", str(self.gpus)]
+        cmd += self.args
+        self.log_path = Path(self.data_dir) / "kflite.log"
+        self._log = open(self.log_path, "ab")
+        self.proc = subprocess.Popen(cmd, stdout=self._log, stderr=subprocess.STDOUT, env=self.env,
+                                     start_new_session=True)
+        deadline = time.time() + self.startup_timeout
+        while time.time() < deadline:
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"kflite exited early ({self.proc.returncode}):\n{self.log_path.read_text()[-3000:]}")
+            if info.exists():
+                try:
+                    d = json.loads(info.read_text())
+                except ValueError:
+                    d = {}
+                if d.get("server") and "gateway" in d:
+                    self.url = d["server"]
+                    self.gateway = d.get("gateway", "")
+                    self.kfam = d.get("kfam", "")
+                    break
+            time.sleep(0.02)
+        else:
+            self.stop()
+            raise TimeoutError("kflite did not come up")
+        self.client = KubeClient(self.url)
+        return self
+
+    def stop(self) -> None:
+        if self.proc and self.proc.poll() is None:
+            try:
+                os.killpg(self.proc.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+            try:
+                self.proc.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                os.killpg(self.proc.pid, signal.SIGKILL)
+                self.proc.wait(timeout=10)
+        if getattr(self, "_log", None):
+            self._log.close()
+            self._log = None
+        if self._tmp:
+            self._tmp.cleanup()
+            self._tmp = None
+
+    def logs(self) -> str:
+        try:
+            return self.log_path.read_text()
+        except OSError:
+            return ""
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

@@ -117,6 +117,12 @@ int main(int argc, char** argv) {
     return 1;
   }
   comps.start();
+  if (comps.gateway_port()) std::printf("kflite: gateway listening on http://%s:%d\n", cf.gateway_addr.c_str(), comps.gateway_port());
+  if (!data_dir.empty())
+    write_file(data_dir + "/kflite.json", Json{{"server", url}, {"pid", static_cast<int64_t>(::getpid())},
+                                               {"gateway", comps.gateway_port() ? "http://" + cf.gateway_addr + ":" + std::to_string(comps.gateway_port()) : ""},
+                                               {"kfam", comps.kfam_port() ? "http://127.0.0.1:" + std::to_string(comps.kfam_port()) : ""}}
+                                                  .dump() + "\n");
   std::printf("kflite: controllers running: %s\n", join(std::vector<std::string>(enabled.begin(), enabled.end()), ",").c_str());
   std::fflush(stdout);
   while (!g_stop) ::usleep(100000);

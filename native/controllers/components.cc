@@ -3,7 +3,9 @@
 
 #include <unistd.h>
 
+#include "controllers/builtin.h"
 #include "controllers/notebook.h"
+#include "node/node.h"
 #include "core/util.h"
 
 namespace kf {
@@ -37,6 +39,10 @@ struct Components::Impl {
   std::shared_ptr<NotebookMetrics> nb_metrics;
   std::unique_ptr<NotebookReconciler> notebook;
   std::unique_ptr<CullingReconciler> culler;
+  std::unique_ptr<BuiltinControllers> builtin;
+  std::unique_ptr<Scheduler> scheduler;
+  std::unique_ptr<Kubelet> kubelet;
+  std::unique_ptr<Gateway> gateway;
   std::vector<std::function<void()>> starters, stoppers;
 };
 
@@ -63,7 +69,54 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.culler = std::make_unique<CullingReconciler>(I.c, CullingOptions::from_env(), I.nb_metrics);
     I.culler->setup(mgr);
   }
-  (void)err;
+  if (enabled.count("builtin")) {
+    I.builtin = std::make_unique<BuiltinControllers>(I.c);
+    I.builtin->setup(mgr, workers);
+  }
+  if (enabled.count("scheduler")) {
+    I.scheduler = std::make_unique<Scheduler>(I.c);
+    I.scheduler->setup(mgr);
+  }
+  if (enabled.count("kubelet")) {
+    KubeletConfig kc;
+    kc.node_name = I.f.node_name;
+    kc.root_dir = I.data_dir.empty() ? "/tmp/kflite-" + random_hex(4) : I.data_dir + "/kubelet";
+    kc.repo_root = I.f.repo_root;
+    if (kc.repo_root.empty()) {
+      char buf[4096];
+      ssize_t n = ::readlink("/proc/self/exe", buf, sizeof buf - 1);
+      std::string exe = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "";
+      // <root>/kubeflow_rm_amd/bin/kflite -> <root>
+      for (int i = 0; i < 3 && !exe.empty(); ++i) exe = exe.substr(0, exe.rfind('/'));
+      kc.repo_root = exe;
+    }
+    {
+      char buf[4096];
+      ssize_t n = ::readlink("/proc/self/exe", buf, sizeof buf - 1);
+      std::string exe = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "";
+      kc.bin_dir = exe.substr(0, exe.rfind('/'));
+    }
+    kc.python = I.f.python;
+    kc.api_url = I.api_url;
+    kc.pod_ip_prefix = I.f.pod_cidr_prefix;
+    kc.restart_backoff = I.f.restart_backoff;
+    kc.gpus = static_cast<int>(I.f.gpus);
+    I.kubelet = std::make_unique<Kubelet>(I.c, kc);
+    I.kubelet->setup(mgr);
+    if (I.api) {
+      Kubelet* k = I.kubelet.get();
+      I.api->set_log_provider([k](const std::string& ns, const std::string& pod, const std::string& cont, int64_t tail,
+                                  std::string& out) { return k->read_logs(ns, pod, cont, tail, out); });
+    }
+    I.starters.push_back([&I] { I.kubelet->start(); });
+    I.stoppers.push_back([&I] { I.kubelet->stop(); });
+  }
+  if (enabled.count("gateway")) {
+    I.gateway = std::make_unique<Gateway>(I.c, I.f.gateway_name);
+    I.gateway->setup(mgr);
+    if (!I.gateway->start(I.f.gateway_addr, static_cast<int>(I.f.gateway_port), err)) return false;
+    I.stoppers.push_back([&I] { I.gateway->stop(); });
+  }
   return true;
 }
 
@@ -77,7 +130,7 @@ void Components::stop() {
   impl_->stoppers.clear();
 }
 
-int Components::gateway_port() const { return 0; }
+int Components::gateway_port() const { return impl_->gateway ? impl_->gateway->port() : 0; }
 int Components::kfam_port() const { return 0; }
 
 }  // namespace kf

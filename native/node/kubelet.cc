@@ -1,0 +1,981 @@
+// kubelet.cc — process-pod kubelet with the MI355X device plugin (see node.h).
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <regex>
+#include <set>
+
+#include "controllers/common.h"
+#include "core/util.h"
+#include "node/node.h"
+
+extern char** environ;
+
+namespace kf {
+
+namespace {
+std::string ms_now() { return rfc3339_ms_now(); }
+
+int64_t probe_i(const Json& probe, const char* key, int64_t def) { return probe[key].as_int(def); }
+
+bool tcp_connect(const std::string& ip, int port, int timeout_ms) {
+  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return false;
+  ::fcntl(fd, F_SETFL, O_NONBLOCK);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons(static_cast<uint16_t>(port));
+  ::inet_pton(AF_INET, ip.c_str(), &sa.sin_addr);
+  int rc = ::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa);
+  bool ok = rc == 0;
+  if (!ok && errno == EINPROGRESS) {
+    pollfd p{fd, POLLOUT, 0};
+    if (::poll(&p, 1, timeout_ms) > 0) {
+      int err = 0;
+      socklen_t l = sizeof err;
+      ::getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &l);
+      ok = err == 0;
+    }
+  }
+  ::close(fd);
+  return ok;
+}
+
+bool executable(const std::string& path) { return ::access(path.c_str(), X_OK) == 0; }
+
+std::string which(const std::string& cmd) {
+  if (cmd.empty()) return "";
+  if (cmd.find('/') != std::string::npos) return executable(cmd) ? cmd : "";
+  for (const auto& dir : split(getenv_or("PATH", "/usr/bin:/bin"), ':', true)) {
+    std::string p = dir + "/" + cmd;
+    if (executable(p)) return p;
+  }
+  return "";
+}
+
+// $(VAR) expansion (Kubernetes command/args semantics; $$ escapes)
+std::string expand_vars(const std::string& s, const std::map<std::string, std::string>& env) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '$' && i + 1 < s.size() && s[i + 1] == '$') {
+      out += '$';
+      ++i;
+    } else if (s[i] == '$' && i + 1 < s.size() && s[i + 1] == '(') {
+      size_t e = s.find(')', i + 2);
+      if (e == std::string::npos) {
+        out += s.substr(i);
+        break;
+      }
+      std::string name = s.substr(i + 2, e - i - 2);
+      auto it = env.find(name);
+      out += it != env.end() ? it->second : s.substr(i, e - i + 1);
+      i = e;
+    } else {
+      out += s[i];
+    }
+  }
+  return out;
+}
+
+const char* kDefaultRecipes = R"([
+  {"match": "cmd:kfamd-readiness|kfamd-readiness|gpu-readiness", "argv": ["{bin}/kfamd-readiness"]},
+  {"match": "cmd:tensorboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
+  {"match": "cmd:jupyter|cmd:start-notebook.sh|cmd:start.sh", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
+  {"match": "oauth-proxy|oauth_proxy", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.oauth_proxy"], "passArgs": true},
+  {"match": "filebrowser", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.filebrowser"], "passArgs": true},
+  {"match": "jupyter-web-app|crud-web-apps/jupyter", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.jupyter"]},
+  {"match": "tensorboards-web-app|crud-web-apps/tensorboards", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.tensorboards"]},
+  {"match": "volumes-web-app|crud-web-apps/volumes", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.volumes"]},
+  {"match": "centraldashboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.dashboard"]},
+  {"match": "tensorboard|tensorflow/tensorflow", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
+  {"match": "jupyter|notebook|scipy|pytorch|tensorflow|codeserver|code-server|rstudio|workbench|s2i-", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
+  {"match": ".*", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.generic_server"], "passArgs": true}
+])";
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+struct ContainerRt {
+  std::string name;
+  bool init = false;
+  pid_t pid = -1;
+  std::string state = "waiting";  // waiting | running | terminated
+  std::string reason = "ContainerCreating";
+  std::string started_at, finished_at, message;
+  int exit_code = 0;
+  int restarts = 0;
+  bool ready = false, started_probe_ok = true;
+  int ready_ok = 0, ready_fail = 0, live_fail = 0, startup_ok = 0, startup_fail = 0;
+  double next_ready_probe = 0, next_live_probe = 0, next_startup_probe = 0, backoff_until = 0;
+  double run_started = 0;
+  Json last_state = Json::object();
+  std::string log_path, term_path;
+};
+
+struct Kubelet::PodRuntime {
+  std::string uid, ns, name, dir, ip;
+  Placement gpus;
+  bool gpu_ok = true;
+  std::map<std::string, std::string> mounts;  // mountPath -> host dir (per container union)
+  std::vector<ContainerRt> init, main;
+  size_t init_done = 0;
+  bool init_failed = false;
+  std::string start_time;
+  bool terminating = false;
+  double kill_deadline = 0;
+  bool announced_kill = false;
+};
+
+Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)), cfg_(std::move(cfg)) {
+  GpuTopology topo = cfg_.gpus >= 0 ? GpuTopology::synthetic(cfg_.gpus) : GpuTopology::discover();
+  alloc_ = std::make_unique<GpuAllocator>(topo);
+  recipes_ = Json::parse(kDefaultRecipes);
+  if (!cfg_.recipes_file.empty()) {
+    std::string t;
+    Json extra;
+    if (read_file(cfg_.recipes_file, t) && Json::try_parse(t, extra) && extra.is_array()) {
+      Json merged = extra;
+      for (const auto& r : recipes_.as_array()) merged.push_back(r);
+      recipes_ = merged;
+    }
+  }
+  if (cfg_.root_dir.empty()) cfg_.root_dir = "/tmp/kflite-" + random_hex(4);
+  make_dirs(cfg_.root_dir + "/pods");
+  make_dirs(cfg_.root_dir + "/pv");
+  rec_ = std::make_unique<EventRecorder>(c_, "kubelet");
+}
+
+Kubelet::~Kubelet() { stop(); }
+
+std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::string* why) const {
+  std::vector<std::string> cmd, args;
+  for (const auto& x : container["command"].as_array()) cmd.push_back(x.as_string());
+  for (const auto& x : container["args"].as_array()) args.push_back(x.as_string());
+  if (!cmd.empty() && !which(cmd[0]).empty()) {
+    if (why) *why = "command";
+    std::vector<std::string> out = cmd;
+    out.insert(out.end(), args.begin(), args.end());
+    return out;
+  }
+  std::vector<std::string> keys;
+  if (!cmd.empty()) {
+    std::string base = cmd[0].substr(cmd[0].rfind('/') == std::string::npos ? 0 : cmd[0].rfind('/') + 1);
+    keys.push_back("cmd:" + base);
+  }
+  keys.push_back(container["image"].as_string());
+  for (const auto& key : keys) {
+    for (const auto& r : recipes_.as_array()) {
+      std::regex re(r["match"].as_string(), std::regex::icase);
+      if (!std::regex_search(key, re)) continue;
+      std::vector<std::string> out;
+      for (const auto& a : r["argv"].as_array()) {
+        std::string s = replace_all(a.as_string(), "{python}", cfg_.python);
+        s = replace_all(s, "{bin}", cfg_.bin_dir);
+        out.push_back(s);
+      }
+      if (r["passArgs"].as_bool()) {
+        if (cmd.size() > 1) out.insert(out.end(), cmd.begin() + 1, cmd.end());
+        out.insert(out.end(), args.begin(), args.end());
+      }
+      if (why) *why = "recipe:" + r["match"].as_string();
+      return out;
+    }
+  }
+  return {"sleep", "infinity"};
+}
+
+// ---- node registration ------------------------------------------------------------------------
+Json Kubelet::node_object() const {
+  const auto& topo = alloc_->topology();
+  int64_t hbm_gib = 0;
+  for (const auto& g : topo.gpus) hbm_gib += g.hbm_bytes >> 30;
+  const long cpus = ::sysconf(_SC_NPROCESSORS_ONLN);
+  const long pages = ::sysconf(_SC_PHYS_PAGES), psize = ::sysconf(_SC_PAGE_SIZE);
+  Json cap{{"cpu", std::to_string(cpus)},
+           {"memory", std::to_string(static_cast<int64_t>(pages) * psize / 1024) + "Ki"},
+           {"pods", "110"},
+           {"ephemeral-storage", "1Ti"},
+           {GPU_RESOURCE, std::to_string(topo.size())},
+           {GPU_MEMORY_RESOURCE, std::to_string(hbm_gib)}};
+  Json labels{{"kubernetes.io/hostname", cfg_.node_name},
+              {"kubernetes.io/os", "linux"},
+              {"kubernetes.io/arch", "amd64"},
+              {"node.kubernetes.io/instance-type", "mi355x-x" + std::to_string(topo.size())},
+              {"amd.com/gpu.present", topo.size() > 0 ? "true" : "false"},
+              {"amd.com/gpu.count", std::to_string(topo.size())}};
+  if (topo.size() > 0) {
+    labels["amd.com/gpu.family"] = "CDNA4";
+    labels["amd.com/gpu.arch"] = topo.gpus[0].gfx;
+    labels["amd.com/gpu.product-name"] = "AMD_Instinct_MI355X";
+    labels["amd.com/gpu.xgmi"] = topo.describe().find("full-mesh") != std::string::npos ? "full-mesh" : "partial";
+  }
+  return Json{{"apiVersion", "v1"},
+              {"kind", "Node"},
+              {"metadata", Json{{"name", cfg_.node_name}, {"labels", labels},
+                                {"annotations", Json{{"amd.com/gpu-topology", topo.to_json().dump()}}}}},
+              {"spec", Json{{"providerID", "kflite://" + cfg_.node_name}}},
+              {"status", Json{{"capacity", cap},
+                              {"allocatable", cap},
+                              {"addresses", Json::array({Json{{"type", "InternalIP"}, {"address", "127.0.0.1"}},
+                                                         Json{{"type", "Hostname"}, {"address", cfg_.node_name}}})},
+                              {"nodeInfo", Json{{"kubeletVersion", "v1.29.0-kflite"}, {"containerRuntimeVersion", "kflite-process://1"},
+                                                {"operatingSystem", "linux"}, {"architecture", "amd64"},
+                                                {"osImage", "kflite process runtime"}}},
+                              {"conditions", Json::array({Json{{"type", "Ready"}, {"status", "True"}, {"reason", "KubeletReady"},
+                                                               {"message", "kubelet is posting ready status"},
+                                                               {"lastHeartbeatTime", rfc3339_now()},
+                                                               {"lastTransitionTime", rfc3339_now()}}})}}}};
+}
+
+void Kubelet::start() {
+  Json node = node_object();
+  Json existing;
+  if (c_->get("v1", "Node", "", cfg_.node_name, existing).code == 404) {
+    Json n = node;
+    c_->create(n);
+  }
+  c_->update_with_retry(
+      "v1", "Node", "", cfg_.node_name,
+      [&](Json& o) {
+        o["status"] = node["status"];
+        return true;
+      },
+      true);
+  c_->update_with_retry("v1", "Node", "", cfg_.node_name, [&](Json& o) {
+    o["metadata"]["labels"] = node.at_path({"metadata", "labels"});
+    o["metadata"]["annotations"] = node.at_path({"metadata", "annotations"});
+    return true;
+  });
+  running_ = true;
+  hb_ = std::thread([this] { heartbeat_loop(); });
+}
+
+void Kubelet::heartbeat_loop() {
+  while (running_) {
+    for (int i = 0; i < 100 && running_; ++i) ::usleep(100000);
+    if (!running_) break;
+    c_->update_with_retry(
+        "v1", "Node", "", cfg_.node_name,
+        [&](Json& o) {
+          for (auto& c : o["status"]["conditions"].mut_array())
+            if (c["type"].as_string() == "Ready") c["lastHeartbeatTime"] = rfc3339_now();
+          return true;
+        },
+        true);
+  }
+}
+
+void Kubelet::stop() {
+  if (!running_.exchange(false)) return;
+  if (hb_.joinable()) hb_.join();
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& kv : pods_) terminate_pod(*kv.second, 0);
+}
+
+// ---- process management ---------------------------------------------------------------------------
+namespace {
+pid_t spawn(const std::vector<std::string>& argv, const std::vector<std::string>& env, const std::string& cwd,
+            const std::string& log_path, std::string* err) {
+  posix_spawn_file_actions_t fa;
+  posix_spawnattr_t at;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawnattr_init(&at);
+  posix_spawnattr_setflags(&at, POSIX_SPAWN_SETSID | POSIX_SPAWN_SETSIGDEF | POSIX_SPAWN_SETSIGMASK);
+  sigset_t all, none;
+  sigfillset(&all);
+  sigemptyset(&none);
+  posix_spawnattr_setsigdefault(&at, &all);
+  posix_spawnattr_setsigmask(&at, &none);
+  posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+  posix_spawn_file_actions_addopen(&fa, 1, log_path.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+  posix_spawn_file_actions_adddup2(&fa, 1, 2);
+  posix_spawn_file_actions_addchdir_np(&fa, cwd.c_str());
+  std::vector<char*> av, ev;
+  for (const auto& a : argv) av.push_back(const_cast<char*>(a.c_str()));
+  av.push_back(nullptr);
+  for (const auto& e : env) ev.push_back(const_cast<char*>(e.c_str()));
+  ev.push_back(nullptr);
+  std::string exe = which(argv[0]);
+  pid_t pid = -1;
+  int rc = exe.empty() ? ENOENT : posix_spawn(&pid, exe.c_str(), &fa, &at, av.data(), ev.data());
+  posix_spawn_file_actions_destroy(&fa);
+  posix_spawnattr_destroy(&at);
+  if (rc != 0) {
+    if (err) *err = std::string("exec ") + argv[0] + ": " + std::strerror(rc);
+    return -1;
+  }
+  return pid;
+}
+
+// returns true when the process has exited (fills status)
+bool reap(pid_t pid, int& exit_code, std::string& reason) {
+  int st = 0;
+  pid_t r = ::waitpid(pid, &st, WNOHANG);
+  if (r == 0) return false;
+  if (r < 0) {
+    exit_code = 128;
+    reason = "Error";
+    return true;
+  }
+  if (WIFEXITED(st)) {
+    exit_code = WEXITSTATUS(st);
+  } else if (WIFSIGNALED(st)) {
+    exit_code = 128 + WTERMSIG(st);
+  }
+  reason = exit_code == 0 ? "Completed" : (exit_code == 137 ? "OOMKilled" : "Error");
+  if (WIFSIGNALED(st) && WTERMSIG(st) == SIGKILL) reason = "Error";
+  return true;
+}
+}  // namespace
+
+void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
+  auto kill_all = [&](int sig) {
+    for (auto* v : {&rt.init, &rt.main})
+      for (auto& c : *v)
+        if (c.pid > 0 && c.state == "running") ::kill(-c.pid, sig);
+  };
+  if (grace_s <= 0) {
+    kill_all(SIGKILL);
+  } else {
+    kill_all(SIGTERM);
+  }
+  for (auto* v : {&rt.init, &rt.main})
+    for (auto& c : *v) {
+      if (c.pid <= 0 || c.state != "running") continue;
+      double deadline = now_seconds() + static_cast<double>(grace_s);
+      int code = 0;
+      std::string reason;
+      while (!reap(c.pid, code, reason)) {
+        if (now_seconds() > deadline) {
+          ::kill(-c.pid, SIGKILL);
+          deadline = now_seconds() + 5;
+        }
+        ::usleep(10000);
+      }
+      c.state = "terminated";
+      c.exit_code = code;
+      c.reason = reason;
+      c.finished_at = ms_now();
+      c.pid = -1;
+    }
+}
+
+bool Kubelet::read_logs(const std::string& ns, const std::string& pod, const std::string& container, int64_t tail,
+                        std::string& out) {
+  std::shared_ptr<PodRuntime> rt;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto k = key_to_uid_.find(ns + "/" + pod);
+    if (k == key_to_uid_.end()) return false;
+    auto it = pods_.find(k->second);
+    if (it == pods_.end()) return false;
+    rt = it->second;
+  }
+  std::string path;
+  for (auto* v : {&rt->main, &rt->init})
+    for (auto& c : *v)
+      if (path.empty() && (container.empty() || c.name == container)) path = c.log_path;
+  if (path.empty()) return false;
+  if (!read_file(path, out)) out.clear();
+  if (tail >= 0) {
+    size_t pos = out.size();
+    int64_t lines = 0;
+    while (pos > 0 && lines <= tail) {
+      pos = out.rfind('\n', pos - 1);
+      if (pos == std::string::npos) {
+        pos = 0;
+        break;
+      }
+      lines++;
+    }
+    if (lines > tail && pos < out.size()) out = out.substr(pos + 1);
+  }
+  return true;
+}
+
+// ---- reconcile ---------------------------------------------------------------------------------
+Result Kubelet::reconcile(const Request& r, std::string* err) {
+  Json pod;
+  ApiError e = c_->get("v1", "Pod", r.ns, r.name, pod);
+  std::shared_ptr<PodRuntime> rt;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto k = key_to_uid_.find(r.ns + "/" + r.name);
+    if (k != key_to_uid_.end()) {
+      auto it = pods_.find(k->second);
+      if (it != pods_.end()) rt = it->second;
+      if (e.code == 404 || (!e && pod.str_at({"metadata", "uid"}) != k->second)) {
+        // pod object is gone (or replaced by a new incarnation): tear the old sandbox down
+        if (rt) {
+          terminate_pod(*rt, 0);
+          alloc_->release(rt->uid);
+          pods_.erase(rt->uid);
+        }
+        key_to_uid_.erase(k);
+        rt.reset();
+        if (e.code == 404) return {};
+      }
+    }
+  }
+  if (e.code == 404) return {};
+  if (e) {
+    *err = e.message;
+    return {};
+  }
+  if (pod.at_path({"spec", "nodeName"}).as_string() != cfg_.node_name) return {};
+  const std::string uid = pod.str_at({"metadata", "uid"});
+  const std::string restart_policy = pod.at_path({"spec", "restartPolicy"}).as_string_or("Always");
+
+  // ---- termination ------------------------------------------------------------------------------
+  if (pod.at_path({"metadata", "deletionTimestamp"}).is_string()) {
+    if (rt) {
+      if (!rt->announced_kill) {
+        rt->announced_kill = true;
+        for (auto& c : rt->main)
+          if (c.state == "running") rec_->event(pod, "Normal", "Killing", "Stopping container " + c.name);
+      }
+      terminate_pod(*rt, pod.at_path({"metadata", "deletionGracePeriodSeconds"}).as_int(30));
+      alloc_->release(uid);
+      std::lock_guard<std::mutex> g(mu_);
+      pods_.erase(uid);
+      key_to_uid_.erase(r.ns + "/" + r.name);
+    }
+    ApiError de = c_->remove("v1", "Pod", r.ns, r.name, "", 0);
+    if (de && de.code != 404) *err = de.message;
+    return {};
+  }
+  const std::string phase = pod.at_path({"status", "phase"}).as_string();
+  if (!rt && (phase == "Succeeded" || phase == "Failed")) return {};
+
+  // ---- admission: sandbox, IP, GPUs, volumes ------------------------------------------------------
+  if (!rt) {
+    rt = std::make_shared<PodRuntime>();
+    rt->uid = uid;
+    rt->ns = r.ns;
+    rt->name = r.name;
+    rt->dir = cfg_.root_dir + "/pods/" + r.ns + "_" + r.name + "_" + uid.substr(0, 8);
+    make_dirs(rt->dir + "/rootfs");
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      uint32_t n = next_ip_++;
+      rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
+    }
+    rt->start_time = ms_now();
+    // device plugin Allocate: topology-aware GPU placement
+    int want_gpus = 0;
+    for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
+      want_gpus += static_cast<int>(resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})));
+    if (want_gpus > 0) {
+      if (!alloc_->allocate(uid, want_gpus, rt->gpus)) {
+        rt->gpu_ok = false;
+      } else {
+        std::vector<std::string> ids, ring;
+        for (int d : rt->gpus.devices) ids.push_back(std::to_string(d));
+        for (int d : rt->gpus.ring) ring.push_back(std::to_string(d));
+        c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
+          o["metadata"]["annotations"][ANNOTATION_GPU_IDS] = join(ids, ",");
+          o["metadata"]["annotations"][ANNOTATION_XGMI_RING] = join(ring, ",");
+          o["metadata"]["annotations"]["amd.com/gpu-placement"] = rt->gpus.reason;
+          return true;
+        });
+      }
+    }
+    // volumes
+    std::map<std::string, std::string> vol_dirs;
+    for (const auto& v : pod.at_path({"spec", "volumes"}).as_array()) {
+      const std::string vname = v["name"].as_string();
+      std::string dir;
+      if (v["persistentVolumeClaim"].is_object()) {
+        dir = cfg_.root_dir + "/pv/" + r.ns + "/" + v.at_path({"persistentVolumeClaim", "claimName"}).as_string();
+      } else if (v["hostPath"].is_object()) {
+        dir = v.at_path({"hostPath", "path"}).as_string();
+      } else {
+        dir = rt->dir + "/volumes/" + vname;
+      }
+      make_dirs(dir);
+      if (v["configMap"].is_object() || v["secret"].is_object()) {
+        const bool secret = v["secret"].is_object();
+        Json src;
+        const std::string sname = secret ? v.at_path({"secret", "secretName"}).as_string() : v.at_path({"configMap", "name"}).as_string();
+        if (!c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, sname, src)) {
+          for (const auto& m : src["data"].as_object())
+            write_file(dir + "/" + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
+          if (secret)
+            for (const auto& m : src["stringData"].as_object()) write_file(dir + "/" + m.first, m.second.as_string());
+        }
+      }
+      vol_dirs[vname] = dir;
+    }
+    auto build = [&](const Json& list, bool init, std::vector<ContainerRt>& out) {
+      for (const auto& c : list.as_array()) {
+        ContainerRt cr;
+        cr.name = c["name"].as_string();
+        cr.init = init;
+        cr.log_path = rt->dir + "/" + cr.name + ".log";
+        cr.term_path = rt->dir + "/" + cr.name + ".termination-log";
+        for (const auto& vm : c["volumeMounts"].as_array()) {
+          auto it = vol_dirs.find(vm["name"].as_string());
+          if (it == vol_dirs.end()) continue;
+          std::string host = it->second;
+          if (!vm["subPath"].as_string().empty()) {
+            host += "/" + vm["subPath"].as_string();
+            if (!file_exists(host)) make_dirs(host);
+          }
+          rt->mounts[vm["mountPath"].as_string()] = host;
+        }
+        out.push_back(cr);
+      }
+    };
+    build(pod.at_path({"spec", "initContainers"}), true, rt->init);
+    build(pod.at_path({"spec", "containers"}), false, rt->main);
+    // materialise mount points inside the pod rootfs as symlinks
+    for (const auto& m : rt->mounts) {
+      std::string link = rt->dir + "/rootfs" + m.first;
+      size_t slash = link.rfind('/');
+      make_dirs(link.substr(0, slash));
+      ::unlink(link.c_str());
+      if (::symlink(m.second.c_str(), link.c_str()) != 0) make_dirs(link);
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    pods_[uid] = rt;
+    key_to_uid_[r.ns + "/" + r.name] = uid;
+  }
+
+  if (!rt->gpu_ok) {
+    // UnexpectedAdmissionError: the device plugin could not satisfy the request
+    c_->update_with_retry(
+        "v1", "Pod", r.ns, r.name,
+        [&](Json& o) {
+          if (o.at_path({"status", "phase"}).as_string() == "Failed") return false;
+          o["status"]["phase"] = "Failed";
+          o["status"]["reason"] = "UnexpectedAdmissionError";
+          o["status"]["message"] = "Allocate failed due to requested number of devices unavailable for amd.com/gpu";
+          return true;
+        },
+        true);
+    return {};
+  }
+
+  // ---- run containers -------------------------------------------------------------------------------
+  const Json& spec = pod["spec"];
+  auto container_spec = [&](const ContainerRt& cr) -> const Json& {
+    for (const auto& c : spec[cr.init ? "initContainers" : "containers"].as_array())
+      if (c["name"].as_string() == cr.name) return c;
+    static const Json empty;
+    return empty;
+  };
+  auto env_for = [&](const Json& c, std::vector<std::string>& envv, std::map<std::string, std::string>& envm) {
+    auto set = [&](const std::string& k, const std::string& v) { envm[k] = v; };
+    for (char** e = environ; *e; ++e) {
+      std::string kv = *e;
+      size_t eq = kv.find('=');
+      if (eq == std::string::npos) continue;
+      std::string k = kv.substr(0, eq);
+      // pass through the host runtime basics only (containers do not inherit the kubelet env)
+      if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || starts_with(k, "HSA_") ||
+          starts_with(k, "KFAMD_") || starts_with(k, "ROCM") || k == "OMP_NUM_THREADS" || k == "PYTHONUNBUFFERED")
+        set(k, kv.substr(eq + 1));
+    }
+    const std::string rootfs = rt->dir + "/rootfs";
+    std::string home = rootfs + "/home/jovyan";
+    auto hm = rt->mounts.find("/home/jovyan");
+    if (hm != rt->mounts.end()) home = hm->second;
+    make_dirs(home);
+    set("HOME", home);
+    set("HOSTNAME", r.name);
+    set("POD_NAME", r.name);
+    set("POD_NAMESPACE", r.ns);
+    set("POD_IP", rt->ip);
+    set("KFAMD_POD_DIR", rt->dir);
+    set("KFAMD_ROOTFS", rootfs);
+    set("KFAMD_TERMINATION_LOG", rt->dir + "/" + c["name"].as_string() + ".termination-log");
+    Json mounts = Json::object();
+    for (const auto& m : rt->mounts) mounts[m.first] = m.second;
+    set("KFAMD_VOLUME_MOUNTS", mounts.dump());
+    set("PYTHONPATH", cfg_.repo_root);
+    set("PYTHONUNBUFFERED", "1");
+    {
+      std::vector<std::string> ports;
+      for (const auto& p : c["ports"].as_array()) ports.push_back(std::to_string(p["containerPort"].as_int()));
+      set("KFAMD_CONTAINER_PORTS", join(ports, ","));
+      set("KFAMD_CONTAINER_NAME", c["name"].as_string());
+    }
+    Url u;
+    if (Url::parse(cfg_.api_url, u)) {
+      set("KUBERNETES_SERVICE_HOST", u.host);
+      set("KUBERNETES_SERVICE_PORT", std::to_string(u.port));
+      set("KFAMD_API_URL", cfg_.api_url);
+    }
+    // GPU wiring from the device plugin allocation
+    const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0;
+    if (wants_gpu && !rt->gpus.devices.empty()) {
+      for (const auto& ev : gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1).as_array())
+        set(ev["name"].as_string(), ev["value"].as_string());
+    }
+    for (const auto& ef : c["envFrom"].as_array()) {
+      const bool secret = ef["secretRef"].is_object();
+      const std::string name = secret ? ef.at_path({"secretRef", "name"}).as_string() : ef.at_path({"configMapRef", "name"}).as_string();
+      Json src;
+      if (c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, name, src)) continue;
+      for (const auto& m : src["data"].as_object())
+        set(ef["prefix"].as_string() + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
+    }
+    for (const auto& ev : c["env"].as_array()) {
+      const std::string name = ev["name"].as_string();
+      if (ev.has("value")) {
+        set(name, expand_vars(ev["value"].as_string(), envm));
+        continue;
+      }
+      const Json& vf = ev["valueFrom"];
+      if (vf["fieldRef"].is_object()) {
+        const std::string path = vf.at_path({"fieldRef", "fieldPath"}).as_string();
+        if (path == "metadata.name") set(name, r.name);
+        else if (path == "metadata.namespace") set(name, r.ns);
+        else if (path == "status.podIP") set(name, rt->ip);
+        else if (path == "spec.nodeName") set(name, cfg_.node_name);
+        else if (path == "metadata.uid") set(name, uid);
+        else if (starts_with(path, "metadata.annotations['")) set(name, annotation(pod, path.substr(22, path.size() - 24)));
+        else if (starts_with(path, "metadata.labels['")) set(name, label(pod, path.substr(17, path.size() - 19)));
+      } else if (vf["configMapKeyRef"].is_object() || vf["secretKeyRef"].is_object()) {
+        const bool secret = vf["secretKeyRef"].is_object();
+        const Json& ref = secret ? vf["secretKeyRef"] : vf["configMapKeyRef"];
+        Json src;
+        if (!c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, ref["name"].as_string(), src)) {
+          const Json& v = src["data"][ref["key"].as_string()];
+          if (v.is_string()) set(name, secret ? base64_decode(v.as_string()) : v.as_string());
+        }
+      } else if (vf["resourceFieldRef"].is_object()) {
+        const std::string res = vf.at_path({"resourceFieldRef", "resource"}).as_string();
+        auto parts = split(res, '.');
+        if (parts.size() == 2) set(name, c.at_path({"resources", parts[0].c_str(), parts[1].c_str()}).as_string());
+      }
+    }
+    envv.clear();
+    for (auto& kv : envm) envv.push_back(kv.first + "=" + kv.second);
+  };
+  auto start_container = [&](ContainerRt& cr) {
+    const Json& c = container_spec(cr);
+    std::vector<std::string> envv;
+    std::map<std::string, std::string> envm;
+    env_for(c, envv, envm);
+    std::string why;
+    std::vector<std::string> argv = resolve_argv(c, &why);
+    for (auto& a : argv) a = expand_vars(a, envm);
+    std::string wd = c["workingDir"].as_string();
+    std::string cwd = rt->dir + "/rootfs";
+    if (!wd.empty()) {
+      auto m = rt->mounts.find(wd);
+      cwd = m != rt->mounts.end() ? m->second : rt->dir + "/rootfs" + wd;
+      make_dirs(cwd);
+      // follow a symlinked mount point
+      char buf[4096];
+      if (!realpath(cwd.c_str(), buf)) make_dirs(cwd);
+    }
+    ::unlink(cr.term_path.c_str());
+    std::string serr;
+    {
+      std::ofstream lf(cr.log_path, std::ios::app);
+      lf << "# kflite: starting " << cr.name << " (" << why << "): " << join(argv, " ") << "\n";
+    }
+    pid_t pid = spawn(argv, envv, cwd, cr.log_path, &serr);
+    if (pid < 0) {
+      cr.state = "waiting";
+      cr.reason = "CreateContainerError";
+      cr.message = serr;
+      rec_->event(pod, "Warning", "Failed", "Error: " + serr);
+      cr.backoff_until = now_seconds() + cfg_.restart_backoff;
+      return;
+    }
+    cr.pid = pid;
+    cr.state = "running";
+    cr.reason = "";
+    cr.started_at = ms_now();
+    cr.run_started = now_seconds();
+    cr.ready = false;
+    cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
+    const Json& sp = c["startupProbe"];
+    cr.started_probe_ok = !sp.is_object();
+    cr.next_startup_probe = now_seconds() + static_cast<double>(probe_i(sp, "initialDelaySeconds", 0));
+    cr.next_ready_probe = now_seconds() + static_cast<double>(probe_i(c["readinessProbe"], "initialDelaySeconds", 0));
+    cr.next_live_probe = now_seconds() + static_cast<double>(probe_i(c["livenessProbe"], "initialDelaySeconds", 0));
+    rec_->event(pod, "Normal", "Started", "Started container " + cr.name);
+  };
+  auto run_probe = [&](const Json& probe, const Json& c) -> bool {
+    const int timeout = static_cast<int>(probe_i(probe, "timeoutSeconds", 1)) * 1000;
+    auto port_of = [&](const Json& p) -> int {
+      if (p.is_number()) return static_cast<int>(p.as_int());
+      for (const auto& cp : c["ports"].as_array())
+        if (cp["name"].as_string() == p.as_string()) return static_cast<int>(cp["containerPort"].as_int());
+      return std::atoi(p.as_string().c_str());
+    };
+    if (probe["httpGet"].is_object()) {
+      const Json& hg = probe["httpGet"];
+      std::string host = hg["host"].as_string_or(rt->ip);
+      std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
+      Headers h;
+      for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
+      HttpResult res = http_request("GET", url, "", h, timeout);
+      return res.status >= 200 && res.status < 400;
+    }
+    if (probe["tcpSocket"].is_object()) return tcp_connect(rt->ip, port_of(probe.at_path({"tcpSocket", "port"})), timeout);
+    if (probe["exec"].is_object()) {
+      std::vector<std::string> argv;
+      for (const auto& a : probe.at_path({"exec", "command"}).as_array()) argv.push_back(a.as_string());
+      if (argv.empty()) return false;
+      std::vector<std::string> envv;
+      std::map<std::string, std::string> envm;
+      env_for(c, envv, envm);
+      pid_t pid = spawn(argv, envv, rt->dir + "/rootfs", rt->dir + "/probe.log", nullptr);
+      if (pid < 0) return false;
+      double deadline = now_seconds() + timeout / 1000.0;
+      int code = 0;
+      std::string reason;
+      while (!reap(pid, code, reason)) {
+        if (now_seconds() > deadline) {
+          ::kill(-pid, SIGKILL);
+          deadline = now_seconds() + 5;
+        }
+        ::usleep(2000);
+      }
+      return code == 0;
+    }
+    return true;
+  };
+  auto handle_exit = [&](ContainerRt& cr) {
+    int code = 0;
+    std::string reason;
+    if (cr.pid <= 0 || cr.state != "running" || !reap(cr.pid, code, reason)) return false;
+    cr.pid = -1;
+    cr.state = "terminated";
+    cr.exit_code = code;
+    cr.reason = reason;
+    cr.finished_at = ms_now();
+    cr.ready = false;
+    std::string msg;
+    if (read_file(cr.term_path, msg)) cr.message = msg.substr(0, 4096);
+    else cr.message.clear();
+    return true;
+  };
+  double next_wake = 1.0;
+  // init containers, sequentially
+  while (rt->init_done < rt->init.size() && !rt->init_failed) {
+    ContainerRt& ic = rt->init[rt->init_done];
+    if (ic.state == "waiting") {
+      if (now_seconds() < ic.backoff_until) {
+        next_wake = std::min(next_wake, ic.backoff_until - now_seconds());
+        break;
+      }
+      start_container(ic);
+      next_wake = 0.05;
+      break;
+    }
+    if (ic.state == "running") {
+      if (handle_exit(ic)) continue;
+      next_wake = 0.05;
+      break;
+    }
+    // terminated
+    if (ic.exit_code == 0) {
+      rt->init_done++;
+      continue;
+    }
+    if (restart_policy == "Never") {
+      rt->init_failed = true;
+      break;
+    }
+    ic.last_state = Json{{"terminated", Json{{"exitCode", ic.exit_code}, {"reason", ic.reason}, {"startedAt", ic.started_at},
+                                             {"finishedAt", ic.finished_at}, {"message", ic.message}}}};
+    ic.restarts++;
+    ic.state = "waiting";
+    ic.reason = "CrashLoopBackOff";
+    ic.backoff_until = now_seconds() + std::min(300.0, cfg_.restart_backoff * (1 << std::min(ic.restarts - 1, 5)));
+    rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + ic.name);
+    break;
+  }
+  const bool initialized = rt->init_done == rt->init.size();
+  if (initialized) {
+    for (auto& cr : rt->main) {
+      const Json& c = container_spec(cr);
+      if (cr.state == "running") {
+        if (handle_exit(cr)) {
+          // fallthrough to restart handling below
+        } else {
+          const double now = now_seconds();
+          // startup probe gates readiness/liveness
+          const Json& sp = c["startupProbe"];
+          if (!cr.started_probe_ok && now >= cr.next_startup_probe) {
+            if (run_probe(sp, c)) {
+              if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
+            } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
+              rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
+              ::kill(-cr.pid, SIGKILL);
+            }
+            cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
+          }
+          if (cr.started_probe_ok) {
+            const Json& rp = c["readinessProbe"];
+            if (!rp.is_object()) {
+              cr.ready = true;
+            } else if (now >= cr.next_ready_probe) {
+              bool ok = run_probe(rp, c);
+              if (ok) {
+                cr.ready_fail = 0;
+                if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
+              } else {
+                cr.ready_ok = 0;
+                if (++cr.ready_fail >= probe_i(rp, "failureThreshold", 3)) {
+                  if (cr.ready) rec_->event(pod, "Warning", "Unhealthy", "Readiness probe failed");
+                  cr.ready = false;
+                }
+              }
+              // probe fast until the first success (cold-start latency), then at periodSeconds
+              cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.1);
+            }
+            const Json& lp = c["livenessProbe"];
+            if (lp.is_object() && now >= cr.next_live_probe) {
+              if (run_probe(lp, c)) {
+                cr.live_fail = 0;
+              } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
+                rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
+                ::kill(-cr.pid, SIGKILL);
+              }
+              cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
+            }
+            if (!cr.ready) next_wake = std::min(next_wake, 0.1);
+            else next_wake = std::min(next_wake, std::max(0.2, std::min(cr.next_ready_probe, cr.next_live_probe) - now));
+          } else {
+            next_wake = std::min(next_wake, 0.1);
+          }
+          continue;
+        }
+      }
+      if (cr.state == "terminated") {
+        const bool restart = restart_policy == "Always" || (restart_policy == "OnFailure" && cr.exit_code != 0);
+        if (!restart) continue;
+        cr.last_state = Json{{"terminated", Json{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at},
+                                                 {"finishedAt", cr.finished_at}, {"message", cr.message}}}};
+        cr.restarts++;
+        cr.state = "waiting";
+        cr.reason = "CrashLoopBackOff";
+        double ran = now_seconds() - cr.run_started;
+        double backoff = ran > 600 ? cfg_.restart_backoff : std::min(300.0, cfg_.restart_backoff * (1 << std::min(cr.restarts - 1, 5)));
+        cr.backoff_until = now_seconds() + backoff;
+        rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + cr.name);
+      }
+      if (cr.state == "waiting") {
+        if (now_seconds() >= cr.backoff_until) {
+          start_container(cr);
+          next_wake = std::min(next_wake, 0.05);
+        } else {
+          next_wake = std::min(next_wake, cr.backoff_until - now_seconds());
+        }
+      }
+    }
+  }
+
+  // ---- status --------------------------------------------------------------------------------------
+  auto cstatus = [&](const ContainerRt& cr) {
+    const Json& c = container_spec(cr);
+    Json state;
+    if (cr.state == "running") {
+      state = Json{{"running", Json{{"startedAt", cr.started_at}}}};
+    } else if (cr.state == "terminated") {
+      Json t{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at}, {"finishedAt", cr.finished_at},
+             {"containerID", "kflite://" + cr.name}};
+      if (!cr.message.empty()) t["message"] = cr.message;
+      state = Json{{"terminated", t}};
+    } else {
+      Json w{{"reason", cr.reason.empty() ? "ContainerCreating" : cr.reason}};
+      if (!cr.message.empty()) w["message"] = cr.message;
+      state = Json{{"waiting", w}};
+    }
+    Json s{{"name", cr.name}, {"state", state}, {"lastState", cr.last_state}, {"ready", cr.ready},
+           {"restartCount", cr.restarts}, {"image", c["image"]}, {"imageID", "kflite-recipe://" + c["image"].as_string()},
+           {"started", cr.state == "running"}};
+    if (cr.pid > 0) s["containerID"] = "kflite://" + std::to_string(cr.pid);
+    return s;
+  };
+  Json init_st = Json::array(), main_st = Json::array();
+  for (const auto& cr : rt->init) init_st.push_back(cstatus(cr));
+  for (const auto& cr : rt->main) main_st.push_back(cstatus(cr));
+  bool all_ready = initialized && !rt->main.empty(), all_running = initialized, any_running = false, all_done = initialized,
+       any_failed = rt->init_failed;
+  for (const auto& cr : rt->main) {
+    all_ready = all_ready && cr.ready;
+    all_running = all_running && cr.state == "running";
+    any_running = any_running || cr.state == "running";
+    all_done = all_done && cr.state == "terminated";
+    any_failed = any_failed || (cr.state == "terminated" && cr.exit_code != 0);
+  }
+  std::string new_phase = "Pending";
+  if (rt->init_failed) new_phase = "Failed";
+  else if (initialized && all_done && restart_policy != "Always") new_phase = any_failed ? "Failed" : "Succeeded";
+  else if (initialized && (any_running || all_done)) new_phase = "Running";
+
+  ApiError ue = c_->update_with_retry(
+      "v1", "Pod", r.ns, r.name,
+      [&](Json& o) {
+        if (o.str_at({"metadata", "uid"}) != uid) return false;
+        Json st = o["status"];
+        const Json old_st = st;
+        st["phase"] = new_phase;
+        st["hostIP"] = "127.0.0.1";
+        st["podIP"] = rt->ip;
+        st["podIPs"] = Json::array({Json{{"ip", rt->ip}}});
+        st["startTime"] = rt->start_time;
+        st["containerStatuses"] = main_st;
+        if (!rt->init.empty()) st["initContainerStatuses"] = init_st;
+        auto cond = [&](const char* type, bool ok, const std::string& reason) {
+          Json conds = Json::array();
+          std::string ts = ms_now();
+          for (const auto& c : st["conditions"].as_array()) {
+            if (c["type"].as_string() == type) {
+              if (c["status"].as_string() == (ok ? "True" : "False")) ts = c["lastTransitionTime"].as_string();
+              continue;
+            }
+            conds.push_back(c);
+          }
+          Json c{{"type", type}, {"status", ok ? "True" : "False"}, {"lastProbeTime", Json()}, {"lastTransitionTime", ts}};
+          if (!ok && !reason.empty()) c["reason"] = reason;
+          conds.push_back(c);
+          st["conditions"] = conds;
+        };
+        cond("Initialized", initialized, "ContainersNotInitialized");
+        cond("ContainersReady", all_ready, "ContainersNotReady");
+        cond("Ready", all_ready, "ContainersNotReady");
+        (void)all_running;
+        if (st == old_st) return false;
+        o["status"] = st;
+        return true;
+      },
+      true);
+  if (ue && ue.code != 404) *err = ue.message;
+  return Result::after(std::max(0.02, next_wake));
+}
+
+void Kubelet::setup(Manager& mgr) {
+  ctl_ = std::make_shared<Controller>("kubelet", [this](const Request& r, std::string* e) { return reconcile(r, e); }, 4);
+  const std::string node = cfg_.node_name;
+  ctl_->For(mgr.informer("v1", "Pod"), [node](const std::string& type, const Json& p, const Json* old) {
+    if (type == "DELETED") return true;
+    const std::string& n = p.at_path({"spec", "nodeName"}).as_string();
+    if (n != node) return false;
+    // status-only writes of our own do not need a new pass (the periodic requeue drives probes)
+    if (type == "MODIFIED" && old && p["spec"] == (*old)["spec"] && p["metadata"]["deletionTimestamp"] == (*old)["metadata"]["deletionTimestamp"])
+      return false;
+    return true;
+  });
+  mgr.add(ctl_);
+}
+
+}  // namespace kf

@@ -1,0 +1,137 @@
+// node.h — the single-node runtime that the reference takes from Kubernetes L0
+// (kube-scheduler, kubelet + AMD device plugin, Istio ingress gateway), re-designed for one
+// 8 x MI355X node:
+//
+//   Scheduler  filters nodes (Ready, taints/tolerations, nodeSelector, required node affinity,
+//              cpu / memory / amd.com/gpu / amd.com/gpu-memory fit) and scores them (preferred
+//              affinity, least-allocated); binds by setting spec.nodeName; records
+//              PodScheduled + Scheduled/FailedScheduling events.
+//   Kubelet    registers the Node (capacity from the xGMI topology: amd.com/gpu, amd.com/gpu-memory
+//              in GiB), runs pods as supervised process groups ("containers" = processes; images
+//              resolve to process recipes), allocates GPUs through the topology-aware allocator at
+//              admission (device-plugin Allocate) and injects HIP_VISIBLE_DEVICES + RCCL/torchrun env,
+//              gives every pod its own loopback IP (127.20.x.y) so every notebook listens on :8888,
+//              materialises volumes (emptyDir / PVC / configMap / secret) under the pod sandbox,
+//              runs init containers in order, HTTP/TCP/exec probes, restart policies with back-off,
+//              graceful termination, termination messages, container logs, and full pod status with
+//              millisecond timestamps (the cold-start phase breakdown of SURVEY §5.1).
+//   Gateway    HTTP reverse proxy that serves Istio VirtualServices (uri prefix match, rewrite,
+//              headers.request.set, timeout) and OpenShift Routes for the embedded cluster.
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/http.h"
+#include "gpu/topology.h"
+#include "runtime/runtime.h"
+
+namespace kf {
+
+// Resource accounting helpers (shared with the quota admission plugin).
+// Effective pod request: max(sum(containers), max(initContainers)) per resource; extended
+// resources default their request to the limit.
+Json pod_requests(const Json& pod);
+double resource_value(const std::string& name, const Json& quantity);  // cpu cores, bytes, counts
+
+class Scheduler {
+ public:
+  explicit Scheduler(std::shared_ptr<Client> c) : c_(std::move(c)) {}
+  void setup(Manager& mgr);
+  Result reconcile(const Request& r, std::string* err);
+  // pure helpers (unit-tested)
+  static bool tolerates(const Json& pod, const Json& node);
+  static bool matches_affinity(const Json& pod, const Json& node);
+  static int64_t preferred_score(const Json& pod, const Json& node);
+
+ private:
+  std::shared_ptr<Client> c_;
+  Informer* pods_ = nullptr;
+  Informer* nodes_ = nullptr;
+  std::unique_ptr<EventRecorder> rec_;
+  std::shared_ptr<Controller> ctl_;
+};
+
+struct KubeletConfig {
+  std::string node_name = "mi355x-node-0";
+  std::string root_dir;      // pod sandboxes, PV dirs, logs
+  std::string repo_root;     // kubeflow_rm_amd location for image recipes
+  std::string bin_dir;       // native binaries (kfamd-readiness)
+  std::string python = "python3";
+  std::string api_url;       // exported to pods as KUBERNETES_SERVICE_HOST/PORT
+  std::string pod_ip_prefix = "127.20";
+  double restart_backoff = 10.0;
+  int gpus = -1;
+  std::string recipes_file;  // optional JSON overriding the image recipes
+};
+
+class Kubelet {
+ public:
+  Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg);
+  ~Kubelet();
+  void setup(Manager& mgr);
+  void start();  // node registration + heartbeat
+  void stop();
+  Result reconcile(const Request& r, std::string* err);
+  bool read_logs(const std::string& ns, const std::string& pod, const std::string& container, int64_t tail,
+                 std::string& out);
+  GpuAllocator& gpus() { return *alloc_; }
+  const std::string& node_name() const { return cfg_.node_name; }
+
+  struct PodRuntime;
+  // image -> argv resolution (unit-tested)
+  std::vector<std::string> resolve_argv(const Json& container, std::string* why = nullptr) const;
+
+ private:
+  Json node_object() const;
+  void heartbeat_loop();
+  void terminate_pod(PodRuntime& rt, int64_t grace_s);
+  std::shared_ptr<Client> c_;
+  KubeletConfig cfg_;
+  std::unique_ptr<GpuAllocator> alloc_;
+  Json recipes_;
+  std::mutex mu_;
+  std::map<std::string, std::shared_ptr<PodRuntime>> pods_;  // uid -> runtime
+  std::map<std::string, std::string> key_to_uid_;            // ns/name -> uid
+  uint32_t next_ip_ = 2;
+  std::unique_ptr<EventRecorder> rec_;
+  std::shared_ptr<Controller> ctl_;
+  std::atomic<bool> running_{false};
+  std::thread hb_;
+};
+
+class Gateway {
+ public:
+  Gateway(std::shared_ptr<Client> c, std::string gateway_name);
+  ~Gateway();
+  void setup(Manager& mgr);
+  bool start(const std::string& addr, int port, std::string* err);
+  void stop();
+  int port() const { return srv_ ? srv_->port() : 0; }
+  void handle(HttpRequest& req, HttpResponse& resp);
+
+  struct Route {
+    std::string prefix, rewrite, dest_host;
+    int dest_port = 80;
+    Json headers;
+    double timeout_s = 300;
+    bool exact = false;
+  };
+  // best matching VirtualService route for host + path (unit-tested)
+  static bool match(const std::vector<Json>& vss, const std::string& gateway, const std::string& host,
+                    const std::string& path, Route& out);
+
+ private:
+  std::shared_ptr<Client> c_;
+  std::string gw_;
+  Informer* vs_ = nullptr;
+  Informer* routes_ = nullptr;
+  std::unique_ptr<HttpServer> srv_;
+};
+
+}  // namespace kf
