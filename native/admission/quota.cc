@@ -1,0 +1,206 @@
+// quota.cc — ResourceQuota admission + status controller with MI355X GPU / HBM accounting (K7).
+#include <algorithm>
+#include <cmath>
+
+#include "admission/admission.h"
+#include "controllers/common.h"
+#include "core/util.h"
+#include "node/node.h"
+
+namespace kf {
+
+std::map<std::string, double> pod_quota_usage(const Json& pod, int64_t hbm_gib_per_gpu) {
+  std::map<std::string, double> use;
+  use["pods"] = 1;
+  use["count/pods"] = 1;
+  auto acc = [&](const Json& list, bool init) {
+    std::map<std::string, double> req, lim;
+    for (const auto& c : list.as_array()) {
+      std::map<std::string, double> r1, l1;
+      for (const auto& m : c.at_path({"resources", "limits"}).as_object()) l1[m.first] = resource_value(m.first, m.second);
+      for (const auto& m : c.at_path({"resources", "requests"}).as_object()) r1[m.first] = resource_value(m.first, m.second);
+      for (auto& kv : l1)
+        if (!r1.count(kv.first)) r1[kv.first] = kv.second;  // requests default to limits
+      for (auto& kv : r1) req[kv.first] = init ? std::max(req[kv.first], kv.second) : req[kv.first] + kv.second;
+      for (auto& kv : l1) lim[kv.first] = init ? std::max(lim[kv.first], kv.second) : lim[kv.first] + kv.second;
+    }
+    return std::make_pair(req, lim);
+  };
+  auto app = acc(pod.at_path({"spec", "containers"}), false);
+  auto ini = acc(pod.at_path({"spec", "initContainers"}), true);
+  for (auto* m : {&app.first, &ini.first})
+    for (auto& kv : *m) use["requests." + kv.first] = std::max(use["requests." + kv.first], kv.second);
+  for (auto* m : {&app.second, &ini.second})
+    for (auto& kv : *m) use["limits." + kv.first] = std::max(use["limits." + kv.first], kv.second);
+  // bare cpu / memory quota keys mean requests
+  if (use.count("requests.cpu")) use["cpu"] = use["requests.cpu"];
+  if (use.count("requests.memory")) use["memory"] = use["requests.memory"];
+  // MI355X: GPUs and HBM. A GPU request implies its 288 GiB of HBM unless stated explicitly.
+  const double gpus = use.count("requests.amd.com/gpu") ? use["requests.amd.com/gpu"] : 0;
+  if (gpus > 0) {
+    use["amd.com/gpu"] = gpus;
+    if (!use.count("requests.amd.com/gpu-memory")) use["requests.amd.com/gpu-memory"] = gpus * static_cast<double>(hbm_gib_per_gpu);
+  }
+  if (use.count("requests.amd.com/gpu-memory")) use["amd.com/gpu-memory"] = use["requests.amd.com/gpu-memory"];
+  return use;
+}
+
+namespace {
+bool pod_counts(const Json& p) {
+  const std::string& ph = p.at_path({"status", "phase"}).as_string();
+  return ph != "Succeeded" && ph != "Failed" && !p.at_path({"metadata", "deletionTimestamp"}).is_string();
+}
+double hard_value(const std::string& key, const Json& q) {
+  // amd.com/gpu-memory quota is expressed in GiB ("2304") or as a quantity ("2304Gi")
+  if (contains(key, "gpu-memory")) {
+    auto v = parse_quantity(q.is_string() ? q.as_string() : q.dump());
+    if (!v) return 0;
+    const std::string s = q.is_string() ? q.as_string() : "";
+    return (ends_with(s, "i") || ends_with(s, "G") || ends_with(s, "M") || ends_with(s, "T")) ? *v / (1024.0 * 1024.0 * 1024.0) : *v;
+  }
+  return resource_value(key, q);
+}
+std::string fmt_num(double v) {
+  char buf[64];
+  if (std::fabs(v - std::round(v)) < 1e-9) std::snprintf(buf, sizeof buf, "%.0f", v);
+  else std::snprintf(buf, sizeof buf, "%.3f", v);
+  return buf;
+}
+}  // namespace
+
+AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
+  return [c, hbm](AdmissionAttrs& a) -> ApiError {
+    if (a.operation != "CREATE" || a.res->kind != "Pod" || !a.res->group.empty() || !a.object) return {};
+    Json quotas;
+    if (c->list("v1", "ResourceQuota", a.ns, ListOptions(), quotas)) return {};
+    if (quotas["items"].empty()) return {};
+    Json pods;
+    c->list("v1", "Pod", a.ns, ListOptions(), pods);
+    std::map<std::string, double> used;
+    for (const auto& p : pods["items"].as_array())
+      if (pod_counts(p))
+        for (auto& kv : pod_quota_usage(p, hbm)) used[kv.first] += kv.second;
+    auto want = pod_quota_usage(*a.object, hbm);
+    for (const auto& q : quotas["items"].as_array()) {
+      std::vector<std::string> exceeded;
+      for (const auto& h : q.at_path({"spec", "hard"}).as_object()) {
+        auto w = want.find(h.first);
+        if (w == want.end() || w->second <= 0) continue;
+        const double hard = hard_value(h.first, h.second);
+        if (used[h.first] + w->second > hard + 1e-9)
+          exceeded.push_back(h.first + "=" + fmt_num(w->second) + ", used: " + h.first + "=" + fmt_num(used[h.first]) +
+                             ", limited: " + h.first + "=" + fmt_num(hard));
+      }
+      if (!exceeded.empty())
+        return ApiError{403, "Forbidden", "pods \"" + a.name + "\" is forbidden: exceeded quota: " + q.str_at({"metadata", "name"}) +
+                                              ", requested: " + join(exceeded, "; ")};
+    }
+    return {};
+  };
+}
+
+Result QuotaController::reconcile(const Request& r, std::string* err) {
+  Json q;
+  ApiError e = c_->get("v1", "ResourceQuota", r.ns, r.name, q);
+  if (e.code == 404) return {};
+  if (e) {
+    *err = e.message;
+    return {};
+  }
+  std::map<std::string, double> used;
+  for (const auto& p : pods_->list(r.ns))
+    if (pod_counts(p))
+      for (auto& kv : pod_quota_usage(p, hbm_)) used[kv.first] += kv.second;
+  Json hard = q.at_path({"spec", "hard"});
+  Json u = Json::object();
+  for (const auto& h : hard.as_object()) u[h.first] = fmt_num(used[h.first]);
+  Json status{{"hard", hard}, {"used", u}};
+  if (q["status"] != status) {
+    q["status"] = status;
+    e = c_->update_status(q);
+    if (e && e.code != 409) *err = e.message;
+  }
+  return {};
+}
+
+void QuotaController::setup(Manager& mgr) {
+  pods_ = &mgr.informer("v1", "Pod");
+  Informer& quotas = mgr.informer("v1", "ResourceQuota");
+  ctl_ = std::make_shared<Controller>("resourcequota", [this](const Request& r, std::string* e) { return reconcile(r, e); });
+  ctl_->For(quotas);
+  ctl_->Watches(*pods_, [&quotas](const std::string&, const Json& p) {
+    std::vector<Request> out;
+    for (const auto& q : quotas.list(p.str_at({"metadata", "namespace"})))
+      out.push_back({q.str_at({"metadata", "namespace"}), q.str_at({"metadata", "name"})});
+    return out;
+  });
+  mgr.add(ctl_);
+}
+
+// ---- HTTP AdmissionReview server -----------------------------------------------------------------
+void AdmissionWebhookServer::add(const std::string& path, AdmissionFn fn, bool mutating, std::shared_ptr<const ResourceInfo> res) {
+  routes_[path] = Entry{std::move(fn), mutating, std::move(res)};
+}
+
+Json AdmissionWebhookServer::review(const std::string& path, const Json& ar) {
+  const Json& req = ar["request"];
+  Json resp{{"uid", req["uid"]}, {"allowed", true}};
+  auto it = routes_.find(path);
+  if (it == routes_.end()) {
+    resp["allowed"] = false;
+    resp["status"] = Json{{"code", 404}, {"message", "no admission handler at " + path}};
+  } else {
+    AdmissionAttrs a;
+    a.operation = req["operation"].as_string();
+    a.res = it->second.res;
+    a.subresource = req["subResource"].as_string();
+    a.ns = req["namespace"].as_string();
+    a.name = req["name"].as_string();
+    a.version = req.at_path({"kind", "version"}).as_string();
+    Json obj = req["object"];
+    Json old = req["oldObject"];
+    UserInfo u;
+    u.username = req.at_path({"userInfo", "username"}).as_string();
+    a.object = obj.is_null() ? nullptr : &obj;
+    a.old_object = old.is_null() ? nullptr : &old;
+    a.user = &u;
+    a.dry_run = req["dryRun"].as_bool();
+    ApiError e = it->second.fn(a);
+    if (e) {
+      resp["allowed"] = false;
+      resp["status"] = Json{{"code", e.code}, {"message", e.message}, {"reason", e.reason}};
+    } else if (it->second.mutating && !req["object"].is_null()) {
+      Json patch = diff_json_patch(req["object"], obj);
+      if (!patch.empty()) {
+        resp["patch"] = base64_encode(patch.dump());
+        resp["patchType"] = "JSONPatch";
+      }
+    }
+  }
+  return Json{{"apiVersion", "admission.k8s.io/v1"}, {"kind", "AdmissionReview"}, {"response", resp}};
+}
+
+bool AdmissionWebhookServer::start(const std::string& addr, int port, std::string* err) {
+  srv_ = std::make_unique<HttpServer>();
+  if (!srv_->listen(addr, port, err)) return false;
+  srv_->set_handler([this](HttpRequest& req, HttpResponse& resp) {
+    if (req.path == "/healthz" || req.path == "/readyz") {
+      resp.text(200, "ok");
+      return;
+    }
+    Json ar;
+    if (req.method != "POST" || !Json::try_parse(req.body, ar)) {
+      resp.json(400, R"({"error":"expected an AdmissionReview"})");
+      return;
+    }
+    resp.json(200, review(req.path, ar).dump());
+  });
+  srv_->start();
+  return true;
+}
+
+void AdmissionWebhookServer::stop() {
+  if (srv_) srv_->stop();
+}
+
+}  // namespace kf

@@ -626,6 +626,7 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
   a.dry_run = o.dry_run;
   err = run_admission(a, true);
   if (err) return err;
+  apply_defaults(res, obj, false);  // mutating admission may add containers: default them too
   to_storage(res, obj);
   obj["metadata"]["namespace"] = ns;
   if (!res->namespaced) obj["metadata"].erase("namespace");
@@ -799,6 +800,7 @@ ApiError ApiServer::r_update(std::shared_ptr<const ResourceInfo> res, const std:
   a.dry_run = o.dry_run;
   ApiError err = run_admission(a, true);
   if (err) return err;
+  if (subresource.empty()) apply_defaults(res, next, false);
   to_storage(res, next);
   err = validate(res, next, &old, subresource);
   if (err) return err;

@@ -247,7 +247,8 @@ bool ApiServer::authorize(const UserInfo& u, const std::string& verb, const std:
     bool subj = false;
     for (const auto& s : b["subjects"].as_array()) subj = subj || subject_matches(s, u);
     if (!subj) continue;
-    for (const auto& rule : rules_of("ClusterRole", "", b.str_at({"roleRef", "name"})).as_array())
+    const Json rules = rules_of("ClusterRole", "", b.str_at({"roleRef", "name"}));
+    for (const auto& rule : rules.as_array())
       if (rule_allows(rule, verb, group, resource, subresource, name, non_resource)) {
         if (reason) *reason = "RBAC: allowed by ClusterRoleBinding \"" + b.str_at({"metadata", "name"}) + "\"";
         return true;
@@ -260,7 +261,8 @@ bool ApiServer::authorize(const UserInfo& u, const std::string& verb, const std:
       bool subj = false;
       for (const auto& s : b["subjects"].as_array()) subj = subj || subject_matches(s, u);
       if (!subj) continue;
-      for (const auto& rule : rules_of(b.str_at({"roleRef", "kind"}), ns, b.str_at({"roleRef", "name"})).as_array())
+      const Json rules = rules_of(b.str_at({"roleRef", "kind"}), ns, b.str_at({"roleRef", "name"}));
+      for (const auto& rule : rules.as_array())
         if (rule_allows(rule, verb, group, resource, subresource, name, non_resource)) {
           if (reason) *reason = "RBAC: allowed by RoleBinding \"" + b.str_at({"metadata", "name"}) + "/" + ns + "\"";
           return true;

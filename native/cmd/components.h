@@ -32,7 +32,7 @@ struct ComponentFlags {
   std::string cluster_admin = "";
   // profile controller
   std::string namespace_labels_path;
-  bool workload_identity = false;
+  std::string workload_identity;  // default GCP service account for the WorkloadIdentity plugin
   // odh
   std::string oauth_proxy_image = "registry.redhat.io/openshift4/ose-oauth-proxy:latest";
   std::string controller_namespace = "opendatahub";
@@ -51,6 +51,7 @@ class Components {
   void stop();
   int gateway_port() const;
   int kfam_port() const;
+  int webhook_port() const;
 
   struct Impl;
 

@@ -3,7 +3,9 @@
 
 #include <unistd.h>
 
+#include "admission/admission.h"
 #include "controllers/builtin.h"
+#include "controllers/profile.h"
 #include "controllers/notebook.h"
 #include "node/node.h"
 #include "core/util.h"
@@ -25,7 +27,7 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("userid-prefix", &userid_prefix, "", "user id prefix (KFAM / profile controller)");
   f.add_string("cluster-admin", &cluster_admin, "", "KFAM cluster admin user");
   f.add_string("namespace-labels-path", &namespace_labels_path, "", "profile controller namespace labels file");
-  f.add_bool("workload-identity", &workload_identity, false, "enable the GCP workload identity plugin");
+  f.add_string("workload-identity", &workload_identity, "", "default GCP service account for the WorkloadIdentity plugin");
   f.add_string("oauth-proxy-image", &oauth_proxy_image, "registry.redhat.io/openshift4/ose-oauth-proxy:latest", "ODH oauth proxy image");
   f.add_string("controller-namespace", &controller_namespace, "opendatahub", "ODH controller namespace");
   f.add_int("webhook-port", &webhook_port, -1, "serve admission webhooks over HTTP on this port (-1 = in-process only)");
@@ -43,6 +45,9 @@ struct Components::Impl {
   std::unique_ptr<Scheduler> scheduler;
   std::unique_ptr<Kubelet> kubelet;
   std::unique_ptr<Gateway> gateway;
+  std::unique_ptr<ProfileReconciler> profile;
+  std::unique_ptr<QuotaController> quota;
+  std::unique_ptr<AdmissionWebhookServer> webhooks;
   std::vector<std::function<void()>> starters, stoppers;
 };
 
@@ -68,6 +73,38 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
   if (enabled.count("culler") && getenv_or("ENABLE_CULLING", "false") == "true") {
     I.culler = std::make_unique<CullingReconciler>(I.c, CullingOptions::from_env(), I.nb_metrics);
     I.culler->setup(mgr);
+  }
+  if (enabled.count("profile")) {
+    ProfileOptions po;
+    po.userid_header = I.f.userid_header;
+    po.userid_prefix = I.f.userid_prefix;
+    po.workload_identity = I.f.workload_identity;
+    po.namespace_labels_path = I.f.namespace_labels_path;
+    I.profile = std::make_unique<ProfileReconciler>(I.c, po, make_configmap_cloud_iam(I.c));
+    I.profile->setup(mgr);
+  }
+  if (enabled.count("webhooks")) {
+    auto pd = make_poddefault_plugin(I.c);
+    auto gpu = make_gpu_readiness_plugin();
+    auto quota = make_quota_plugin(I.c);
+    if (I.api) {
+      // kflite: in-process admission chain (same order as the webhook configurations)
+      I.api->add_mutating_plugin("poddefaults.admission.kubeflow.org", pd);
+      I.api->add_mutating_plugin("gpu-readiness.kfamd.io", gpu);
+      I.api->add_validating_plugin("ResourceQuota", quota);
+    }
+    if (I.f.webhook_port >= 0) {
+      I.webhooks = std::make_unique<AdmissionWebhookServer>();
+      ResourceRegistry reg;
+      auto pods = reg.by_kind("v1", "Pod");
+      I.webhooks->add("/apply-poddefault", pd, true, pods);
+      I.webhooks->add("/gpu-readiness", gpu, true, pods);
+      I.webhooks->add("/quota", quota, false, pods);
+      if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
+      I.stoppers.push_back([&I] { I.webhooks->stop(); });
+    }
+    I.quota = std::make_unique<QuotaController>(I.c);
+    I.quota->setup(mgr);
   }
   if (enabled.count("builtin")) {
     I.builtin = std::make_unique<BuiltinControllers>(I.c);
@@ -132,5 +169,6 @@ void Components::stop() {
 
 int Components::gateway_port() const { return impl_->gateway ? impl_->gateway->port() : 0; }
 int Components::kfam_port() const { return 0; }
+int Components::webhook_port() const { return impl_->webhooks ? impl_->webhooks->port() : 0; }
 
 }  // namespace kf

@@ -250,6 +250,14 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
       Json g;
       if (Json::try_parse(gr, g)) status["gpuReadiness"] = g;
     }
+    // the gpu-readiness init container's termination message (kfamd-readiness JSON summary)
+    for (const auto& ics : pod.at_path({"status", "initContainerStatuses"}).as_array()) {
+      if (ics["name"].as_string() != "gpu-readiness") continue;
+      const Json& t = ics.at_path({"state", "terminated"}).is_object() ? ics.at_path({"state", "terminated"})
+                                                                       : ics.at_path({"lastState", "terminated"});
+      Json g;
+      if (t.is_object() && Json::try_parse(t["message"].as_string(), g)) status["gpuReadiness"] = g;
+    }
     if (pod.at_path({"metadata", "annotations"}).has(ANNOTATION_GPU_IDS))
       status["gpus"] = annotation(pod, ANNOTATION_GPU_IDS);
   }

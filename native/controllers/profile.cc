@@ -1,0 +1,601 @@
+// profile.cc — N12 ProfileReconciler, N13 plugins, N14 monitoring (see profile.h).
+#include "controllers/profile.h"
+
+#include <sys/inotify.h>
+#include <poll.h>
+#include <unistd.h>
+
+#include <algorithm>
+
+#include "core/util.h"
+
+namespace kf {
+
+// ---- monitoring ---------------------------------------------------------------------------------
+namespace {
+std::string trunc30(const std::string& s) { return s.size() > 30 ? s.substr(0, 30) : s; }
+}  // namespace
+
+void inc_request_counter(const std::string& kind, const std::string& component) {
+  static auto c = Registry::global().counter("request_kf", "Number of request_counter", {"component", "kind"});
+  c->inc({component, trunc30(kind)});
+}
+void inc_request_error_counter(const std::string& kind, const std::string& severity, const std::string& component) {
+  static auto c = Registry::global().counter("request_kf_failure", "Number of request_failure_counter",
+                                             {"component", "kind", "severity"});
+  c->inc({component, trunc30(kind), severity});
+}
+Heartbeat::Heartbeat(std::string component, double period_s) : component_(std::move(component)) {
+  static auto hb = Registry::global().counter("service_heartbeat", "Heartbeat signal every 10 seconds", {"component", "severity"});
+  th_ = std::thread([this, period_s] {
+    while (run_) {
+      hb->inc({component_, "minor"});
+      for (int i = 0; i < static_cast<int>(period_s * 10) && run_; ++i) ::usleep(100000);
+    }
+  });
+}
+Heartbeat::~Heartbeat() {
+  run_ = false;
+  if (th_.joinable()) th_.join();
+}
+
+// ---- YAML flat map / namespace labels ----------------------------------------------------------------
+std::map<std::string, std::string> parse_flat_yaml_map(const std::string& text, bool* ok) {
+  std::map<std::string, std::string> out;
+  bool good = true;
+  for (auto line : split(text, '\n')) {
+    size_t hash = std::string::npos;
+    bool in_s = false, in_d = false;
+    for (size_t i = 0; i < line.size(); ++i) {
+      if (line[i] == '\'' && !in_d) in_s = !in_s;
+      if (line[i] == '"' && !in_s) in_d = !in_d;
+      if (line[i] == '#' && !in_s && !in_d && (i == 0 || std::isspace(static_cast<unsigned char>(line[i - 1])))) {
+        hash = i;
+        break;
+      }
+    }
+    if (hash != std::string::npos) line = line.substr(0, hash);
+    line = trim(line);
+    if (line.empty() || line == "---") continue;
+    size_t colon = line.find(": ");
+    if (colon == std::string::npos && ends_with(line, ":")) colon = line.size() - 1;
+    if (colon == std::string::npos) {
+      good = false;
+      continue;
+    }
+    std::string k = trim(line.substr(0, colon)), v = trim(line.substr(colon + 1));
+    auto unq = [](std::string s) {
+      if (s.size() >= 2 && ((s.front() == '"' && s.back() == '"') || (s.front() == '\'' && s.back() == '\'')))
+        return s.substr(1, s.size() - 2);
+      return s;
+    };
+    out[unq(k)] = unq(v);
+  }
+  if (ok) *ok = good;
+  return out;
+}
+
+void set_namespace_labels(Json& ns, const std::map<std::string, std::string>& labels) {
+  Json& l = ns["metadata"]["labels"];
+  if (!l.is_object()) l = Json::object();
+  for (const auto& kv : labels) {
+    const bool exists = l.has(kv.first);
+    if (kv.second.empty()) {
+      if (exists) l.erase(kv.first);
+    } else if (!exists) {
+      l[kv.first] = kv.second;
+    }
+  }
+}
+
+// ---- AWS / GCP plugin helpers ------------------------------------------------------------------------
+std::string get_issuer_url_from_provider_arn(const std::string& arn) {
+  size_t p = arn.find('/');
+  return p == std::string::npos ? arn : arn.substr(p + 1);
+}
+std::string get_iam_role_name_from_iam_role_arn(const std::string& arn) {
+  size_t p = arn.rfind('/');
+  return p == std::string::npos ? arn : arn.substr(p + 1);
+}
+
+namespace {
+Json make_assume_role_doc(const std::string& provider_arn, const Json& condition) {
+  Json stmt{{"Effect", "Allow"}, {"Action", "sts:AssumeRoleWithWebIdentity"},
+            {"Principal", Json{{"Federated", provider_arn}}}, {"Condition", condition}};
+  return Json{{"Version", "2012-10-17"}, {"Statement", Json::array({stmt})}};
+}
+}  // namespace
+
+bool add_service_account_in_assume_role_policy(const std::string& doc, const std::string& ns, const std::string& sa,
+                                               std::string& out, bool* exists) {
+  if (exists) *exists = false;
+  Json d;
+  if (!Json::try_parse(doc, d)) return false;
+  const std::string provider = d["Statement"][0].at_path({"Principal", "Federated"}).as_string();
+  const std::string issuer = get_issuer_url_from_provider_arn(provider);
+  const std::string key = issuer + ":sub";
+  const std::string trust = "system:serviceaccount:" + ns + ":" + sa;
+  Json ids = Json::array();
+  const Json& cur = d["Statement"][0].at_path({"Condition", "StringEquals"})[key];
+  std::vector<Json> existing;
+  if (cur.is_array()) existing.assign(cur.as_array().begin(), cur.as_array().end());
+  else if (cur.is_string()) existing.push_back(cur);
+  for (const auto& i : existing) {
+    if (i.as_string() == trust) {
+      out = doc;
+      if (exists) *exists = true;
+      return false;
+    }
+    ids.push_back(i);
+  }
+  ids.push_back(trust);
+  Json cond{{"StringEquals", Json{{issuer + ":aud", Json::array({"sts.amazonaws.com"})}, {key, ids}}}};
+  out = make_assume_role_doc(provider, cond).dump();
+  return true;
+}
+
+bool remove_service_account_in_assume_role_policy(const std::string& doc, const std::string& ns, const std::string& sa,
+                                                  std::string& out) {
+  Json d;
+  if (!Json::try_parse(doc, d)) return false;
+  const std::string provider = d["Statement"][0].at_path({"Principal", "Federated"}).as_string();
+  const std::string issuer = get_issuer_url_from_provider_arn(provider);
+  const std::string key = issuer + ":sub";
+  const std::string trust = "system:serviceaccount:" + ns + ":" + sa;
+  Json ids = Json::array();
+  const Json& cur = d["Statement"][0].at_path({"Condition", "StringEquals"})[key];
+  std::vector<Json> existing;
+  if (cur.is_array()) existing.assign(cur.as_array().begin(), cur.as_array().end());
+  else if (cur.is_string()) existing.push_back(cur);
+  for (const auto& i : existing)
+    if (i.as_string() != trust) ids.push_back(i);
+  Json se{{issuer + ":aud", Json::array({"sts.amazonaws.com"})}};
+  if (!ids.empty()) se[key] = ids;  // never emit a null list (would break the policy)
+  out = make_assume_role_doc(provider, Json{{"StringEquals", se}}).dump();
+  return true;
+}
+
+void gcp_add_binding(Json& policy, const std::string& member) {
+  policy["bindings"].push_back(Json{{"role", WORKLOAD_IDENTITY_ROLE}, {"members", Json::array({member})}});
+}
+void gcp_revoke_binding(Json& policy, const std::string& member) {
+  for (auto& b : policy["bindings"].mut_array()) {
+    if (b["role"].as_string() != WORKLOAD_IDENTITY_ROLE) continue;
+    Json m = Json::array();
+    for (const auto& x : b["members"].as_array())
+      if (x.as_string() != member) m.push_back(x);
+    b["members"] = m;
+  }
+}
+
+namespace {
+class ConfigMapCloudIam : public CloudIam {
+ public:
+  ConfigMapCloudIam(std::shared_ptr<Client> c, std::string ns) : c_(std::move(c)), ns_(std::move(ns)) {}
+  ApiError get_role_trust_policy(const std::string& role, std::string& doc) override { return get("aws-role-" + role, doc); }
+  ApiError set_role_trust_policy(const std::string& role, const std::string& doc) override { return set("aws-role-" + role, doc); }
+  ApiError get_sa_iam_policy(const std::string& sa, Json& policy) override {
+    std::string s;
+    ApiError e = get("gcp-sa-" + sanitize(sa), s);
+    if (e.code == 404) {
+      policy = Json{{"bindings", Json::array()}};
+      return {};
+    }
+    if (!e) Json::try_parse(s, policy);
+    return e;
+  }
+  ApiError set_sa_iam_policy(const std::string& sa, const Json& policy) override { return set("gcp-sa-" + sanitize(sa), policy.dump()); }
+
+ private:
+  static std::string sanitize(std::string s) {
+    for (auto& ch : s)
+      if (!std::isalnum(static_cast<unsigned char>(ch)) && ch != '-' && ch != '.') ch = '-';
+    return to_lower(s);
+  }
+  ApiError get(const std::string& key, std::string& out) {
+    Json cm;
+    ApiError e = c_->get("v1", "ConfigMap", ns_, "kfamd-cloud-iam", cm);
+    if (e) return e;
+    const Json& v = cm["data"][key];
+    if (!v.is_string()) return ApiError::NotFound("iam policy", key);
+    out = v.as_string();
+    return {};
+  }
+  ApiError set(const std::string& key, const std::string& val) {
+    Json cm;
+    ApiError e = c_->get("v1", "ConfigMap", ns_, "kfamd-cloud-iam", cm);
+    if (e.code == 404) {
+      cm = Json{{"apiVersion", "v1"}, {"kind", "ConfigMap"}, {"metadata", Json{{"name", "kfamd-cloud-iam"}, {"namespace", ns_}}},
+                {"data", Json{{key, val}}}};
+      return c_->create(cm);
+    }
+    if (e) return e;
+    return c_->update_with_retry("v1", "ConfigMap", ns_, "kfamd-cloud-iam", [&](Json& o) {
+      o["data"][key] = val;
+      return true;
+    });
+  }
+  std::shared_ptr<Client> c_;
+  std::string ns_;
+};
+}  // namespace
+
+std::shared_ptr<CloudIam> make_configmap_cloud_iam(std::shared_ptr<Client> c, std::string ns) {
+  return std::make_shared<ConfigMapCloudIam>(std::move(c), std::move(ns));
+}
+
+// ---- AuthorizationPolicy -----------------------------------------------------------------------
+Json authorization_policy_spec(const Json& profile, const ProfileOptions& o) {
+  const std::string nb_principal = getenv_or("NOTEBOOK_CONTROLLER_PRINCIPAL", "cluster.local/ns/kubeflow/sa/notebook-controller-service-account");
+  const std::string igw = getenv_or("ISTIO_INGRESS_GATEWAY_PRINCIPAL", "cluster.local/ns/istio-system/sa/istio-ingressgateway-service-account");
+  const std::string kfp = getenv_or("KFP_UI_PRINCIPAL", "cluster.local/ns/kubeflow/sa/ml-pipeline-ui");
+  const std::string owner = profile.at_path({"spec", "owner", "name"}).as_string();
+  return Json{
+      {"action", "ALLOW"},
+      {"rules",
+       Json::array({
+           Json{{"when", Json::array({Json{{"key", "request.headers[" + o.userid_header + "]"},
+                                           {"values", Json::array({o.userid_prefix + owner})}}})},
+                {"from", Json::array({Json{{"source", Json{{"principals", Json::array({igw, kfp})}}}}})}},
+           Json{{"when", Json::array({Json{{"key", "source.namespace"}, {"values", Json::array({profile.str_at({"metadata", "name"})})}}})}},
+           Json{{"to", Json::array({Json{{"operation", Json{{"paths", Json::array({"/healthz", "/metrics", "/wait-for-drain"})}}}}})}},
+           Json{{"from", Json::array({Json{{"source", Json{{"principals", Json::array({nb_principal})}}}}})},
+                {"to", Json::array({Json{{"operation", Json{{"methods", Json::array({"GET"})}, {"paths", Json::array({"*/api/kernels"})}}}}})}},
+       })}};
+}
+
+// ---- reconciler -------------------------------------------------------------------------------------
+ProfileReconciler::ProfileReconciler(std::shared_ptr<Client> c, ProfileOptions o, std::shared_ptr<CloudIam> iam)
+    : c_(std::move(c)), o_(std::move(o)), iam_(std::move(iam)) {}
+
+ProfileReconciler::~ProfileReconciler() {
+  watching_ = false;
+  if (watch_th_.joinable()) watch_th_.join();
+}
+
+std::map<std::string, std::string> ProfileReconciler::read_labels() {
+  if (o_.namespace_labels_path.empty()) return o_.default_labels;
+  std::string text;
+  if (!read_file(o_.namespace_labels_path, text)) {
+    // Q5 deviation: the reference os.Exit(1)s the controller; we keep running on the defaults.
+    KF_ERROR("profile-controller", "namespace labels properties file doesn't exist; using defaults",
+             Json{{"path", o_.namespace_labels_path}});
+    return o_.default_labels;
+  }
+  bool ok = true;
+  auto m = parse_flat_yaml_map(text, &ok);
+  if (!ok) KF_ERROR("profile-controller", "Unable to parse default namespace labels (partially applied)");
+  return m;
+}
+
+Result ProfileReconciler::fail_condition(Json& profile, const std::string& msg, std::string* err) {
+  Json& conds = profile["status"]["conditions"];
+  for (const auto& c : conds.as_array())
+    if (c["type"].as_string() == "Failed" && c["message"].as_string() == msg) return {};
+  conds.push_back(Json{{"type", "Failed"}, {"message", msg}});
+  ApiError e = c_->update_status(profile);
+  if (e) *err = e.message;
+  return {};
+}
+
+ApiError ProfileReconciler::apply_plugins(const Json& profile, bool revoke) {
+  const std::string ns = profile.str_at({"metadata", "name"});
+  for (const auto& p : profile.at_path({"spec", "plugins"}).as_array()) {
+    const std::string kind = p["kind"].as_string();
+    const Json& spec = p["spec"];
+    if (kind == KIND_WORKLOAD_IDENTITY) {
+      const std::string gsa = spec["gcpServiceAccount"].as_string();
+      ApiError e = c_->update_with_retry("v1", "ServiceAccount", ns, DEFAULT_EDITOR, [&](Json& sa) {
+        if (revoke) return sa["metadata"]["annotations"].erase(GCP_ANNOTATION_KEY);
+        if (annotation(sa, GCP_ANNOTATION_KEY) == gsa) return false;
+        set_annotation(sa, GCP_ANNOTATION_KEY, gsa);
+        return true;
+      });
+      if (e && e.code != 404) return e;
+      // IAM binding on the GCP service account: <project>.svc.id.goog[ns/default-editor]
+      const size_t at = gsa.find('@');
+      std::string project = at == std::string::npos ? "" : gsa.substr(at + 1);
+      size_t dot = project.find('.');
+      if (dot != std::string::npos) project = project.substr(0, dot);
+      const std::string member = "serviceAccount:" + project + ".svc.id.goog[" + ns + "/" + DEFAULT_EDITOR + "]";
+      Json policy;
+      e = iam_->get_sa_iam_policy(gsa, policy);
+      if (e) return e;
+      if (revoke) {
+        gcp_revoke_binding(policy, member);
+      } else {
+        bool have = false;
+        for (const auto& b : policy["bindings"].as_array())
+          for (const auto& m : b["members"].as_array()) have = have || (b["role"].as_string() == WORKLOAD_IDENTITY_ROLE && m.as_string() == member);
+        if (!have) gcp_add_binding(policy, member);
+      }
+      e = iam_->set_sa_iam_policy(gsa, policy);
+      if (e) return e;
+    } else if (kind == KIND_AWS_IAM_FOR_SERVICE_ACCOUNT) {
+      const std::string role = spec["awsIamRole"].as_string();
+      ApiError e = c_->update_with_retry("v1", "ServiceAccount", ns, DEFAULT_EDITOR, [&](Json& sa) {
+        if (revoke) return sa["metadata"]["annotations"].erase(AWS_ANNOTATION_KEY);
+        if (annotation(sa, AWS_ANNOTATION_KEY) == role) return false;
+        set_annotation(sa, AWS_ANNOTATION_KEY, role);
+        return true;
+      });
+      if (e && e.code != 404) return e;
+      if (spec["annotateOnly"].as_bool()) continue;
+      std::string doc;
+      const std::string role_name = get_iam_role_name_from_iam_role_arn(role);
+      e = iam_->get_role_trust_policy(role_name, doc);
+      if (e.code == 404) continue;  // role unknown to the (offline) IAM backend
+      if (e) return e;
+      std::string out;
+      bool exists = false;
+      bool changed = revoke ? remove_service_account_in_assume_role_policy(doc, ns, DEFAULT_EDITOR, out)
+                            : add_service_account_in_assume_role_policy(doc, ns, DEFAULT_EDITOR, out, &exists);
+      if (changed && out != doc) {
+        e = iam_->set_role_trust_policy(role_name, out);
+        if (e) return e;
+      }
+    } else {
+      KF_INFO("profile-controller", "Plugin not recgonized: " + kind);
+    }
+  }
+  return {};
+}
+
+Result ProfileReconciler::reconcile(const Request& r, std::string* err) {
+  auto labels = read_labels();
+  Json profile;
+  ApiError e = c_->get("kubeflow.org/v1", "Profile", "", r.name, profile);
+  if (e.code == 404) {
+    inc_request_counter("profile deletion");
+    return {};
+  }
+  if (e) {
+    inc_request_error_counter("error reading the profile object", "major");
+    *err = e.message;
+    return {};
+  }
+  const std::string name = profile.str_at({"metadata", "name"});
+  const std::string owner = profile.at_path({"spec", "owner", "name"}).as_string();
+  const bool deleting = profile.at_path({"metadata", "deletionTimestamp"}).is_string();
+  if (!deleting) {
+    // ---- 1. namespace
+    Json ns{{"apiVersion", "v1"}, {"kind", "Namespace"},
+            {"metadata", Json{{"name", name}, {"annotations", Json{{"owner", owner}}}, {"labels", Json{{"istio-injection", "enabled"}}}}}};
+    set_namespace_labels(ns, labels);
+    set_controller_reference(profile, ns);
+    Json found;
+    e = c_->get("v1", "Namespace", "", name, found);
+    if (e.code == 404) {
+      KF_INFO("profile-controller", "Creating Namespace: " + name);
+      Json n = ns;
+      e = c_->create(n);
+      if (e) {
+        inc_request_error_counter("error creating namespace", "major");
+        *err = e.message;
+        return {};
+      }
+      // wait for completion (constant backoff, 5 x 3 s in the reference)
+      double deadline = now_seconds() + o_.namespace_wait_s;
+      while (c_->get("v1", "Namespace", "", name, found)) {
+        if (now_seconds() > deadline) {
+          inc_request_error_counter("error namespace create completion", "major");
+          return fail_condition(profile, "Owning namespace failed to create within 15 seconds", err);
+        }
+        ::usleep(50000);
+      }
+    } else if (e) {
+      *err = e.message;
+      return {};
+    } else {
+      if (annotation(found, "owner") == owner && has_annotation(found, "owner")) {
+        Json updated = found;
+        set_namespace_labels(updated, labels);
+        if (updated.at_path({"metadata", "labels"}) != found.at_path({"metadata", "labels"})) {
+          e = c_->update(updated);
+          if (e) {
+            *err = e.message;
+            return {};
+          }
+        }
+      } else {
+        inc_request_counter("reject profile taking over existing namespace");
+        return fail_condition(profile, "namespace already exist, but not owned by profile creator " + owner, err);
+      }
+    }
+    // ---- 2. Istio AuthorizationPolicy
+    Json ap{{"apiVersion", "security.istio.io/v1beta1"}, {"kind", "AuthorizationPolicy"},
+            {"metadata", Json{{"name", AUTHZ_POLICY_ISTIO}, {"namespace", name}, {"annotations", Json{{"user", owner}, {"role", "admin"}}}}},
+            {"spec", authorization_policy_spec(profile, o_)}};
+    set_controller_reference(profile, ap);
+    e = reconcile_owned(*c_, ap, CopyKind::Generic);
+    if (e) {
+      inc_request_error_counter("error updating Istio AuthorizationPolicy permission", "major");
+      *err = e.message;
+      return {};
+    }
+    // ---- 3. ServiceAccounts + their RoleBindings
+    auto rolebinding = [&](const std::string& rb_name, const std::string& cluster_role, const Json& subject, const Json& ann) {
+      Json rb{{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "RoleBinding"},
+              {"metadata", Json{{"name", rb_name}, {"namespace", name}}},
+              {"roleRef", Json{{"apiGroup", "rbac.authorization.k8s.io"}, {"kind", "ClusterRole"}, {"name", cluster_role}}},
+              {"subjects", Json::array({subject})}};
+      if (ann.is_object()) rb["metadata"]["annotations"] = ann;
+      set_controller_reference(profile, rb);
+      Json cur;
+      ApiError ge = c_->get("rbac.authorization.k8s.io/v1", "RoleBinding", name, rb_name, cur);
+      if (ge.code == 404) return c_->create(rb);
+      if (ge) return ge;
+      if (cur["roleRef"] == rb["roleRef"] && cur["subjects"] == rb["subjects"]) return ApiError{};
+      cur["roleRef"] = rb["roleRef"];
+      cur["subjects"] = rb["subjects"];
+      return c_->update(cur);
+    };
+    for (auto sa_role : {std::make_pair(DEFAULT_EDITOR, "kubeflow-edit"), std::make_pair(DEFAULT_VIEWER, "kubeflow-view")}) {
+      Json sa{{"apiVersion", "v1"}, {"kind", "ServiceAccount"}, {"metadata", Json{{"name", sa_role.first}, {"namespace", name}}}};
+      set_controller_reference(profile, sa);
+      Json cur;
+      ApiError ge = c_->get("v1", "ServiceAccount", name, sa_role.first, cur);
+      if (ge.code == 404) ge = c_->create(sa);
+      if (ge) {
+        inc_request_error_counter("error updating ServiceAccount", "major");
+        *err = ge.message;
+        return {};
+      }
+      ge = rolebinding(sa_role.first, sa_role.second,
+                       Json{{"kind", "ServiceAccount"}, {"name", sa_role.first}, {"namespace", name}}, Json());
+      if (ge) {
+        *err = ge.message;
+        return {};
+      }
+    }
+    // ---- 4. owner RoleBinding "namespaceAdmin"
+    Json owner_subject = profile.at_path({"spec", "owner"});
+    e = rolebinding("namespaceAdmin", "kubeflow-admin", owner_subject, Json{{"user", owner}, {"role", "admin"}});
+    if (e) {
+      inc_request_error_counter("error updating Owner Rolebinding", "major");
+      *err = e.message;
+      return {};
+    }
+    // ---- 5. ResourceQuota
+    const Json& rq = profile.at_path({"spec", "resourceQuotaSpec"});
+    if (rq["hard"].is_object() && !rq["hard"].empty()) {
+      Json q{{"apiVersion", "v1"}, {"kind", "ResourceQuota"}, {"metadata", Json{{"name", KF_QUOTA}, {"namespace", name}}}, {"spec", rq}};
+      set_controller_reference(profile, q);
+      Json cur;
+      ApiError ge = c_->get("v1", "ResourceQuota", name, KF_QUOTA, cur);
+      if (ge.code == 404) ge = c_->create(q);
+      else if (!ge && cur["spec"] != rq) {
+        cur["spec"] = rq;
+        ge = c_->update(cur);
+      }
+      if (ge) {
+        inc_request_error_counter("error updating resource quota", "major");
+        *err = ge.message;
+        return {};
+      }
+    } else {
+      ApiError de = c_->remove("v1", "ResourceQuota", name, KF_QUOTA);
+      if (de && de.code != 404) {
+        *err = de.message;
+        return {};
+      }
+    }
+    // ---- 6. default plugins (Q5 fix: only write when something is added)
+    if (!o_.workload_identity.empty()) {
+      bool have = false;
+      for (const auto& p : profile.at_path({"spec", "plugins"}).as_array()) have = have || p["kind"].as_string() == KIND_WORKLOAD_IDENTITY;
+      if (!have) {
+        profile["spec"]["plugins"].push_back(
+            Json{{"kind", KIND_WORKLOAD_IDENTITY}, {"spec", Json{{"gcpServiceAccount", o_.workload_identity}}}});
+        e = c_->update(profile);
+        if (e) {
+          inc_request_error_counter("error patching DefaultPluginSpec", "major");
+          *err = e.message;
+          return {};
+        }
+      }
+    }
+    // ---- 7. plugins
+    e = apply_plugins(profile, false);
+    if (e) {
+      inc_request_error_counter("error applying plugin", "major");
+      *err = e.message;
+      return {};
+    }
+    // ---- 8. finalizer
+    bool has_fin = false;
+    for (const auto& f : profile.at_path({"metadata", "finalizers"}).as_array()) has_fin = has_fin || f.as_string() == PROFILE_FINALIZER;
+    if (!has_fin) {
+      e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", name, [](Json& o) {
+        for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
+          if (f.as_string() == PROFILE_FINALIZER) return false;
+        o["metadata"]["finalizers"].push_back(PROFILE_FINALIZER);
+        return true;
+      });
+      if (e) {
+        inc_request_error_counter("error updating finalizer", "major");
+        *err = e.message;
+        return {};
+      }
+    }
+  } else {
+    bool has_fin = false;
+    for (const auto& f : profile.at_path({"metadata", "finalizers"}).as_array()) has_fin = has_fin || f.as_string() == PROFILE_FINALIZER;
+    if (has_fin) {
+      e = apply_plugins(profile, true);
+      if (e) {
+        inc_request_error_counter("error revoking plugin", "major");
+        *err = e.message;
+        return {};
+      }
+      e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", name, [](Json& o) {
+        Json fins = Json::array();
+        for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
+          if (f.as_string() != PROFILE_FINALIZER) fins.push_back(f);
+        o["metadata"]["finalizers"] = fins;
+        return true;
+      });
+      if (e) {
+        inc_request_error_counter("error removing finalizer", "major");
+        *err = e.message;
+        return {};
+      }
+    }
+  }
+  inc_request_counter("reconcile");
+  return {};
+}
+
+void ProfileReconciler::setup(Manager& mgr) {
+  hb_ = std::make_unique<Heartbeat>("profile-controller");
+  ctl_ = std::make_shared<Controller>("profile-controller", [this](const Request& r, std::string* e) { return reconcile(r, e); });
+  Informer& profiles = mgr.informer("kubeflow.org/v1", "Profile");
+  ctl_->For(profiles);
+  ctl_->Owns(mgr.informer("v1", "Namespace"), "Profile");
+  ctl_->Owns(mgr.informer("security.istio.io/v1beta1", "AuthorizationPolicy"), "Profile");
+  ctl_->Owns(mgr.informer("v1", "ServiceAccount"), "Profile");
+  ctl_->Owns(mgr.informer("rbac.authorization.k8s.io/v1", "RoleBinding"), "Profile");
+  mgr.add(ctl_);
+  // fsnotify equivalent: inotify on the labels file -> re-enqueue every Profile
+  if (!o_.namespace_labels_path.empty()) {
+    watching_ = true;
+    Informer* pinf = &profiles;
+    watch_th_ = std::thread([this, pinf] {
+      int fd = ::inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+      int wd = -1;
+      int64_t last_mtime = file_mtime_ns(o_.namespace_labels_path);
+      while (watching_) {
+        if (fd >= 0 && wd < 0) wd = ::inotify_add_watch(fd, o_.namespace_labels_path.c_str(), IN_MODIFY | IN_CLOSE_WRITE | IN_DELETE_SELF | IN_MOVE_SELF);
+        bool fire = false;
+        if (fd >= 0) {
+          pollfd p{fd, POLLIN, 0};
+          if (::poll(&p, 1, 200) > 0) {
+            char buf[4096];
+            ssize_t n = ::read(fd, buf, sizeof buf);
+            for (ssize_t i = 0; i < n;) {
+              auto* ev = reinterpret_cast<inotify_event*>(buf + i);
+              if (ev->mask & (IN_DELETE_SELF | IN_MOVE_SELF | IN_IGNORED)) {
+                ::inotify_rm_watch(fd, wd);
+                wd = -1;  // re-add (editors replace files)
+              }
+              fire = true;
+              i += static_cast<ssize_t>(sizeof(inotify_event) + ev->len);
+            }
+          }
+        } else {
+          ::usleep(500000);
+        }
+        int64_t m = file_mtime_ns(o_.namespace_labels_path);
+        if (m != last_mtime) {
+          last_mtime = m;
+          fire = true;
+        }
+        if (fire)
+          for (const auto& p : pinf->list()) ctl_->enqueue({"", p.str_at({"metadata", "name"})});
+      }
+      if (fd >= 0) ::close(fd);
+    });
+  }
+}
+
+}  // namespace kf

@@ -306,6 +306,7 @@ Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu) {
   add("KFAMD_GPU_IDS", join(ids, ","));
   add("KFAMD_XGMI_RING", join(ring, ","));
   add("KFAMD_GPU_TOPOLOGY", t.describe());
+  if (t.source == "synthetic") add("KFAMD_SIMULATED_GPUS", "1");  // CI node: no /dev/kfd behind these ids
   if (multi_gpu) {
     // single-node torchrun / RCCL wiring: one process per GPU, loopback rendezvous,
     // xGMI P2P enabled, no IB/socket fallbacks inside the pod.

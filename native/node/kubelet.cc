@@ -89,7 +89,7 @@ std::string expand_vars(const std::string& s, const std::map<std::string, std::s
 }
 
 const char* kDefaultRecipes = R"([
-  {"match": "cmd:kfamd-readiness|kfamd-readiness|gpu-readiness", "argv": ["{bin}/kfamd-readiness"]},
+  {"match": "cmd:kfamd-readiness|kfamd-readiness|gpu-readiness", "argv": ["{bin}/kfamd-readiness"], "passArgs": true},
   {"match": "cmd:tensorboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
   {"match": "cmd:jupyter|cmd:start-notebook.sh|cmd:start.sh", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
   {"match": "oauth-proxy|oauth_proxy", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.oauth_proxy"], "passArgs": true},
@@ -619,8 +619,8 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     // GPU wiring from the device plugin allocation
     const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0;
     if (wants_gpu && !rt->gpus.devices.empty()) {
-      for (const auto& ev : gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1).as_array())
-        set(ev["name"].as_string(), ev["value"].as_string());
+      const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1);
+      for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
     }
     for (const auto& ef : c["envFrom"].as_array()) {
       const bool secret = ef["secretRef"].is_object();

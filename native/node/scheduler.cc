@@ -119,7 +119,8 @@ Result Scheduler::reconcile(const Request& r, std::string* err) {
       const std::string& ph = p.at_path({"status", "phase"}).as_string();
       if (ph == "Succeeded" || ph == "Failed") continue;
       npods++;
-      for (const auto& m : pod_requests(p).as_object()) used[m.first] += m.second.as_double();
+      const Json req = pod_requests(p);
+      for (const auto& m : req.as_object()) used[m.first] += m.second.as_double();
     }
     const Json& alloc = node.at_path({"status", "allocatable"});
     bool fits = true;
