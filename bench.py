@@ -31,7 +31,7 @@ def parse_args():
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--n", type=int, default=8192)
     p.add_argument("--k", type=int, default=8192)
-    p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "0")),
+    p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "3")),
                    help="notebook cold-start runs through the native control plane (rank 0)")
     p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
     return p.parse_args()
@@ -113,6 +113,7 @@ def main() -> int:
             extra["cold_start_p50_s"] = cs["p50_s"]
             extra["cold_start_p90_s"] = cs["p90_s"]
             extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
+            extra["cold_start_readiness"] = cs.get("readiness")
         except Exception as e:  # reported, never fatal for the GEMM number
             extra["cold_start_error"] = f"{type(e).__name__}: {e}"
 

@@ -1,0 +1,122 @@
+"""Notebook pod cold-start benchmark (BASELINE.json headline, first half).
+
+Brings up the single-binary control plane (``kflite``: API server + notebook/profile
+controllers + admission + GPU-aware scheduler + process-pod kubelet + gateway), then for each
+run creates a Notebook CR requesting ``gpus_per_notebook`` MI355X GPUs and measures
+
+* ``cold_start_s``   Notebook CREATE -> ``status.readyReplicas == 1`` (wall clock, client side),
+* phases from the pod's own (ms-precision) timestamps: reconcile (CR -> StatefulSet),
+  schedule (pod -> PodScheduled), init (gpu-readiness op: HIP init + in-pod bf16 MFMA GEMM /
+  LayerNorm / RCCL all-reduce on the allocated GPUs), start (container start -> Ready).
+
+The reference publishes no cold-start numbers: the controller path it measures is
+notebook_controller.go Reconcile -> StatefulSet -> kubelet; here every hop is native and the
+in-pod readiness op is the hand-written gfx950 kernel set (kfamd-readiness).
+
+Usage: ``python -m kubeflow_rm_amd.bench_coldstart --runs 5 --gpus-per-notebook 1``.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime as _dt
+import json
+import statistics
+import time
+
+from .cluster import LocalCluster
+
+
+def _ts(s: str | None) -> float | None:
+    if not s:
+        return None
+    s = s.rstrip("Z")
+    fmt = "%Y-%m-%dT%H:%M:%S.%f" if "." in s else "%Y-%m-%dT%H:%M:%S"
+    return _dt.datetime.strptime(s, fmt).replace(tzinfo=_dt.timezone.utc).timestamp()
+
+
+def _cond(pod: dict, typ: str) -> float | None:
+    for c in pod.get("status", {}).get("conditions", []) or []:
+        if c.get("type") == typ and c.get("status") == "True":
+            return _ts(c.get("lastTransitionTime"))
+    return None
+
+
+def _pct(xs: list[float], q: float) -> float:
+    xs = sorted(xs)
+    if not xs:
+        return float("nan")
+    k = (len(xs) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
+                       readiness: bool = True, timeout: float = 120.0, namespace: str = "bench") -> dict:
+    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...}}."""
+    out_runs = []
+    with LocalCluster(gpus=gpus) as cl:
+        c = cl.client
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": namespace}})
+        for i in range(runs):
+            name = f"cs-{i}"
+            ann = {} if readiness else {"kfamd.io/gpu-readiness-op": "false"}
+            nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook",
+                  "metadata": {"name": name, "namespace": namespace, "annotations": ann},
+                  "spec": {"template": {"spec": {"containers": [{"name": name, "image": image,
+                                                                 "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}}}]}}}}
+            t0 = time.time()
+            c.create(nb)
+            obj = c.wait_for("kubeflow.org/v1", "Notebook", name, namespace,
+                             lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout)
+            t1 = time.time()
+            pod = c.get("v1", "Pod", f"{name}-0", namespace)
+            t_sched = _cond(pod, "PodScheduled")
+            t_init = _cond(pod, "Initialized")
+            t_ready = _cond(pod, "Ready")
+            phases = {}
+            if t_sched and t_init:
+                phases["schedule_to_initialized_s"] = t_init - t_sched
+            if t_init and t_ready:
+                phases["initialized_to_ready_s"] = t_ready - t_init
+            if t_ready:
+                phases["create_to_pod_ready_s"] = t_ready - t0
+            if t_sched:
+                phases["create_to_scheduled_s"] = t_sched - t0
+            out_runs.append({"cold_start_s": t1 - t0, "phases": phases,
+                             "gpus": (obj.get("status") or {}).get("gpus"),
+                             "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
+            c.delete("kubeflow.org/v1", "Notebook", name, namespace)
+            c.wait_gone("kubeflow.org/v1", "Notebook", name, namespace, timeout=60)
+            # the StatefulSet / pod are garbage collected asynchronously; wait for the GPU to free up
+            deadline = time.time() + 60
+            while time.time() < deadline:
+                try:
+                    c.get("v1", "Pod", f"{name}-0", namespace)
+                except Exception:
+                    break
+                time.sleep(0.02)
+    xs = [r["cold_start_s"] for r in out_runs]
+    phase_keys = sorted({k for r in out_runs for k in r["phases"]})
+    res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "runs": out_runs,
+           "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
+    rd = [r["gpuReadiness"] for r in out_runs if r.get("gpuReadiness")]
+    if rd:
+        res["readiness"] = rd[-1]
+    return res
+
+
+def main() -> int:
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--runs", type=int, default=5)
+    p.add_argument("--gpus-per-notebook", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None, help="node GPUs (default: discover; -> synthetic 8 without /dev/kfd)")
+    p.add_argument("--no-readiness", action="store_true")
+    a = p.parse_args()
+    r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness)
+    print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
+    print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

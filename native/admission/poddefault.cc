@@ -206,7 +206,7 @@ AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o) {
     if (a.operation != "CREATE" || a.res->kind != "Pod" || !a.res->group.empty() || !a.object) return {};
     Json& pod = *a.object;
     if (o.only_notebooks && label(pod, "notebook-name").empty()) return {};
-    if (annotation(pod, "notebooks.kubeflow.org/gpu-readiness-op") == "false") return {};
+    if (annotation(pod, "kfamd.io/gpu-readiness-op") == "false") return {};
     int64_t gpus = 0;
     for (const auto& c : pod.at_path({"spec", "containers"}).as_array()) {
       const Json& q = c.at_path({"resources", "limits", GPU_RESOURCE});

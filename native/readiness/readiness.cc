@@ -18,6 +18,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -45,8 +49,30 @@ namespace {
 Json g_result = Json::object();
 std::string g_error;
 
+const char* volatile g_stage = "start";
+
 void fail(const std::string& msg) {
   if (g_error.empty()) g_error = msg;
+}
+
+// A fault in the op must still leave a diagnosable termination message (the pod's init
+// container status is the only place a notebook user sees it).
+void on_fatal(int sig) {
+  char buf[256];
+  int n = std::snprintf(buf, sizeof buf, "kfamd-readiness: fatal signal %d during stage '%s'\n", sig, g_stage);
+  ssize_t w = ::write(2, buf, static_cast<size_t>(n));
+  (void)w;
+  void* frames[64];
+  int nf = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, nf, 2);
+  if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
+    FILE* f = std::fopen(tl, "w");
+    if (f) {
+      std::fprintf(f, "{\"ok\":false,\"error\":\"fatal signal %d during %s\"}", sig, g_stage);
+      std::fclose(f);
+    }
+  }
+  ::_exit(128 + sig);
 }
 
 __global__ void fill_uniform(__bf16* p, size_t n, uint32_t seed) {
@@ -83,6 +109,7 @@ struct Args {
 };
 
 bool gemm_check(int dev, const Args& a, Json& out) {
+  g_stage = "gemm:setup";
   HIP_OK(hipSetDevice(dev));
   hipStream_t s;
   HIP_OK(hipStreamCreate(&s));
@@ -96,11 +123,13 @@ bool gemm_check(int dev, const Args& a, Json& out) {
   auto run = [&]() {
     return kfamd_gemm_nt_bf16(A, B, C, nullptr, nullptr, a.m, a.n, a.k, 1, a.k, a.k, a.n, 0, 0, 0, 0, 0, 1.0f, 0, s);
   };
+  g_stage = "gemm:first-launch";
   int rc = run();
   if (rc != 0) {
     fail("kfamd_gemm_nt_bf16 returned " + std::to_string(rc));
     return false;
   }
+  g_stage = "gemm:verify";
   // verify 8 sampled rows against fp32
   const int nrows = 8;
   std::vector<int> rows(nrows);
@@ -128,6 +157,7 @@ bool gemm_check(int dev, const Args& a, Json& out) {
     }
   }
   const bool ok = max_err <= 1e-2 * max_ref + 1e-2;
+  g_stage = "gemm:timing";
   // timing
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
@@ -158,6 +188,7 @@ bool gemm_check(int dev, const Args& a, Json& out) {
 }
 
 bool ln_check(int dev, const Args& a, Json& out) {
+  g_stage = "layernorm";
   HIP_OK(hipSetDevice(dev));
   hipStream_t s;
   HIP_OK(hipStreamCreate(&s));
@@ -233,6 +264,7 @@ __global__ void fill_const(float* p, size_t n, float v) {
 }
 
 bool allreduce_check(int ndev, const Args& a, Json& out) {
+  g_stage = "allreduce";
   std::vector<ncclComm_t> comms(ndev);
   std::vector<int> devs(ndev);
   for (int i = 0; i < ndev; ++i) devs[i] = i;
@@ -310,6 +342,10 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  ::signal(SIGSEGV, on_fatal);
+  ::signal(SIGBUS, on_fatal);
+  ::signal(SIGABRT, on_fatal);
+  ::signal(SIGFPE, on_fatal);
   Args a;
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
@@ -330,6 +366,7 @@ int main(int argc, char** argv) {
     else if (s == "--skip-allreduce") a.skip_ar = true;
   }
   auto t0 = std::chrono::steady_clock::now();
+  g_stage = "hip-init";
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -344,6 +381,7 @@ int main(int argc, char** argv) {
   } else {
     Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
     for (int d = 0; d < ndev; ++d) {
+      g_stage = "device-query";
       hipDeviceProp_t p;
       if (hipGetDeviceProperties(&p, d) == hipSuccess)
         devs.push_back(Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
@@ -368,6 +406,7 @@ int main(int argc, char** argv) {
       g_result["allreduce"] = ar;
     }
   }
+  g_stage = "report";
   g_result["ok"] = g_error.empty();
   if (!g_error.empty()) g_result["error"] = g_error;
   g_result["total_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
