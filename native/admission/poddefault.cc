@@ -116,7 +116,7 @@ std::string safe_to_apply_pod_defaults(const Json& pod, const std::vector<Json>&
 }
 
 void set_command_and_args(Json& c, const std::vector<Json>& pds) {
-  if (c["name"].as_string() == kIstioProxy) return;
+  if (static_cast<const Json&>(c)["name"].as_string() == kIstioProxy) return;  // const read: no autovivify
   for (const auto& pd : pds) {
     if (!c.has("command") && pd.at_path({"spec", "command"}).is_array()) c["command"] = pd.at_path({"spec", "command"});
     if (!c.has("args") && pd.at_path({"spec", "args"}).is_array()) c["args"] = pd.at_path({"spec", "args"});
@@ -165,6 +165,7 @@ void apply_pod_defaults(Json& pod, const std::vector<Json>& pds) {
   for (const auto& pd : pds)
     pod["metadata"]["annotations"][std::string(kAnnotationPrefix) + "/poddefault-" + pd_name(pd)] =
         pd.str_at({"metadata", "resourceVersion"});
+  prune_nulls(pod);  // the merge helpers read through operator[] on the mutable pod
 }
 
 AdmissionFn make_poddefault_plugin(std::shared_ptr<Client> c, PodDefaultOptions o) {

@@ -215,6 +215,7 @@ void ApiServer::convert_out(std::shared_ptr<const ResourceInfo> res, const std::
   obj["kind"] = res->kind;
 }
 void ApiServer::to_storage(std::shared_ptr<const ResourceInfo> res, Json& obj) const {
+  prune_nulls(obj);
   obj["apiVersion"] = res->storage_api_version();
   obj["kind"] = res->kind;
 }

@@ -1,0 +1,329 @@
+// capi.cc — libkfcore_capi.so: a C ABI over the control plane's pure functions.
+//
+// One entry point, `kf_call(name, args_json)`, dispatches to the reconcilers' pure helpers
+// (StatefulSet/Service/VirtualService generation, notebook status, culling decisions, profile
+// label merge / IAM trust-policy edits, PodDefault merge, quota accounting, xGMI placement,
+// selectors, patches, schema validation, ...). The Python test-suite drives the reference's
+// table-driven unit cases through it (tests/test_unit_*.py), and the web apps reuse the same
+// native code instead of re-implementing it in Python.
+//
+// Result: malloc'd JSON {"ok": true, "result": ...} | {"ok": false, "error": "..."}; release it
+// with kf_free().
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <set>
+#include <string>
+
+#include "admission/admission.h"
+#include "apiserver/resources.h"
+#include "apiserver/selector.h"
+#include "capi/registry.h"
+#include "controllers/common.h"
+#include "controllers/notebook.h"
+#include "controllers/profile.h"
+#include "core/util.h"
+#include "gpu/topology.h"
+
+namespace kf {
+namespace {
+
+NotebookOptions nb_opts(const Json& o) {
+  NotebookOptions r;
+  if (o["use_istio"].is_bool()) r.use_istio = o["use_istio"].as_bool();
+  if (o["istio_gateway"].is_string()) r.istio_gateway = o["istio_gateway"].as_string();
+  if (o["istio_host"].is_string()) r.istio_host = o["istio_host"].as_string();
+  if (o["cluster_domain"].is_string()) r.cluster_domain = o["cluster_domain"].as_string();
+  if (o["add_fsgroup"].is_bool()) r.add_fsgroup = o["add_fsgroup"].as_bool();
+  return r;
+}
+
+std::vector<Json> vec(const Json& a) { return std::vector<Json>(a.as_array().begin(), a.as_array().end()); }
+
+GpuTopology topo_from(const Json& a) {
+  return GpuTopology::synthetic(static_cast<int>(a["gpus"].as_int(8)), static_cast<int>(a["numa_nodes"].as_int(2)));
+}
+
+Json placement_json(const Placement& p) {
+  Json d = Json::array(), r = Json::array();
+  for (int x : p.devices) d.push_back(x);
+  for (int x : p.ring) r.push_back(x);
+  return Json{{"devices", d}, {"ring", r}, {"numa_node", p.numa_node}, {"reason", p.reason}};
+}
+
+void register_core(CapiRegistry& R) {
+  R.add("parse_quantity", [](const Json& a) -> Json {
+    auto v = parse_quantity(a["q"].as_string());
+    return v ? Json(*v) : Json();
+  });
+  R.add("label_selector_matches", [](const Json& a) -> Json {
+    LabelSelector sel;
+    if (a["selector"].is_string()) {
+      std::string err;
+      if (!LabelSelector::parse(a["selector"].as_string(), sel, &err)) throw std::runtime_error(err);
+    } else {
+      sel = LabelSelector::from_json(a["selector"], a["null_matches_nothing"].as_bool());
+    }
+    return sel.matches(a["labels"]);
+  });
+  R.add("field_selector_matches", [](const Json& a) -> Json {
+    FieldSelector sel;
+    std::string err;
+    if (!FieldSelector::parse(a["selector"].as_string(), sel, &err)) throw std::runtime_error(err);
+    return sel.matches(a["object"]);
+  });
+  R.add("merge_patch", [](const Json& a) -> Json { return merge_patch(a["target"], a["patch"]); });
+  R.add("diff_merge_patch", [](const Json& a) -> Json { return diff_merge_patch(a["from"], a["to"]); });
+  R.add("apply_json_patch", [](const Json& a) -> Json { return apply_json_patch(a["target"], a["ops"]); });
+  R.add("diff_json_patch", [](const Json& a) -> Json { return diff_json_patch(a["from"], a["to"]); });
+  R.add("strategic_merge_patch", [](const Json& a) -> Json { return strategic_merge_patch(a["target"], a["patch"]); });
+  R.add("validate_schema", [](const Json& a) -> Json {
+    Json out = Json::array();
+    for (const auto& e : validate_schema(a["schema"], a["value"])) out.push_back(e);
+    return out;
+  });
+  R.add("builtin_crds", [](const Json&) -> Json {
+    Json out = Json::array();
+    for (const auto& c : builtin_crds()) out.push_back(c);
+    return out;
+  });
+}
+
+void register_notebook(CapiRegistry& R) {
+  R.add("generate_statefulset", [](const Json& a) -> Json { return generate_statefulset(a["notebook"], nb_opts(a["options"])); });
+  R.add("generate_service", [](const Json& a) -> Json { return generate_service(a["notebook"]); });
+  R.add("generate_virtual_service", [](const Json& a) -> Json { return generate_virtual_service(a["notebook"], nb_opts(a["options"])); });
+  R.add("virtual_service_name", [](const Json& a) -> Json { return virtual_service_name(a["name"].as_string(), a["namespace"].as_string()); });
+  R.add("create_notebook_status", [](const Json& a) -> Json { return create_notebook_status(a["notebook"], a["statefulset"], a["pod"]); });
+  R.add("pod_cond_to_notebook_cond", [](const Json& a) -> Json { return pod_cond_to_notebook_cond(a["condition"]); });
+  R.add("copy_statefulset_fields", [](const Json& a) -> Json {
+    Json to = a["to"];
+    bool changed = copy_statefulset_fields(a["from"], to);
+    return Json{{"changed", changed}, {"to", to}};
+  });
+  R.add("copy_service_fields", [](const Json& a) -> Json {
+    Json to = a["to"];
+    bool changed = copy_service_fields(a["from"], to);
+    return Json{{"changed", changed}, {"to", to}};
+  });
+  R.add("stop_annotation_is_set", [](const Json& a) -> Json { return stop_annotation_is_set(a["object"]); });
+  R.add("set_stop_annotation", [](const Json& a) -> Json {
+    Json nb = a["object"];
+    set_stop_annotation(nb, nullptr);
+    return nb;
+  });
+  R.add("all_kernels_are_idle", [](const Json& a) -> Json { return all_kernels_are_idle(a["kernels"]); });
+  R.add("notebook_recent_time", [](const Json& a) -> Json {
+    std::vector<std::string> t;
+    for (const auto& x : a["times"].as_array()) t.push_back(x.as_string());
+    return notebook_recent_time(t);
+  });
+  R.add("update_timestamp_from_kernels_activity", [](const Json& a) -> Json {
+    Json ann = a["annotations"].is_object() ? a["annotations"] : Json::object();
+    bool ch = update_timestamp_from_kernels_activity(ann, a["kernels"]);
+    return Json{{"changed", ch}, {"annotations", ann}};
+  });
+  R.add("update_timestamp_from_terminals_activity", [](const Json& a) -> Json {
+    Json ann = a["annotations"].is_object() ? a["annotations"] : Json::object();
+    bool ch = update_timestamp_from_terminals_activity(ann, a["terminals"]);
+    return Json{{"changed", ch}, {"annotations", ann}};
+  });
+  R.add("notebook_is_idle", [](const Json& a) -> Json {
+    return notebook_is_idle(a["notebook"], a["cull_idle_minutes"].as_int(1440), a["now_ms"].as_int(now_unix_ms()));
+  });
+  R.add("culling_check_period_has_passed", [](const Json& a) -> Json {
+    return culling_check_period_has_passed(a["notebook"], a["period_s"].as_double(), a["now_ms"].as_int(now_unix_ms()));
+  });
+}
+
+void register_profile(CapiRegistry& R) {
+  R.add("set_namespace_labels", [](const Json& a) -> Json {
+    Json ns = a["namespace"];
+    std::map<std::string, std::string> l;
+    for (const auto& m : a["labels"].as_object()) l[m.first] = m.second.as_string();
+    set_namespace_labels(ns, l);
+    return ns;
+  });
+  R.add("parse_flat_yaml_map", [](const Json& a) -> Json {
+    bool ok = true;
+    Json m = Json::object();
+    for (const auto& kv : parse_flat_yaml_map(a["text"].as_string(), &ok)) m[kv.first] = kv.second;
+    return Json{{"ok", ok}, {"map", m}};
+  });
+  R.add("get_issuer_url_from_provider_arn", [](const Json& a) -> Json { return get_issuer_url_from_provider_arn(a["arn"].as_string()); });
+  R.add("get_iam_role_name_from_iam_role_arn", [](const Json& a) -> Json { return get_iam_role_name_from_iam_role_arn(a["arn"].as_string()); });
+  R.add("add_service_account_in_assume_role_policy", [](const Json& a) -> Json {
+    std::string out;
+    bool exists = false;
+    bool ch = add_service_account_in_assume_role_policy(a["doc"].as_string(), a["namespace"].as_string(), a["sa"].as_string(), out, &exists);
+    return Json{{"changed", ch}, {"exists", exists}, {"doc", out}};
+  });
+  R.add("remove_service_account_in_assume_role_policy", [](const Json& a) -> Json {
+    std::string out;
+    bool ch = remove_service_account_in_assume_role_policy(a["doc"].as_string(), a["namespace"].as_string(), a["sa"].as_string(), out);
+    return Json{{"changed", ch}, {"doc", out}};
+  });
+  R.add("gcp_project_id", [](const Json& a) -> Json { return gcp_project_id(a["sa"].as_string()); });
+  R.add("gcp_add_binding", [](const Json& a) -> Json {
+    Json p = a["policy"];
+    gcp_add_binding(p, a["member"].as_string());
+    return p;
+  });
+  R.add("gcp_revoke_binding", [](const Json& a) -> Json {
+    Json p = a["policy"];
+    gcp_revoke_binding(p, a["member"].as_string());
+    return p;
+  });
+  R.add("authorization_policy_spec", [](const Json& a) -> Json {
+    ProfileOptions o;
+    if (a["userid_header"].is_string()) o.userid_header = a["userid_header"].as_string();
+    if (a["userid_prefix"].is_string()) o.userid_prefix = a["userid_prefix"].as_string();
+    return authorization_policy_spec(a["profile"], o);
+  });
+}
+
+void register_admission(CapiRegistry& R) {
+  R.add("merge_map", [](const Json& a) -> Json {
+    Json out;
+    std::string err;
+    bool ok = merge_map(a["existing"], vec(a["defaults"]), out, &err);
+    return Json{{"ok", ok}, {"out", out}, {"error", err}};
+  });
+  R.add("filter_pod_defaults", [](const Json& a) -> Json {
+    Json out = Json::array();
+    for (const auto& p : filter_pod_defaults(vec(a["poddefaults"]), a["pod"])) out.push_back(p);
+    return out;
+  });
+  R.add("safe_to_apply_pod_defaults", [](const Json& a) -> Json { return safe_to_apply_pod_defaults(a["pod"], vec(a["poddefaults"])); });
+  R.add("apply_pod_defaults", [](const Json& a) -> Json {
+    Json pod = a["pod"];
+    apply_pod_defaults(pod, vec(a["poddefaults"]));
+    return pod;
+  });
+  R.add("set_command_and_args", [](const Json& a) -> Json {
+    Json c = a["container"];
+    set_command_and_args(c, vec(a["poddefaults"]));
+    return c;
+  });
+  R.add("pod_quota_usage", [](const Json& a) -> Json {
+    Json out = Json::object();
+    for (const auto& kv : pod_quota_usage(a["pod"], a["hbm_gib_per_gpu"].as_int(288))) out[kv.first] = kv.second;
+    return out;
+  });
+  R.add("gpu_readiness_mutate", [](const Json& a) -> Json {
+    auto fn = make_gpu_readiness_plugin();
+    Json pod = a["pod"];
+    AdmissionAttrs at;
+    at.operation = "CREATE";
+    auto res = std::make_shared<ResourceInfo>();
+    res->kind = "Pod";
+    at.res = res;
+    at.object = &pod;
+    ApiError e = fn(at);
+    if (e) throw std::runtime_error(e.message);
+    return pod;
+  });
+}
+
+void register_gpu(CapiRegistry& R) {
+  R.add("topology_synthetic", [](const Json& a) -> Json { return topo_from(a).to_json(); });
+  R.add("topology_discover", [](const Json& a) -> Json {
+    return a["root"].is_string() ? GpuTopology::discover(a["root"].as_string()).to_json() : GpuTopology::discover().to_json();
+  });
+  R.add("gpu_choose", [](const Json& a) -> Json {
+    GpuTopology t = topo_from(a);
+    std::set<int> free;
+    if (a["free"].is_array()) {
+      for (const auto& x : a["free"].as_array()) free.insert(static_cast<int>(x.as_int()));
+    } else {
+      for (int i = 0; i < t.size(); ++i) free.insert(i);
+    }
+    Placement p;
+    if (!GpuAllocator::choose(t, free, static_cast<int>(a["n"].as_int()), p)) return Json();
+    return placement_json(p);
+  });
+  R.add("gpu_allocate_sequence", [](const Json& a) -> Json {
+    // [{"owner": "...", "n": 2} | {"release": "..."}] -> placements, exercising the allocator state
+    GpuAllocator alloc(topo_from(a));
+    Json out = Json::array();
+    for (const auto& op : a["ops"].as_array()) {
+      if (op["release"].is_string()) {
+        alloc.release(op["release"].as_string());
+        out.push_back(Json{{"released", op["release"]}, {"free", alloc.free_count()}});
+        continue;
+      }
+      Placement p;
+      bool ok = alloc.allocate(op["owner"].as_string(), static_cast<int>(op["n"].as_int()), p);
+      Json r = ok ? placement_json(p) : Json::object();
+      r["ok"] = ok;
+      r["free"] = alloc.free_count();
+      out.push_back(r);
+    }
+    return out;
+  });
+  R.add("gpu_env_for", [](const Json& a) -> Json {
+    GpuTopology t = topo_from(a);
+    Placement p;
+    for (const auto& x : a["devices"].as_array()) p.devices.push_back(static_cast<int>(x.as_int()));
+    p.ring = GpuAllocator::ring_order(t, p.devices);
+    return gpu_env_for(p, t, p.devices.size() > 1);
+  });
+}
+
+}  // namespace
+
+CapiRegistry& CapiRegistry::global() {
+  static CapiRegistry* r = [] {
+    auto* reg = new CapiRegistry();
+    register_core(*reg);
+    register_notebook(*reg);
+    register_profile(*reg);
+    register_admission(*reg);
+    register_gpu(*reg);
+    for (auto& ext : capi_extensions()) ext(*reg);
+    return reg;
+  }();
+  return *r;
+}
+
+std::vector<std::function<void(CapiRegistry&)>>& capi_extensions() {
+  static std::vector<std::function<void(CapiRegistry&)>> v;
+  return v;
+}
+
+}  // namespace kf
+
+extern "C" {
+
+char* kf_call(const char* name, const char* args_json) {
+  kf::Json out;
+  try {
+    kf::Json args;
+    std::string perr;
+    if (args_json && *args_json && !kf::Json::try_parse(args_json, args, &perr)) throw std::runtime_error("bad args json: " + perr);
+    auto& R = kf::CapiRegistry::global();
+    auto it = R.fns.find(name ? name : "");
+    if (it == R.fns.end()) throw std::runtime_error(std::string("unknown function: ") + (name ? name : ""));
+    out = kf::Json{{"ok", true}, {"result", it->second(args)}};
+  } catch (const std::exception& e) {
+    out = kf::Json{{"ok", false}, {"error", e.what()}};
+  }
+  const std::string s = out.dump();
+  char* buf = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return buf;
+}
+
+void kf_free(char* p) { std::free(p); }
+
+char* kf_functions() {
+  kf::Json names = kf::Json::array();
+  for (const auto& kv : kf::CapiRegistry::global().fns) names.push_back(kv.first);
+  const std::string s = names.dump();
+  char* buf = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return buf;
+}
+
+}  // extern "C"

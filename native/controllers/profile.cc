@@ -155,6 +155,14 @@ bool remove_service_account_in_assume_role_policy(const std::string& doc, const 
   return true;
 }
 
+std::string gcp_project_id(const std::string& gsa) {
+  // <name>@<project>.iam.gserviceaccount.com -> <project>
+  const size_t at = gsa.find('@');
+  std::string project = at == std::string::npos ? "" : gsa.substr(at + 1);
+  const size_t dot = project.find('.');
+  return dot == std::string::npos ? project : project.substr(0, dot);
+}
+
 void gcp_add_binding(Json& policy, const std::string& member) {
   policy["bindings"].push_back(Json{{"role", WORKLOAD_IDENTITY_ROLE}, {"members", Json::array({member})}});
 }
@@ -293,10 +301,7 @@ ApiError ProfileReconciler::apply_plugins(const Json& profile, bool revoke) {
       });
       if (e && e.code != 404) return e;
       // IAM binding on the GCP service account: <project>.svc.id.goog[ns/default-editor]
-      const size_t at = gsa.find('@');
-      std::string project = at == std::string::npos ? "" : gsa.substr(at + 1);
-      size_t dot = project.find('.');
-      if (dot != std::string::npos) project = project.substr(0, dot);
+      const std::string project = gcp_project_id(gsa);
       const std::string member = "serviceAccount:" + project + ".svc.id.goog[" + ns + "/" + DEFAULT_EDITOR + "]";
       Json policy;
       e = iam_->get_sa_iam_policy(gsa, policy);

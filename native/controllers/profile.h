@@ -58,6 +58,7 @@ bool add_service_account_in_assume_role_policy(const std::string& doc, const std
                                                std::string& out, bool* exists);
 bool remove_service_account_in_assume_role_policy(const std::string& doc, const std::string& ns, const std::string& sa,
                                                   std::string& out);
+std::string gcp_project_id(const std::string& gcp_service_account);
 void gcp_add_binding(Json& policy, const std::string& member);
 void gcp_revoke_binding(Json& policy, const std::string& member);
 

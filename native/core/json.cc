@@ -760,4 +760,20 @@ Json strategic_merge_patch(const Json& target, const Json& patch, const std::str
   return result;
 }
 
+void prune_nulls(Json& v) {
+  if (v.is_object()) {
+    auto& o = v.mut_object();
+    for (auto it = o.begin(); it != o.end();) {
+      if (it->second.is_null()) {
+        it = o.erase(it);
+      } else {
+        prune_nulls(it->second);
+        ++it;
+      }
+    }
+  } else if (v.is_array()) {
+    for (auto& e : v.mut_array()) prune_nulls(e);
+  }
+}
+
 }  // namespace kf

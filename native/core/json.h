@@ -121,6 +121,9 @@ class Json {
 
 // RFC 7386: null values delete, objects merge recursively, everything else replaces.
 Json merge_patch(const Json& target, const Json& patch);
+// Drops null-valued object members recursively (typed Kubernetes decoding and CRD pruning treat
+// an explicit null like an absent field); array elements are kept but recursed into.
+void prune_nulls(Json& v);
 // RFC 7396-style diff producing a merge patch that turns `from` into `to`.
 Json diff_merge_patch(const Json& from, const Json& to);
 // RFC 6902 apply. Throws JsonError on a failed `test` or invalid path.

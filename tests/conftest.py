@@ -33,3 +33,33 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def _ensure_native() -> None:
+    """Build the native control plane (and the kernel library it links) when missing."""
+    lib = ROOT / "kubeflow_rm_amd" / "lib"
+    bin_dir = ROOT / "kubeflow_rm_amd" / "bin"
+    if (lib / "libkfcore_capi.so").exists() and (bin_dir / "kflite").exists():
+        return
+    from kubeflow_rm_amd import _build
+    if not (lib / "libkfamd_kernels.so").exists():
+        _build.build_kernels()
+    _build.build_native()
+
+
+@pytest.fixture(scope="session")
+def native():
+    _ensure_native()
+    from kubeflow_rm_amd import native as nat
+    return nat
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    """One kube-lite control plane (all controllers, synthetic 8x MI355X node) per test module."""
+    _ensure_native()
+    from kubeflow_rm_amd.cluster import LocalCluster
+    cl = LocalCluster(env={"ENABLE_CULLING": "false"})
+    cl.start()
+    yield cl
+    cl.stop()

@@ -1,0 +1,149 @@
+"""Admission plugins (native): PodDefault merge, GPU readiness injection, MI355X quota accounting.
+
+Ported cases: reference components/admission-webhook/main_test.go:12-324 (mergeMap,
+applyPodDefaultsOnPod, setCommandAndArgs). Note the reference's TestApplyPodDefaultsOnPod asserts
+with an inverted DeepEqual check (it fails only when the output *equals* the expectation); these
+tests assert the intended result.
+"""
+import pytest
+
+ANN = "poddefault.admission.kubeflow.org/poddefault-"
+
+
+def test_merge_map_conflict(native):
+    r = native.call("merge_map", existing={"foo": "bar"}, defaults=[{"foo": "buz"}])
+    assert r["ok"] is False and "foo" in r["error"]
+
+
+@pytest.mark.parametrize("existing,default,out", [
+    ({"foo": "bar"}, {"baz": "bux"}, {"foo": "bar", "baz": "bux"}),
+    ({"foo": "bar"}, {}, {"foo": "bar"}),
+    ({"foo": "bar"}, {"foo": "bar"}, {"foo": "bar"}),
+], ids=["Add annotation", "Add nothing", "Same k/v in annotations"])
+def test_merge_map_good(native, existing, default, out):
+    r = native.call("merge_map", existing=existing, defaults=[default])
+    assert r["ok"] and r["out"] == out
+
+
+def _pd(name="", **spec):
+    return {"metadata": {"name": name, "namespace": "ns", "resourceVersion": ""}, "spec": spec}
+
+
+def _apply(native, pod, pds):
+    assert native.call("safe_to_apply_pod_defaults", pod=pod, poddefaults=pds) == ""
+    return native.call("apply_pod_defaults", pod=pod, poddefaults=pds)
+
+
+def test_apply_annotations_sa_automount(native):
+    out = _apply(native, {"metadata": {"annotations": {"foo": "bar"}}, "spec": {}},
+                 [_pd(annotations={"baz": "bux"}, serviceAccountName="some-service-account", automountServiceAccountToken=True)])
+    assert out["metadata"]["annotations"] == {"foo": "bar", "baz": "bux", ANN: ""}
+    assert out["spec"]["serviceAccountName"] == "some-service-account"
+    assert out["spec"]["automountServiceAccountToken"] is True
+
+
+def test_apply_same_kv(native):
+    out = _apply(native, {"metadata": {"annotations": {"foo": "bar"}}, "spec": {}}, [_pd(annotations={"foo": "bar"})])
+    assert out["metadata"]["annotations"] == {"foo": "bar", ANN: ""}
+
+
+def test_apply_tolerations(native):
+    old = {"key": "oldToleration", "operator": "Exists", "effect": "NoSchedule"}
+    new = {"key": "newToleration", "operator": "Equal", "value": "foo", "effect": "NoSchedule"}
+    out = _apply(native, {"metadata": {}, "spec": {"tolerations": [old]}}, [_pd(tolerations=[new])])
+    assert out["spec"]["tolerations"] == [old, new]
+
+
+def test_apply_init_containers(native):
+    ic = {"command": ["cmd1"], "args": ["arg1", "arg2"], "image": "nginx", "name": "test initcontainer and sidecar"}
+    out = _apply(native, {"metadata": {}, "spec": {"containers": []}}, [_pd(initContainers=[ic])])
+    assert out["spec"]["initContainers"] == [ic]
+
+
+def test_apply_env_volumes_mounts_sidecars(native):
+    pod = {"metadata": {"name": "p", "namespace": "ns", "labels": {"x": "y"}},
+           "spec": {"containers": [{"name": "main", "image": "img", "env": [{"name": "A", "value": "1"}]}]}}
+    pd = _pd("gpu-env", env=[{"name": "HSA_XNACK", "value": "0"}],
+             envFrom=[{"configMapRef": {"name": "cm"}}],
+             volumes=[{"name": "shm", "emptyDir": {"medium": "Memory"}}],
+             volumeMounts=[{"name": "shm", "mountPath": "/dev/shm"}],
+             sidecars=[{"name": "side", "image": "busybox"}],
+             labels={"team": "ml"})
+    out = _apply(native, pod, [pd])
+    main = out["spec"]["containers"][0]
+    assert main["env"] == [{"name": "A", "value": "1"}, {"name": "HSA_XNACK", "value": "0"}]
+    assert main["envFrom"] == [{"configMapRef": {"name": "cm"}}]
+    assert main["volumeMounts"] == [{"name": "shm", "mountPath": "/dev/shm"}]
+    assert out["spec"]["volumes"] == [{"name": "shm", "emptyDir": {"medium": "Memory"}}]
+    assert [c["name"] for c in out["spec"]["containers"]] == ["main", "side"]
+    assert out["metadata"]["labels"] == {"x": "y", "team": "ml"}
+    assert out["metadata"]["annotations"]["poddefault.admission.kubeflow.org/poddefault-gpu-env"] == ""
+
+
+@pytest.mark.parametrize("field,pod_spec,pd_spec", [
+    ("env", {"containers": [{"name": "c", "image": "i", "env": [{"name": "A", "value": "1"}]}]}, {"env": [{"name": "A", "value": "2"}]}),
+    ("volumes", {"volumes": [{"name": "v", "emptyDir": {}}], "containers": []}, {"volumes": [{"name": "v", "hostPath": {"path": "/x"}}]}),
+    ("mount path", {"containers": [{"name": "c", "image": "i", "volumeMounts": [{"name": "a", "mountPath": "/data"}]}]},
+     {"volumeMounts": [{"name": "b", "mountPath": "/data"}]}),
+])
+def test_conflicts_are_rejected(native, field, pod_spec, pd_spec):
+    err = native.call("safe_to_apply_pod_defaults", pod={"metadata": {}, "spec": pod_spec}, poddefaults=[_pd("pd", **pd_spec)])
+    assert "conflict" in err
+
+
+def test_set_command_and_args(native):
+    pds = [_pd("test-pod-default", command=["cmd1"], args=["arg1", "arg2"])]
+    assert native.call("set_command_and_args", container={}, poddefaults=pds) == {"command": ["cmd1"], "args": ["arg1", "arg2"]}
+    c = {"command": ["cmd2"], "args": ["arg3", "arg4"]}
+    assert native.call("set_command_and_args", container=c, poddefaults=pds) == c
+    # never on the istio sidecar
+    assert native.call("set_command_and_args", container={"name": "istio-proxy"}, poddefaults=pds) == {"name": "istio-proxy"}
+
+
+def test_filter_pod_defaults(native):
+    pds = [{"metadata": {"name": "a", "namespace": "ns"}, "spec": {"selector": {"matchLabels": {"add-a": "true"}}}},
+           {"metadata": {"name": "b", "namespace": "ns"}, "spec": {"selector": {"matchLabels": {"add-b": "true"}}}},
+           {"metadata": {"name": "c", "namespace": "other"}, "spec": {"selector": {"matchLabels": {"add-a": "true"}}}}]
+    pod = {"metadata": {"namespace": "ns", "labels": {"add-a": "true"}}}
+    assert [p["metadata"]["name"] for p in native.call("filter_pod_defaults", poddefaults=pds, pod=pod)] == ["a"]
+
+
+# ---- GPU readiness init container (MI355X) ------------------------------------------------------
+def test_gpu_readiness_injected_for_gpu_notebooks(native):
+    pod = {"metadata": {"labels": {"notebook-name": "nb"}},
+           "spec": {"containers": [{"name": "nb", "image": "x", "resources": {"limits": {"amd.com/gpu": "2"}}}]}}
+    out = native.call("gpu_readiness_mutate", pod=pod)
+    ic = out["spec"]["initContainers"][0]
+    assert ic["name"] == "gpu-readiness" and ic["command"] == ["kfamd-readiness"]
+    assert ic["resources"]["limits"]["amd.com/gpu"] == "2"
+    # idempotent
+    assert native.call("gpu_readiness_mutate", pod=out)["spec"]["initContainers"] == out["spec"]["initContainers"]
+
+
+@pytest.mark.parametrize("pod", [
+    {"metadata": {"labels": {"notebook-name": "nb"}}, "spec": {"containers": [{"name": "nb", "image": "x"}]}},
+    {"metadata": {}, "spec": {"containers": [{"name": "nb", "image": "x", "resources": {"limits": {"amd.com/gpu": "1"}}}]}},
+    {"metadata": {"labels": {"notebook-name": "nb"}, "annotations": {"kfamd.io/gpu-readiness-op": "false"}},
+     "spec": {"containers": [{"name": "nb", "image": "x", "resources": {"limits": {"amd.com/gpu": "1"}}}]}},
+], ids=["no-gpu", "not-a-notebook", "opted-out"])
+def test_gpu_readiness_not_injected(native, pod):
+    assert "initContainers" not in native.call("gpu_readiness_mutate", pod=pod)["spec"]
+
+
+# ---- quota ----------------------------------------------------------------------------------
+def test_pod_quota_usage_gpu_and_hbm(native):
+    pod = {"spec": {"containers": [
+        {"name": "a", "resources": {"limits": {"amd.com/gpu": "2", "cpu": "4", "memory": "8Gi"}}},
+        {"name": "b", "resources": {"requests": {"cpu": "500m"}}}],
+        "initContainers": [{"name": "i", "resources": {"limits": {"amd.com/gpu": "2", "cpu": "8"}}}]}}
+    u = native.call("pod_quota_usage", pod=pod)
+    assert u["requests.amd.com/gpu"] == 2 and u["amd.com/gpu"] == 2
+    assert u["amd.com/gpu-memory"] == 2 * 288  # 288 GiB HBM3E per MI355X
+    assert u["requests.cpu"] == 8  # max(sum(app)=4.5, max(init)=8)
+    assert u["limits.memory"] == 8 * 2 ** 30
+    assert u["pods"] == 1
+
+
+def test_pod_quota_usage_explicit_hbm(native):
+    pod = {"spec": {"containers": [{"name": "a", "resources": {"limits": {"amd.com/gpu": "1", "amd.com/gpu-memory": "96"}}}]}}
+    assert native.call("pod_quota_usage", pod=pod)["amd.com/gpu-memory"] == 96
