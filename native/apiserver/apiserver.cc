@@ -510,7 +510,7 @@ void ApiServer::broadcast(std::shared_ptr<const ResourceInfo> res, const std::st
   }
 }
 
-void ApiServer::commit_put(std::shared_ptr<const ResourceInfo> res, const std::string& key, Json obj,
+void ApiServer::commit_put(std::shared_ptr<const ResourceInfo> res, const std::string& key, Json& obj,
                            const std::string& type) {
   // caller holds mu_
   const std::string rk = res->key();

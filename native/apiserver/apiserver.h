@@ -205,7 +205,7 @@ class ApiServer {
   void convert_out(std::shared_ptr<const ResourceInfo> res, const std::string& version, Json& obj) const;
   void to_storage(std::shared_ptr<const ResourceInfo> res, Json& obj) const;
   std::string object_key(const std::string& ns, const std::string& name) const { return ns + "/" + name; }
-  void commit_put(std::shared_ptr<const ResourceInfo> res, const std::string& key, Json obj, const std::string& type);
+  void commit_put(std::shared_ptr<const ResourceInfo> res, const std::string& key, Json& obj, const std::string& type);  // stamps obj.metadata.resourceVersion
   void commit_delete(std::shared_ptr<const ResourceInfo> res, const std::string& key);
   void broadcast(std::shared_ptr<const ResourceInfo> res, const std::string& type, const Json& obj,
                  const Json* old_obj, int64_t rv);

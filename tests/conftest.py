@@ -59,7 +59,7 @@ def cluster():
     """One kube-lite control plane (all controllers, synthetic 8x MI355X node) per test module."""
     _ensure_native()
     from kubeflow_rm_amd.cluster import LocalCluster
-    cl = LocalCluster(env={"ENABLE_CULLING": "false"})
+    cl = LocalCluster(env={"ENABLE_CULLING": "false", "USE_ISTIO": "true"})
     cl.start()
     yield cl
     cl.stop()
