@@ -74,3 +74,28 @@ def port_free(host: str, port: int) -> bool:
             return True
         except OSError:
             return False
+
+
+def mounts() -> dict:
+    """Container mountPath -> host directory for this process pod (set by the kflite kubelet)."""
+    try:
+        return json.loads(os.environ.get("KFAMD_VOLUME_MOUNTS") or "{}")
+    except ValueError:
+        return {}
+
+
+def resolve_path(container_path: str) -> str:
+    """Translate a path as the container sees it into the host path backing it (longest mount
+    prefix wins; anything else lives under the pod's rootfs)."""
+    best = ""
+    for mp in mounts():
+        norm = mp.rstrip("/") or "/"
+        if (container_path == norm or container_path.startswith(norm.rstrip("/") + "/")) and len(norm) > len(best):
+            best = norm
+    if best:
+        rest = container_path[len(best):].lstrip("/")
+        return os.path.join(mounts().get(best) or mounts().get(best + "/"), rest)
+    root = os.environ.get("KFAMD_ROOTFS")
+    if root and os.path.isabs(container_path):
+        return os.path.join(root, container_path.lstrip("/"))
+    return container_path

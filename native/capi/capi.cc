@@ -23,6 +23,8 @@
 #include "controllers/common.h"
 #include "controllers/notebook.h"
 #include "controllers/profile.h"
+#include "controllers/tensorboard.h"
+#include "core/yaml.h"
 #include "core/util.h"
 #include "gpu/topology.h"
 
@@ -83,6 +85,15 @@ void register_core(CapiRegistry& R) {
     for (const auto& e : validate_schema(a["schema"], a["value"])) out.push_back(e);
     return out;
   });
+  R.add("parse_yaml_all", [](const Json& a) -> Json {
+    std::vector<Json> docs;
+    std::string err;
+    if (!parse_yaml_all(a["text"].as_string(), docs, &err)) throw std::runtime_error(err);
+    Json out = Json::array();
+    for (auto& d : docs) out.push_back(d);
+    return out;
+  });
+  R.add("dump_yaml", [](const Json& a) -> Json { return dump_yaml(a["value"]); });
   R.add("builtin_crds", [](const Json&) -> Json {
     Json out = Json::array();
     for (const auto& c : builtin_crds()) out.push_back(c);
@@ -226,6 +237,37 @@ void register_admission(CapiRegistry& R) {
   });
 }
 
+void register_tensorboard(CapiRegistry& R) {
+  R.add("tb_paths", [](const Json& a) -> Json {
+    const std::string p = a["path"].as_string();
+    return Json{{"cloud", tb_is_cloud_path(p)}, {"gcs", tb_is_gcs_path(p)}, {"pvc", tb_is_pvc_path(p)},
+                {"pvc_name", tb_extract_pvc_name(p)}, {"pvc_subpath", tb_extract_pvc_subpath(p)}};
+  });
+  R.add("tb_generate_deployment", [](const Json& a) -> Json {
+    return tb_generate_deployment(a["tensorboard"], a["image"].as_string(), preferred_node_affinity(a["node"].as_string()));
+  });
+  R.add("tb_generate_service", [](const Json& a) -> Json { return tb_generate_service(a["tensorboard"]); });
+  R.add("tb_generate_virtual_service", [](const Json& a) -> Json {
+    return tb_generate_virtual_service(a["tensorboard"], a["gateway"].as_string(), a["host"].as_string());
+  });
+  R.add("tb_copy_deployment_fields", [](const Json& a) -> Json {
+    Json to = a["to"];
+    bool ch = tb_copy_deployment_fields(a["from"], to);
+    return Json{{"changed", ch}, {"to", to}};
+  });
+  R.add("tb_status", [](const Json& a) -> Json { return tb_status(a["tensorboard"], a["deployment"]); });
+  R.add("pvcviewer_default", [](const Json& a) -> Json { return pvcviewer_default(a["viewer"], a["default_pod_spec"]); });
+  R.add("pvcviewer_validate", [](const Json& a) -> Json { return pvcviewer_validate(a["viewer"]); });
+  R.add("pvcviewer_generate_deployment", [](const Json& a) -> Json {
+    return pvcviewer_generate_deployment(a["viewer"], preferred_node_affinity(a["node"].as_string()));
+  });
+  R.add("pvcviewer_generate_service", [](const Json& a) -> Json { return pvcviewer_generate_service(a["viewer"]); });
+  R.add("pvcviewer_generate_virtual_service", [](const Json& a) -> Json {
+    return pvcviewer_generate_virtual_service(a["viewer"], a["gateway"].as_string());
+  });
+  R.add("pvcviewer_rwo_node", [](const Json& a) -> Json { return pvcviewer_rwo_node(a["pvc"], vec(a["pods"])); });
+}
+
 void register_gpu(CapiRegistry& R) {
   R.add("topology_synthetic", [](const Json& a) -> Json { return topo_from(a).to_json(); });
   R.add("topology_discover", [](const Json& a) -> Json {
@@ -281,6 +323,7 @@ CapiRegistry& CapiRegistry::global() {
     register_profile(*reg);
     register_admission(*reg);
     register_gpu(*reg);
+    register_tensorboard(*reg);
     for (auto& ext : capi_extensions()) ext(*reg);
     return reg;
   }();

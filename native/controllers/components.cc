@@ -6,6 +6,7 @@
 #include "admission/admission.h"
 #include "controllers/builtin.h"
 #include "controllers/profile.h"
+#include "controllers/tensorboard.h"
 #include "controllers/notebook.h"
 #include "node/node.h"
 #include "core/util.h"
@@ -47,6 +48,8 @@ struct Components::Impl {
   std::unique_ptr<Gateway> gateway;
   std::unique_ptr<ProfileReconciler> profile;
   std::unique_ptr<QuotaController> quota;
+  std::unique_ptr<TensorboardReconciler> tensorboard;
+  std::unique_ptr<PVCViewerReconciler> pvcviewer;
   std::unique_ptr<AdmissionWebhookServer> webhooks;
   std::vector<std::function<void()>> starters, stoppers;
 };
@@ -100,11 +103,32 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       I.webhooks->add("/apply-poddefault", pd, true, pods);
       I.webhooks->add("/gpu-readiness", gpu, true, pods);
       I.webhooks->add("/quota", quota, false, pods);
+      auto viewers = reg.by_kind("kubeflow.org/v1alpha1", "PVCViewer");
+      I.webhooks->add("/mutate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_defaulter(), true, viewers);
+      I.webhooks->add("/validate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_validator(), false, viewers);
       if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
       I.stoppers.push_back([&I] { I.webhooks->stop(); });
     }
     I.quota = std::make_unique<QuotaController>(I.c);
     I.quota->setup(mgr);
+  }
+  if (enabled.count("tensorboard")) {
+    std::string terr;
+    TensorboardOptions to = TensorboardOptions::from_env(&terr);
+    if (!terr.empty()) {
+      *err = terr;
+      return false;
+    }
+    I.tensorboard = std::make_unique<TensorboardReconciler>(I.c, to);
+    I.tensorboard->setup(mgr, workers);
+  }
+  if (enabled.count("pvcviewer")) {
+    I.pvcviewer = std::make_unique<PVCViewerReconciler>(I.c);
+    I.pvcviewer->setup(mgr, workers);
+    if (I.api) {
+      I.api->add_mutating_plugin("mpvcviewer.kb.io", make_pvcviewer_defaulter());
+      I.api->add_validating_plugin("vpvcviewer.kb.io", make_pvcviewer_validator());
+    }
   }
   if (enabled.count("builtin")) {
     I.builtin = std::make_unique<BuiltinControllers>(I.c);
