@@ -25,6 +25,7 @@
 #include "controllers/profile.h"
 #include "controllers/tensorboard.h"
 #include "core/yaml.h"
+#include "kfam/kfam.h"
 #include "core/util.h"
 #include "gpu/topology.h"
 
@@ -268,6 +269,14 @@ void register_tensorboard(CapiRegistry& R) {
   R.add("pvcviewer_rwo_node", [](const Json& a) -> Json { return pvcviewer_rwo_node(a["pvc"], vec(a["pods"])); });
 }
 
+void register_kfam(CapiRegistry& R) {
+  R.add("kfam_binding_name", [](const Json& a) -> Json { return kfam_binding_name(a["binding"]); });
+  R.add("kfam_role_map", [](const Json& a) -> Json { return kfam_role_map(a["role"].as_string()); });
+  R.add("kfam_authorization_policy_spec", [](const Json& a) -> Json {
+    return kfam_authorization_policy_spec(a["binding"], a["userid_header"].as_string(), a["userid_prefix"].as_string());
+  });
+}
+
 void register_gpu(CapiRegistry& R) {
   R.add("topology_synthetic", [](const Json& a) -> Json { return topo_from(a).to_json(); });
   R.add("topology_discover", [](const Json& a) -> Json {
@@ -324,6 +333,7 @@ CapiRegistry& CapiRegistry::global() {
     register_admission(*reg);
     register_gpu(*reg);
     register_tensorboard(*reg);
+    register_kfam(*reg);
     for (auto& ext : capi_extensions()) ext(*reg);
     return reg;
   }();

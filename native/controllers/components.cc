@@ -7,6 +7,7 @@
 #include "controllers/builtin.h"
 #include "controllers/profile.h"
 #include "controllers/tensorboard.h"
+#include "kfam/kfam.h"
 #include "controllers/notebook.h"
 #include "node/node.h"
 #include "core/util.h"
@@ -50,6 +51,7 @@ struct Components::Impl {
   std::unique_ptr<QuotaController> quota;
   std::unique_ptr<TensorboardReconciler> tensorboard;
   std::unique_ptr<PVCViewerReconciler> pvcviewer;
+  std::unique_ptr<KfamService> kfam;
   std::unique_ptr<AdmissionWebhookServer> webhooks;
   std::vector<std::function<void()>> starters, stoppers;
 };
@@ -130,6 +132,15 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       I.api->add_validating_plugin("vpvcviewer.kb.io", make_pvcviewer_validator());
     }
   }
+  if (enabled.count("kfam") || I.f.kfam_port >= 0) {
+    KfamOptions ko;
+    ko.userid_header = I.f.userid_header;
+    ko.userid_prefix = I.f.userid_prefix;
+    if (!I.f.cluster_admin.empty()) ko.cluster_admins.push_back(I.f.cluster_admin);
+    I.kfam = std::make_unique<KfamService>(I.c, ko, &mgr.informer("rbac.authorization.k8s.io/v1", "RoleBinding"));
+    if (!I.kfam->start("127.0.0.1", static_cast<int>(I.f.kfam_port < 0 ? 0 : I.f.kfam_port), err)) return false;
+    I.stoppers.push_back([&I] { I.kfam->stop(); });
+  }
   if (enabled.count("builtin")) {
     I.builtin = std::make_unique<BuiltinControllers>(I.c);
     I.builtin->setup(mgr, workers);
@@ -192,7 +203,7 @@ void Components::stop() {
 }
 
 int Components::gateway_port() const { return impl_->gateway ? impl_->gateway->port() : 0; }
-int Components::kfam_port() const { return 0; }
+int Components::kfam_port() const { return impl_->kfam ? impl_->kfam->port() : 0; }
 int Components::webhook_port() const { return impl_->webhooks ? impl_->webhooks->port() : 0; }
 
 }  // namespace kf

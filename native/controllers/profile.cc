@@ -16,20 +16,41 @@ namespace {
 std::string trunc30(const std::string& s) { return s.size() > 30 ? s.substr(0, 30) : s; }
 }  // namespace
 
+// One family per metric name for the whole process (kflite hosts profile controller + KFAM):
+// the label set is the union of both components' (monitoring.go of each), unused ones empty.
+namespace {
+std::shared_ptr<CounterVec> request_family() {
+  static auto c = Registry::global().counter("request_kf", "Number of request_counter",
+                                             {"component", "kind", "request_user", "action", "path"});
+  return c;
+}
+std::shared_ptr<CounterVec> request_failure_family() {
+  static auto c = Registry::global().counter("request_kf_failure", "Number of request_failure_counter",
+                                             {"component", "kind", "request_user", "action", "path", "severity"});
+  return c;
+}
+}  // namespace
+
 void inc_request_counter(const std::string& kind, const std::string& component) {
-  static auto c = Registry::global().counter("request_kf", "Number of request_counter", {"component", "kind"});
-  c->inc({component, trunc30(kind)});
+  request_family()->inc({component, trunc30(kind), "", "", ""});
 }
 void inc_request_error_counter(const std::string& kind, const std::string& severity, const std::string& component) {
-  static auto c = Registry::global().counter("request_kf_failure", "Number of request_failure_counter",
-                                             {"component", "kind", "severity"});
-  c->inc({component, trunc30(kind), severity});
+  request_failure_family()->inc({component, trunc30(kind), "", "", "", severity});
 }
-Heartbeat::Heartbeat(std::string component, double period_s) : component_(std::move(component)) {
+void inc_request_counter_full(const std::string& component, const std::string& kind, const std::string& user,
+                              const std::string& action, const std::string& path) {
+  request_family()->inc({component, trunc30(kind), user, action, path});
+}
+void inc_request_error_counter_full(const std::string& component, const std::string& kind, const std::string& user,
+                                    const std::string& action, const std::string& path, const std::string& severity) {
+  request_failure_family()->inc({component, trunc30(kind), user, action, path, severity});
+}
+Heartbeat::Heartbeat(std::string component, double period_s, std::string severity)
+    : component_(std::move(component)), severity_(std::move(severity)) {
   static auto hb = Registry::global().counter("service_heartbeat", "Heartbeat signal every 10 seconds", {"component", "severity"});
   th_ = std::thread([this, period_s] {
     while (run_) {
-      hb->inc({component_, "minor"});
+      hb->inc({component_, severity_});
       for (int i = 0; i < static_cast<int>(period_s * 10) && run_; ++i) ::usleep(100000);
     }
   });

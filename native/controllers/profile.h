@@ -28,13 +28,18 @@ constexpr const char* WORKLOAD_IDENTITY_ROLE = "roles/iam.workloadIdentityUser";
 void inc_request_counter(const std::string& kind, const std::string& component = "profile-controller");
 void inc_request_error_counter(const std::string& kind, const std::string& severity,
                                const std::string& component = "profile-controller");
+// KFAM flavour (kfam/monitoring.go): also labels the requesting user, action and path.
+void inc_request_counter_full(const std::string& component, const std::string& kind, const std::string& user,
+                              const std::string& action, const std::string& path);
+void inc_request_error_counter_full(const std::string& component, const std::string& kind, const std::string& user,
+                                    const std::string& action, const std::string& path, const std::string& severity);
 class Heartbeat {
  public:
-  explicit Heartbeat(std::string component, double period_s = 10.0);
+  explicit Heartbeat(std::string component, double period_s = 10.0, std::string severity = "minor");
   ~Heartbeat();
 
  private:
-  std::string component_;
+  std::string component_, severity_;
   std::atomic<bool> run_{true};
   std::thread th_;
 };

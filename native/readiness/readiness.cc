@@ -173,14 +173,14 @@ bool gemm_check(int dev, const Args& a, Json& out) {
   out = Json{{"device", dev}, {"shape", std::to_string(a.m) + "x" + std::to_string(a.n) + "x" + std::to_string(a.k)},
              {"tflops", std::round(tflops * 10) / 10}, {"ms_per_gemm", ms / a.iters}, {"max_abs_err", max_err},
              {"correct", ok}};
-  hipFree(A);
-  hipFree(B);
-  hipFree(C);
-  hipFree(drows);
-  hipFree(dref);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipStreamDestroy(s);
+  (void)hipFree(A);
+  (void)hipFree(B);
+  (void)hipFree(C);
+  (void)hipFree(drows);
+  (void)hipFree(dref);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
   if (!ok) fail("GEMM result mismatch on device " + std::to_string(dev));
   if (a.min_tflops > 0 && tflops < a.min_tflops)
     fail("GEMM " + std::to_string(tflops) + " TFLOPS below --min-tflops on device " + std::to_string(dev));
@@ -247,13 +247,13 @@ bool ln_check(int dev, const Args& a, Json& out) {
   const bool ok = max_err < 5e-2;
   out = Json{{"device", dev}, {"shape", std::to_string(a.ln_rows) + "x" + std::to_string(a.ln_hidden)},
              {"GBps", std::round(gbps)}, {"max_abs_err", max_err}, {"correct", ok}};
-  hipFree(x);
-  hipFree(y);
-  hipFree(g);
-  hipFree(b);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipStreamDestroy(s);
+  (void)hipFree(x);
+  (void)hipFree(y);
+  (void)hipFree(g);
+  (void)hipFree(b);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
   if (!ok) fail("LayerNorm mismatch on device " + std::to_string(dev));
   return ok;
 }
@@ -329,9 +329,9 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
                          {"busbw_GBps", algbw * 2.0 * (ndev - 1) / ndev}});
   }
   for (int i = 0; i < ndev; ++i) {
-    hipSetDevice(i);
-    hipFree(buf[i]);
-    hipStreamDestroy(st[i]);
+    (void)hipSetDevice(i);
+    (void)hipFree(buf[i]);
+    (void)hipStreamDestroy(st[i]);
     ncclCommDestroy(comms[i]);
   }
   out = Json{{"devices", ndev}, {"comm_init_ms", init_ms}, {"peer_access", peer}, {"sweep", sweep}, {"correct", ok}};
