@@ -325,6 +325,13 @@ void ApiServer::apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& ob
           any = any || !c.at_path({"resources", "requests"}).empty() || !c.at_path({"resources", "limits"}).empty();
         if (any) obj["status"]["qosClass"] = "Burstable";
       }
+    } else if (k == "Secret") {
+      // stringData is write-only convenience: merged into data (base64) and dropped
+      if (obj["stringData"].is_object()) {
+        for (const auto& kv : obj["stringData"].as_object()) obj["data"][kv.first] = base64_encode(kv.second.as_string());
+        obj.erase("stringData");
+      }
+      if (!obj.has("type")) obj["type"] = "Opaque";
     } else if (k == "Service") {
       Json& spec = obj["spec"];
       if (!spec.has("type")) spec["type"] = "ClusterIP";

@@ -26,6 +26,7 @@
 #include "controllers/tensorboard.h"
 #include "core/yaml.h"
 #include "kfam/kfam.h"
+#include "controllers/odh.h"
 #include "core/util.h"
 #include "gpu/topology.h"
 
@@ -277,6 +278,45 @@ void register_kfam(CapiRegistry& R) {
   });
 }
 
+void register_odh(CapiRegistry& R) {
+  R.add("odh_flags", [](const Json& a) -> Json {
+    const Json& nb = a["notebook"];
+    return Json{{"oauth", odh_oauth_enabled(nb)}, {"mesh", odh_service_mesh_enabled(nb)}, {"lock", odh_lock_enabled(nb)}};
+  });
+  R.add("odh_inject_oauth_proxy", [](const Json& a) -> Json {
+    Json nb = a["notebook"];
+    odh_inject_oauth_proxy(nb, a["image"].as_string());
+    return nb;
+  });
+  R.add("odh_inject_cert_config", [](const Json& a) -> Json {
+    Json nb = a["notebook"];
+    odh_inject_cert_config(nb, a["configmap"].as_string());
+    return nb;
+  });
+  R.add("odh_unset_cert_config", [](const Json& a) -> Json {
+    Json nb = a["notebook"];
+    bool ch = odh_unset_cert_config(nb);
+    return Json{{"changed", ch}, {"notebook", nb}};
+  });
+  R.add("odh_set_image_from_imagestreams", [](const Json& a) -> Json {
+    Json nb = a["notebook"];
+    std::string err = odh_set_image_from_imagestreams(nb, vec(a["imagestreams"]));
+    return Json{{"error", err}, {"notebook", nb}};
+  });
+  R.add("json_first_difference", [](const Json& a) -> Json { return json_first_difference(a["a"], a["b"], a["type"].as_string()); });
+  R.add("pem_certificate_valid", [](const Json& a) -> Json { return pem_certificate_valid(a["pem"].as_string()); });
+  R.add("odh_objects", [](const Json& a) -> Json {
+    const Json& nb = a["notebook"];
+    return Json{{"network_policy", odh_network_policy(nb, a["controller_namespace"].as_string())},
+                {"oauth_network_policy", odh_oauth_network_policy(nb)},
+                {"route", odh_route(nb)},
+                {"oauth_route", odh_oauth_route(nb)},
+                {"service_account", odh_service_account(nb)},
+                {"oauth_service", odh_oauth_service(nb)},
+                {"oauth_secret", odh_oauth_secret(nb)}};
+  });
+}
+
 void register_gpu(CapiRegistry& R) {
   R.add("topology_synthetic", [](const Json& a) -> Json { return topo_from(a).to_json(); });
   R.add("topology_discover", [](const Json& a) -> Json {
@@ -334,6 +374,7 @@ CapiRegistry& CapiRegistry::global() {
     register_gpu(*reg);
     register_tensorboard(*reg);
     register_kfam(*reg);
+    register_odh(*reg);
     for (auto& ext : capi_extensions()) ext(*reg);
     return reg;
   }();

@@ -438,6 +438,44 @@ void BuiltinControllers::setup(Manager& mgr, int workers) {
     return out;
   });
   mgr.add(pvc_);
+  sa_ = std::make_shared<Controller>("serviceaccount-pull-secrets",
+                                     [this](const Request& r, std::string* e) { return reconcile_service_account(r, e); });
+  sa_->For(mgr.informer("v1", "ServiceAccount"));
+  mgr.add(sa_);
+}
+
+// OpenShift's service-account controller gives every ServiceAccount a dockercfg pull secret; the
+// ODH reconciler waits for it before releasing its reconciliation lock, so kube-lite emulates it.
+Result BuiltinControllers::reconcile_service_account(const Request& r, std::string* err) {
+  Json sa;
+  ApiError e = c_->get("v1", "ServiceAccount", r.ns, r.name, sa);
+  if (e.code == 404) return {};
+  if (e) {
+    *err = e.message;
+    return {};
+  }
+  if (!sa["imagePullSecrets"].empty() || sa.at_path({"metadata", "deletionTimestamp"}).is_string()) return {};
+  std::string sname = r.name + "-dockercfg-" + random_hex(3).substr(0, 5);
+  Json sec{{"apiVersion", "v1"},
+           {"kind", "Secret"},
+           {"metadata", Json{{"name", sname}, {"namespace", r.ns},
+                             {"annotations", Json{{"kubernetes.io/service-account.name", r.name}}}}},
+           {"type", "kubernetes.io/dockercfg"},
+           {"data", Json{{".dockercfg", base64_encode("{}")}}}};
+  set_controller_reference(sa, sec);
+  e = c_->create(sec);
+  if (e && e.code != 409) {
+    *err = e.message;
+    return {};
+  }
+  e = c_->update_with_retry("v1", "ServiceAccount", r.ns, r.name, [&](Json& o) {
+    if (!o["imagePullSecrets"].empty()) return false;
+    o["imagePullSecrets"] = Json::array({Json{{"name", sname}}});
+    o["secrets"].push_back(Json{{"name", sname}});
+    return true;
+  });
+  if (e && e.code != 404) *err = e.message;
+  return {};
 }
 
 }  // namespace kf

@@ -23,12 +23,13 @@ class BuiltinControllers {
   Result reconcile_deployment(const Request& r, std::string* err);
   Result reconcile_replicaset(const Request& r, std::string* err);
   Result reconcile_pvc(const Request& r, std::string* err);
+  Result reconcile_service_account(const Request& r, std::string* err);
 
  private:
   Json make_pod(const Json& owner, const Json& tmpl, const std::string& name, const Json& extra_labels);
   std::shared_ptr<Client> c_;
   Informer* pods_ = nullptr;
-  std::shared_ptr<Controller> sts_, dep_, rs_, pvc_;
+  std::shared_ptr<Controller> sts_, dep_, rs_, pvc_, sa_;
 };
 
 }  // namespace kf

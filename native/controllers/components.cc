@@ -5,6 +5,7 @@
 
 #include "admission/admission.h"
 #include "controllers/builtin.h"
+#include "controllers/odh.h"
 #include "controllers/profile.h"
 #include "controllers/tensorboard.h"
 #include "kfam/kfam.h"
@@ -52,6 +53,7 @@ struct Components::Impl {
   std::unique_ptr<TensorboardReconciler> tensorboard;
   std::unique_ptr<PVCViewerReconciler> pvcviewer;
   std::unique_ptr<KfamService> kfam;
+  std::unique_ptr<OdhNotebookReconciler> odh;
   std::unique_ptr<AdmissionWebhookServer> webhooks;
   std::vector<std::function<void()>> starters, stoppers;
 };
@@ -108,8 +110,7 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       auto viewers = reg.by_kind("kubeflow.org/v1alpha1", "PVCViewer");
       I.webhooks->add("/mutate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_defaulter(), true, viewers);
       I.webhooks->add("/validate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_validator(), false, viewers);
-      if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
-      I.stoppers.push_back([&I] { I.webhooks->stop(); });
+
     }
     I.quota = std::make_unique<QuotaController>(I.c);
     I.quota->setup(mgr);
@@ -131,6 +132,17 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       I.api->add_mutating_plugin("mpvcviewer.kb.io", make_pvcviewer_defaulter());
       I.api->add_validating_plugin("vpvcviewer.kb.io", make_pvcviewer_validator());
     }
+  }
+  if (enabled.count("odh")) {
+    OdhOptions oo;
+    oo.oauth_proxy_image = I.f.oauth_proxy_image;
+    oo.controller_namespace = I.f.controller_namespace;
+    oo.set_pipeline_rbac = to_lower(trim(getenv_or("SET_PIPELINE_RBAC", ""))) == "true";
+    I.odh = std::make_unique<OdhNotebookReconciler>(I.c, oo);
+    I.odh->setup(mgr, workers);
+    auto hook = make_odh_notebook_webhook(I.c, oo);
+    if (I.api) I.api->add_mutating_plugin("notebooks.opendatahub.io", hook);
+    if (I.webhooks) I.webhooks->add("/mutate-notebook-v1", hook, true, ResourceRegistry().by_kind("kubeflow.org/v1", "Notebook"));
   }
   if (enabled.count("kfam") || I.f.kfam_port >= 0) {
     KfamOptions ko;
@@ -188,6 +200,11 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.gateway->setup(mgr);
     if (!I.gateway->start(I.f.gateway_addr, static_cast<int>(I.f.gateway_port), err)) return false;
     I.stoppers.push_back([&I] { I.gateway->stop(); });
+  }
+  if (I.webhooks) {
+    // started last: every plugin route is registered before the first request
+    if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
+    I.stoppers.push_back([&I] { I.webhooks->stop(); });
   }
   return true;
 }

@@ -79,24 +79,48 @@ def test_dry_run_does_not_persist(c):
     assert not c.exists("v1", "ConfigMap", "cm-dry", "t-api")
 
 
-def test_generation_and_status_subresource(c):
-    nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook", "metadata": {"name": "gen", "namespace": "t-api",
-                                                                             "annotations": {"kubeflow-resource-stopped": "x"}},
-          "spec": {"template": {"spec": {"containers": [{"name": "gen", "image": "jupyter:1"}]}}}}
-    o = c.create(nb)
+WIDGET_CRD = {
+    "apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
+    "metadata": {"name": "widgets.example.com"},
+    "spec": {"group": "example.com", "scope": "Namespaced",
+             "names": {"kind": "Widget", "plural": "widgets", "singular": "widget", "listKind": "WidgetList"},
+             "versions": [{"name": "v1", "served": True, "storage": True, "subresources": {"status": {}},
+                           "schema": {"openAPIV3Schema": {"type": "object", "properties": {
+                               "spec": {"type": "object", "required": ["size"],
+                                        "properties": {"size": {"type": "integer", "minimum": 1}}},
+                               "status": {"type": "object", "properties": {"ready": {"type": "boolean"}}}}}}}]}}
+
+
+def test_dynamic_crd_generation_and_status_subresource(c):
+    c.create(WIDGET_CRD)
+    w = {"apiVersion": "example.com/v1", "kind": "Widget", "metadata": {"name": "w1", "namespace": "t-api"}, "spec": {"size": 1}}
+    deadline = time.time() + 5
+    while True:  # the new resource is served as soon as the CRD is established
+        try:
+            o = c.create(w)
+            break
+        except ApiException as e:
+            if e.status != 404 or time.time() > deadline:
+                raise
+            time.sleep(0.05)
     assert o["metadata"]["generation"] == 1
     o["metadata"]["labels"] = {"x": "y"}
     o = c.update(o)
     assert o["metadata"]["generation"] == 1  # metadata-only change
-    o["spec"]["template"]["spec"]["containers"][0]["image"] = "jupyter:2"
+    o["spec"]["size"] = 2
     o = c.update(o)
     assert o["metadata"]["generation"] == 2
     # spec changes through /status are ignored, status changes through the main resource too
-    o["status"] = {"readyReplicas": 7, "conditions": [], "containerState": {}}
-    o["spec"]["template"]["spec"]["containers"][0]["image"] = "jupyter:3"
+    o["status"] = {"ready": True}
+    o["spec"]["size"] = 3
     s = c.update_status(o)
-    assert s["status"]["readyReplicas"] == 7
-    assert s["spec"]["template"]["spec"]["containers"][0]["image"] == "jupyter:2"
+    assert s["status"]["ready"] is True and s["spec"]["size"] == 2
+    s["status"] = {"ready": False}
+    s = c.update(s)
+    assert s["status"]["ready"] is True
+    with pytest.raises(ApiException) as e:
+        c.create({**w, "metadata": {"name": "w2", "namespace": "t-api"}, "spec": {"size": 0}})
+    assert e.value.status == 422
 
 
 def test_crd_schema_validation_and_versions(c):
