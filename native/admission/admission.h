@@ -79,6 +79,9 @@ class AdmissionWebhookServer {
   bool start(const std::string& addr, int port, std::string* err);
   void stop();
   int port() const { return srv_ ? srv_->port() : 0; }
+  // Mutating + ValidatingWebhookConfiguration objects pointing at base_url (self-registration of
+  // the split binaries; the reference ships them as manifests).
+  std::vector<Json> webhook_configurations(const std::string& base_url, const std::string& name) const;
   // Processes one AdmissionReview (exposed for tests).
   Json review(const std::string& path, const Json& admission_review);
 

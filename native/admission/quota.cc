@@ -180,6 +180,39 @@ Json AdmissionWebhookServer::review(const std::string& path, const Json& ar) {
   return Json{{"apiVersion", "admission.k8s.io/v1"}, {"kind", "AdmissionReview"}, {"response", resp}};
 }
 
+std::vector<Json> AdmissionWebhookServer::webhook_configurations(const std::string& base_url, const std::string& name) const {
+  Json mut = Json::array(), val = Json::array();
+  for (const auto& kv : routes_) {
+    const auto& res = kv.second.res;
+    if (!res) continue;
+    Json versions = Json::array();
+    for (const auto& v : res->versions) versions.push_back(v);
+    std::string hook = kv.first.substr(1);
+    for (auto& ch : hook)
+      if (ch == '/') ch = '-';
+    Json wh{{"name", hook + "." + name + ".kfamd.io"},
+            {"clientConfig", Json{{"url", base_url + kv.first}}},
+            {"rules", Json::array({Json{{"apiGroups", Json::array({res->group})},
+                                        {"apiVersions", versions},
+                                        {"operations", Json::array({"CREATE", "UPDATE"})},
+                                        {"resources", Json::array({res->plural})}}})},
+            {"failurePolicy", "Fail"},
+            {"sideEffects", "None"},
+            {"admissionReviewVersions", Json::array({"v1"})}};
+    if (res->kind == "Pod" && kv.first == "/apply-poddefault")
+      wh["namespaceSelector"] = Json{{"matchLabels", Json{{"app.kubernetes.io/part-of", "kubeflow-profile"}}}};
+    (kv.second.mutating ? mut : val).push_back(wh);
+  }
+  std::vector<Json> out;
+  if (!mut.empty())
+    out.push_back(Json{{"apiVersion", "admissionregistration.k8s.io/v1"}, {"kind", "MutatingWebhookConfiguration"},
+                       {"metadata", Json{{"name", name}}}, {"webhooks", mut}});
+  if (!val.empty())
+    out.push_back(Json{{"apiVersion", "admissionregistration.k8s.io/v1"}, {"kind", "ValidatingWebhookConfiguration"},
+                       {"metadata", Json{{"name", name}}}, {"webhooks", val}});
+  return out;
+}
+
 bool AdmissionWebhookServer::start(const std::string& addr, int port, std::string* err) {
   srv_ = std::make_unique<HttpServer>();
   if (!srv_->listen(addr, port, err)) return false;

@@ -318,4 +318,13 @@ std::vector<Json> builtin_crds() {
   return out;
 }
 
+const ResourceRegistry& builtin_registry() {
+  static ResourceRegistry* r = [] {
+    auto* reg = new ResourceRegistry();
+    for (const auto& crd : builtin_crds()) reg->add_crd(crd);
+    return reg;
+  }();
+  return *r;
+}
+
 }  // namespace kf

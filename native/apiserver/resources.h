@@ -61,6 +61,9 @@ class ResourceRegistry {
 // Built-in CRD objects of this framework (Notebook v1/v1beta1/v1alpha1, Profile v1/v1beta1,
 // Tensorboard, PVCViewer, PodDefault) and the third-party kinds (Istio, OpenShift, app.k8s.io).
 std::vector<Json> builtin_crds();
+// Process-wide registry of the built-in kinds + built-in CRDs (for components that need
+// ResourceInfo without an embedded API server, e.g. webhook self-registration).
+const ResourceRegistry& builtin_registry();
 
 // Minimal structural OpenAPI v3 validation (type, required, properties, items, minItems,
 // maxItems, enum, minimum, maximum, pattern-free). Returns error strings (empty = valid).

@@ -90,6 +90,8 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.profile = std::make_unique<ProfileReconciler>(I.c, po, make_configmap_cloud_iam(I.c));
     I.profile->setup(mgr);
   }
+  // HTTP admission server (split binaries); each component below adds its own routes
+  if (I.f.webhook_port >= 0 && !I.api) I.webhooks = std::make_unique<AdmissionWebhookServer>();
   if (enabled.count("webhooks")) {
     auto pd = make_poddefault_plugin(I.c);
     auto gpu = make_gpu_readiness_plugin();
@@ -100,17 +102,11 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       I.api->add_mutating_plugin("gpu-readiness.kfamd.io", gpu);
       I.api->add_validating_plugin("ResourceQuota", quota);
     }
-    if (I.f.webhook_port >= 0) {
-      I.webhooks = std::make_unique<AdmissionWebhookServer>();
-      ResourceRegistry reg;
-      auto pods = reg.by_kind("v1", "Pod");
+    if (I.webhooks) {
+      auto pods = builtin_registry().by_kind("v1", "Pod");
       I.webhooks->add("/apply-poddefault", pd, true, pods);
       I.webhooks->add("/gpu-readiness", gpu, true, pods);
       I.webhooks->add("/quota", quota, false, pods);
-      auto viewers = reg.by_kind("kubeflow.org/v1alpha1", "PVCViewer");
-      I.webhooks->add("/mutate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_defaulter(), true, viewers);
-      I.webhooks->add("/validate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_validator(), false, viewers);
-
     }
     I.quota = std::make_unique<QuotaController>(I.c);
     I.quota->setup(mgr);
@@ -132,6 +128,11 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       I.api->add_mutating_plugin("mpvcviewer.kb.io", make_pvcviewer_defaulter());
       I.api->add_validating_plugin("vpvcviewer.kb.io", make_pvcviewer_validator());
     }
+    if (I.webhooks) {
+      auto viewers = builtin_registry().by_kind("kubeflow.org/v1alpha1", "PVCViewer");
+      I.webhooks->add("/mutate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_defaulter(), true, viewers);
+      I.webhooks->add("/validate-kubeflow-org-v1alpha1-pvcviewer", make_pvcviewer_validator(), false, viewers);
+    }
   }
   if (enabled.count("odh")) {
     OdhOptions oo;
@@ -142,7 +143,7 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.odh->setup(mgr, workers);
     auto hook = make_odh_notebook_webhook(I.c, oo);
     if (I.api) I.api->add_mutating_plugin("notebooks.opendatahub.io", hook);
-    if (I.webhooks) I.webhooks->add("/mutate-notebook-v1", hook, true, ResourceRegistry().by_kind("kubeflow.org/v1", "Notebook"));
+    if (I.webhooks) I.webhooks->add("/mutate-notebook-v1", hook, true, builtin_registry().by_kind("kubeflow.org/v1", "Notebook"));
   }
   if (enabled.count("kfam") || I.f.kfam_port >= 0) {
     KfamOptions ko;
@@ -205,6 +206,25 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     // started last: every plugin route is registered before the first request
     if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
     I.stoppers.push_back([&I] { I.webhooks->stop(); });
+    if (!I.api) {
+      // split mode: register our hooks with the remote API server (the manifests' job upstream)
+      const std::string base = "http://127.0.0.1:" + std::to_string(I.webhooks->port());
+      std::string cfg_name = "kfamd";
+      for (const auto& c : enabled) cfg_name += "-" + c;
+      for (auto cfg : I.webhooks->webhook_configurations(base, cfg_name)) {
+        Json live;
+        ApiError e = I.c->get(cfg["apiVersion"].as_string(), cfg["kind"].as_string(), "", cfg_name, live);
+        if (e.code == 404) e = I.c->create(cfg);
+        else if (!e) {
+          live["webhooks"] = cfg["webhooks"];
+          e = I.c->update(live);
+        }
+        if (e) {
+          *err = "registering webhooks: " + e.message;
+          return false;
+        }
+      }
+    }
   }
   return true;
 }

@@ -352,3 +352,40 @@ std::string label(const Json& obj, const std::string& key, const std::string& de
 }
 
 }  // namespace kf
+
+namespace kf {
+// Cluster-DNS equivalent for processes that talk to a remote API server (split binaries):
+// <svc>.<ns>[.svc[.<domain>]] -> a Ready pod of the service's selector + resolved targetPort.
+bool resolve_service_via(Client& c, const std::string& host, int port, std::string& ip, int& out_port) {
+  auto parts = split(host, '.');
+  if (parts.size() < 2 || (parts.size() > 2 && parts[2] != "svc") || host == "localhost" || starts_with(host, "127.")) return false;
+  Json s;
+  if (c.get("v1", "Service", parts[1], parts[0], s)) return false;
+  Json target;
+  for (const auto& p : s.at_path({"spec", "ports"}).as_array())
+    if (p["port"].as_int() == port || s.at_path({"spec", "ports"}).size() == 1) target = p["targetPort"];
+  if (target.is_null()) target = port;
+  if (s.at_path({"spec", "selector"}).empty()) return false;
+  LabelSelector sel = LabelSelector::from_json(Json{{"matchLabels", s.at_path({"spec", "selector"})}}, true);
+  Json pods;
+  if (c.list("v1", "Pod", parts[1], ListOptions(), pods)) return false;
+  for (const auto& p : pods["items"].as_array()) {
+    if (!sel.matches(p.at_path({"metadata", "labels"})) || p.at_path({"metadata", "deletionTimestamp"}).is_string()) continue;
+    const std::string pip = p.at_path({"status", "podIP"}).as_string();
+    bool ready = false;
+    for (const auto& cond : p.at_path({"status", "conditions"}).as_array())
+      ready = ready || (cond["type"].as_string() == "Ready" && cond["status"].as_string() == "True");
+    if (pip.empty() || !ready) continue;
+    int tp = target.is_number() ? static_cast<int>(target.as_int()) : 0;
+    if (!target.is_number())
+      for (const auto& ct : p.at_path({"spec", "containers"}).as_array())
+        for (const auto& cp : ct["ports"].as_array())
+          if (cp["name"].as_string() == target.as_string()) tp = static_cast<int>(cp["containerPort"].as_int());
+    if (tp == 0) continue;
+    ip = pip;
+    out_port = tp;
+    return true;
+  }
+  return false;
+}
+}  // namespace kf

@@ -65,6 +65,8 @@ class Client {
                              const std::string& name, const std::function<bool(Json&)>& mutate, bool status = false);
 };
 
+bool resolve_service_via(Client& c, const std::string& host, int port, std::string& ip, int& out_port);
+
 class LocalClient : public Client {
  public:
   explicit LocalClient(ApiServer* s, UserInfo user = UserInfo()) : s_(s), user_(std::move(user)) {}

@@ -1,0 +1,121 @@
+"""Split deployment: every component as its own process against one API server over REST.
+
+kflite runs only the API server and the node stack (--controllers builtin,scheduler,kubelet,gateway);
+notebook-controller, profile-controller, admission-webhook, odh-notebook-controller,
+pvcviewer-controller, tensorboard-controller and access-management connect with --server and
+self-register their admission webhooks (Mutating/ValidatingWebhookConfiguration -> HTTP), which
+exercises the RestClient, remote informers/watches and the API server's webhook dispatch.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import time
+import urllib.request
+
+import pytest
+
+from kubeflow_rm_amd.cluster import BIN, LocalCluster
+
+NB = "kubeflow.org/v1"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def split():
+    from tests.conftest import _ensure_native
+    _ensure_native()
+    cl = LocalCluster(controllers="builtin,scheduler,kubelet,gateway", env={"USE_ISTIO": "true"})
+    cl.start()
+    kfam_port = _free_port()
+    procs = []
+    logs = {}
+    env = dict(os.environ, USE_ISTIO="true", ENABLE_CULLING="false")
+    common = ["--server", cl.url, "--metrics-addr", "0", "--probe-addr", "0", "--token-file", "/nonexistent"]
+    for name, extra in [("notebook-controller", []), ("profile-controller", []), ("admission-webhook", ["--webhook-port", "0"]),
+                        ("odh-notebook-controller", ["--webhook-port", "0"]), ("pvcviewer-controller", ["--webhook-port", "0"]),
+                        ("tensorboard-controller", []), ("access-management", ["--kfam-port", str(kfam_port)])]:
+        log = open(os.path.join(cl.data_dir, name + ".log"), "wb")
+        logs[name] = log
+        procs.append(subprocess.Popen([str(BIN / name), *common, *extra], stdout=log, stderr=subprocess.STDOUT, env=env,
+                                      start_new_session=True))
+    # webhooks registered = components up
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        n = len(cl.client.list("admissionregistration.k8s.io/v1", "MutatingWebhookConfiguration")["items"])
+        if n >= 3:
+            break
+        time.sleep(0.1)
+    yield cl, f"http://127.0.0.1:{kfam_port}"
+    for p in procs:
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+    for p in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+    for f in logs.values():
+        f.close()
+    cl.stop()
+
+
+def test_webhooks_self_registered(split):
+    cl, _ = split
+    mut = cl.client.list("admissionregistration.k8s.io/v1", "MutatingWebhookConfiguration")["items"]
+    paths = {w["clientConfig"]["url"].rsplit("/", 1)[-1] for m in mut for w in m["webhooks"]}
+    assert {"apply-poddefault", "gpu-readiness", "mutate-notebook-v1", "mutate-kubeflow-org-v1alpha1-pvcviewer"} <= paths
+
+
+def test_profile_notebook_poddefault_over_rest(split):
+    cl, _ = split
+    c = cl.client
+    c.create({"apiVersion": "kubeflow.org/v1", "kind": "Profile", "metadata": {"name": "remote"},
+              "spec": {"owner": {"kind": "User", "name": "r@example.com"}}})
+    c.wait_for("rbac.authorization.k8s.io/v1", "RoleBinding", "namespaceAdmin", "remote", lambda o: True, timeout=15)
+    c.create({"apiVersion": "kubeflow.org/v1alpha1", "kind": "PodDefault", "metadata": {"name": "pd", "namespace": "remote"},
+              "spec": {"selector": {"matchLabels": {"pd": "on"}}, "desc": "d", "env": [{"name": "REMOTE", "value": "1"}]}})
+    nb = c.create({"apiVersion": NB, "kind": "Notebook", "metadata": {"name": "nb", "namespace": "remote", "labels": {"pd": "on"}},
+                   "spec": {"template": {"spec": {"containers": [{"name": "nb", "image": "jupyter:1",
+                                                                   "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}})
+    # the ODH webhook (HTTP) ran on CREATE
+    assert nb["metadata"]["annotations"]["kubeflow-resource-stopped"] == "odh-notebook-controller-lock"
+    c.wait_for(NB, "Notebook", "nb", "remote", lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=40)
+    pod = c.get("v1", "Pod", "nb-0", "remote")
+    assert {"name": "REMOTE", "value": "1"} in pod["spec"]["containers"][0]["env"]
+    assert pod["spec"]["initContainers"][0]["name"] == "gpu-readiness"
+    assert c.exists("route.openshift.io/v1", "Route", "nb", "remote")
+    with urllib.request.urlopen(cl.gateway + "/notebook/remote/nb/api/status", timeout=5) as r:
+        assert r.status == 200
+
+
+def test_pvcviewer_webhook_over_rest(split):
+    cl, _ = split
+    from kubeflow_rm_amd.client import ApiException
+    with pytest.raises(ApiException) as e:
+        cl.client.create({"apiVersion": "kubeflow.org/v1alpha1", "kind": "PVCViewer", "metadata": {"name": "v", "namespace": "remote"},
+                          "spec": {"pvc": "", "rwoScheduling": False}})
+    assert "PVC name must be specified" in str(e.value.body)
+
+
+def test_kfam_over_rest(split):
+    cl, kfam = split
+    deadline = time.time() + 10
+    while True:
+        try:
+            with urllib.request.urlopen(kfam + "/kfam/v1/bindings?namespace=remote", timeout=5) as r:
+                body = json.loads(r.read())
+            break
+        except OSError:
+            if time.time() > deadline:
+                raise
+            time.sleep(0.1)
+    assert [b["user"]["name"] for b in body["bindings"]] == ["r@example.com"]
