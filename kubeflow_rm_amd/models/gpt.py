@@ -1,0 +1,152 @@
+"""GPT-style decoder LM built on the framework's gfx950 ops — the in-notebook workload.
+
+Used by the multi-GPU notebook smoke (BASELINE config 4: DP/TP over RCCL inside a pod), the
+examples and ``smoke()``. Every projection runs on the hand-written MFMA GEMM with its fused
+epilogue (bias + GELU for the MLP up-projection; residual for the down-projection), LayerNorm
+on the wave-per-row kernel, attention on ``scaled_dot_product_attention`` (ROCm flash path).
+With a tensor-parallel group the attention heads and the MLP are split Megatron-style
+(QKV / fc1 column-parallel, out-proj / fc2 row-parallel: one all-reduce per sub-block).
+
+On CPU tensors the same module runs torch's reference ops (used by the gloo tests).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from kubeflow_rm_amd.parallel import tp as tpl
+
+
+@dataclass
+class GPTConfig:
+    vocab_size: int = 32000
+    d_model: int = 1024
+    n_layers: int = 12
+    n_heads: int = 16
+    d_ff: int = 4096
+    max_seq: int = 2048
+    dropout: float = 0.0
+    dtype: torch.dtype = torch.bfloat16
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_heads
+
+
+CONFIGS = {
+    "gpt-tiny": GPTConfig(vocab_size=512, d_model=256, n_layers=2, n_heads=4, d_ff=1024, max_seq=256),
+    "gpt-small": GPTConfig(vocab_size=32000, d_model=768, n_layers=12, n_heads=12, d_ff=3072, max_seq=2048),
+    "gpt-1b": GPTConfig(vocab_size=32000, d_model=2048, n_layers=24, n_heads=16, d_ff=8192, max_seq=4096),
+}
+
+
+def _layer_norm(x, w, b, eps=1e-5):
+    if x.is_cuda:
+        from kubeflow_rm_amd import ops
+        return ops.layer_norm(x, w, b, eps)
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+class LayerNorm(torch.nn.Module):
+    def __init__(self, d, dtype, device=None):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.ones(d, dtype=dtype, device=device))
+        self.bias = torch.nn.Parameter(torch.zeros(d, dtype=dtype, device=device))
+
+    def forward(self, x):
+        return _layer_norm(x, self.weight, self.bias)
+
+
+def _qkv_shard(cfg: GPTConfig, tp: int, rank: int, seed: int, device) -> torch.Tensor:
+    full = tpl.full_weight((3 * cfg.d_model, cfg.d_model), seed)
+    hl, hd = cfg.n_heads // tp, cfg.head_dim
+    rows = []
+    for part in range(3):  # q, k, v
+        base = part * cfg.d_model + rank * hl * hd
+        rows.append(full[base:base + hl * hd])
+    return torch.cat(rows, 0).to(dtype=cfg.dtype, device=device)
+
+
+class Block(torch.nn.Module):
+    def __init__(self, cfg: GPTConfig, layer: int, tp_group=None, device=None):
+        super().__init__()
+        tp = tpl._world(tp_group)
+        if cfg.n_heads % tp:
+            raise ValueError(f"n_heads={cfg.n_heads} not divisible by tp={tp}")
+        self.cfg, self.tp_group = cfg, tp_group
+        self.local_heads = cfg.n_heads // tp
+        seed = 1000 * (layer + 1)
+        self.ln1 = LayerNorm(cfg.d_model, cfg.dtype, device)
+        # fused QKV, column-parallel: each rank owns local_heads of q, k and v
+        self.qkv = tpl.ColumnParallelLinear(cfg.d_model, 3 * cfg.d_model, group=tp_group, dtype=cfg.dtype, device=device,
+                                            seed=seed + 1)
+        if tp > 1:
+            # the canonical full QKV weight is [q_all; k_all; v_all]; this rank's column shard must
+            # hold q, k and v rows of *its* heads so the sharded model equals the unsharded one
+            with torch.no_grad():
+                self.qkv.weight.copy_(_qkv_shard(cfg, tp, tpl._rank(tp_group), seed + 1, device))
+        self.proj = tpl.RowParallelLinear(cfg.d_model, cfg.d_model, group=tp_group, dtype=cfg.dtype, device=device, seed=seed + 2)
+        self.ln2 = LayerNorm(cfg.d_model, cfg.dtype, device)
+        self.fc1 = tpl.ColumnParallelLinear(cfg.d_model, cfg.d_ff, act="gelu_tanh", group=tp_group, dtype=cfg.dtype,
+                                            device=device, seed=seed + 3)
+        self.fc2 = tpl.RowParallelLinear(cfg.d_ff, cfg.d_model, group=tp_group, dtype=cfg.dtype, device=device, seed=seed + 4)
+
+    def attention(self, x):
+        B, T, _ = x.shape
+        h, hd = self.local_heads, self.cfg.head_dim
+        qkv = self.qkv(x)  # [B, T, 3 * h * hd] — the column shard is [q_h | k_h | v_h] per rank
+        q, k, v = qkv.view(B, T, 3, h, hd).permute(2, 0, 3, 1, 4)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return self.proj(y.transpose(1, 2).reshape(B, T, h * hd))
+
+    def forward(self, x):
+        x = x + self.attention(self.ln1(x))
+        return x + self.fc2(self.fc1(self.ln2(x)))
+
+
+class GPT(torch.nn.Module):
+    def __init__(self, cfg: GPTConfig, tp_group=None, device=None):
+        super().__init__()
+        self.cfg = cfg
+        g = torch.Generator(device="cpu").manual_seed(7)
+        emb = torch.randn(cfg.vocab_size, cfg.d_model, generator=g) * 0.02
+        pos = torch.randn(cfg.max_seq, cfg.d_model, generator=g) * 0.01
+        self.tok = torch.nn.Parameter(emb.to(dtype=cfg.dtype, device=device))
+        self.pos = torch.nn.Parameter(pos.to(dtype=cfg.dtype, device=device))
+        self.blocks = torch.nn.ModuleList([Block(cfg, i, tp_group, device) for i in range(cfg.n_layers)])
+        self.ln_f = LayerNorm(cfg.d_model, cfg.dtype, device)
+
+    def forward(self, idx, targets=None):
+        B, T = idx.shape
+        x = F.embedding(idx, self.tok) + self.pos[:T]
+        for blk in self.blocks:
+            x = blk(x)
+        x = self.ln_f(x)
+        logits = tpl._linear(x, self.tok)  # tied output head [B, T, vocab]
+        if targets is None:
+            return logits
+        loss = F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
+        return logits, loss
+
+    def flops_per_token(self, seq: int) -> float:
+        """Training FLOPs/token (fwd+bwd = 3x fwd): dense matmuls + attention scores."""
+        c = self.cfg
+        dense = 2 * (4 * c.d_model * c.d_model + 2 * c.d_model * c.d_ff) * c.n_layers + 2 * c.d_model * c.vocab_size
+        attn = 2 * 2 * seq * c.d_model * c.n_layers
+        return 3.0 * (dense + attn)
+
+
+def build(name_or_cfg, tp_group=None, device=None) -> GPT:
+    cfg = CONFIGS[name_or_cfg] if isinstance(name_or_cfg, str) else name_or_cfg
+    return GPT(cfg, tp_group=tp_group, device=device)
+
+
+def num_params(model: torch.nn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())
+
+
+def init_scale(d: int) -> float:
+    return 1.0 / math.sqrt(d)

@@ -1,0 +1,97 @@
+"""Process-group bring-up for multi-GPU notebooks (one process per GPU, RCCL over xGMI).
+
+The notebook pod spec carries the wiring (injected by the kubelet's device plugin allocation,
+native/gpu/topology.cc gpu_env_for): HIP_VISIBLE_DEVICES (pod-local ordinals 0..n-1),
+KFAMD_XGMI_RING (ring order over direct xGMI links), WORLD_SIZE / LOCAL_WORLD_SIZE,
+MASTER_ADDR=127.0.0.1, MASTER_PORT, NCCL_IB_DISABLE=1, NCCL_P2P_LEVEL=SYS,
+HSA_ENABLE_IPC_MODE_LEGACY=0. ``torchrun`` (or this module's ``spawn``) supplies RANK/LOCAL_RANK.
+
+``init()`` maps LOCAL_RANK to the device at position LOCAL_RANK of the xGMI ring, so that ring
+neighbours in RCCL's rank order are physically adjacent on the fabric (each hop is one direct
+xGMI link; on a fully-connected 8x MI355X node every order is a ring, but on partial fabrics or
+GPU subsets this keeps the collective on direct links).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "gloo"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+_ENV: DistEnv | None = None
+
+
+def xgmi_ring() -> list[int]:
+    ring = os.environ.get("KFAMD_XGMI_RING", "")
+    try:
+        return [int(x) for x in ring.split(",") if x != ""]
+    except ValueError:
+        return []
+
+
+def device_for_local_rank(local_rank: int) -> int:
+    ring = xgmi_ring()
+    if ring and local_rank < len(ring):
+        return ring[local_rank]
+    return local_rank
+
+
+def init(backend: str | None = None, timeout_s: float = 600.0) -> DistEnv:
+    """Initialise torch.distributed from the env (idempotent). backend: nccl (=RCCL on ROCm) when
+    GPUs are visible, else gloo."""
+    global _ENV
+    if _ENV is not None:
+        return _ENV
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    device = torch.device("cpu")
+    if use_gpu:
+        dev = device_for_local_rank(local_rank) % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        device = torch.device("cuda", dev)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=_dt.timedelta(seconds=timeout_s), **kw)
+    _ENV = DistEnv(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend)
+    return _ENV
+
+
+def env() -> DistEnv:
+    return _ENV if _ENV is not None else DistEnv()
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if env().backend == "nccl":
+            dist.barrier(device_ids=[env().device.index])
+        else:
+            dist.barrier()
+
+
+def shutdown() -> None:
+    global _ENV
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _ENV = None
