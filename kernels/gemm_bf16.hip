@@ -543,6 +543,11 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 }  // namespace
 
+extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
+                                            int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
+                                            long long ldr, long long sa, long long sb, long long sc, long long sr,
+                                            float alpha, int act, void* stream);
+
 extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* C,
                                           const void* bias, const void* R, int M, int N, int K,
                                           int batch, long long lda, long long ldb, long long ldc,
@@ -577,6 +582,10 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   __bf16* c = static_cast<__bf16*>(C);
   const __bf16* bs = static_cast<const __bf16*>(bias);
   const __bf16* r = static_cast<const __bf16*>(R);
+  if (fast && variant == 6) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
+    return kfamd_gemm_nt_bf16_w4_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
+                                        stride_c, stride_r, alpha, act, stream);
+  }
   if (fast) {
     dim3 grid((M / kBM) * (N / kBN), batch), block(kThreads);
     if (variant == 0 || variant == 4) {  // default fast path: pipelined + pinned interleave
