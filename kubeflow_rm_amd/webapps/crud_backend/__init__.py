@@ -1,0 +1,126 @@
+"""Shared backend of the CRUD web apps (reference components/crud-web-apps/common/backend).
+
+``create_app(name, static_dir, cfg)`` returns a Flask app with: authentication (user header)
+and CSRF checks before every request, JSON error envelopes, liveness/readiness probes, generic
+routes (/info, /api/namespaces, /api/storageclasses[/default]) and SPA serving (index.html with
+its <base href> set to APP_PREFIX, CSRF cookie refreshed, no-cache).
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+from flask import Flask, Response, jsonify, request
+from werkzeug import exceptions
+
+from kubeflow_rm_amd.client import ApiException
+
+from . import api, authn, config, csrf, helpers, settings
+
+LOG_FORMAT = "%(asctime)s | %(name)s | %(levelname)s | %(message)s"
+log = logging.getLogger(__name__)
+
+
+def _register_errors(app: Flask) -> None:
+    @app.errorhandler(ApiException)
+    def api_exception(e: ApiException):
+        log.error("Kubernetes API error on %s: %s", request.url, e)
+        msg = "The requested resource could not be found in the API Server" if e.status == 404 else (e.message or str(e))
+        return api.failed_response(msg, e.status)
+
+    @app.errorhandler(exceptions.HTTPException)
+    def http_error(e):
+        return api.failed_response(e.description, e.code)
+
+    @app.errorhandler(Exception)
+    def catch_all(e):
+        log.exception(e)
+        return api.failed_response("An error occured in the backend.", 500)
+
+
+def _register_base_routes(app: Flask) -> None:
+    @app.route("/healthz/liveness")
+    @authn.no_authentication
+    def liveness():
+        return jsonify("alive"), 200
+
+    @app.route("/healthz/readiness")
+    @authn.no_authentication
+    def readiness():
+        return jsonify("ready"), 200
+
+    @app.route("/info")
+    def info():
+        return api.success_response("info", {})
+
+    @app.route("/api/namespaces")
+    def namespaces():
+        return api.success_response("namespaces", [ns["metadata"]["name"] for ns in api.list_namespaces()["items"]])
+
+    @app.route("/api/storageclasses")
+    def storageclasses():
+        return api.success_response("storageClasses", [sc["metadata"]["name"] for sc in api.list_storageclasses()["items"]])
+
+    @app.route("/api/storageclasses/default")
+    def default_storageclass():
+        keys = ("storageclass.kubernetes.io/is-default-class", "storageclass.beta.kubernetes.io/is-default-class")
+        for sc in api.list_storageclasses()["items"]:
+            ann = sc["metadata"].get("annotations") or {}
+            if any(ann.get(k, "false") == "true" for k in keys):
+                return api.success_response("defaultStorageClass", sc["metadata"]["name"])
+        return api.success_response("defaultStorageClass", "")
+
+
+COMMON_STATIC = os.path.join(os.path.abspath(os.path.dirname(__file__)), "static")
+
+
+def _register_serving(app: Flask) -> None:
+    from flask import send_from_directory
+
+    @app.route("/common/<path:fname>")
+    @authn.no_authentication
+    def common_static(fname):
+        return send_from_directory(COMMON_STATIC, fname)
+
+    def serve_index(path="/"):
+        resp = Response(helpers.get_prefixed_index_html(), mimetype="text/html",
+                        headers={"Cache-Control": csrf.NO_CACHE})
+        csrf.set_cookie(resp)
+        return resp
+
+    serve_index.no_authentication = False
+    app.add_url_rule("/", "serve_index", serve_index)
+    app.add_url_rule("/index.html", "serve_index_html", serve_index)
+    app.add_url_rule("/<path:path>", "serve_path", serve_index)
+
+
+def create_app(name: str, static_dir: str, cfg: config.Config | None = None) -> Flask:
+    cfg = cfg or config.Config()
+    settings.reload()
+    logging.basicConfig(format=LOG_FORMAT, level=cfg.LOG_LEVEL)
+    app = Flask(name, static_folder=os.path.join(static_dir, "assets") if static_dir else None,
+                static_url_path="/assets")
+    app.config.from_object(cfg)
+    app.config["PREFIX"] = cfg.PREFIX
+    app.config["STATIC_DIR"] = static_dir
+    if cfg.ENV == "development":
+        log.warning("RUNNING IN DEVELOPMENT MODE")
+    app.before_request(authn.check_authentication)
+    app.before_request(csrf.check_endpoint)
+    _register_errors(app)
+    _register_base_routes(app)
+    return app
+
+
+def finalize(app: Flask) -> Flask:
+    """Register the SPA catch-all last (after the app's own API routes)."""
+    _register_serving(app)
+    return app
+
+
+def serve(app: Flask, default_port: int = 5000) -> None:
+    """Serve with the stdlib-backed werkzeug server on POD_IP:port (threaded)."""
+    from werkzeug.serving import run_simple
+    port = int(os.environ.get("PORT") or (os.environ.get("KFAMD_CONTAINER_PORTS") or str(default_port)).split(",")[0])
+    host = os.environ.get("POD_IP", "0.0.0.0")
+    run_simple(host, port, app, threaded=True, use_reloader=False)
