@@ -135,3 +135,7 @@ def custom_api(verb, group, version, plural, kind, namespace, name=None, body=No
     if verb == "patch":
         return c.patch(av, kind, name, body, namespace, "merge")
     raise ValueError(verb)
+
+
+def list_pvc_events(namespace, pvc_name):
+    return list_events(namespace, events_field_selector("PersistentVolumeClaim", pvc_name))
