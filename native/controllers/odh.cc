@@ -496,6 +496,11 @@ Result OdhNotebookReconciler::reconcile(const Request& r, std::string* err) {
     *err = e.message;
     return {};
   }
+  // Conscious deviation: the reference reconciles a Notebook that is being deleted and so keeps
+  // re-creating its network policies / Route / OAuth objects while a foreground deletion waits for
+  // them (the GC deletes them again: deletion took 10-40 s on kube-lite). A terminating Notebook
+  // owns nothing new, as in the core notebook controller (notebook_controller.go:135-137).
+  if (nb.at_path({"metadata", "deletionTimestamp"}).is_string()) return {};
   auto owned = [&](Json obj) {
     set_controller_reference(nb, obj);
     return obj;
