@@ -138,7 +138,7 @@ def main() -> int:
                 "parallelism": f"dp{world}",
             },
             "per_gpu_tflops": round(per_gpu_tflops, 2),
-            "kernel": "kfamd gemm_nt_256p (MFMA 16x16x32 bf16, 256x256x64, glds double buffer, register-pipelined LDS reads, XCD remap)",
+            "kernel": "kfamd gemm_nt_256w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring, XCD remap)",
             "correct": bool(ok),
             "max_abs_err_vs_fp32": err,
             **extra,

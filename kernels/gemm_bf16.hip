@@ -3,7 +3,10 @@
 // SURVEY.md §2.7.2 K1 / §7.1 C. The reference has no GPU code at all; this kernel is
 // the in-pod readiness op and the notebook-facing matmul of the MI355X build.
 //
-// Fast path  (gemm_nt_256): 256x256 output tile per 512-thread workgroup (8 waves, 2(M) x 4(N)),
+// Default fast path: gemm_bf16_w4.hip (4 waves x 128x128, one wave per SIMD, asm MFMA with AGPR
+//   accumulators, buffer_load...lds into a 5-slot LDS ring). The 8-wave kernels below are the
+//   previous fast paths (variants pipe / pipe_sched) and the fallback for >= 2 GiB panels.
+// 8-wave path (gemm_nt_256): 256x256 output tile per 512-thread workgroup (8 waves, 2(M) x 4(N)),
 //   BK = 64, one workgroup per CU (128 KiB LDS: two stages of A+B), operands staged HBM -> LDS with
 //   global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip), XOR-swizzled LDS image (the swizzle is
 //   applied to the per-lane SOURCE address because the DMA destination is lane-linear), counted
@@ -548,6 +551,9 @@ extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* 
                                             long long ldr, long long sa, long long sb, long long sc, long long sr,
                                             float alpha, int act, void* stream);
 
+extern "C" int kfamd_gemm_nt_bf16_w4rg_launch(const void* A, const void* B, void* C, int M, int N, int K,
+                                              long long lda, long long ldb, long long ldc, int rg, void* stream);
+
 extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* C,
                                           const void* bias, const void* R, int M, int N, int K,
                                           int batch, long long lda, long long ldb, long long ldc,
@@ -582,13 +588,20 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   __bf16* c = static_cast<__bf16*>(C);
   const __bf16* bs = static_cast<const __bf16*>(bias);
   const __bf16* r = static_cast<const __bf16*>(R);
-  if (fast && variant == 6) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
+  if (fast && (variant == 7 || variant == 8)) {  // w4 read-gap experiments (plain GEMM only)
+    if (bias || R || act != KFAMD_ACT_NONE || batch != 1 || alpha != 1.0f) return KFAMD_EINVAL;
+    return kfamd_gemm_nt_bf16_w4rg_launch(A, B, C, M, N, K, lda, ldb, ldc, variant == 7 ? 3 : 4, stream);
+  }
+  // default fast path: the 4-wave w4 kernel (one wave per SIMD, 5-slot LDS ring; profiles/r1_gemm_w4c);
+  // the 8-wave pipe_sched kernel when a 256-row panel spans >= 2 GiB (w4's 32-bit buffer offsets)
+  const bool w4_ok = (long long)kBM * lda * 2 < (1LL << 31) && (long long)kBN * ldb * 2 < (1LL << 31);
+  if (fast && (variant == 6 || (variant == 0 && w4_ok))) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
     return kfamd_gemm_nt_bf16_w4_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
                                         stride_c, stride_r, alpha, act, stream);
   }
   if (fast) {
     dim3 grid((M / kBM) * (N / kBN), batch), block(kThreads);
-    if (variant == 0 || variant == 4) {  // default fast path: pipelined + pinned interleave
+    if (variant == 0 || variant == 4) {  // 8 waves: pipelined + pinned interleave
       KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 1, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
                          ldr, stride_a, stride_b, stride_c, stride_r, alpha);
     } else if (variant == 3) {

@@ -40,8 +40,8 @@ namespace {
 
 constexpr int kBM = 256, kBN = 256, kBK = 64, kThreads = 256;
 constexpr int kTileBytes = kBM * kBK * 2;    // 32 KiB per operand tile
-constexpr int kStageBytes = 2 * kTileBytes;  // A + B
-constexpr int kLdsBytes = 2 * kStageBytes;   // 128 KiB
+constexpr int kSlots = 5;                    // operand-tile slots (A or B each)
+constexpr int kLdsBytes = kSlots * kTileBytes;  // 160 KiB: all of the CU's LDS
 constexpr int kRsrcWord3 = 0x00020000;       // gfx9 raw buffer: 32-bit dword format, no swizzle
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -65,12 +65,12 @@ __device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& 
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
-template <int ACT, bool HAS_BIAS, bool HAS_RES>
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DIAG = false, int RG = 2, int ABL = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(1, 1)))
 void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                    const __bf16* __restrict__ bias, const __bf16* __restrict__ R, int M, int N, int K,
                    long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
-                   long long sc, long long sr, float alpha) {
+                   long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -93,8 +93,11 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   C += bz * sc;
   if (HAS_RES) R += bz * sr;
   // wave-uniform buffer resources over this block's 256-row panels (launcher checks < 2 GiB)
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, kRsrcWord3);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, kRsrcWord3);
+  // ABL (timing-only ablation builds, w4_diag): 1 = zero-record descriptors (every DMA dropped in
+  // the address unit, instruction stream kept), 2 = no K-loop ds_reads.
+  const int nrec = (DIAG && ABL == 1) ? 0 : 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, nrec, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, nrec, kRsrcWord3);
 
   // 32 one-KiB pieces (8 rows each) per operand tile, 8 per wave: piece p = wid*8 + j covers rows
   // 8p..8p+7; lane i lands at LDS p*1024 + 16*i (row 8p + (i>>3), swizzled chunk (i&7)) and must
@@ -109,11 +112,19 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
     vb[par] = (int)(((long long)lrow * ldb + chunk * 8) * 2);
   }
   const int rowstep_a = (int)(8 * lda * 2), rowstep_b = (int)(8 * ldb * 2);
-  auto stage_piece = [&](int kt, int buf, int j) {
-    char* base = smem + buf * kStageBytes + (wid * 8 + j) * 1024;
-    const int koff = kt * kBK * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(base), 16, va[j & 1], j * rowstep_a + koff, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(base + kTileBytes), 16, vb[j & 1], j * rowstep_b + koff, 0, 0);
+  // LDS = 5 slots of 32 KiB, each holding ONE operand tile (A_t or B_t). With 4 slots live
+  // (tile t being read, tile t+1 landing) the fifth lets A_{t+2} stream in during substep 0 of
+  // iteration t, B_{t+2} during substep 1 (into A_t's slot, free after the mid barrier); B_t's
+  // slot becomes the next free one. So the DMA is spread over the whole K-tile (1 per 8 MFMAs:
+  // concentrated DMA issue stalled the single MFMA wave per SIMD — w4_diag: +30..80 cycles per
+  // DMA) and A gets 3, B 2 substeps of lookahead instead of 1.5.
+  auto dma_a = [&](int kt, int slot, int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(smem + slot * kTileBytes + (wid * 8 + j) * 1024), 16,
+                                             va[j & 1], j * rowstep_a + kt * kBK * 2, 0, 0);
+  };
+  auto dma_b = [&](int kt, int slot, int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(smem + slot * kTileBytes + (wid * 8 + j) * 1024), 16,
+                                             vb[j & 1], j * rowstep_b + kt * kBK * 2, 0, 0);
   };
 
   const int lr = lane & 15, lh = lane >> 4;
@@ -121,7 +132,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int off0 = lr * 128 + (sw << 4);
   const int off1 = lr * 128 + ((sw ^ 4) << 4);
   const int a_base = (wm * 128) * 128;
-  const int b_base = kTileBytes + (wn * 128) * 128;
+  const int b_base = (wn * 128) * 128;
 
   f32x4 acc[8][8];
 #pragma unroll
@@ -131,17 +142,25 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
 
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   // fragment q of a set: q < 8 -> B fragment q, q >= 8 -> A fragment q-8
-  auto read_frag = [&](const char* sbuf, int off, bf16x8(&af)[8], bf16x8(&bf)[8], int q) {
-    if (q < 8) bf[q] = *reinterpret_cast<const bf16x8*>(sbuf + b_base + q * 2048 + off);
-    else af[q - 8] = *reinterpret_cast<const bf16x8*>(sbuf + a_base + (q - 8) * 2048 + off);
+  auto read_frag = [&](int sa_slot, int sb_slot, int off, bf16x8(&af)[8], bf16x8(&bf)[8], int q) {
+    if (q < 8) bf[q] = *reinterpret_cast<const bf16x8*>(smem + sb_slot * kTileBytes + b_base + q * 2048 + off);
+    else af[q - 8] = *reinterpret_cast<const bf16x8*>(smem + sa_slot * kTileBytes + a_base + (q - 8) * 2048 + off);
   };
 
   const int nk = K / kBK;
+  // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
+  int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) stage_piece(0, 0, j);
+  for (int j = 0; j < 8; ++j) {
+    dma_a(0, sa0, j);
+    dma_b(0, sb0, j);
+  }
   if (nk > 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) stage_piece(1, 1, j);
+    for (int j = 0; j < 8; ++j) {
+      dma_a(1, sa1, j);
+      dma_b(1, sb1, j);
+    }
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -150,61 +169,77 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   __builtin_amdgcn_s_barrier();
   COMPILER_FENCE();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) read_frag(smem, off0, a0, b0, q);
+  for (int q = 0; q < 16; ++q) read_frag(sa0, sb0, off0, a0, b0, q);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   PIN();
   __builtin_amdgcn_s_setprio(1);
 
-  // The reads (and DMA) of a substep go out in its FIRST half, 1 ds_read (+1 DMA) per 2 MFMAs, so
-  // the lgkmcnt(0) / vmcnt(0) at the substep's end finds them landed: with one wave per SIMD no
-  // other wave's MFMAs cover a read still in flight there (issuing them evenly over the substep
-  // left the last read ~4 MFMAs before its wait).
-  auto body = [&](int kt, auto do_stage, auto do_next) {
-    constexpr bool kStage = decltype(do_stage)::value;
-    constexpr bool kNext = decltype(do_next)::value;
-    const char* cur = smem + (kt & 1) * kStageBytes;
-    const char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
-    // substep 0: MFMAs on F0 while F1 (substep 1 of this tile) streams in
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      if (q < 16) read_frag(cur, off1, a1, b1, q);
+  // ds_reads of a substep go out 1 per RG MFMAs from its start (RG = 2: all in the first half, so
+  // the waits at its end find them landed); DMA 1 per 8 MFMAs across the substep.
+  // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
+  // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
+  unsigned long long seg[4] = {0, 0, 0, 0};
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (DIAG) {
       PIN();
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int idx = q * 2 + t, i = idx >> 3, n = idx & 7;
-        mfma(acc[i][n], b0[n], a0[i]);
-      }
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
       PIN();
     }
-    // tile kt+1 landed (vmcnt(0)) and F1 / this buffer fully read (lgkmcnt(0)), then one barrier
-    __builtin_amdgcn_s_waitcnt(0x0070);
+    return t;
+  };
+  auto body = [&](int kt, auto do_stage, auto do_next) {
+    constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
+    constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
+    const unsigned long long t0 = stamp();
+    // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
+#pragma unroll
+    for (int m = 0; m < 64; ++m) {
+      if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 16) read_frag(sa0, sb0, off1, a1, b1, m / RG);
+      if (kStage && (m & 7) == 2) dma_a(kt + 2, sf, m >> 3);
+      PIN();
+      mfma(acc[m >> 3][m & 7], b0[m & 7], a0[m >> 3]);
+      PIN();
+    }
+    const unsigned long long t1 = stamp();
+    // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
+    // after it tile kt's slots are free
+    if (kStage) {
+      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    }
     COMPILER_FENCE();
     __builtin_amdgcn_s_barrier();
     COMPILER_FENCE();
     PIN();
-    // substep 1: MFMAs on F1; beside them the DMA of tile kt+2 into the buffer just released and
-    // the reads of F0(kt+1)
+    const unsigned long long t2 = stamp();
+    // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
 #pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      if (kStage && q < 16) {
-        char* base = smem + (kt & 1) * kStageBytes + (wid * 8 + (q >> 1)) * 1024;
-        const int j = q >> 1, koff = (kt + 2) * kBK * 2;
-        if (q & 1)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(base + kTileBytes), 16, vb[j & 1], j * rowstep_b + koff, 0, 0);
-        else
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(base), 16, va[j & 1], j * rowstep_a + koff, 0, 0);
-      }
-      if (kNext && q < 16) read_frag(nxt, off0, a0, b0, q);
+    for (int m = 0; m < 64; ++m) {
+      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 16) read_frag(sa1, sb1, off0, a0, b0, m / RG);
+      if (kStage && (m & 7) == 2) dma_b(kt + 2, sa0, m >> 3);
       PIN();
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int idx = q * 2 + t, i = idx >> 3, n = idx & 7;
-        mfma(acc[i][n], b1[n], a1[i]);
-      }
+      mfma(acc[m >> 3][m & 7], b1[m & 7], a1[m >> 3]);
       PIN();
     }
+    const unsigned long long t3 = stamp();
     if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
     PIN();
+    // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
+    const int na = sf, nb = sa0;
+    sf = sb0;
+    sa0 = sa1;
+    sb0 = sb1;
+    sa1 = na;
+    sb1 = nb;
+    if (DIAG) {
+      const unsigned long long t4 = stamp();
+      seg[0] += t1 - t0;
+      seg[1] += t2 - t1;
+      seg[2] += t3 - t2;
+      seg[3] += t4 - t3;
+    }
   };
   using T = std::integral_constant<bool, true>;
   using F = std::integral_constant<bool, false>;
@@ -216,6 +251,10 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   }
   if (kt < nk) body(kt, F{}, F{});
   __builtin_amdgcn_s_setprio(0);
+  if (DIAG && lane == 0) {
+    unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 4;
+    for (int j = 0; j < 4; ++j) d[j] = seg[j];
+  }
   // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
@@ -292,6 +331,50 @@ extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* 
       return KFAMD_EINVAL;
   }
 #undef W4_LAUNCH
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+// Diagnostic launch (no epilogue variants): per-wave K-loop segment cycle sums into diag
+// [(M/256)*(N/256) blocks][4 waves][4 segments] (tools/kbench.py --diag-w4).
+extern "C" int kfamd_gemm_nt_bf16_w4_diag(const void* A, const void* B, void* C, int M, int N, int K,
+                                          unsigned long long* diag, int abl, void* stream) {
+  if (M % kBM || N % kBN || K % kBK || !diag) return KFAMD_EINVAL;
+  dim3 grid((M / kBM) * (N / kBN), 1), block(kThreads);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* a = static_cast<const __bf16*>(A);
+  const __bf16* b = static_cast<const __bf16*>(B);
+  __bf16* c = static_cast<__bf16*>(C);
+#define W4_DIAG(AB)                                                                                              \
+  hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, true, 2, AB>), grid, block, 0, s, a, b, c, nullptr, \
+                     nullptr, M, N, K, (long long)K, (long long)K, (long long)N, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, diag)
+  if (abl == 0) W4_DIAG(0);
+  else if (abl == 1) W4_DIAG(1);
+  else if (abl == 2) W4_DIAG(2);
+  else return KFAMD_EINVAL;
+#undef W4_DIAG
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+// Read-gap experiments (no epilogue): RG = 3 / 4 spreads a substep's 16 ds_reads over 48 / 64 MFMAs.
+extern "C" int kfamd_gemm_nt_bf16_w4rg_launch(const void* A, const void* B, void* C, int M, int N, int K,
+                                              long long lda, long long ldb, long long ldc, int rg, void* stream) {
+  if (M % kBM || N % kBN || K % kBK) return KFAMD_EINVAL;
+  if ((long long)kBM * lda * 2 >= (1LL << 31) || (long long)kBN * ldb * 2 >= (1LL << 31)) return KFAMD_EINVAL;
+  dim3 grid((M / kBM) * (N / kBN), 1), block(kThreads);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* a = static_cast<const __bf16*>(A);
+  const __bf16* b = static_cast<const __bf16*>(B);
+  __bf16* c = static_cast<__bf16*>(C);
+  if (rg == 3)
+    hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, false, 3>), grid, block, 0, s, a, b, c, nullptr,
+                       nullptr, M, N, K, lda, ldb, ldc, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, nullptr);
+  else if (rg == 4)
+    hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, false, 4>), grid, block, 0, s, a, b, c, nullptr,
+                       nullptr, M, N, K, lda, ldb, ldc, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, nullptr);
+  else
+    return KFAMD_EINVAL;
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }

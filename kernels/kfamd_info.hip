@@ -3,6 +3,6 @@
 #include "kfamd_kernels.h"
 
 extern "C" const char* kfamd_build_info(void) {
-  return "kfamd-kernels gfx950 (MFMA bf16 GEMM 256x256x64 glds, LayerNorm/RMSNorm wave-per-row) "
+  return "kfamd-kernels gfx950 (MFMA bf16 GEMM 256x256 w4: 4 waves, LDS-DMA 5-slot ring; LayerNorm/RMSNorm wave-per-row) "
          "built " __DATE__ " " __TIME__;
 }

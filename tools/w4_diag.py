@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""w4 GEMM K-loop stamps: shares of substep-0 issue (+F1 reads landing), DMA wait + barrier,
+substep-1 issue, final read wait — per wave, averaged over the grid (diagnostic build only;
+read shares, not the total). Also times the real kernel in the same process for reference."""
+import ctypes
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    import torch
+    from kubeflow_rm_amd import ops
+    from kubeflow_rm_amd.ops import _lib
+    L = _lib.lib()
+    f = L.kfamd_gemm_nt_bf16_w4_diag
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    for s in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096,8192,16384").split(",")]:
+        a = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
+        nblk = (s // 256) ** 2
+        diag = torch.zeros(nblk * 4 * 4, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        abl_cycles = {}
+        for abl in (1, 2, 0):
+            for _ in range(3):
+                rc = f(a.data_ptr(), b.data_ptr(), c.data_ptr(), s, s, s, diag.data_ptr(), abl, stream)
+                assert rc == 0, rc
+            torch.cuda.synchronize()
+            d = diag.view(nblk, 4, 4).double()
+            abl_cycles[abl] = round(d.sum(-1).mean().item() / (s // 64))
+        tot = d.sum(-1, keepdim=True)
+        share = (d / tot).mean(dim=(0, 1)).tolist()
+        cyc = d.mean(dim=(0, 1)).tolist()
+        # real kernel time, same process
+        for _ in range(3):
+            ops.gemm_nt(a, b, out=c, variant="w4")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 10
+        for _ in range(n):
+            ops.gemm_nt(a, b, out=c, variant="w4")
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        print(json.dumps({"size": s, "segments": ["substep0_issue+F1_land", "dma_wait+barrier", "substep1_issue",
+                                                   "F0_land"], "share": [round(x, 4) for x in share],
+                          "mean_cycles_per_wave": [round(x) for x in cyc], "w4_tflops": round(2 * s ** 3 / dt / 1e12, 1),
+                          "loop_cycles_per_ktile": round(sum(cyc) / (s // 64)),
+                          "ablation_loop_cycles_per_ktile": {"no_dma": abl_cycles[1], "no_ds_read": abl_cycles[2],
+                                                             "full": abl_cycles[0]}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
