@@ -76,6 +76,8 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
+  unsigned long long t_start = 0;
+  if (DIAG) t_start = __builtin_amdgcn_s_memtime();
 
   const int tiles_m = M / kBM, tiles_n = N / kBN, nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -179,6 +181,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
   // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
   unsigned long long seg[4] = {0, 0, 0, 0};
+  unsigned long long t_loop0 = 0, t_loop1 = 0;
   auto stamp = [&]() -> unsigned long long {
     unsigned long long t = 0;
     if (DIAG) {
@@ -243,6 +246,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   };
   using T = std::integral_constant<bool, true>;
   using F = std::integral_constant<bool, false>;
+  if (DIAG) t_loop0 = stamp();
   int kt = 0;
   for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
   if (kt + 1 < nk) {
@@ -251,10 +255,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   }
   if (kt < nk) body(kt, F{}, F{});
   __builtin_amdgcn_s_setprio(0);
-  if (DIAG && lane == 0) {
-    unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 4;
-    for (int j = 0; j < 4; ++j) d[j] = seg[j];
-  }
+  if (DIAG) t_loop1 = stamp();
   // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
@@ -285,6 +286,16 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
       *reinterpret_cast<bf16x4*>(C + (long long)m * ldc + col) = o;
+    }
+  }
+  if (DIAG) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 8;
+      for (int j = 0; j < 4; ++j) d[j] = seg[j];
+      d[4] = t_loop0 - t_start;  // prologue (address setup, first two tiles, F0(0))
+      d[5] = t_end - t_loop1;    // epilogue (stores issued)
+      d[6] = t_loop1 - t_loop0;  // K loop
     }
   }
 }

@@ -26,7 +26,7 @@ def main():
         b = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
         c = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
         nblk = (s // 256) ** 2
-        diag = torch.zeros(nblk * 4 * 4, dtype=torch.int64, device=dev)
+        diag = torch.zeros(nblk * 4 * 8, dtype=torch.int64, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
         abl_cycles = {}
         for abl in (1, 2, 0):
@@ -34,7 +34,8 @@ def main():
                 rc = f(a.data_ptr(), b.data_ptr(), c.data_ptr(), s, s, s, diag.data_ptr(), abl, stream)
                 assert rc == 0, rc
             torch.cuda.synchronize()
-            d = diag.view(nblk, 4, 4).double()
+            d8 = diag.view(nblk, 4, 8).double()
+            d = d8[..., :4]
             abl_cycles[abl] = round(d.sum(-1).mean().item() / (s // 64))
         tot = d.sum(-1, keepdim=True)
         share = (d / tot).mean(dim=(0, 1)).tolist()
@@ -53,6 +54,8 @@ def main():
                                                    "F0_land"], "share": [round(x, 4) for x in share],
                           "mean_cycles_per_wave": [round(x) for x in cyc], "w4_tflops": round(2 * s ** 3 / dt / 1e12, 1),
                           "loop_cycles_per_ktile": round(sum(cyc) / (s // 64)),
+                          "prologue_cycles": round(d8[..., 4].mean().item()), "epilogue_issue_cycles": round(d8[..., 5].mean().item()),
+                          "kloop_cycles": round(d8[..., 6].mean().item()),
                           "ablation_loop_cycles_per_ktile": {"no_dma": abl_cycles[1], "no_ds_read": abl_cycles[2],
                                                              "full": abl_cycles[0]}}), flush=True)
 
