@@ -90,6 +90,13 @@ std::string expand_vars(const std::string& s, const std::map<std::string, std::s
 
 const char* kDefaultRecipes = R"([
   {"match": "cmd:kfamd-readiness|kfamd-readiness|gpu-readiness", "argv": ["{bin}/kfamd-readiness"], "passArgs": true},
+  {"match": "odh-notebook-controller", "argv": ["{bin}/odh-notebook-controller"], "passArgs": true},
+  {"match": "kfamd/notebook-controller|notebook-controller:", "argv": ["{bin}/notebook-controller"], "passArgs": true},
+  {"match": "profile-controller", "argv": ["{bin}/profile-controller"], "passArgs": true},
+  {"match": "access-management|/kfam", "argv": ["{bin}/access-management"], "passArgs": true},
+  {"match": "tensorboard-controller", "argv": ["{bin}/tensorboard-controller"], "passArgs": true},
+  {"match": "pvcviewer-controller", "argv": ["{bin}/pvcviewer-controller"], "passArgs": true},
+  {"match": "admission-webhook|poddefaults-webhook", "argv": ["{bin}/admission-webhook"], "passArgs": true},
   {"match": "cmd:tensorboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
   {"match": "cmd:jupyter|cmd:start-notebook.sh|cmd:start.sh", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
   {"match": "oauth-proxy|oauth_proxy", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.oauth_proxy"], "passArgs": true},
