@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import os
+import random
 import signal
 import subprocess
 import tempfile
@@ -57,6 +58,11 @@ class LocalCluster:
                "--restart-backoff", self.env.get("KFAMD_RESTART_BACKOFF", "1")]
         if self.gpus is not None:
             cmd += ["--gpus", str(self.gpus)]
+        if not any(a.startswith("--pod-cidr-prefix") for a in self.args):
+            # every pod listens on <pod-ip>:8888; a private loopback /16 per cluster keeps clusters
+            # that overlap in time (pytest-xdist workers, a previous cluster's pods still in their
+            # termination grace period) from answering each other's requests
+            cmd += ["--pod-cidr-prefix", f"127.{random.randint(20, 250)}"]
         cmd += self.args
         self.log_path = Path(self.data_dir) / "kflite.log"
         self._log = open(self.log_path, "ab")

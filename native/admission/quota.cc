@@ -108,9 +108,10 @@ Result QuotaController::reconcile(const Request& r, std::string* err) {
     return {};
   }
   std::map<std::string, double> used;
-  for (const auto& p : pods_->list(r.ns))
+  pods_->visit(r.ns, [&](const Json& p) {
     if (pod_counts(p))
       for (auto& kv : pod_quota_usage(p, hbm_)) used[kv.first] += kv.second;
+  });
   Json hard = q.at_path({"spec", "hard"});
   Json u = Json::object();
   for (const auto& h : hard.as_object()) u[h.first] = fmt_num(used[h.first]);

@@ -36,8 +36,12 @@ bool Watch::next(WatchEvent& ev, int timeout_ms) {
   std::unique_lock<std::mutex> g(mu_);
   if (!cv_.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || closed_; })) return false;
   if (q_.empty()) return false;
-  ev = std::move(q_.front());
+  Item it = std::move(q_.front());
   q_.pop_front();
+  g.unlock();
+  ev.type = std::move(it.type);
+  ev.object = *it.obj;
+  ev.rv = it.rv;
   return true;
 }
 void Watch::stop() {
@@ -49,7 +53,7 @@ bool Watch::closed() const {
   std::lock_guard<std::mutex> g(mu_);
   return closed_ && q_.empty();
 }
-void Watch::push(WatchEvent ev) {
+void Watch::push(Item ev) {
   std::lock_guard<std::mutex> g(mu_);
   if (closed_) return;
   if (q_.size() >= max_queue_) {  // slow consumer: terminate the watch (client re-lists)
@@ -205,7 +209,10 @@ void ApiServer::bootstrap() {
 
 void ApiServer::start_background() {
   if (running_.exchange(true)) return;
-  bg_ = std::thread([this] { background_loop(); });
+  bg_ = std::thread([this] {
+    set_thread_name("apiserver-bg");
+    background_loop();
+  });
 }
 
 // ---- conversion ---------------------------------------------------------------------------------
@@ -487,8 +494,10 @@ void ApiServer::broadcast(std::shared_ptr<const ResourceInfo> res, const std::st
   // caller holds mu_
   const std::string rk = res->key();
   const std::string& ns = obj.str_at({"metadata", "namespace"});
-  log_.emplace_back(rk, WatchEvent{type, obj, rv});
+  auto snap = std::make_shared<const Json>(obj);
+  log_.push_back(LogEntry{rk, type, snap, rv});
   while (log_.size() > cfg_.watch_log_size) log_.pop_front();
+  std::map<std::string, std::shared_ptr<const Json>> converted;  // served version -> snapshot
   int64_t drop = 0;
   bool dropping = take_fault("dropwatch", res->plural, &drop);
   for (auto it = watchers_.begin(); it != watchers_.end();) {
@@ -511,9 +520,17 @@ void ApiServer::broadcast(std::shared_ptr<const ResourceInfo> res, const std::st
     } else if (!now) {
       continue;
     }
-    Json out = obj;
-    if (!w->version_.empty()) convert_out(res, w->version_, out);
-    w->push(WatchEvent{t, std::move(out), rv});
+    std::shared_ptr<const Json> out = snap;
+    if (!w->version_.empty()) {
+      auto& cv = converted[w->version_];
+      if (!cv) {
+        Json o = obj;
+        convert_out(res, w->version_, o);
+        cv = o == obj ? snap : std::make_shared<const Json>(std::move(o));
+      }
+      out = cv;
+    }
+    w->push(Watch::Item{t, std::move(out), rv});
   }
 }
 
@@ -1004,29 +1021,29 @@ WatchPtr ApiServer::r_watch(std::shared_ptr<const ResourceInfo> res, const std::
         if (!w->labels_.matches(kv.second.at_path({"metadata", "labels"})) || !w->fields_.matches(kv.second)) continue;
         Json o = kv.second;
         convert_out(res, version, o);
-        w->q_.push_back(WatchEvent{"ADDED", std::move(o), rv_});
+        w->q_.push_back(Watch::Item{"ADDED", std::make_shared<const Json>(std::move(o)), rv_});
       }
     }
   } else {
     int64_t from = std::atoll(lo.resource_version.c_str());
-    if (!log_.empty() && log_.front().second.rv > from + 1 && from < rv_) {
+    if (!log_.empty() && log_.front().rv > from + 1 && from < rv_) {
       // events between `from` and the oldest retained one are gone
       bool covered = false;
       for (const auto& e : log_)
-        if (e.second.rv == from + 1) covered = true;
+        if (e.rv == from + 1) covered = true;
       if (!covered) {
-        if (err) *err = ApiError{410, "Expired", "too old resource version: " + lo.resource_version + " (" + std::to_string(log_.front().second.rv) + ")"};
+        if (err) *err = ApiError{410, "Expired", "too old resource version: " + lo.resource_version + " (" + std::to_string(log_.front().rv) + ")"};
         return nullptr;
       }
     }
     for (const auto& e : log_) {
-      if (e.first != w->res_key_ || e.second.rv <= from) continue;
-      const Json& obj = e.second.object;
+      if (e.res_key != w->res_key_ || e.rv <= from) continue;
+      const Json& obj = *e.obj;
       if (!w->ns_.empty() && obj.str_at({"metadata", "namespace"}) != w->ns_) continue;
       if (!w->labels_.matches(obj.at_path({"metadata", "labels"})) || !w->fields_.matches(obj)) continue;
       Json o = obj;
       convert_out(res, version, o);
-      w->q_.push_back(WatchEvent{e.second.type, std::move(o), e.second.rv});
+      w->q_.push_back(Watch::Item{e.type, std::make_shared<const Json>(std::move(o)), e.rv});
     }
   }
   watchers_.push_back(w);

@@ -90,10 +90,18 @@ class Watch {
 
  private:
   friend class ApiServer;
-  void push(WatchEvent ev);
+  // Events are queued as shared immutable snapshots: one object per (write, served version) is
+  // shared by every watcher and by the resume log; each consumer copies it in next(), on its own
+  // thread and outside the API server's lock (fan-out cost no longer scales the write latency).
+  struct Item {
+    std::string type;
+    std::shared_ptr<const Json> obj;
+    int64_t rv = 0;
+  };
+  void push(Item ev);
   mutable std::mutex mu_;
   std::condition_variable cv_;
-  std::deque<WatchEvent> q_;
+  std::deque<Item> q_;
   bool closed_ = false;
   // filter
   std::string res_key_, ns_, version_;
@@ -234,7 +242,12 @@ class ApiServer {
   std::map<std::string, ObjMap> data_;  // res key -> objects
   std::map<std::string, std::string> uid_index_;  // uid -> "reskey|ns/name"
   int64_t rv_ = 1;
-  std::deque<std::pair<std::string, WatchEvent>> log_;  // (res key, event) for resumable watches
+  struct LogEntry {
+    std::string res_key, type;
+    std::shared_ptr<const Json> obj;  // storage version
+    int64_t rv = 0;
+  };
+  std::deque<LogEntry> log_;  // for resumable watches
   std::list<std::weak_ptr<Watch>> watchers_;
   std::vector<std::pair<std::string, AdmissionFn>> mutating_, validating_;
   LogProvider log_provider_;

@@ -17,6 +17,8 @@ struct ComponentFlags {
   // kubelet / node
   std::string node_name = "mi355x-node-0";
   int64_t gpus = -1;  // -1 = discover from KFD sysfs (or KFAMD_FAKE_GPUS)
+  int64_t node_cpus = 0;  // advertised node CPU capacity (0 = online host CPUs)
+  int64_t node_memory_gib = 0;  // advertised node memory (0 = host RAM)
   std::string repo_root;  // where kubeflow_rm_amd lives (pod "image" recipes run from here)
   std::string python = "python3";
   double restart_backoff = 10.0;

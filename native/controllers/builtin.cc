@@ -39,8 +39,9 @@ bool being_deleted(const Json& o) { return o.at_path({"metadata", "deletionTimes
 
 std::vector<Json> owned_pods(Informer* pods, const Json& owner) {
   std::vector<Json> out;
-  for (auto& p : pods->list(owner.str_at({"metadata", "namespace"})))
+  pods->visit(owner.str_at({"metadata", "namespace"}), [&](const Json& p) {
     if (is_controlled_by(p, owner)) out.push_back(p);
+  });
   return out;
 }
 
@@ -366,11 +367,11 @@ Result BuiltinControllers::reconcile_pvc(const Request& r, std::string* err) {
   if (sc.is_null() && !sc_name.empty()) return {};  // no provisioner for this class: stays Pending
   if (sc["volumeBindingMode"].as_string() == "WaitForFirstConsumer") {
     bool consumer = false;
-    for (const auto& p : pods_->list(r.ns)) {
-      if (p.at_path({"spec", "nodeName"}).as_string().empty()) continue;
+    pods_->visit(r.ns, [&](const Json& p) {
+      if (p.at_path({"spec", "nodeName"}).as_string().empty()) return;
       for (const auto& v : p.at_path({"spec", "volumes"}).as_array())
         consumer = consumer || v.at_path({"persistentVolumeClaim", "claimName"}).as_string() == r.name;
-    }
+    });
     if (!consumer) return {};
   }
   const std::string pv_name = "pvc-" + pvc.str_at({"metadata", "uid"});

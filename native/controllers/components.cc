@@ -18,6 +18,8 @@ namespace kf {
 void ComponentFlags::register_flags(Flags& f) {
   f.add_string("node-name", &node_name, "mi355x-node-0", "kubelet node name");
   f.add_int("gpus", &gpus, -1, "GPUs advertised by the device plugin (-1 = discover from KFD sysfs / KFAMD_FAKE_GPUS)");
+  f.add_int("node-cpus", &node_cpus, 0, "node CPU capacity advertised by the kubelet (0 = online host CPUs)");
+  f.add_int("node-memory-gib", &node_memory_gib, 0, "node memory capacity advertised by the kubelet (0 = host RAM)");
   f.add_string("repo-root", &repo_root, "", "framework root used by pod image recipes (default: derived from the binary path)");
   f.add_string("python", &python, "python3", "python interpreter for pod image recipes");
   f.add_double("restart-backoff", &restart_backoff, 10.0, "base container restart back-off in seconds");
@@ -165,6 +167,8 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
   if (enabled.count("kubelet")) {
     KubeletConfig kc;
     kc.node_name = I.f.node_name;
+    kc.node_cpus = static_cast<int>(I.f.node_cpus);
+    kc.node_memory_gib = I.f.node_memory_gib;
     kc.root_dir = I.data_dir.empty() ? "/tmp/kflite-" + random_hex(4) : I.data_dir + "/kubelet";
     kc.repo_root = I.f.repo_root;
     if (kc.repo_root.empty()) {

@@ -432,6 +432,7 @@ void HttpServer::accept_loop() {
     }
     active_++;
     std::thread([this, fd, remote] {
+      set_thread_name("http-conn");
       serve_conn(fd, remote);
       {
         std::lock_guard<std::mutex> g(conns_mu_);

@@ -271,26 +271,59 @@ double Json::as_double(double def) const {
   if (t_ == Type::Int) return static_cast<double>(i_);
   return def;
 }
+Json::Json(const Json& o)
+    : t_(o.t_), b_(o.b_), i_(o.i_), d_(o.d_), s_(o.s_),
+      a_(o.a_ ? std::make_unique<Array>(*o.a_) : nullptr),
+      o_(o.o_ ? std::make_unique<Object>(*o.o_) : nullptr) {}
+Json::Json(Json&& o) noexcept
+    : t_(o.t_), b_(o.b_), i_(o.i_), d_(o.d_), s_(std::move(o.s_)), a_(std::move(o.a_)), o_(std::move(o.o_)) {
+  o.t_ = Type::Null;
+}
+void Json::swap(Json& o) noexcept {
+  std::swap(t_, o.t_);
+  std::swap(b_, o.b_);
+  std::swap(i_, o.i_);
+  std::swap(d_, o.d_);
+  s_.swap(o.s_);
+  a_.swap(o.a_);
+  o_.swap(o.o_);
+}
+// copy/move into a temporary first: `x = x["child"]` (source inside the target) stays valid
+Json& Json::operator=(const Json& o) {
+  if (this != &o) {
+    Json tmp(o);
+    swap(tmp);
+  }
+  return *this;
+}
+Json& Json::operator=(Json&& o) noexcept {
+  if (this != &o) {
+    Json tmp(std::move(o));
+    swap(tmp);
+  }
+  return *this;
+}
+
 const std::string& Json::as_string() const { return t_ == Type::String ? s_ : kEmptyStr; }
-const Json::Array& Json::as_array() const { return t_ == Type::Array ? a_ : kEmptyArr; }
+const Json::Array& Json::as_array() const { return t_ == Type::Array ? *a_ : kEmptyArr; }
 Json::Array& Json::mut_array() {
   if (t_ != Type::Array) {
     *this = Json(Array{});
   }
-  return a_;
+  return *a_;
 }
-const Json::Object& Json::as_object() const { return t_ == Type::Object ? o_ : kEmptyObj; }
+const Json::Object& Json::as_object() const { return t_ == Type::Object ? *o_ : kEmptyObj; }
 Json::Object& Json::mut_object() {
   if (t_ != Type::Object) *this = Json(Object{});
-  return o_;
+  return *o_;
 }
 
 Json& Json::operator[](const std::string& key) {
   if (t_ != Type::Object) *this = Json(Object{});
-  for (auto& m : o_)
+  for (auto& m : *o_)
     if (m.first == key) return m.second;
-  o_.emplace_back(key, Json());
-  return o_.back().second;
+  o_->emplace_back(key, Json());
+  return o_->back().second;
 }
 const Json& Json::get(const std::string& key) const {
   const Json* p = find(key);
@@ -298,40 +331,40 @@ const Json& Json::get(const std::string& key) const {
 }
 const Json* Json::find(const std::string& key) const {
   if (t_ != Type::Object) return nullptr;
-  for (auto& m : o_)
+  for (auto& m : *o_)
     if (m.first == key) return &m.second;
   return nullptr;
 }
 Json* Json::find(const std::string& key) {
   if (t_ != Type::Object) return nullptr;
-  for (auto& m : o_)
+  for (auto& m : *o_)
     if (m.first == key) return &m.second;
   return nullptr;
 }
 bool Json::erase(const std::string& key) {
   if (t_ != Type::Object) return false;
-  for (auto it = o_.begin(); it != o_.end(); ++it)
+  for (auto it = o_->begin(); it != o_->end(); ++it)
     if (it->first == key) {
-      o_.erase(it);
+      o_->erase(it);
       return true;
     }
   return false;
 }
 Json& Json::operator[](size_t i) {
-  if (t_ != Type::Array || i >= a_.size()) throw JsonError("json: array index out of range");
-  return a_[i];
+  if (t_ != Type::Array || i >= a_->size()) throw JsonError("json: array index out of range");
+  return (*a_)[i];
 }
 const Json& Json::operator[](size_t i) const {
-  if (t_ != Type::Array || i >= a_.size()) return kNull;
-  return a_[i];
+  if (t_ != Type::Array || i >= a_->size()) return kNull;
+  return (*a_)[i];
 }
 void Json::push_back(Json v) {
   if (t_ != Type::Array) *this = Json(Array{});
-  a_.push_back(std::move(v));
+  a_->push_back(std::move(v));
 }
 size_t Json::size() const {
-  if (t_ == Type::Array) return a_.size();
-  if (t_ == Type::Object) return o_.size();
+  if (t_ == Type::Array) return a_->size();
+  if (t_ == Type::Object) return o_->size();
   return 0;
 }
 
@@ -349,8 +382,8 @@ const Json& Json::at_path(const std::vector<std::string>& path) const {
     if (cur->is_array()) {
       char* end = nullptr;
       long idx = std::strtol(k.c_str(), &end, 10);
-      if (!end || *end || idx < 0 || static_cast<size_t>(idx) >= cur->a_.size()) return kNull;
-      cur = &cur->a_[idx];
+      if (!end || *end || idx < 0 || static_cast<size_t>(idx) >= cur->a_->size()) return kNull;
+      cur = &(*cur->a_)[idx];
       continue;
     }
     cur = cur->find(k);
@@ -404,25 +437,25 @@ void Json::dump_to(std::string& out, int indent, int depth) const {
     case Type::String: dump_string(out, s_); break;
     case Type::Array: {
       out += '[';
-      for (size_t i = 0; i < a_.size(); ++i) {
+      for (size_t i = 0; i < a_->size(); ++i) {
         if (i) out += ',';
         nl(depth + 1);
-        a_[i].dump_to(out, indent, depth + 1);
+        (*a_)[i].dump_to(out, indent, depth + 1);
       }
-      if (!a_.empty()) nl(depth);
+      if (!a_->empty()) nl(depth);
       out += ']';
       break;
     }
     case Type::Object: {
       out += '{';
-      for (size_t i = 0; i < o_.size(); ++i) {
+      for (size_t i = 0; i < o_->size(); ++i) {
         if (i) out += ',';
         nl(depth + 1);
-        dump_string(out, o_[i].first);
+        dump_string(out, (*o_)[i].first);
         out += indent >= 0 ? ": " : ":";
-        o_[i].second.dump_to(out, indent, depth + 1);
+        (*o_)[i].second.dump_to(out, indent, depth + 1);
       }
-      if (!o_.empty()) nl(depth);
+      if (!o_->empty()) nl(depth);
       out += '}';
       break;
     }
@@ -445,10 +478,10 @@ bool Json::operator==(const Json& o) const {
     case Type::Null: return true;
     case Type::Bool: return b_ == o.b_;
     case Type::String: return s_ == o.s_;
-    case Type::Array: return a_ == o.a_;
+    case Type::Array: return *a_ == *o.a_;
     case Type::Object: {
-      if (o_.size() != o.o_.size()) return false;
-      for (const auto& m : o_) {
+      if (o_->size() != o.o_->size()) return false;
+      for (const auto& m : *o_) {
         const Json* v = o.find(m.first);
         if (!v || !(*v == m.second)) return false;
       }

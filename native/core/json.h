@@ -14,6 +14,7 @@
 #include <deque>
 #include <initializer_list>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -47,9 +48,15 @@ class Json {
   Json(double v) : t_(Type::Double), d_(v) {}
   Json(const char* s) : t_(Type::String), s_(s) {}
   Json(std::string s) : t_(Type::String), s_(std::move(s)) {}
-  Json(Array a) : t_(Type::Array), a_(std::move(a)) {}
-  Json(Object o) : t_(Type::Object), o_(std::move(o)) {}
-  Json(std::initializer_list<Member> init) : t_(Type::Object), o_(init) {}
+  Json(Array a) : t_(Type::Array), a_(std::make_unique<Array>(std::move(a))) {}
+  Json(Object o) : t_(Type::Object), o_(std::make_unique<Object>(std::move(o))) {}
+  Json(std::initializer_list<Member> init) : t_(Type::Object), o_(std::make_unique<Object>(init)) {}
+  Json(const Json& o);
+  Json(Json&& o) noexcept;
+  Json& operator=(const Json& o);
+  Json& operator=(Json&& o) noexcept;
+  ~Json() = default;
+  void swap(Json& o) noexcept;
 
   static Json object() { return Json(Object{}); }
   static Json array() { return Json(Array{}); }
@@ -115,8 +122,11 @@ class Json {
   int64_t i_ = 0;
   double d_ = 0.0;
   std::string s_;
-  Array a_;
-  Object o_;
+  // Containers live behind a pointer, present iff t_ is Array / Object: a scalar node allocates
+  // nothing, and a deep copy costs one container per array/object instead of two (allocating)
+  // empty std::deques per node — the copy is on every informer / watch / admission path.
+  std::unique_ptr<Array> a_;
+  std::unique_ptr<Object> o_;
 };
 
 // RFC 7386: null values delete, objects merge recursively, everything else replaces.

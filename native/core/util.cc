@@ -1,4 +1,5 @@
 // util.cc — see util.h.
+#include <pthread.h>
 #include "core/util.h"
 
 #include <sys/stat.h>
@@ -459,6 +460,11 @@ std::string Flags::usage() const {
   for (const auto& kv : flags_)
     out += "  -" + kv.first + " (" + kv.second.kind + ", default \"" + kv.second.def + "\")\n      " + kv.second.help + "\n";
   return out;
+}
+
+void set_thread_name(const std::string& name) {
+  const std::string n = name.substr(0, 15);
+  ::pthread_setname_np(::pthread_self(), n.c_str());
 }
 
 }  // namespace kf

@@ -38,7 +38,9 @@ std::string format_quantity_int(int64_t v);
 
 // ---- time -----------------------------------------------------------------------------------
 int64_t now_unix_ms();
-double now_seconds();  // monotonic
+double now_seconds();
+// Name the calling thread (<= 15 chars, truncated) so per-thread CPU shows in /proc/<pid>/task/*/comm.
+void set_thread_name(const std::string& name);  // monotonic
 std::string rfc3339_now();                 // second precision, "Z" (Kubernetes metav1.Time)
 std::string rfc3339_ms_now();              // millisecond precision (MicroTime-like)
 std::string rfc3339_from_ms(int64_t unix_ms, bool with_ms = false);

@@ -1,4 +1,6 @@
 // gateway.cc — Istio-ingress-equivalent HTTP gateway (see node.h).
+#include <unistd.h>
+
 #include <algorithm>
 
 #include "core/util.h"
@@ -125,6 +127,12 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   h["X-Forwarded-Prefix"] = rt.prefix;
   h["X-Envoy-Original-Path"] = req.path;
   HttpResult r = http_request(req.method, url, req.body, h, static_cast<int>(rt.timeout_s * 1000));
+  // Istio's default retry policy: 2 retries on connect-failure / refused-stream (a pod that is
+  // Ready without a readiness probe may not be listening yet)
+  for (int attempt = 0; attempt < 2 && r.status == 0; ++attempt) {
+    ::usleep(25000);
+    r = http_request(req.method, url, req.body, h, static_cast<int>(rt.timeout_s * 1000));
+  }
   if (r.status == 0) {
     resp.text(503, "upstream connect error or disconnect/reset before headers. reset reason: " + r.error + "\n");
     return;

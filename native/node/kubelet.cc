@@ -206,10 +206,11 @@ Json Kubelet::node_object() const {
   const auto& topo = alloc_->topology();
   int64_t hbm_gib = 0;
   for (const auto& g : topo.gpus) hbm_gib += g.hbm_bytes >> 30;
-  const long cpus = ::sysconf(_SC_NPROCESSORS_ONLN);
+  const long cpus = cfg_.node_cpus > 0 ? cfg_.node_cpus : ::sysconf(_SC_NPROCESSORS_ONLN);
   const long pages = ::sysconf(_SC_PHYS_PAGES), psize = ::sysconf(_SC_PAGE_SIZE);
   Json cap{{"cpu", std::to_string(cpus)},
-           {"memory", std::to_string(static_cast<int64_t>(pages) * psize / 1024) + "Ki"},
+           {"memory", cfg_.node_memory_gib > 0 ? std::to_string(cfg_.node_memory_gib) + "Gi"
+                                                : std::to_string(static_cast<int64_t>(pages) * psize / 1024) + "Ki"},
            {"pods", "110"},
            {"ephemeral-storage", "1Ti"},
            {GPU_RESOURCE, std::to_string(topo.size())},
@@ -264,7 +265,10 @@ void Kubelet::start() {
     return true;
   });
   running_ = true;
-  hb_ = std::thread([this] { heartbeat_loop(); });
+  hb_ = std::thread([this] {
+    set_thread_name("kubelet-hb");
+    heartbeat_loop();
+  });
 }
 
 void Kubelet::heartbeat_loop() {
@@ -858,8 +862,16 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
               }
               cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
             }
-            if (!cr.ready) next_wake = std::min(next_wake, 0.1);
-            else next_wake = std::min(next_wake, std::max(0.2, std::min(cr.next_ready_probe, cr.next_live_probe) - now));
+            if (!cr.ready) {
+              next_wake = std::min(next_wake, 0.1);
+            } else {
+              // wake for the next due probe; a container without probes only needs the 1 s
+              // exit-detection relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
+              double due = 1e30;
+              if (rp.is_object()) due = std::min(due, cr.next_ready_probe);
+              if (lp.is_object()) due = std::min(due, cr.next_live_probe);
+              if (due < 1e30) next_wake = std::min(next_wake, std::max(0.2, due - now));
+            }
           } else {
             next_wake = std::min(next_wake, 0.1);
           }
@@ -929,8 +941,10 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   else if (initialized && all_done && restart_policy != "Always") new_phase = any_failed ? "Failed" : "Succeeded";
   else if (initialized && (any_running || all_done)) new_phase = "Running";
 
-  ApiError ue = c_->update_with_retry(
-      "v1", "Pod", r.ns, r.name,
+  if (!pod.has("apiVersion")) pod["apiVersion"] = "v1";
+  if (!pod.has("kind")) pod["kind"] = "Pod";
+  ApiError ue = c_->update_with_retry_from(
+      std::move(pod),
       [&](Json& o) {
         if (o.str_at({"metadata", "uid"}) != uid) return false;
         Json st = o["status"];

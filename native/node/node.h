@@ -55,6 +55,12 @@ class Scheduler {
   Informer* nodes_ = nullptr;
   std::unique_ptr<EventRecorder> rec_;
   std::shared_ptr<Controller> ctl_;
+  // bound by us, not yet visible in the pod cache (touched only by the single scheduler worker)
+  struct Assumed {
+    std::string ns, name, node;
+    Json requests;
+  };
+  std::map<std::string, Assumed> assumed_;
 };
 
 struct KubeletConfig {
@@ -67,6 +73,8 @@ struct KubeletConfig {
   std::string pod_ip_prefix = "127.20";
   double restart_backoff = 10.0;
   int gpus = -1;
+  int node_cpus = 0;         // advertised CPU capacity (0 = online host CPUs)
+  int64_t node_memory_gib = 0;  // advertised memory (0 = host RAM)
   std::string recipes_file;  // optional JSON overriding the image recipes
 };
 

@@ -2,6 +2,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <set>
 
 #include "apiserver/selector.h"
 #include "core/util.h"
@@ -111,16 +112,33 @@ Result Scheduler::reconcile(const Request& r, std::string* err) {
       reasons.push_back("node(s) didn't match Pod's node affinity/selector");
       continue;
     }
-    // resource fit
+    // resource fit: bound pods from the cache + pods this scheduler assumed onto the node whose
+    // binding the cache has not shown yet (kube-scheduler's assume cache)
     std::map<std::string, double> used;
     int64_t npods = 0;
-    for (const auto& p : pods_->list()) {
-      if (p.at_path({"spec", "nodeName"}).as_string() != name) continue;
+    std::set<std::string> cached_bound;
+    pods_->visit("", [&](const Json& p) {
+      const std::string& bound = p.at_path({"spec", "nodeName"}).as_string();
+      if (!bound.empty() && assumed_.count(ns_name(p))) cached_bound.insert(ns_name(p));
+      if (bound != name) return;
       const std::string& ph = p.at_path({"status", "phase"}).as_string();
-      if (ph == "Succeeded" || ph == "Failed") continue;
+      if (ph == "Succeeded" || ph == "Failed") return;
       npods++;
       const Json req = pod_requests(p);
       for (const auto& m : req.as_object()) used[m.first] += m.second.as_double();
+    });
+    for (auto it = assumed_.begin(); it != assumed_.end();) {
+      Json cur;
+      if (cached_bound.count(it->first) || !pods_->get(it->second.ns, it->second.name, cur) ||
+          !cur.at_path({"spec", "nodeName"}).as_string().empty()) {
+        it = assumed_.erase(it);
+        continue;
+      }
+      if (it->second.node == name) {
+        npods++;
+        for (const auto& m : it->second.requests.as_object()) used[m.first] += m.second.as_double();
+      }
+      ++it;
     }
     const Json& alloc = node.at_path({"status", "allocatable"});
     bool fits = true;
@@ -206,13 +224,9 @@ Result Scheduler::reconcile(const Request& r, std::string* err) {
       },
       true);
   rec_->event(pod, "Normal", "Scheduled", "Successfully assigned " + r.ns + "/" + r.name + " to " + best);
-  // "assume" the binding: wait until our cache reflects it so the next decision (single worker)
-  // accounts for this pod's GPUs / HBM.
-  for (int i = 0; i < 400; ++i) {
-    Json cur;
-    if (!pods_->get(r.ns, r.name, cur) || !cur.at_path({"spec", "nodeName"}).as_string().empty()) break;
-    ::usleep(5000);
-  }
+  // assume the binding so the next decision accounts for this pod's CPU / GPUs / HBM before the
+  // watch event reaches our cache (instead of blocking the worker until it does)
+  assumed_[r.ns + "/" + r.name] = Assumed{r.ns, r.name, best, req};
   return {};
 }
 
@@ -227,9 +241,10 @@ void Scheduler::setup(Manager& mgr) {
   // capacity changes (node updates, pods finishing) re-trigger pending pods
   auto requeue_pending = [this](const std::string&, const Json&) {
     std::vector<Request> out;
-    for (const auto& p : pods_->list())
+    pods_->visit("", [&](const Json& p) {
       if (p.at_path({"spec", "nodeName"}).as_string().empty())
         out.push_back({p.str_at({"metadata", "namespace"}), p.str_at({"metadata", "name"})});
+    });
     return out;
   };
   ctl_->Watches(*nodes_, requeue_pending, [](const std::string& type, const Json& n, const Json* old) {

@@ -32,6 +32,14 @@ ApiError Client::update_with_retry(const std::string& av, const std::string& kin
   return e;
 }
 
+ApiError Client::update_with_retry_from(Json cur, const std::function<bool(Json&)>& mutate, bool status) {
+  if (!mutate(cur)) return {};
+  ApiError e = status ? update_status(cur) : update(cur);
+  if (e.code != 409) return e;
+  return update_with_retry(cur["apiVersion"].as_string(), cur["kind"].as_string(), cur.str_at({"metadata", "namespace"}),
+                           cur.str_at({"metadata", "name"}), mutate, status);
+}
+
 // ---- LocalClient ------------------------------------------------------------------------------------
 namespace {
 class LocalWatch : public WatchSource {

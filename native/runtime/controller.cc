@@ -50,7 +50,10 @@ void Controller::Watches(Informer& inf, std::function<std::vector<Request>(const
 
 void Controller::start() {
   if (running_.exchange(true)) return;
-  for (int i = 0; i < workers_; ++i) threads_.emplace_back([this] { worker(); });
+  for (int i = 0; i < workers_; ++i) threads_.emplace_back([this] {
+    set_thread_name("c:" + name_);
+    worker();
+  });
 }
 
 void Controller::stop() {

@@ -35,7 +35,10 @@ void Informer::add_index(const std::string& name, IndexFn fn) {
 
 void Informer::start() {
   if (running_.exchange(true)) return;
-  th_ = std::thread([this] { run(); });
+  th_ = std::thread([this] {
+    set_thread_name("i:" + kind_);
+    run();
+  });
 }
 
 void Informer::stop() {
@@ -75,6 +78,16 @@ std::vector<Json> Informer::list(const std::string& ns, const LabelSelector& sel
     if (sel.matches(it->second.at_path({"metadata", "labels"}))) out.push_back(it->second);
   }
   return out;
+}
+
+void Informer::visit(const std::string& ns, const std::function<void(const Json&)>& fn) const {
+  std::lock_guard<std::mutex> g(mu_);
+  const std::string prefix = ns + "/";
+  auto it = ns.empty() ? items_.begin() : items_.lower_bound(prefix);
+  for (; it != items_.end(); ++it) {
+    if (!ns.empty() && it->first.compare(0, prefix.size(), prefix) != 0) break;
+    fn(it->second);
+  }
 }
 
 std::vector<Json> Informer::by_index(const std::string& index, const std::string& value) const {

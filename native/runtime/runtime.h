@@ -63,6 +63,9 @@ class Client {
   // RetryOnConflict(DefaultRetry) helper: re-get + mutate + update until no 409 (5 attempts).
   ApiError update_with_retry(const std::string& api_version, const std::string& kind, const std::string& ns,
                              const std::string& name, const std::function<bool(Json&)>& mutate, bool status = false);
+  // Same, but the first attempt mutates `cur` (an object the caller already read) instead of a
+  // fresh GET: an unchanged status costs no API call at all (kubelet per-pod sync loop).
+  ApiError update_with_retry_from(Json cur, const std::function<bool(Json&)>& mutate, bool status = false);
 };
 
 bool resolve_service_via(Client& c, const std::string& host, int port, std::string& ip, int& out_port);
@@ -148,6 +151,10 @@ class Informer {
   bool synced() const { return synced_.load(); }
   bool get(const std::string& ns, const std::string& name, Json& out) const;
   std::vector<Json> list(const std::string& ns = "", const LabelSelector& sel = LabelSelector()) const;
+  // Zero-copy scan of the cache (ns = "" for all) under the cache lock: the hot paths (owned-pod
+  // lookup, scheduler fit, quota usage) read a few fields of every pod, and copying each cached
+  // object for that was O(pods) deep copies per reconcile. fn must not call back into this informer.
+  void visit(const std::string& ns, const std::function<void(const Json&)>& fn) const;
   std::vector<Json> by_index(const std::string& index, const std::string& value) const;
   const std::string& api_version() const { return av_; }
   const std::string& kind() const { return kind_; }
@@ -191,7 +198,10 @@ class WorkQueue {
   bool get(Request& out, int timeout_ms);  // false on timeout or shutdown
   void done(const Request& r);
   void shutdown();
-  bool shutting_down() const { return shutdown_; }
+  bool shutting_down() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return shutdown_;
+  }
   size_t len() const;
 
  private:
@@ -206,12 +216,14 @@ class WorkQueue {
   std::deque<Request> queue_;
   std::set<Request> dirty_, processing_;
   std::map<Request, int> failures_;
+  std::map<Request, double> added_at_;  // when an item became dirty (queue-latency histogram)
   std::multimap<double, Request> delayed_;
   std::condition_variable delay_cv_;
   std::thread delay_th_;
   bool shutdown_ = false;
   std::shared_ptr<GaugeVec> depth_;
   std::shared_ptr<CounterVec> adds_, retries_;
+  std::shared_ptr<HistogramVec> queue_dur_;
 };
 
 // ---- controller ------------------------------------------------------------------------------

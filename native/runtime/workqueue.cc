@@ -14,7 +14,15 @@ WorkQueue::WorkQueue(std::string name, double base_delay, double max_delay, doub
   depth_ = Registry::global().gauge("workqueue_depth", "Current depth of workqueue", {"name"});
   adds_ = Registry::global().counter("workqueue_adds_total", "Total number of adds handled by workqueue", {"name"});
   retries_ = Registry::global().counter("workqueue_retries_total", "Total number of retries handled by workqueue", {"name"});
-  delay_th_ = std::thread([this] { delay_loop(); });
+  // client-go parity: time from an item becoming dirty (watch event / requeue) to a worker taking it.
+  // Watch-event -> reconcile-done latency = this + controller_runtime_reconcile_time_seconds.
+  queue_dur_ = Registry::global().histogram("workqueue_queue_duration_seconds",
+                                            "How long in seconds an item stays in workqueue before being requested",
+                                            {"name"}, HistogramVec::exponential(0.00001, 2, 24));
+  delay_th_ = std::thread([this] {
+    set_thread_name("q:" + name_);
+    delay_loop();
+  });
 }
 
 WorkQueue::~WorkQueue() {
@@ -28,6 +36,7 @@ void WorkQueue::add(const Request& r) {
   adds_->inc({name_});
   if (dirty_.count(r)) return;
   dirty_.insert(r);
+  added_at_.emplace(r, now_seconds());
   if (processing_.count(r)) return;  // re-queued by done()
   queue_.push_back(r);
   depth_->set({name_}, static_cast<double>(queue_.size()));
@@ -92,6 +101,11 @@ bool WorkQueue::get(Request& out, int timeout_ms) {
   queue_.pop_front();
   dirty_.erase(out);
   processing_.insert(out);
+  auto at = added_at_.find(out);
+  if (at != added_at_.end()) {
+    queue_dur_->observe({name_}, now_seconds() - at->second);
+    added_at_.erase(at);
+  }
   depth_->set({name_}, static_cast<double>(queue_.size()));
   return true;
 }
@@ -136,6 +150,7 @@ void WorkQueue::delay_loop() {
     delayed_.erase(it);
     if (!dirty_.count(r)) {
       dirty_.insert(r);
+      added_at_.emplace(r, now);
       if (!processing_.count(r)) {
         queue_.push_back(r);
         cv_.notify_one();

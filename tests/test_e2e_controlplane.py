@@ -7,6 +7,7 @@ by the ingress gateway, and are garbage collected.
 """
 import json
 import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -48,10 +49,19 @@ def test_notebook_to_statefulset_service_and_ready(c, cluster):
     nb = c.wait_for(NB, "Notebook", "nb1", "e2e", _ready, timeout=30)
     assert "running" in nb["status"]["containerState"]
     assert any(x["type"] == "Ready" for x in nb["status"]["conditions"])
-    # through the ingress gateway, like the browser would
-    with urllib.request.urlopen(cluster.gateway + "/notebook/e2e/nb1/api/status", timeout=5) as r:
-        assert r.status == 200
-        assert "started" in json.loads(r.read())
+    # through the ingress gateway, like the browser would (the notebook has no readiness probe, as
+    # in the reference's spawner template, so Ready can precede the server listening: poll briefly)
+    deadline = time.time() + 15
+    while True:
+        try:
+            with urllib.request.urlopen(cluster.gateway + "/notebook/e2e/nb1/api/status", timeout=5) as r:
+                assert r.status == 200
+                assert "started" in json.loads(r.read())
+                break
+        except urllib.error.HTTPError as e:
+            if e.code != 503 or time.time() > deadline:
+                raise
+            time.sleep(0.1)
 
 
 def test_stop_and_restart_notebook(c):
