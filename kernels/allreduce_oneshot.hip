@@ -1,0 +1,179 @@
+// allreduce_oneshot.hip — K3 small-message fast path: a one-shot
+// all-reduce over the peer-visible buffers of N ranks on one node (xGMI point-to-point).
+//
+// Why: a ring all-reduce of a KB-sized message is 2(N-1) latency-bound hops; over a full xGMI
+// mesh every GPU can read every peer's buffer directly, so the whole reduction is ONE kernel:
+//   entry barrier  -> every rank's input is published (release) and every peer has arrived,
+//   reduce         -> block b sums slice b of all N inputs (16-byte loads, fp32 accumulation in
+//                     rank order 0..N-1, so every rank produces bit-identical output),
+//   exit barrier   -> no rank returns (and lets its caller overwrite its input) while a peer may
+//                     still be reading it.
+// Each barrier is per block pair: block b of rank r stores its epoch into flags[p][phase][r][b]
+// of every peer p (system-scope atomic), then polls its own flags[r][phase][p][b] for every p.
+// Epochs are per call (caller passes 1, 2, 3, ...; never 0); flags are zeroed once at allocation.
+// Every spin is bounded: a peer that never arrives sets *timeout and the kernel drains (the caller
+// reports the failure, the GPU never hangs).
+//
+// Ranks may be separate devices (peer access / IPC-opened buffers: the readiness op, DP) or, for
+// tests on one GPU, several ranks simulated in ONE launch (gridDim.y = ranks in this launch,
+// rank = rank0 + blockIdx.y): all blocks of a small grid are co-resident, so the same barrier
+// protocol is exercised end to end.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kfamd_kernels.h"
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kThreads = 256;
+constexpr unsigned kSpinLimit = 1u << 22;  // x s_sleep(1): tens of ms before declaring a timeout
+
+struct Peers {
+  const void* in[kMaxRanks];
+  void* out[kMaxRanks];
+  uint32_t* flags[kMaxRanks];
+};
+
+__device__ __forceinline__ void store_flag(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t load_flag(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Block-pair barrier: thread t < nranks signals peer t, then waits for peer t's signal.
+__device__ __forceinline__ void barrier(const Peers& P, int me, int nranks, int phase, uint32_t epoch,
+                                        unsigned* timeout) {
+  const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  __syncthreads();  // every thread's reads / writes of this phase are done before anyone signals
+  if (t < nranks) {
+    // release: this rank's input (written by earlier work on its stream) and, at the exit
+    // barrier, this block's reads are complete before the peer can observe the flag
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    store_flag(P.flags[t] + ((size_t)phase * nranks + me) * nb + b, epoch);
+    uint32_t* mine = P.flags[me] + ((size_t)phase * nranks + t) * nb + b;
+    unsigned spins = 0;
+    while (load_flag(mine) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    // acquire: drop any stale cached copy of the peers' buffers before reading them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+template <typename T>
+struct Vec;
+template <>
+struct Vec<float> {
+  static constexpr int kElems = 4;
+  __device__ static void acc(float (&s)[8], const uint4& v) {
+    s[0] += __uint_as_float(v.x);
+    s[1] += __uint_as_float(v.y);
+    s[2] += __uint_as_float(v.z);
+    s[3] += __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const float (&s)[8]) {
+    return uint4{__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])};
+  }
+  __device__ static float load1(const void* p, long long i) { return static_cast<const float*>(p)[i]; }
+  __device__ static void store1(void* p, long long i, float v) { static_cast<float*>(p)[i] = v; }
+};
+template <>
+struct Vec<__bf16> {
+  static constexpr int kElems = 8;
+  __device__ static float lo(uint32_t w) { return __uint_as_float(w << 16); }
+  __device__ static float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+  __device__ static void acc(float (&s)[8], const uint4& v) {
+    s[0] += lo(v.x); s[1] += hi(v.x);
+    s[2] += lo(v.y); s[3] += hi(v.y);
+    s[4] += lo(v.z); s[5] += hi(v.z);
+    s[6] += lo(v.w); s[7] += hi(v.w);
+  }
+  __device__ static uint32_t pk(float a, float b) {
+    const __bf16 x = (__bf16)a, y = (__bf16)b;  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
+    return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+  }
+  __device__ static uint4 pack(const float (&s)[8]) {
+    return uint4{pk(s[0], s[1]), pk(s[2], s[3]), pk(s[4], s[5]), pk(s[6], s[7])};
+  }
+  __device__ static float load1(const void* p, long long i) { return (float)static_cast<const __bf16*>(p)[i]; }
+  __device__ static void store1(void* p, long long i, float v) { static_cast<__bf16*>(p)[i] = (__bf16)v; }
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long n, int nranks, int rank0,
+                                                              uint32_t epoch, unsigned* timeout) {
+  using V = Vec<T>;
+  const int me = rank0 + blockIdx.y;
+  barrier(P, me, nranks, 0, epoch, timeout);
+  // 16-byte vectors; rank r's vector i lives at in[r] + 16 i
+  const long long nvec = n / V::kElems;
+  const long long stride = (long long)gridDim.x * kThreads;
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 v[kMaxRanks];
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)  // issue every peer's load before the first add
+      if (r < nranks) v[r] = static_cast<const uint4*>(P.in[r])[i];
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+      if (r < nranks) V::acc(s, v[r]);
+    static_cast<uint4*>(P.out[me])[i] = V::pack(s);
+  }
+  // tail (n not a multiple of the vector width): block 0 only
+  if (blockIdx.x == 0) {
+    for (long long i = nvec * V::kElems + threadIdx.x; i < n; i += kThreads) {
+      float s = 0.f;
+      for (int r = 0; r < nranks; ++r) s += V::load1(P.in[r], i);
+      V::store1(P.out[me], i, s);
+    }
+  }
+  barrier(P, me, nranks, 1, epoch, timeout);
+}
+
+}  // namespace
+
+extern "C" long long kfamd_allreduce_oneshot_flag_bytes(int nranks, int nblocks) {
+  return (long long)2 * nranks * nblocks * (long long)sizeof(uint32_t);
+}
+
+extern "C" int kfamd_allreduce_oneshot_blocks(long long n, int dtype) {
+  const long long vec = dtype == KFAMD_DTYPE_BF16 ? 8 : 4;
+  const long long nvec = (n + vec - 1) / vec;
+  long long b = (nvec + kThreads * 4 - 1) / (kThreads * 4);  // ~4 vectors per thread
+  return (int)(b < 1 ? 1 : (b > 64 ? 64 : b));
+}
+
+extern "C" int kfamd_allreduce_oneshot(const void* const* inputs, void* const* outputs, uint32_t* const* flags,
+                                       int nranks, int rank0, int launch_ranks, long long n, int dtype,
+                                       unsigned epoch, int nblocks, unsigned* timeout, void* stream) {
+  if (nranks < 1 || nranks > kMaxRanks || launch_ranks < 1 || rank0 < 0 || rank0 + launch_ranks > nranks ||
+      n < 0 || epoch == 0 || nblocks < 1 || !timeout || (dtype != KFAMD_DTYPE_F32 && dtype != KFAMD_DTYPE_BF16))
+    return KFAMD_EINVAL;
+  Peers P{};
+  for (int r = 0; r < nranks; ++r) {
+    if (!inputs[r] || !flags[r]) return KFAMD_EINVAL;
+    if (reinterpret_cast<uintptr_t>(inputs[r]) & 15) return KFAMD_EALIGN;
+    P.in[r] = inputs[r];
+    P.flags[r] = flags[r];
+  }
+  for (int r = rank0; r < rank0 + launch_ranks; ++r) {
+    if (!outputs[r]) return KFAMD_EINVAL;
+    if (reinterpret_cast<uintptr_t>(outputs[r]) & 15) return KFAMD_EALIGN;
+    P.out[r] = outputs[r];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(nblocks, launch_ranks), block(kThreads);
+  if (dtype == KFAMD_DTYPE_BF16)
+    hipLaunchKernelGGL(allreduce_oneshot<__bf16>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch, timeout);
+  else
+    hipLaunchKernelGGL(allreduce_oneshot<float>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch, timeout);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}

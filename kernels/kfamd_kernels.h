@@ -3,7 +3,8 @@
 // This library is the MI355X compute path of the framework (SURVEY.md §2.7.2, K1–K3):
 //   K1  bf16 GEMM on MFMA (v_mfma_f32_16x16x32_bf16), LDS-tiled, global_load_lds staging
 //   K2  LayerNorm / RMSNorm forward+backward (bf16 I/O, fp32 statistics)
-//   K3  (collectives live in RCCL; see kfamd_readiness.cpp / kubeflow_rm_amd.parallel)
+//   K3  one-shot peer all-reduce for small messages (allreduce_oneshot.hip); large messages
+//       go to RCCL (native/readiness, kubeflow_rm_amd.parallel)
 //
 // It is consumed three ways, all in-tree:
 //   * Python (kubeflow_rm_amd.ops) through ctypes — one HIP runtime shared with torch;
@@ -65,6 +66,20 @@ long long kfamd_layernorm_bwd_workspace(int rows, int hidden);
 int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, const float* mean,
                              const float* rstd, void* dx, float* dgamma, float* dbeta,
                              float* workspace, int rows, int hidden, void* stream);
+
+// ---- K3: one-shot all-reduce over peer-visible buffers ------------------------------------------
+enum kfamd_dtype { KFAMD_DTYPE_F32 = 0, KFAMD_DTYPE_BF16 = 1 };
+// out[r] = sum over ranks of in[*] (fp32 accumulation in rank order: bit-identical on every rank).
+// inputs/flags: nranks pointers (peer-visible: same device, peer-access or IPC-opened), 16-B
+// aligned; outputs: rank-indexed, only [rank0, rank0 + launch_ranks) are written. One launch serves
+// launch_ranks ranks (1 per device in real use; several to simulate ranks on one GPU). flags[r]:
+// kfamd_allreduce_oneshot_flag_bytes(nranks, nblocks) zeroed bytes per rank, reused across calls
+// with epoch = 1, 2, 3, ... (same nblocks every call). *timeout is set if a peer never arrived.
+long long kfamd_allreduce_oneshot_flag_bytes(int nranks, int nblocks);
+int kfamd_allreduce_oneshot_blocks(long long n, int dtype);
+int kfamd_allreduce_oneshot(const void* const* inputs, void* const* outputs, uint32_t* const* flags,
+                            int nranks, int rank0, int launch_ranks, long long n, int dtype,
+                            unsigned epoch, int nblocks, unsigned* timeout, void* stream);
 
 // Library identity (for the loud "native code loaded" check).
 const char* kfamd_build_info(void);

@@ -78,6 +78,9 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     return KERNEL_LIB
 
 
+SANITIZER_CXX = "/opt/rocm/lib/llvm/bin/clang++"
+
+
 def build_native(force: bool = False, jobs: int = 8, build_type: str = "Release",
                  sanitize: str = "") -> Path:
     """Configure + build the C++ control plane with CMake/Ninja; install binaries into bin/."""
@@ -92,6 +95,11 @@ def build_native(force: bool = False, jobs: int = 8, build_type: str = "Release"
     cfg = ["cmake", *gen, str(src), f"-DCMAKE_BUILD_TYPE={build_type}",
            f"-DKFAMD_SANITIZE={sanitize}", f"-DKFAMD_BIN_DIR={BIN_DIR if not sanitize else bdir / 'bin'}",
            f"-DKFAMD_KERNEL_DIR={KERNEL_DIR}", f"-DKFAMD_OFFLOAD_ARCH={ARCH}"]
+    if sanitize and Path(SANITIZER_CXX).exists():
+        # GCC 11's libtsan has no pthread_cond_clockwait interceptor, which libstdc++ 11 uses for
+        # every condition_variable::wait_for: it then reports "double lock" + phantom races on
+        # every queue. ROCm's LLVM ships current tsan/asan/ubsan runtimes that intercept it.
+        cfg.append(f"-DCMAKE_CXX_COMPILER={SANITIZER_CXX}")
     if not (bdir / "CMakeCache.txt").exists():
         _run(cfg, cwd=bdir)
     _run(["cmake", "--build", str(bdir), "-j", str(jobs)], cwd=bdir)

@@ -45,6 +45,10 @@ def _split_api_version(api_version: str) -> tuple[str, str]:
     return "", api_version
 
 
+# Sanitizer builds of the control plane (tools/sanitize.sh) run 5-15x slower: every wait scales.
+_TIMEOUT_SCALE = float(os.environ.get("KFAMD_TIMEOUT_SCALE", "1"))
+
+
 class KubeClient:
     """REST client. ``base_url`` defaults to $KFAMD_API_URL / in-cluster KUBERNETES_SERVICE_HOST."""
 
@@ -220,7 +224,7 @@ class KubeClient:
     # ---- waits ------------------------------------------------------------------------------------
     def wait_for(self, api_version: str, kind: str, name: str, namespace: str | None,
                  predicate: Callable[[dict], bool], timeout: float = 30.0, interval: float = 0.05) -> dict:
-        deadline = time.time() + timeout
+        deadline = time.time() + timeout * _TIMEOUT_SCALE
         last: Any = None
         while time.time() < deadline:
             try:
@@ -235,7 +239,7 @@ class KubeClient:
         raise TimeoutError(f"timed out waiting for {kind} {namespace}/{name}; last={str(last)[:500]}")
 
     def wait_gone(self, api_version: str, kind: str, name: str, namespace: str | None, timeout: float = 30.0) -> None:
-        deadline = time.time() + timeout
+        deadline = time.time() + timeout * _TIMEOUT_SCALE
         while time.time() < deadline:
             if not self.exists(api_version, kind, name, namespace):
                 return

@@ -63,6 +63,10 @@ class LocalCluster:
             # that overlap in time (pytest-xdist workers, a previous cluster's pods still in their
             # termination grace period) from answering each other's requests
             cmd += ["--pod-cidr-prefix", f"127.{random.randint(20, 250)}"]
+        if not any(a.startswith("--repo-root") for a in self.args):
+            # explicit: a kflite built elsewhere (sanitizer builds under build/) cannot derive the
+            # package root from its own path, and pod image recipes run `python -m kubeflow_rm_amd...`
+            cmd += ["--repo-root", str(ROOT)]
         cmd += self.args
         self.log_path = Path(self.data_dir) / "kflite.log"
         self._log = open(self.log_path, "ab")

@@ -32,6 +32,10 @@ _SIGNATURES = {
     "kfamd_layernorm_bwd_workspace": (c_ll, [c_int, c_int]),
     "kfamd_layernorm_bwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_int, c_int, c_vp]),
+    "kfamd_allreduce_oneshot_flag_bytes": (c_ll, [c_int, c_int]),
+    "kfamd_allreduce_oneshot_blocks": (c_int, [c_ll, c_int]),
+    "kfamd_allreduce_oneshot": (c_int, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_int, c_int,
+                                        c_int, c_ll, c_int, ctypes.c_uint, c_int, c_vp, c_vp]),
     "kfamd_build_info": (ctypes.c_char_p, []),
 }
 

@@ -184,6 +184,12 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       ssize_t n = ::readlink("/proc/self/exe", buf, sizeof buf - 1);
       std::string exe = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "";
       kc.bin_dir = exe.substr(0, exe.rfind('/'));
+      // the in-pod readiness op is a HIP binary that only the regular build produces: a kflite
+      // from a sanitizer build dir uses the package's bin/ for it
+      const std::string pkg_bin = kc.repo_root + "/kubeflow_rm_amd/bin";
+      if (::access((kc.bin_dir + "/kfamd-readiness").c_str(), X_OK) != 0 &&
+          ::access((pkg_bin + "/kfamd-readiness").c_str(), X_OK) == 0)
+        kc.bin_dir = pkg_bin;
     }
     kc.python = I.f.python;
     kc.api_url = I.api_url;

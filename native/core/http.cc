@@ -393,17 +393,20 @@ bool HttpServer::listen(const std::string& addr, int port, std::string* err) {
 
 void HttpServer::start() {
   running_ = true;
-  accept_thread_ = std::thread([this] { accept_loop(); });
+  const int fd = listen_fd_;
+  accept_thread_ = std::thread([this, fd] { accept_loop(fd); });
 }
 
 void HttpServer::stop() {
   if (!running_.exchange(false)) return;
+  // shutdown() wakes the accept thread; the fd is closed only after it has exited, so its number
+  // cannot be reused by another socket while the loop still polls it (found by TSAN)
+  if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  if (accept_thread_.joinable()) accept_thread_.join();
   if (listen_fd_ >= 0) {
-    ::shutdown(listen_fd_, SHUT_RDWR);
     ::close(listen_fd_);
     listen_fd_ = -1;
   }
-  if (accept_thread_.joinable()) accept_thread_.join();
   {
     std::lock_guard<std::mutex> g(conns_mu_);
     for (int fd : conn_fds_) ::shutdown(fd, SHUT_RDWR);
@@ -412,14 +415,14 @@ void HttpServer::stop() {
   for (int i = 0; i < 500 && active_.load() > 0; ++i) ::usleep(10000);
 }
 
-void HttpServer::accept_loop() {
+void HttpServer::accept_loop(int listen_fd) {
   while (running_) {
-    struct pollfd p {listen_fd_, POLLIN, 0};
+    struct pollfd p {listen_fd, POLLIN, 0};
     int pr = ::poll(&p, 1, 200);
     if (pr <= 0) continue;
     struct sockaddr_in ca {};
     socklen_t cl = sizeof ca;
-    int fd = ::accept4(listen_fd_, reinterpret_cast<sockaddr*>(&ca), &cl, SOCK_CLOEXEC);
+    int fd = ::accept4(listen_fd, reinterpret_cast<sockaddr*>(&ca), &cl, SOCK_CLOEXEC);
     if (fd < 0) continue;
     int one = 1;
     ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);

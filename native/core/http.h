@@ -101,7 +101,7 @@ class HttpServer {
   size_t active_connections() const { return active_.load(); }
 
  private:
-  void accept_loop();
+  void accept_loop(int listen_fd);
   void serve_conn(int fd, std::string remote);
   Handler handler_;
   int listen_fd_ = -1;
