@@ -8,13 +8,17 @@
 //   3. K2: LayerNorm (kernels/layernorm_bf16.hip) verified on sampled rows -> GB/s;
 //   4. K3: with >= 2 visible GPUs, peer-access matrix + RCCL communicator over all devices
 //      (ncclCommInitAll, one process) and an all-reduce sweep with algbw / busbw
-//      (busbw = algbw * 2(n-1)/n), checked for correctness.
+//      (busbw = algbw * 2(n-1)/n), checked for correctness; plus the hand-written one-shot
+//      peer all-reduce (kernels/allreduce_oneshot.hip) over the same devices for the
+//      latency-bound sizes (8 B .. 256 KiB), verified and timed next to RCCL.
+//      --oneshot-sim N runs the one-shot kernel with N ranks simulated on device 0 (1-GPU boxes).
 // The JSON result goes to stdout and to $KFAMD_TERMINATION_LOG (the pod's termination message,
 // mirrored into the Notebook status by the notebook controller). Exit code != 0 fails the pod's
 // initialisation (pod not Ready -> Notebook status shows the failure).
 //
 // Flags: --m/--n/--k GEMM size (default 4096^3), --iters, --ln-rows/--ln-hidden,
-//        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce.
+//        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
+//        --oneshot-sim N.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -106,6 +110,7 @@ struct Args {
   long long ar_max = 64ll << 20;
   double min_tflops = 0;
   bool skip_ln = false, skip_ar = false;
+  int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
 };
 
 bool gemm_check(int dev, const Args& a, Json& out) {
@@ -339,6 +344,109 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
   return ok;
 }
 
+// K3 fast path: one-shot peer all-reduce. sim_ranks > 0: that many ranks on device 0, one launch.
+bool oneshot_check(int ndev, int sim_ranks, Json& out) {
+  g_stage = "allreduce-oneshot";
+  const bool sim = sim_ranks > 0;
+  const int nranks = sim ? sim_ranks : ndev;
+  if (nranks < 2 || nranks > 8) {
+    out = Json{{"skipped", "needs 2..8 ranks"}};
+    return true;
+  }
+  const size_t max_bytes = 256 << 10;
+  const int max_blocks = 64;
+  const long long fbytes = kfamd_allreduce_oneshot_flag_bytes(nranks, max_blocks);
+  if (!sim) {
+    for (int i = 0; i < nranks; ++i) {
+      HIP_OK(hipSetDevice(i));
+      for (int j = 0; j < nranks; ++j) {
+        if (i == j) continue;
+        hipError_t pe = hipDeviceEnablePeerAccess(j, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+          fail(std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(pe));
+          return false;
+        }
+      }
+    }
+  }
+  auto dev_of = [&](int r) { return sim ? 0 : r; };
+  std::vector<void*> in(8, nullptr), outb(8, nullptr);
+  std::vector<uint32_t*> flags(8, nullptr);
+  std::vector<unsigned*> tmo(nranks, nullptr);
+  std::vector<hipStream_t> st(sim ? 1 : nranks);
+  for (int r = 0; r < nranks; ++r) {
+    HIP_OK(hipSetDevice(dev_of(r)));
+    HIP_OK(hipMalloc(&in[r], max_bytes));
+    HIP_OK(hipMalloc(&outb[r], max_bytes));
+    // flags are polled across devices: uncached so a peer's atomic store is seen without a flush
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags[r]), fbytes, hipDeviceMallocUncached) != hipSuccess)
+      HIP_OK(hipMalloc(&flags[r], fbytes));
+    HIP_OK(hipMemset(flags[r], 0, fbytes));
+    HIP_OK(hipMalloc(&tmo[r], sizeof(unsigned)));
+    HIP_OK(hipMemset(tmo[r], 0, sizeof(unsigned)));
+    if (!sim || r == 0) HIP_OK(hipStreamCreate(&st[r]));
+  }
+  unsigned epoch = 0;
+  bool ok = true;
+  auto launch_all = [&](size_t n) -> bool {
+    ++epoch;
+    const int nb = kfamd_allreduce_oneshot_blocks((long long)n, KFAMD_DTYPE_F32);
+    for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      int rc = kfamd_allreduce_oneshot(in.data(), outb.data(), flags.data(), nranks, sim ? 0 : r, sim ? nranks : 1,
+                                       (long long)n, KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r]);
+      if (rc != 0) {
+        fail("kfamd_allreduce_oneshot rc=" + std::to_string(rc));
+        return false;
+      }
+    }
+    for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      HIP_OK(hipStreamSynchronize(st[r]));
+    }
+    return true;
+  };
+  Json sweep = Json::array();
+  for (size_t bytes = 16; bytes <= max_bytes; bytes *= 4) {
+    const size_t n = bytes / 4;
+    for (int r = 0; r < nranks; ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      hipLaunchKernelGGL(fill_const, dim3(64), dim3(256), 0, st[sim ? 0 : r], static_cast<float*>(in[r]), n, (float)(r + 1));
+      HIP_OK(hipStreamSynchronize(st[sim ? 0 : r]));
+    }
+    if (!launch_all(n)) return false;
+    const float want = (float)nranks * (nranks + 1) / 2;
+    std::vector<float> h(n);
+    for (int r = 0; r < nranks; ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      HIP_OK(hipMemcpy(h.data(), outb[r], bytes, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < n; ++i)
+        if (h[i] != want) ok = false;
+      unsigned t = 0;
+      HIP_OK(hipMemcpy(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost));
+      if (t) ok = false;
+    }
+    const int iters = 50;
+    auto t1 = std::chrono::steady_clock::now();
+    for (int it = 0; it < iters; ++it)
+      if (!launch_all(n)) return false;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / iters;
+    sweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}});
+  }
+  for (int r = 0; r < nranks; ++r) {
+    (void)hipSetDevice(dev_of(r));
+    (void)hipFree(in[r]);
+    (void)hipFree(outb[r]);
+    (void)hipFree(flags[r]);
+    (void)hipFree(tmo[r]);
+  }
+  for (auto s : st) (void)hipStreamDestroy(s);
+  out = Json{{"mode", sim ? "simulated-on-device-0" : "peer"}, {"ranks", nranks}, {"sweep", sweep}, {"correct", ok},
+             {"note", "us = host wall per call incl. launch + stream sync"}};
+  if (!ok) fail("one-shot all-reduce mismatch or peer timeout");
+  return ok;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -364,6 +472,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--min-tflops")) a.min_tflops = std::atof(v);
     else if (s == "--skip-ln") a.skip_ln = true;
     else if (s == "--skip-allreduce") a.skip_ar = true;
+    else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
   }
   auto t0 = std::chrono::steady_clock::now();
   g_stage = "hip-init";
@@ -404,6 +513,11 @@ int main(int argc, char** argv) {
       Json ar;
       allreduce_check(ndev, a, ar);
       g_result["allreduce"] = ar;
+    }
+    if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
+      Json os;
+      oneshot_check(ndev, a.oneshot_sim, os);
+      g_result["allreduce_oneshot"] = os;
     }
   }
   g_stage = "report";
