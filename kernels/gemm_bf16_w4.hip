@@ -259,33 +259,47 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
+  // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
+  // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
+  // groups (cdna_hip_programming.md T21, 16-lane form), after which every lane holds 8 contiguous
+  // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
+  // lh 3 -> block n+1 cols 8-15. Half the store instructions (dwordx4 instead of dwordx2), every
+  // row segment 64 contiguous bytes; the tail is ~5 % of a block at 8192^3 (w4_diag epilogue stamps).
+  auto finish = [&](int i, int n, int m) -> uint2 {
+    const int col = n0 + wn * 128 + n * 16 + lh * 4;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
+    if (HAS_BIAS) {
+      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+    }
+    if (ACT != KFAMD_ACT_NONE) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
+    }
+    if (HAS_RES) {
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+    return __builtin_bit_cast(uint2, o);
+  };
+  const int swap_col = 16 * (lh & 1) + 8 * (lh >> 1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + lr;
+    __bf16* crow = C + (long long)m * ldc + n0 + wn * 128 + swap_col;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) {
-      const int col = n0 + wn * 128 + n * 16 + lh * 4;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
-      if (HAS_BIAS) {
-        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
-      }
-      if (ACT != KFAMD_ACT_NONE) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
-      }
-      if (HAS_RES) {
-        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
-      *reinterpret_cast<bf16x4*>(C + (long long)m * ldc + col) = o;
+    for (int n = 0; n < 8; n += 2) {
+      uint2 p = finish(i, n, m), q = finish(i, n + 1, m);
+      const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
+      *reinterpret_cast<uint4*>(crow + n * 16) = uint4{sx[0], sy[0], sx[1], sy[1]};
     }
   }
   if (DIAG) {
