@@ -551,6 +551,11 @@ extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* 
                                             long long ldr, long long sa, long long sb, long long sc, long long sr,
                                             float alpha, int act, void* stream);
 
+extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
+                                             int M, int N, int K, int batch, long long lda, long long ldb,
+                                             long long ldc, long long ldr, long long sa, long long sb, long long sc,
+                                             long long sr, float alpha, int act, void* stream);
+
 extern "C" int kfamd_gemm_nt_bf16_w4rg_launch(const void* A, const void* B, void* C, int M, int N, int K,
                                               long long lda, long long ldb, long long ldc, int rg, void* stream);
 
@@ -575,6 +580,21 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
                         (!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0) &&
                         (!R || ((reinterpret_cast<uintptr_t>(R) & 7) == 0 && ldr % 4 == 0 && stride_r % 4 == 0));
   bool fast = shapes_ok && align_ok;
+  // 128x128 w4 tiles: any M, N % 128 (K % 64) with the fast-path alignment. Auto picks them when the
+  // problem has at most half as many 256x256 tiles as MI355X has CUs (256): 2048^2 is 64 tiles of
+  // 256^2 (a quarter of the chip) but 256 of 128^2 at two blocks per CU (profiles/r1_gemm_w4s:
+  // 1024^3 92 -> 206 TF, 2048^3 430 -> 848; at 3072^3, 144 tiles, the 256 tile still wins 980 : 904).
+  const bool shapes128 = (M % 128 == 0) && (N % 128 == 0) && (K % kBK == 0);
+  const long long tiles256 = shapes_ok ? (long long)(M / kBM) * (N / kBN) * batch : 0;
+  const bool w4s_ok = (long long)128 * lda * 2 < (1LL << 31) && (long long)128 * ldb * 2 < (1LL << 31);
+  // the w4 epilogues store 16 B (8 columns) per lane: C rows must be 16-byte aligned
+  const bool c16 = (ldc % 8 == 0) && (stride_c % 8 == 0);
+  if (variant == 9 || (variant == 0 && align_ok && c16 && shapes128 && w4s_ok && tiles256 <= 128)) {
+    if (!shapes128) return KFAMD_EINVAL;
+    if (!align_ok || !c16) return KFAMD_EALIGN;
+    return kfamd_gemm_nt_bf16_w4s_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
+                                         stride_c, stride_r, alpha, act, stream);
+  }
   if (variant == 1 || variant >= 3) {
     if (!shapes_ok) return KFAMD_EINVAL;
     if (!align_ok) return KFAMD_EALIGN;
@@ -595,7 +615,8 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   // default fast path: the 4-wave w4 kernel (one wave per SIMD, 5-slot LDS ring; profiles/r1_gemm_w4c);
   // the 8-wave pipe_sched kernel when a 256-row panel spans >= 2 GiB (w4's 32-bit buffer offsets)
   const bool w4_ok = (long long)kBM * lda * 2 < (1LL << 31) && (long long)kBN * ldb * 2 < (1LL << 31);
-  if (fast && (variant == 6 || (variant == 0 && w4_ok))) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
+  if (fast && variant == 6 && !c16) return KFAMD_EALIGN;
+  if (fast && (variant == 6 || (variant == 0 && w4_ok && c16))) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
     return kfamd_gemm_nt_bf16_w4_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
                                         stride_c, stride_r, alpha, act, stream);
   }

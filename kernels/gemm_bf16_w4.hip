@@ -65,13 +65,23 @@ __device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& 
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DIAG = false, int RG = 2, int ABL = 0>
-__global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads), amdgpu_waves_per_eu(1, 1)))
+// BM = 256: the 256x256 tile above (one 160 KiB block per CU). BM = 128 ("w4s"): the same
+// pipeline on a 128x128 tile, 64x64 per wave, 80 KiB of LDS -> two blocks per CU; chosen when a
+// problem has fewer 256-tiles than CUs (2048^2: 64 tiles of 256^2 vs 256 of 128^2).
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DIAG = false, int RG = 2, int ABL = 0, int BM = 256>
+__global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
+                          amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                    const __bf16* __restrict__ bias, const __bf16* __restrict__ R, int M, int N, int K,
                    long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
                    long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag = nullptr) {
-  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+  constexpr int BN = BM, WT = BM / 2, NR = WT / 16;    // wave tile WT x WT = NR x NR MFMA blocks
+  constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
+  constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
+  constexpr int MF = NR * NR;                            // MFMAs per wave per k32 substep
+  constexpr int DMA_EVERY = MF / PIECES;               // one DMA per DMA_EVERY MFMAs
+  static_assert(BM == 256 || BM == 128, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -79,7 +89,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   unsigned long long t_start = 0;
   if (DIAG) t_start = __builtin_amdgcn_s_memtime();
 
-  const int tiles_m = M / kBM, tiles_n = N / kBN, nwg = tiles_m * tiles_n;
+  const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
   constexpr int kGroupM = 4;
   const int per_group = kGroupM * tiles_n;
@@ -87,7 +97,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int gm = min(tiles_m - first_m, kGroupM);
   const int tm = first_m + (wg % per_group) % gm;
   const int tn = (wg % per_group) / gm;
-  const int m0 = tm * kBM, n0 = tn * kBN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const long long bz = blockIdx.y;
   A += bz * sa + (long long)m0 * lda;
@@ -105,7 +115,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // 8p..8p+7; lane i lands at LDS p*1024 + 16*i (row 8p + (i>>3), swizzled chunk (i&7)) and must
   // fetch global chunk (i&7) ^ ((row>>1)&7) = (i&7) ^ ((4*(j&1) + (i>>4)) & 7): two lane offsets
   // per operand (j even / odd); the row offset 8j*ld is wave-uniform (SGPR soffset).
-  const int lrow = wid * 64 + (lane >> 3);
+  const int lrow = wid * (BM / 4) + (lane >> 3);
   int va[2], vb[2];
 #pragma unroll
   for (int par = 0; par < 2; ++par) {
@@ -121,11 +131,11 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // concentrated DMA issue stalled the single MFMA wave per SIMD — w4_diag: +30..80 cycles per
   // DMA) and A gets 3, B 2 substeps of lookahead instead of 1.5.
   auto dma_a = [&](int kt, int slot, int j) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(smem + slot * kTileBytes + (wid * 8 + j) * 1024), 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
                                              va[j & 1], j * rowstep_a + kt * kBK * 2, 0, 0);
   };
   auto dma_b = [&](int kt, int slot, int j) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(smem + slot * kTileBytes + (wid * 8 + j) * 1024), 16,
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
                                              vb[j & 1], j * rowstep_b + kt * kBK * 2, 0, 0);
   };
 
@@ -133,37 +143,38 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int sw = lh ^ (lr >> 1);
   const int off0 = lr * 128 + (sw << 4);
   const int off1 = lr * 128 + ((sw ^ 4) << 4);
-  const int a_base = (wm * 128) * 128;
-  const int b_base = (wn * 128) * 128;
+  const int a_base = (wm * WT) * 128;
+  const int b_base = (wn * WT) * 128;
 
-  f32x4 acc[8][8];
+  f32x4 acc[NR][NR];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NR; ++i)
 #pragma unroll
-    for (int n = 0; n < 8; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NR; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  // fragment q of a set: q < 8 -> B fragment q, q >= 8 -> A fragment q-8
-  auto read_frag = [&](int sa_slot, int sb_slot, int off, bf16x8(&af)[8], bf16x8(&bf)[8], int q) {
-    if (q < 8) bf[q] = *reinterpret_cast<const bf16x8*>(smem + sb_slot * kTileBytes + b_base + q * 2048 + off);
-    else af[q - 8] = *reinterpret_cast<const bf16x8*>(smem + sa_slot * kTileBytes + a_base + (q - 8) * 2048 + off);
+  bf16x8 a0[NR], b0[NR], a1[NR], b1[NR];
+  // fragment q of a set: q < R -> B fragment q, q >= R -> A fragment q-R
+  auto read_frag = [&](int sa_slot, int sb_slot, int off, bf16x8(&af)[NR], bf16x8(&bf)[NR], int q) {
+    if (q < NR) bf[q] = *reinterpret_cast<const bf16x8*>(smem + sb_slot * TILE + b_base + q * 2048 + off);
+    else af[q - NR] = *reinterpret_cast<const bf16x8*>(smem + sa_slot * TILE + a_base + (q - NR) * 2048 + off);
   };
 
   const int nk = K / kBK;
   // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
   int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < PIECES; ++j) {
     dma_a(0, sa0, j);
     dma_b(0, sb0, j);
   }
   if (nk > 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < PIECES; ++j) {
       dma_a(1, sa1, j);
       dma_b(1, sb1, j);
     }
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -171,7 +182,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   __builtin_amdgcn_s_barrier();
   COMPILER_FENCE();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) read_frag(sa0, sb0, off0, a0, b0, q);
+  for (int q = 0; q < 2 * NR; ++q) read_frag(sa0, sb0, off0, a0, b0, q);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   PIN();
   __builtin_amdgcn_s_setprio(1);
@@ -197,18 +208,19 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
     const unsigned long long t0 = stamp();
     // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
 #pragma unroll
-    for (int m = 0; m < 64; ++m) {
-      if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 16) read_frag(sa0, sb0, off1, a1, b1, m / RG);
-      if (kStage && (m & 7) == 2) dma_a(kt + 2, sf, m >> 3);
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag(sa0, sb0, off1, a1, b1, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_a(kt + 2, sf, m / DMA_EVERY);
       PIN();
-      mfma(acc[m >> 3][m & 7], b0[m & 7], a0[m >> 3]);
+      mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
       PIN();
     }
     const unsigned long long t1 = stamp();
     // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
     // after it tile kt's slots are free
     if (kStage) {
-      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
+      if constexpr (BM == 256) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0074);                      // vmcnt(4) expcnt(7) lgkmcnt(0)
     } else {
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     }
@@ -219,11 +231,11 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
     const unsigned long long t2 = stamp();
     // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
 #pragma unroll
-    for (int m = 0; m < 64; ++m) {
-      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 16) read_frag(sa1, sb1, off0, a0, b0, m / RG);
-      if (kStage && (m & 7) == 2) dma_b(kt + 2, sa0, m >> 3);
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag(sa1, sb1, off0, a0, b0, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_b(kt + 2, sa0, m / DMA_EVERY);
       PIN();
-      mfma(acc[m >> 3][m & 7], b1[m & 7], a1[m >> 3]);
+      mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
       PIN();
     }
     const unsigned long long t3 = stamp();
@@ -266,7 +278,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // lh 3 -> block n+1 cols 8-15. Half the store instructions (dwordx4 instead of dwordx2), every
   // row segment 64 contiguous bytes; the tail is ~5 % of a block at 8192^3 (w4_diag epilogue stamps).
   auto finish = [&](int i, int n, int m) -> uint2 {
-    const int col = n0 + wn * 128 + n * 16 + lh * 4;
+    const int col = n0 + wn * WT + n * 16 + lh * 4;
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
@@ -291,11 +303,11 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   };
   const int swap_col = 16 * (lh & 1) + 8 * (lh >> 1);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + lr;
-    __bf16* crow = C + (long long)m * ldc + n0 + wn * 128 + swap_col;
+  for (int i = 0; i < NR; ++i) {
+    const int m = m0 + wm * WT + i * 16 + lr;
+    __bf16* crow = C + (long long)m * ldc + n0 + wn * WT + swap_col;
 #pragma unroll
-    for (int n = 0; n < 8; n += 2) {
+    for (int n = 0; n < NR; n += 2) {
       uint2 p = finish(i, n, m), q = finish(i, n + 1, m);
       const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
       const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
@@ -316,23 +328,24 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
 
 }  // namespace
 
-// Caller (kfamd_gemm_nt_bf16_variant) has validated shapes (M,N % 256, K % 64) and alignment;
-// the buffer offsets are 32-bit, so a block's 256-row panel must span < 2 GiB.
-extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
-                                            int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
-                                            long long ldr, long long sa, long long sb, long long sc, long long sr,
-                                            float alpha, int act, void* stream) {
-  if ((long long)kBM * lda * 2 >= (1LL << 31) || (long long)kBN * ldb * 2 >= (1LL << 31)) return KFAMD_EINVAL;
+namespace {
+template <int BM>
+int launch_w4(const void* A, const void* B, void* C, const void* bias, const void* R, int M, int N, int K, int batch,
+              long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb, long long sc,
+              long long sr, float alpha, int act, void* stream) {
+  if ((long long)BM * lda * 2 >= (1LL << 31) || (long long)BM * ldb * 2 >= (1LL << 31)) return KFAMD_EINVAL;
+  if (M % BM || N % BM || K % kBK) return KFAMD_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((M / kBM) * (N / kBN), batch), block(kThreads);
+  dim3 grid((M / BM) * (N / BM), batch), block(kThreads);
   const __bf16* a = static_cast<const __bf16*>(A);
   const __bf16* b = static_cast<const __bf16*>(B);
   __bf16* c = static_cast<__bf16*>(C);
   const __bf16* bs = static_cast<const __bf16*>(bias);
   const __bf16* r = static_cast<const __bf16*>(R);
   const bool hb = bias != nullptr, hr = R != nullptr;
-#define W4_LAUNCH(ACTV, HB, HR) \
-  hipLaunchKernelGGL((gemm_nt_256w4<ACTV, HB, HR>), grid, block, 0, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha)
+#define W4_LAUNCH(ACTV, HB, HR)                                                                                  \
+  hipLaunchKernelGGL((gemm_nt_256w4<ACTV, HB, HR, false, 2, 0, BM>), grid, block, 0, s, a, b, c, bs, r, M, N, K, lda, \
+                     ldb, ldc, ldr, sa, sb, sc, sr, alpha)
   switch (act) {
     case KFAMD_ACT_NONE:
       if (hb && hr) W4_LAUNCH(KFAMD_ACT_NONE, true, true);
@@ -358,6 +371,24 @@ extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* 
 #undef W4_LAUNCH
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+}  // namespace
+
+// Caller (kfamd_gemm_nt_bf16_variant) has validated alignment; shapes are re-checked per tile
+// size. The buffer offsets are 32-bit, so a block's BM-row panel must span < 2 GiB.
+extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
+                                            int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
+                                            long long ldr, long long sa, long long sb, long long sc, long long sr,
+                                            float alpha, int act, void* stream) {
+  return launch_w4<256>(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, act, stream);
+}
+
+// 128x128 tiles (two blocks per CU) for problems with fewer 256-tiles than CUs.
+extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
+                                             int M, int N, int K, int batch, long long lda, long long ldb,
+                                             long long ldc, long long ldr, long long sa, long long sb, long long sc,
+                                             long long sr, float alpha, int act, void* stream) {
+  return launch_w4<128>(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, act, stream);
 }
 
 // Diagnostic launch (no epilogue variants): per-wave K-loop segment cycle sums into diag

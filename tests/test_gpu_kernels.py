@@ -37,7 +37,7 @@ def test_native_library_loaded():
     assert "gfx950" in ops.build_info()
 
 
-@pytest.mark.parametrize("variant", ["fast", "pipe", "pipe_sched", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "pipe", "pipe_sched", "w4", "w4s", "auto"])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 256, 128), (512, 768, 192), (512, 768, 1024),
                                    (1024, 1024, 4096), (4096, 4096, 4096)])
 def test_gemm_fast_path(M, N, K, variant):
@@ -54,7 +54,7 @@ def test_gemm_identity_asymmetric():
     n = 256
     eye = torch.eye(n, device="cuda", dtype=torch.bfloat16)
     b = (torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
-    for v in ("fast", "pipe", "pipe_sched", "w4"):
+    for v in ("fast", "pipe", "pipe_sched", "w4", "w4s"):
         out = gemm_nt(eye, b, variant=v)  # = I @ b^T = b^T
         assert torch.equal(out.float(), b.float().t())
         out2 = gemm_nt(b, eye, variant=v)  # = b
@@ -70,7 +70,7 @@ def test_gemm_generic_path(M, N, K):
     _assert_close(out, _ref_gemm(a, b), K)
 
 
-@pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4", "w4s"])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
 def test_gemm_epilogue(variant, act):
     from kubeflow_rm_amd.ops import gemm_nt
@@ -80,7 +80,7 @@ def test_gemm_epilogue(variant, act):
     _assert_close(out, _ref_gemm(a, b, bias, act, alpha=0.5), K)
 
 
-@pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4", "w4s"])
 def test_gemm_residual_and_batch(variant):
     from kubeflow_rm_amd.ops import gemm_nt
     B, M, N, K = 3, 256, 512, 128
@@ -131,3 +131,21 @@ def test_rmsnorm(rows, H):
     xf = x.float()
     ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * w.float()
     assert (y.float() - ref).abs().max().item() < 3e-2
+
+
+def test_gemm_w4_needs_16b_output_rows():
+    """The w4 / w4s epilogues store 16 B per lane: an output with ldc % 8 != 0 is refused by the
+    explicit variants and routed to an 8-byte-store kernel by auto (same result)."""
+    from kubeflow_rm_amd.ops import NativeLibraryError, gemm_nt
+    M = N = K = 512
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    big = torch.zeros(M, N + 4, device="cuda", dtype=torch.bfloat16)
+    out = big[:, :N]
+    for v in ("w4", "w4s"):
+        with pytest.raises(NativeLibraryError):
+            gemm_nt(a, b, out=out, variant=v)
+    gemm_nt(a, b, out=out, variant="auto")
+    ref = (a.float() @ b.float().t())
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
+    assert torch.all(big[:, N:] == 0)  # nothing written past the row
