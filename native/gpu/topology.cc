@@ -81,6 +81,7 @@ GpuTopology GpuTopology::discover(const std::string& root) {
     d.kfd_node = node;
     d.simd_count = static_cast<int>(to_i(props, "simd_count"));
     d.xcc_count = static_cast<int>(to_i(props, "num_xcc", 1));
+    if (props.count("drm_render_minor")) d.drm_render_minor = static_cast<int>(to_i(props, "drm_render_minor"));
     int64_t gfx = to_i(props, "gfx_target_version");
     if (gfx) {
       char buf[32];

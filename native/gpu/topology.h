@@ -37,6 +37,7 @@ struct GpuDevice {
   int simd_count = 1024;  // 256 CUs x 4 SIMDs
   int xcc_count = 8;
   std::string pci_bus;
+  int drm_render_minor = -1;  // /sys/class/drm/renderD<minor>: amdgpu sysfs (VRAM use, busy %)
 };
 
 struct GpuTopology {

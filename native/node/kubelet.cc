@@ -287,6 +287,12 @@ void Kubelet::heartbeat_loop() {
 }
 
 void Kubelet::stop() {
+  if (metrics_registered_) {  // the collectors capture `this`
+    for (const char* n : {"kfamd_gpu_allocated", "kfamd_gpu_hbm_allocated_bytes", "kfamd_gpu_vram_used_bytes",
+                          "kfamd_gpu_vram_total_bytes", "kfamd_gpu_busy_percent"})
+      Registry::global().unregister(n);
+    metrics_registered_ = false;
+  }
   if (!running_.exchange(false)) return;
   if (hb_.joinable()) hb_.join();
   std::lock_guard<std::mutex> g(mu_);
@@ -984,7 +990,70 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   return Result::after(std::max(0.02, next_wake));
 }
 
+// GPU metrics (SURVEY §5.5 build additions), scraped from the kubelet's registry: which pod holds
+// which MI355X, HBM allocated per namespace (what amd.com/gpu-memory quota charges), and the live
+// amdgpu sysfs counters of every discovered GPU (VRAM used/total, busy %).
+void Kubelet::register_gpu_metrics() {
+  auto& reg = Registry::global();
+  reg.add_collector(std::make_shared<CollectorFamily>(
+      "kfamd_gpu_allocated", "1 for every MI355X allocated to a pod by the device plugin", "gauge",
+      std::vector<std::string>{"gpu", "namespace", "pod"}, [this]() {
+        std::vector<std::pair<Labels, double>> out;
+        const auto allocs = alloc_->allocations();
+        std::lock_guard<std::mutex> g(mu_);
+        for (const auto& a : allocs) {
+          auto it = pods_.find(a.first);
+          const std::string ns = it != pods_.end() ? it->second->ns : "", name = it != pods_.end() ? it->second->name : a.first;
+          for (int d : a.second) out.push_back({{std::to_string(d), ns, name}, 1.0});
+        }
+        return out;
+      }));
+  reg.add_collector(std::make_shared<CollectorFamily>(
+      "kfamd_gpu_hbm_allocated_bytes", "HBM of the MI355X GPUs allocated to pods, per namespace", "gauge",
+      std::vector<std::string>{"namespace"}, [this]() {
+        std::vector<std::pair<Labels, double>> out;
+        const auto allocs = alloc_->allocations();
+        const auto& topo = alloc_->topology();
+        std::map<std::string, double> per_ns;
+        std::lock_guard<std::mutex> g(mu_);
+        for (const auto& a : allocs) {
+          auto it = pods_.find(a.first);
+          const std::string ns = it != pods_.end() ? it->second->ns : "";
+          for (int d : a.second)
+            if (d >= 0 && d < topo.size()) per_ns[ns] += static_cast<double>(topo.gpus[d].hbm_bytes);
+        }
+        for (auto& kv : per_ns) out.push_back({{kv.first}, kv.second});
+        return out;
+      }));
+  struct SysfsMetric {
+    const char* name;
+    const char* help;
+    const char* file;
+  };
+  static const SysfsMetric kSysfs[] = {
+      {"kfamd_gpu_vram_used_bytes", "amdgpu mem_info_vram_used", "mem_info_vram_used"},
+      {"kfamd_gpu_vram_total_bytes", "amdgpu mem_info_vram_total", "mem_info_vram_total"},
+      {"kfamd_gpu_busy_percent", "amdgpu gpu_busy_percent", "gpu_busy_percent"},
+  };
+  for (const auto& m : kSysfs) {
+    const std::string file = m.file;
+    reg.add_collector(std::make_shared<CollectorFamily>(
+        m.name, m.help, "gauge", std::vector<std::string>{"gpu"}, [this, file]() {
+          std::vector<std::pair<Labels, double>> out;
+          for (const auto& g : alloc_->topology().gpus) {
+            if (g.drm_render_minor < 0) continue;
+            std::string v;
+            if (read_file("/sys/class/drm/renderD" + std::to_string(g.drm_render_minor) + "/device/" + file, v))
+              out.push_back({{std::to_string(g.index)}, std::atof(v.c_str())});
+          }
+          return out;
+        }));
+  }
+  metrics_registered_ = true;
+}
+
 void Kubelet::setup(Manager& mgr) {
+  register_gpu_metrics();
   ctl_ = std::make_shared<Controller>("kubelet", [this](const Request& r, std::string* e) { return reconcile(r, e); }, 4);
   const std::string node = cfg_.node_name;
   ctl_->For(mgr.informer("v1", "Pod"), [node](const std::string& type, const Json& p, const Json* old) {

@@ -98,6 +98,8 @@ class Kubelet {
  private:
   Json node_object() const;
   void heartbeat_loop();
+  void register_gpu_metrics();
+  bool metrics_registered_ = false;
   void terminate_pod(PodRuntime& rt, int64_t grace_s);
   std::shared_ptr<Client> c_;
   KubeletConfig cfg_;

@@ -94,6 +94,20 @@ def test_gpu_notebook_gets_xgmi_placement(c):
     assert env is not None
 
 
+def test_gpu_allocation_metrics(c, cluster):
+    """kubelet GPU metrics: which pod holds which MI355X, HBM allocated per namespace."""
+    pod = c.get("v1", "Pod", "gpu4-0", "e2e")
+    ids = set(pod["metadata"]["annotations"]["amd.com/gpu-ids"].split(","))
+    with urllib.request.urlopen(cluster.url + "/metrics", timeout=5) as r:
+        text = r.read().decode()
+    held = {line.split('gpu="')[1].split('"')[0] for line in text.splitlines()
+            if line.startswith("kfamd_gpu_allocated{") and 'pod="gpu4-0"' in line and 'namespace="e2e"' in line}
+    assert held == ids
+    hbm = [float(line.split()[-1]) for line in text.splitlines()
+           if line.startswith('kfamd_gpu_hbm_allocated_bytes{namespace="e2e"}')]
+    assert hbm and hbm[0] >= 4 * 288 * 2**30
+
+
 def test_gpu_oversubscription_is_unschedulable(c):
     c.create(_notebook("gpu16", "e2e", gpus=16))
 
