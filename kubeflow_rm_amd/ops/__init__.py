@@ -3,3 +3,4 @@ from ._lib import NativeLibraryError, available, build_info, lib  # noqa: F401
 from .gemm import flops, gemm_nt, linear, matmul  # noqa: F401
 from .layernorm import layer_norm, layer_norm_fwd, rms_norm  # noqa: F401
 from .allreduce import OneShotAllReduce  # noqa: F401
+from .graph import GraphedCallable  # noqa: F401
