@@ -177,3 +177,55 @@ extern "C" int kfamd_allreduce_oneshot(const void* const* inputs, void* const* o
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
+
+// ---- cross-process registration (one process per GPU, torch.distributed) ---------------------------
+// Buffers the peers map through HIP IPC (dmabuf on this platform: HSA_ENABLE_IPC_MODE_LEGACY=0).
+// Flags prefer uncached memory (a peer's atomic store is then seen without a cache flush); if the
+// driver cannot export such an allocation, plain device memory + the system-scope atomics/fences of
+// the kernel are used. The allocation is zeroed (flags must start at epoch 0).
+extern "C" int kfamd_ipc_alloc(long long bytes, int uncached, void** ptr, void* handle64) {
+  if (bytes <= 0 || !ptr || !handle64) return KFAMD_EINVAL;
+  *ptr = nullptr;
+  hipError_t e = hipErrorUnknown;
+  if (uncached) {
+    e = hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached);
+    if (e == hipSuccess && hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle64), *ptr) != hipSuccess) {
+      (void)hipFree(*ptr);
+      *ptr = nullptr;
+      e = hipErrorUnknown;
+    }
+  }
+  if (e != hipSuccess) {
+    e = hipMalloc(ptr, (size_t)bytes);
+    if (e != hipSuccess) return static_cast<int>(e);
+    e = hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle64), *ptr);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  e = hipMemset(*ptr, 0, (size_t)bytes);
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_ipc_open(const void* handle64, void** ptr) {
+  if (!handle64 || !ptr) return KFAMD_EINVAL;
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, handle64, sizeof h);
+  const hipError_t e = hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_ipc_close(void* ptr) {
+  const hipError_t e = hipIpcCloseMemHandle(ptr);
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_ipc_free(void* ptr) {
+  const hipError_t e = hipFree(ptr);
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+// Stream-ordered device-to-device copy into a registered buffer (the one-shot's input staging).
+extern "C" int kfamd_copy_async(void* dst, const void* src, long long bytes, void* stream) {
+  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice,
+                                      reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}

@@ -81,6 +81,13 @@ int kfamd_allreduce_oneshot(const void* const* inputs, void* const* outputs, uin
                             int nranks, int rank0, int launch_ranks, long long n, int dtype,
                             unsigned epoch, int nblocks, unsigned* timeout, void* stream);
 
+// HIP IPC registration for one-process-per-GPU ranks (64-byte handles exchanged by the caller).
+int kfamd_ipc_alloc(long long bytes, int uncached, void** ptr, void* handle64);
+int kfamd_ipc_open(const void* handle64, void** ptr);
+int kfamd_ipc_close(void* ptr);
+int kfamd_ipc_free(void* ptr);
+int kfamd_copy_async(void* dst, const void* src, long long bytes, void* stream);
+
 // Library identity (for the loud "native code loaded" check).
 const char* kfamd_build_info(void);
 

@@ -78,3 +78,40 @@ def test_oneshot_rejects_bad_arguments():
     assert L.kfamd_allreduce_oneshot(p, p, p, 2, 0, 2, 16, 0, 0, 1, tmo.data_ptr(), None) == -1  # epoch 0
     assert L.kfamd_allreduce_oneshot(arr(*([t.data_ptr() + 4] * 8)), p, p, 2, 0, 2, 16, 0, 1, 1,
                                      tmo.data_ptr(), None) == -2  # misaligned input
+
+
+def _ipc_worker(rank):
+    import torch.distributed as dist
+    from kubeflow_rm_amd.parallel.oneshot import IpcOneShotAllReduce
+    torch.cuda.set_device(0)  # the test box has one GPU: both ranks share it (IPC within a device)
+    dist.init_process_group("gloo")
+    world = dist.get_world_size()
+    ar = IpcOneShotAllReduce(max_bytes=1 << 20)
+    worst = 0.0
+    for dtype in (torch.float32, torch.bfloat16):
+        for it, n in enumerate((8, 1001, 65536, 200_000)):
+            def data(r):
+                g = torch.Generator(device="cuda").manual_seed(1000 * r + it)
+                return torch.randn(n, device="cuda", generator=g).to(dtype)
+            t = data(rank)
+            ar(t)
+            torch.cuda.synchronize()
+            ref = torch.zeros(n, device="cuda")
+            for r in range(world):
+                ref += data(r).float()
+            worst = max(worst, (t.float() - ref.to(dtype).float()).abs().max().item())
+    out = {"timed_out": ar.timed_out(), "worst": worst, "epochs": ar.epoch}
+    ar.close()
+    dist.destroy_process_group()
+    return out
+
+
+def test_ipc_oneshot_two_ranks_as_processes():
+    """torch.distributed ranks (separate processes) over HIP IPC-mapped buffers; on the 1-GPU box
+    both processes share the device, exercising registration, handle exchange and the barrier."""
+    from kubeflow_rm_amd.parallel.launch import spawn
+    res = spawn(_ipc_worker, 2, timeout=180)
+    for r in res:
+        assert r["timed_out"] is False, r
+        assert r["worst"] == 0.0, r
+        assert r["epochs"] == 8
