@@ -37,6 +37,26 @@ def _linear(x, w, b=None, act="none"):
     return y
 
 
+# Optional K3 fast path per TP group (kubeflow_rm_amd.parallel.oneshot): the row-parallel forward
+# all-reduce of a decode step is a few KB, where one one-shot kernel beats RCCL's ring steps.
+_FAST: dict = {}
+
+
+def enable_oneshot(group=None, max_bytes: int = 1 << 20):
+    """Route this group's TP all-reduces of <= max_bytes through the one-shot IPC kernel."""
+    from kubeflow_rm_amd.parallel.oneshot import IpcOneShotAllReduce
+    _FAST[group] = IpcOneShotAllReduce(group, max_bytes)
+    return _FAST[group]
+
+
+def _all_reduce(x, group):
+    fast = _FAST.get(group)
+    if fast is not None and x.is_cuda:
+        return fast.all_reduce(x)
+    dist.all_reduce(x, group=group)
+    return x
+
+
 def _world(group):
     return dist.get_world_size(group) if dist.is_initialized() else 1
 
@@ -54,8 +74,7 @@ class _CopyToTP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         if _world(ctx.group) > 1:
-            g = g.contiguous()
-            dist.all_reduce(g, group=ctx.group)
+            g = _all_reduce(g.contiguous(), ctx.group)
         return g, None
 
 
@@ -63,8 +82,7 @@ class _ReduceFromTP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
         if _world(group) > 1:
-            x = x.contiguous()
-            dist.all_reduce(x, group=group)
+            x = _all_reduce(x.contiguous(), group)
         return x
 
     @staticmethod

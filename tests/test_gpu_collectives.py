@@ -115,3 +115,32 @@ def test_ipc_oneshot_two_ranks_as_processes():
         assert r["timed_out"] is False, r
         assert r["worst"] == 0.0, r
         assert r["epochs"] == 8
+
+
+def _tp_oneshot_worker(rank):
+    import torch.distributed as dist
+    from kubeflow_rm_amd.models import GPT, GPTConfig
+    from kubeflow_rm_amd.parallel import tp as tpl
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    cfg = GPTConfig(vocab_size=512, d_model=256, n_layers=2, n_heads=4, d_ff=1024, max_seq=64)
+    torch.manual_seed(0)
+    idx = torch.randint(0, 512, (1, 32)).cuda()
+    model = GPT(cfg, tp_group=dist.group.WORLD, device="cuda").eval()
+    with torch.no_grad():
+        ref = model(idx).float().cpu()  # TP all-reduces through gloo
+        fast = tpl.enable_oneshot(dist.group.WORLD)
+        out = model(idx).float().cpu()  # the same all-reduces on the one-shot IPC kernel
+    torch.cuda.synchronize()
+    res = {"max_diff": (out - ref).abs().max().item(), "calls": fast.epoch, "timed_out": fast.timed_out()}
+    fast.close()
+    tpl._FAST.clear()
+    dist.destroy_process_group()
+    return res
+
+
+def test_tp_forward_on_oneshot_matches_reference_all_reduce():
+    from kubeflow_rm_amd.parallel.launch import spawn
+    for r in spawn(_tp_oneshot_worker, 2, timeout=180):
+        assert r["timed_out"] is False and r["calls"] >= 4, r  # 2 row-parallel reduces per block
+        assert r["max_diff"] == 0.0, r
