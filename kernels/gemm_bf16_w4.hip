@@ -86,8 +86,11 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  unsigned long long t_start = 0;
-  if (DIAG) t_start = __builtin_amdgcn_s_memtime();
+  unsigned long long t_start = 0, rt_start = 0;
+  if (DIAG) {
+    t_start = __builtin_amdgcn_s_memtime();
+    rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock: in-kernel clock + gaps
+  }
 
   const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -316,12 +319,21 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   }
   if (DIAG) {
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores retired: the block's real end
+    const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+    unsigned hw_id, xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
     if (lane == 0) {
-      unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 8;
+      unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 16;
       for (int j = 0; j < 4; ++j) d[j] = seg[j];
       d[4] = t_loop0 - t_start;  // prologue (address setup, first two tiles, F0(0))
       d[5] = t_end - t_loop1;    // epilogue (stores issued)
       d[6] = t_loop1 - t_loop0;  // K loop
+      d[7] = t_end - t_start;    // shader clocks, whole block (to the last store issue)
+      d[8] = rt_start;           // 100 MHz realtime at block start / end (stores retired)
+      d[9] = rt_end;
+      d[10] = ((unsigned long long)(xcc_id & 0xf) << 32) | hw_id;  // which CU ran the block
     }
   }
 }

@@ -26,7 +26,7 @@ def main():
         b = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
         c = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
         nblk = (s // 256) ** 2
-        diag = torch.zeros(nblk * 4 * 8, dtype=torch.int64, device=dev)
+        diag = torch.zeros(nblk * 4 * 16, dtype=torch.int64, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
         abl_cycles = {}
         for abl in (1, 2, 0):
@@ -34,9 +34,33 @@ def main():
                 rc = f(a.data_ptr(), b.data_ptr(), c.data_ptr(), s, s, s, diag.data_ptr(), abl, stream)
                 assert rc == 0, rc
             torch.cuda.synchronize()
-            d8 = diag.view(nblk, 4, 8).double()
+            d8 = diag.view(nblk, 4, 16).double()
+            draw = diag.view(nblk, 4, 16)
             d = d8[..., :4]
             abl_cycles[abl] = round(d.sum(-1).mean().item() / (s // 64))
+        # in-kernel clock (MHz) = shader clocks / realtime ticks * 100, per block (wave 0)
+        w0 = draw[:, 0, :]
+        rt = (w0[:, 9] - w0[:, 8]).double()
+        clk_mhz = (w0[:, 7].double() / rt.clamp(min=1) * 100.0)
+        # per-CU timeline: gaps between consecutive blocks on the same CU (realtime ticks = 10 ns)
+        hw = w0[:, 10]
+        cu_key = ((hw >> 32) & 0xF) * 8192 + ((hw >> 13) & 0x7) * 1024 + ((hw >> 12) & 1) * 512 + ((hw >> 8) & 0xF)
+        starts, ends = w0[:, 8], w0[:, 9]
+        gaps, blocks_per_cu = [], []
+        t_first, t_last = starts.min().item(), ends.max().item()
+        for key in torch.unique(cu_key).tolist():
+            sel = (cu_key == key).nonzero().flatten()
+            order = sel[torch.argsort(starts[sel])]
+            blocks_per_cu.append(len(order))
+            for a_, b_ in zip(order[:-1].tolist(), order[1:].tolist()):
+                gaps.append((starts[b_] - ends[a_]).item() * 10.0)  # ns
+        gaps_t = torch.tensor(gaps, dtype=torch.float64) if gaps else torch.zeros(1, dtype=torch.float64)
+        timeline = {"cus_used": len(blocks_per_cu), "blocks_per_cu_max": max(blocks_per_cu),
+                    "inter_block_gap_ns_median": round(gaps_t.median().item(), 1),
+                    "inter_block_gap_ns_mean": round(gaps_t.mean().item(), 1),
+                    "kernel_span_us": round((t_last - t_first) * 0.01, 1),
+                    "block_us_median": round((ends - starts).double().median().item() * 0.01, 2),
+                    "clock_MHz_median": round(clk_mhz.median().item(), 1)}
         tot = d.sum(-1, keepdim=True)
         share = (d / tot).mean(dim=(0, 1)).tolist()
         cyc = d.mean(dim=(0, 1)).tolist()
@@ -56,6 +80,7 @@ def main():
                           "loop_cycles_per_ktile": round(sum(cyc) / (s // 64)),
                           "prologue_cycles": round(d8[..., 4].mean().item()), "epilogue_issue_cycles": round(d8[..., 5].mean().item()),
                           "kloop_cycles": round(d8[..., 6].mean().item()),
+                          "block_cycles": round(d8[..., 7].mean().item()), "timeline": timeline,
                           "ablation_loop_cycles_per_ktile": {"no_dma": abl_cycles[1], "no_ds_read": abl_cycles[2],
                                                              "full": abl_cycles[0]}}), flush=True)
 
