@@ -1,5 +1,6 @@
 // Volumes web app frontend: PVC list (polled) with the notebooks using each one, create / delete,
-// and the PVCViewer (file browser) lifecycle: browse -> create viewer -> open its URL when ready.
+// volume details (overview / events / pods using it / YAML) and the PVCViewer (file browser)
+// lifecycle: browse -> create viewer -> open its URL when ready.
 (function () {
   "use strict";
   const $ = (id) => document.getElementById(id);
@@ -16,14 +17,41 @@
     try { await kf.call(method, path, body); $("error").textContent = ""; } catch (e) { $("error").textContent = e.message; }
     poller.reset();
   }
+  // volume page: overview / events / pods / YAML (VWA frontend pages/volume-details-page)
+  function showDetails(ns, name) {
+    const base = `/api/namespaces/${ns}/pvcs/${name}`;
+    const e = kf.esc;
+    return kf.details(`Volume ${ns}/${name}`, [
+      { name: "Overview", render: async () => {
+        const pvc = (await kf.call("GET", base)).pvc;
+        const spec = pvc.spec || {}, st = pvc.status || {};
+        return kf.kvTable([
+          ["Name", pvc.metadata.name], ["Namespace", pvc.metadata.namespace], ["Created", pvc.metadata.creationTimestamp],
+          ["Phase", st.phase || "-"], ["Requested", ((spec.resources || {}).requests || {}).storage || "-"],
+          ["Capacity", (st.capacity || {}).storage || "-"], ["Access modes", (spec.accessModes || []).join(", ")],
+          ["Storage class", spec.storageClassName || "(default)"], ["Volume", spec.volumeName || "-"],
+        ]);
+      } },
+      { name: "Events", render: async () => kf.eventsTable((await kf.call("GET", `${base}/events`)).events) },
+      { name: "Pods", render: async () => {
+        const pods = (await kf.call("GET", `${base}/pods`)).pods;
+        if (!pods.length) return '<p class="muted">Not mounted by any pod.</p>';
+        return kf.kvTable(pods.map((p) => [p.metadata.name, `${(p.status || {}).phase || ""} on ${(p.spec || {}).nodeName || "-"}`]));
+      } },
+      { name: "YAML", render: async () => `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).pvc))}</pre>` },
+    ]);
+  }
+
   async function refresh() {
     const ns = kf.namespace();
     if (!ns) return null;
     const { pvcs } = await kf.call("GET", `/api/namespaces/${ns}/pvcs`);
     $("rows").querySelector("tbody").replaceChildren(...pvcs.map((p) => {
       const tr = kf.h("tr", {});
-      tr.innerHTML = `<td>${kf.statusCell(p.status)}</td><td>${p.name}</td><td>${p.age}</td><td>${p.capacity}</td>
-        <td>${(p.modes || []).join(", ")}</td><td>${p.class || ""}</td><td>${p.notebooks.join(", ")}</td>`;
+      const e = kf.esc;
+      tr.innerHTML = `<td>${kf.statusCell(p.status)}</td><td><a class="name">${e(p.name)}</a></td><td>${e(p.age)}</td><td>${e(p.capacity)}</td>
+        <td>${e((p.modes || []).join(", "))}</td><td>${e(p.class || "")}</td><td>${e(p.notebooks.join(", "))}</td>`;
+      tr.querySelector("a.name").addEventListener("click", () => showDetails(ns, p.name));
       const v = p.viewer || {};
       const browse = kf.h("button", { onclick: () => (v.status === "ready" && v.url ? window.open(v.url)
         : v.status === "uninitialized" ? act("POST", `/api/namespaces/${ns}/viewers`, { name: p.name }) : null) },
