@@ -224,6 +224,10 @@ AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o) {
             {"args", args},
             {"resources", Json{{"limits", Json{{GPU_RESOURCE, std::to_string(gpus)}}}}},
             {"terminationMessagePolicy", "FallbackToLogsOnError"}};
+    // kfamd.io/gpu-readiness-profile: "true" -> the op runs itself under rocprofv3 and reports the
+    // per-kernel stats with its result (Notebook status.gpuReadiness.rocprof_top)
+    if (annotation(pod, "kfamd.io/gpu-readiness-profile") == "true")
+      ic["env"] = Json::array({Json{{"name", "KFAMD_READINESS_PROFILE"}, {"value", "1"}}});
     Json& ics = pod["spec"]["initContainers"];
     Json out = Json::array({ic});
     for (const auto& x : ics.as_array()) out.push_back(x);

@@ -12,6 +12,10 @@
 //      peer all-reduce (kernels/allreduce_oneshot.hip) over the same devices for the
 //      latency-bound sizes (8 B .. 256 KiB), verified and timed next to RCCL.
 //      --oneshot-sim N runs the one-shot kernel with N ranks simulated on device 0 (1-GPU boxes).
+//   5. KFAMD_READINESS_PROFILE=1 (pod annotation kfamd.io/gpu-readiness-profile: "true"): before
+//      touching the GPU the op re-runs itself as a CHILD under `rocprofv3 --kernel-trace --stats`
+//      (never exec: the profiler initialises the GPU), then merges the per-kernel summary of the
+//      rocprofv3 kernel_stats.csv into its JSON / termination message.
 // The JSON result goes to stdout and to $KFAMD_TERMINATION_LOG (the pod's termination message,
 // mirrored into the Notebook status by the notebook controller). Exit code != 0 fails the pod's
 // initialisation (pod not Ready -> Notebook status shows the failure).
@@ -22,8 +26,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dirent.h>
 #include <execinfo.h>
 #include <signal.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -285,7 +293,7 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
     Json row = Json::array();
     for (int j = 0; j < ndev; ++j) {
       int can = 0;
-      if (i != j) hipDeviceCanAccessPeer(&can, i, j);
+      if (i != j) (void)hipDeviceCanAccessPeer(&can, i, j);
       row.push_back(i == j ? 1 : can);
     }
     peer.push_back(row);
@@ -449,7 +457,174 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
 
 }  // namespace
 
+extern "C" char** environ;
+
+namespace {
+// ---- rocprofv3 wrapper (profile mode) ------------------------------------------------------------
+
+std::string find_file(const std::string& dir, const std::string& suffix) {
+  DIR* d = ::opendir(dir.c_str());
+  if (!d) return "";
+  std::string found;
+  while (dirent* e = ::readdir(d)) {
+    const std::string n = e->d_name;
+    if (n == "." || n == "..") continue;
+    const std::string p = dir + "/" + n;
+    struct stat st {};
+    if (::stat(p.c_str(), &st) != 0) continue;
+    if (S_ISDIR(st.st_mode)) {
+      found = find_file(p, suffix);
+    } else if (n.size() >= suffix.size() && n.compare(n.size() - suffix.size(), suffix.size(), suffix) == 0) {
+      found = p;
+    }
+    if (!found.empty()) break;
+  }
+  ::closedir(d);
+  return found;
+}
+
+// one CSV line -> fields ("..." quoting with "" escapes; kernel names contain commas)
+std::vector<std::string> csv_fields(const std::string& line) {
+  std::vector<std::string> out;
+  std::string cur;
+  bool q = false;
+  for (size_t i = 0; i < line.size(); ++i) {
+    const char c = line[i];
+    if (q) {
+      if (c == '"' && i + 1 < line.size() && line[i + 1] == '"') cur += '"', ++i;
+      else if (c == '"') q = false;
+      else cur += c;
+    } else if (c == '"') {
+      q = true;
+    } else if (c == ',') {
+      out.push_back(cur);
+      cur.clear();
+    } else if (c != '\r') {
+      cur += c;
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+Json kernel_stats_summary(const std::string& csv_path, size_t top) {
+  Json rows = Json::array();
+  FILE* f = std::fopen(csv_path.c_str(), "r");
+  if (!f) return rows;
+  char buf[1 << 16];
+  std::vector<std::string> hdr;
+  while (std::fgets(buf, sizeof buf, f)) {
+    std::string line(buf);
+    while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+    auto fl = csv_fields(line);
+    if (hdr.empty()) {
+      hdr = fl;
+      continue;
+    }
+    Json r = Json::object();
+    for (size_t i = 0; i < hdr.size() && i < fl.size(); ++i) {
+      if (hdr[i] == "Name") {
+        std::string n = fl[i];
+        if (n.size() > 96) n = n.substr(0, 96) + "...";
+        r["kernel"] = n;
+      } else if (hdr[i] == "Calls") {
+        r["calls"] = std::atoll(fl[i].c_str());
+      } else if (hdr[i] == "AverageNs") {
+        r["avg_us"] = std::atof(fl[i].c_str()) / 1000.0;
+      } else if (hdr[i] == "Percentage") {
+        r["pct"] = std::atof(fl[i].c_str());
+      }
+    }
+    if (r.has("kernel") && rows.size() < top) rows.push_back(r);
+  }
+  std::fclose(f);
+  return rows;
+}
+
+// Runs argv[0] again under rocprofv3 as a child, merges the kernel stats into its report.
+int run_profiled(int argc, char** argv) {
+  std::string prof = "/opt/rocm/bin/rocprofv3";
+  if (::access(prof.c_str(), X_OK) != 0) {
+    std::fprintf(stderr, "profile mode: rocprofv3 not found, running unprofiled\n");
+    return -1;
+  }
+  char exe[4096];
+  const ssize_t n = ::readlink("/proc/self/exe", exe, sizeof exe - 1);
+  if (n <= 0) return -1;
+  exe[n] = 0;
+  const char* pdir = std::getenv("KFAMD_PROFILE_DIR");
+  const std::string dir = pdir && *pdir ? pdir : "/tmp/kfamd-readiness-prof-" + std::to_string(::getpid());
+  const std::string child_log = dir + "/child-termination.json";
+  ::mkdir(dir.c_str(), 0755);
+  std::vector<std::string> args = {prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", dir + "/out",
+                                   "-o", "readiness", "--", exe};
+  for (int i = 1; i < argc; ++i) args.push_back(argv[i]);
+  std::vector<char*> av;
+  for (auto& s : args) av.push_back(&s[0]);
+  av.push_back(nullptr);
+  std::vector<std::string> envs;
+  for (char** e = environ; *e; ++e) {
+    const std::string kv = *e;
+    if (kv.rfind("KFAMD_TERMINATION_LOG=", 0) == 0 || kv.rfind("TMPDIR=", 0) == 0) continue;
+    envs.push_back(kv);
+  }
+  envs.push_back("KFAMD_READINESS_CHILD=1");
+  envs.push_back("KFAMD_TERMINATION_LOG=" + child_log);
+  envs.push_back("TMPDIR=/tmp");
+  std::vector<char*> ev;
+  for (auto& s : envs) ev.push_back(&s[0]);
+  ev.push_back(nullptr);
+  pid_t pid = 0;
+  if (::posix_spawn(&pid, prof.c_str(), nullptr, nullptr, av.data(), ev.data()) != 0) return -1;
+  int status = 0;
+  ::waitpid(pid, &status, 0);
+  const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+  Json brief = Json::object();
+  std::string text;
+  if (FILE* f = std::fopen(child_log.c_str(), "r")) {
+    char b[8192];
+    size_t m = std::fread(b, 1, sizeof b, f);
+    std::fclose(f);
+    text.assign(b, m);
+  }
+  if (!Json::try_parse(text, brief)) brief = Json{{"ok", false}, {"error", "readiness child left no report (exit " + std::to_string(code) + ")"}};
+  const std::string csv = find_file(dir + "/out", "kernel_stats.csv");
+  Json stats = kernel_stats_summary(csv, 6);
+  Json report = brief;
+  report["rocprof"] = Json{{"kernel_stats", stats}, {"dir", dir}, {"exit", code}};
+  std::printf("%s\n", report.dump().c_str());
+  if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
+    // 4 KiB cap: keep the three heaviest kernels
+    Json small = brief;
+    Json top = Json::array();
+    for (size_t i = 0; i < stats.size() && i < 3; ++i) top.push_back(stats[i]);
+    small["rocprof_top"] = top;
+    if (FILE* f = std::fopen(tl, "w")) {
+      std::fputs(small.dump().c_str(), f);
+      std::fclose(f);
+    }
+  }
+  return code;
+}
+
+int readiness_main(int argc, char** argv);
+
+}  // namespace
+
 int main(int argc, char** argv) {
+  {
+    const char* prof = std::getenv("KFAMD_READINESS_PROFILE");
+    const char* child = std::getenv("KFAMD_READINESS_CHILD");
+    if (prof && std::string(prof) == "1" && !child) {
+      const int rc = run_profiled(argc, argv);  // before any HIP call in this process
+      if (rc >= 0) return rc;
+    }
+  }
+  return readiness_main(argc, argv);
+}
+
+namespace {
+int readiness_main(int argc, char** argv) {
   ::signal(SIGSEGV, on_fatal);
   ::signal(SIGBUS, on_fatal);
   ::signal(SIGABRT, on_fatal);
@@ -546,3 +721,5 @@ int main(int argc, char** argv) {
   }
   return g_error.empty() ? 0 : 1;
 }
+
+}  // namespace

@@ -116,8 +116,17 @@ def test_gpu_readiness_injected_for_gpu_notebooks(native):
     ic = out["spec"]["initContainers"][0]
     assert ic["name"] == "gpu-readiness" and ic["command"] == ["kfamd-readiness"]
     assert ic["resources"]["limits"]["amd.com/gpu"] == "2"
+    assert "env" not in ic
     # idempotent
     assert native.call("gpu_readiness_mutate", pod=out)["spec"]["initContainers"] == out["spec"]["initContainers"]
+
+
+def test_gpu_readiness_profile_annotation_enables_rocprof(native):
+    """kfamd.io/gpu-readiness-profile: the op re-runs itself under rocprofv3 (SURVEY CS6 counters)."""
+    pod = {"metadata": {"labels": {"notebook-name": "nb"}, "annotations": {"kfamd.io/gpu-readiness-profile": "true"}},
+           "spec": {"containers": [{"name": "nb", "image": "x", "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+    ic = native.call("gpu_readiness_mutate", pod=pod)["spec"]["initContainers"][0]
+    assert {"name": "KFAMD_READINESS_PROFILE", "value": "1"} in ic["env"]
 
 
 @pytest.mark.parametrize("pod", [
