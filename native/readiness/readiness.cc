@@ -554,7 +554,7 @@ int run_profiled(int argc, char** argv) {
   exe[n] = 0;
   const char* pdir = std::getenv("KFAMD_PROFILE_DIR");
   const std::string dir = pdir && *pdir ? pdir : "/tmp/kfamd-readiness-prof-" + std::to_string(::getpid());
-  const std::string child_log = dir + "/child-termination.json";
+  const std::string child_log = dir + "/child-termination.json", child_report = dir + "/child-report.json";
   ::mkdir(dir.c_str(), 0755);
   std::vector<std::string> args = {prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", dir + "/out",
                                    "-o", "readiness", "--", exe};
@@ -570,6 +570,7 @@ int run_profiled(int argc, char** argv) {
   }
   envs.push_back("KFAMD_READINESS_CHILD=1");
   envs.push_back("KFAMD_TERMINATION_LOG=" + child_log);
+  envs.push_back("KFAMD_READINESS_REPORT=" + child_report);
   envs.push_back("TMPDIR=/tmp");
   std::vector<char*> ev;
   for (auto& s : envs) ev.push_back(&s[0]);
@@ -579,18 +580,23 @@ int run_profiled(int argc, char** argv) {
   int status = 0;
   ::waitpid(pid, &status, 0);
   const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
-  Json brief = Json::object();
-  std::string text;
-  if (FILE* f = std::fopen(child_log.c_str(), "r")) {
-    char b[8192];
-    size_t m = std::fread(b, 1, sizeof b, f);
-    std::fclose(f);
-    text.assign(b, m);
-  }
-  if (!Json::try_parse(text, brief)) brief = Json{{"ok", false}, {"error", "readiness child left no report (exit " + std::to_string(code) + ")"}};
+  auto slurp = [](const std::string& path) {
+    std::string text;
+    if (FILE* f = std::fopen(path.c_str(), "r")) {
+      char b[65536];
+      size_t m;
+      while ((m = std::fread(b, 1, sizeof b, f)) > 0) text.append(b, m);
+      std::fclose(f);
+    }
+    return text;
+  };
+  Json brief = Json::object(), full = Json::object();
+  if (!Json::try_parse(slurp(child_log), brief))
+    brief = Json{{"ok", false}, {"error", "readiness child left no report (exit " + std::to_string(code) + ")"}};
+  if (!Json::try_parse(slurp(child_report), full)) full = brief;
   const std::string csv = find_file(dir + "/out", "kernel_stats.csv");
   Json stats = kernel_stats_summary(csv, 6);
-  Json report = brief;
+  Json report = full;
   report["rocprof"] = Json{{"kernel_stats", stats}, {"dir", dir}, {"exit", code}};
   std::printf("%s\n", report.dump().c_str());
   if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
@@ -701,7 +707,14 @@ int readiness_main(int argc, char** argv) {
   g_result["total_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   g_result["kernels"] = kfamd_build_info();
   const std::string text = g_result.dump();
-  std::printf("%s\n", text.c_str());
+  const char* report_path = std::getenv("KFAMD_READINESS_REPORT");  // profile-mode child: to the parent
+  FILE* rf = report_path ? std::fopen(report_path, "w") : nullptr;
+  if (rf) {
+    std::fputs(text.c_str(), rf);
+    std::fclose(rf);
+  } else {
+    std::printf("%s\n", text.c_str());
+  }
   if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
     // the termination message is capped at 4 KiB like Kubernetes'; keep the summary fields first
     Json brief = Json{{"ok", g_result["ok"]}, {"gemm_tflops_aggregate", g_result["gemm_tflops_aggregate"]},
