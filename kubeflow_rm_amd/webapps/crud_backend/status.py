@@ -1,7 +1,12 @@
-"""Status phases the frontends understand (crud_backend/status.py contract)."""
+"""Status vocabulary shared by the backends and the frontends' status icons.
+
+Every list row carries ``status = {phase, message, state}``; ``phase`` is one of the names below
+(the frontends map them to icons: kf.js ``statusCell``).
+"""
+import enum
 
 
-class STATUS_PHASE:
+class Phase(str, enum.Enum):
     READY = "ready"
     WAITING = "waiting"
     WARNING = "warning"
@@ -12,5 +17,9 @@ class STATUS_PHASE:
     STOPPED = "stopped"
 
 
+# attribute-style access used by the app modules (STATUS_PHASE.READY == "ready")
+STATUS_PHASE = type("STATUS_PHASE", (), {p.name: p.value for p in Phase})
+
+
 def create_status(phase: str = "", message: str = "", state: str = "") -> dict:
-    return {"phase": phase, "message": message, "state": state}
+    return dict(phase=str(phase), message=message, state=state)

@@ -98,9 +98,8 @@ def create_app(cfg: config.Config | None = None):
             raise exceptions.BadRequest("Request body is missing the 'name' field")
         body.setdefault("namespace", namespace)
         user = authn.get_username()
-        nb = helpers.load_param_yaml(utils.NOTEBOOK_TEMPLATE_YAML, name=body["name"], namespace=namespace,
-                                     serviceAccount="default-editor",
-                                     creator=user if user is not None else "anonymous@kubeflow.org")
+        nb = utils.new_notebook(body["name"], namespace, service_account="default-editor",
+                                creator=user if user is not None else "anonymous@kubeflow.org")
         defaults = utils.load_spawner_ui_config()
         for setter in (form.set_notebook_image, form.set_notebook_image_pull_policy, form.set_server_type,
                        form.set_notebook_cpu, form.set_notebook_memory, form.set_notebook_gpus,

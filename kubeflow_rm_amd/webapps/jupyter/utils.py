@@ -16,7 +16,6 @@ from . import status
 
 log = logging.getLogger(__name__)
 HERE = os.path.abspath(os.path.dirname(__file__))
-NOTEBOOK_TEMPLATE_YAML = os.path.join(HERE, "yaml", "notebook_template.yaml")
 DEV_CONFIG = os.path.join(HERE, "yaml", "spawner_ui_config.yaml")
 CONFIGS = ["/etc/config/spawner_ui_config.yaml", DEV_CONFIG]
 LAST_ACTIVITY_ANNOTATION = "notebooks.kubeflow.org/last-activity"
@@ -24,6 +23,19 @@ LAST_ACTIVITY_ANNOTATION = "notebooks.kubeflow.org/last-activity"
 _cfg_lock = threading.Lock()
 _cfg_cache: tuple[float, dict] | None = None
 CONFIG_TTL_S = 60.0
+
+
+def new_notebook(name: str, namespace: str, service_account: str, creator: str) -> dict:
+    """The Notebook the spawner form is applied to (reference: the JWA notebook_template.yaml):
+    served version v1beta1, one container named after the notebook, minimal requests the form
+    overrides, creator + empty server-type annotations, ``app`` label."""
+    container = {"name": name, "image": "", "env": [], "volumeMounts": [],
+                 "resources": {"requests": {"cpu": "0.1", "memory": "0.1Gi"}}}
+    pod_spec = {"serviceAccountName": service_account, "containers": [container], "volumes": [], "tolerations": []}
+    meta = {"name": name, "namespace": namespace, "labels": {"app": name},
+            "annotations": {"notebooks.kubeflow.org/server-type": "", "notebooks.kubeflow.org/creator": creator}}
+    return {"apiVersion": "kubeflow.org/v1beta1", "kind": "Notebook", "metadata": meta,
+            "spec": {"template": {"spec": pod_spec}}}
 
 
 def random_string(size=9, chars=string.ascii_lowercase + string.digits) -> str:
