@@ -34,6 +34,8 @@ def parse_args():
     p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "3")),
                    help="notebook cold-start runs through the native control plane (rank 0)")
     p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
+    p.add_argument("--no-allreduce-sweep", action="store_true",
+                   help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
     return p.parse_args()
 
 
@@ -96,6 +98,17 @@ def main() -> int:
     value = per_gpu_tflops * world
 
     extra = {}
+    if world > 1 and not args.no_allreduce_sweep:
+        # BASELINE §3 "RCCL all-reduce busbw over xGMI" on the same N GPUs, outside the timed GEMM
+        # region (every rank participates; rank 0 reports)
+        try:
+            from kubeflow_rm_amd.parallel.collectives import allreduce_sweep
+            sw = allreduce_sweep(max_bytes=256 << 20, min_bytes=8 << 10, step=16, iters_small=20, iters_large=5,
+                                 device=dev)
+            extra["rccl_allreduce_fp32"] = [{"bytes": r["bytes"], "us": round(r["us"], 1),
+                                             "busbw_GBps": round(r["busbw_GBps"], 1)} for r in sw]
+        except Exception as e:  # reported, never fatal for the GEMM number
+            extra["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
     if args.compare_torch and rank == 0:
         for _ in range(5):
             torch.matmul(a, b.t())
