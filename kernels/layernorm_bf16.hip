@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   float v[VPL][8];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
-    const bf16x8 t = xr[j * 64 + lane];
+    // streamed once: non-temporal (no L2/MALL allocation for data nobody re-reads)
+    const bf16x8 t = __builtin_nontemporal_load(&xr[j * 64 + lane]);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[j][e] = (float)t[e];
   }
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
       if (!RMS && beta) r += (float)b[e];
       o[e] = (__bf16)r;
     }
-    yr[j * 64 + lane] = o;
+    __builtin_nontemporal_store(o, &yr[j * 64 + lane]);
   }
 }
 
