@@ -218,6 +218,9 @@ AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o) {
       if (ic["name"].as_string() == "gpu-readiness") return {};
     Json args = Json::array();
     for (const auto& s : o.args) args.push_back(s);
+    // kfamd.io/gpu-readiness-args: extra op flags, e.g. "--min-tflops 1200" (fail a notebook whose
+    // GPU underperforms) or "--inject-fault gemm" (fault-injection drills)
+    for (const auto& s : split(annotation(pod, "kfamd.io/gpu-readiness-args"), ' ', true)) args.push_back(s);
     Json ic{{"name", "gpu-readiness"},
             {"image", o.image},
             {"command", Json::array({"kfamd-readiness"})},

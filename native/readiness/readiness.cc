@@ -119,6 +119,7 @@ struct Args {
   double min_tflops = 0;
   bool skip_ln = false, skip_ar = false;
   int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
+  std::string inject_fault;  // fault injection: fail the op at this stage
 };
 
 bool gemm_check(int dev, const Args& a, Json& out) {
@@ -654,6 +655,7 @@ int readiness_main(int argc, char** argv) {
     else if (s == "--skip-ln") a.skip_ln = true;
     else if (s == "--skip-allreduce") a.skip_ar = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
+    else if (const char* v = val("--inject-fault")) a.inject_fault = v;
   }
   auto t0 = std::chrono::steady_clock::now();
   g_stage = "hip-init";
@@ -661,6 +663,7 @@ int readiness_main(int argc, char** argv) {
   hipError_t e = hipGetDeviceCount(&ndev);
   double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   g_result["hip_init_ms"] = init_ms;
+  if (!a.inject_fault.empty()) fail("injected fault at stage " + a.inject_fault + " (--inject-fault)");
   const char* sim = std::getenv("KFAMD_SIMULATED_GPUS");
   if (const char* vis = std::getenv("HIP_VISIBLE_DEVICES")) g_result["visible_devices"] = vis;
   if ((e != hipSuccess || ndev == 0) && sim && std::string(sim) == "1") {

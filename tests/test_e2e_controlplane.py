@@ -108,6 +108,23 @@ def test_gpu_allocation_metrics(c, cluster):
     assert hbm and hbm[0] >= 4 * 288 * 2**30
 
 
+def test_gpu_readiness_failure_surfaces_on_notebook(c):
+    """a GPU-side fault in the readiness op -> pod not Ready -> the Notebook status
+    carries the op's error (fault injected through kfamd.io/gpu-readiness-args)."""
+    c.create(_notebook("faulty", "e2e", gpus=1, annotations={"kfamd.io/gpu-readiness-args": "--inject-fault gemm"}))
+
+    def failed(o):
+        g = (o.get("status") or {}).get("gpuReadiness") or {}
+        return g.get("ok") is False
+    nb = c.wait_for(NB, "Notebook", "faulty", "e2e", failed, timeout=30)
+    assert "injected fault at stage gemm" in nb["status"]["gpuReadiness"]["error"]
+    assert not (nb["status"] or {}).get("readyReplicas")
+    pod = c.get("v1", "Pod", "faulty-0", "e2e")
+    ready = [x for x in pod["status"]["conditions"] if x["type"] == "Ready"][0]
+    assert ready["status"] == "False"
+    c.delete(NB, "Notebook", "faulty", "e2e")
+
+
 def test_gpu_oversubscription_is_unschedulable(c):
     c.create(_notebook("gpu16", "e2e", gpus=16))
 
