@@ -134,7 +134,7 @@
     const ns = kf.namespace();
     const { poddefaults } = await kf.call("GET", `/api/namespaces/${ns}/poddefaults`);
     $("f-configs").innerHTML = poddefaults.map((pd) =>
-      `<label class="muted"><input type="checkbox" value="${pd.label}"> ${pd.desc}</label><br>`).join("") || '<span class="muted">none</span>';
+      `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("") || '<span class="muted">none</span>';
     let pvcs = [];
     try { pvcs = (await kf.call("GET", `/api/namespaces/${ns}/pvcs`)).pvcs; } catch (e) { /* optional */ }
     $("f-datavols").replaceChildren();

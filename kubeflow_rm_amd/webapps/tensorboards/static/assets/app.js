@@ -18,7 +18,7 @@
     const { tensorboards } = await kf.call("GET", `/api/namespaces/${ns}/tensorboards`);
     $("rows").querySelector("tbody").replaceChildren(...tensorboards.map((tb) => {
       const tr = kf.h("tr", {});
-      tr.innerHTML = `<td>${kf.statusCell(tb.status)}</td><td>${tb.name}</td><td>${tb.logspath}</td><td>${tb.age}</td>`;
+      tr.innerHTML = `<td>${kf.statusCell(tb.status)}</td><td>${kf.esc(tb.name)}</td><td>${kf.esc(tb.logspath)}</td><td>${kf.esc(tb.age)}</td>`;
       const connect = kf.h("button", { onclick: () => window.open(`/tensorboard/${ns}/${tb.name}/`) }, "Connect");
       connect.disabled = tb.status.phase !== "ready";
       tr.append(kf.h("td", {}, connect, kf.h("button", { onclick: async () => {
@@ -34,8 +34,8 @@
     const ns = kf.namespace();
     const [{ pvcs }, { poddefaults }] = await Promise.all([kf.call("GET", `/api/namespaces/${ns}/pvcs`),
       kf.call("GET", `/api/namespaces/${ns}/poddefaults`)]);
-    $("f-pvc").innerHTML = pvcs.map((p) => `<option>${p}</option>`).join("");
-    $("f-configs").innerHTML = poddefaults.map((pd) => `<label class="muted"><input type="checkbox" value="${pd.label}"> ${pd.desc}</label><br>`).join("");
+    $("f-pvc").innerHTML = pvcs.map((p) => `<option>${kf.esc(p)}</option>`).join("");
+    $("f-configs").innerHTML = poddefaults.map((pd) => `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("");
     $("dlg").showModal();
   }
   async function submit(ev) {
