@@ -67,7 +67,8 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
             t0 = time.time()
             c.create(nb)
             obj = c.wait_for("kubeflow.org/v1", "Notebook", name, namespace,
-                             lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout)
+                             lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout,
+                             interval=0.005)
             t1 = time.time()
             pod = c.get("v1", "Pod", f"{name}-0", namespace)
             t_sched = _cond(pod, "PodScheduled")

@@ -784,6 +784,9 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     return true;
   };
   double next_wake = 1.0;
+  // Until a pod is Ready the kubelet re-syncs it every 10 ms (cold start is on the notebook's
+  // critical path; a sync of an unchanged pod costs no API call), afterwards at the 1 s relist.
+  constexpr double kStartupPoll = 0.01;
   // init containers, sequentially
   while (rt->init_done < rt->init.size() && !rt->init_failed) {
     ContainerRt& ic = rt->init[rt->init_done];
@@ -793,12 +796,12 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         break;
       }
       start_container(ic);
-      next_wake = 0.05;
+      next_wake = kStartupPoll;
       break;
     }
     if (ic.state == "running") {
       if (handle_exit(ic)) continue;
-      next_wake = 0.05;
+      next_wake = kStartupPoll;  // init containers gate the pod: notice their exit within ~10 ms
       break;
     }
     // terminated
@@ -869,7 +872,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
               cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
             }
             if (!cr.ready) {
-              next_wake = std::min(next_wake, 0.1);
+              next_wake = std::min(next_wake, kStartupPoll);
             } else {
               // wake for the next due probe; a container without probes only needs the 1 s
               // exit-detection relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
@@ -900,7 +903,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       if (cr.state == "waiting") {
         if (now_seconds() >= cr.backoff_until) {
           start_container(cr);
-          next_wake = std::min(next_wake, 0.05);
+          next_wake = std::min(next_wake, kStartupPoll);
         } else {
           next_wake = std::min(next_wake, cr.backoff_until - now_seconds());
         }
