@@ -51,8 +51,15 @@ def _pct(xs: list[float], q: float) -> float:
 
 
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
-                       readiness: bool = True, timeout: float = 120.0, namespace: str = "bench") -> dict:
-    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...}}."""
+                       readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
+                       settle_s: float = 0.5) -> dict:
+    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...}}.
+
+    ``settle_s``: pause after the previous run's pod is gone, so runs are independent cold starts.
+    The amdgpu KFD tears a GPU process down asynchronously after it exits and the next open of
+    /dev/kfd waits for that (100-130 ms right after an exit, 0.1 ms after >= 0.25 s:
+    ``profiles/r1_coldstart2/kfd_gap.txt``); back to back, run i+1 would pay run i's teardown.
+    """
     out_runs = []
     with LocalCluster(gpus=gpus) as cl:
         c = cl.client
@@ -83,7 +90,17 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                 phases["create_to_pod_ready_s"] = t_ready - t0
             if t_sched:
                 phases["create_to_scheduled_s"] = t_sched - t0
-            out_runs.append({"cold_start_s": t1 - t0, "phases": phases,
+            stages = {}
+            for st in (pod.get("status") or {}).get("initContainerStatuses") or []:
+                msg = ((st.get("state") or {}).get("terminated") or {}).get("message") or ""
+                try:
+                    rep = json.loads(msg)
+                except ValueError:
+                    continue
+                stages = {"hip_init_ms": rep.get("hip_init_ms"), "total_ms": rep.get("total_ms"),
+                          **{f"{k}_ms": v for k, v in (rep.get("stages_ms") or {}).items()},
+                          **{f"gemm_{k}": v for k, v in (rep.get("gemm0_stages_ms") or {}).items()}}
+            out_runs.append({"cold_start_s": t1 - t0, "phases": phases, "readiness_stages": stages,
                              "gpus": (obj.get("status") or {}).get("gpus"),
                              "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
             c.delete("kubeflow.org/v1", "Notebook", name, namespace)
@@ -96,10 +113,15 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                 except Exception:
                     break
                 time.sleep(0.02)
+            time.sleep(settle_s)
     xs = [r["cold_start_s"] for r in out_runs]
     phase_keys = sorted({k for r in out_runs for k in r["phases"]})
-    res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "runs": out_runs,
+    res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs,
            "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
+    stage_keys = sorted({k for r in out_runs for k, v in r["readiness_stages"].items() if v is not None})
+    if stage_keys:
+        res["readiness_stages_p50_ms"] = {k: _pct([r["readiness_stages"][k] for r in out_runs
+                                                    if r["readiness_stages"].get(k) is not None], 0.5) for k in stage_keys}
     rd = [r["gpuReadiness"] for r in out_runs if r.get("gpuReadiness")]
     if rd:
         res["readiness"] = rd[-1]
@@ -112,8 +134,10 @@ def main() -> int:
     p.add_argument("--gpus-per-notebook", type=int, default=1)
     p.add_argument("--gpus", type=int, default=None, help="node GPUs (default: discover; -> synthetic 8 without /dev/kfd)")
     p.add_argument("--no-readiness", action="store_true")
+    p.add_argument("--settle", type=float, default=0.5, help="seconds between runs (0: back to back)")
     a = p.parse_args()
-    r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness)
+    r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness,
+                           settle_s=a.settle)
     print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
     print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
     return 0

@@ -22,7 +22,7 @@
 //
 // Flags: --m/--n/--k GEMM size (default 4096^3), --iters, --ln-rows/--ln-hidden,
 //        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
-//        --oneshot-sim N.
+//        --oneshot-sim N, --rccl-single (run the RCCL stage with one device).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -124,6 +124,7 @@ struct Args {
   long long ar_max = 64ll << 20;
   double min_tflops = 0;
   bool skip_ln = false, skip_ar = false;
+  bool force_rccl = false;  // --rccl-single: RCCL stage on a 1-GPU pod too (loader smoke)
   int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
   std::string inject_fault;  // fault injection: fail the op at this stage
 };
@@ -290,8 +291,27 @@ __global__ void fill_const(float* p, size_t n, float v) {
   for (; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// Library banners (RCCL prints its version block to stdout on communicator init) must not
+// corrupt the one-line JSON report on stdout: the RCCL stage runs with fd 1 pointed at stderr.
+struct StdoutToStderr {
+  int saved = -1;
+  StdoutToStderr() {
+    std::fflush(stdout);
+    saved = dup(1);
+    if (saved >= 0) dup2(2, 1);
+  }
+  ~StdoutToStderr() {
+    std::fflush(stdout);
+    if (saved >= 0) {
+      dup2(saved, 1);
+      close(saved);
+    }
+  }
+};
+
 bool allreduce_check(int ndev, const Args& a, Json& out) {
   g_stage = "allreduce";
+  StdoutToStderr quiet;
   std::vector<ncclComm_t> comms(ndev);
   std::vector<int> devs(ndev);
   for (int i = 0; i < ndev; ++i) devs[i] = i;
@@ -667,6 +687,7 @@ int readiness_main(int argc, char** argv) {
     else if (const char* v = val("--min-tflops")) a.min_tflops = std::atof(v);
     else if (s == "--skip-ln") a.skip_ln = true;
     else if (s == "--skip-allreduce") a.skip_ar = true;
+    else if (s == "--rccl-single") a.force_rccl = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
     else if (const char* v = val("--inject-fault")) a.inject_fault = v;
   }
@@ -686,30 +707,45 @@ int readiness_main(int argc, char** argv) {
     fail(std::string("no GPU visible: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices"));
   } else {
     Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
+    // wall time per stage, summed over devices (where a cold start's milliseconds go)
+    double st_query = 0, st_gemm = 0, st_ln = 0;
+    auto lap = [](std::chrono::steady_clock::time_point& t) {
+      auto now = std::chrono::steady_clock::now();
+      double ms = std::chrono::duration<double, std::milli>(now - t).count();
+      t = now;
+      return ms;
+    };
     for (int d = 0; d < ndev; ++d) {
       g_stage = "device-query";
+      auto ts = std::chrono::steady_clock::now();
       hipDeviceProp_t p;
       if (hipGetDeviceProperties(&p, d) == hipSuccess)
         devs.push_back(Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
                             {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}});
+      st_query += lap(ts);
       Json g;
       if (gemm_check(d, a, g)) gemms.push_back(g);
       else gemms.push_back(Json{{"device", d}, {"error", g_error}});
+      st_gemm += lap(ts);
       if (!a.skip_ln) {
         Json l;
         if (ln_check(d, a, l)) lns.push_back(l);
+        st_ln += lap(ts);
       }
     }
+    g_result["stages_ms"] = Json{{"device_query", st_query}, {"gemm", st_gemm}, {"layernorm", st_ln}};
     g_result["devices"] = devs;
     g_result["gemm"] = gemms;
     if (!a.skip_ln) g_result["layernorm"] = lns;
     double agg = 0;
     for (const auto& gm : gemms.as_array()) agg += gm["tflops"].as_double();
     g_result["gemm_tflops_aggregate"] = agg;
-    if (ndev >= 2 && !a.skip_ar) {
+    if ((ndev >= 2 || a.force_rccl) && !a.skip_ar) {
       Json ar;
+      auto ts = std::chrono::steady_clock::now();
       allreduce_check(ndev, a, ar);
       g_result["allreduce"] = ar;
+      g_result["stages_ms"]["allreduce"] = lap(ts);
     }
     if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
       Json os;
@@ -738,6 +774,9 @@ int readiness_main(int argc, char** argv) {
     if (g_result.has("error")) brief["error"] = g_result["error"];
     if (g_result.has("devices")) brief["devices"] = (long long)g_result["devices"].size();
     if (g_result.has("simulated")) brief["simulated"] = true;
+    if (g_result.has("stages_ms")) brief["stages_ms"] = g_result["stages_ms"];
+    if (g_result.has("gemm") && g_result["gemm"].size() && g_result["gemm"][0].has("stages"))
+      brief["gemm0_stages_ms"] = g_result["gemm"][0]["stages"];
     if (g_result.has("layernorm") && g_result["layernorm"].size()) brief["layernorm_GBps"] = g_result["layernorm"][0]["GBps"];
     if (g_result.has("allreduce")) {
       const Json& sw = g_result["allreduce"]["sweep"];
