@@ -24,6 +24,7 @@
 //        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
 //        --oneshot-sim N, --rccl-single (run the RCCL stage with one device).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <dirent.h>
@@ -40,6 +41,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "core/json.h"
@@ -309,16 +311,56 @@ struct StdoutToStderr {
   }
 };
 
+// RCCL (librccl.so is ~570 MB of fat binaries) is dlopen'ed only by pods that can use it (>= 2
+// visible GPUs or --rccl-single), and BEFORE the HIP runtime initialises: a dlopen after HIP
+// init registers its code objects eagerly (4.8 s measured), before it costs what linking did.
+struct Rccl {
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  std::string error = "not loaded";
+
+  void load() {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      error = e ? e : "dlopen librccl.so.1 failed";
+      return;
+    }
+    error.clear();
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn && error.empty()) error = std::string("missing symbol ") + name;
+    };
+    sym(comm_init_all, "ncclCommInitAll");
+    sym(error_string, "ncclGetErrorString");
+    sym(group_start, "ncclGroupStart");
+    sym(group_end, "ncclGroupEnd");
+    sym(all_reduce, "ncclAllReduce");
+    sym(comm_destroy, "ncclCommDestroy");
+  }
+};
+Rccl g_rccl;
+
 bool allreduce_check(int ndev, const Args& a, Json& out) {
+  Rccl& nccl = g_rccl;
+  if (!nccl.error.empty()) {
+    fail("RCCL: " + nccl.error);
+    return false;
+  }
   g_stage = "allreduce";
   StdoutToStderr quiet;
   std::vector<ncclComm_t> comms(ndev);
   std::vector<int> devs(ndev);
   for (int i = 0; i < ndev; ++i) devs[i] = i;
   auto t0 = std::chrono::steady_clock::now();
-  ncclResult_t nr = ncclCommInitAll(comms.data(), ndev, devs.data());
+  ncclResult_t nr = nccl.comm_init_all(comms.data(), ndev, devs.data());
   if (nr != ncclSuccess) {
-    fail(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+    fail(std::string("ncclCommInitAll: ") + nccl.error_string(nr));
     return false;
   }
   double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -349,9 +391,9 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
       hipLaunchKernelGGL(fill_const, dim3(256), dim3(256), 0, st[i], buf[i], n, (float)(i + 1));
     }
     auto once = [&]() {
-      ncclGroupStart();
-      for (int i = 0; i < ndev; ++i) ncclAllReduce(buf[i], buf[i], n, ncclFloat, ncclSum, comms[i], st[i]);
-      ncclGroupEnd();
+      nccl.group_start();
+      for (int i = 0; i < ndev; ++i) nccl.all_reduce(buf[i], buf[i], n, ncclFloat, ncclSum, comms[i], st[i]);
+      nccl.group_end();
     };
     once();
     for (int i = 0; i < ndev; ++i) {
@@ -379,7 +421,7 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
     (void)hipSetDevice(i);
     (void)hipFree(buf[i]);
     (void)hipStreamDestroy(st[i]);
-    ncclCommDestroy(comms[i]);
+    nccl.comm_destroy(comms[i]);
   }
   out = Json{{"devices", ndev}, {"comm_init_ms", init_ms}, {"peer_access", peer}, {"sweep", sweep}, {"correct", ok}};
   if (!ok) fail("all-reduce result mismatch");
@@ -690,6 +732,23 @@ int readiness_main(int argc, char** argv) {
     else if (s == "--rccl-single") a.force_rccl = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
     else if (const char* v = val("--inject-fault")) a.inject_fault = v;
+  }
+  {
+    // how many GPUs the pod was given, without touching the GPU (the device plugin's env)
+    int visible = -1;
+    for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"}) {
+      const char* v = std::getenv(var);
+      if (v && *v) {
+        visible = 1;
+        for (const char* c = v; *c; ++c) visible += *c == ',';
+        break;
+      }
+    }
+    if (!a.skip_ar && (a.force_rccl || visible != 1)) {
+      auto tl = std::chrono::steady_clock::now();
+      g_rccl.load();
+      g_result["rccl_load_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count();
+    }
   }
   auto t0 = std::chrono::steady_clock::now();
   g_stage = "hip-init";
