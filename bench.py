@@ -3,13 +3,22 @@
 (+ notebook cold-start p50 from the native control plane when requested).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
-``torch.distributed.run`` with one rank per GPU (RCCL). Each rank is one notebook pod's GPU running
+``torch.distributed.run`` with one rank per GPU (RCCL). Run directly with ``--gpus N > 1`` (no
+WORLD_SIZE in the env) it launches the N ranks itself (kubeflow_rm_amd.parallel.launch.run_ranks:
+child processes started before this process touches the GPU, private rendezvous port, one failing
+rank stops the rest and fails the run). Each rank is one notebook pod's GPU running
 the K1 readiness op: a bf16 GEMM C = A @ B^T (8192^3 by default) on the hand-written gfx950 MFMA
 kernel. A "step" = one such GEMM on every GPU. W untimed warmup steps, then exactly K timed steps
 bracketed by barrier + device sync on both sides; the slowest rank's time is used. ``value`` is
 the whole-job aggregate TFLOPS (N x per-GEMM FLOPs / max-rank time). Weak scaling: per-GPU work
 is fixed as N grows. Data: synthetic uniform [-1, 1) bf16 operands (random data, not zeros:
 zero operands inflate MFMA clocks — cdna_hip_programming.md §5.4 rule 25).
+
+Cold start (rank 0, after the timed region, while the other ranks wait on a CPU-side barrier with
+their GPU memory released): ``--coldstart-runs`` (default 10) Notebook CREATE -> Ready runs of ONE
+notebook requesting all N GPUs, through the native control plane (process pods: no container
+runtime), with the in-pod readiness op on the allocated GPUs (N >= 2: one-shot peer all-reduce over
+xGMI). Reported with p50 / p90 and the per-phase p50 breakdown.
 """
 from __future__ import annotations
 
@@ -31,16 +40,27 @@ def parse_args():
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--n", type=int, default=8192)
     p.add_argument("--k", type=int, default=8192)
-    p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "3")),
-                   help="notebook cold-start runs through the native control plane (rank 0)")
+    p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "10")),
+                   help="cold-start runs of one N-GPU notebook through the native control plane (rank 0)")
     p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
     p.add_argument("--no-allreduce-sweep", action="store_true",
                    help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
     return p.parse_args()
 
 
+def self_launch(args) -> int:
+    """``--gpus N`` without a launcher: run N ranks of this script (or of the JSON argv in
+    KFAMD_BENCH_RANK_ARGV — the CPU test's stub worker) and return the job's exit code."""
+    from kubeflow_rm_amd.parallel.launch import run_ranks
+    argv = json.loads(os.environ.get("KFAMD_BENCH_RANK_ARGV") or "null") or \
+        [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    return run_ranks(argv, args.gpus, master_addr="127.0.0.1")
+
+
 def main() -> int:
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
     import torch
     import torch.distributed as dist
 
@@ -48,7 +68,7 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world} (n_gpus reports WORLD_SIZE)", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -119,16 +139,30 @@ def main() -> int:
         torch.cuda.synchronize(dev)
         extra["torch_matmul_tflops_per_gpu"] = round(flops * args.steps / (time.perf_counter() - t1) / 1e12, 1)
 
-    if args.coldstart_runs > 0 and rank == 0:
-        try:
-            from kubeflow_rm_amd.bench_coldstart import measure_cold_start
-            cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=1)
-            extra["cold_start_p50_s"] = cs["p50_s"]
-            extra["cold_start_p90_s"] = cs["p90_s"]
-            extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
-            extra["cold_start_readiness"] = cs.get("readiness")
-        except Exception as e:  # reported, never fatal for the GEMM number
-            extra["cold_start_error"] = f"{type(e).__name__}: {e}"
+    if args.coldstart_runs > 0:
+        # the N-GPU notebook needs every GPU: free this rank's memory, park ranks != 0 on a CPU
+        # (gloo) barrier — an RCCL barrier would keep a spinning kernel on their GPUs
+        del a, b, c
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+        if world > 1:
+            dist.barrier(group=cpu_group)
+        if rank == 0:
+            try:
+                from kubeflow_rm_amd.bench_coldstart import measure_cold_start
+                cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world)
+                extra["cold_start_gpus_per_notebook"] = world
+                extra["cold_start_runs"] = len(cs["runs"])
+                extra["cold_start_p50_s"] = cs["p50_s"]
+                extra["cold_start_p90_s"] = cs["p90_s"]
+                extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
+                extra["cold_start_readiness"] = cs.get("readiness")
+                extra["cold_start_note"] = "process pods (no container runtime); notebook server = stub recipe"
+            except Exception as e:  # reported, never fatal for the GEMM number
+                extra["cold_start_error"] = f"{type(e).__name__}: {e}"
+        if world > 1:
+            dist.barrier(group=cpu_group)
 
     if rank == 0:
         line = {

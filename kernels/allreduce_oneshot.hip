@@ -11,8 +11,13 @@
 // Each barrier is per block pair: block b of rank r stores its epoch into flags[p][phase][r][b]
 // of every peer p (system-scope atomic), then polls its own flags[r][phase][p][b] for every p.
 // Epochs are per call (caller passes 1, 2, 3, ...; never 0); flags are zeroed once at allocation.
-// Every spin is bounded: a peer that never arrives sets *timeout and the kernel drains (the caller
-// reports the failure, the GPU never hangs).
+// Every spin is bounded by a wall-clock deadline (s_memrealtime, 100 MHz; default 5 s, settable with
+// kfamd_allreduce_oneshot_set_timeout_ms): a peer that never arrives sets *timeout and the kernel
+// drains, so the GPU never hangs. A timed-out call must never look like a result: every output
+// element of a block whose entry barrier timed out is written as a quiet NaN (the peer's staging
+// buffer may hold a stale epoch), the exit barrier is skipped, and the flag stays set until the
+// caller resets it — the flag protocol is out of step after a timeout, so callers treat it as fatal
+// for the communicator (parallel/oneshot.py raises and refuses further calls).
 //
 // Ranks may be separate devices (peer access / IPC-opened buffers: the readiness op, DP) or, for
 // tests on one GPU, several ranks simulated in ONE launch (gridDim.y = ranks in this launch,
@@ -27,7 +32,7 @@ namespace {
 
 constexpr int kMaxRanks = 8;
 constexpr int kThreads = 256;
-constexpr unsigned kSpinLimit = 1u << 22;  // x s_sleep(1): tens of ms before declaring a timeout
+constexpr uint64_t kTicksPerMs = 100000;  // s_memrealtime runs at a constant 100 MHz
 
 struct Peers {
   const void* in[kMaxRanks];
@@ -43,9 +48,12 @@ __device__ __forceinline__ uint32_t load_flag(uint32_t* p) {
 }
 
 // Block-pair barrier: thread t < nranks signals peer t, then waits for peer t's signal.
-__device__ __forceinline__ void barrier(const Peers& P, int me, int nranks, int phase, uint32_t epoch,
-                                        unsigned* timeout) {
+// Returns true (in every thread of the block) when some peer missed the deadline.
+__device__ __forceinline__ bool barrier(const Peers& P, int me, int nranks, int phase, uint32_t epoch,
+                                        uint64_t timeout_ticks, unsigned* timeout) {
   const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  __shared__ int missed;
+  if (t == 0) missed = 0;
   __syncthreads();  // every thread's reads / writes of this phase are done before anyone signals
   if (t < nranks) {
     // release: this rank's input (written by earlier work on its stream) and, at the exit
@@ -53,11 +61,12 @@ __device__ __forceinline__ void barrier(const Peers& P, int me, int nranks, int 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     store_flag(P.flags[t] + ((size_t)phase * nranks + me) * nb + b, epoch);
     uint32_t* mine = P.flags[me] + ((size_t)phase * nranks + t) * nb + b;
-    unsigned spins = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (load_flag(mine) != epoch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
         __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        missed = 1;
         break;
       }
     }
@@ -65,6 +74,7 @@ __device__ __forceinline__ void barrier(const Peers& P, int me, int nranks, int 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+  return missed != 0;
 }
 
 template <typename T>
@@ -108,13 +118,19 @@ struct Vec<__bf16> {
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long n, int nranks, int rank0,
-                                                              uint32_t epoch, unsigned* timeout) {
+                                                              uint32_t epoch, uint64_t timeout_ticks,
+                                                              unsigned* timeout) {
   using V = Vec<T>;
   const int me = rank0 + blockIdx.y;
-  barrier(P, me, nranks, 0, epoch, timeout);
-  // 16-byte vectors; rank r's vector i lives at in[r] + 16 i
   const long long nvec = n / V::kElems;
   const long long stride = (long long)gridDim.x * kThreads;
+  if (barrier(P, me, nranks, 0, epoch, timeout_ticks, timeout)) {
+    // a peer's input may be stale: poison this block's share of the output, skip the exit barrier
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
+      V::store1(P.out[me], i, __builtin_nanf(""));
+    return;
+  }
+  // 16-byte vectors; rank r's vector i lives at in[r] + 16 i
   for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride) {
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     uint4 v[kMaxRanks];
@@ -134,10 +150,16 @@ __global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long
       V::store1(P.out[me], i, s);
     }
   }
-  barrier(P, me, nranks, 1, epoch, timeout);
+  barrier(P, me, nranks, 1, epoch, timeout_ticks, timeout);
 }
 
+uint64_t g_timeout_ticks = 5000 * kTicksPerMs;
+
 }  // namespace
+
+extern "C" void kfamd_allreduce_oneshot_set_timeout_ms(int ms) {
+  g_timeout_ticks = (uint64_t)(ms < 1 ? 1 : ms) * kTicksPerMs;
+}
 
 extern "C" long long kfamd_allreduce_oneshot_flag_bytes(int nranks, int nblocks) {
   return (long long)2 * nranks * nblocks * (long long)sizeof(uint32_t);
@@ -171,9 +193,11 @@ extern "C" int kfamd_allreduce_oneshot(const void* const* inputs, void* const* o
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(nblocks, launch_ranks), block(kThreads);
   if (dtype == KFAMD_DTYPE_BF16)
-    hipLaunchKernelGGL(allreduce_oneshot<__bf16>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch, timeout);
+    hipLaunchKernelGGL(allreduce_oneshot<__bf16>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch,
+                       g_timeout_ticks, timeout);
   else
-    hipLaunchKernelGGL(allreduce_oneshot<float>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch, timeout);
+    hipLaunchKernelGGL(allreduce_oneshot<float>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch,
+                       g_timeout_ticks, timeout);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }

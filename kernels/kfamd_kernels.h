@@ -77,6 +77,8 @@ enum kfamd_dtype { KFAMD_DTYPE_F32 = 0, KFAMD_DTYPE_BF16 = 1 };
 // with epoch = 1, 2, 3, ... (same nblocks every call). *timeout is set if a peer never arrived.
 long long kfamd_allreduce_oneshot_flag_bytes(int nranks, int nblocks);
 int kfamd_allreduce_oneshot_blocks(long long n, int dtype);
+// Barrier deadline per call (default 5000 ms); a missed deadline sets *timeout and NaN-poisons the output.
+void kfamd_allreduce_oneshot_set_timeout_ms(int ms);
 int kfamd_allreduce_oneshot(const void* const* inputs, void* const* outputs, uint32_t* const* flags,
                             int nranks, int rank0, int launch_ranks, long long n, int dtype,
                             unsigned epoch, int nblocks, unsigned* timeout, void* stream);

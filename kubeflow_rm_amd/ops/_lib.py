@@ -34,6 +34,7 @@ _SIGNATURES = {
                                          c_int, c_int, c_vp]),
     "kfamd_allreduce_oneshot_flag_bytes": (c_ll, [c_int, c_int]),
     "kfamd_allreduce_oneshot_blocks": (c_int, [c_ll, c_int]),
+    "kfamd_allreduce_oneshot_set_timeout_ms": (None, [c_int]),
     "kfamd_allreduce_oneshot": (c_int, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_int, c_int,
                                         c_int, c_ll, c_int, ctypes.c_uint, c_int, c_vp, c_vp]),
     "kfamd_ipc_alloc": (c_int, [c_ll, c_int, ctypes.POINTER(c_vp), ctypes.c_char_p]),

@@ -3,7 +3,8 @@
 The notebook pod spec carries the wiring (injected by the kubelet's device plugin allocation,
 native/gpu/topology.cc gpu_env_for): HIP_VISIBLE_DEVICES (pod-local ordinals 0..n-1),
 KFAMD_XGMI_RING (ring order over direct xGMI links), WORLD_SIZE / LOCAL_WORLD_SIZE,
-MASTER_ADDR=127.0.0.1, MASTER_PORT, NCCL_IB_DISABLE=1, NCCL_P2P_LEVEL=SYS,
+MASTER_ADDR / MASTER_PORT (the pod's own rendezvous endpoint: its 127.x address and a port
+unique on the node, so concurrent multi-GPU notebooks never share a TCPStore), NCCL_IB_DISABLE=1, NCCL_P2P_LEVEL=SYS,
 HSA_ENABLE_IPC_MODE_LEGACY=0. ``torchrun`` (or this module's ``spawn``) supplies RANK/LOCAL_RANK.
 
 ``init()`` maps LOCAL_RANK to the device at position LOCAL_RANK of the xGMI ring, so that ring
@@ -71,7 +72,10 @@ def init(backend: str | None = None, timeout_s: float = 600.0) -> DistEnv:
         device = torch.device("cuda", dev)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29500")
+        if not os.environ.get("MASTER_PORT"):
+            # no silent shared default: two jobs on one host would meet in the same TCPStore
+            raise RuntimeError("WORLD_SIZE > 1 but MASTER_PORT is unset: run under torchrun, "
+                               "kubeflow_rm_amd.parallel.launch, or a multi-GPU notebook pod (injected env)")
         kw = {"device_id": device} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, timeout=_dt.timedelta(seconds=timeout_s), **kw)
     _ENV = DistEnv(rank=rank, world_size=world, local_rank=local_rank, device=device, backend=backend)

@@ -13,6 +13,12 @@ Design for MI355X (not a DDP transliteration):
   world size and copies back.
 * Gradients are reduced in their own dtype (bf16 grads halve link traffic; fp32 for master
   weights) — pass ``reduce_dtype`` to override.
+* Collective order is identical on every rank whatever subset of parameters got gradients
+  (conditional branches, MoE experts): a bucket that completes early is only *marked* ready;
+  buckets are launched strictly in index order (the next index as soon as it is ready), and
+  ``finish()`` launches every remaining bucket in order, zero-filling missing grads — including
+  buckets that saw no gradient at all on this rank. So rank A can never issue b0,b2,b1 while
+  rank B issues b0,b1,b2 (an RCCL hang or mismatched-size reduce).
 """
 from __future__ import annotations
 
@@ -22,13 +28,14 @@ import torch
 import torch.distributed as dist
 
 
-@dataclass
+@dataclass(eq=False)
 class _Bucket:
     params: list
     numel: int
     dtype: torch.dtype
     buffer: torch.Tensor | None = None
     pending: int = 0
+    ready: bool = False
     work: object = None
     offsets: list = field(default_factory=list)
 
@@ -63,7 +70,9 @@ class GradBucketer:
                 self._param_bucket[p] = bi
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self._callback_queued = False
+        self._next = 0  # index of the next bucket to launch (same sequence on every rank)
         self.comm_bytes = 0
+        self.launch_order: list[int] = []  # this step's launch sequence (tests / debugging)
 
     def _add_bucket(self, params, dtype):
         numel = sum(p.numel() for p in params)
@@ -82,9 +91,17 @@ class GradBucketer:
         b = self.buckets[self._param_bucket[p]]
         b.pending -= 1
         if b.pending == 0:
-            self._launch(b)
+            b.ready = True
+            # in-order launch: only the next expected index may go; later ready buckets wait
+            while self._next < len(self.buckets) and self.buckets[self._next].ready:
+                self._launch(self._next)
+                self._next += 1
 
-    def _launch(self, b: _Bucket) -> None:
+    def _launch(self, bi: int) -> None:
+        b = self.buckets[bi]
+        for p in b.params:
+            if p.grad is None:  # no grad on this rank this step: contribute zeros
+                p.grad = torch.zeros_like(p)
         dev = b.params[0].grad.device
         if b.buffer is None or b.buffer.device != dev:
             b.buffer = torch.empty(b.numel, dtype=b.dtype, device=dev)
@@ -94,23 +111,27 @@ class GradBucketer:
             b.buffer.div_(self.world)
         b.work = dist.all_reduce(b.buffer, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.comm_bytes += b.buffer.numel() * b.buffer.element_size()
+        self.launch_order.append(bi)
 
     def finish(self) -> None:
-        """Wait for every bucket and scatter the reduced gradients back (end of backward)."""
+        """Launch what is left (in index order, zero-filled), wait for every bucket and scatter the
+        reduced gradients back (end of backward). Call it directly after a backward in which this
+        rank produced no gradient at all (no hook fired, so nothing queued it)."""
         self._callback_queued = False
+        if self.world > 1:
+            while self._next < len(self.buckets):
+                self._launch(self._next)
+                self._next += 1
         for b in self.buckets:
-            if b.work is None and b.pending != len(b.params):
-                # some params of this bucket had no grad this step: reduce what we have
-                for p in b.params:
-                    if p.grad is None:
-                        p.grad = torch.zeros_like(p)
-                self._launch(b)
             if b.work is not None:
                 b.work.wait()
                 for p, off in zip(b.params, b.offsets):
                     p.grad.copy_(b.buffer[off:off + p.numel()].view_as(p.grad))
                 b.work = None
             b.pending = len(b.params)
+            b.ready = False
+        self._next = 0
+        self.last_launch_order, self.launch_order = self.launch_order, []
 
     def remove(self) -> None:
         for h in self._hooks:

@@ -4,11 +4,22 @@
 inherited HIP state), exports RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
 MASTER_PORT and HSA_ENABLE_IPC_MODE_LEGACY=0, runs ``fn(rank, *args)`` in each and returns the
 per-rank results in rank order; any rank failure raises in the parent.
+
+``run_ranks(argv, nproc)`` / ``python -m kubeflow_rm_amd.parallel.launch [--nproc N] -- prog ...``
+is the command-line form used inside a multi-GPU notebook pod and by ``bench.py --gpus N``: it
+starts ``nproc`` child processes (never exec — the parent may not have touched the GPU, but a
+child is always safe) with RANK / LOCAL_RANK set and the pod's injected rendezvous
+(MASTER_ADDR / MASTER_PORT from the kubelet, a private free port otherwise), forwards their
+output, and returns the first non-zero exit code; one failing rank terminates the others.
 """
 from __future__ import annotations
 
 import os
+import signal
 import socket
+import subprocess
+import sys
+import time
 import traceback
 
 import torch.multiprocessing as mp
@@ -68,3 +79,85 @@ def spawn(fn, nprocs: int, *args, env: dict | None = None, timeout: float = 600.
     if errors:
         raise RuntimeError("\n".join(errors))
     return [results[r] for r in range(nprocs)]
+
+
+def rank_env(rank: int, nproc: int, master_addr: str, master_port: int, base: dict | None = None) -> dict:
+    """Environment of local rank ``rank`` of ``nproc`` (single node: RANK == LOCAL_RANK)."""
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(nproc),
+                "LOCAL_WORLD_SIZE": str(nproc), "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port),
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    return env
+
+
+def run_ranks(argv: list[str], nproc: int, master_addr: str | None = None, master_port: int | None = None,
+              extra_env: dict | None = None, timeout: float | None = None, poll_s: float = 0.05) -> int:
+    """Run ``argv`` as ``nproc`` local ranks; returns 0 or the first failing rank's exit code
+    (124 on ``timeout``). Rendezvous: explicit args, else the pod's MASTER_ADDR / MASTER_PORT
+    (per-pod values injected by the kubelet), else 127.0.0.1 and a free port."""
+    addr = master_addr or os.environ.get("MASTER_ADDR") or "127.0.0.1"
+    port = master_port or int(os.environ.get("MASTER_PORT") or 0) or free_port()
+    procs = []
+    for r in range(nproc):
+        env = rank_env(r, nproc, addr, port)
+        env.update(extra_env or {})
+        # own process group per rank: a failure can take down the rank's whole tree
+        procs.append(subprocess.Popen(argv, env=env, start_new_session=True))
+    deadline = None if timeout is None else time.monotonic() + timeout
+    rc = 0
+    try:
+        live = set(range(nproc))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"launch: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+            if rc != 0:
+                break
+            if deadline is not None and time.monotonic() > deadline:
+                print(f"launch: timeout after {timeout}s", file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc
+
+
+def main(args: list[str] | None = None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(prog="python -m kubeflow_rm_amd.parallel.launch",
+                                 description="run a program as N local ranks (one per GPU of this pod)")
+    ap.add_argument("--nproc", type=int, default=int(os.environ.get("LOCAL_WORLD_SIZE") or 0) or None,
+                    help="ranks to start (default: the pod's LOCAL_WORLD_SIZE)")
+    ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("prog", nargs=argparse.REMAINDER)
+    ns = ap.parse_args(args)
+    prog = ns.prog[1:] if ns.prog and ns.prog[0] == "--" else ns.prog
+    if not prog:
+        ap.error("no program given")
+    if prog[0].endswith(".py"):
+        prog = [sys.executable, "-u"] + prog
+    return run_ranks(prog, ns.nproc or 1, timeout=ns.timeout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

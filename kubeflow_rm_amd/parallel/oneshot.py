@@ -7,6 +7,14 @@ are exchanged once over the process group, and every rank maps its peers' buffer
 writes the sum into the tensor. For the latency-bound sizes of TP decode / small DP buckets this
 replaces RCCL's 2(N-1) ring steps with one kernel; :func:`all_reduce` routes larger tensors to
 ``torch.distributed.all_reduce`` (RCCL).
+
+Failure model: the kernel's barriers wait at most ``timeout_ms`` (wall clock) for a peer. A missed
+deadline NaN-poisons that call's output and sets a device flag; the flag protocol is then out of
+step between ranks, so a timeout is fatal for this communicator. The flag is read back every
+``check_every`` calls (one tiny D2H copy, so the hot path stays asynchronous) and by
+:meth:`check`; once seen, every later call raises :class:`OneShotTimeout` — results between the
+timeout and the check are NaN, never silently wrong. Re-create the object (collectively) to
+recover.
 """
 from __future__ import annotations
 
@@ -21,15 +29,22 @@ _DTYPES = {torch.float32: 0, torch.bfloat16: 1}
 MAX_BLOCKS = 64
 
 
+class OneShotTimeout(RuntimeError):
+    """A peer missed the one-shot barrier deadline; this communicator is unusable."""
+
+
 class IpcOneShotAllReduce:
-    def __init__(self, group=None, max_bytes: int = 1 << 20):
+    def __init__(self, group=None, max_bytes: int = 1 << 20, timeout_ms: int = 5000, check_every: int = 64):
         self.group = group
+        self.timeout_ms, self.check_every = timeout_ms, max(1, check_every)
+        self.broken = False
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if not 1 <= self.world <= 8:
             raise ValueError("one-shot all-reduce serves 1..8 ranks (one xGMI hive)")
         self.max_bytes = max_bytes
         L = _lib.lib()
+        L.kfamd_allreduce_oneshot_set_timeout_ms(int(timeout_ms))
         fbytes = L.kfamd_allreduce_oneshot_flag_bytes(self.world, MAX_BLOCKS)
         self._own: list[int] = []
         mine = []
@@ -69,6 +84,8 @@ class IpcOneShotAllReduce:
         nbytes = t.numel() * t.element_size()
         if nbytes > self.max_bytes:
             raise ValueError(f"{nbytes} B > registered {self.max_bytes} B (use RCCL)")
+        if self.broken:
+            raise OneShotTimeout(f"one-shot all-reduce (rank {self.rank}) timed out earlier; re-create it")
         L = _lib.lib()
         stream = torch.cuda.current_stream(t.device).cuda_stream
         # own registered input buffer <- t, stream-ordered before the kernel (whose entry barrier
@@ -81,10 +98,19 @@ class IpcOneShotAllReduce:
         rc = L.kfamd_allreduce_oneshot(self._in, self._out, self._flags, self.world, self.rank, 1, t.numel(), dt,
                                        self.epoch, nb, self.timeout.data_ptr(), stream)
         _lib.check(rc, f"allreduce_oneshot[rank {self.rank}/{self.world}, {t.numel()}]")
+        if self.epoch % self.check_every == 0:
+            self.check()
         return t
 
     def timed_out(self) -> bool:
         return bool(self.timeout.item())
+
+    def check(self) -> None:
+        """Raise :class:`OneShotTimeout` if any call so far missed a peer (synchronises the stream)."""
+        if self.broken or self.timed_out():
+            self.broken = True
+            raise OneShotTimeout(f"one-shot all-reduce: a peer of rank {self.rank} missed the "
+                                 f"{self.timeout_ms} ms barrier deadline; outputs since the last check are NaN")
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """One-shot for registered-size fp32/bf16 tensors, RCCL (torch.distributed) otherwise."""
@@ -96,6 +122,8 @@ class IpcOneShotAllReduce:
     def close(self) -> None:
         L = _lib.lib()
         torch.cuda.synchronize()
+        if not self._own:
+            return
         for p in self._opened:
             L.kfamd_ipc_close(p)
         for p in self._own:

@@ -293,7 +293,8 @@ std::map<std::string, std::vector<int>> GpuAllocator::allocations() const {
   return alloc_;
 }
 
-Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu) {
+Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu, const std::string& master_addr,
+                 int master_port) {
   Json env = Json::array();
   auto add = [&](const std::string& k, const std::string& v) { env.push_back(Json{{"name", k}, {"value", v}}); };
   std::vector<std::string> ids, ring;
@@ -309,12 +310,12 @@ Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu) {
   add("KFAMD_GPU_TOPOLOGY", t.describe());
   if (t.source == "synthetic") add("KFAMD_SIMULATED_GPUS", "1");  // CI node: no /dev/kfd behind these ids
   if (multi_gpu) {
-    // single-node torchrun / RCCL wiring: one process per GPU, loopback rendezvous,
-    // xGMI P2P enabled, no IB/socket fallbacks inside the pod.
+    // single-node torchrun / RCCL wiring: one process per GPU, a rendezvous endpoint
+    // private to this pod, xGMI P2P enabled, no IB/socket fallbacks inside the pod.
     add("LOCAL_WORLD_SIZE", std::to_string(p.devices.size()));
     add("WORLD_SIZE", std::to_string(p.devices.size()));
-    add("MASTER_ADDR", "127.0.0.1");
-    add("MASTER_PORT", "29500");
+    add("MASTER_ADDR", master_addr.empty() ? "127.0.0.1" : master_addr);
+    add("MASTER_PORT", std::to_string(master_port > 0 ? master_port : 29500));
     add("NCCL_IB_DISABLE", "1");
     add("NCCL_P2P_LEVEL", "SYS");
     add("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1");

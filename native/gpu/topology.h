@@ -88,6 +88,8 @@ class GpuAllocator {
 };
 
 // Env for a pod's containers given its placement (HIP_VISIBLE_DEVICES, RCCL/torch rendezvous).
-Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu);
+// master_addr/master_port: the pod's own rendezvous endpoint (multi-GPU pods only)
+Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu, const std::string& master_addr = "127.0.0.1",
+                 int master_port = 29500);
 
 }  // namespace kf

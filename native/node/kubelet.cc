@@ -132,6 +132,7 @@ struct ContainerRt {
 struct Kubelet::PodRuntime {
   std::string uid, ns, name, dir, ip;
   Placement gpus;
+  int rdzv_port = 0;  // torch.distributed rendezvous port of a multi-GPU pod (unique on the node)
   bool gpu_ok = true;
   std::map<std::string, std::string> mounts;  // mountPath -> host dir (per container union)
   std::vector<ContainerRt> init, main;
@@ -160,6 +161,30 @@ Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)
   make_dirs(cfg_.root_dir + "/pods");
   make_dirs(cfg_.root_dir + "/pv");
   rec_ = std::make_unique<EventRecorder>(c_, "kubelet");
+}
+
+// Process pods share the host network namespace, and torch's TCPStore listens on the wildcard
+// address: two multi-GPU notebooks with the same MASTER_PORT would collide whatever MASTER_ADDR
+// says. Each multi-GPU pod gets its own port (unique among this node's pods and free on the host
+// when handed out); MASTER_ADDR is the pod's own 127.x address. (In a real cluster every pod has
+// its own network namespace and the fixed port would do.)
+int Kubelet::alloc_rdzv_port() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int port = 29500; port < 29500 + 4096; ++port) {
+    if (rdzv_ports_.count(port)) continue;
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) break;
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port));
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    const bool free_now = ::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0;
+    ::close(fd);
+    if (!free_now) continue;
+    rdzv_ports_.insert(port);
+    return port;
+  }
+  return 29500;  // nothing free in the range: fall back to torch's default and let it report
 }
 
 Kubelet::~Kubelet() { stop(); }
@@ -436,6 +461,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         if (rt) {
           terminate_pod(*rt, 0);
           alloc_->release(rt->uid);
+          rdzv_ports_.erase(rt->rdzv_port);
           pods_.erase(rt->uid);
         }
         key_to_uid_.erase(k);
@@ -464,6 +490,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       terminate_pod(*rt, pod.at_path({"metadata", "deletionGracePeriodSeconds"}).as_int(30));
       alloc_->release(uid);
       std::lock_guard<std::mutex> g(mu_);
+      rdzv_ports_.erase(rt->rdzv_port);
       pods_.erase(uid);
       key_to_uid_.erase(r.ns + "/" + r.name);
     }
@@ -499,10 +526,12 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         std::vector<std::string> ids, ring;
         for (int d : rt->gpus.devices) ids.push_back(std::to_string(d));
         for (int d : rt->gpus.ring) ring.push_back(std::to_string(d));
+        if (rt->gpus.devices.size() > 1) rt->rdzv_port = alloc_rdzv_port();
         c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
           o["metadata"]["annotations"][ANNOTATION_GPU_IDS] = join(ids, ",");
           o["metadata"]["annotations"][ANNOTATION_XGMI_RING] = join(ring, ",");
           o["metadata"]["annotations"]["amd.com/gpu-placement"] = rt->gpus.reason;
+          if (rt->rdzv_port) o["metadata"]["annotations"]["kfamd.io/rendezvous"] = rt->ip + ":" + std::to_string(rt->rdzv_port);
           return true;
         });
       }
@@ -636,7 +665,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     // GPU wiring from the device plugin allocation
     const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0;
     if (wants_gpu && !rt->gpus.devices.empty()) {
-      const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1);
+      const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1, rt->ip, rt->rdzv_port);
       for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
       // Node-level code-object cache shared by every GPU container (the device plugin's Allocate
       // response carries this env + mount). comgr caches the runtime's device-code builds under

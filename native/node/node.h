@@ -21,6 +21,7 @@
 
 #include <atomic>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -109,6 +110,8 @@ class Kubelet {
   std::map<std::string, std::shared_ptr<PodRuntime>> pods_;  // uid -> runtime
   std::map<std::string, std::string> key_to_uid_;            // ns/name -> uid
   uint32_t next_ip_ = 2;
+  std::set<int> rdzv_ports_;  // MASTER_PORTs handed to running multi-GPU pods
+  int alloc_rdzv_port();
   std::unique_ptr<EventRecorder> rec_;
   std::shared_ptr<Controller> ctl_;
   std::atomic<bool> running_{false};

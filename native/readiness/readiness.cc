@@ -6,11 +6,15 @@
 //   2. K1: bf16 GEMM on the hand-written MFMA kernel (kernels/gemm_bf16.hip), verified against an
 //      fp32 reference kernel on sampled rows, timed with hipEvents -> TFLOPS per GPU;
 //   3. K2: LayerNorm (kernels/layernorm_bf16.hip) verified on sampled rows -> GB/s;
-//   4. K3: with >= 2 visible GPUs, peer-access matrix + RCCL communicator over all devices
-//      (ncclCommInitAll, one process) and an all-reduce sweep with algbw / busbw
-//      (busbw = algbw * 2(n-1)/n), checked for correctness; plus the hand-written one-shot
-//      peer all-reduce (kernels/allreduce_oneshot.hip) over the same devices for the
-//      latency-bound sizes (8 B .. 256 KiB), verified and timed next to RCCL.
+//      Steps 2-3 run concurrently on every visible device (one host thread per GPU), so an
+//      8-GPU pod's readiness costs about what a 1-GPU pod's does.
+//   4. K3: with >= 2 visible GPUs, the hand-written one-shot peer all-reduce
+//      (kernels/allreduce_oneshot.hip) over every device pair's xGMI link: peer access enabled,
+//      the latency-bound sizes (16 B .. 256 KiB) verified against the host sum and timed. This is
+//      the default multi-GPU check: it needs no communicator, so it adds milliseconds.
+//      --rccl (pod annotation kfamd.io/gpu-readiness-args: "--rccl") additionally builds an RCCL
+//      communicator over all devices (ncclCommInitAll, one process; 5-6 s of code-object loading
+//      in a fresh process) and runs the all-reduce busbw sweep (busbw = algbw * 2(n-1)/n).
 //      --oneshot-sim N runs the one-shot kernel with N ranks simulated on device 0 (1-GPU boxes).
 //   5. KFAMD_READINESS_PROFILE=1 (pod annotation kfamd.io/gpu-readiness-profile: "true"): before
 //      touching the GPU the op re-runs itself as a CHILD under `rocprofv3 --kernel-trace --stats`
@@ -22,7 +26,8 @@
 //
 // Flags: --m/--n/--k GEMM size (default 4096^3), --iters, --ln-rows/--ln-hidden,
 //        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
-//        --oneshot-sim N, --rccl-single (run the RCCL stage with one device).
+//        --oneshot-sim N, --rccl (RCCL sweep on >= 2 GPUs), --rccl-single (RCCL stage with one
+//        device), --serial (devices one after another).
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <rccl/rccl.h>
@@ -35,12 +40,15 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -62,18 +70,26 @@ namespace {
 
 Json g_result = Json::object();
 std::string g_error;
+std::mutex g_error_mu;  // per-device worker threads report failures concurrently
 
-const char* volatile g_stage = "start";
+std::atomic<const char*> g_stage{"start"};
 
 void fail(const std::string& msg) {
+  std::lock_guard<std::mutex> lk(g_error_mu);
   if (g_error.empty()) g_error = msg;
+}
+
+std::string first_error() {
+  std::lock_guard<std::mutex> lk(g_error_mu);
+  return g_error;
 }
 
 // A fault in the op must still leave a diagnosable termination message (the pod's init
 // container status is the only place a notebook user sees it).
 void on_fatal(int sig) {
   char buf[256];
-  int n = std::snprintf(buf, sizeof buf, "kfamd-readiness: fatal signal %d during stage '%s'\n", sig, g_stage);
+  const char* stage = g_stage.load();
+  int n = std::snprintf(buf, sizeof buf, "kfamd-readiness: fatal signal %d during stage '%s'\n", sig, stage);
   ssize_t w = ::write(2, buf, static_cast<size_t>(n));
   (void)w;
   void* frames[64];
@@ -82,7 +98,7 @@ void on_fatal(int sig) {
   if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
     FILE* f = std::fopen(tl, "w");
     if (f) {
-      std::fprintf(f, "{\"ok\":false,\"error\":\"fatal signal %d during %s\"}", sig, g_stage);
+      std::fprintf(f, "{\"ok\":false,\"error\":\"fatal signal %d during %s\"}", sig, stage);
       std::fclose(f);
     }
   }
@@ -127,6 +143,8 @@ struct Args {
   double min_tflops = 0;
   bool skip_ln = false, skip_ar = false;
   bool force_rccl = false;  // --rccl-single: RCCL stage on a 1-GPU pod too (loader smoke)
+  bool rccl = false;        // --rccl: RCCL communicator + busbw sweep on >= 2 GPUs (opt-in)
+  bool serial = false;      // --serial: check devices one after another
   int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
   std::string inject_fault;  // fault injection: fail the op at this stage
 };
@@ -730,6 +748,8 @@ int readiness_main(int argc, char** argv) {
     else if (s == "--skip-ln") a.skip_ln = true;
     else if (s == "--skip-allreduce") a.skip_ar = true;
     else if (s == "--rccl-single") a.force_rccl = true;
+    else if (s == "--rccl") a.rccl = true;
+    else if (s == "--serial") a.serial = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
     else if (const char* v = val("--inject-fault")) a.inject_fault = v;
   }
@@ -744,7 +764,7 @@ int readiness_main(int argc, char** argv) {
         break;
       }
     }
-    if (!a.skip_ar && (a.force_rccl || visible != 1)) {
+    if (!a.skip_ar && (a.force_rccl || (a.rccl && visible != 1))) {
       auto tl = std::chrono::steady_clock::now();
       g_rccl.load();
       g_result["rccl_load_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count();
@@ -765,41 +785,66 @@ int readiness_main(int argc, char** argv) {
   } else if (e != hipSuccess || ndev == 0) {
     fail(std::string("no GPU visible: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices"));
   } else {
-    Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
-    // wall time per stage, summed over devices (where a cold start's milliseconds go)
-    double st_query = 0, st_gemm = 0, st_ln = 0;
+    // one worker per device: query, GEMM check, LayerNorm check (per-device wall times reported)
+    struct DevResult {
+      Json dev = Json(), gemm = Json(), ln = Json();
+      double query_ms = 0, gemm_ms = 0, ln_ms = 0;
+    };
+    std::vector<DevResult> res(ndev);
     auto lap = [](std::chrono::steady_clock::time_point& t) {
       auto now = std::chrono::steady_clock::now();
       double ms = std::chrono::duration<double, std::milli>(now - t).count();
       t = now;
       return ms;
     };
-    for (int d = 0; d < ndev; ++d) {
+    auto check_device = [&](int d) {
+      DevResult& r = res[d];
       g_stage = "device-query";
       auto ts = std::chrono::steady_clock::now();
       hipDeviceProp_t p;
       if (hipGetDeviceProperties(&p, d) == hipSuccess)
-        devs.push_back(Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
-                            {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}});
-      st_query += lap(ts);
+        r.dev = Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
+                     {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}};
+      r.query_ms = lap(ts);
       Json g;
-      if (gemm_check(d, a, g)) gemms.push_back(g);
-      else gemms.push_back(Json{{"device", d}, {"error", g_error}});
-      st_gemm += lap(ts);
+      if (gemm_check(d, a, g)) r.gemm = g;
+      else r.gemm = Json{{"device", d}, {"error", first_error()}};
+      r.gemm_ms = lap(ts);
       if (!a.skip_ln) {
         Json l;
-        if (ln_check(d, a, l)) lns.push_back(l);
-        st_ln += lap(ts);
+        if (ln_check(d, a, l)) r.ln = l;
+        r.ln_ms = lap(ts);
       }
+    };
+    auto tw = std::chrono::steady_clock::now();
+    if (ndev == 1 || a.serial) {
+      for (int d = 0; d < ndev; ++d) check_device(d);
+    } else {
+      std::vector<std::thread> workers;
+      for (int d = 0; d < ndev; ++d) workers.emplace_back(check_device, d);
+      for (auto& w : workers) w.join();
+    }
+    g_result["devices_wall_ms"] = lap(tw);
+    g_result["devices_parallel"] = ndev > 1 && !a.serial;
+    Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
+    double st_query = 0, st_gemm = 0, st_ln = 0;  // summed over devices
+    for (int d = 0; d < ndev; ++d) {
+      if (!res[d].dev.is_null()) devs.push_back(res[d].dev);
+      gemms.push_back(res[d].gemm);
+      if (!res[d].ln.is_null()) lns.push_back(res[d].ln);
+      st_query += res[d].query_ms;
+      st_gemm += res[d].gemm_ms;
+      st_ln += res[d].ln_ms;
     }
     g_result["stages_ms"] = Json{{"device_query", st_query}, {"gemm", st_gemm}, {"layernorm", st_ln}};
     g_result["devices"] = devs;
     g_result["gemm"] = gemms;
     if (!a.skip_ln) g_result["layernorm"] = lns;
     double agg = 0;
-    for (const auto& gm : gemms.as_array()) agg += gm["tflops"].as_double();
+    for (const auto& gm : gemms.as_array())
+      if (gm.has("tflops")) agg += gm["tflops"].as_double();
     g_result["gemm_tflops_aggregate"] = agg;
-    if ((ndev >= 2 || a.force_rccl) && !a.skip_ar) {
+    if (((ndev >= 2 && a.rccl) || a.force_rccl) && !a.skip_ar) {
       Json ar;
       auto ts = std::chrono::steady_clock::now();
       allreduce_check(ndev, a, ar);
@@ -808,11 +853,14 @@ int readiness_main(int argc, char** argv) {
     }
     if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
       Json os;
+      auto ts = std::chrono::steady_clock::now();
       oneshot_check(ndev, a.oneshot_sim, os);
       g_result["allreduce_oneshot"] = os;
+      g_result["stages_ms"]["allreduce_oneshot"] = lap(ts);
     }
   }
   g_stage = "report";
+  g_error = first_error();
   g_result["ok"] = g_error.empty();
   if (!g_error.empty()) g_result["error"] = g_error;
   g_result["total_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -837,6 +885,14 @@ int readiness_main(int argc, char** argv) {
     if (g_result.has("gemm") && g_result["gemm"].size() && g_result["gemm"][0].has("stages"))
       brief["gemm0_stages_ms"] = g_result["gemm"][0]["stages"];
     if (g_result.has("layernorm") && g_result["layernorm"].size()) brief["layernorm_GBps"] = g_result["layernorm"][0]["GBps"];
+    if (g_result.has("devices_wall_ms")) brief["devices_wall_ms"] = g_result["devices_wall_ms"];
+    if (g_result.has("allreduce_oneshot") && g_result["allreduce_oneshot"].has("sweep")) {
+      const Json& os = g_result["allreduce_oneshot"];
+      const Json& sw = os["sweep"];
+      brief["oneshot"] = Json{{"ranks", os["ranks"]}, {"mode", os["mode"]}, {"correct", os["correct"]},
+                              {"us_16B", sw.size() ? sw[0]["us"] : Json()},
+                              {"us_256KiB", sw.size() ? sw[sw.size() - 1]["us"] : Json()}};
+    }
     if (g_result.has("allreduce")) {
       const Json& sw = g_result["allreduce"]["sweep"];
       if (sw.size()) brief["allreduce_busbw_GBps_max"] = sw[sw.size() - 1]["busbw_GBps"];

@@ -1,0 +1,61 @@
+"""bench.py contract on the CPU: ``python bench.py --gpus N`` without a launcher starts N ranks
+itself, each with its own RANK and the shared private rendezvous, exactly one
+JSON line comes out (rank 0), and a failing rank fails the whole run."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+_STUB = r"""
+import json, os, sys
+d = sys.argv[1]
+r = int(os.environ["RANK"])
+open(os.path.join(d, "rank%d" % r), "w").write(json.dumps({k: os.environ[k] for k in
+    ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}))
+if os.environ.get("STUB_FAIL_RANK") == str(r):
+    sys.exit(3)
+if r == 0:
+    print(json.dumps({"metric": "stub", "n_gpus": int(os.environ["WORLD_SIZE"])}), flush=True)
+"""
+
+
+def _run(tmp_path, n, extra_env=None):
+    stub = tmp_path / "stub.py"
+    stub.write_text(_STUB)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    env["KFAMD_BENCH_RANK_ARGV"] = json.dumps([sys.executable, str(stub), str(tmp_path)])
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--steps", "1", "--warmup", "0"],
+                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+
+
+def test_bench_self_launches_n_ranks(tmp_path):
+    p = _run(tmp_path, 4)
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 4
+    ranks = [json.loads((tmp_path / f"rank{r}").read_text()) for r in range(4)]
+    assert sorted(int(x["RANK"]) for x in ranks) == [0, 1, 2, 3]
+    assert all(x["WORLD_SIZE"] == "4" and x["LOCAL_RANK"] == x["RANK"] for x in ranks)
+    assert len({(x["MASTER_ADDR"], x["MASTER_PORT"]) for x in ranks}) == 1
+
+
+def test_bench_rank_failure_fails_the_run(tmp_path):
+    p = _run(tmp_path, 2, {"STUB_FAIL_RANK": "1"})
+    assert p.returncode == 3, (p.returncode, p.stderr)
+
+
+def test_launch_cli_runs_program_per_rank(tmp_path):
+    stub = tmp_path / "stub.py"
+    stub.write_text(_STUB)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    env.update({"LOCAL_WORLD_SIZE": "3", "MASTER_ADDR": "127.0.0.9", "MASTER_PORT": "29999"})
+    p = subprocess.run([sys.executable, "-m", "kubeflow_rm_amd.parallel.launch", "--", str(stub), str(tmp_path)],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    ranks = [json.loads((tmp_path / f"rank{r}").read_text()) for r in range(3)]
+    # the pod's injected rendezvous is used as is
+    assert all(x["MASTER_ADDR"] == "127.0.0.9" and x["MASTER_PORT"] == "29999" for x in ranks)

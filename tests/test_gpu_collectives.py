@@ -4,6 +4,7 @@ On the single-GPU test box the ranks are simulated on one device in ONE launch (
 the barrier protocol, vector/tail paths, epoch reuse and the timeout drain all run on the hardware.
 """
 import ctypes
+import time
 
 import pytest
 import torch
@@ -58,12 +59,21 @@ def test_oneshot_missing_peer_times_out_instead_of_hanging():
              for _ in range(2)]
     tmo = torch.zeros(1, dtype=torch.int32, device="cuda")
     arr = ctypes.c_void_p * 8
-    rc = L.kfamd_allreduce_oneshot(arr(*[t.data_ptr() for t in ins]), arr(*[t.data_ptr() for t in outs]),
-                                   arr(*[t.data_ptr() for t in flags]), 2, 0, 1, n, 0, 1, nb, tmo.data_ptr(),
-                                   torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
-    torch.cuda.synchronize()  # rank 1 never launched: both barriers give up, the kernel drains
+    L.kfamd_allreduce_oneshot_set_timeout_ms(200)
+    try:
+        t0 = time.perf_counter()
+        rc = L.kfamd_allreduce_oneshot(arr(*[t.data_ptr() for t in ins]), arr(*[t.data_ptr() for t in outs]),
+                                       arr(*[t.data_ptr() for t in flags]), 2, 0, 1, n, 0, 1, nb, tmo.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()  # rank 1 never launched: the entry barrier gives up, the kernel drains
+        dt = time.perf_counter() - t0
+    finally:
+        L.kfamd_allreduce_oneshot_set_timeout_ms(5000)
     assert tmo.item() == 1
+    assert 0.15 < dt < 3.0, dt  # wall-clock deadline, not a spin count
+    # a timed-out call never looks like a result: rank 0's output is NaN-poisoned, not a stale sum
+    assert torch.isnan(outs[0]).all().item()
 
 
 def test_oneshot_rejects_bad_arguments():
@@ -104,6 +114,49 @@ def _ipc_worker(rank):
     ar.close()
     dist.destroy_process_group()
     return out
+
+
+def _ipc_late_worker(rank, sleep_s, timeout_ms):
+    import torch.distributed as dist
+    from kubeflow_rm_amd.parallel.oneshot import IpcOneShotAllReduce, OneShotTimeout
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    ar = IpcOneShotAllReduce(max_bytes=1 << 16, timeout_ms=timeout_ms, check_every=1)
+    res = {"ok": None, "raised": False}
+    t = torch.full((1024,), float(rank + 1), device="cuda")
+    if rank == 1:
+        time.sleep(sleep_s)  # host-side skew: GC pause, logging, checkpointing on one TP rank
+    try:
+        ar(t)
+        torch.cuda.synchronize()
+        res["ok"] = bool(torch.all(t == 3.0).item())
+    except OneShotTimeout:
+        res["raised"] = True
+        res["nan"] = bool(torch.isnan(t).all().item())
+        try:
+            ar(t)
+        except OneShotTimeout:
+            res["refuses_after"] = True
+    dist.barrier()
+    ar.close()
+    dist.destroy_process_group()
+    return res
+
+
+def test_ipc_oneshot_tolerates_half_second_host_skew():
+    """a 0.5 s late rank must not corrupt the sum (the deadline is wall clock, 5 s)."""
+    from kubeflow_rm_amd.parallel.launch import spawn
+    for r in spawn(_ipc_late_worker, 2, 0.5, 5000, timeout=180):
+        assert r["raised"] is False and r["ok"] is True, r
+
+
+def test_ipc_oneshot_timeout_is_fatal_not_silent():
+    """A peer later than the deadline: NaN output + OneShotTimeout, and the communicator refuses
+    further calls instead of running with out-of-step flags."""
+    from kubeflow_rm_amd.parallel.launch import spawn
+    res = spawn(_ipc_late_worker, 2, 1.5, 200, timeout=180)
+    r0 = res[0]
+    assert r0["raised"] is True and r0["nan"] is True and r0.get("refuses_after") is True, r0
 
 
 def test_ipc_oneshot_two_ranks_as_processes():

@@ -1,5 +1,7 @@
-"""DP / TP wiring on the CPU (gloo, world_size 2): the same code paths the multi-GPU notebook runs
-over RCCL, checked for exact equivalence with the single-process model."""
+"""DP / TP wiring on the CPU (gloo, world_size 2 / 4 / 8 — one xGMI hive's worth of ranks): the
+same code paths the multi-GPU notebook runs over RCCL, checked for exact equivalence with the
+single-process model."""
+import pytest
 import torch
 
 from kubeflow_rm_amd.parallel.launch import spawn
@@ -7,7 +9,7 @@ from kubeflow_rm_amd.parallel.launch import spawn
 
 def _tiny_cfg():
     from kubeflow_rm_amd.models import GPTConfig
-    return GPTConfig(vocab_size=64, d_model=32, n_layers=2, n_heads=4, d_ff=64, max_seq=16, dtype=torch.float32)
+    return GPTConfig(vocab_size=64, d_model=32, n_layers=2, n_heads=8, d_ff=64, max_seq=16, dtype=torch.float32)
 
 
 def _tp_worker(rank):
@@ -27,7 +29,8 @@ def _tp_worker(rank):
     return out
 
 
-def test_tensor_parallel_matches_single_process():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tensor_parallel_matches_single_process(world):
     from kubeflow_rm_amd.models import GPT
     torch.manual_seed(0)
     idx = torch.randint(0, 64, (2, 8))
@@ -35,7 +38,8 @@ def test_tensor_parallel_matches_single_process():
     ref = GPT(_tiny_cfg())
     logits, loss = ref(idx, tgt)
     loss.backward()
-    outs = spawn(_tp_worker, 2)
+    outs = spawn(_tp_worker, world)
+    assert len(outs) == world
     for o in outs:
         assert torch.allclose(torch.from_numpy(o["logits"]), logits.detach(), atol=1e-5, rtol=1e-4)
         assert abs(o["loss"] - loss.item()) < 1e-5
@@ -67,8 +71,9 @@ def _dp_worker(rank):
     return grads, ref, nb
 
 
-def test_bucketed_data_parallel_grads():
-    for grads, ref, nbuckets in spawn(_dp_worker, 2):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bucketed_data_parallel_grads(world):
+    for grads, ref, nbuckets in spawn(_dp_worker, world):
         assert nbuckets > 1
         for g, r in zip(grads, ref):
             assert torch.allclose(torch.from_numpy(g), torch.from_numpy(r), atol=1e-6)
@@ -85,3 +90,90 @@ def _coll_worker(rank):
 def test_allreduce_sweep_gloo():
     res = spawn(_coll_worker, 2)
     assert len(res[0]) >= 4 and all(x["busbw_GBps"] >= 0 for x in res[0])
+
+
+class _Branchy(torch.nn.Module):
+    """Conditional compute (MoE-like): each rank routes through a different subset of experts, so
+    ranks see gradients for different parameter subsets (and some buckets get none at all)."""
+
+    def __init__(self):
+        super().__init__()
+        self.inp = torch.nn.Linear(8, 8)
+        self.experts = torch.nn.ModuleList(torch.nn.Linear(8, 8) for _ in range(4))
+        self.out = torch.nn.Linear(8, 4)
+
+    def forward(self, x, use):
+        h = self.inp(x)
+        for i in use:
+            h = h + self.experts[i](h)
+        return self.out(h)
+
+
+def _dp_branchy_worker(rank):
+    import torch.distributed as dist
+    from kubeflow_rm_amd import parallel
+    parallel.init(backend="gloo")
+    torch.manual_seed(7)
+    net = _Branchy()
+    dp = parallel.DataParallel(net, bucket_mb=400 / 2**20)  # 400 B: one Linear (288 B) per bucket
+    uses = {0: [0], 1: [2, 3], 2: [], 3: [1, 3]}
+    x = torch.randn(3, 8, generator=torch.Generator().manual_seed(rank))
+    orders = []
+    for step in range(2):  # twice: state must reset between steps
+        net.zero_grad(set_to_none=True)
+        dp(x, uses[(rank + step) % 4]).sum().backward()
+        orders.append(dp.bucketer.last_launch_order)
+    grads = [p.grad.clone() for p in net.parameters()]
+    # reference: the same step without the bucketer, grads zero-filled and averaged explicitly
+    net2 = _Branchy()
+    net2.load_state_dict(net.state_dict())
+    net2(x, uses[(rank + 1) % 4]).sum().backward()
+    ref = []
+    for p in net2.parameters():
+        g = p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+        dist.all_reduce(g)
+        ref.append(g / dist.get_world_size())
+    nb = len(dp.bucketer.buckets)
+    parallel.shutdown()
+    return {"grads": grads, "ref": ref, "orders": orders, "nb": nb}
+
+
+def test_data_parallel_conditional_grads_keep_collective_order():
+    """ranks with different grad subsets must issue the same collective sequence."""
+    res = spawn(_dp_branchy_worker, 4, timeout=120)
+    nb = res[0]["nb"]
+    assert nb >= 4
+    for r in res:
+        for order in r["orders"]:
+            assert order == list(range(nb)), order  # strictly in index order, every bucket, every rank
+        for g, ref in zip(r["grads"], r["ref"]):
+            assert torch.allclose(torch.from_numpy(g), torch.from_numpy(ref), atol=1e-6)
+
+
+def _ring_worker(rank):
+    from kubeflow_rm_amd.parallel import dist as kd
+    env = kd.init(backend="gloo")
+    import torch.distributed as dist
+    t = torch.tensor([float(kd.device_for_local_rank(env.local_rank))])
+    gathered = [torch.zeros(1) for _ in range(env.world_size)]
+    dist.all_gather(gathered, t)
+    kd.shutdown()
+    return [int(g.item()) for g in gathered]
+
+
+def test_xgmi_ring_order_maps_local_rank_to_ring_position():
+    """KFAMD_XGMI_RING (pod-local ordinals, from the kubelet's placement) decides which device
+    each local rank drives: RCCL rank neighbours are then xGMI-link neighbours."""
+    ring = [3, 1, 0, 2]
+    res = spawn(_ring_worker, 4, env={"KFAMD_XGMI_RING": ",".join(map(str, ring))})
+    assert all(r == ring for r in res)
+
+
+def test_dist_init_refuses_shared_default_port(monkeypatch):
+    from kubeflow_rm_amd.parallel import dist as kd
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.delenv("MASTER_PORT", raising=False)
+    monkeypatch.setattr(kd, "_ENV", None)
+    with pytest.raises(RuntimeError, match="MASTER_PORT"):
+        kd.init(backend="gloo")
