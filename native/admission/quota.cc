@@ -1,6 +1,9 @@
 // quota.cc — ResourceQuota admission + status controller with MI355X GPU / HBM accounting (K7).
 #include <algorithm>
 #include <cmath>
+#include <memory>
+#include <mutex>
+#include <set>
 
 #include "admission/admission.h"
 #include "controllers/common.h"
@@ -68,18 +71,82 @@ std::string fmt_num(double v) {
 }
 }  // namespace
 
+// Quota admission is check-then-commit, and the commit happens after admission returns. Two
+// concurrent creates in one namespace would both see the same committed pods and both pass, so
+// each admitted pod holds a reservation in this ledger from its check until it is visible in the
+// store: the check and the reservation are one critical section per namespace, and the usage it
+// checks against is committed pods + every other live reservation. A reservation ends when the
+// request's completion hook fires (in-process API server: committed or not), when the pod shows
+// up in the namespace's pod list (webhook mode, where no completion hook exists), or after
+// kReservationTtl (a webhook-admitted create that the API server then failed).
+// Reference quota semantics: profile-controller/controllers/profile_controller.go:559-589
+// (the Profile's ResourceQuota) enforced by kube-apiserver's quota admission.
+namespace {
+constexpr double kReservationTtl = 30.0;
+
+struct QuotaLedger {
+  struct Reservation {
+    std::map<std::string, double> use;
+    double expires;
+  };
+  std::mutex mu;
+  std::map<std::string, std::map<std::string, Reservation>> by_ns;  // ns -> pod name -> usage
+  std::map<std::string, std::unique_ptr<std::mutex>> ns_locks;
+
+  std::mutex& ns_lock(const std::string& ns) {
+    std::lock_guard<std::mutex> g(mu);
+    auto& m = ns_locks[ns];
+    if (!m) m = std::make_unique<std::mutex>();
+    return *m;
+  }
+  // live reservations of ns other than pods already in `committed`; drops expired / landed ones
+  std::vector<std::map<std::string, double>> live(const std::string& ns, const std::set<std::string>& committed) {
+    std::lock_guard<std::mutex> g(mu);
+    std::vector<std::map<std::string, double>> out;
+    auto it = by_ns.find(ns);
+    if (it == by_ns.end()) return out;
+    const double now = now_seconds();
+    for (auto r = it->second.begin(); r != it->second.end();) {
+      if (r->second.expires < now || committed.count(r->first)) {
+        r = it->second.erase(r);
+      } else {
+        out.push_back(r->second.use);
+        ++r;
+      }
+    }
+    return out;
+  }
+  void reserve(const std::string& ns, const std::string& name, std::map<std::string, double> use) {
+    std::lock_guard<std::mutex> g(mu);
+    by_ns[ns][name] = Reservation{std::move(use), now_seconds() + kReservationTtl};
+  }
+  void release(const std::string& ns, const std::string& name) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = by_ns.find(ns);
+    if (it != by_ns.end()) it->second.erase(name);
+  }
+};
+}  // namespace
+
 AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
-  return [c, hbm](AdmissionAttrs& a) -> ApiError {
+  auto ledger = std::make_shared<QuotaLedger>();
+  return [c, hbm, ledger](AdmissionAttrs& a) -> ApiError {
     if (a.operation != "CREATE" || a.res->kind != "Pod" || !a.res->group.empty() || !a.object) return {};
     Json quotas;
     if (c->list("v1", "ResourceQuota", a.ns, ListOptions(), quotas)) return {};
     if (quotas["items"].empty()) return {};
+    std::lock_guard<std::mutex> serial(ledger->ns_lock(a.ns));
     Json pods;
     c->list("v1", "Pod", a.ns, ListOptions(), pods);
     std::map<std::string, double> used;
-    for (const auto& p : pods["items"].as_array())
+    std::set<std::string> committed;
+    for (const auto& p : pods["items"].as_array()) {
+      committed.insert(p.str_at({"metadata", "name"}));
       if (pod_counts(p))
         for (auto& kv : pod_quota_usage(p, hbm)) used[kv.first] += kv.second;
+    }
+    for (const auto& r : ledger->live(a.ns, committed))
+      for (const auto& kv : r) used[kv.first] += kv.second;
     auto want = pod_quota_usage(*a.object, hbm);
     for (const auto& q : quotas["items"].as_array()) {
       std::vector<std::string> exceeded;
@@ -95,6 +162,11 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
         return ApiError{403, "Forbidden", "pods \"" + a.name + "\" is forbidden: exceeded quota: " + q.str_at({"metadata", "name"}) +
                                               ", requested: " + join(exceeded, "; ")};
     }
+    if (a.dry_run) return {};
+    ledger->reserve(a.ns, a.name, std::move(want));
+    const std::string ns = a.ns, name = a.name;
+    // in-process: the pod is in the store (its list entry replaces the reservation) or never will be
+    a.on_done.push_back([ledger, ns, name](bool) { ledger->release(ns, name); });
     return {};
   };
 }

@@ -236,7 +236,9 @@ std::string ApiServer::inject_fault(const std::string& spec) {
   f.plural = parts[1];
   f.count = std::atoi(parts[2].c_str());
   f.arg = parts.size() > 3 ? std::atoll(parts[3].c_str()) : 0;
-  if (f.kind != "conflict" && f.kind != "error" && f.kind != "delay" && f.kind != "dropwatch")
+  // commitdelay: sleep arg ms between admission and the store commit of a create (widens the
+  // check-then-commit window for admission race tests)
+  if (f.kind != "conflict" && f.kind != "error" && f.kind != "delay" && f.kind != "dropwatch" && f.kind != "commitdelay")
     return "unknown fault kind " + f.kind;
   std::lock_guard<std::mutex> g(fault_mu_);
   faults_.push_back(f);
@@ -649,6 +651,14 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
   a.object = &obj;
   a.user = &o.user;
   a.dry_run = o.dry_run;
+  // fires every admission completion hook on every exit path below
+  struct DoneGuard {
+    AdmissionAttrs& a;
+    bool committed = false;
+    ~DoneGuard() {
+      for (auto& f : a.on_done) f(committed);
+    }
+  } done{a};
   err = run_admission(a, true);
   if (err) return err;
   apply_defaults(res, obj, false);  // mutating admission may add containers: default them too
@@ -659,6 +669,7 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
   if (err) return err;
   err = run_admission(a, false);
   if (err) return err;
+  if (take_fault("commitdelay", res->plural, &delay)) ::usleep(static_cast<useconds_t>(delay * 1000));
 
   const std::string name = obj.str_at({"metadata", "name"});
   const std::string key = object_key(ns, name);
@@ -674,6 +685,7 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
     md2.erase("resourceVersion");
     if (!o.dry_run) {
       commit_put(res, key, obj, "ADDED");
+      done.committed = true;
     } else {
       obj["metadata"]["resourceVersion"] = std::to_string(rv_);
     }

@@ -120,6 +120,9 @@ struct AdmissionAttrs {
   const Json* old_object = nullptr;  // UPDATE/DELETE
   const UserInfo* user = nullptr;
   bool dry_run = false;
+  // Called once when the request ends (true = object committed, false = rejected / failed / dry
+  // run). Lets an admission plugin hold a reservation across the check -> commit window (quota).
+  std::vector<std::function<void(bool committed)>> on_done;
 };
 using AdmissionFn = std::function<ApiError(AdmissionAttrs&)>;
 using LogProvider = std::function<bool(const std::string& ns, const std::string& pod, const std::string& container,

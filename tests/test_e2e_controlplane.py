@@ -190,3 +190,50 @@ def test_profile_rejects_foreign_namespace(c):
                    lambda o: any(x["type"] == "Failed" for x in (o.get("status") or {}).get("conditions", [])), timeout=10)
     assert "not owned by profile creator" in p["status"]["conditions"][0]["message"]
     assert not c.exists("rbac.authorization.k8s.io/v1", "RoleBinding", "namespaceAdmin", "taken")
+
+
+@pytest.mark.parametrize("hard_key,hard,per_pod,admitted", [
+    ("amd.com/gpu", "2", {"amd.com/gpu": "1"}, 2),
+    # HBM quota in GiB: 3 x 288 GiB fits in 900, the 4th does not
+    ("amd.com/gpu-memory", "900", {"amd.com/gpu": "1"}, 3),
+])
+def test_concurrent_pod_creates_never_overcommit_quota(c, cluster, hard_key, hard, per_pod, admitted):
+    """K7: 16 concurrent 1-GPU pod creates against one ResourceQuota admit exactly the quota
+    (admission reserves under a per-namespace lock until the pod is in the store). Every create
+    sleeps 50 ms between admission and commit (``commitdelay`` fault), so without the reservation
+    all 16 would pass the check against the same committed pods."""
+    import concurrent.futures as cf
+    ns = "qrace-" + hard_key.replace("amd.com/", "").replace("-", "")
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+    c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q", "namespace": ns},
+              "spec": {"hard": {hard_key: hard}}})
+
+    def create(i):
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"p{i}", "namespace": ns},
+               # unschedulable on purpose: the pods stay Pending (and keep counting against the quota)
+               "spec": {"nodeSelector": {"kfamd.io/no-such-node": "true"},
+                        "containers": [{"name": "x", "image": "x", "resources": {"limits": dict(per_pod)}}]}}
+        try:
+            c.create(pod)
+            return True
+        except ApiException as e:
+            assert e.status == 403 and "exceeded quota" in str(e.body), (e.status, e.body)
+            return False
+
+    req = urllib.request.Request(cluster.url + "/debug/faults", data=json.dumps({"spec": "commitdelay:pods:24:50"}).encode(),
+                                 method="POST", headers={"Content-Type": "application/json"})
+    urllib.request.urlopen(req, timeout=5).close()
+    try:
+        with cf.ThreadPoolExecutor(16) as ex:
+            results = list(ex.map(create, range(16)))
+    finally:
+        urllib.request.urlopen(urllib.request.Request(cluster.url + "/debug/faults", method="DELETE"), timeout=5).close()
+    assert sum(results) == admitted, results
+    assert len(c.list("v1", "Pod", ns)["items"]) == admitted
+    # a rejected-then-freed slot: deleting one admitted pod lets exactly one more in
+    victim = c.list("v1", "Pod", ns)["items"][0]["metadata"]["name"]
+    c.delete("v1", "Pod", victim, ns)
+    c.wait_gone("v1", "Pod", victim, ns, timeout=15)
+    with cf.ThreadPoolExecutor(8) as ex:
+        results = list(ex.map(create, range(100, 108)))
+    assert sum(results) == 1, results
