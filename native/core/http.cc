@@ -8,7 +8,12 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <signal.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/types.h>
 #include <unistd.h>
 
@@ -116,39 +121,107 @@ void Router::dispatch(HttpRequest& req, HttpResponse& resp) const {
   }
 }
 
-// ---- socket helpers ---------------------------------------------------------------------------
+// ---- connections (plain TCP or TLS) -------------------------------------------------------------
 namespace {
 
-bool send_all(int fd, const char* data, size_t n) {
-  while (n > 0) {
-    ssize_t w = ::send(fd, data, n, MSG_NOSIGNAL);
-    if (w < 0) {
-      if (errno == EINTR) continue;
-      return false;
-    }
-    data += w;
-    n -= static_cast<size_t>(w);
+std::string tls_error(const std::string& what) {
+  std::string out = what;
+  unsigned long e;
+  while ((e = ERR_get_error()) != 0) {
+    char buf[256];
+    ERR_error_string_n(e, buf, sizeof buf);
+    out += std::string(": ") + buf;
   }
-  return true;
+  return out;
 }
-bool send_all(int fd, const std::string& s) { return send_all(fd, s.data(), s.size()); }
 
-// Buffered reader over a socket.
+class Conn : public RawConn {
+ public:
+  Conn(int fd, SSL* ssl, bool own_fd) : fd_(fd), ssl_(ssl), own_fd_(own_fd) {}
+  using RawConn::write;
+  ~Conn() override {
+    if (ssl_) {
+      SSL_shutdown(ssl_);
+      SSL_free(ssl_);
+    }
+    if (own_fd_ && fd_ >= 0) ::close(fd_);
+  }
+  long read(char* buf, size_t n) override {
+    for (;;) {
+      if (!ssl_) {
+        ssize_t r = ::recv(fd_, buf, n, 0);
+        if (r < 0 && errno == EINTR) continue;
+        return static_cast<long>(r);
+      }
+      ERR_clear_error();
+      errno = 0;
+      int r = SSL_read(ssl_, buf, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+      if (r > 0) return r;
+      int e = SSL_get_error(ssl_, r);
+      if (e == SSL_ERROR_ZERO_RETURN) return 0;
+      if (e == SSL_ERROR_SYSCALL && errno == EINTR) continue;
+      if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) {
+        errno = EAGAIN;  // receive timeout on the blocking socket
+        return -1;
+      }
+      if (e == SSL_ERROR_SYSCALL && errno == 0) return 0;  // peer closed without close_notify
+      return -1;
+    }
+  }
+  bool write(const char* p, size_t n) override {
+    while (n > 0) {
+      if (!ssl_) {
+        ssize_t w = ::send(fd_, p, n, MSG_NOSIGNAL);
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          return false;
+        }
+        p += w;
+        n -= static_cast<size_t>(w);
+        continue;
+      }
+      ERR_clear_error();
+      int w = SSL_write(ssl_, p, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+      if (w <= 0) {
+        int e = SSL_get_error(ssl_, w);
+        if (e == SSL_ERROR_SYSCALL && errno == EINTR) continue;
+        return false;
+      }
+      p += w;
+      n -= static_cast<size_t>(w);
+    }
+    return true;
+  }
+  int fd() const override { return fd_; }
+  bool has_buffered() const override { return ssl_ && SSL_pending(ssl_) > 0; }
+  void set_timeout_ms(int ms) override {
+    struct timeval tv;
+    tv.tv_sec = ms / 1000;
+    tv.tv_usec = (ms % 1000) * 1000;
+    ::setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    ::setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+  }
+
+ private:
+  int fd_;
+  SSL* ssl_;
+  bool own_fd_;
+};
+
+// Buffered reader over a connection.
 class Reader {
  public:
-  explicit Reader(int fd) : fd_(fd) {}
+  explicit Reader(RawConn& c) : c_(c) {}
   // returns false on EOF/error/timeout
   bool fill() {
     char tmp[16384];
-    for (;;) {
-      ssize_t r = ::recv(fd_, tmp, sizeof tmp, 0);
-      if (r > 0) {
-        buf_.append(tmp, static_cast<size_t>(r));
-        return true;
-      }
-      if (r < 0 && errno == EINTR) continue;
-      return false;
+    long r = c_.read(tmp, sizeof tmp);
+    if (r > 0) {
+      buf_.append(tmp, static_cast<size_t>(r));
+      return true;
     }
+    last_timeout_ = r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK);
+    return false;
   }
   bool read_line(std::string& line, size_t max = 1 << 20) {
     for (;;) {
@@ -178,15 +251,35 @@ class Reader {
     pos_ = 0;
     char tmp[16384];
     for (;;) {
-      ssize_t r = ::recv(fd_, tmp, sizeof tmp, 0);
+      long r = c_.read(tmp, sizeof tmp);
       if (r > 0) {
         out.append(tmp, static_cast<size_t>(r));
         continue;
       }
-      if (r < 0 && errno == EINTR) continue;
       return r == 0;
     }
   }
+  // up to max buffered bytes (reading once from the connection when none are buffered)
+  int read_some(std::string& out, size_t max) {
+    if (buf_.size() == pos_) {
+      buf_.clear();
+      pos_ = 0;
+      if (!fill()) return last_timeout_ ? -2 : 0;
+    }
+    size_t take = std::min(max, buf_.size() - pos_);
+    out.append(buf_, pos_, take);
+    pos_ += take;
+    compact();
+    return static_cast<int>(take);
+  }
+  std::string take_buffered() {
+    std::string out = buf_.substr(pos_);
+    buf_.clear();
+    pos_ = 0;
+    return out;
+  }
+  size_t buffered() const { return buf_.size() - pos_; }
+  bool last_timeout() const { return last_timeout_; }
 
  private:
   void compact() {
@@ -195,9 +288,10 @@ class Reader {
       pos_ = 0;
     }
   }
-  int fd_;
+  RawConn& c_;
   std::string buf_;
   size_t pos_ = 0;
+  bool last_timeout_ = false;
 };
 
 bool read_headers(Reader& rd, Headers& h) {
@@ -246,31 +340,31 @@ void parse_query(const std::string& raw, std::map<std::string, std::vector<std::
 
 class ChunkWriter : public StreamWriter {
  public:
-  explicit ChunkWriter(int fd) : fd_(fd) {}
+  explicit ChunkWriter(RawConn& c) : c_(c) {}
   bool write(const std::string& data) override {
     if (dead_) return false;
     if (data.empty()) return true;
     char hdr[32];
     std::snprintf(hdr, sizeof hdr, "%zx\r\n", data.size());
-    if (!send_all(fd_, hdr) || !send_all(fd_, data) || !send_all(fd_, "\r\n")) dead_ = true;
+    if (!c_.write(std::string(hdr) + data + "\r\n")) dead_ = true;
     return !dead_;
   }
   bool alive() override {
     if (dead_) return false;
-    struct pollfd p {fd_, POLLIN | POLLRDHUP, 0};
+    struct pollfd p {c_.fd(), POLLIN | POLLRDHUP, 0};
     int r = ::poll(&p, 1, 0);
     if (r > 0 && (p.revents & (POLLHUP | POLLERR | POLLRDHUP))) dead_ = true;
     if (r > 0 && (p.revents & POLLIN)) {
       char c;
-      ssize_t n = ::recv(fd_, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+      ssize_t n = ::recv(c_.fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT);
       if (n == 0) dead_ = true;
     }
     return !dead_;
   }
-  bool finish() { return !dead_ && send_all(fd_, "0\r\n\r\n"); }
+  bool finish() { return !dead_ && c_.write("0\r\n\r\n"); }
 
  private:
-  int fd_;
+  RawConn& c_;
   bool dead_ = false;
 };
 
@@ -350,11 +444,189 @@ void set_timeouts(int fd, int ms) {
   ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
 }
 
+
+std::shared_ptr<SSL_CTX> make_server_ctx(const TlsServerConfig& c, std::string* err) {
+  std::shared_ptr<SSL_CTX> ctx(SSL_CTX_new(TLS_server_method()), SSL_CTX_free);
+  if (!ctx) {
+    if (err) *err = tls_error("SSL_CTX_new");
+    return nullptr;
+  }
+  SSL_CTX_set_min_proto_version(ctx.get(), TLS1_2_VERSION);
+  if (SSL_CTX_use_certificate_chain_file(ctx.get(), c.cert_file.c_str()) != 1) {
+    if (err) *err = tls_error("load certificate " + c.cert_file);
+    return nullptr;
+  }
+  if (SSL_CTX_use_PrivateKey_file(ctx.get(), c.key_file.c_str(), SSL_FILETYPE_PEM) != 1 ||
+      SSL_CTX_check_private_key(ctx.get()) != 1) {
+    if (err) *err = tls_error("load private key " + c.key_file);
+    return nullptr;
+  }
+  if (!c.client_ca_file.empty()) {
+    if (SSL_CTX_load_verify_locations(ctx.get(), c.client_ca_file.c_str(), nullptr) != 1) {
+      if (err) *err = tls_error("load client CA " + c.client_ca_file);
+      return nullptr;
+    }
+    SSL_CTX_set_verify(ctx.get(), SSL_VERIFY_PEER | (c.require_client_cert ? SSL_VERIFY_FAIL_IF_NO_PEER_CERT : 0), nullptr);
+  }
+  return ctx;
+}
+
+// client contexts, cached per option set (loading a CA bundle costs milliseconds)
+std::mutex& tls_client_mu() {
+  static std::mutex m;
+  return m;
+}
+TlsClientOptions& tls_client_default() {
+  static TlsClientOptions o;
+  return o;
+}
+std::shared_ptr<SSL_CTX> client_ctx(const TlsClientOptions& o, std::string* err) {
+  static std::map<std::string, std::shared_ptr<SSL_CTX>> cache;
+  const std::string key = o.ca_file + '\0' + o.ca_pem + '\0' + o.cert_file + '\0' + o.key_file + '\0' +
+                          (o.insecure_skip_verify ? "1" : "0");
+  std::lock_guard<std::mutex> g(tls_client_mu());
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  std::shared_ptr<SSL_CTX> ctx(SSL_CTX_new(TLS_client_method()), SSL_CTX_free);
+  if (!ctx) {
+    if (err) *err = tls_error("SSL_CTX_new");
+    return nullptr;
+  }
+  SSL_CTX_set_min_proto_version(ctx.get(), TLS1_2_VERSION);
+  if (o.insecure_skip_verify) {
+    SSL_CTX_set_verify(ctx.get(), SSL_VERIFY_NONE, nullptr);
+  } else {
+    SSL_CTX_set_verify(ctx.get(), SSL_VERIFY_PEER, nullptr);
+    bool loaded = false;
+    if (!o.ca_file.empty()) {
+      if (SSL_CTX_load_verify_locations(ctx.get(), o.ca_file.c_str(), nullptr) != 1) {
+        if (err) *err = tls_error("load CA bundle " + o.ca_file);
+        return nullptr;
+      }
+      loaded = true;
+    }
+    if (!o.ca_pem.empty()) {
+      std::unique_ptr<BIO, decltype(&BIO_free)> bio(BIO_new_mem_buf(o.ca_pem.data(), static_cast<int>(o.ca_pem.size())),
+                                                    BIO_free);
+      X509_STORE* store = SSL_CTX_get_cert_store(ctx.get());
+      int n = 0;
+      while (X509* x = PEM_read_bio_X509(bio.get(), nullptr, nullptr, nullptr)) {
+        X509_STORE_add_cert(store, x);
+        X509_free(x);
+        ++n;
+      }
+      ERR_clear_error();  // the read loop ends on a "no start line" error
+      if (n == 0) {
+        if (err) *err = "CA bundle holds no PEM certificate";
+        return nullptr;
+      }
+      loaded = true;
+    }
+    if (!loaded) SSL_CTX_set_default_verify_paths(ctx.get());
+  }
+  if (!o.cert_file.empty()) {
+    if (SSL_CTX_use_certificate_chain_file(ctx.get(), o.cert_file.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(ctx.get(), (o.key_file.empty() ? o.cert_file : o.key_file).c_str(), SSL_FILETYPE_PEM) != 1) {
+      if (err) *err = tls_error("load client certificate " + o.cert_file);
+      return nullptr;
+    }
+  }
+  cache[key] = ctx;
+  return ctx;
+}
+
+bool is_ip_literal(const std::string& host) {
+  struct in_addr a4;
+  struct in6_addr a6;
+  return ::inet_pton(AF_INET, host.c_str(), &a4) == 1 || ::inet_pton(AF_INET6, host.c_str(), &a6) == 1;
+}
+
+// connect + (https) handshake with hostname verification against the URL's host
+std::unique_ptr<Conn> open_conn(const Url& u, int timeout_ms, std::string* err, const TlsClientOptions* tls) {
+  if (u.scheme != "http" && u.scheme != "https") {
+    if (err) *err = "unsupported scheme " + u.scheme;
+    return nullptr;
+  }
+  int fd = connect_to(u.host, u.port, timeout_ms, err);
+  if (fd < 0) return nullptr;
+  set_timeouts(fd, timeout_ms);
+  if (u.scheme == "http") return std::make_unique<Conn>(fd, nullptr, true);
+  TlsClientOptions opts = tls ? *tls : default_tls_client();
+  auto ctx = client_ctx(opts, err);
+  if (!ctx) {
+    ::close(fd);
+    return nullptr;
+  }
+  SSL* ssl = SSL_new(ctx.get());
+  SSL_set_fd(ssl, fd);
+  if (!is_ip_literal(u.host)) SSL_set_tlsext_host_name(ssl, u.host.c_str());
+  if (!opts.insecure_skip_verify) {
+    X509_VERIFY_PARAM* vp = SSL_get0_param(ssl);
+    if (is_ip_literal(u.host)) X509_VERIFY_PARAM_set1_ip_asc(vp, u.host.c_str());
+    else X509_VERIFY_PARAM_set1_host(vp, u.host.c_str(), 0);
+  }
+  ERR_clear_error();
+  if (SSL_connect(ssl) != 1) {
+    long vr = SSL_get_verify_result(ssl);
+    if (err) {
+      *err = vr != X509_V_OK ? std::string("tls: certificate verify failed: ") + X509_verify_cert_error_string(vr)
+                             : tls_error("tls handshake with " + u.host);
+    }
+    SSL_free(ssl);
+    ::close(fd);
+    return nullptr;
+  }
+  return std::make_unique<Conn>(fd, ssl, true);
+}
+
 }  // namespace
+
+void set_default_tls_client(const TlsClientOptions& o) {
+  std::lock_guard<std::mutex> g(tls_client_mu());
+  tls_client_default() = o;
+}
+TlsClientOptions default_tls_client() {
+  std::lock_guard<std::mutex> g(tls_client_mu());
+  return tls_client_default();
+}
 
 // ---- server ------------------------------------------------------------------------------------
 HttpServer::HttpServer() { ::signal(SIGPIPE, SIG_IGN); }
 HttpServer::~HttpServer() { stop(); }
+
+bool HttpServer::enable_tls(const TlsServerConfig& cfg, std::string* err) {
+  auto ctx = make_server_ctx(cfg, err);
+  if (!ctx) return false;
+  std::lock_guard<std::mutex> g(tls_mu_);
+  tls_cfg_ = cfg;
+  tls_ctx_ = ctx;
+  tls_mtime_ = file_mtime_ns(cfg.cert_file) ^ (file_mtime_ns(cfg.key_file) << 1);
+  tls_checked_ = now_seconds();
+  return true;
+}
+
+std::shared_ptr<SSL_CTX> HttpServer::current_tls_ctx() {
+  std::lock_guard<std::mutex> g(tls_mu_);
+  if (!tls_ctx_) return nullptr;
+  const double now = now_seconds();
+  if (now - tls_checked_ >= 0.2) {  // certwatcher: a rotated pair is served from the next connection on
+    tls_checked_ = now;
+    const long long m = file_mtime_ns(tls_cfg_.cert_file) ^ (file_mtime_ns(tls_cfg_.key_file) << 1);
+    if (m != tls_mtime_) {
+      std::string err;
+      auto ctx = make_server_ctx(tls_cfg_, &err);
+      if (ctx) {
+        tls_ctx_ = ctx;
+        tls_mtime_ = m;
+        KF_INFO("http", "reloaded TLS certificate", Json{{"cert", tls_cfg_.cert_file}});
+      } else {
+        // a half-written pair: keep serving the old one, retry on a later connection
+        KF_WARN("http", "TLS certificate reload failed", Json{{"error", err}});
+      }
+    }
+  }
+  return tls_ctx_;
+}
 
 bool HttpServer::listen(const std::string& addr, int port, std::string* err) {
   int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -449,7 +721,21 @@ void HttpServer::accept_loop(int listen_fd) {
 
 void HttpServer::serve_conn(int fd, std::string remote) {
   set_timeouts(fd, 120000);
-  Reader rd(fd);
+  SSL* ssl = nullptr;
+  if (auto ctx = current_tls_ctx()) {
+    set_timeouts(fd, 10000);  // handshake budget
+    ssl = SSL_new(ctx.get());
+    SSL_set_fd(ssl, fd);
+    ERR_clear_error();
+    if (SSL_accept(ssl) != 1) {
+      KF_DEBUG("http", "TLS handshake failed", Json{{"remote", remote}, {"error", tls_error("SSL_accept")}});
+      SSL_free(ssl);
+      return;
+    }
+    set_timeouts(fd, 120000);
+  }
+  Conn conn(fd, ssl, false);  // the accept thread's wrapper closes fd
+  Reader rd(conn);
   while (running_) {
     HttpRequest req;
     std::string line;
@@ -479,12 +765,18 @@ void HttpServer::serve_conn(int fd, std::string remote) {
       resp = HttpResponse();
       resp.json(500, std::string(R"({"error":)") + json_quote(e.what()) + "}");
     }
+    if (resp.upgrade) {
+      const std::string pending = rd.take_buffered();
+      conn.set_timeout_ms(0);  // a tunnel may idle for as long as its peers like
+      resp.upgrade(conn, pending);
+      return;
+    }
     std::string head = "HTTP/1.1 " + std::to_string(resp.status) + " " + http_status_text(resp.status) + "\r\n";
     if (resp.stream) {
       for (const auto& h : resp.headers) head += h.first + ": " + h.second + "\r\n";
       head += "Transfer-Encoding: chunked\r\nConnection: close\r\n\r\n";
-      if (!send_all(fd, head)) return;
-      ChunkWriter w(fd);
+      if (!conn.write(head)) return;
+      ChunkWriter w(conn);
       resp.stream(w);
       w.finish();
       return;
@@ -493,8 +785,8 @@ void HttpServer::serve_conn(int fd, std::string remote) {
     for (const auto& h : resp.headers) head += h.first + ": " + h.second + "\r\n";
     head += "Content-Length: " + std::to_string(resp.body.size()) + "\r\n";
     head += keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
-    if (!send_all(fd, head)) return;
-    if (req.method != "HEAD" && !send_all(fd, resp.body)) return;
+    if (req.method != "HEAD") head += resp.body;  // one write: one TLS record for small responses
+    if (!conn.write(head)) return;
     if (!keep_alive) return;
   }
 }
@@ -529,22 +821,82 @@ void set_host_resolver(HostResolver r) {
   resolver_slot() = std::move(r);
 }
 
-HttpResult http_request(const std::string& method, const std::string& url, const std::string& body,
-                        const Headers& headers, int timeout_ms) {
-  HttpResult res;
+namespace {
+class ClientResponse : public HttpClientResponse {
+ public:
+  explicit ClientResponse(std::unique_ptr<Conn> c) : c_(std::move(c)), rd_(*c_) {}
+  Reader& reader() { return rd_; }
+  Next next(std::string& piece) override {
+    if (done_) return kEnd;
+    if (chunked) {
+      if (chunk_left_ == 0) {
+        std::string line;
+        if (!rd_.read_line(line)) return rd_.last_timeout() ? kTimeout : kError;
+        if (line.empty()) {  // CRLF that ended the previous chunk
+          if (!rd_.read_line(line)) return rd_.last_timeout() ? kTimeout : kError;
+        }
+        chunk_left_ = std::strtoull(line.c_str(), nullptr, 16);
+        if (chunk_left_ == 0) {
+          rd_.read_line(line);  // trailer CRLF
+          done_ = true;
+          return kEnd;
+        }
+      }
+      std::string out;
+      int r = rd_.read_some(out, static_cast<size_t>(std::min<unsigned long long>(chunk_left_, 1 << 16)));
+      if (r == -2) return kTimeout;
+      if (r <= 0) return kError;
+      chunk_left_ -= static_cast<unsigned long long>(r);
+      piece = std::move(out);
+      return kData;
+    }
+    if (length >= 0 && got_ >= length) {
+      done_ = true;
+      return kEnd;
+    }
+    std::string out;
+    const size_t want = length >= 0 ? static_cast<size_t>(std::min<long long>(length - got_, 1 << 16)) : (1 << 16);
+    int r = rd_.read_some(out, want);
+    if (r == -2) return kTimeout;
+    if (r == 0) {
+      done_ = true;
+      return length >= 0 ? kError : kEnd;  // EOF-delimited body ends here
+    }
+    if (r < 0) return kError;
+    got_ += r;
+    piece = std::move(out);
+    return kData;
+  }
+  RawConn& conn() override { return *c_; }
+
+ private:
+  std::unique_ptr<Conn> c_;
+  Reader rd_;
+  unsigned long long chunk_left_ = 0;
+  long long got_ = 0;
+  bool done_ = false;
+};
+}  // namespace
+
+std::string HttpClientResponse::read_all() {
+  std::string out, piece;
+  while (next(piece) == kData) out += piece;
+  return out;
+}
+
+std::unique_ptr<HttpClientResponse> http_open(const std::string& method, const std::string& url, const std::string& body,
+                                              const Headers& headers, int timeout_ms, std::string* err,
+                                              const TlsClientOptions* tls) {
   Url u;
   if (!Url::parse(url, u)) {
-    res.error = "bad url " + url;
-    return res;
+    if (err) *err = "bad url " + url;
+    return nullptr;
   }
-  if (u.scheme != "http") {
-    res.error = "unsupported scheme " + u.scheme;
-    return res;
-  }
-  int fd = connect_to(u.host, u.port, timeout_ms, &res.error);
-  if (fd < 0) return res;
-  set_timeouts(fd, timeout_ms);
-  std::string req = method + " " + u.target() + " HTTP/1.1\r\nHost: " + u.host + ":" + std::to_string(u.port) + "\r\n";
+  auto conn = open_conn(u, timeout_ms, err, tls);
+  if (!conn) return nullptr;
+  const bool default_port = (u.scheme == "https" && u.port == 443) || (u.scheme == "http" && u.port == 80);
+  std::string req = method + " " + u.target() + " HTTP/1.1\r\nHost: " + u.host +
+                    (default_port ? "" : ":" + std::to_string(u.port)) + "\r\n";
   bool has_ct = false;
   for (const auto& h : headers) {
     req += h.first + ": " + h.second + "\r\n";
@@ -553,121 +905,129 @@ HttpResult http_request(const std::string& method, const std::string& url, const
   if (!body.empty() && !has_ct) req += "Content-Type: application/json\r\n";
   req += "Content-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n";
   req += body;
-  if (!send_all(fd, req)) {
-    res.error = "send failed";
-    ::close(fd);
-    return res;
+  if (!conn->write(req)) {
+    if (err) *err = "send failed";
+    return nullptr;
   }
-  Reader rd(fd);
+  auto resp = std::make_unique<ClientResponse>(std::move(conn));
   std::string line;
-  if (!rd.read_line(line)) {
-    res.error = "no response (timeout or connection closed)";
-    ::close(fd);
-    return res;
+  if (!resp->reader().read_line(line)) {
+    if (err) *err = "no response (timeout or connection closed)";
+    return nullptr;
   }
   auto parts = split(line, ' ', true);
-  if (parts.size() < 2) {
-    res.error = "bad status line";
-    ::close(fd);
-    return res;
+  if (parts.size() < 2 || !starts_with(parts[0], "HTTP/")) {
+    if (err) *err = "bad status line";
+    return nullptr;
   }
-  int status = std::atoi(parts[1].c_str());
-  if (!read_headers(rd, res.headers) || !read_body(rd, res.headers, res.body, method != "HEAD")) {
-    if (res.body.empty() && status != 204) {
-      res.error = "truncated response";
-    }
+  resp->status = std::atoi(parts[1].c_str());
+  if (!read_headers(resp->reader(), resp->headers)) {
+    if (err) *err = "truncated response headers";
+    return nullptr;
   }
-  res.status = status;
-  ::close(fd);
+  auto te = resp->headers.find("Transfer-Encoding");
+  resp->chunked = te != resp->headers.end() && contains(to_lower(te->second), "chunked");
+  auto cl = resp->headers.find("Content-Length");
+  if (!resp->chunked && cl != resp->headers.end()) resp->length = std::strtoll(cl->second.c_str(), nullptr, 10);
+  if (method == "HEAD" || resp->status == 204 || resp->status == 304) resp->length = 0;
+  return resp;
+}
+
+std::unique_ptr<RawConn> http_dial(const std::string& url, int timeout_ms, std::string* err, const TlsClientOptions* tls) {
+  Url u;
+  if (!Url::parse(url, u)) {
+    if (err) *err = "bad url " + url;
+    return nullptr;
+  }
+  return open_conn(u, timeout_ms, err, tls);
+}
+
+HttpResult http_request(const std::string& method, const std::string& url, const std::string& body,
+                        const Headers& headers, int timeout_ms, const TlsClientOptions* tls) {
+  HttpResult res;
+  auto r = http_open(method, url, body, headers, timeout_ms, &res.error, tls);
+  if (!r) return res;
+  res.headers = r->headers;
+  std::string piece;
+  HttpClientResponse::Next n;
+  while ((n = r->next(piece)) == HttpClientResponse::kData) res.body += piece;
+  if (n != HttpClientResponse::kEnd && res.body.empty() && r->status != 204) res.error = "truncated response";
+  res.status = r->status;
   return res;
+}
+
+std::pair<long long, long long> pump_bidirectional(RawConn& a, RawConn& b, const std::string& a_pending,
+                                                   const std::string& b_pending, int idle_ms) {
+  long long ab = 0, ba = 0;
+  if (!a_pending.empty()) {
+    if (!b.write(a_pending)) return {ab, ba};
+    ab += static_cast<long long>(a_pending.size());
+  }
+  if (!b_pending.empty()) {
+    if (!a.write(b_pending)) return {ab, ba};
+    ba += static_cast<long long>(b_pending.size());
+  }
+  // each side's socket waits in poll(); reads never block (bytes are there or TLS has them)
+  a.set_timeout_ms(1000);
+  b.set_timeout_ms(1000);
+  char buf[32768];
+  double last = now_seconds();
+  for (;;) {
+    struct pollfd p[2] = {{a.fd(), POLLIN, 0}, {b.fd(), POLLIN, 0}};
+    const bool ra = a.has_buffered(), rb = b.has_buffered();
+    int pr = (ra || rb) ? 1 : ::poll(p, 2, 250);
+    if (pr < 0 && errno != EINTR) break;
+    if (pr == 0) {
+      if (idle_ms > 0 && (now_seconds() - last) * 1000 > idle_ms) break;
+      continue;
+    }
+    bool closed = false;
+    auto move = [&](RawConn& from, RawConn& to, long long& count) {
+      long n = from.read(buf, sizeof buf);
+      if (n > 0) {
+        if (!to.write(buf, static_cast<size_t>(n))) closed = true;
+        count += n;
+        last = now_seconds();
+      } else if (!(n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))) {
+        closed = true;
+      }
+    };
+    if (ra || (p[0].revents & (POLLIN | POLLHUP | POLLERR))) move(a, b, ab);
+    if (!closed && (rb || (p[1].revents & (POLLIN | POLLHUP | POLLERR)))) move(b, a, ba);
+    if (closed) break;
+  }
+  return {ab, ba};
 }
 
 int http_stream_lines(const std::string& method, const std::string& url, const Headers& headers,
                       const std::function<bool(const std::string&)>& on_line, const std::atomic<bool>* stop,
                       int connect_timeout_ms, std::string* err) {
-  Url u;
-  if (!Url::parse(url, u)) {
-    if (err) *err = "bad url";
-    return 0;
-  }
-  int fd = connect_to(u.host, u.port, connect_timeout_ms, err);
-  if (fd < 0) return 0;
-  set_timeouts(fd, 1000);  // short recv timeout so *stop is observed
-  std::string req = method + " " + u.target() + " HTTP/1.1\r\nHost: " + u.host + "\r\n";
-  for (const auto& h : headers) req += h.first + ": " + h.second + "\r\n";
-  req += "Connection: close\r\n\r\n";
-  if (!send_all(fd, req)) {
-    ::close(fd);
-    return 0;
-  }
-  std::string buf;
-  int status = 0;
-  bool headers_done = false, chunked = false;
-  std::string pending;  // body bytes not yet split into lines
-  size_t chunk_left = 0;
-  int cstate = 0;
-  char tmp[8192];
+  auto r = http_open(method, url, "", headers, connect_timeout_ms, err);
+  if (!r) return 0;
+  r->conn().set_timeout_ms(1000);  // short receive timeout so *stop is observed
+  const int status = r->status;
+  std::string pending, piece;
   for (;;) {
     if (stop && stop->load()) break;
-    ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
-    if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) continue;
-    if (r <= 0) break;
-    buf.append(tmp, static_cast<size_t>(r));
-    if (!headers_done) {
-      size_t he = buf.find("\r\n\r\n");
-      if (he == std::string::npos) continue;
-      std::string head = buf.substr(0, he);
-      buf.erase(0, he + 4);
-      auto lines = split(head, '\n');
-      if (!lines.empty()) {
-        auto parts = split(trim(lines[0]), ' ', true);
-        if (parts.size() >= 2) status = std::atoi(parts[1].c_str());
-      }
-      for (auto& l : lines)
-        if (contains(to_lower(l), "transfer-encoding") && contains(to_lower(l), "chunked")) chunked = true;
-      headers_done = true;
-    }
-    // decode body: chunk state machine (0 = size line, 1 = data, 2 = CRLF after data)
-    if (chunked) {
-      for (;;) {
-        if (cstate == 0) {
-          size_t nl = buf.find("\r\n");
-          if (nl == std::string::npos) break;
-          std::string h = buf.substr(0, nl);
-          buf.erase(0, nl + 2);
-          if (h.empty()) continue;
-          chunk_left = std::strtoul(h.c_str(), nullptr, 16);
-          if (chunk_left == 0) goto done;
-          cstate = 1;
-        } else if (cstate == 1) {
-          size_t take = std::min(chunk_left, buf.size());
-          if (take == 0) break;
-          pending.append(buf, 0, take);
-          buf.erase(0, take);
-          chunk_left -= take;
-          if (chunk_left == 0) cstate = 2;
-        } else {
-          if (buf.size() < 2) break;
-          buf.erase(0, 2);
-          cstate = 0;
-        }
-      }
-    } else {
-      pending += buf;
-      buf.clear();
-    }
+    const auto n = r->next(piece);
+    if (n == HttpClientResponse::kTimeout) continue;
+    if (n != HttpClientResponse::kData) break;
+    pending += piece;
     size_t nl;
+    bool quit = false;
     while ((nl = pending.find('\n')) != std::string::npos) {
       std::string line = pending.substr(0, nl);
       pending.erase(0, nl + 1);
       if (!line.empty() && line.back() == '\r') line.pop_back();
       if (line.empty()) continue;
-      if (!on_line(line)) goto done;
+      if (!on_line(line)) {
+        quit = true;
+        break;
+      }
     }
+    if (quit) return status;
   }
-done:
-  if (!pending.empty() && (!stop || !stop->load())) on_line(trim(pending));
-  ::close(fd);
+  if (!trim(pending).empty() && (!stop || !stop->load())) on_line(trim(pending));
   return status;
 }
 
