@@ -49,21 +49,41 @@ def _split_api_version(api_version: str) -> tuple[str, str]:
 _TIMEOUT_SCALE = float(os.environ.get("KFAMD_TIMEOUT_SCALE", "1"))
 
 
+_SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
 class KubeClient:
-    """REST client. ``base_url`` defaults to $KFAMD_API_URL / in-cluster KUBERNETES_SERVICE_HOST."""
+    """REST client. ``base_url`` defaults to $KFAMD_API_URL / in-cluster KUBERNETES_SERVICE_HOST.
+
+    https servers are verified against ``ca_file`` (default $KFAMD_CA_FILE, else the service
+    account's ca.crt in-cluster, else the system trust store); ``verify=False`` skips it."""
 
     def __init__(self, base_url: str | None = None, token: str | None = None, impersonate: str | None = None,
-                 impersonate_groups: list[str] | None = None, timeout: float = 30.0):
+                 impersonate_groups: list[str] | None = None, timeout: float = 30.0,
+                 ca_file: str | None = None, verify: bool = True, client_cert: tuple[str, str] | None = None):
+        in_cluster = False
         if base_url is None:
             base_url = os.environ.get("KFAMD_API_URL")
             if not base_url and os.environ.get("KUBERNETES_SERVICE_HOST"):
-                base_url = f"http://{os.environ['KUBERNETES_SERVICE_HOST']}:{os.environ.get('KUBERNETES_SERVICE_PORT', '80')}"
+                # rest.InClusterConfig: the kubernetes service is HTTPS
+                base_url = f"https://{os.environ['KUBERNETES_SERVICE_HOST']}:{os.environ.get('KUBERNETES_SERVICE_PORT', '443')}"
+                in_cluster = True
         if not base_url:
             raise ValueError("no API server URL (set KFAMD_API_URL)")
         self.base = base_url.rstrip("/")
         self.timeout = timeout
         self.session = requests.Session()
         self.session.trust_env = False
+        if ca_file is None:
+            ca_file = os.environ.get("KFAMD_CA_FILE") or None
+            if ca_file is None and in_cluster and os.path.exists(f"{_SA_DIR}/ca.crt"):
+                ca_file = f"{_SA_DIR}/ca.crt"
+        self.session.verify = (ca_file or True) if verify else False
+        if client_cert:
+            self.session.cert = client_cert
+        if token is None and in_cluster and os.path.exists(f"{_SA_DIR}/token"):
+            with open(f"{_SA_DIR}/token") as f:
+                token = f.read().strip()
         self.headers: dict[str, str] = {"Accept": "application/json"}
         if token:
             self.headers["Authorization"] = f"Bearer {token}"

@@ -32,7 +32,8 @@ def kflite_binary() -> Path:
 
 class LocalCluster:
     def __init__(self, data_dir: str | None = None, env: dict | None = None, args: list[str] | None = None,
-                 controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0):
+                 controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0,
+                 ca_file: str | None = None):
         self._tmp = None
         if data_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="kflite-")
@@ -44,6 +45,7 @@ class LocalCluster:
         self.controllers = controllers
         self.gpus = gpus
         self.startup_timeout = startup_timeout
+        self.ca_file = ca_file  # verifies an https API server (kflite --tls-cert-file ...)
         self.proc: subprocess.Popen | None = None
         self.url = ""
         self.gateway = ""
@@ -90,7 +92,7 @@ class LocalCluster:
         else:
             self.stop()
             raise TimeoutError("kflite did not come up")
-        self.client = KubeClient(self.url)
+        self.client = KubeClient(self.url, ca_file=self.ca_file)
         return self
 
     def stop(self) -> None:

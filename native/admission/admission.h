@@ -76,12 +76,15 @@ class AdmissionWebhookServer {
  public:
   // path -> (plugin, mutating)
   void add(const std::string& path, AdmissionFn fn, bool mutating, std::shared_ptr<const ResourceInfo> res);
-  bool start(const std::string& addr, int port, std::string* err);
+  // tls != nullptr: serve HTTPS (the pair is re-read when it changes on disk)
+  bool start(const std::string& addr, int port, std::string* err, const TlsServerConfig* tls = nullptr);
   void stop();
   int port() const { return srv_ ? srv_->port() : 0; }
   // Mutating + ValidatingWebhookConfiguration objects pointing at base_url (self-registration of
   // the split binaries; the reference ships them as manifests).
-  std::vector<Json> webhook_configurations(const std::string& base_url, const std::string& name) const;
+  // ca_pem non-empty: set as every webhook's clientConfig.caBundle (base64).
+  std::vector<Json> webhook_configurations(const std::string& base_url, const std::string& name,
+                                           const std::string& ca_pem = "") const;
   // Processes one AdmissionReview (exposed for tests).
   Json review(const std::string& path, const Json& admission_review);
 

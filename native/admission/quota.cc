@@ -253,7 +253,8 @@ Json AdmissionWebhookServer::review(const std::string& path, const Json& ar) {
   return Json{{"apiVersion", "admission.k8s.io/v1"}, {"kind", "AdmissionReview"}, {"response", resp}};
 }
 
-std::vector<Json> AdmissionWebhookServer::webhook_configurations(const std::string& base_url, const std::string& name) const {
+std::vector<Json> AdmissionWebhookServer::webhook_configurations(const std::string& base_url, const std::string& name,
+                                                                 const std::string& ca_pem) const {
   Json mut = Json::array(), val = Json::array();
   for (const auto& kv : routes_) {
     const auto& res = kv.second.res;
@@ -272,6 +273,7 @@ std::vector<Json> AdmissionWebhookServer::webhook_configurations(const std::stri
             {"failurePolicy", "Fail"},
             {"sideEffects", "None"},
             {"admissionReviewVersions", Json::array({"v1"})}};
+    if (!ca_pem.empty()) wh["clientConfig"]["caBundle"] = base64_encode(ca_pem);
     if (res->kind == "Pod" && kv.first == "/apply-poddefault")
       wh["namespaceSelector"] = Json{{"matchLabels", Json{{"app.kubernetes.io/part-of", "kubeflow-profile"}}}};
     (kv.second.mutating ? mut : val).push_back(wh);
@@ -286,8 +288,9 @@ std::vector<Json> AdmissionWebhookServer::webhook_configurations(const std::stri
   return out;
 }
 
-bool AdmissionWebhookServer::start(const std::string& addr, int port, std::string* err) {
+bool AdmissionWebhookServer::start(const std::string& addr, int port, std::string* err, const TlsServerConfig* tls) {
   srv_ = std::make_unique<HttpServer>();
+  if (tls && !srv_->enable_tls(*tls, err)) return false;
   if (!srv_->listen(addr, port, err)) return false;
   srv_->set_handler([this](HttpRequest& req, HttpResponse& resp) {
     if (req.path == "/healthz" || req.path == "/readyz") {

@@ -449,11 +449,16 @@ ApiError ApiServer::call_webhooks(AdmissionAttrs& a, bool mutating) {
           !LabelSelector::from_json(wh["objectSelector"]).matches(target.at_path({"metadata", "labels"})))
         continue;
       std::string url = wh.at_path({"clientConfig", "url"}).as_string();
+      const std::string ca_b64 = wh.at_path({"clientConfig", "caBundle"}).as_string();
       if (url.empty() && wh.at_path({"clientConfig", "service"}).is_object()) {
+        // kube-apiserver calls service webhooks over HTTPS; kube-lite keeps plain HTTP for a
+        // service webhook registered without a caBundle (development manifests)
         const Json& svc = wh.at_path({"clientConfig", "service"});
-        url = "http://" + svc["name"].as_string() + "." + svc["namespace"].as_string() + ".svc:" +
-              std::to_string(svc["port"].as_int(443)) + svc["path"].as_string();
+        url = std::string(ca_b64.empty() ? "http://" : "https://") + svc["name"].as_string() + "." +
+              svc["namespace"].as_string() + ".svc:" + std::to_string(svc["port"].as_int(443)) + svc["path"].as_string();
       }
+      TlsClientOptions tls;
+      if (!ca_b64.empty()) tls.ca_pem = base64_decode(ca_b64);
       const std::string uid = uuid4();
       Json review{{"apiVersion", "admission.k8s.io/v1"}, {"kind", "AdmissionReview"},
                   {"request", Json{{"uid", uid},
@@ -468,7 +473,8 @@ ApiError ApiServer::call_webhooks(AdmissionAttrs& a, bool mutating) {
                                    {"oldObject", a.old_object ? *a.old_object : Json()},
                                    {"dryRun", a.dry_run}}}};
       int timeout = static_cast<int>(wh["timeoutSeconds"].as_int(10)) * 1000;
-      HttpResult r = http_request("POST", url, review.dump(), {{"Content-Type", "application/json"}}, timeout);
+      HttpResult r = http_request("POST", url, review.dump(), {{"Content-Type", "application/json"}}, timeout,
+                                  ca_b64.empty() ? nullptr : &tls);
       bool fail_closed = wh["failurePolicy"].as_string_or("Fail") != "Ignore";
       Json resp;
       if (!r.ok() || !Json::try_parse(r.body, resp)) {

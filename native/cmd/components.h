@@ -38,8 +38,14 @@ struct ComponentFlags {
   // odh
   std::string oauth_proxy_image = "registry.redhat.io/openshift4/ose-oauth-proxy:latest";
   std::string controller_namespace = "opendatahub";
-  // admission webhooks as HTTP services (split mode); in kflite they run in-process
+  // admission webhooks as HTTP(S) services (split mode); in kflite they run in-process
   int64_t webhook_port = -1;
+  std::string webhook_host = "127.0.0.1";
+  // controller-runtime layout: <dir>/tls.crt + tls.key (+ ca.crt for the registered caBundle);
+  // explicit files override it (admission-webhook's --tlsCertFile / --tlsKeyFile)
+  std::string webhook_cert_dir = "/tmp/k8s-webhook-server/serving-certs";
+  std::string webhook_cert_file, webhook_key_file, webhook_ca_file;
+  std::string webhook_tls = "auto";  // auto (TLS when the pair exists) | on | off
 
   void register_flags(Flags& f);
 };

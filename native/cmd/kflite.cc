@@ -29,12 +29,15 @@ static void on_signal(int) { g_stop = true; }
 
 int main(int argc, char** argv) {
   Flags f;
-  std::string data_dir, api_addr, controllers, metrics_addr, probe_addr, token_file, authz;
+  std::string data_dir, api_addr, controllers, metrics_addr, probe_addr, token_file, authz, tls_cert, tls_key, client_ca;
   int64_t api_port = 0, workers = 1;
   bool log_json = false, debug = false;
   f.add_string("data-dir", &data_dir, "", "directory for the WAL and pod sandboxes (empty = in-memory)");
   f.add_string("bind-address", &api_addr, "127.0.0.1", "API server bind address");
   f.add_int("port", &api_port, 0, "API server port (0 = ephemeral)");
+  f.add_string("tls-cert-file", &tls_cert, "", "serve the API over HTTPS with this certificate (kube-apiserver flag)");
+  f.add_string("tls-private-key-file", &tls_key, "", "private key for --tls-cert-file");
+  f.add_string("client-ca-file", &client_ca, "", "verify client certificates against this CA (optional mTLS)");
   f.add_string("controllers", &controllers, "all",
                "comma list: notebook,culler,odh,profile,tensorboard,pvcviewer,webhooks,kfam,builtin,scheduler,kubelet,gateway (or all)");
   f.add_string("metrics-addr", &metrics_addr, "0", "controller metrics address (0 = disabled; the API server serves /metrics)");
@@ -82,13 +85,20 @@ int main(int argc, char** argv) {
   });
 
   HttpServer srv;
+  if (!tls_cert.empty()) {
+    TlsServerConfig tls{tls_cert, tls_key.empty() ? tls_cert : tls_key, client_ca, false};
+    if (!srv.enable_tls(tls, &err)) {
+      std::fprintf(stderr, "apiserver: %s\n", err.c_str());
+      return 1;
+    }
+  }
   if (!srv.listen(api_addr, static_cast<int>(api_port), &err)) {
     std::fprintf(stderr, "apiserver: %s\n", err.c_str());
     return 1;
   }
   srv.set_handler([&api](HttpRequest& req, HttpResponse& resp) { api.handle_http(req, resp); });
   srv.start();
-  const std::string url = "http://" + api_addr + ":" + std::to_string(srv.port());
+  const std::string url = std::string(srv.tls() ? "https://" : "http://") + api_addr + ":" + std::to_string(srv.port());
   if (!data_dir.empty()) {
     make_dirs(data_dir);
     write_file(data_dir + "/kflite.json", Json{{"server", url}, {"pid", static_cast<int64_t>(::getpid())}}.dump() + "\n");

@@ -41,11 +41,17 @@ inline std::atomic<bool>& split_stop_flag() {
 
 inline int run_split(int argc, char** argv, SplitSpec spec) {
   Flags f;
-  std::string server, token_file, metrics_addr = spec.metrics_addr, probe_addr = spec.probe_addr, le_ns;
-  bool leader = false, log_json = false, debug = false;
+  std::string server, token_file, metrics_addr = spec.metrics_addr, probe_addr = spec.probe_addr, le_ns, ca_file,
+      client_cert, client_key;
+  bool leader = false, log_json = false, debug = false, insecure = false;
   int64_t qps = 0, burst = 0, workers = 1;
   f.add_string("server", &server, "", "API server URL (default: $KFAMD_API_URL or in-cluster service env)");
   f.add_string("token-file", &token_file, "/var/run/secrets/kubernetes.io/serviceaccount/token", "bearer token file");
+  f.add_string("certificate-authority", &ca_file, "/var/run/secrets/kubernetes.io/serviceaccount/ca.crt",
+               "CA bundle that signs the API server's certificate (https servers)");
+  f.add_string("client-certificate", &client_cert, "", "client certificate for the API server (mutual TLS)");
+  f.add_string("client-key", &client_key, "", "client key for --client-certificate");
+  f.add_bool("insecure-skip-tls-verify", &insecure, false, "do not verify the API server's certificate");
   f.add_string("metrics-addr", &metrics_addr, spec.metrics_addr, "metrics endpoint address");
   f.add_string("metrics-bind-address", &metrics_addr, spec.metrics_addr, "metrics endpoint address (alias)");
   f.add_string("probe-addr", &probe_addr, spec.probe_addr, "health probe address");
@@ -73,8 +79,18 @@ inline int run_split(int argc, char** argv, SplitSpec spec) {
   ::signal(SIGINT, [](int) { split_stop_flag() = true; });
   ::signal(SIGTERM, [](int) { split_stop_flag() = true; });
   if (server.empty()) server = getenv_or("KFAMD_API_URL", "");
+  // in-cluster: the kubernetes service is HTTPS, verified with the service account's ca.crt
+  // (client-go rest.InClusterConfig)
   if (server.empty() && !getenv_or("KUBERNETES_SERVICE_HOST", "").empty())
-    server = "http://" + getenv_or("KUBERNETES_SERVICE_HOST", "") + ":" + getenv_or("KUBERNETES_SERVICE_PORT", "443");
+    server = "https://" + getenv_or("KUBERNETES_SERVICE_HOST", "") + ":" + getenv_or("KUBERNETES_SERVICE_PORT", "443");
+  {
+    TlsClientOptions tls;
+    if (!ca_file.empty() && file_exists(ca_file)) tls.ca_file = ca_file;
+    tls.cert_file = client_cert;
+    tls.key_file = client_key;
+    tls.insecure_skip_verify = insecure;
+    set_default_tls_client(tls);
+  }
   if (server.empty()) {
     std::fprintf(stderr, "%s: no API server (--server / KFAMD_API_URL)\n", spec.name.c_str());
     return 2;

@@ -35,7 +35,14 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("workload-identity", &workload_identity, "", "default GCP service account for the WorkloadIdentity plugin");
   f.add_string("oauth-proxy-image", &oauth_proxy_image, "registry.redhat.io/openshift4/ose-oauth-proxy:latest", "ODH oauth proxy image");
   f.add_string("controller-namespace", &controller_namespace, "opendatahub", "ODH controller namespace");
-  f.add_int("webhook-port", &webhook_port, -1, "serve admission webhooks over HTTP on this port (-1 = in-process only)");
+  f.add_int("webhook-port", &webhook_port, -1, "serve admission webhooks on this port (-1 = in-process only)");
+  f.add_string("webhook-host", &webhook_host, "127.0.0.1", "webhook server bind address");
+  f.add_string("webhook-cert-dir", &webhook_cert_dir, "/tmp/k8s-webhook-server/serving-certs",
+               "directory holding tls.crt / tls.key (and ca.crt) for the webhook server");
+  f.add_string("webhook-tls-cert-file", &webhook_cert_file, "", "webhook serving certificate (overrides --webhook-cert-dir)");
+  f.add_string("webhook-tls-key-file", &webhook_key_file, "", "webhook serving key (overrides --webhook-cert-dir)");
+  f.add_string("webhook-ca-file", &webhook_ca_file, "", "CA bundle registered as the webhooks' caBundle (default: <dir>/ca.crt, else the serving certificate)");
+  f.add_string("webhook-tls", &webhook_tls, "auto", "auto (HTTPS when the certificate pair exists) | on | off");
 }
 
 struct Components::Impl {
@@ -214,14 +221,34 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
   }
   if (I.webhooks) {
     // started last: every plugin route is registered before the first request
-    if (!I.webhooks->start("127.0.0.1", static_cast<int>(I.f.webhook_port), err)) return false;
+    // HTTPS like the reference's webhook servers (admission-webhook :4443 ListenAndServeTLS,
+    // controller-runtime :8443 / :9443 from the serving-certs dir); plain HTTP only for kube-lite
+    // development (--webhook-tls=off, or auto with no certificate pair present)
+    TlsServerConfig tls;
+    tls.cert_file = I.f.webhook_cert_file.empty() ? I.f.webhook_cert_dir + "/tls.crt" : I.f.webhook_cert_file;
+    tls.key_file = I.f.webhook_key_file.empty() ? I.f.webhook_cert_dir + "/tls.key" : I.f.webhook_key_file;
+    const bool have_pair = file_exists(tls.cert_file) && file_exists(tls.key_file);
+    const bool use_tls = I.f.webhook_tls == "on" || (I.f.webhook_tls == "auto" && have_pair);
+    if (I.f.webhook_tls == "on" && !have_pair) {
+      *err = "webhook TLS: missing " + tls.cert_file + " / " + tls.key_file;
+      return false;
+    }
+    if (!I.webhooks->start(I.f.webhook_host, static_cast<int>(I.f.webhook_port), err, use_tls ? &tls : nullptr)) return false;
     I.stoppers.push_back([&I] { I.webhooks->stop(); });
+    if (!use_tls) KF_WARN("webhooks", "serving admission webhooks over plain HTTP (no certificate pair)", Json{{"cert", tls.cert_file}});
     if (!I.api) {
       // split mode: register our hooks with the remote API server (the manifests' job upstream)
-      const std::string base = "http://127.0.0.1:" + std::to_string(I.webhooks->port());
+      const std::string host = I.f.webhook_host == "0.0.0.0" ? "127.0.0.1" : I.f.webhook_host;
+      const std::string base = std::string(use_tls ? "https://" : "http://") + host + ":" + std::to_string(I.webhooks->port());
+      std::string ca_pem;
+      if (use_tls) {
+        std::string ca_file = I.f.webhook_ca_file;
+        if (ca_file.empty()) ca_file = file_exists(I.f.webhook_cert_dir + "/ca.crt") ? I.f.webhook_cert_dir + "/ca.crt" : tls.cert_file;
+        read_file(ca_file, ca_pem);
+      }
       std::string cfg_name = "kfamd";
       for (const auto& c : enabled) cfg_name += "-" + c;
-      for (auto cfg : I.webhooks->webhook_configurations(base, cfg_name)) {
+      for (auto cfg : I.webhooks->webhook_configurations(base, cfg_name, ca_pem)) {
         Json live;
         ApiError e = I.c->get(cfg["apiVersion"].as_string(), cfg["kind"].as_string(), "", cfg_name, live);
         if (e.code == 404) e = I.c->create(cfg);
