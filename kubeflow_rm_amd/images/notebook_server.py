@@ -7,15 +7,23 @@ and the Jupyter REST endpoints the culler polls (notebook-controller/controllers
   GET  {prefix}/api/terminals -> [{name, last_activity}]
 Kernels/terminals can be created (POST), deleted (DELETE) and driven busy/idle
 (POST {prefix}/api/kernels/{id}/execute {"seconds": s}) so culling is testable end to end.
+Kernel channels are a real WebSocket (RFC 6455) at {prefix}/api/kernels/{id}/channels speaking
+the Jupyter messaging protocol's JSON form (kernel_info / execute requests get status, stream,
+execute_reply messages; an open channel counts in the kernel's `connections`, which the culler
+reads). {prefix}/api/events/stream is a text/event-stream (server-sent events) endpoint, for
+checking that proxies relay responses as they are produced.
 Requests that arrive without the prefix (rewritten routes of group-one / group-two servers) are
 served too. GET {prefix}/api/gpu reports the GPUs this pod was given (HIP_VISIBLE_DEVICES) and
 the readiness-op result when present.
 """
 from __future__ import annotations
 
+import base64
 import datetime as _dt
+import hashlib
 import json
 import os
+import struct
 import sys
 import threading
 import time
@@ -43,6 +51,62 @@ def _kernel_view(k: dict) -> dict:
             "execution_state": state, "connections": k.get("connections", 0)}
 
 
+_WS_GUID = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11"
+
+
+def _ws_read_frame(rfile):
+    """One client frame -> (opcode, payload); None on EOF. Client frames are masked (RFC 6455 5.3)."""
+    h = rfile.read(2)
+    if len(h) < 2:
+        return None
+    op, n = h[0] & 0x0F, h[1] & 0x7F
+    if n == 126:
+        n = struct.unpack(">H", rfile.read(2))[0]
+    elif n == 127:
+        n = struct.unpack(">Q", rfile.read(8))[0]
+    mask = rfile.read(4) if h[1] & 0x80 else b"\0\0\0\0"
+    data = bytearray(rfile.read(n))
+    for i in range(len(data)):
+        data[i] ^= mask[i & 3]
+    return op, bytes(data)
+
+
+def _ws_frame(payload: bytes, op: int = 1) -> bytes:
+    n = len(payload)
+    if n < 126:
+        head = struct.pack(">BB", 0x80 | op, n)
+    elif n < 1 << 16:
+        head = struct.pack(">BBH", 0x80 | op, 126, n)
+    else:
+        head = struct.pack(">BBQ", 0x80 | op, 127, n)
+    return head + payload
+
+
+def _jmsg(parent: dict, msg_type: str, channel: str, content: dict) -> dict:
+    return {"header": {"msg_id": str(uuid.uuid4()), "msg_type": msg_type, "session": parent.get("header", {}).get("session", ""),
+                       "username": "kflite", "date": _now(), "version": "5.3"},
+            "parent_header": parent.get("header", {}), "metadata": {}, "content": content, "channel": channel}
+
+
+def _kernel_replies(k: dict, msg: dict) -> list[dict]:
+    mt = msg.get("header", {}).get("msg_type", "")
+    if mt == "kernel_info_request":
+        return [_jmsg(msg, "kernel_info_reply", "shell",
+                      {"status": "ok", "protocol_version": "5.3", "implementation": "kfamd-kflite",
+                       "language_info": {"name": "python", "version": sys.version.split()[0]}})]
+    if mt == "execute_request":
+        k["execution_count"] = k.get("execution_count", 0) + 1
+        k["last_activity"] = _now()
+        code = msg.get("content", {}).get("code", "")
+        return [_jmsg(msg, "status", "iopub", {"execution_state": "busy"}),
+                _jmsg(msg, "execute_input", "iopub", {"code": code, "execution_count": k["execution_count"]}),
+                _jmsg(msg, "stream", "iopub", {"name": "stdout", "text": code}),
+                _jmsg(msg, "execute_reply", "shell", {"status": "ok", "execution_count": k["execution_count"]}),
+                _jmsg(msg, "status", "iopub", {"execution_state": "idle"})]
+    return [_jmsg(msg, mt.replace("_request", "_reply") if mt.endswith("_request") else "error", "shell",
+                  {"status": "error", "ename": "NotImplemented", "evalue": mt})]
+
+
 def make_handler(prefix: str):
     prefix = prefix.rstrip("/")
 
@@ -53,8 +117,75 @@ def make_handler(prefix: str):
                 path = path[len(prefix):] or "/"
             return path
 
+        def _kernel_channels(self, kid: str):
+            with _LOCK:
+                k = KERNELS.get(kid)
+            if not k:
+                return self.send_json(404, {"message": "kernel not found"})
+            key = self.headers.get("Sec-WebSocket-Key", "")
+            if self.headers.get("Upgrade", "").lower() != "websocket" or not key:
+                return self.send_json(400, {"message": "expected a WebSocket upgrade"})
+            accept = base64.b64encode(hashlib.sha1((key + _WS_GUID).encode()).digest()).decode()
+            self.send_response(101, "Switching Protocols")
+            self.send_header("Upgrade", "websocket")
+            self.send_header("Connection", "Upgrade")
+            self.send_header("Sec-WebSocket-Accept", accept)
+            self.end_headers()
+            self.wfile.flush()
+            self.close_connection = True
+            with _LOCK:
+                k["connections"] = k.get("connections", 0) + 1
+            try:
+                while True:
+                    fr = _ws_read_frame(self.rfile)
+                    if fr is None or fr[0] == 8:  # EOF / close
+                        if fr is not None:
+                            self.wfile.write(_ws_frame(b"", 8))
+                        return
+                    op, data = fr
+                    if op == 9:  # ping -> pong
+                        self.wfile.write(_ws_frame(data, 10))
+                        continue
+                    if op != 1:
+                        continue
+                    try:
+                        msg = json.loads(data)
+                    except ValueError:
+                        continue
+                    with _LOCK:
+                        replies = _kernel_replies(k, msg)
+                    for r in replies:
+                        self.wfile.write(_ws_frame(json.dumps(r).encode()))
+                    self.wfile.flush()
+            except OSError:
+                return
+            finally:
+                with _LOCK:
+                    k["connections"] = max(0, k.get("connections", 1) - 1)
+
+        def _event_stream(self):
+            q = dict(pair.split("=", 1) for pair in (self.path.split("?", 1)[1:] or [""])[0].split("&") if "=" in pair)
+            n, interval = int(q.get("n", "5")), float(q.get("interval_ms", "100")) / 1000.0
+            self.send_response(200)
+            self.send_header("Content-Type", "text/event-stream")
+            self.send_header("Cache-Control", "no-cache")
+            self.send_header("Transfer-Encoding", "chunked")
+            self.end_headers()
+            for i in range(n):
+                ev = f"id: {i}\ndata: {json.dumps({'seq': i, 't': time.time()})}\n\n".encode()
+                self.wfile.write(b"%x\r\n%s\r\n" % (len(ev), ev))
+                self.wfile.flush()
+                time.sleep(interval)
+            self.wfile.write(b"0\r\n\r\n")
+            self.close_connection = True
+
         def do_GET(self):
             p = self._route()
+            parts = p.strip("/").split("/")
+            if len(parts) == 4 and parts[:2] == ["api", "kernels"] and parts[3] == "channels":
+                return self._kernel_channels(parts[2])
+            if p == "/api/events/stream":
+                return self._event_stream()
             if p in ("/api", "/api/"):
                 return self.send_json(200, {"version": "2.14.0-kflite"})
             if p == "/api/status":

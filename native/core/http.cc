@@ -895,8 +895,8 @@ std::unique_ptr<HttpClientResponse> http_open(const std::string& method, const s
   auto conn = open_conn(u, timeout_ms, err, tls);
   if (!conn) return nullptr;
   const bool default_port = (u.scheme == "https" && u.port == 443) || (u.scheme == "http" && u.port == 80);
-  std::string req = method + " " + u.target() + " HTTP/1.1\r\nHost: " + u.host +
-                    (default_port ? "" : ":" + std::to_string(u.port)) + "\r\n";
+  std::string req = method + " " + u.target() + " HTTP/1.1\r\n";
+  if (!headers.count("Host")) req += "Host: " + u.host + (default_port ? "" : ":" + std::to_string(u.port)) + "\r\n";
   bool has_ct = false;
   for (const auto& h : headers) {
     req += h.first + ": " + h.second + "\r\n";

@@ -8,7 +8,11 @@
 
 namespace kf {
 
-Gateway::Gateway(std::shared_ptr<Client> c, std::string gateway_name) : c_(std::move(c)), gw_(std::move(gateway_name)) {}
+Gateway::Gateway(std::shared_ptr<Client> c, std::string gateway_name)
+    : c_(std::move(c)),
+      gw_(std::move(gateway_name)),
+      upgrades_(Registry::global().counter("gateway_upgraded_connections_total", "connections tunnelled after an HTTP Upgrade (WebSocket)")),
+      streams_(Registry::global().counter("gateway_streamed_responses_total", "responses relayed incrementally (chunked / unframed / large)")) {}
 Gateway::~Gateway() { stop(); }
 
 void Gateway::setup(Manager& mgr) {
@@ -117,33 +121,85 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   }
   std::string url = "http://" + rt.dest_host + ":" + std::to_string(rt.dest_port) + target_path +
                     (req.raw_query.empty() ? "" : "?" + req.raw_query);
+  const bool upgrade = contains(to_lower(req.header("Connection")), "upgrade") && !req.header("Upgrade").empty();
   Headers h;
   for (const auto& kv : req.headers) {
     std::string k = to_lower(kv.first);
-    if (k == "content-length" || k == "connection" || k == "transfer-encoding") continue;
+    if (k == "content-length" || k == "transfer-encoding") continue;
+    if (k == "connection" && !upgrade) continue;
     h[kv.first] = kv.second;
   }
   for (const auto& m : rt.headers.as_object()) h[m.first] = m.second.as_string();
   h["X-Forwarded-Prefix"] = rt.prefix;
   h["X-Envoy-Original-Path"] = req.path;
-  HttpResult r = http_request(req.method, url, req.body, h, static_cast<int>(rt.timeout_s * 1000));
+  const int timeout_ms = static_cast<int>(rt.timeout_s * 1000);
   // Istio's default retry policy: 2 retries on connect-failure / refused-stream (a pod that is
   // Ready without a readiness probe may not be listening yet)
-  for (int attempt = 0; attempt < 2 && r.status == 0; ++attempt) {
-    ::usleep(25000);
-    r = http_request(req.method, url, req.body, h, static_cast<int>(rt.timeout_s * 1000));
-  }
-  if (r.status == 0) {
-    resp.text(503, "upstream connect error or disconnect/reset before headers. reset reason: " + r.error + "\n");
+  auto with_retries = [](auto attempt) {
+    auto r = attempt();
+    for (int i = 0; i < 2 && !r; ++i) {
+      ::usleep(25000);
+      r = attempt();
+    }
+    return r;
+  };
+  std::string err;
+  if (upgrade) {
+    // WebSocket (JupyterLab kernel channels, terminals): forward the handshake, then the
+    // connection is a byte tunnel until either side closes
+    auto up = with_retries([&] { return http_dial(url, timeout_ms, &err); });
+    if (!up) {
+      resp.text(503, "upstream connect error or disconnect/reset before headers. reset reason: " + err + "\n");
+      return;
+    }
+    Url u;
+    Url::parse(url, u);
+    std::string head = req.method + " " + u.target() + " HTTP/1.1\r\n";
+    if (!h.count("Host")) head += "Host: " + u.host + ":" + std::to_string(u.port) + "\r\n";
+    for (const auto& kv : h) head += kv.first + ": " + kv.second + "\r\n";
+    if (!req.body.empty()) head += "Content-Length: " + std::to_string(req.body.size()) + "\r\n";
+    head += "\r\n" + req.body;
+    if (!up->write(head)) {
+      resp.text(503, "upstream reset before the upgrade\n");
+      return;
+    }
+    std::shared_ptr<RawConn> upstream(std::move(up));
+    upgrades_->inc();
+    resp.upgrade = [upstream](RawConn& client, const std::string& pending) {
+      pump_bidirectional(client, *upstream, pending, "");
+    };
     return;
   }
-  resp.status = r.status;
-  resp.body = std::move(r.body);
-  for (const auto& kv : r.headers) {
+  auto r = with_retries([&] { return http_open(req.method, url, req.body, h, timeout_ms, &err); });
+  if (!r) {
+    resp.text(503, "upstream connect error or disconnect/reset before headers. reset reason: " + err + "\n");
+    return;
+  }
+  resp.status = r->status;
+  for (const auto& kv : r->headers) {
     std::string k = to_lower(kv.first);
     if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
     resp.headers[kv.first] = kv.second;
   }
+  if (!r->chunked && r->length >= 0 && r->length <= (4 << 20)) {
+    resp.body = r->read_all();  // small, framed body: buffered (keeps the client connection alive)
+    return;
+  }
+  // chunked / EOF-delimited / large bodies (log follow, watch, server-sent events, downloads)
+  // are relayed piece by piece as they arrive
+  std::shared_ptr<HttpClientResponse> body(std::move(r));
+  streams_->inc();
+  resp.stream = [body](StreamWriter& w) {
+    std::string piece;
+    for (;;) {
+      const auto n = body->next(piece);
+      if (n == HttpClientResponse::kTimeout) {
+        if (!w.alive()) return;
+        continue;
+      }
+      if (n != HttpClientResponse::kData || !w.write(piece)) return;
+    }
+  };
 }
 
 }  // namespace kf

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "core/http.h"
+#include "core/metrics.h"
 #include "gpu/topology.h"
 #include "runtime/runtime.h"
 
@@ -145,6 +146,7 @@ class Gateway {
   Informer* vs_ = nullptr;
   Informer* routes_ = nullptr;
   std::unique_ptr<HttpServer> srv_;
+  std::shared_ptr<CounterVec> upgrades_, streams_;
 };
 
 }  // namespace kf

@@ -237,3 +237,106 @@ def test_concurrent_pod_creates_never_overcommit_quota(c, cluster, hard_key, har
     with cf.ThreadPoolExecutor(8) as ex:
         results = list(ex.map(create, range(100, 108)))
     assert sum(results) == 1, results
+
+
+def _ws_client_frame(payload: bytes, op: int = 1) -> bytes:
+    import os as _os
+    import struct
+    mask = _os.urandom(4)
+    n = len(payload)
+    head = struct.pack(">BB", 0x80 | op, 0x80 | n) if n < 126 else struct.pack(">BBH", 0x80 | op, 0x80 | 126, n)
+    return head + mask + bytes(b ^ mask[i & 3] for i, b in enumerate(payload))
+
+
+def _ws_read(sock_file):
+    import struct
+    h = sock_file.read(2)
+    op, n = h[0] & 0x0F, h[1] & 0x7F
+    if n == 126:
+        n = struct.unpack(">H", sock_file.read(2))[0]
+    elif n == 127:
+        n = struct.unpack(">Q", sock_file.read(8))[0]
+    return op, sock_file.read(n)
+
+
+def test_gateway_tunnels_kernel_websocket_and_streams_events(c, cluster):
+    """JupyterLab's kernel channel WebSocket through the notebook's
+    VirtualService route (notebook_controller.go:519-619), and a streamed (chunked) response
+    relayed as it is produced instead of buffered."""
+    import base64
+    import hashlib
+    import os as _os
+    import socket
+    import urllib.parse
+    c.create(_notebook("ws1", "e2e"))
+    c.wait_for(NB, "Notebook", "ws1", "e2e", _ready, timeout=30)
+    base = cluster.gateway + "/notebook/e2e/ws1"
+    deadline = time.time() + 15
+    while True:
+        try:
+            req = urllib.request.Request(base + "/api/kernels", data=b'{"name": "python3"}', method="POST",
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=5) as r:
+                kid = json.loads(r.read())["id"]
+            break
+        except (urllib.error.URLError, ConnectionError):
+            if time.time() > deadline:
+                raise
+            time.sleep(0.2)
+    gw = urllib.parse.urlparse(cluster.gateway)
+    key = base64.b64encode(_os.urandom(16)).decode()
+    s = socket.create_connection((gw.hostname, gw.port), timeout=10)
+    try:
+        s.sendall((f"GET /notebook/e2e/ws1/api/kernels/{kid}/channels?session_id=abc HTTP/1.1\r\n"
+                   f"Host: {gw.hostname}:{gw.port}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+                   f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\n\r\n").encode())
+        f = s.makefile("rb")
+        status = f.readline()
+        assert b" 101 " in status, status
+        headers = {}
+        while True:
+            line = f.readline().strip()
+            if not line:
+                break
+            k, v = line.decode().split(":", 1)
+            headers[k.strip().lower()] = v.strip()
+        want = base64.b64encode(hashlib.sha1((key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11").encode()).digest()).decode()
+        assert headers["sec-websocket-accept"] == want
+        # the open channel is visible to the culler as a connection
+        with urllib.request.urlopen(base + f"/api/kernels/{kid}", timeout=5) as r:
+            assert json.loads(r.read())["connections"] == 1
+        msg = {"header": {"msg_id": "m1", "msg_type": "execute_request", "session": "abc", "version": "5.3"},
+               "parent_header": {}, "metadata": {}, "channel": "shell",
+               "content": {"code": "print(355)", "silent": False}}
+        s.sendall(_ws_client_frame(json.dumps(msg).encode()))
+        seen = []
+        while "execute_reply" not in seen:
+            op, data = _ws_read(f)
+            assert op == 1
+            m = json.loads(data)
+            assert m["parent_header"]["msg_id"] == "m1"
+            seen.append(m["header"]["msg_type"])
+            if m["header"]["msg_type"] == "stream":
+                assert m["content"]["text"] == "print(355)"
+        assert seen[:3] == ["status", "execute_input", "stream"]
+        s.sendall(_ws_client_frame(b"", op=8))
+        ops = []
+        while not ops or ops[-1] != 8:
+            op, data = _ws_read(f)
+            ops.append(op)
+            if op == 1:  # the trailing idle status
+                assert json.loads(data)["content"] == {"execution_state": "idle"}
+        assert ops[-1] == 8
+    finally:
+        s.close()
+    # streamed response: 6 events 250 ms apart; the first must arrive long before the last
+    t0 = time.time()
+    with urllib.request.urlopen(base + "/api/events/stream?n=6&interval_ms=250", timeout=10) as r:
+        assert r.headers["Content-Type"] == "text/event-stream"
+        first = r.readline()
+        t_first = time.time() - t0
+        rest = r.read()
+    t_all = time.time() - t0
+    assert first.startswith(b"id: 0") and rest.count(b"data: ") == 6
+    assert t_all >= 1.2 and t_first < 0.6, (t_first, t_all)
+    c.delete(NB, "Notebook", "ws1", "e2e")
