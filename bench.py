@@ -42,6 +42,8 @@ def parse_args():
     p.add_argument("--k", type=int, default=8192)
     p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "10")),
                    help="cold-start runs of one N-GPU notebook through the native control plane (rank 0)")
+    p.add_argument("--coldstart-torch-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_TORCH_RUNS", "5")),
+                   help="cold-start runs with the torch-ready notebook server (torch import + GEMM before Ready)")
     p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
     p.add_argument("--no-allreduce-sweep", action="store_true",
                    help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
@@ -158,7 +160,16 @@ def main() -> int:
                 extra["cold_start_p90_s"] = cs["p90_s"]
                 extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
                 extra["cold_start_readiness"] = cs.get("readiness")
-                extra["cold_start_note"] = "process pods (no container runtime); notebook server = stub recipe"
+                extra["cold_start_note"] = ("process pods (no container runtime); notebook server = stub recipe "
+                                            "(no torch import); cold_start_torch_ready_* = same path with a server "
+                                            "that imports torch + runs a GEMM on the GPU before Ready")
+                if args.coldstart_torch_runs > 0:
+                    ct = measure_cold_start(runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready",
+                                            namespace="bench-torch")
+                    extra["cold_start_torch_ready_runs"] = len(ct["runs"])
+                    extra["cold_start_torch_ready_p50_s"] = ct["p50_s"]
+                    extra["cold_start_torch_ready_p90_s"] = ct["p90_s"]
+                    extra["cold_start_torch_ready_phases_p50_s"] = ct.get("phases_p50_s")
             except Exception as e:  # reported, never fatal for the GEMM number
                 extra["cold_start_error"] = f"{type(e).__name__}: {e}"
         if world > 1:

@@ -50,10 +50,21 @@ def _pct(xs: list[float], q: float) -> float:
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
+SERVERS = {
+    # stdlib HTTP notebook server (no torch import): the control plane + readiness-op path alone
+    "stub": {},
+    # jupyter-pytorch-rocm: the server imports torch + kubeflow_rm_amd.ops and runs a GEMM on the
+    # allocated GPU before it listens; a readinessProbe makes Ready wait for it
+    "torch-ready": {"env": [{"name": "KFAMD_WARMUP", "value": "torch"}], "probe": True},
+}
+
+
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
                        readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
-                       settle_s: float = 0.5) -> dict:
+                       settle_s: float = 0.5, server: str = "stub") -> dict:
     """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...}}.
+
+    ``server``: "stub" or "torch-ready" (see SERVERS). Both are process pods (no container runtime).
 
     ``settle_s``: pause after the previous run's pod is gone, so runs are independent cold starts.
     The amdgpu KFD tears a GPU process down asynchronously after it exits and the next open of
@@ -67,10 +78,16 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
         for i in range(runs):
             name = f"cs-{i}"
             ann = {} if readiness else {"kfamd.io/gpu-readiness-op": "false"}
+            ctr = {"name": name, "image": image, "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}}}
+            srv = SERVERS[server]
+            if srv.get("env"):
+                ctr["env"] = list(srv["env"])
+            if srv.get("probe"):
+                ctr["readinessProbe"] = {"httpGet": {"path": f"/notebook/{namespace}/{name}/api/status", "port": 8888},
+                                         "periodSeconds": 5}
             nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook",
                   "metadata": {"name": name, "namespace": namespace, "annotations": ann},
-                  "spec": {"template": {"spec": {"containers": [{"name": name, "image": image,
-                                                                 "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}}}]}}}}
+                  "spec": {"template": {"spec": {"containers": [ctr]}}}}
             t0 = time.time()
             c.create(nb)
             obj = c.wait_for("kubeflow.org/v1", "Notebook", name, namespace,
@@ -100,7 +117,14 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                 stages = {"hip_init_ms": rep.get("hip_init_ms"), "total_ms": rep.get("total_ms"),
                           **{f"{k}_ms": v for k, v in (rep.get("stages_ms") or {}).items()},
                           **{f"gemm_{k}": v for k, v in (rep.get("gemm0_stages_ms") or {}).items()}}
+            ctl_phases = None
+            try:
+                ctl_phases = json.loads((c.get("kubeflow.org/v1", "Notebook", name, namespace)["metadata"].get("annotations")
+                                         or {}).get("notebooks.kubeflow.org/cold-start-phases", "null"))
+            except Exception:
+                pass
             out_runs.append({"cold_start_s": t1 - t0, "phases": phases, "readiness_stages": stages,
+                             "controller_phases_ms": ctl_phases,
                              "gpus": (obj.get("status") or {}).get("gpus"),
                              "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
             c.delete("kubeflow.org/v1", "Notebook", name, namespace)
@@ -116,7 +140,7 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
             time.sleep(settle_s)
     xs = [r["cold_start_s"] for r in out_runs]
     phase_keys = sorted({k for r in out_runs for k in r["phases"]})
-    res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs,
+    res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs, "server": server,
            "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
     stage_keys = sorted({k for r in out_runs for k, v in r["readiness_stages"].items() if v is not None})
     if stage_keys:
@@ -135,9 +159,11 @@ def main() -> int:
     p.add_argument("--gpus", type=int, default=None, help="node GPUs (default: discover; -> synthetic 8 without /dev/kfd)")
     p.add_argument("--no-readiness", action="store_true")
     p.add_argument("--settle", type=float, default=0.5, help="seconds between runs (0: back to back)")
+    p.add_argument("--server", choices=sorted(SERVERS), default="stub",
+                   help="notebook server recipe: stub (no torch) or torch-ready (torch import + GEMM before Ready)")
     a = p.parse_args()
     r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness,
-                           settle_s=a.settle)
+                           settle_s=a.settle, server=a.server)
     print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
     print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
     return 0

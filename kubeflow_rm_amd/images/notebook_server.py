@@ -12,6 +12,11 @@ the Jupyter messaging protocol's JSON form (kernel_info / execute requests get s
 execute_reply messages; an open channel counts in the kernel's `connections`, which the culler
 reads). {prefix}/api/events/stream is a text/event-stream (server-sent events) endpoint, for
 checking that proxies relay responses as they are produced.
+KFAMD_WARMUP=torch (the jupyter-pytorch-rocm recipe in the cold-start bench): before it listens,
+the server imports torch and kubeflow_rm_amd.ops and runs one bf16 MFMA GEMM on the pod's GPU —
+the kernel-runtime start that SURVEY §7.4(5) names as the dominant cold-start phase; with a
+readinessProbe on {prefix}/api/status the pod is Ready only once torch can use the GPU. The
+timings are served at {prefix}/api/gpu ("warmup").
 Requests that arrive without the prefix (rewritten routes of group-one / group-two servers) are
 served too. GET {prefix}/api/gpu reports the GPUs this pod was given (HIP_VISIBLE_DEVICES) and
 the readiness-op result when present.
@@ -35,6 +40,26 @@ _LOCK = threading.Lock()
 KERNELS: dict[str, dict] = {}
 TERMINALS: dict[str, dict] = {}
 STARTED = time.time()
+WARMUP: dict = {}
+
+
+def warmup_torch() -> dict:
+    """import torch + the framework's kernels and run one GEMM on cuda:0 (the pod's first GPU)."""
+    t0 = time.perf_counter()
+    import torch
+    t1 = time.perf_counter()
+    from kubeflow_rm_amd import ops
+    t2 = time.perf_counter()
+    dev = torch.device("cuda", 0)
+    a = torch.randn(1024, 1024, device=dev).to(torch.bfloat16)
+    b = torch.randn(1024, 1024, device=dev).to(torch.bfloat16)
+    c = ops.gemm_nt(a, b)
+    torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
+    ok = bool(torch.isfinite(c.float()).all().item())
+    return {"ok": ok, "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
+            "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1),
+            "device": torch.cuda.get_device_name(dev)}
 
 
 def _now() -> str:
@@ -208,7 +233,7 @@ def make_handler(prefix: str):
             if p == "/api/gpu":
                 info = {"HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
                         "ring": os.environ.get("KFAMD_XGMI_RING"),
-                        "topology": os.environ.get("KFAMD_GPU_TOPOLOGY")}
+                        "topology": os.environ.get("KFAMD_GPU_TOPOLOGY"), "warmup": WARMUP or None}
                 return self.send_json(200, info)
             if p in ("/", "/lab", "/tree", "/lab/"):
                 html = (f"<html><head><title>kflite notebook</title></head><body><h1>Notebook server</h1>"
@@ -258,6 +283,9 @@ def make_handler(prefix: str):
 def main(argv=None) -> int:
     prefix = os.environ.get("NB_PREFIX", "")
     port = int(os.environ.get("NB_PORT", (os.environ.get("KFAMD_CONTAINER_PORTS") or "8888").split(",")[0] or 8888))
+    if os.environ.get("KFAMD_WARMUP") == "torch":
+        WARMUP.update(warmup_torch())
+        print(f"[kflite-notebook] warmup {json.dumps(WARMUP)}", flush=True)
     srv = serve(make_handler(prefix), port)
     print(f"[kflite-notebook] serving {prefix or '/'} on {srv.server_address[0]}:{port} home={os.environ.get('HOME')}",
           flush=True)

@@ -125,6 +125,11 @@ std::shared_ptr<NotebookMetrics> NotebookMetrics::install(std::shared_ptr<Client
   m->culling_total = reg.counter("notebook_culling_total", "Total times of culling notebooks", {"namespace", "name"});
   m->last_culling_timestamp = reg.gauge("last_notebook_culling_timestamp_seconds", "Timestamp of the last notebook culling in seconds",
                                         {"namespace", "name"});
+  m->cold_start_seconds = reg.histogram(
+      "notebook_cold_start_seconds",
+      "Notebook first start by phase: observed->statefulset, statefulset->scheduled, scheduled->initialized "
+      "(in-pod GPU readiness op), initialized->ready, total (observed->notebook ready)",
+      {"phase"}, HistogramVec::exponential(0.001, 2, 18));
   reg.add_collector(std::make_shared<CollectorFamily>(
       "notebook_running", "Current running notebooks in the cluster", "gauge", std::vector<std::string>{"namespace"},
       [c]() {

@@ -32,6 +32,7 @@ constexpr const char* GPU_MEMORY_RESOURCE = "amd.com/gpu-memory";
 constexpr const char* ANNOTATION_GPU_IDS = "amd.com/gpu-ids";
 constexpr const char* ANNOTATION_XGMI_RING = "amd.com/xgmi-ring";
 constexpr const char* ANNOTATION_GPU_READINESS = "notebooks.kubeflow.org/gpu-readiness";
+// first-start phase breakdown (ms) written once on the Notebook when it is Ready (notebook.cc)
 constexpr const char* ANNOTATION_COLD_START = "notebooks.kubeflow.org/cold-start-phases";
 
 bool stop_annotation_is_set(const Json& obj);
@@ -54,6 +55,8 @@ ApiError reconcile_owned(Client& c, const Json& desired, CopyKind kind, Json* li
 struct NotebookMetrics {
   std::shared_ptr<CounterVec> create_total, create_failed_total, culling_total;
   std::shared_ptr<GaugeVec> last_culling_timestamp;
+  // MI355X extension: first-start latency of each Notebook by phase (seconds)
+  std::shared_ptr<HistogramVec> cold_start_seconds;
   // notebook_running is computed at scrape time from the StatefulSet list (metrics.go:82-99)
   static std::shared_ptr<NotebookMetrics> install(std::shared_ptr<Client> c);
 };

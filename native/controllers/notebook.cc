@@ -1,4 +1,6 @@
 // notebook.cc — N2 NotebookReconciler (reference notebook-controller/controllers/notebook_controller.go).
+#include <cmath>
+
 #include "controllers/notebook.h"
 
 #include "core/util.h"
@@ -181,7 +183,16 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
     return {};
   }
   // foreground deletion by the JWA: do nothing while terminating
-  if (nb.at_path({"metadata", "deletionTimestamp"}).is_string()) return {};
+  if (nb.at_path({"metadata", "deletionTimestamp"}).is_string()) {
+    std::lock_guard<std::mutex> g(cs_mu_);
+    cold_.erase(nb.str_at({"metadata", "uid"}));
+    return {};
+  }
+  if (annotation(nb, ANNOTATION_COLD_START).empty() && nb.at_path({"status", "readyReplicas"}).as_int(0) != 1) {
+    std::lock_guard<std::mutex> g(cs_mu_);
+    auto& cs = cold_[nb.str_at({"metadata", "uid"})];
+    if (cs.seen == 0) cs.seen = now_seconds();
+  }
 
   // ---- StatefulSet
   Json ss = generate_statefulset(nb, o_);
@@ -201,6 +212,9 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
       return {};
     }
     found = obj;
+    std::lock_guard<std::mutex> g(cs_mu_);
+    auto it = cold_.find(nb.str_at({"metadata", "uid"}));
+    if (it != cold_.end()) it->second.sts = now_seconds();
   } else if (e) {
     *err = e.message;
     return {};
@@ -271,6 +285,7 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
     }
     nb = upd;
   }
+  track_cold_start(nb, pod, status);
   // ---- restart annotation: delete the pod once, then clear the annotation
   if (annotation(nb, ANNOTATION_NOTEBOOK_RESTART) == "true") {
     KF_INFO("notebook-controller", "Annotation restart-pod is set, restarting the pod", Json{{"notebook", req.str()}});
@@ -290,6 +305,53 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
     }
   }
   return {};
+}
+
+// the cold-start phases of a Notebook's first start, from the controller's own
+// observations (first reconcile, StatefulSet create, Ready) and the pod's condition transition
+// times (the kubelet stamps them with ms precision). Exported as the notebook_cold_start_seconds
+// histogram and as the kfamd.io/cold-start annotation on the Notebook.
+void NotebookReconciler::track_cold_start(const Json& nb, const Json& pod, const Json& status) {
+  const std::string uid = nb.str_at({"metadata", "uid"});
+  ColdStart cs;
+  {
+    std::lock_guard<std::mutex> g(cs_mu_);
+    auto it = cold_.find(uid);
+    if (it == cold_.end()) return;
+    if (status["readyReplicas"].as_int(0) != 1) return;
+    cs = it->second;
+    cold_.erase(it);
+  }
+  const double now = now_seconds();
+  auto cond_time = [&](const std::string& type) -> double {
+    for (const auto& c : pod.at_path({"status", "conditions"}).as_array())
+      if (c["type"].as_string() == type && c["status"].as_string() == "True") {
+        auto ms = parse_rfc3339_ms(c["lastTransitionTime"].as_string());
+        if (ms) return static_cast<double>(*ms) / 1000.0;
+      }
+    return 0;
+  };
+  const double sched = cond_time("PodScheduled"), init = cond_time("Initialized"), ready = cond_time("Ready");
+  Json phases = Json::object();
+  auto phase = [&](const char* name, double a, double b) {
+    if (a <= 0 || b <= 0 || b < a) return;
+    m_->cold_start_seconds->observe({name}, b - a);
+    phases[std::string(name) + "_ms"] = std::round((b - a) * 1e4) / 10.0;
+  };
+  phase("observed_to_statefulset", cs.seen, cs.sts);
+  phase("statefulset_to_scheduled", cs.sts, sched);
+  phase("scheduled_to_initialized", sched, init);
+  phase("initialized_to_ready", init, ready);
+  phase("total", cs.seen, now);
+  const std::string val = phases.dump();
+  ApiError e = c_->update_with_retry("kubeflow.org/v1beta1", "Notebook", nb.str_at({"metadata", "namespace"}),
+                                     nb.str_at({"metadata", "name"}), [&val](Json& o) {
+                                       if (!o["metadata"]["annotations"].is_object()) o["metadata"]["annotations"] = Json::object();
+                                       if (o["metadata"]["annotations"].has(ANNOTATION_COLD_START)) return false;
+                                       o["metadata"]["annotations"][ANNOTATION_COLD_START] = val;
+                                       return true;
+                                     });
+  if (e) KF_WARN("notebook-controller", "cannot record cold-start phases", Json{{"error", e.message}});
 }
 
 void NotebookReconciler::setup(Manager& mgr, int workers) {

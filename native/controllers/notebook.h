@@ -2,6 +2,9 @@
 // components/notebook-controller/controllers/{notebook_controller.go,culling_controller.go}).
 #pragma once
 
+#include <map>
+#include <mutex>
+
 #include <memory>
 #include <string>
 
@@ -41,11 +44,19 @@ class NotebookReconciler {
 
  private:
   Result reemit_event(const Json& event, std::string* err);
+  void track_cold_start(const Json& nb, const Json& pod, const Json& status);
   std::shared_ptr<Client> c_;
   NotebookOptions o_;
   std::shared_ptr<NotebookMetrics> m_;
   std::unique_ptr<EventRecorder> rec_;
   std::shared_ptr<Controller> ctl_;
+  // first-start tracking, by Notebook uid: when the controller first saw it, when it created the
+  // StatefulSet (process-local clock; a restarted controller simply skips in-flight notebooks)
+  struct ColdStart {
+    double seen = 0, sts = 0;
+  };
+  std::mutex cs_mu_;
+  std::map<std::string, ColdStart> cold_;
 };
 
 struct CullingOptions {

@@ -895,7 +895,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
                 }
               }
               // probe fast until the first success (cold-start latency), then at periodSeconds
-              cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.1);
+              cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.02);
             }
             const Json& lp = c["livenessProbe"];
             if (lp.is_object() && now >= cr.next_live_probe) {

@@ -340,3 +340,23 @@ def test_gateway_tunnels_kernel_websocket_and_streams_events(c, cluster):
     assert first.startswith(b"id: 0") and rest.count(b"data: ") == 6
     assert t_all >= 1.2 and t_first < 0.6, (t_first, t_all)
     c.delete(NB, "Notebook", "ws1", "e2e")
+
+
+def test_cold_start_phases_recorded_on_notebook_and_exported(c, cluster):
+    """the first start of a Notebook is broken into phases by the controller
+    (annotation notebooks.kubeflow.org/cold-start-phases + notebook_cold_start_seconds histogram)."""
+    c.create(_notebook("cs1", "e2e", gpus=1))
+    nb = c.wait_for(NB, "Notebook", "cs1", "e2e",
+                    lambda o: "notebooks.kubeflow.org/cold-start-phases" in (o["metadata"].get("annotations") or {}),
+                    timeout=30)
+    ph = json.loads(nb["metadata"]["annotations"]["notebooks.kubeflow.org/cold-start-phases"])
+    for k in ("observed_to_statefulset_ms", "statefulset_to_scheduled_ms", "scheduled_to_initialized_ms",
+              "initialized_to_ready_ms", "total_ms"):
+        assert k in ph and ph[k] >= 0, ph
+    assert ph["total_ms"] >= ph["scheduled_to_initialized_ms"]
+    with urllib.request.urlopen(cluster.url + "/metrics", timeout=5) as r:
+        text = r.read().decode()
+    count = [ln for ln in text.splitlines() if ln.startswith('notebook_cold_start_seconds_count{phase="total"}')]
+    assert count and float(count[0].split()[-1]) >= 1
+    # written once: a pod restart does not rewrite it
+    c.delete(NB, "Notebook", "cs1", "e2e")
