@@ -55,6 +55,11 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
     out_shape = (batch, M, N) if batched else (*a.shape[:-1], N)
     if out is None:
         out = torch.empty(out_shape, dtype=torch.bfloat16, device=a.device)
+    else:
+        # the kernel writes bf16 bit patterns with a 16-byte-aligned, unit-stride row layout
+        _check_operand(out, "out")
+        if out.device != a.device or tuple(out.shape) != tuple(out_shape):
+            raise ValueError(f"out must be a bf16 {tuple(out_shape)} tensor on {a.device}, got {tuple(out.shape)} on {out.device}")
     c3 = out.view(batch, M, N) if batched else out.view(M, N)
     lda = a3.stride(-2) if a3.dim() >= 2 else K
     ldb = b.stride(-2)

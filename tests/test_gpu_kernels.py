@@ -149,3 +149,18 @@ def test_gemm_w4_needs_16b_output_rows():
     ref = (a.float() @ b.float().t())
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
     assert torch.all(big[:, N:] == 0)  # nothing written past the row
+
+
+def test_gemm_rejects_bad_out_tensor():
+    """a user-supplied ``out`` of the wrong dtype / shape / device must be refused, not
+    filled with bf16 bit patterns."""
+    from kubeflow_rm_amd import ops
+    a, b = _rand(256, 64), _rand(256, 64, seed=1)
+    with pytest.raises(TypeError):
+        ops.gemm_nt(a, b, out=torch.empty(256, 256, device="cuda", dtype=torch.float32))
+    with pytest.raises(ValueError):
+        ops.gemm_nt(a, b, out=torch.empty(256 * 256, device="cuda", dtype=torch.bfloat16))
+    with pytest.raises(ValueError):
+        ops.gemm_nt(a, b, out=torch.empty(256, 512, device="cuda", dtype=torch.bfloat16)[:, ::2])
+    out = torch.empty(256, 256, device="cuda", dtype=torch.bfloat16)
+    assert ops.gemm_nt(a, b, out=out) is out
