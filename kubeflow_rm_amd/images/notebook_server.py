@@ -233,7 +233,9 @@ def make_handler(prefix: str):
             if p == "/api/gpu":
                 info = {"HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
                         "ring": os.environ.get("KFAMD_XGMI_RING"),
-                        "topology": os.environ.get("KFAMD_GPU_TOPOLOGY"), "warmup": WARMUP or None}
+                        "topology": os.environ.get("KFAMD_GPU_TOPOLOGY"), "warmup": WARMUP or None,
+                        "KFAMD_CPU_AFFINITY": os.environ.get("KFAMD_CPU_AFFINITY"),
+                        "cpus_allowed": sorted(os.sched_getaffinity(0))}
                 return self.send_json(200, info)
             if p in ("/", "/lab", "/tree", "/lab/"):
                 html = (f"<html><head><title>kflite notebook</title></head><body><h1>Notebook server</h1>"

@@ -49,6 +49,21 @@ std::map<std::string, double> pod_quota_usage(const Json& pod, int64_t hbm_gib_p
 }
 
 namespace {
+// HBM per schedulable GPU as the nodes advertise it (capacity amd.com/gpu-memory / amd.com/gpu):
+// 288 GiB on an SPX/NPS1 MI355X, a share of it per partition in CPX/NPS2 modes. The largest value
+// across nodes is charged (conservative when nodes differ); `fallback` when no node has GPUs.
+int64_t hbm_per_gpu(Client& c, int64_t fallback) {
+  Json nodes;
+  if (c.list("v1", "Node", "", ListOptions(), nodes)) return fallback;
+  double best = 0;
+  for (const auto& n : nodes["items"].as_array()) {
+    const double g = resource_value(GPU_RESOURCE, n.at_path({"status", "capacity", GPU_RESOURCE}));
+    const double m = resource_value(GPU_MEMORY_RESOURCE, n.at_path({"status", "capacity", GPU_MEMORY_RESOURCE}));
+    if (g > 0 && m > 0) best = std::max(best, m / g);
+  }
+  return best > 0 ? static_cast<int64_t>(std::llround(best)) : fallback;
+}
+
 bool pod_counts(const Json& p) {
   const std::string& ph = p.at_path({"status", "phase"}).as_string();
   return ph != "Succeeded" && ph != "Failed" && !p.at_path({"metadata", "deletionTimestamp"}).is_string();
@@ -136,6 +151,7 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
     if (c->list("v1", "ResourceQuota", a.ns, ListOptions(), quotas)) return {};
     if (quotas["items"].empty()) return {};
     std::lock_guard<std::mutex> serial(ledger->ns_lock(a.ns));
+    const int64_t hbm_dev = hbm_per_gpu(*c, hbm);
     Json pods;
     c->list("v1", "Pod", a.ns, ListOptions(), pods);
     std::map<std::string, double> used;
@@ -143,11 +159,11 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
     for (const auto& p : pods["items"].as_array()) {
       committed.insert(p.str_at({"metadata", "name"}));
       if (pod_counts(p))
-        for (auto& kv : pod_quota_usage(p, hbm)) used[kv.first] += kv.second;
+        for (auto& kv : pod_quota_usage(p, hbm_dev)) used[kv.first] += kv.second;
     }
     for (const auto& r : ledger->live(a.ns, committed))
       for (const auto& kv : r) used[kv.first] += kv.second;
-    auto want = pod_quota_usage(*a.object, hbm);
+    auto want = pod_quota_usage(*a.object, hbm_dev);
     for (const auto& q : quotas["items"].as_array()) {
       std::vector<std::string> exceeded;
       for (const auto& h : q.at_path({"spec", "hard"}).as_object()) {
@@ -180,9 +196,10 @@ Result QuotaController::reconcile(const Request& r, std::string* err) {
     return {};
   }
   std::map<std::string, double> used;
+  const int64_t hbm_dev = hbm_per_gpu(*c_, hbm_);
   pods_->visit(r.ns, [&](const Json& p) {
     if (pod_counts(p))
-      for (auto& kv : pod_quota_usage(p, hbm_)) used[kv.first] += kv.second;
+      for (auto& kv : pod_quota_usage(p, hbm_dev)) used[kv.first] += kv.second;
   });
   Json hard = q.at_path({"spec", "hard"});
   Json u = Json::object();

@@ -318,8 +318,23 @@ void register_odh(CapiRegistry& R) {
 }
 
 void register_gpu(CapiRegistry& R) {
+  R.add("cpulist_roundtrip", [](const Json& a) -> Json {
+    auto v = parse_cpulist(a["s"].as_string());
+    Json arr = Json::array();
+    for (int c : v) arr.push_back(c);
+    return Json{{"cpus", arr}, {"formatted", format_cpulist(v)}};
+  });
   R.add("topology_synthetic", [](const Json& a) -> Json { return topo_from(a).to_json(); });
   R.add("topology_discover", [](const Json& a) -> Json {
+    if (a["sysfs_root"].is_string()) {
+      GpuTopology t = GpuTopology::discover(SysfsRoots::under(a["sysfs_root"].as_string()));
+      Json j = t.to_json();
+      j["describe"] = t.describe();
+      Json lc = Json::array();
+      for (int c : t.local_cpus({0})) lc.push_back(c);
+      j["localCpusDevice0"] = lc;
+      return j;
+    }
     return a["root"].is_string() ? GpuTopology::discover(a["root"].as_string()).to_json() : GpuTopology::discover().to_json();
   });
   R.add("gpu_choose", [](const Json& a) -> Json {

@@ -23,6 +23,8 @@ struct ComponentFlags {
   std::string python = "python3";
   double restart_backoff = 10.0;
   std::string pod_cidr_prefix = "127.20";
+  std::string sysfs_root;  // GPU discovery root ("" = /sys)
+  bool numa_pinning = true;
   // gateway (Istio ingress equivalent)
   std::string gateway_addr = "127.0.0.1";
   int64_t gateway_port = 0;

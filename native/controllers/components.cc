@@ -24,6 +24,8 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("python", &python, "python3", "python interpreter for pod image recipes");
   f.add_double("restart-backoff", &restart_backoff, 10.0, "base container restart back-off in seconds");
   f.add_string("pod-cidr-prefix", &pod_cidr_prefix, "127.20", "pod IPs are allocated as <prefix>.x.y (loopback)");
+  f.add_string("sysfs-root", &sysfs_root, "", "sysfs root for GPU / PCI / NUMA discovery (default /sys)");
+  f.add_bool("numa-pinning", &numa_pinning, true, "pin GPU pods to their GPUs' NUMA-local CPUs");
   f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
   f.add_int("gateway-port", &gateway_port, 0, "ingress gateway port (0 = ephemeral)");
   f.add_string("gateway-name", &gateway_name, "kubeflow/kubeflow-gateway", "VirtualService gateway served by the ingress");
@@ -203,6 +205,8 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     kc.pod_ip_prefix = I.f.pod_cidr_prefix;
     kc.restart_backoff = I.f.restart_backoff;
     kc.gpus = static_cast<int>(I.f.gpus);
+    kc.sysfs_root = I.f.sysfs_root;
+    kc.numa_pinning = I.f.numa_pinning;
     I.kubelet = std::make_unique<Kubelet>(I.c, kc);
     I.kubelet->setup(mgr);
     if (I.api) {

@@ -191,7 +191,7 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
   if (annotation(nb, ANNOTATION_COLD_START).empty() && nb.at_path({"status", "readyReplicas"}).as_int(0) != 1) {
     std::lock_guard<std::mutex> g(cs_mu_);
     auto& cs = cold_[nb.str_at({"metadata", "uid"})];
-    if (cs.seen == 0) cs.seen = now_seconds();
+    if (cs.seen == 0) cs.seen = now_unix_ms() / 1000.0;  // wall clock: compared with pod condition times
   }
 
   // ---- StatefulSet
@@ -214,7 +214,7 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
     found = obj;
     std::lock_guard<std::mutex> g(cs_mu_);
     auto it = cold_.find(nb.str_at({"metadata", "uid"}));
-    if (it != cold_.end()) it->second.sts = now_seconds();
+    if (it != cold_.end()) it->second.sts = now_unix_ms() / 1000.0;
   } else if (e) {
     *err = e.message;
     return {};
@@ -322,7 +322,7 @@ void NotebookReconciler::track_cold_start(const Json& nb, const Json& pod, const
     cs = it->second;
     cold_.erase(it);
   }
-  const double now = now_seconds();
+  const double now = now_unix_ms() / 1000.0;
   auto cond_time = [&](const std::string& type) -> double {
     for (const auto& c : pod.at_path({"status", "conditions"}).as_array())
       if (c["type"].as_string() == type && c["status"].as_string() == "True") {

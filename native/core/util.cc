@@ -58,6 +58,10 @@ std::string to_lower(std::string s) {
   for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
   return s;
 }
+std::string to_upper(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+  return s;
+}
 std::string replace_all(std::string s, const std::string& from, const std::string& to) {
   if (from.empty()) return s;
   size_t pos = 0;

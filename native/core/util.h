@@ -23,6 +23,7 @@ bool starts_with(const std::string& s, const std::string& p);
 bool ends_with(const std::string& s, const std::string& p);
 bool contains(const std::string& s, const std::string& p);
 std::string to_lower(std::string s);
+std::string to_upper(std::string s);
 std::string replace_all(std::string s, const std::string& from, const std::string& to);
 std::string url_decode(const std::string& s);
 std::string url_encode(const std::string& s);

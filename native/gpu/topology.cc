@@ -50,6 +50,7 @@ GpuTopology GpuTopology::synthetic(int n, int numa_nodes) {
     char bus[32];
     std::snprintf(bus, sizeof bus, "0000:%02x:00.0", 0x05 + i * 0x10);
     d.pci_bus = bus;
+    d.physical = i;
     t.gpus.push_back(d);
   }
   t.link.assign(n, std::vector<int>(n, 1));
@@ -61,9 +62,68 @@ GpuTopology GpuTopology::synthetic(int n, int numa_nodes) {
   return t;
 }
 
+std::vector<int> parse_cpulist(const std::string& s) {
+  std::set<int> out;
+  for (const auto& part : split(trim(s), ',', true)) {
+    const size_t dash = part.find('-');
+    const int a = std::atoi(part.c_str());
+    const int b = dash == std::string::npos ? a : std::atoi(part.c_str() + dash + 1);
+    for (int c = a; c <= b && c - a < 65536; ++c) out.insert(c);
+  }
+  return {out.begin(), out.end()};
+}
+
+std::string format_cpulist(const std::vector<int>& cpus) {
+  std::vector<int> v(cpus);
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  std::string out;
+  for (size_t i = 0; i < v.size();) {
+    size_t j = i;
+    while (j + 1 < v.size() && v[j + 1] == v[j] + 1) ++j;
+    if (!out.empty()) out += ",";
+    out += std::to_string(v[i]);
+    if (j > i) out += "-" + std::to_string(v[j]);
+    i = j + 1;
+  }
+  return out;
+}
+
+SysfsRoots SysfsRoots::under(const std::string& prefix) {
+  SysfsRoots r;
+  r.kfd = prefix + "/class/kfd/kfd/topology/nodes";
+  r.pci = prefix + "/bus/pci/devices";
+  r.node = prefix + "/devices/system/node";
+  return r;
+}
+
+std::vector<int> GpuTopology::local_cpus(const std::vector<int>& devices) const {
+  std::vector<int> out;
+  for (int d : devices) {
+    if (d < 0 || d >= size()) continue;
+    for (int c : parse_cpulist(gpus[d].cpulist)) out.push_back(c);
+  }
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  return out;
+}
+
+int GpuTopology::physical_count() const {
+  std::set<int> p;
+  for (const auto& g : gpus) p.insert(g.physical);
+  return static_cast<int>(p.size());
+}
+
 GpuTopology GpuTopology::discover(const std::string& root) {
+  SysfsRoots r;
+  r.kfd = root;
+  return discover(r);
+}
+
+GpuTopology GpuTopology::discover(const SysfsRoots& roots) {
   const std::string fake = getenv_or("KFAMD_FAKE_GPUS", "");
   if (!fake.empty()) return synthetic(std::atoi(fake.c_str()));
+  const std::string& root = roots.kfd;
   GpuTopology t;
   t.source = "kfd-sysfs";
   std::map<int, int> node_to_gpu;  // kfd node id -> gpu index
@@ -104,10 +164,35 @@ GpuTopology GpuTopology::discover(const std::string& root) {
       hbm += to_i(mp, "size_in_bytes");
     }
     if (hbm > 0) d.hbm_bytes = hbm;
+    // the PCI function: partition modes, NUMA node and the CPUs local to it
+    const std::string pdir = roots.pci + "/" + d.pci_bus;
+    std::string v;
+    if (read_file(pdir + "/current_compute_partition", v) && !trim(v).empty()) d.compute_partition = to_upper(trim(v));
+    if (read_file(pdir + "/current_memory_partition", v) && !trim(v).empty()) d.memory_partition = to_upper(trim(v));
+    if (read_file(pdir + "/local_cpulist", v)) d.cpulist = trim(v);
+    if (read_file(pdir + "/numa_node", v) && std::atoi(trim(v).c_str()) >= 0) d.numa_node = std::atoi(trim(v).c_str());
     node_to_gpu[node] = d.index;
     t.gpus.push_back(d);
   }
   if (t.gpus.empty()) return synthetic(8);
+  // partitions of one package share its PCI function: number packages and partitions in order
+  {
+    std::map<std::string, int> phys, parts;
+    for (auto& g : t.gpus) {
+      if (!phys.count(g.pci_bus)) phys[g.pci_bus] = static_cast<int>(phys.size());
+      g.physical = phys[g.pci_bus];
+      g.partition = parts[g.pci_bus]++;
+    }
+    // KFD reports each node's memory partition (NPSn: 1/n of the package); compute partitions
+    // sharing it split it for accounting: CPX/NPS2 -> 288 / 8 = 36 GiB per device
+    for (auto& g : t.gpus) {
+      g.hbm_visible_bytes = g.hbm_bytes;
+      int nps = std::atoi(g.memory_partition.c_str() + (starts_with(g.memory_partition, "NPS") ? 3 : 0));
+      if (nps <= 0) nps = 1;
+      const int np = std::max(1, parts[g.pci_bus]);
+      g.hbm_bytes = g.hbm_visible_bytes * nps / np;
+    }
+  }
   const int n = t.size();
   t.link.assign(n, std::vector<int>(n, 2));
   t.bandwidth_gbps.assign(n, std::vector<double>(n, 0.0));
@@ -128,6 +213,10 @@ GpuTopology GpuTopology::discover(const std::string& root) {
       }
     }
   }
+  for (auto& g : t.gpus) {
+    std::string v;
+    if (g.cpulist.empty() && read_file(roots.node + "/node" + std::to_string(g.numa_node) + "/cpulist", v)) g.cpulist = trim(v);
+  }
   return t;
 }
 
@@ -141,7 +230,10 @@ Json GpuTopology::to_json() const {
   Json devs = Json::array();
   for (const auto& g : gpus)
     devs.push_back(Json{{"index", g.index}, {"gfx", g.gfx}, {"product", g.product}, {"numa", g.numa_node},
-                        {"hbmBytes", g.hbm_bytes}, {"pciBus", g.pci_bus}, {"xgmiDegree", xgmi_degree(g.index)}});
+                        {"hbmBytes", g.hbm_bytes}, {"hbmVisibleBytes", g.hbm_visible_bytes}, {"pciBus", g.pci_bus}, {"xgmiDegree", xgmi_degree(g.index)},
+                        {"computePartition", g.compute_partition}, {"memoryPartition", g.memory_partition},
+                        {"physical", g.physical}, {"partition", g.partition}, {"simdCount", g.simd_count},
+                        {"cpulist", g.cpulist}});
   Json m = Json::array();
   for (const auto& row : link) {
     Json r = Json::array();
@@ -160,7 +252,11 @@ std::string GpuTopology::describe() const {
     for (int j = 0; j < size(); ++j)
       if (i != j && !xgmi(i, j)) mesh = false;
   }
-  return std::to_string(size()) + "x " + gpus[0].gfx + (mesh ? " full-mesh xGMI" : " partial xGMI") + ", " +
+  std::string parts;
+  if (gpus[0].compute_partition != "SPX" || gpus[0].memory_partition != "NPS1")
+    parts = " (" + std::to_string(physical_count()) + " packages in " + gpus[0].compute_partition + "/" +
+            gpus[0].memory_partition + ")";
+  return std::to_string(size()) + "x " + gpus[0].gfx + parts + (mesh ? " full-mesh xGMI" : " partial xGMI") + ", " +
          std::to_string(numa.size()) + " NUMA node(s)";
 }
 

@@ -33,11 +33,29 @@ struct GpuDevice {
   int numa_node = 0;
   std::string gfx = "gfx950";
   std::string product = "AMD Instinct MI355X";
-  int64_t hbm_bytes = 288LL << 30;
+  int64_t hbm_bytes = 288LL << 30;          // this device's share of its package's HBM (quota unit)
+  int64_t hbm_visible_bytes = 288LL << 30;  // what a process on it can address (its memory partition)
   int simd_count = 1024;  // 256 CUs x 4 SIMDs
   int xcc_count = 8;
   std::string pci_bus;
   int drm_render_minor = -1;  // /sys/class/drm/renderD<minor>: amdgpu sysfs (VRAM use, busy %)
+  std::string compute_partition = "SPX";  // SPX | DPX | QPX | CPX
+  std::string memory_partition = "NPS1";  // NPS1 | NPS2 | NPS4 | NPS8
+  int physical = 0;   // physical MI355X package this device (partition) belongs to
+  int partition = 0;  // partition index within the package
+  std::string cpulist;  // NUMA-local CPUs ("0-47,96-143"); "" = unknown
+};
+
+// "0-3,8,10-11" <-> sorted CPU ids
+std::vector<int> parse_cpulist(const std::string& s);
+std::string format_cpulist(const std::vector<int>& cpus);
+
+struct SysfsRoots {
+  std::string kfd = "/sys/class/kfd/kfd/topology/nodes";
+  std::string pci = "/sys/bus/pci/devices";
+  std::string node = "/sys/devices/system/node";
+  // all three under one prefix (tests: a fake tree)
+  static SysfsRoots under(const std::string& prefix);
 };
 
 struct GpuTopology {
@@ -49,6 +67,10 @@ struct GpuTopology {
   std::string source;  // "kfd-sysfs" | "synthetic"
 
   static GpuTopology discover(const std::string& sysfs_root = "/sys/class/kfd/kfd/topology/nodes");
+  static GpuTopology discover(const SysfsRoots& roots);
+  // CPUs local to a set of devices (union of their cpulists); empty = unknown
+  std::vector<int> local_cpus(const std::vector<int>& devices) const;
+  int physical_count() const;
   static GpuTopology synthetic(int n, int numa_nodes = 2);
   int size() const { return static_cast<int>(gpus.size()); }
   bool xgmi(int a, int b) const { return a != b && link[a][b] == 1; }

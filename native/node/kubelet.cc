@@ -4,6 +4,7 @@
 #include <netinet/in.h>
 #include <poll.h>
 #include <signal.h>
+#include <sched.h>
 #include <spawn.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -145,7 +146,9 @@ struct Kubelet::PodRuntime {
 };
 
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)), cfg_(std::move(cfg)) {
-  GpuTopology topo = cfg_.gpus >= 0 ? GpuTopology::synthetic(cfg_.gpus) : GpuTopology::discover();
+  GpuTopology topo = cfg_.gpus >= 0            ? GpuTopology::synthetic(cfg_.gpus)
+                     : !cfg_.sysfs_root.empty() ? GpuTopology::discover(SysfsRoots::under(cfg_.sysfs_root))
+                                                : GpuTopology::discover();
   alloc_ = std::make_unique<GpuAllocator>(topo);
   recipes_ = Json::parse(kDefaultRecipes);
   if (!cfg_.recipes_file.empty()) {
@@ -251,6 +254,11 @@ Json Kubelet::node_object() const {
     labels["amd.com/gpu.arch"] = topo.gpus[0].gfx;
     labels["amd.com/gpu.product-name"] = "AMD_Instinct_MI355X";
     labels["amd.com/gpu.xgmi"] = topo.describe().find("full-mesh") != std::string::npos ? "full-mesh" : "partial";
+    // partition modes and the HBM each schedulable device really has (CPX/NPS2 split a package)
+    labels["amd.com/gpu.compute-partitioning-mode"] = to_lower(topo.gpus[0].compute_partition);
+    labels["amd.com/gpu.memory-partitioning-mode"] = to_lower(topo.gpus[0].memory_partition);
+    labels["amd.com/gpu.hbm-gib-per-device"] = std::to_string(topo.gpus[0].hbm_bytes >> 30);
+    labels["amd.com/gpu.packages"] = std::to_string(topo.physical_count());
   }
   return Json{{"apiVersion", "v1"},
               {"kind", "Node"},
@@ -326,8 +334,28 @@ void Kubelet::stop() {
 
 // ---- process management ---------------------------------------------------------------------------
 namespace {
+// The child inherits the spawning thread's CPU mask: pin this thread to `cpus` around the spawn
+// (race-free: the child starts with the mask, before any of its threads exist), then restore.
+struct ScopedThreadAffinity {
+  cpu_set_t saved;
+  bool active = false;
+  explicit ScopedThreadAffinity(const std::vector<int>& cpus) {
+    if (cpus.empty() || ::sched_getaffinity(0, sizeof saved, &saved) != 0) return;
+    cpu_set_t want;
+    CPU_ZERO(&want);
+    for (int c : cpus)
+      if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &saved)) CPU_SET(c, &want);  // within our own cgroup/cpuset
+    if (CPU_COUNT(&want) == 0) return;
+    active = ::sched_setaffinity(0, sizeof want, &want) == 0;
+  }
+  ~ScopedThreadAffinity() {
+    if (active) ::sched_setaffinity(0, sizeof saved, &saved);
+  }
+};
+
 pid_t spawn(const std::vector<std::string>& argv, const std::vector<std::string>& env, const std::string& cwd,
-            const std::string& log_path, std::string* err) {
+            const std::string& log_path, std::string* err, const std::vector<int>& cpus = {}) {
+  ScopedThreadAffinity pin(cpus);
   posix_spawn_file_actions_t fa;
   posix_spawnattr_t at;
   posix_spawn_file_actions_init(&fa);
@@ -667,6 +695,8 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     if (wants_gpu && !rt->gpus.devices.empty()) {
       const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1, rt->ip, rt->rdzv_port);
       for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
+      const auto local = alloc_->topology().local_cpus(rt->gpus.devices);
+      if (cfg_.numa_pinning && !local.empty()) set("KFAMD_CPU_AFFINITY", format_cpulist(local));
       // Node-level code-object cache shared by every GPU container (the device plugin's Allocate
       // response carries this env + mount). comgr caches the runtime's device-code builds under
       // $HOME/.cache/comgr by default, and every pod starts with an empty HOME: that miss cost
@@ -742,7 +772,13 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       std::ofstream lf(cr.log_path, std::ios::app);
       lf << "# kflite: starting " << cr.name << " (" << why << "): " << join(argv, " ") << "\n";
     }
-    pid_t pid = spawn(argv, envv, cwd, cr.log_path, &serr);
+    // topology-manager "single-numa-node"-style placement for GPU containers: the process tree
+    // runs on the CPUs local to its GPUs (host<->HBM copies, RCCL proxy threads, data loaders)
+    std::vector<int> cpus;
+    if (cfg_.numa_pinning && !rt->gpus.devices.empty() &&
+        resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0)
+      cpus = alloc_->topology().local_cpus(rt->gpus.devices);
+    pid_t pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
     if (pid < 0) {
       cr.state = "waiting";
       cr.reason = "CreateContainerError";

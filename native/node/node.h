@@ -78,6 +78,8 @@ struct KubeletConfig {
   int node_cpus = 0;         // advertised CPU capacity (0 = online host CPUs)
   int64_t node_memory_gib = 0;  // advertised memory (0 = host RAM)
   std::string recipes_file;  // optional JSON overriding the image recipes
+  std::string sysfs_root;    // "" = /sys (tests: a fake tree with class/kfd, bus/pci, devices/system/node)
+  bool numa_pinning = true;  // pin GPU pods' processes to their devices' NUMA-local CPUs
 };
 
 class Kubelet {

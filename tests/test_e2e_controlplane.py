@@ -352,7 +352,7 @@ def test_cold_start_phases_recorded_on_notebook_and_exported(c, cluster):
     ph = json.loads(nb["metadata"]["annotations"]["notebooks.kubeflow.org/cold-start-phases"])
     for k in ("observed_to_statefulset_ms", "statefulset_to_scheduled_ms", "scheduled_to_initialized_ms",
               "initialized_to_ready_ms", "total_ms"):
-        assert k in ph and ph[k] >= 0, ph
+        assert k in ph and 0 <= ph[k] < 30000, ph
     assert ph["total_ms"] >= ph["scheduled_to_initialized_ms"]
     with urllib.request.urlopen(cluster.url + "/metrics", timeout=5) as r:
         text = r.read().decode()
