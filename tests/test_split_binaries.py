@@ -12,6 +12,7 @@ import signal
 import socket
 import subprocess
 import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -93,8 +94,18 @@ def test_profile_notebook_poddefault_over_rest(split):
     assert {"name": "REMOTE", "value": "1"} in pod["spec"]["containers"][0]["env"]
     assert pod["spec"]["initContainers"][0]["name"] == "gpu-readiness"
     assert c.exists("route.openshift.io/v1", "Route", "nb", "remote")
-    with urllib.request.urlopen(cl.gateway + "/notebook/remote/nb/api/status", timeout=5) as r:
-        assert r.status == 200
+    # no readiness probe (as in the reference's spawner template): Ready can precede the server
+    # listening, so poll briefly through the gateway
+    deadline = time.time() + 15
+    while True:
+        try:
+            with urllib.request.urlopen(cl.gateway + "/notebook/remote/nb/api/status", timeout=5) as r:
+                assert r.status == 200
+                break
+        except urllib.error.HTTPError as e:
+            if e.code != 503 or time.time() > deadline:
+                raise
+            time.sleep(0.1)
 
 
 def test_pvcviewer_webhook_over_rest(split):
