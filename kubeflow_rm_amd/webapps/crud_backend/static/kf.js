@@ -1,8 +1,14 @@
 // kf.js — shared frontend runtime of the CRUD apps (the kubeflow-common-lib role, vanilla JS):
 // backend calls with the CSRF double-submit header, exponential-backoff poller (1 s -> 8 s, reset
 // when the data changes), namespace selection bound to the central dashboard's iframe protocol
-// (library.js: parent-connected / iframe-connected / namespace-selected / all-namespaces), status
-// icons and small DOM helpers.
+// (library.js: parent-connected / iframe-connected / namespace-selected / all-namespaces), and the
+// library's components: resource table (sortable, filterable, per-row actions, the same data-cy
+// hooks as kubeflow-common-lib's resource-table), status icons (lib-status-icon semantics),
+// conditions table, logs viewer, form validators (DNS-1123 names, CPU / memory quantities, limit
+// >= request), snack bar, details dialog with tabs, YAML view.
+//
+// Every component has a pure render function (string in, string out) so node can unit-test it
+// without a DOM; the DOM classes only bind those strings to elements and events.
 (function (global) {
   "use strict";
   function cookie(name) {
@@ -124,6 +130,172 @@
     await show(0);
     return dlg;
   }
+  // ---- status icon (lib-status-icon: ready check_circle, stopped custom:stoppedResource,
+  // unavailable timelapse, warning/error warning/error, waiting/terminating spinner) ------------
+  const STATUS_ICON = { ready: "check_circle", stopped: "custom:stoppedResource", unavailable: "timelapse",
+                        warning: "warning", error: "error", uninitialized: "remove_circle_outline" };
+  function statusIcon(st) {
+    st = st || {};
+    const phase = st.phase || "";
+    if (phase === "waiting" || phase === "terminating")
+      return `<span class="status-icon st-${esc(phase)}" title="${esc(st.message || "")}"><span class="spinner" data-icon="spinner"></span></span>`;
+    const icon = STATUS_ICON[phase] || "help";
+    return `<span class="status-icon st-${esc(phase)}" title="${esc(st.message || "")}"><span class="icon" data-icon="${esc(icon)}">${icons[phase] || "?"}</span></span>`;
+  }
+
+  // ---- resource table -----------------------------------------------------------------------
+  // cfg.columns: [{title, value(row) -> text (sort/filter key), html(row) -> cell html (default:
+  // escaped value), sortable (default true)}]; cfg.actions: [{name, label, enabled(row)}]
+  // state: {sortCol, sortDir: 1|-1, filter}. Default order: the "Name" column ascending (the
+  // reference tables' default sort).
+  function colValue(c, row) { return c.value ? c.value(row) : row[c.field || c.title.toLowerCase()]; }
+  function sortedRows(cfg, rows, state) {
+    state = state || {};
+    const cols = cfg.columns;
+    let idx = state.sortCol;
+    if (idx === undefined || idx === null) idx = cols.findIndex((c) => c.title === "Name");
+    const dir = state.sortDir || 1;
+    let out = rows.slice();
+    const f = (state.filter || "").trim().toLowerCase();
+    if (f) out = out.filter((r) => cols.some((c) => String(colValue(c, r) == null ? "" : colValue(c, r)).toLowerCase().includes(f)));
+    if (idx >= 0 && cols[idx] && cols[idx].sortable !== false) {
+      const c = cols[idx];
+      out.sort((a, b) => {
+        const x = colValue(c, a), y = colValue(c, b);
+        const nx = typeof x === "number" ? x : NaN, ny = typeof y === "number" ? y : NaN;
+        const r = !isNaN(nx) && !isNaN(ny) ? nx - ny : String(x == null ? "" : x).localeCompare(String(y == null ? "" : y));
+        return r * dir;
+      });
+    }
+    return out;
+  }
+  function renderTable(cfg, rows, state) {
+    state = state || {};
+    const view = sortedRows(cfg, rows, state);
+    const sortIdx = state.sortCol === undefined || state.sortCol === null ? cfg.columns.findIndex((c) => c.title === "Name") : state.sortCol;
+    const head = cfg.columns.map((c, i) => {
+      const arrow = i === sortIdx ? ((state.sortDir || 1) > 0 ? " &#9650;" : " &#9660;") : "";
+      return `<th data-cy-table-header-row="${esc(c.title)}" data-col="${i}"${c.sortable === false ? "" : ' class="sortable"'}>${esc(c.title)}${arrow}</th>`;
+    }).join("") + (cfg.actions && cfg.actions.length ? "<th></th>" : "");
+    const body = view.map((r) => {
+      const key = esc(cfg.key ? cfg.key(r) : (r.namespace ? r.namespace + "/" : "") + r.name);
+      const cells = cfg.columns.map((c) => `<td data-cy-resource-table-row="${esc(c.title)}">${c.html ? c.html(r) : esc(colValue(c, r))}</td>`).join("");
+      const acts = (cfg.actions || []).map((a) => {
+        const on = a.enabled ? a.enabled(r) : true;
+        return `<button data-action="${esc(a.name)}" data-key="${key}"${on ? "" : " disabled"}>${esc(typeof a.label === "function" ? a.label(r) : a.label)}</button>`;
+      }).join("");
+      return `<tr data-key="${key}">${cells}${cfg.actions && cfg.actions.length ? `<td class="actions">${acts}</td>` : ""}</tr>`;
+    }).join("");
+    const empty = view.length ? "" : `<tr><td colspan="${cfg.columns.length + 1}" class="muted">${esc(cfg.empty || "No resources.")}</td></tr>`;
+    return `<table class="rt"><thead><tr>${head}</tr></thead><tbody>${body}${empty}</tbody></table>`;
+  }
+  // DOM binding: header click sorts (again: reverse), filter box, action buttons -> cfg.onAction
+  class ResourceTable {
+    constructor(el, cfg) {
+      this.el = el; this.cfg = cfg; this.rows = []; this.state = { sortCol: null, sortDir: 1, filter: "" };
+      el.addEventListener("click", (ev) => {
+        const th = ev.target.closest("th[data-col]");
+        if (th) {
+          const i = Number(th.dataset.col);
+          if (this.cfg.columns[i].sortable === false) return;
+          const cur = this.state.sortCol === null ? this.cfg.columns.findIndex((c) => c.title === "Name") : this.state.sortCol;
+          this.state.sortDir = cur === i ? -this.state.sortDir : 1;
+          this.state.sortCol = i;
+          this.render();
+          return;
+        }
+        const b = ev.target.closest("button[data-action]");
+        if (b && this.cfg.onAction) {
+          const row = this.rows.find((r) => (this.cfg.key ? this.cfg.key(r) : (r.namespace ? r.namespace + "/" : "") + r.name) === b.dataset.key);
+          if (row) this.cfg.onAction(b.dataset.action, row);
+        }
+        const a = ev.target.closest("a[data-open]");
+        if (a && this.cfg.onOpen) {
+          const row = this.rows.find((r) => (this.cfg.key ? this.cfg.key(r) : (r.namespace ? r.namespace + "/" : "") + r.name) === a.dataset.open);
+          if (row) this.cfg.onOpen(row);
+        }
+      });
+    }
+    setFilter(f) { this.state.filter = f; this.render(); }
+    setRows(rows) { this.rows = rows || []; this.render(); }
+    render() { this.el.innerHTML = renderTable(this.cfg, this.rows, this.state); }
+  }
+  // the Name cell of a resource table: a link that opens the details page
+  function nameLink(row) {
+    return `<a class="name" data-open="${esc((row.namespace ? row.namespace + "/" : "") + row.name)}">${esc(row.name)}</a>`;
+  }
+
+  // ---- conditions table (common-lib conditions-table) -----------------------------------------
+  function conditionsTable(conds) {
+    if (!conds || !conds.length) return '<p class="muted">No conditions.</p>';
+    const rows = conds.map((c) => {
+      const ok = c.status === "True";
+      return `<tr><td>${statusIcon({ phase: ok ? "ready" : "warning", message: c.status })}</td><td>${esc(c.type)}</td>` +
+        `<td>${esc(c.lastTransitionTime || c.lastProbeTime || "")}</td><td>${esc(c.reason || "")}</td><td>${esc(c.message || "")}</td></tr>`;
+    });
+    return `<table class="kv conditions"><thead><tr><th>Status</th><th>Type</th><th>Last Transition Time</th><th>Reason</th><th>Message</th></tr></thead><tbody>${rows.join("")}</tbody></table>`;
+  }
+
+  // ---- logs viewer (common-lib logs-viewer) -----------------------------------------------------
+  function renderLogs(lines, filter) {
+    const f = (filter || "").toLowerCase();
+    const shown = [];
+    (lines || []).forEach((l, i) => { if (!f || String(l).toLowerCase().includes(f)) shown.push([i + 1, l]); });
+    if (!shown.length) return '<p class="muted">No logs.</p>';
+    return `<pre class="logs">${shown.map(([n, l]) => `<span class="ln">${n}</span> ${esc(l)}`).join("\n")}</pre>`;
+  }
+  // polls fetchLines() while following; the filter box narrows the view
+  class LogsViewer {
+    constructor(el, fetchLines, periodMs) { this.el = el; this.fetch = fetchLines; this.period = periodMs || 3000; this.lines = []; this.filter = ""; this.t = null; }
+    async refresh() {
+      try { this.lines = await this.fetch(); } catch (e) { this.el.innerHTML = `<p class="err">${esc(e.message)}</p>`; return; }
+      this.el.innerHTML = renderLogs(this.lines, this.filter);
+      const pre = this.el.querySelector("pre");
+      if (pre) pre.scrollTop = pre.scrollHeight;
+    }
+    follow() { this.stop(); const tick = async () => { await this.refresh(); this.t = setTimeout(tick, this.period); }; tick(); return this; }
+    stop() { if (this.t) clearTimeout(this.t); this.t = null; }
+  }
+
+  // ---- form validators (common-lib form/validators) -------------------------------------------
+  const DNS1123 = /^[a-z0-9]([-a-z0-9]*[a-z0-9])?$/;
+  const QTY = /^([0-9]+(\.[0-9]+)?|\.[0-9]+)(m|k|M|G|T|P|E|Ki|Mi|Gi|Ti|Pi|Ei)?$/;
+  const SUFFIX = { m: 1e-3, k: 1e3, M: 1e6, G: 1e9, T: 1e12, P: 1e15, E: 1e18,
+                   Ki: 1024, Mi: 1024 ** 2, Gi: 1024 ** 3, Ti: 1024 ** 4, Pi: 1024 ** 5, Ei: 1024 ** 6 };
+  function parseQuantity(q) {
+    const s = String(q == null ? "" : q).trim();
+    const m = s.match(QTY);
+    if (!m) return NaN;
+    return parseFloat(m[1]) * (m[3] ? SUFFIX[m[3]] : 1);
+  }
+  const validators = {
+    name(v, maxLen) {
+      const s = String(v || "");
+      if (!s) return "Name is required";
+      if (s.length > (maxLen || 63)) return `Name must be at most ${maxLen || 63} characters`;
+      if (!DNS1123.test(s)) return "Name must consist of lowercase alphanumeric characters or '-', and must start and end with an alphanumeric character";
+      return "";
+    },
+    cpu(v) { return isNaN(parseQuantity(v)) || parseQuantity(v) <= 0 ? `Invalid CPU value: ${v}` : ""; },
+    memory(v) { return isNaN(parseQuantity(v)) || parseQuantity(v) <= 0 ? `Invalid memory value: ${v}` : ""; },
+    limitAtLeastRequest(request, limit, what) {
+      if (limit === "" || limit == null) return "";
+      return parseQuantity(limit) < parseQuantity(request) ? `${what} limit must be greater than or equal to the request` : "";
+    },
+  };
+
+  // ---- snack bar ------------------------------------------------------------------------------
+  function snack(message, status) {
+    let el = document.getElementById("kf-snack");
+    if (!el) { el = document.createElement("div"); el.id = "kf-snack"; document.body.append(el); }
+    el.className = "snack";
+    el.setAttribute("data-cy-snack-status", status || "INFO");
+    el.textContent = message;
+    el.hidden = false;
+    clearTimeout(el._t);
+    el._t = setTimeout(() => { el.hidden = true; }, status === "ERROR" ? 8000 : 3000);
+  }
+
   function h(tag, attrs, ...children) {
     const e = document.createElement(tag);
     Object.entries(attrs || {}).forEach(([k, v]) => (k.startsWith("on") ? e.addEventListener(k.slice(2), v) : e.setAttribute(k, v)));
@@ -131,6 +303,7 @@
     return e;
   }
   global.kf = { call, Poller, cookie, setNamespace, onNamespace, namespace: () => currentNs, statusCell, h,
-                esc, toYaml, eventsTable, kvTable, details };
+                esc, toYaml, eventsTable, kvTable, details, statusIcon, renderTable, sortedRows, ResourceTable, nameLink,
+                conditionsTable, renderLogs, LogsViewer, validators, parseQuantity, snack };
   if (typeof module !== "undefined" && module.exports) module.exports = global.kf;  // node unit tests
 })(typeof window !== "undefined" ? window : globalThis);

@@ -1,182 +1,366 @@
-// Jupyter web app frontend: notebook table (polled with backoff), connect / start / stop / delete,
-// notebook details (overview / events / logs / YAML), and the spawner dialog built from /api/config
-// (MI355X GPU counts from the amd.com/gpu vendor, workspace + data volumes new or existing,
-// affinity / toleration groups, PodDefault configurations, shared memory).
-(function () {
+// Jupyter web app frontend (reference crud-web-apps/jupyter/frontend): the notebook table (common
+// resource table, polled with backoff; "All namespaces" adds a Namespace column), connect / start /
+// stop / delete, notebook details (overview + conditions / events / logs viewer / YAML), and the
+// spawner built from /api/config: image groups, CPU and memory requests with their limits
+// (form-cpu-ram: the admin's limitFactor pre-fills the limit until the user edits it), MI355X GPU
+// counts on the amd.com/gpu vendor, workspace volume (name from the {notebook-name} template, size,
+// access mode), data volumes (mount follows the volume name until edited), affinity / toleration
+// groups, PodDefault configurations, shared memory.
+//
+// The `JWA` object holds the pure parts (form defaults, limits, volume naming, request body,
+// validation, table columns): node unit-tests them against the reference's Cypress fixtures.
+(function (global) {
   "use strict";
-  const $ = (id) => document.getElementById(id);
-  let config = null, poller = null;
+  const kf = global.kf || (typeof require !== "undefined" ? require("../../../crud_backend/static/kf.js") : null);
+  const ALL = "*all-namespaces*";
+  const HOME = "/home/jovyan";
 
-  async function loadNamespaces() {
-    let namespaces = [];
-    try { namespaces = (await kf.call("GET", "/api/namespaces")).namespaces; }
-    catch (e) { namespaces = kf.namespace() ? [kf.namespace()] : []; }  // not cluster-wide: dashboard drives it
-    const sel = $("ns");
-    sel.innerHTML = namespaces.map((n) => `<option>${n}</option>`).join("");
-    if (!kf.namespace() && namespaces.length) kf.setNamespace(namespaces[0]);
-    sel.value = kf.namespace();
-    sel.onchange = () => kf.setNamespace(sel.value);
-  }
+  // ---- pure helpers ---------------------------------------------------------------------------
+  const JWA = {
+    ALL,
+    columns(allNamespaces) {
+      const e = kf.esc;
+      const cols = [
+        { title: "Status", value: (r) => r.status.phase, html: (r) => kf.statusIcon(r.status) },
+        { title: "Name", value: (r) => r.name, html: (r) => kf.nameLink(r) },
+      ];
+      if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
+      cols.push(
+        { title: "Type", value: (r) => r.serverType },
+        { title: "Age", value: (r) => r.age },
+        { title: "Image", value: (r) => r.shortImage, html: (r) => `<span title="${e(r.image)}">${e(r.shortImage)}</span>` },
+        { title: "GPUs", value: (r) => (r.gpus || {}).count || 0, html: (r) => `<span title="${e((r.gpus || {}).message || "")}">${e((r.gpus || {}).count || 0)}</span>` },
+        { title: "CPUs", value: (r) => r.cpu },
+        { title: "Memory", value: (r) => r.memory },
+        { title: "Volumes", value: (r) => (r.volumes || []).join(", "), sortable: false },
+      );
+      return cols;
+    },
+    // "{notebook-name}-workspace" -> "<name>-workspace" ("-workspace" while the name is empty)
+    volumeName(template, notebookName) { return String(template || "").split("{notebook-name}").join(notebookName || ""); },
+    // "20Gi" -> {size: "20", unit: "Gi"}
+    splitSize(q) {
+      const m = String(q || "").match(/^([0-9.]+)\s*([A-Za-z]*)$/);
+      return m ? { size: m[1], unit: m[2] || "Gi" } : { size: "", unit: "Gi" };
+    },
+    mountFor(volumeName) { return `${HOME}/${volumeName}`; },
+    // limit = request x factor, one decimal (form.py _limit); "" when the admin set no factor
+    limitFrom(request, factor, unit) {
+      if (!factor || factor === "none" || request === "" || request == null) return "";
+      const v = parseFloat(String(request).replace(unit || "", ""));
+      if (isNaN(v)) return "";
+      return `${Math.round(v * parseFloat(factor) * 10) / 10}${unit || ""}`;
+    },
+    formDefaults(config, notebookName) {
+      const c = config || {};
+      const ws = ((c.workspaceVolume || {}).value) || {};
+      const pvc = ws.newPvc || {};
+      const size = JWA.splitSize((((pvc.spec || {}).resources || {}).requests || {}).storage);
+      const gpu = ((c.gpus || {}).value) || {};
+      const cpu = String(((c.cpu || {}).value) || "0.5"), mem = String(((c.memory || {}).value) || "1.0Gi");
+      return {
+        name: notebookName || "", serverType: "jupyter",
+        image: ((c.image || {}).value) || "", imageGroupOne: ((c.imageGroupOne || {}).value) || "",
+        imageGroupTwo: ((c.imageGroupTwo || {}).value) || "", customImage: "",
+        imagePullPolicy: ((c.imagePullPolicy || {}).value) || "IfNotPresent",
+        cpu, cpuLimit: JWA.limitFrom(cpu, (c.cpu || {}).limitFactor, ""),
+        memory: mem, memoryLimit: JWA.limitFrom(mem, (c.memory || {}).limitFactor, "Gi"),
+        gpus: { num: gpu.num || "none", vendor: gpu.vendor || ((gpu.vendors || [])[0] || {}).limitsKey || "" },
+        shm: !!((c.shm || {}).value),
+        workspace: ws.newPvc || ws.existingSource ? {
+          enabled: true, type: ws.existingSource ? "existing" : "new", template: (pvc.metadata || {}).name || "{notebook-name}-workspace",
+          name: JWA.volumeName((pvc.metadata || {}).name || "{notebook-name}-workspace", notebookName),
+          size: size.size, unit: size.unit, accessMode: ((pvc.spec || {}).accessModes || ["ReadWriteOnce"])[0],
+          mount: ws.mount || HOME, existing: ((ws.existingSource || {}).persistentVolumeClaim || {}).claimName || "",
+        } : { enabled: false },
+        datavols: [],
+        affinityConfig: ((c.affinityConfig || {}).value) || "none",
+        tolerationGroup: ((c.tolerationGroup || {}).value) || "none",
+        configurations: (((c.configurations || {}).value) || []).slice(),
+      };
+    },
+    // a new data volume row; its mount tracks the name until the user types in the mount field
+    newDataVolume(notebookName, index) {
+      const name = `${notebookName || ""}-datavol-${index}`;
+      return { type: "new", name, size: "5", unit: "Gi", accessMode: "ReadWriteOnce", mount: JWA.mountFor(name), mountDirty: false, existing: "" };
+    },
+    renameDataVolume(vol, name) {
+      const out = Object.assign({}, vol, { name });
+      if (!vol.mountDirty) out.mount = JWA.mountFor(name);
+      return out;
+    },
+    editMount(vol, mount) { return Object.assign({}, vol, { mount, mountDirty: true }); },
+    validate(f) {
+      const errs = [];
+      const n = kf.validators.name(f.name, 52);  // StatefulSet pod names: <name>-0 within 63
+      if (n) errs.push(n);
+      for (const [what, v, lim, check] of [["CPU", f.cpu, f.cpuLimit, kf.validators.cpu], ["Memory", f.memory, f.memoryLimit, kf.validators.memory]]) {
+        const e1 = check(v);
+        if (e1) errs.push(e1);
+        if (lim) {
+          const e2 = check(lim) || kf.validators.limitAtLeastRequest(v, lim, what);
+          if (e2) errs.push(e2);
+        }
+      }
+      (f.datavols || []).forEach((d) => {
+        if (d.type === "new" && kf.validators.name(d.name)) errs.push(`Data volume: ${kf.validators.name(d.name)}`);
+        if (!String(d.mount || "").startsWith("/")) errs.push(`Data volume mount must be an absolute path: ${d.mount}`);
+      });
+      return errs;
+    },
+    // POST /api/namespaces/<ns>/notebooks body (backend form.py contract)
+    buildBody(f, config, namespace) {
+      const image = f.serverType === "group-one" ? f.imageGroupOne : f.serverType === "group-two" ? f.imageGroupTwo : f.image;
+      const vol = (v) => (v.type === "existing"
+        ? { mount: v.mount, existingSource: { persistentVolumeClaim: { claimName: v.existing } } }
+        : { mount: v.mount, newPvc: { metadata: { name: v.template || v.name },
+                                      spec: { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] } } });
+      const body = {
+        name: f.name, namespace, serverType: f.serverType,
+        image: f.customImage ? f.customImage.trim() : image, customImage: !!f.customImage,
+        imagePullPolicy: f.imagePullPolicy, cpu: String(f.cpu), memory: String(f.memory),
+        gpus: f.gpus.num === "none" ? { num: "none" } : { num: String(f.gpus.num), vendor: f.gpus.vendor },
+        tolerationGroup: f.tolerationGroup || "none", affinityConfig: f.affinityConfig || "none",
+        shm: !!f.shm, configurations: (f.configurations || []).slice(), datavols: (f.datavols || []).map(vol),
+      };
+      if (f.cpuLimit) body.cpuLimit = String(f.cpuLimit);
+      if (f.memoryLimit) body.memoryLimit = String(f.memoryLimit);
+      if (f.workspace && f.workspace.enabled) body.workspace = vol(f.workspace);
+      // fields the admin pinned readOnly must not be sent (form.py get_form_value -> 400)
+      const ro = { cpu: "cpu", memory: "memory", gpus: "gpus", shm: "shm", imagePullPolicy: "imagePullPolicy",
+                   tolerationGroup: "tolerationGroup", affinityConfig: "affinityConfig", configurations: "configurations",
+                   workspace: "workspaceVolume", datavols: "dataVolumes" };
+      Object.keys(ro).forEach((k) => { if (((config || {})[ro[k]] || {}).readOnly) delete body[k]; });
+      if (((config || {}).cpu || {}).readOnly) delete body.cpuLimit;
+      if (((config || {}).memory || {}).readOnly) delete body.memoryLimit;
+      return body;
+    },
+    // the union of several namespaces' notebook lists (all-namespaces view)
+    merge(lists) { return [].concat(...lists); },
+  };
 
-  function row(nb, ns) {
-    const tr = kf.h("tr", {});
-    const stopped = nb.status.phase === "stopped";
-    const e = kf.esc;
-    tr.innerHTML = `<td>${kf.statusCell(nb.status)}</td><td><a class="name">${e(nb.name)}</a></td><td>${e(nb.serverType)}</td><td>${e(nb.age)}</td>
-      <td title="${e(nb.image)}">${e(nb.shortImage)}</td><td>${e(nb.gpus.count || 0)}</td><td>${e(nb.cpu)}</td><td>${e(nb.memory)}</td>
-      <td>${e((nb.volumes || []).join(", "))}</td>`;
-    tr.querySelector("a.name").addEventListener("click", () => showDetails(ns, nb.name));
-    const td = kf.h("td", {});
-    const connect = kf.h("button", { onclick: () => window.open(`/notebook/${ns}/${nb.name}/`) }, "Connect");
-    if (nb.status.phase !== "ready") connect.disabled = true;
-    td.append(connect,
-      kf.h("button", { onclick: () => act("PATCH", ns, nb.name, { stopped: !stopped }) }, stopped ? "Start" : "Stop"),
-      kf.h("button", { onclick: () => confirm(`Delete notebook ${nb.name}?`) && act("DELETE", ns, nb.name) }, "Delete"));
-    tr.append(td);
-    return tr;
-  }
+  // ---- DOM ------------------------------------------------------------------------------------
+  function app() {
+    const $ = (id) => document.getElementById(id);
+    let config = null, poller = null, table = null, namespaces = [], form = null;
 
-  async function refresh() {
-    const ns = kf.namespace();
-    if (!ns) return null;
-    const { notebooks } = await kf.call("GET", `/api/namespaces/${ns}/notebooks`);
-    const body = $("notebooks").querySelector("tbody");
-    body.replaceChildren(...notebooks.map((nb) => row(nb, ns)));
-    return notebooks.map((nb) => [nb.name, nb.status.phase]);
-  }
-
-  // notebook page: overview / events / logs / YAML (JWA frontend pages/notebook-page)
-  function showDetails(ns, name) {
-    const base = `/api/namespaces/${ns}/notebooks/${name}`;
-    const e = kf.esc;
-    return kf.details(`Notebook ${ns}/${name}`, [
-      { name: "Overview", render: async () => {
-        const nb = (await kf.call("GET", base)).notebook;
-        const spec = ((nb.spec || {}).template || {}).spec || {};
-        const c = (spec.containers || [])[0] || {};
-        const lim = (c.resources || {}).limits || {}, req = (c.resources || {}).requests || {};
-        const ann = (nb.metadata || {}).annotations || {};
-        const st = nb.status || {};
-        return kf.kvTable([
-          ["Name", nb.metadata.name], ["Namespace", nb.metadata.namespace],
-          ["Created", nb.metadata.creationTimestamp], ["Image", c.image],
-          ["Server type", ann["notebooks.kubeflow.org/server-type"] || "jupyter"],
-          ["CPU (request / limit)", `${req.cpu || "-"} / ${lim.cpu || "-"}`],
-          ["Memory (request / limit)", `${req.memory || "-"} / ${lim.memory || "-"}`],
-          ["MI355X GPUs", lim["amd.com/gpu"] || "0"], ["Allocated GPU ids", st.gpus || "-"],
-          ["Volumes", (spec.volumes || []).map((v) => v.name).join(", ")],
-          ["Ready replicas", st.readyReplicas || 0],
-          ["Last activity", ann["notebooks.kubeflow.org/last-activity"] || "-"],
-          ["Stopped", ann["kubeflow-resource-stopped"] || "no"],
-        ]) + (st.gpuReadiness ? `<h3>GPU readiness op</h3><pre class="yaml">${e(kf.toYaml(st.gpuReadiness))}</pre>` : "") +
-          `<h3>Conditions</h3>${kf.kvTable((st.conditions || []).map((x) => [x.type, `${x.status} ${x.reason || ""} ${x.message || ""}`]))}`;
-      } },
-      { name: "Events", render: async () => kf.eventsTable((await kf.call("GET", `${base}/events`)).events) },
-      { name: "Logs", render: async () => {
-        const pod = (await kf.call("GET", `${base}/pod`)).pod;
-        const logs = (await kf.call("GET", `${base}/pod/${pod.metadata.name}/logs`)).logs;
-        return `<p class="muted">Pod ${e(pod.metadata.name)}</p><pre class="logs">${e(logs.join("\n"))}</pre>`;
-      } },
-      { name: "YAML", render: async () => `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).notebook))}</pre>` },
-    ]);
-  }
-
-  // data volumes: rows of {type new|existing, name, size, mode, mount}
-  function addDataVolume(existing) {
-    const rowEl = document.createElement("div");
-    rowEl.className = "datavol";
-    const pvcs = existing || [];
-    rowEl.innerHTML = `<select class="dv-type"><option value="new">new</option><option value="existing">existing</option></select>
-      <input class="dv-name" placeholder="{notebook-name}-data" size="16">
-      <select class="dv-existing" hidden>${pvcs.map((p) => `<option>${kf.esc(p.name)}</option>`).join("")}</select>
-      <input class="dv-size" value="10Gi" size="5"><select class="dv-mode"><option>ReadWriteOnce</option><option>ReadWriteMany</option><option>ReadOnlyMany</option></select>
-      <input class="dv-mount" placeholder="/home/jovyan/data" size="18"><button type="button" class="dv-rm">&times;</button>`;
-    rowEl.querySelector(".dv-type").onchange = (ev) => {
-      const ex = ev.target.value === "existing";
-      rowEl.querySelector(".dv-existing").hidden = !ex;
-      ["dv-name", "dv-size", "dv-mode"].forEach((c) => { rowEl.querySelector("." + c).hidden = ex; });
-    };
-    rowEl.querySelector(".dv-rm").onclick = () => rowEl.remove();
-    $("f-datavols").append(rowEl);
-  }
-
-  function dataVolumes() {
-    return [...$("f-datavols").querySelectorAll(".datavol")].map((r) => {
-      const q = (c) => r.querySelector("." + c).value.trim();
-      const mount = q("dv-mount") || "/home/jovyan/data";
-      if (q("dv-type") === "existing") return { mount, existingSource: { persistentVolumeClaim: { claimName: q("dv-existing") } } };
-      return { mount, newPvc: { metadata: { name: q("dv-name") || "{notebook-name}-data" },
-                                spec: { resources: { requests: { storage: q("dv-size") } }, accessModes: [q("dv-mode")] } } };
-    });
-  }
-
-  async function act(method, ns, name, body) {
-    try { await kf.call(method, `/api/namespaces/${ns}/notebooks/${name}`, body); $("error").textContent = ""; }
-    catch (e) { $("error").textContent = e.message; }
-    poller.reset();
-  }
-
-  function fillSpawner() {
-    const imgs = config.image.options || [];
-    $("f-image").innerHTML = imgs.map((i) => `<option ${i === config.image.value ? "selected" : ""}>${i}</option>`).join("");
-    $("f-cpu").value = config.cpu.value; $("f-mem").value = config.memory.value;
-    const gpu = config.gpus.value;
-    const counts = gpu.options || ["none", "1", "2", "4", "8"];
-    $("f-gpus").innerHTML = counts.map((c) => `<option ${c === gpu.num ? "selected" : ""}>${c}</option>`).join("");
-    $("f-shm").checked = !!config.shm.value;
-    const opts = (key) => ['<option value="none">None</option>'].concat(((config[key] || {}).options || [])
-      .map((o) => `<option value="${kf.esc(o.configKey)}" ${o.configKey === (config[key] || {}).value ? "selected" : ""}>${kf.esc(o.displayName || o.configKey)}</option>`)).join("");
-    $("f-affinity").innerHTML = opts("affinityConfig");
-    $("f-toleration").innerHTML = opts("tolerationGroup");
-  }
-
-  async function openSpawner() {
-    const ns = kf.namespace();
-    const { poddefaults } = await kf.call("GET", `/api/namespaces/${ns}/poddefaults`);
-    $("f-configs").innerHTML = poddefaults.map((pd) =>
-      `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("") || '<span class="muted">none</span>';
-    let pvcs = [];
-    try { pvcs = (await kf.call("GET", `/api/namespaces/${ns}/pvcs`)).pvcs; } catch (e) { /* optional */ }
-    $("f-datavols").replaceChildren();
-    $("f-add-vol").onclick = () => addDataVolume(pvcs);
-    $("f-error").textContent = "";
-    $("spawner").showModal();
-  }
-
-  async function submit(ev) {
-    if (ev.submitter && ev.submitter.value !== "ok") return;
-    ev.preventDefault();
-    const ns = kf.namespace(), name = $("f-name").value;
-    const gpus = $("f-gpus").value;
-    const custom = $("f-custom").value.trim();
-    const body = {
-      name, namespace: ns, serverType: $("f-type").value,
-      image: custom || $("f-image").value, customImage: !!custom, imagePullPolicy: config.imagePullPolicy.value,
-      cpu: $("f-cpu").value, memory: $("f-mem").value,
-      gpus: gpus === "none" ? { num: "none" } : { num: gpus, vendor: config.gpus.value.vendor },
-      tolerationGroup: $("f-toleration").value || "none", affinityConfig: $("f-affinity").value || "none",
-      shm: $("f-shm").checked,
-      configurations: [...$("f-configs").querySelectorAll("input:checked")].map((i) => i.value),
-      datavols: dataVolumes(),
-    };
-    if ($("f-ws").checked) {
-      body.workspace = JSON.parse(JSON.stringify(config.workspaceVolume.value));
+    async function loadNamespaces() {
+      try { namespaces = (await kf.call("GET", "/api/namespaces")).namespaces; }
+      catch (e) { namespaces = kf.namespace() ? [kf.namespace()] : []; }  // not cluster-wide: the dashboard drives it
+      const sel = $("ns");
+      sel.innerHTML = namespaces.map((n) => `<option value="${kf.esc(n)}">${kf.esc(n)}</option>`).join("") +
+        (namespaces.length > 1 ? `<option value="${ALL}">All namespaces</option>` : "");
+      if (!kf.namespace() && namespaces.length) kf.setNamespace(namespaces[0]);
+      sel.value = kf.namespace();
+      sel.onchange = () => { if (sel.value === ALL) { setAll(true); } else { setAll(false); kf.setNamespace(sel.value); } };
     }
-    try { await kf.call("POST", `/api/namespaces/${ns}/notebooks`, body); $("spawner").close(); poller.reset(); }
-    catch (e) { $("f-error").textContent = e.message; }
+    let allNs = false;
+    function setAll(v) {
+      allNs = v;
+      table = new kf.ResourceTable($("notebooks"), tableConfig());
+      poller.reset();
+    }
+    function tableConfig() {
+      return {
+        columns: JWA.columns(allNs), empty: "No notebooks in this namespace.",
+        actions: [
+          { name: "connect", label: "Connect", enabled: (r) => r.status.phase === "ready" },
+          { name: "toggle", label: (r) => (r.status.phase === "stopped" ? "Start" : "Stop") },
+          { name: "delete", label: "Delete" },
+        ],
+        onOpen: (r) => showDetails(r.namespace, r.name),
+        onAction: (name, r) => {
+          if (name === "connect") window.open(`/notebook/${r.namespace}/${r.name}/`);
+          if (name === "toggle") act("PATCH", r.namespace, r.name, { stopped: r.status.phase !== "stopped" });
+          if (name === "delete" && confirm(`Delete notebook ${r.name}?`)) act("DELETE", r.namespace, r.name);
+        },
+      };
+    }
+
+    async function refresh() {
+      const list = allNs ? namespaces : [kf.namespace()].filter(Boolean);
+      if (!list.length) return null;
+      const rows = JWA.merge(await Promise.all(list.map(async (ns) =>
+        (await kf.call("GET", `/api/namespaces/${ns}/notebooks`)).notebooks.map((r) => Object.assign({ namespace: ns }, r)))));
+      table.setRows(rows);
+      return rows.map((r) => [r.namespace, r.name, r.status.phase]);
+    }
+
+    // notebook page: overview + conditions / events / logs / YAML (JWA pages/notebook-page)
+    function showDetails(ns, name) {
+      const base = `/api/namespaces/${ns}/notebooks/${name}`;
+      const e = kf.esc;
+      let logs = null;
+      return kf.details(`Notebook ${ns}/${name}`, [
+        { name: "Overview", render: async () => {
+          if (logs) logs.stop();
+          const nb = (await kf.call("GET", base)).notebook;
+          const spec = ((nb.spec || {}).template || {}).spec || {};
+          const c = (spec.containers || [])[0] || {};
+          const lim = (c.resources || {}).limits || {}, req = (c.resources || {}).requests || {};
+          const ann = (nb.metadata || {}).annotations || {};
+          const st = nb.status || {};
+          return kf.kvTable([
+            ["Name", nb.metadata.name], ["Namespace", nb.metadata.namespace],
+            ["Created", nb.metadata.creationTimestamp], ["Image", c.image],
+            ["Server type", ann["notebooks.kubeflow.org/server-type"] || "jupyter"],
+            ["CPU (request / limit)", `${req.cpu || "-"} / ${lim.cpu || "-"}`],
+            ["Memory (request / limit)", `${req.memory || "-"} / ${lim.memory || "-"}`],
+            ["MI355X GPUs", lim["amd.com/gpu"] || "0"], ["Allocated GPU ids", st.gpus || "-"],
+            ["Volumes", (spec.volumes || []).map((v) => v.name).join(", ")],
+            ["Ready replicas", st.readyReplicas || 0],
+            ["Last activity", ann["notebooks.kubeflow.org/last-activity"] || "-"],
+            ["Cold start (ms)", ann["notebooks.kubeflow.org/cold-start-phases"] || "-"],
+            ["Stopped", ann["kubeflow-resource-stopped"] || "no"],
+          ]) + (st.gpuReadiness ? `<h3>GPU readiness op</h3><pre class="yaml">${e(kf.toYaml(st.gpuReadiness))}</pre>` : "") +
+            `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
+        } },
+        { name: "Events", render: async () => { if (logs) logs.stop(); return kf.eventsTable((await kf.call("GET", `${base}/events`)).events); } },
+        { name: "Logs", render: async () => {
+          const pod = (await kf.call("GET", `${base}/pod`)).pod;
+          setTimeout(() => {
+            const el = document.querySelector("#kf-details .tab-body .logs-host");
+            if (!el) return;
+            logs = new kf.LogsViewer(el, async () => (await kf.call("GET", `${base}/pod/${pod.metadata.name}/logs`)).logs).follow();
+          }, 0);
+          return `<p class="muted">Pod ${e(pod.metadata.name)} (following)</p><div class="logs-host"></div>`;
+        } },
+        { name: "YAML", render: async () => { if (logs) logs.stop(); return `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).notebook))}</pre>`; } },
+      ]);
+    }
+
+    async function act(method, ns, name, body) {
+      try { await kf.call(method, `/api/namespaces/${ns}/notebooks/${name}`, body); }
+      catch (e) { kf.snack(e.message, "ERROR"); }
+      poller.reset();
+    }
+
+    // ---- spawner ----
+    function renderDataVolumes() {
+      const host = $("f-datavols");
+      host.innerHTML = form.datavols.map((d, i) => `<div class="datavol${i === form.datavols.length - 1 ? " last" : ""}" data-cy="data volumes" data-i="${i}">
+        <select class="dv-type"><option value="new"${d.type === "new" ? " selected" : ""}>new</option><option value="existing"${d.type === "existing" ? " selected" : ""}>existing</option></select>
+        <input class="dv-name" data-cy="volume name input" value="${kf.esc(d.name)}" size="16"${d.type === "existing" ? " hidden" : ""}>
+        <select class="dv-existing"${d.type === "existing" ? "" : " hidden"}>${(form.pvcs || []).map((p) => `<option${p.name === d.existing ? " selected" : ""}>${kf.esc(p.name)}</option>`).join("")}</select>
+        <input class="dv-size" value="${kf.esc(d.size)}" size="4"${d.type === "existing" ? " hidden" : ""}><span class="muted"${d.type === "existing" ? " hidden" : ""}>Gi</span>
+        <select class="dv-mode"${d.type === "existing" ? " hidden" : ""}>${["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map((m) => `<option${m === d.accessMode ? " selected" : ""}>${m}</option>`).join("")}</select>
+        <input class="dv-mount" data-cy="mount path" value="${kf.esc(d.mount)}" size="20"><button type="button" class="dv-rm">&times;</button></div>`).join("");
+      host.querySelectorAll(".datavol").forEach((row) => {
+        const i = Number(row.dataset.i);
+        row.querySelector(".dv-type").onchange = (ev) => { form.datavols[i].type = ev.target.value; if (ev.target.value === "existing" && form.pvcs && form.pvcs[0]) form.datavols[i].existing = form.pvcs[0].name; renderDataVolumes(); };
+        row.querySelector(".dv-name").oninput = (ev) => { form.datavols[i] = JWA.renameDataVolume(form.datavols[i], ev.target.value); row.querySelector(".dv-mount").value = form.datavols[i].mount; };
+        row.querySelector(".dv-existing").onchange = (ev) => { form.datavols[i].existing = ev.target.value; };
+        row.querySelector(".dv-size").oninput = (ev) => { form.datavols[i].size = ev.target.value; };
+        row.querySelector(".dv-mode").onchange = (ev) => { form.datavols[i].accessMode = ev.target.value; };
+        row.querySelector(".dv-mount").oninput = (ev) => { form.datavols[i] = JWA.editMount(form.datavols[i], ev.target.value); };
+        row.querySelector(".dv-rm").onclick = () => { form.datavols.splice(i, 1); renderDataVolumes(); };
+      });
+    }
+    function renderWorkspace() {
+      const w = form.workspace;
+      $("f-ws").checked = !!w.enabled;
+      $("f-ws-panel").hidden = !w.enabled;
+      $("f-ws-header").textContent = w.enabled ? (w.type === "existing" ? w.existing : w.name) : "none";
+      $("f-ws-name").value = w.name || "";
+      $("f-ws-size").value = w.size || "";
+      document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.checked = r.value === w.accessMode; });
+    }
+    function fillSpawner() {
+      const opts = (list, value) => (list || []).map((i) => `<option${i === value ? " selected" : ""}>${kf.esc(i)}</option>`).join("");
+      $("f-image").innerHTML = opts(config.image.options, config.image.value);
+      $("f-image-g1").innerHTML = opts((config.imageGroupOne || {}).options, (config.imageGroupOne || {}).value);
+      $("f-image-g2").innerHTML = opts((config.imageGroupTwo || {}).options, (config.imageGroupTwo || {}).value);
+      $("f-custom-row").hidden = config.allowCustomImage === false;
+      const counts = (config.gpus.value || {}).options || ["none", "1", "2", "4", "8"];
+      $("f-gpus").innerHTML = counts.map((c) => `<option${c === form.gpus.num ? " selected" : ""}>${c}</option>`).join("");
+      $("f-cpu").value = form.cpu; $("f-cpu-limit").value = form.cpuLimit;
+      $("f-mem").value = form.memory; $("f-mem-limit").value = form.memoryLimit;
+      $("f-shm").checked = form.shm;
+      const groups = (key) => ['<option value="none">None</option>'].concat(((config[key] || {}).options || [])
+        .map((o) => `<option value="${kf.esc(o.configKey)}"${o.configKey === (config[key] || {}).value ? " selected" : ""}>${kf.esc(o.displayName || o.configKey)}</option>`)).join("");
+      $("f-affinity").innerHTML = groups("affinityConfig");
+      $("f-toleration").innerHTML = groups("tolerationGroup");
+      for (const [id, key] of [["f-cpu", "cpu"], ["f-cpu-limit", "cpu"], ["f-mem", "memory"], ["f-mem-limit", "memory"], ["f-gpus", "gpus"], ["f-shm", "shm"]])
+        $(id).disabled = !!(config[key] || {}).readOnly;
+      renderWorkspace();
+      renderDataVolumes();
+    }
+    let cpuLimitDirty = false, memLimitDirty = false;
+    function bindSpawner() {
+      $("f-name").oninput = (ev) => {
+        form.name = ev.target.value;
+        if (form.workspace.enabled && form.workspace.type === "new") { form.workspace.name = JWA.volumeName(form.workspace.template, form.name); renderWorkspace(); }
+      };
+      $("f-type").onchange = (ev) => {
+        form.serverType = ev.target.value;
+        $("f-image-row").hidden = form.serverType !== "jupyter";
+        $("f-image-g1-row").hidden = form.serverType !== "group-one";
+        $("f-image-g2-row").hidden = form.serverType !== "group-two";
+      };
+      $("f-cpu").oninput = (ev) => { form.cpu = ev.target.value; if (!cpuLimitDirty) { form.cpuLimit = JWA.limitFrom(form.cpu, config.cpu.limitFactor, ""); $("f-cpu-limit").value = form.cpuLimit; } };
+      $("f-mem").oninput = (ev) => { form.memory = ev.target.value; if (!memLimitDirty) { form.memoryLimit = JWA.limitFrom(form.memory, config.memory.limitFactor, "Gi"); $("f-mem-limit").value = form.memoryLimit; } };
+      $("f-cpu-limit").oninput = (ev) => { cpuLimitDirty = true; form.cpuLimit = ev.target.value; };
+      $("f-mem-limit").oninput = (ev) => { memLimitDirty = true; form.memoryLimit = ev.target.value; };
+      $("f-ws").onchange = (ev) => { form.workspace.enabled = ev.target.checked; renderWorkspace(); };
+      $("f-ws-name").oninput = (ev) => { form.workspace.name = ev.target.value; form.workspace.template = ev.target.value; $("f-ws-header").textContent = ev.target.value; };
+      $("f-ws-size").oninput = (ev) => { form.workspace.size = ev.target.value; };
+      document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.onchange = () => { form.workspace.accessMode = r.value; }; });
+      $("f-add-vol").onclick = () => { form.datavols.push(JWA.newDataVolume(form.name, form.datavols.length + 1)); renderDataVolumes(); };
+    }
+
+    async function openSpawner() {
+      const ns = kf.namespace();
+      form = JWA.formDefaults(config, "");
+      cpuLimitDirty = memLimitDirty = false;
+      $("f-name").value = "";
+      try {
+        const { poddefaults } = await kf.call("GET", `/api/namespaces/${ns}/poddefaults`);
+        $("f-configs").innerHTML = poddefaults.map((pd) =>
+          `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"${form.configurations.includes(pd.label) ? " checked" : ""}> ${kf.esc(pd.desc)}</label><br>`).join("") || '<span class="muted">none</span>';
+      } catch (e) { $("f-configs").innerHTML = '<span class="muted">none</span>'; }
+      try { form.pvcs = (await kf.call("GET", `/api/namespaces/${ns}/pvcs`)).pvcs; } catch (e) { form.pvcs = []; }
+      fillSpawner();
+      $("f-error").textContent = "";
+      $("spawner").showModal();
+    }
+
+    async function submit(ev) {
+      if (ev.submitter && ev.submitter.value !== "ok") return;
+      ev.preventDefault();
+      const ns = kf.namespace();
+      form.customImage = $("f-custom").value.trim();
+      form.gpus = $("f-gpus").value === "none" ? { num: "none", vendor: form.gpus.vendor } : { num: $("f-gpus").value, vendor: form.gpus.vendor };
+      form.shm = $("f-shm").checked;
+      form.affinityConfig = $("f-affinity").value || "none";
+      form.tolerationGroup = $("f-toleration").value || "none";
+      form.configurations = [...$("f-configs").querySelectorAll("input:checked")].map((i) => i.value);
+      const errs = JWA.validate(form);
+      if (errs.length) { $("f-error").textContent = errs.join("; "); return; }
+      try {
+        await kf.call("POST", `/api/namespaces/${ns}/notebooks`, JWA.buildBody(form, config, ns));
+        $("spawner").close(); kf.snack(`Notebook ${form.name} created`, "SUCCESS"); poller.reset();
+      } catch (e) { $("f-error").textContent = e.message; }
+    }
+
+    async function main() {
+      poller = new kf.Poller(refresh);
+      table = new kf.ResourceTable($("notebooks"), tableConfig());
+      $("filter").oninput = (ev) => table.setFilter(ev.target.value);
+      try {
+        config = (await kf.call("GET", "/api/config")).config;
+        await loadNamespaces();
+      } catch (e) { kf.snack(e.message, "ERROR"); }
+      form = JWA.formDefaults(config || {}, "");
+      $("new").onclick = openSpawner;
+      $("form").addEventListener("submit", submit);
+      bindSpawner();
+      kf.onNamespace((ns) => { if (!allNs) { $("ns").value = ns; poller.reset(); } });
+      poller.start();
+    }
+    main();
   }
 
-  async function main() {
-    try {
-      config = (await kf.call("GET", "/api/config")).config;
-      fillSpawner();
-      await loadNamespaces();
-    } catch (e) { $("error").textContent = e.message; }
-    $("new").onclick = openSpawner;
-    $("form").addEventListener("submit", submit);
-    poller = new kf.Poller(refresh);
-    kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
-    poller.start();
-  }
-  main();
-})();
+  global.JWA = JWA;
+  if (typeof module !== "undefined" && module.exports) module.exports = JWA;  // node unit tests
+  else if (typeof document !== "undefined") app();
+})(typeof window !== "undefined" ? window : globalThis);

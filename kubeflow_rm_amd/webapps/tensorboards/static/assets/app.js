@@ -1,58 +1,101 @@
-// TensorBoards web app frontend: list (polled), create from a PVC path (pvc://<claim>/<path>) or an
-// object-store URL, delete, connect at /tensorboard/<ns>/<name>/.
-(function () {
+// TensorBoards web app frontend (reference crud-web-apps/tensorboards/frontend): table (common
+// resource table, polled), create from a PVC path (pvc://<claim>/<path>) or an object-store URL
+// (s3:// gs://), PodDefault configurations, delete, connect at /tensorboard/<ns>/<name>/.
+// `TWA` holds the pure parts (columns, logspath building, validation) for the node tests.
+(function (global) {
   "use strict";
-  const $ = (id) => document.getElementById(id);
-  let poller = null;
-  async function namespaces() {
-    let list = [];
-    try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
-    $("ns").innerHTML = list.map((n) => `<option>${n}</option>`).join("");
-    if (!kf.namespace() && list.length) kf.setNamespace(list[0]);
-    $("ns").value = kf.namespace();
-    $("ns").onchange = () => kf.setNamespace($("ns").value);
+  const kf = global.kf || (typeof require !== "undefined" ? require("../../../crud_backend/static/kf.js") : null);
+
+  const TWA = {
+    columns(allNamespaces) {
+      const cols = [
+        { title: "Status", value: (r) => r.status.phase, html: (r) => kf.statusIcon(r.status) },
+        { title: "Name", value: (r) => r.name },
+      ];
+      if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
+      cols.push({ title: "Logspath", value: (r) => r.logspath }, { title: "Created at", value: (r) => r.age });
+      return cols;
+    },
+    logspath(kind, pvc, path) {
+      const p = String(path || "").trim();
+      return kind === "pvc" ? `pvc://${pvc}/${p.replace(/^\/+/, "")}` : p;
+    },
+    validate(name, kind, pvc, path) {
+      const errs = [];
+      const n = kf.validators.name(name);
+      if (n) errs.push(n);
+      if (kind === "pvc" && !pvc) errs.push("Select a PVC");
+      if (kind !== "pvc" && !/^(s3|gs):\/\/[^/]+/.test(String(path || "").trim())) errs.push("Object store paths look like s3://bucket/path or gs://bucket/path");
+      return errs;
+    },
+  };
+
+  function app() {
+    const $ = (id) => document.getElementById(id);
+    let poller = null, table = null;
+    async function namespaces() {
+      let list = [];
+      try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
+      $("ns").innerHTML = list.map((n) => `<option value="${kf.esc(n)}">${kf.esc(n)}</option>`).join("");
+      if (!kf.namespace() && list.length) kf.setNamespace(list[0]);
+      $("ns").value = kf.namespace();
+      $("ns").onchange = () => kf.setNamespace($("ns").value);
+    }
+    function tableConfig() {
+      return {
+        columns: TWA.columns(false), empty: "No TensorBoards in this namespace.",
+        actions: [{ name: "connect", label: "Connect", enabled: (r) => r.status.phase === "ready" }, { name: "delete", label: "Delete" }],
+        onAction: async (name, r) => {
+          if (name === "connect") window.open(`/tensorboard/${r.namespace}/${r.name}/`);
+          if (name === "delete" && confirm(`Delete TensorBoard ${r.name}?`)) {
+            try { await kf.call("DELETE", `/api/namespaces/${r.namespace}/tensorboards/${r.name}`); } catch (e) { kf.snack(e.message, "ERROR"); }
+            poller.reset();
+          }
+        },
+      };
+    }
+    async function refresh() {
+      const ns = kf.namespace();
+      if (!ns) return null;
+      const { tensorboards } = await kf.call("GET", `/api/namespaces/${ns}/tensorboards`);
+      table.setRows(tensorboards.map((t) => Object.assign({ namespace: ns }, t)));
+      return tensorboards.map((t) => [t.name, t.status.phase]);
+    }
+    async function open() {
+      const ns = kf.namespace();
+      const [{ pvcs }, { poddefaults }] = await Promise.all([kf.call("GET", `/api/namespaces/${ns}/pvcs`),
+        kf.call("GET", `/api/namespaces/${ns}/poddefaults`)]);
+      $("f-pvc").innerHTML = pvcs.map((p) => `<option>${kf.esc(p)}</option>`).join("");
+      $("f-configs").innerHTML = poddefaults.map((pd) => `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("");
+      $("f-error").textContent = "";
+      $("dlg").showModal();
+    }
+    async function submit(ev) {
+      if (ev.submitter && ev.submitter.value !== "ok") return;
+      ev.preventDefault();
+      const ns = kf.namespace(), kind = $("f-kind").value;
+      const errs = TWA.validate($("f-name").value, kind, $("f-pvc").value, $("f-path").value);
+      if (errs.length) { $("f-error").textContent = errs.join("; "); return; }
+      const logspath = TWA.logspath(kind, $("f-pvc").value, $("f-path").value);
+      const configurations = [...$("f-configs").querySelectorAll("input:checked")].map((i) => i.value);
+      try {
+        await kf.call("POST", `/api/namespaces/${ns}/tensorboards`, { name: $("f-name").value, logspath, configurations });
+        $("dlg").close(); kf.snack(`TensorBoard ${$("f-name").value} created`, "SUCCESS"); poller.reset();
+      } catch (e) { $("f-error").textContent = e.message; }
+    }
+    (async function main() {
+      poller = new kf.Poller(refresh);
+      table = new kf.ResourceTable($("rows"), tableConfig());
+      $("filter").oninput = (ev) => table.setFilter(ev.target.value);
+      await namespaces();
+      $("new").onclick = open;
+      $("form").addEventListener("submit", submit);
+      kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
+      poller.start();
+    })();
   }
-  async function refresh() {
-    const ns = kf.namespace();
-    if (!ns) return null;
-    const { tensorboards } = await kf.call("GET", `/api/namespaces/${ns}/tensorboards`);
-    $("rows").querySelector("tbody").replaceChildren(...tensorboards.map((tb) => {
-      const tr = kf.h("tr", {});
-      tr.innerHTML = `<td>${kf.statusCell(tb.status)}</td><td>${kf.esc(tb.name)}</td><td>${kf.esc(tb.logspath)}</td><td>${kf.esc(tb.age)}</td>`;
-      const connect = kf.h("button", { onclick: () => window.open(`/tensorboard/${ns}/${tb.name}/`) }, "Connect");
-      connect.disabled = tb.status.phase !== "ready";
-      tr.append(kf.h("td", {}, connect, kf.h("button", { onclick: async () => {
-        if (!confirm(`Delete TensorBoard ${tb.name}?`)) return;
-        try { await kf.call("DELETE", `/api/namespaces/${ns}/tensorboards/${tb.name}`); } catch (e) { $("error").textContent = e.message; }
-        poller.reset();
-      } }, "Delete")));
-      return tr;
-    }));
-    return tensorboards.map((t) => [t.name, t.status.phase]);
-  }
-  async function open() {
-    const ns = kf.namespace();
-    const [{ pvcs }, { poddefaults }] = await Promise.all([kf.call("GET", `/api/namespaces/${ns}/pvcs`),
-      kf.call("GET", `/api/namespaces/${ns}/poddefaults`)]);
-    $("f-pvc").innerHTML = pvcs.map((p) => `<option>${kf.esc(p)}</option>`).join("");
-    $("f-configs").innerHTML = poddefaults.map((pd) => `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("");
-    $("dlg").showModal();
-  }
-  async function submit(ev) {
-    if (ev.submitter && ev.submitter.value !== "ok") return;
-    ev.preventDefault();
-    const ns = kf.namespace(), path = $("f-path").value.trim();
-    const logspath = $("f-kind").value === "pvc" ? `pvc://${$("f-pvc").value}/${path.replace(/^\//, "")}` : path;
-    const configurations = [...$("f-configs").querySelectorAll("input:checked")].map((i) => i.value);
-    try { await kf.call("POST", `/api/namespaces/${ns}/tensorboards`, { name: $("f-name").value, logspath, configurations }); $("dlg").close(); poller.reset(); }
-    catch (e) { $("f-error").textContent = e.message; }
-  }
-  (async function main() {
-    await namespaces();
-    $("new").onclick = open;
-    $("form").addEventListener("submit", submit);
-    poller = new kf.Poller(refresh);
-    kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
-    poller.start();
-  })();
-})();
+
+  global.TWA = TWA;
+  if (typeof module !== "undefined" && module.exports) module.exports = TWA;
+  else if (typeof document !== "undefined") app();
+})(typeof window !== "undefined" ? window : globalThis);

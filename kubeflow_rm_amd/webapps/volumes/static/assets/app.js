@@ -1,90 +1,147 @@
-// Volumes web app frontend: PVC list (polled) with the notebooks using each one, create / delete,
-// volume details (overview / events / pods using it / YAML) and the PVCViewer (file browser)
-// lifecycle: browse -> create viewer -> open its URL when ready.
-(function () {
+// Volumes web app frontend (reference crud-web-apps/volumes/frontend): PVC table (common resource
+// table, polled) with the notebooks using each claim, create / delete, volume details (overview +
+// conditions / events / pods using it / YAML) and the PVCViewer (file browser) lifecycle: browse
+// -> viewer created -> open its URL when ready -> close.
+// `VWA` holds the pure parts (columns, viewer button state, request body) for the node tests.
+(function (global) {
   "use strict";
-  const $ = (id) => document.getElementById(id);
-  let poller = null;
-  async function namespaces() {
-    let list = [];
-    try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
-    $("ns").innerHTML = list.map((n) => `<option>${n}</option>`).join("");
-    if (!kf.namespace() && list.length) kf.setNamespace(list[0]);
-    $("ns").value = kf.namespace();
-    $("ns").onchange = () => kf.setNamespace($("ns").value);
-  }
-  async function act(method, path, body) {
-    try { await kf.call(method, path, body); $("error").textContent = ""; } catch (e) { $("error").textContent = e.message; }
-    poller.reset();
-  }
-  // volume page: overview / events / pods / YAML (VWA frontend pages/volume-details-page)
-  function showDetails(ns, name) {
-    const base = `/api/namespaces/${ns}/pvcs/${name}`;
-    const e = kf.esc;
-    return kf.details(`Volume ${ns}/${name}`, [
-      { name: "Overview", render: async () => {
-        const pvc = (await kf.call("GET", base)).pvc;
-        const spec = pvc.spec || {}, st = pvc.status || {};
-        return kf.kvTable([
-          ["Name", pvc.metadata.name], ["Namespace", pvc.metadata.namespace], ["Created", pvc.metadata.creationTimestamp],
-          ["Phase", st.phase || "-"], ["Requested", ((spec.resources || {}).requests || {}).storage || "-"],
-          ["Capacity", (st.capacity || {}).storage || "-"], ["Access modes", (spec.accessModes || []).join(", ")],
-          ["Storage class", spec.storageClassName || "(default)"], ["Volume", spec.volumeName || "-"],
-        ]);
-      } },
-      { name: "Events", render: async () => kf.eventsTable((await kf.call("GET", `${base}/events`)).events) },
-      { name: "Pods", render: async () => {
-        const pods = (await kf.call("GET", `${base}/pods`)).pods;
-        if (!pods.length) return '<p class="muted">Not mounted by any pod.</p>';
-        return kf.kvTable(pods.map((p) => [p.metadata.name, `${(p.status || {}).phase || ""} on ${(p.spec || {}).nodeName || "-"}`]));
-      } },
-      { name: "YAML", render: async () => `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).pvc))}</pre>` },
-    ]);
+  const kf = global.kf || (typeof require !== "undefined" ? require("../../../crud_backend/static/kf.js") : null);
+
+  const VWA = {
+    columns(allNamespaces) {
+      const cols = [
+        { title: "Status", value: (r) => r.status.phase, html: (r) => kf.statusIcon(r.status) },
+        { title: "Name", value: (r) => r.name, html: (r) => kf.nameLink(r) },
+      ];
+      if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
+      cols.push(
+        { title: "Created at", value: (r) => r.age },
+        { title: "Size", value: (r) => r.capacity },
+        { title: "Access Mode", value: (r) => (r.modes || []).join(", ") },
+        { title: "Storage Class", value: (r) => r.class || "" },
+        { title: "Used by", value: (r) => (r.notebooks || []).join(", "), sortable: false },
+      );
+      return cols;
+    },
+    // backend rows carry viewer {status, url} (volumes backend get.py); older payloads a bare status
+    viewerState(row) {
+      const v = row.viewer;
+      return typeof v === "string" ? { status: v, url: null } : { status: (v || {}).status || "uninitialized", url: (v || {}).url || null };
+    },
+    browseLabel(row) {
+      const v = VWA.viewerState(row);
+      return v.status === "ready" ? "Open browser" : v.status === "uninitialized" ? "Browse" : `Browser ${v.status}`;
+    },
+    newPvcBody(name, size, mode, storageClass) {
+      return { name, size: /[A-Za-z]$/.test(String(size)) ? String(size) : `${size}Gi`, mode, class: storageClass || "{empty}", type: "empty" };
+    },
+    validate(name, size) {
+      const errs = [];
+      const n = kf.validators.name(name);
+      if (n) errs.push(n);
+      if (kf.validators.memory(/[A-Za-z]$/.test(String(size)) ? size : `${size}Gi`)) errs.push(`Invalid size: ${size}`);
+      return errs;
+    },
+  };
+
+  function app() {
+    const $ = (id) => document.getElementById(id);
+    let poller = null, table = null;
+    async function namespaces() {
+      let list = [];
+      try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
+      $("ns").innerHTML = list.map((n) => `<option value="${kf.esc(n)}">${kf.esc(n)}</option>`).join("");
+      if (!kf.namespace() && list.length) kf.setNamespace(list[0]);
+      $("ns").value = kf.namespace();
+      $("ns").onchange = () => kf.setNamespace($("ns").value);
+    }
+    async function act(method, path, body) {
+      try { await kf.call(method, path, body); } catch (e) { kf.snack(e.message, "ERROR"); }
+      poller.reset();
+    }
+    // volume page: overview + conditions / events / pods / YAML (VWA pages/volume-details-page)
+    function showDetails(ns, name) {
+      const base = `/api/namespaces/${ns}/pvcs/${name}`;
+      const e = kf.esc;
+      return kf.details(`Volume ${ns}/${name}`, [
+        { name: "Overview", render: async () => {
+          const pvc = (await kf.call("GET", base)).pvc;
+          const spec = pvc.spec || {}, st = pvc.status || {};
+          return kf.kvTable([
+            ["Name", pvc.metadata.name], ["Namespace", pvc.metadata.namespace], ["Created", pvc.metadata.creationTimestamp],
+            ["Phase", st.phase || "-"], ["Requested", ((spec.resources || {}).requests || {}).storage || "-"],
+            ["Capacity", (st.capacity || {}).storage || "-"], ["Access modes", (spec.accessModes || []).join(", ")],
+            ["Storage class", spec.storageClassName || "(default)"], ["Volume", spec.volumeName || "-"],
+          ]) + `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
+        } },
+        { name: "Events", render: async () => kf.eventsTable((await kf.call("GET", `${base}/events`)).events) },
+        { name: "Pods", render: async () => {
+          const pods = (await kf.call("GET", `${base}/pods`)).pods;
+          if (!pods.length) return '<p class="muted">Not mounted by any pod.</p>';
+          return kf.kvTable(pods.map((p) => [p.metadata.name, `${(p.status || {}).phase || ""} on ${(p.spec || {}).nodeName || "-"}`]));
+        } },
+        { name: "YAML", render: async () => `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).pvc))}</pre>` },
+      ]);
+    }
+    function tableConfig() {
+      return {
+        columns: VWA.columns(false), empty: "No volumes in this namespace.",
+        actions: [
+          { name: "browse", label: (r) => VWA.browseLabel(r), enabled: (r) => ["ready", "uninitialized"].includes(VWA.viewerState(r).status) },
+          { name: "close", label: "Close browser", enabled: (r) => VWA.viewerState(r).status !== "uninitialized" },
+          { name: "delete", label: "Delete" },
+        ],
+        onOpen: (r) => showDetails(r.namespace, r.name),
+        onAction: (name, r) => {
+          const ns = r.namespace, v = VWA.viewerState(r);
+          if (name === "browse") {
+            if (v.status === "ready" && v.url) window.open(v.url);
+            else if (v.status === "uninitialized") act("POST", `/api/namespaces/${ns}/viewers`, { name: r.name });
+          }
+          if (name === "close") act("DELETE", `/api/namespaces/${ns}/viewers/${r.name}`);
+          if (name === "delete" && confirm(`Delete volume ${r.name}?`)) act("DELETE", `/api/namespaces/${ns}/pvcs/${r.name}`);
+        },
+      };
+    }
+    async function refresh() {
+      const ns = kf.namespace();
+      if (!ns) return null;
+      const { pvcs } = await kf.call("GET", `/api/namespaces/${ns}/pvcs`);
+      table.setRows(pvcs.map((p) => Object.assign({ namespace: ns }, p)));
+      return pvcs.map((p) => [p.name, p.status.phase, VWA.viewerState(p).status]);
+    }
+    async function open() {
+      let classes = [], def = "";
+      try { classes = (await kf.call("GET", "/api/storageclasses")).storageClasses; def = (await kf.call("GET", "/api/storageclasses/default")).defaultStorageClass; } catch (e) { /* not cluster-readable */ }
+      $("f-class").innerHTML = `<option value="{empty}">(default${def ? ": " + kf.esc(def) : ""})</option><option value="{none}">(none)</option>` +
+        classes.map((c) => `<option>${kf.esc(c)}</option>`).join("");
+      $("f-error").textContent = "";
+      $("dlg").showModal();
+    }
+    async function submit(ev) {
+      if (ev.submitter && ev.submitter.value !== "ok") return;
+      ev.preventDefault();
+      const ns = kf.namespace();
+      const errs = VWA.validate($("f-name").value, $("f-size").value);
+      if (errs.length) { $("f-error").textContent = errs.join("; "); return; }
+      try {
+        await kf.call("POST", `/api/namespaces/${ns}/pvcs`, VWA.newPvcBody($("f-name").value, $("f-size").value, $("f-mode").value, $("f-class").value));
+        $("dlg").close(); kf.snack(`Volume ${$("f-name").value} created`, "SUCCESS"); poller.reset();
+      } catch (e) { $("f-error").textContent = e.message; }
+    }
+    (async function main() {
+      poller = new kf.Poller(refresh);
+      table = new kf.ResourceTable($("rows"), tableConfig());
+      $("filter").oninput = (ev) => table.setFilter(ev.target.value);
+      await namespaces();
+      $("new").onclick = open;
+      $("form").addEventListener("submit", submit);
+      kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
+      poller.start();
+    })();
   }
 
-  async function refresh() {
-    const ns = kf.namespace();
-    if (!ns) return null;
-    const { pvcs } = await kf.call("GET", `/api/namespaces/${ns}/pvcs`);
-    $("rows").querySelector("tbody").replaceChildren(...pvcs.map((p) => {
-      const tr = kf.h("tr", {});
-      const e = kf.esc;
-      tr.innerHTML = `<td>${kf.statusCell(p.status)}</td><td><a class="name">${e(p.name)}</a></td><td>${e(p.age)}</td><td>${e(p.capacity)}</td>
-        <td>${e((p.modes || []).join(", "))}</td><td>${e(p.class || "")}</td><td>${e(p.notebooks.join(", "))}</td>`;
-      tr.querySelector("a.name").addEventListener("click", () => showDetails(ns, p.name));
-      const v = p.viewer || {};
-      const browse = kf.h("button", { onclick: () => (v.status === "ready" && v.url ? window.open(v.url)
-        : v.status === "uninitialized" ? act("POST", `/api/namespaces/${ns}/viewers`, { name: p.name }) : null) },
-        v.status === "ready" ? "Open browser" : v.status === "uninitialized" ? "Browse" : `Browser ${v.status}`);
-      const close = kf.h("button", { onclick: () => act("DELETE", `/api/namespaces/${ns}/viewers/${p.name}`) }, "Close browser");
-      close.disabled = v.status === "uninitialized";
-      const del = kf.h("button", { onclick: () => confirm(`Delete volume ${p.name}?`) && act("DELETE", `/api/namespaces/${ns}/pvcs/${p.name}`) }, "Delete");
-      tr.append(kf.h("td", {}, browse, close, del));
-      return tr;
-    }));
-    return pvcs.map((p) => [p.name, p.status.phase, (p.viewer || {}).status]);
-  }
-  async function open() {
-    let classes = [], def = "";
-    try { classes = (await kf.call("GET", "/api/storageclasses")).storageClasses; def = (await kf.call("GET", "/api/storageclasses/default")).defaultStorageClass; } catch (e) { /* not cluster-readable */ }
-    $("f-class").innerHTML = `<option value="{empty}">(default${def ? ": " + def : ""})</option><option value="{none}">(none)</option>` +
-      classes.map((c) => `<option>${c}</option>`).join("");
-    $("dlg").showModal();
-  }
-  async function submit(ev) {
-    if (ev.submitter && ev.submitter.value !== "ok") return;
-    ev.preventDefault();
-    const ns = kf.namespace();
-    const body = { name: $("f-name").value, size: $("f-size").value, mode: $("f-mode").value, class: $("f-class").value, type: "empty" };
-    try { await kf.call("POST", `/api/namespaces/${ns}/pvcs`, body); $("dlg").close(); poller.reset(); }
-    catch (e) { $("f-error").textContent = e.message; }
-  }
-  (async function main() {
-    await namespaces();
-    $("new").onclick = open;
-    $("form").addEventListener("submit", submit);
-    poller = new kf.Poller(refresh);
-    kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
-    poller.start();
-  })();
-})();
+  global.VWA = VWA;
+  if (typeof module !== "undefined" && module.exports) module.exports = VWA;
+  else if (typeof document !== "undefined") app();
+})(typeof window !== "undefined" ? window : globalThis);
