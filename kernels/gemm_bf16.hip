@@ -338,20 +338,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_256p(
     if (kStage) stage(kt + 2, kt & 1);
     if (kNext) read_frags(nxt, off0, a0, b0);
     mfmas(a1, b1);
-    if (SCHED == 2 && kStage && kNext) {
-      // 12 ds_reads first (they feed the NEXT tile's first cluster), then glds spread 1 per 2 MFMAs
-#pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
-    } else if (SCHED) {
+    if (SCHED) {
       if (kStage) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -556,9 +543,6 @@ extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void*
                                              long long ldc, long long ldr, long long sa, long long sb, long long sc,
                                              long long sr, float alpha, int act, void* stream);
 
-extern "C" int kfamd_gemm_nt_bf16_w4rg_launch(const void* A, const void* B, void* C, int M, int N, int K,
-                                              long long lda, long long ldb, long long ldc, int rg, void* stream);
-
 extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* C,
                                           const void* bias, const void* R, int M, int N, int K,
                                           int batch, long long lda, long long ldb, long long ldc,
@@ -566,6 +550,8 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
                                           long long stride_c, long long stride_r, float alpha,
                                           int act, void* stream) {
   if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return KFAMD_EINVAL;
+  // variants: 0 auto, 1 fast (8-wave 256^2), 2 generic, 3 pipe, 4 pipe_sched, 6 w4, 9 w4s
+  if (variant < 0 || variant > 9 || variant == 5 || variant == 7 || variant == 8) return KFAMD_EINVAL;
   if (lda < K || ldb < K || ldc < N || (R && ldr < N)) return KFAMD_EINVAL;
   if (act < KFAMD_ACT_NONE || act > KFAMD_ACT_SILU) return KFAMD_EINVAL;
   // activation + residual together is only compiled for act == NONE (residual = "add & norm"
@@ -608,10 +594,6 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   __bf16* c = static_cast<__bf16*>(C);
   const __bf16* bs = static_cast<const __bf16*>(bias);
   const __bf16* r = static_cast<const __bf16*>(R);
-  if (fast && (variant == 7 || variant == 8)) {  // w4 read-gap experiments (plain GEMM only)
-    if (bias || R || act != KFAMD_ACT_NONE || batch != 1 || alpha != 1.0f) return KFAMD_EINVAL;
-    return kfamd_gemm_nt_bf16_w4rg_launch(A, B, C, M, N, K, lda, ldb, ldc, variant == 7 ? 3 : 4, stream);
-  }
   // default fast path: the 4-wave w4 kernel (one wave per SIMD, 5-slot LDS ring; profiles/r1_gemm_w4c);
   // the 8-wave pipe_sched kernel when a 256-row panel spans >= 2 GiB (w4's 32-bit buffer offsets)
   const bool w4_ok = (long long)kBM * lda * 2 < (1LL << 31) && (long long)kBN * ldb * 2 < (1LL << 31);
@@ -627,9 +609,6 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
                          ldr, stride_a, stride_b, stride_c, stride_r, alpha);
     } else if (variant == 3) {
       KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 0, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
-                         ldr, stride_a, stride_b, stride_c, stride_r, alpha);
-    } else if (variant == 5) {
-      KFAMD_DISPATCH_EPI(gemm_nt_256p, KFAMD_COMMA 2, grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc,
                          ldr, stride_a, stride_b, stride_c, stride_r, alpha);
     } else {
       KFAMD_DISPATCH_EPI(gemm_nt_256, , grid, block, s, a, b, c, bs, r, M, N, K, lda, ldb, ldc, ldr,

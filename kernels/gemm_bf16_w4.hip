@@ -403,7 +403,9 @@ extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void*
   return launch_w4<128>(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, act, stream);
 }
 
-// Diagnostic launch (no epilogue variants): per-wave K-loop segment cycle sums into diag
+#ifdef KFAMD_DIAG
+// Diagnostic build only (libkfamd_kernels_diag.so, kubeflow_rm_amd._build.build_diag_kernels; never
+// in the production library): per-wave K-loop segment cycle sums into diag
 // [(M/256)*(N/256) blocks][4 waves][4 segments] (tools/kbench.py --diag-w4).
 extern "C" int kfamd_gemm_nt_bf16_w4_diag(const void* A, const void* B, void* C, int M, int N, int K,
                                           unsigned long long* diag, int abl, void* stream) {
@@ -424,25 +426,4 @@ extern "C" int kfamd_gemm_nt_bf16_w4_diag(const void* A, const void* B, void* C,
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
-
-// Read-gap experiments (no epilogue): RG = 3 / 4 spreads a substep's 16 ds_reads over 48 / 64 MFMAs.
-extern "C" int kfamd_gemm_nt_bf16_w4rg_launch(const void* A, const void* B, void* C, int M, int N, int K,
-                                              long long lda, long long ldb, long long ldc, int rg, void* stream) {
-  if (M % kBM || N % kBN || K % kBK) return KFAMD_EINVAL;
-  if ((long long)kBM * lda * 2 >= (1LL << 31) || (long long)kBN * ldb * 2 >= (1LL << 31)) return KFAMD_EINVAL;
-  dim3 grid((M / kBM) * (N / kBN), 1), block(kThreads);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const __bf16* a = static_cast<const __bf16*>(A);
-  const __bf16* b = static_cast<const __bf16*>(B);
-  __bf16* c = static_cast<__bf16*>(C);
-  if (rg == 3)
-    hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, false, 3>), grid, block, 0, s, a, b, c, nullptr,
-                       nullptr, M, N, K, lda, ldb, ldc, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, nullptr);
-  else if (rg == 4)
-    hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, false, 4>), grid, block, 0, s, a, b, c, nullptr,
-                       nullptr, M, N, K, lda, ldb, ldc, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, nullptr);
-  else
-    return KFAMD_EINVAL;
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
-}
+#endif  // KFAMD_DIAG

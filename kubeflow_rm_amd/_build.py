@@ -55,6 +55,21 @@ def _newer(target: Path, sources: list[Path]) -> bool:
     return all(s.stat().st_mtime <= t for s in sources)
 
 
+DIAG_LIB = LIB_DIR / "libkfamd_kernels_diag.so"
+
+
+def build_diag_kernels() -> Path:
+    """Diagnostic GEMM build (in-kernel s_memtime stamps + ablation switches: tools/w4_diag.py).
+    Kept out of libkfamd_kernels.so: compiled only on request, with -DKFAMD_DIAG."""
+    src = KERNEL_DIR / "gemm_bf16_w4.hip"
+    obj = BUILD_DIR / "kernels" / "gemm_bf16_w4_diag.o"
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    LIB_DIR.mkdir(parents=True, exist_ok=True)
+    _run([HIPCC, *HIP_FLAGS, "-DKFAMD_DIAG", "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(DIAG_LIB), str(obj)])
+    return DIAG_LIB
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     """Compile kernels/*.hip for gfx950 and link libkfamd_kernels.so (incremental)."""
     srcs = sorted(KERNEL_DIR.glob("*.hip"))

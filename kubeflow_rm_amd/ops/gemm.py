@@ -12,7 +12,7 @@ import torch
 from . import _lib
 
 ACTS = {"none": 0, "relu": 1, "gelu_tanh": 2, "gelu": 2, "silu": 3}
-VARIANTS = {"auto": 0, "fast": 1, "generic": 2, "pipe": 3, "pipe_sched": 4, "pipe_sched2": 5, "w4": 6, "w4r3": 7, "w4r4": 8, "w4s": 9}
+VARIANTS = {"auto": 0, "fast": 1, "generic": 2, "pipe": 3, "pipe_sched": 4, "w4": 6, "w4s": 9}
 
 
 def _stream_ptr(t: torch.Tensor) -> int:

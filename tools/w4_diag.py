@@ -13,9 +13,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 def main():
     import torch
-    from kubeflow_rm_amd import ops
-    from kubeflow_rm_amd.ops import _lib
-    L = _lib.lib()
+    from kubeflow_rm_amd import _build, ops
+    # the stamped / ablation kernels live in their own library (never in libkfamd_kernels.so);
+    # build it on the host first: python -c "from kubeflow_rm_amd import _build; _build.build_diag_kernels()"
+    if not _build.DIAG_LIB.exists():
+        raise SystemExit(f"{_build.DIAG_LIB} missing: build it with _build.build_diag_kernels()")
+    L = ctypes.CDLL(str(_build.DIAG_LIB))
     f = L.kfamd_gemm_nt_bf16_w4_diag
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
