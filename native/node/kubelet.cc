@@ -181,6 +181,9 @@ int Kubelet::alloc_rdzv_port() {
     a.sin_family = AF_INET;
     a.sin_port = htons(static_cast<uint16_t>(port));
     a.sin_addr.s_addr = htonl(INADDR_ANY);
+    // torch's TCPStore listens with SO_REUSEADDR, so a released port in TIME_WAIT is reusable
+    const int one = 1;
+    ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
     const bool free_now = ::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0;
     ::close(fd);
     if (!free_now) continue;
