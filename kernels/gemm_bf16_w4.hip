@@ -31,7 +31,6 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 #define COMPILER_FENCE() asm volatile("" ::: "memory")
@@ -69,13 +68,7 @@ __device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& 
 // BM = 256: the 256x256 tile above (one 160 KiB block per CU). BM = 128 ("w4s"): the same
 // pipeline on a 128x128 tile, 64x64 per wave, 80 KiB of LDS -> two blocks per CU; chosen when a
 // problem has fewer 256-tiles than CUs (2048^2: 64 tiles of 256^2 vs 256 of 128^2).
-// KN (schedule knobs, 0 = the production schedule; other values are built only into the diagnostic
-// library for A/B runs, tools/gemm_explore.py): bits 0-1 DMA placement inside a substep (0: one per
-// DMA_EVERY MFMAs from m = 2; 1: all in the substep's second half, after the fragment reads),
-// bits 2-3 C store flavour (0 plain, 1 nontemporal, 2 sc1 write-through), bit 4 persistent grid
-// (one block per CU loops over tiles; the next tile's first two K-tiles stream in during the last
-// substep of the current one, so its prologue overlaps the epilogue stores).
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DIAG = false, int RG = 2, int ABL = 0, int BM = 256, int KN = 0>
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool DIAG = false, int RG = 2, int ABL = 0, int BM = 256>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
@@ -87,10 +80,7 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
   constexpr int MF = NR * NR;                            // MFMAs per wave per k32 substep
   constexpr int DMA_EVERY = MF / PIECES;               // one DMA per DMA_EVERY MFMAs
-  constexpr int DMAP = KN & 3, STF = (KN >> 2) & 3;
-  constexpr bool PERSIST = (KN >> 4) & 1;
   static_assert(BM == 256 || BM == 128, "tile");
-  static_assert(!(PERSIST && DIAG), "stamps assume one tile per block");
   __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -103,31 +93,26 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   }
 
   const int tiles_m = M / BM, tiles_n = N / BN, nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
   constexpr int kGroupM = 4;
   const int per_group = kGroupM * tiles_n;
-  // tile t -> origin: XCD remap (blocks t and t+8 share an XCD; each XCD gets a contiguous run of
-  // remapped tiles), then bands of kGroupM tile rows walked column by column. A persistent block's
-  // tiles t, t+G, t+2G... (G a multiple of 8) stay on its XCD and keep the same band order.
-  auto tile_origin = [&](int t, int& m0, int& n0) {
-    const int wg = xcd_remap(t, nwg);
-    const int g = wg / per_group, first_m = g * kGroupM;
-    const int gm = min(tiles_m - first_m, kGroupM);
-    m0 = (first_m + (wg % per_group) % gm) * BM;
-    n0 = ((wg % per_group) / gm) * BN;
-  };
+  const int g = wg / per_group, first_m = g * kGroupM;
+  const int gm = min(tiles_m - first_m, kGroupM);
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const long long bz = blockIdx.y;
-  A += bz * sa;
-  B += bz * sb;
+  A += bz * sa + (long long)m0 * lda;
+  B += bz * sb + (long long)n0 * ldb;
   C += bz * sc;
   if (HAS_RES) R += bz * sr;
-  // wave-uniform buffer resources over a tile's BM-row panels (launcher checks < 2 GiB)
+  // wave-uniform buffer resources over this block's 256-row panels (launcher checks < 2 GiB)
   // ABL (timing-only ablation builds, w4_diag): 1 = zero-record descriptors (every DMA dropped in
   // the address unit, instruction stream kept), 2 = no K-loop ds_reads.
   const int nrec = (DIAG && ABL == 1) ? 0 : 0x7fffffff;
-  auto rsrc = [&](const __bf16* base, long long row0, long long ld, int records) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + row0 * ld), (short)0, records, kRsrcWord3);
-  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, nrec, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, nrec, kRsrcWord3);
 
   // 32 one-KiB pieces (8 rows each) per operand tile, 8 per wave: piece p = wid*8 + j covers rows
   // 8p..8p+7; lane i lands at LDS p*1024 + 16*i (row 8p + (i>>3), swizzled chunk (i&7)) and must
@@ -148,17 +133,14 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   // slot becomes the next free one. So the DMA is spread over the whole K-tile (1 per 8 MFMAs:
   // concentrated DMA issue stalled the single MFMA wave per SIMD — w4_diag: +30..80 cycles per
   // DMA) and A gets 3, B 2 substeps of lookahead instead of 1.5.
-  auto dma_a = [&](const __amdgpu_buffer_rsrc_t& r, int kt, int slot, int j) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
+  auto dma_a = [&](int kt, int slot, int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
                                              va[j & 1], j * rowstep_a + kt * kBK * 2, 0, 0);
   };
-  auto dma_b = [&](const __amdgpu_buffer_rsrc_t& r, int kt, int slot, int j) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
+  auto dma_b = [&](int kt, int slot, int j) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
                                              vb[j & 1], j * rowstep_b + kt * kBK * 2, 0, 0);
   };
-  // DMA slot of a substep: DMAP 0 -> one per DMA_EVERY MFMAs from m = 2; DMAP 1 -> the second half
-  auto dma_at = [](int m) { return DMAP == 0 ? (m % DMA_EVERY == 2) : (m >= MF / 2 && (m - MF / 2) % (DMA_EVERY / 2) == 0); };
-  auto dma_idx = [](int m) { return DMAP == 0 ? m / DMA_EVERY : (m - MF / 2) / (DMA_EVERY / 2); };
 
   const int lr = lane & 15, lh = lane >> 4;
   const int sw = lh ^ (lr >> 1);
@@ -167,6 +149,13 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   const int a_base = (wm * WT) * 128;
   const int b_base = (wn * WT) * 128;
 
+  f32x4 acc[NR][NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[NR], b0[NR], a1[NR], b1[NR];
   // fragment q of a set: q < R -> B fragment q, q >= R -> A fragment q-R
   auto read_frag = [&](int sa_slot, int sb_slot, int off, bf16x8(&af)[NR], bf16x8(&bf)[NR], int q) {
     if (q < NR) bf[q] = *reinterpret_cast<const bf16x8*>(smem + sb_slot * TILE + b_base + q * 2048 + off);
@@ -174,221 +163,163 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   };
 
   const int nk = K / kBK;
-  constexpr int NST = NR * NR / 2;           // epilogue stores per wave
-  constexpr int PF_EVERY = MF / (4 * PIECES);  // persistent prefetch: A0,B0,A1,B1 over one substep
-  static_assert(PF_EVERY >= 1, "prefetch density");
-  int t = blockIdx.x;
-  const int tstep = PERSIST ? (int)gridDim.x : nwg;
-  int m0, n0;
-  tile_origin(t, m0, n0);
-  __amdgpu_buffer_rsrc_t ra = rsrc(A, m0, lda, nrec), rb = rsrc(B, n0, ldb, nrec);
-  __amdgpu_buffer_rsrc_t nra = ra, nrb = rb;
-  bool prefetched = false;
+  // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
+  int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) {
+    dma_a(0, sa0, j);
+    dma_b(0, sb0, j);
+  }
+  if (nk > 1) {
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      dma_a(1, sa1, j);
+      dma_b(1, sb1, j);
+    }
+    if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  COMPILER_FENCE();
+  __builtin_amdgcn_s_barrier();
+  COMPILER_FENCE();
+#pragma unroll
+  for (int q = 0; q < 2 * NR; ++q) read_frag(sa0, sb0, off0, a0, b0, q);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  PIN();
+  __builtin_amdgcn_s_setprio(1);
+
+  // ds_reads of a substep go out 1 per RG MFMAs from its start (RG = 2: all in the first half, so
+  // the waits at its end find them landed); DMA 1 per 8 MFMAs across the substep.
   // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
   // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
   unsigned long long seg[4] = {0, 0, 0, 0};
   unsigned long long t_loop0 = 0, t_loop1 = 0;
   auto stamp = [&]() -> unsigned long long {
-    unsigned long long ts = 0;
+    unsigned long long t = 0;
     if (DIAG) {
       PIN();
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts)::"memory");
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
       PIN();
     }
-    return ts;
+    return t;
   };
-  using T = std::integral_constant<bool, true>;
-  using F = std::integral_constant<bool, false>;
-  // K-tiles 0 and 1 of the first tile (K-tile 0 twice when K = 64: the wait counts stay uniform)
-  const int kt1 = nk > 1 ? 1 : 0;
+  auto body = [&](int kt, auto do_stage, auto do_next) {
+    constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
+    constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
+    const unsigned long long t0 = stamp();
+    // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
 #pragma unroll
-  for (int j = 0; j < PIECES; ++j) {
-    dma_a(ra, 0, 0, j);
-    dma_b(rb, 0, 1, j);
-  }
-#pragma unroll
-  for (int j = 0; j < PIECES; ++j) {
-    dma_a(ra, kt1, 2, j);
-    dma_b(rb, kt1, 3, j);
-  }
-
-  for (;;) {
-    // wait for K-tile 0: younger are K-tile 1's 2*PIECES DMAs (+ the previous tile's NST epilogue
-    // stores when this tile was prefetched during that tile's last substep)
-    if (PERSIST && prefetched) {
-      if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag(sa0, sb0, off1, a1, b1, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_a(kt + 2, sf, m / DMA_EVERY);
+      PIN();
+      mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
+      PIN();
+    }
+    const unsigned long long t1 = stamp();
+    // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
+    // after it tile kt's slots are free
+    if (kStage) {
+      if constexpr (BM == 256) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0074);                      // vmcnt(4) expcnt(7) lgkmcnt(0)
     } else {
-      if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     }
     COMPILER_FENCE();
     __builtin_amdgcn_s_barrier();
     COMPILER_FENCE();
-
-    // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
-    int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
-    f32x4 acc[NR][NR];
-    bf16x8 a0[NR], b0[NR], a1[NR], b1[NR];
-#pragma unroll
-    for (int q = 0; q < 2 * NR; ++q) read_frag(sa0, sb0, off0, a0, b0, q);
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-      for (int n = 0; n < NR; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     PIN();
-    __builtin_amdgcn_s_setprio(1);
-
-    // ds_reads of a substep go out 1 per RG MFMAs from its start (RG = 2: all in the first half, so
-    // the waits at its end find them landed); DMA 1 per DMA_EVERY MFMAs across the substep.
-    auto body = [&](int kt, auto do_stage, auto do_next, auto do_pf) {
-      constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
-      constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
-      constexpr bool kPf = decltype(do_pf)::value;        // last K-tile: prefetch the next output tile
-      const unsigned long long t0 = stamp();
-      // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
+    const unsigned long long t2 = stamp();
+    // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
 #pragma unroll
-      for (int m = 0; m < MF; ++m) {
-        if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag(sa0, sb0, off1, a1, b1, m / RG);
-        if (kStage && dma_at(m)) dma_a(ra, kt + 2, sf, dma_idx(m));
-        PIN();
-        mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
-        PIN();
-      }
-      const unsigned long long t1 = stamp();
-      // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
-      // after it tile kt's slots are free (and on the last K-tile, every slot: no reads follow)
-      if (kStage) {
-        if constexpr (BM == 256) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
-        else __builtin_amdgcn_s_waitcnt(0x0074);                      // vmcnt(4) expcnt(7) lgkmcnt(0)
-      } else {
-        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-      }
-      COMPILER_FENCE();
-      __builtin_amdgcn_s_barrier();
-      COMPILER_FENCE();
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag(sa1, sb1, off0, a0, b0, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_b(kt + 2, sa0, m / DMA_EVERY);
       PIN();
-      const unsigned long long t2 = stamp();
-      // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
-#pragma unroll
-      for (int m = 0; m < MF; ++m) {
-        if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag(sa1, sb1, off0, a0, b0, m / RG);
-        if (kStage && dma_at(m)) dma_b(rb, kt + 2, sa0, dma_idx(m));
-        if constexpr (kPf) {
-          if (m % PF_EVERY == 0) {
-            const int q = m / PF_EVERY, part = q / PIECES, j = q % PIECES;  // A0, B0, A1, B1
-            if (part == 0) dma_a(nra, 0, 0, j);
-            else if (part == 1) dma_b(nrb, 0, 1, j);
-            else if (part == 2) dma_a(nra, kt1, 2, j);
-            else dma_b(nrb, kt1, 3, j);
-          }
-        }
-        PIN();
-        mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
-        PIN();
-      }
-      const unsigned long long t3 = stamp();
-      if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
+      mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
       PIN();
-      // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
-      const int na = sf, nb = sa0;
-      sf = sb0;
-      sa0 = sa1;
-      sb0 = sb1;
-      sa1 = na;
-      sb1 = nb;
-      if (DIAG) {
-        const unsigned long long t4 = stamp();
-        seg[0] += t1 - t0;
-        seg[1] += t2 - t1;
-        seg[2] += t3 - t2;
-        seg[3] += t4 - t3;
-      }
-    };
-    if (DIAG) t_loop0 = stamp();
-    int kt = 0;
-    for (; kt + 2 < nk; ++kt) body(kt, T{}, T{}, F{});
-    if (kt + 1 < nk) {
-      body(kt, F{}, T{}, F{});
-      ++kt;
     }
-    // next output tile (persistent grid), computed here so its descriptors are not live in the loop
-    const int t_next = t + tstep;
-    const bool has_next = PERSIST && t_next < nwg;
-    int m0n = m0, n0n = n0;
-    if (has_next) tile_origin(t_next, m0n, n0n);
-    // the last tile's prefetch DMAs get zero-record descriptors: dropped, nothing lands
-    nra = rsrc(A, m0n, lda, has_next ? nrec : 0);
-    nrb = rsrc(B, n0n, ldb, has_next ? nrec : 0);
-    if (kt < nk) {
-      if constexpr (PERSIST) body(kt, F{}, F{}, T{});
-      else body(kt, F{}, F{}, F{});
+    const unsigned long long t3 = stamp();
+    if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
+    PIN();
+    // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
+    const int na = sf, nb = sa0;
+    sf = sb0;
+    sa0 = sa1;
+    sb0 = sb1;
+    sa1 = na;
+    sb1 = nb;
+    if (DIAG) {
+      const unsigned long long t4 = stamp();
+      seg[0] += t1 - t0;
+      seg[1] += t2 - t1;
+      seg[2] += t3 - t2;
+      seg[3] += t4 - t3;
     }
-    __builtin_amdgcn_s_setprio(0);
-    if (DIAG) t_loop1 = stamp();
-    // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  };
+  using T = std::integral_constant<bool, true>;
+  using F = std::integral_constant<bool, false>;
+  if (DIAG) t_loop0 = stamp();
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
+  if (kt + 1 < nk) {
+    body(kt, F{}, T{});
+    ++kt;
+  }
+  if (kt < nk) body(kt, F{}, F{});
+  __builtin_amdgcn_s_setprio(0);
+  if (DIAG) t_loop1 = stamp();
+  // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
-    // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
-    // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
-    // groups (cdna_hip_programming.md T21, 16-lane form), after which every lane holds 8 contiguous
-    // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
-    // lh 3 -> block n+1 cols 8-15. Half the store instructions (dwordx4 instead of dwordx2), every
-    // row segment 64 contiguous bytes; the tail is ~5 % of a block at 8192^3 (w4_diag epilogue stamps).
-    // lane id re-derived here (v_mbcnt) so no lane-derived VGPR has to survive the K loop: with every
-    // VGPR taken by fragments a survivor gets spilled, and its reload's vmcnt(0) would also wait for
-    // the persistent prefetch DMAs
-    const int elane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const int elr = elane & 15, elh = elane >> 4;
-    auto finish = [&](int i, int n, int m) -> uint2 {
-      const int col = n0 + wn * WT + n * 16 + elh * 4;
-      float v[4];
+  // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
+  // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
+  // groups (cdna_hip_programming.md T21, 16-lane form), after which every lane holds 8 contiguous
+  // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
+  // lh 3 -> block n+1 cols 8-15. Half the store instructions (dwordx4 instead of dwordx2), every
+  // row segment 64 contiguous bytes; the tail is ~5 % of a block at 8192^3 (w4_diag epilogue stamps).
+  // lane id re-derived here (v_mbcnt) so no lane-derived VGPR has to survive the K loop (with every
+  // VGPR taken by fragments such a survivor was spilled to scratch: profiles/r2_gemm_knobs)
+  const int elane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int elr = elane & 15, elh = elane >> 4;
+  auto finish = [&](int i, int n, int m) -> uint2 {
+    const int col = n0 + wn * WT + n * 16 + elh * 4;
+    float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
-      if (HAS_BIAS) {
-        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+    for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
+    if (HAS_BIAS) {
+      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
-      }
-      if (ACT != KFAMD_ACT_NONE) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
-      }
-      if (HAS_RES) {
-        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
-      return __builtin_bit_cast(uint2, o);
-    };
-    const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int m = m0 + wm * WT + i * 16 + elr;
-      __bf16* crow = C + (long long)m * ldc + n0 + wn * WT + swap_col;
-#pragma unroll
-      for (int n = 0; n < NR; n += 2) {
-        uint2 p = finish(i, n, m), q = finish(i, n + 1, m);
-        const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
-        const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
-        const u32x4 w = {sx[0], sy[0], sx[1], sy[1]};
-        u32x4* dst = reinterpret_cast<u32x4*>(crow + n * 16);
-        if constexpr (STF == 1) __builtin_nontemporal_store(w, dst);
-        else if constexpr (STF == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
-        else *dst = w;
-      }
+      for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
     }
-    if (!has_next) break;
-    t = t_next;
-    m0 = m0n;
-    n0 = n0n;
-    ra = nra;
-    rb = nrb;
-    prefetched = true;
+    if (ACT != KFAMD_ACT_NONE) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
+    }
+    if (HAS_RES) {
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+    return __builtin_bit_cast(uint2, o);
+  };
+  const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int m = m0 + wm * WT + i * 16 + elr;
+    __bf16* crow = C + (long long)m * ldc + n0 + wn * WT + swap_col;
+#pragma unroll
+    for (int n = 0; n < NR; n += 2) {
+      uint2 p = finish(i, n, m), q = finish(i, n + 1, m);
+      const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
+      *reinterpret_cast<uint4*>(crow + n * 16) = uint4{sx[0], sy[0], sx[1], sy[1]};
+    }
   }
   if (DIAG) {
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
@@ -477,49 +408,6 @@ extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void*
 }
 
 #ifdef KFAMD_DIAG
-// Schedule-knob A/B builds (diagnostic library only; tools/gemm_explore.py): plain C = A B^T at
-// 256^2 tiles with the knob word KN of gemm_nt_256w4 (0 = production). Persistent knobs launch one
-// block per CU (a multiple of 8, so each block's tiles stay on its XCD).
-extern "C" int kfamd_gemm_nt_bf16_w4_knob(int kn, const void* A, const void* B, void* C, int M, int N, int K,
-                                          void* stream) {
-  if (M % kBM || N % kBN || K % kBK || (long long)kBM * K * 2 >= (1LL << 31)) return KFAMD_EINVAL;
-  const int nwg = (M / kBM) * (N / kBN);
-  int grid_x = nwg;
-  if (kn & 16) {
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return KFAMD_EINVAL;
-    grid_x = ncu < nwg ? (ncu / 8) * 8 : nwg;
-    if (grid_x <= 0) grid_x = nwg;
-  }
-  dim3 grid(grid_x, 1), block(kThreads);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const __bf16* a = static_cast<const __bf16*>(A);
-  const __bf16* b = static_cast<const __bf16*>(B);
-  __bf16* c = static_cast<__bf16*>(C);
-#define W4_KNOB(KNV)                                                                                              \
-  case KNV:                                                                                                       \
-    hipLaunchKernelGGL((gemm_nt_256w4<KFAMD_ACT_NONE, false, false, false, 2, 0, 256, KNV>), grid, block, 0, s, a, b, \
-                       c, nullptr, nullptr, M, N, K, (long long)K, (long long)K, (long long)N, 0LL, 0LL, 0LL, 0LL,     \
-                       0LL, 1.0f, nullptr);                                                                         \
-    break;
-  switch (kn) {
-    W4_KNOB(0)
-    W4_KNOB(1)
-    W4_KNOB(4)
-    W4_KNOB(8)
-    W4_KNOB(16)
-    W4_KNOB(17)
-    W4_KNOB(20)
-    W4_KNOB(24)
-    default:
-      return KFAMD_EINVAL;
-  }
-#undef W4_KNOB
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
-}
-
 // Diagnostic build only (libkfamd_kernels_diag.so, kubeflow_rm_amd._build.build_diag_kernels; never
 // in the production library): per-wave K-loop segment cycle sums into diag
 // [(M/256)*(N/256) blocks][4 waves][4 segments] (tools/kbench.py --diag-w4).
