@@ -203,3 +203,52 @@ def test_spawner_body_built_in_js_is_accepted_by_the_backend(apps):
     assert ctr["resources"]["limits"]["amd.com/gpu"] == "1"
     assert {"name": "jsform-data", "mountPath": "/home/jovyan/jsform-data"} in ctr["volumeMounts"]
     assert c.get("v1", "PersistentVolumeClaim", "jsform-workspace", NS)["spec"]["accessModes"] == ["ReadWriteOnce"]
+
+
+DASH_FIXTURES = Path("/root/reference/components/centraldashboard-angular/frontend/cypress/fixtures")
+
+
+@pytest.mark.skipif(not DASH_FIXTURES.exists(), reason="reference Cypress fixtures not present")
+@needs_node
+def test_dashboard_against_reference_specs():
+    """cdb.js (namespace selection, URL mirroring, menu state, pages) vs the angular dashboard's
+    namespace-selector / url-syncing Cypress specs and the Polymer dashboard's unit specs."""
+    r = subprocess.run([NODE, str(ROOT / "tests/js/test_dashboard.js"), str(DASH_FIXTURES.parents[3])],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not DASH_FIXTURES.exists(), reason="reference Cypress fixtures not present")
+def test_dashboard_env_info_has_the_fixture_shape(monkeypatch):
+    """/api/workgroup/env-info answers with envinfo.json's keys (the shell's only input besides links)."""
+    from kubeflow_rm_amd.webapps import dashboard as dash
+    want = json.loads((DASH_FIXTURES / "envinfo.json").read_text())
+
+    class FakeKfam:
+        def __init__(self, *_a, **_k):
+            pass
+
+        def is_cluster_admin(self, _u):
+            return False
+
+        def read_bindings(self, **_k):
+            return [{"user": {"kind": "User", "name": "user"}, "referredNamespace": "kubeflow-user",
+                     "roleRef": {"kind": "ClusterRole", "name": "admin"}}]
+
+    class FakeK8s:
+        def __init__(self, *_a, **_k):
+            pass
+
+        def get_platform_info(self):
+            return {"provider": "other://", "providerName": "other", "kubeflowVersion": "mi355x"}
+
+    monkeypatch.setattr(dash, "KfamClient", FakeKfam)
+    monkeypatch.setattr(dash, "KubernetesService", FakeK8s)
+    app = dash.create_app(k8s_client=object(), kfam_url="http://unused", metrics=None)
+    got = app.test_client().get("/api/workgroup/env-info", headers={"kubeflow-userid": "user"}).get_json()
+    assert set(got) == set(want)
+    assert set(got["namespaces"][0]) == set(want["namespaces"][0])
+    assert got["namespaces"][0]["role"] == "owner"
+    shell = app.test_client().get("/")
+    assert b"/cdb.js" in shell.data
+    assert app.test_client().get("/cdb.js").status_code == 200
