@@ -28,6 +28,7 @@
 #include "kfam/kfam.h"
 #include "controllers/odh.h"
 #include "core/util.h"
+#include "gpu/smi.h"
 #include "gpu/topology.h"
 
 namespace kf {
@@ -374,6 +375,27 @@ void register_gpu(CapiRegistry& R) {
     for (const auto& x : a["devices"].as_array()) p.devices.push_back(static_cast<int>(x.as_int()));
     p.ring = GpuAllocator::ring_order(t, p.devices);
     return gpu_env_for(p, t, p.devices.size() > 1);
+  });
+  // one AMD SMI telemetry sample (what the kubelet's collectors export), matched to the KFD topology
+  R.add("smi_sample", [](const Json&) -> Json {
+    Json devs = Json::array();
+    for (const auto& t : AmdSmi::instance().sample()) {
+      Json rd = Json::array(), wr = Json::array();
+      for (int l = 0; l < t.xgmi_links; ++l) {
+        rd.push_back(t.xgmi_read_bytes[l]);
+        wr.push_back(t.xgmi_write_bytes[l]);
+      }
+      devs.push_back(Json{{"bdf", t.bdf}, {"gfx_activity", t.gfx_activity}, {"umc_activity", t.umc_activity},
+                          {"power_w", t.power_w}, {"temp_hotspot_c", t.temp_hotspot_c}, {"temp_mem_c", t.temp_mem_c},
+                          {"gfxclk_mhz", t.gfxclk_mhz}, {"energy_j", t.energy_j}, {"xgmi_read_bytes", rd},
+                          {"xgmi_write_bytes", wr}, {"accumulation_counter", static_cast<double>(t.accumulation_counter)},
+                          {"ppt_residency_acc", static_cast<double>(t.ppt_residency_acc)},
+                          {"thermal_residency_acc", static_cast<double>(t.thermal_residency_acc)}});
+    }
+    Json buses = Json::array();
+    for (const auto& g : GpuTopology::discover().gpus) buses.push_back(g.pci_bus);
+    return Json{{"available", AmdSmi::instance().available()}, {"error", AmdSmi::instance().error()},
+                {"devices", devs}, {"topology_buses", buses}};
   });
 }
 

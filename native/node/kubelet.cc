@@ -19,6 +19,7 @@
 
 #include "controllers/common.h"
 #include "core/util.h"
+#include "gpu/smi.h"
 #include "node/node.h"
 
 extern char** environ;
@@ -325,7 +326,10 @@ void Kubelet::heartbeat_loop() {
 void Kubelet::stop() {
   if (metrics_registered_) {  // the collectors capture `this`
     for (const char* n : {"kfamd_gpu_allocated", "kfamd_gpu_hbm_allocated_bytes", "kfamd_gpu_vram_used_bytes",
-                          "kfamd_gpu_vram_total_bytes", "kfamd_gpu_busy_percent"})
+                          "kfamd_gpu_vram_total_bytes", "kfamd_gpu_busy_percent", "kfamd_gpu_gfx_activity_percent",
+                          "kfamd_gpu_hbm_activity_percent", "kfamd_gpu_power_watts", "kfamd_gpu_temperature_celsius",
+                          "kfamd_gpu_gfxclk_mhz", "kfamd_gpu_energy_joules_total", "kfamd_gpu_xgmi_read_bytes_total",
+                          "kfamd_gpu_xgmi_write_bytes_total", "kfamd_gpu_throttle_residency_ratio"})
       Registry::global().unregister(n);
     metrics_registered_ = false;
   }
@@ -1129,7 +1133,166 @@ void Kubelet::register_gpu_metrics() {
           return out;
         }));
   }
+  register_telemetry_metrics();
   metrics_registered_ = true;
+}
+
+// Live SMU telemetry per MI355X (AMD SMI gpu_metrics, gpu/smi.h), labelled with the pod that holds
+// the device: what a notebook's GPUs are doing (GFX / HBM-controller activity), the clock they
+// hold under load (MFMA-dense kernels are clock-limited on this part), power, temperatures,
+// energy, xGMI traffic per link (RCCL rings over xGMI) and power/thermal throttle residency. One
+// AMD SMI sample serves every family of a scrape (cached 1 s).
+void Kubelet::register_telemetry_metrics() {
+  auto& reg = Registry::global();
+  struct Cache {
+    std::mutex mu;
+    double at = -1e9;
+    std::vector<GpuTelemetry> last, prev;  // prev: the sample before, for throttle-residency deltas
+  };
+  auto cache = std::make_shared<Cache>();
+  // (device index, telemetry, previous telemetry or null, namespace, pod) for every discovered GPU
+  struct Row {
+    int gpu;
+    GpuTelemetry t;
+    bool has_prev;
+    GpuTelemetry prev;
+    std::string ns, pod;
+  };
+  auto rows = [this, cache]() {
+    std::vector<Row> out;
+    std::vector<GpuTelemetry> cur, prev;
+    {
+      std::lock_guard<std::mutex> g(cache->mu);
+      const double t = now_seconds();
+      if (t - cache->at > 1.0) {
+        auto s = AmdSmi::instance().sample();
+        if (!s.empty()) {
+          cache->prev = std::move(cache->last);
+          cache->last = std::move(s);
+        }
+        cache->at = t;
+      }
+      cur = cache->last;
+      prev = cache->prev;
+    }
+    if (cur.empty()) return out;
+    std::map<int, std::pair<std::string, std::string>> owner;
+    const auto allocs = alloc_->allocations();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& a : allocs) {
+        auto it = pods_.find(a.first);
+        for (int d : a.second)
+          owner[d] = it != pods_.end() ? std::make_pair(it->second->ns, it->second->name) : std::make_pair(std::string(), a.first);
+      }
+    }
+    for (const auto& gdev : alloc_->topology().gpus) {
+      for (const auto& t : cur) {
+        if (t.bdf != gdev.pci_bus) continue;
+        Row r{gdev.index, t, false, {}, "", ""};
+        for (const auto& p : prev)
+          if (p.bdf == t.bdf) {
+            r.has_prev = true;
+            r.prev = p;
+          }
+        auto o = owner.find(gdev.index);
+        if (o != owner.end()) {
+          r.ns = o->second.first;
+          r.pod = o->second.second;
+        }
+        out.push_back(r);
+        break;
+      }
+    }
+    return out;
+  };
+  using Field = double (*)(const GpuTelemetry&);
+  struct PerPod {
+    const char* name;
+    const char* help;
+    Field f;
+  };
+  static const PerPod kPerPod[] = {
+      {"kfamd_gpu_gfx_activity_percent", "GFX engine activity (SMU average), labelled with the holding pod",
+       [](const GpuTelemetry& t) { return t.gfx_activity; }},
+      {"kfamd_gpu_hbm_activity_percent", "HBM memory-controller (UMC) activity, labelled with the holding pod",
+       [](const GpuTelemetry& t) { return t.umc_activity; }},
+  };
+  for (const auto& m : kPerPod) {
+    const Field f = m.f;
+    reg.add_collector(std::make_shared<CollectorFamily>(
+        m.name, m.help, "gauge", std::vector<std::string>{"gpu", "namespace", "pod"}, [rows, f]() {
+          std::vector<std::pair<Labels, double>> out;
+          for (const auto& r : rows()) {
+            const double v = f(r.t);
+            if (v >= 0) out.push_back({{std::to_string(r.gpu), r.ns, r.pod}, v});
+          }
+          return out;
+        }));
+  }
+  struct PerGpu {
+    const char* name;
+    const char* help;
+    const char* type;
+    Field f;
+  };
+  static const PerGpu kPerGpu[] = {
+      {"kfamd_gpu_power_watts", "socket power", "gauge", [](const GpuTelemetry& t) { return t.power_w; }},
+      {"kfamd_gpu_gfxclk_mhz", "current GFX clock: the clock the GPU holds under load", "gauge",
+       [](const GpuTelemetry& t) { return t.gfxclk_mhz; }},
+      {"kfamd_gpu_energy_joules_total", "energy accumulated since driver load", "counter",
+       [](const GpuTelemetry& t) { return t.energy_j; }},
+  };
+  for (const auto& m : kPerGpu) {
+    const Field f = m.f;
+    reg.add_collector(std::make_shared<CollectorFamily>(
+        m.name, m.help, m.type, std::vector<std::string>{"gpu"}, [rows, f]() {
+          std::vector<std::pair<Labels, double>> out;
+          for (const auto& r : rows()) {
+            const double v = f(r.t);
+            if (v >= 0) out.push_back({{std::to_string(r.gpu)}, v});
+          }
+          return out;
+        }));
+  }
+  reg.add_collector(std::make_shared<CollectorFamily>(
+      "kfamd_gpu_temperature_celsius", "hotspot and HBM temperature", "gauge", std::vector<std::string>{"gpu", "sensor"},
+      [rows]() {
+        std::vector<std::pair<Labels, double>> out;
+        for (const auto& r : rows()) {
+          if (r.t.temp_hotspot_c >= 0) out.push_back({{std::to_string(r.gpu), "hotspot"}, r.t.temp_hotspot_c});
+          if (r.t.temp_mem_c >= 0) out.push_back({{std::to_string(r.gpu), "hbm"}, r.t.temp_mem_c});
+        }
+        return out;
+      }));
+  for (int dir = 0; dir < 2; ++dir) {
+    reg.add_collector(std::make_shared<CollectorFamily>(
+        dir == 0 ? "kfamd_gpu_xgmi_read_bytes_total" : "kfamd_gpu_xgmi_write_bytes_total",
+        dir == 0 ? "bytes read over each xGMI link since driver load" : "bytes written over each xGMI link since driver load",
+        "counter", std::vector<std::string>{"gpu", "link"}, [rows, dir]() {
+          std::vector<std::pair<Labels, double>> out;
+          for (const auto& r : rows())
+            for (int l = 0; l < r.t.xgmi_links; ++l)
+              out.push_back({{std::to_string(r.gpu), std::to_string(l)},
+                             dir == 0 ? r.t.xgmi_read_bytes[l] : r.t.xgmi_write_bytes[l]});
+          return out;
+        }));
+  }
+  reg.add_collector(std::make_shared<CollectorFamily>(
+      "kfamd_gpu_throttle_residency_ratio",
+      "share of the last sampling interval spent power-limited (PVIOL) or thermally limited (TVIOL)", "gauge",
+      std::vector<std::string>{"gpu", "cause"}, [rows]() {
+        std::vector<std::pair<Labels, double>> out;
+        for (const auto& r : rows()) {
+          if (!r.has_prev || r.t.accumulation_counter <= r.prev.accumulation_counter) continue;
+          const double dt = static_cast<double>(r.t.accumulation_counter - r.prev.accumulation_counter);
+          out.push_back({{std::to_string(r.gpu), "power"},
+                         static_cast<double>(r.t.ppt_residency_acc - r.prev.ppt_residency_acc) / dt});
+          out.push_back({{std::to_string(r.gpu), "thermal"},
+                         static_cast<double>(r.t.thermal_residency_acc - r.prev.thermal_residency_acc) / dt});
+        }
+        return out;
+      }));
 }
 
 void Kubelet::setup(Manager& mgr) {

@@ -103,6 +103,7 @@ class Kubelet {
   Json node_object() const;
   void heartbeat_loop();
   void register_gpu_metrics();
+  void register_telemetry_metrics();
   bool metrics_registered_ = false;
   void terminate_pod(PodRuntime& rt, int64_t grace_s);
   std::shared_ptr<Client> c_;
