@@ -473,14 +473,30 @@ void ApiServer::add_validating_plugin(const std::string& name, AdmissionFn fn) {
   validating_.emplace_back(name, std::move(fn));
 }
 
+// kube-apiserver's admission latency families: one observation per in-process plugin
+// (GPU placement, quota, PodDefault, readiness injection, ...) and per webhook call, labelled with
+// the plugin/webhook name, operation, mutating|validating and whether it rejected the request.
+std::shared_ptr<HistogramVec> admission_latency(bool webhook) {
+  static auto plugin_h = Registry::global().histogram(
+      "apiserver_admission_controller_admission_duration_seconds", "in-process admission plugin latency",
+      {"name", "operation", "type", "rejected"}, HistogramVec::exponential(0.00001, 2, 22));
+  static auto webhook_h = Registry::global().histogram(
+      "apiserver_admission_webhook_admission_duration_seconds", "admission webhook call latency (AdmissionReview round trip)",
+      {"name", "operation", "type", "rejected"}, HistogramVec::exponential(0.0001, 2, 18));
+  return webhook ? webhook_h : plugin_h;
+}
+
 ApiError ApiServer::run_admission(AdmissionAttrs& a, bool mutating) {
   std::vector<std::pair<std::string, AdmissionFn>> plugins;
   {
     std::lock_guard<std::mutex> g(mu_);
     plugins = mutating ? mutating_ : validating_;
   }
+  const char* type = mutating ? "admit" : "validate";
   for (auto& p : plugins) {
+    const double t0 = now_seconds();
     ApiError e = p.second(a);
+    admission_latency(false)->observe({p.first, a.operation, type, e ? "true" : "false"}, now_seconds() - t0);
     if (e) {
       if (e.message.find("admission webhook") == std::string::npos && e.reason != "Forbidden")
         e.message = "admission webhook \"" + p.first + "\" denied the request: " + e.message;

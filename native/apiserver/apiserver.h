@@ -30,8 +30,13 @@
 #include "apiserver/selector.h"
 #include "core/http.h"
 #include "core/json.h"
+#include "core/metrics.h"
 
 namespace kf {
+
+// admission latency histograms (in-process plugins / webhooks), apiserver.cc
+std::shared_ptr<HistogramVec> admission_latency(bool webhook);
+
 
 struct UserInfo {
   std::string username = "system:admin";

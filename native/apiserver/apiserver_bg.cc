@@ -473,11 +473,16 @@ ApiError ApiServer::call_webhooks(AdmissionAttrs& a, bool mutating) {
                                    {"oldObject", a.old_object ? *a.old_object : Json()},
                                    {"dryRun", a.dry_run}}}};
       int timeout = static_cast<int>(wh["timeoutSeconds"].as_int(10)) * 1000;
+      const double t0 = now_seconds();
       HttpResult r = http_request("POST", url, review.dump(), {{"Content-Type", "application/json"}}, timeout,
                                   ca_b64.empty() ? nullptr : &tls);
       bool fail_closed = wh["failurePolicy"].as_string_or("Fail") != "Ignore";
       Json resp;
-      if (!r.ok() || !Json::try_parse(r.body, resp)) {
+      const bool parsed = r.ok() && Json::try_parse(r.body, resp);
+      const bool rejected = !parsed ? fail_closed : !resp.at_path({"response", "allowed"}).as_bool();
+      admission_latency(true)->observe({wh["name"].as_string(), a.operation, mutating ? "admit" : "validate",
+                                        rejected ? "true" : "false"}, now_seconds() - t0);
+      if (!parsed) {
         if (fail_closed)
           return ApiError::Internal("Internal error occurred: failed calling webhook \"" + wh["name"].as_string() +
                                     "\": " + (r.error.empty() ? "HTTP " + std::to_string(r.status) : r.error));

@@ -360,3 +360,18 @@ def test_cold_start_phases_recorded_on_notebook_and_exported(c, cluster):
     assert count and float(count[0].split()[-1]) >= 1
     # written once: a pod restart does not rewrite it
     c.delete(NB, "Notebook", "cs1", "e2e")
+
+
+def test_admission_latency_histograms(c, cluster):
+    """admission latency per in-process plugin (kube-apiserver's metric names), with the
+    operation, admit/validate and rejected labels; GPU pods went through placement/readiness plugins."""
+    with urllib.request.urlopen(cluster.url + "/metrics", timeout=5) as r:
+        text = r.read().decode()
+    name = "apiserver_admission_controller_admission_duration_seconds_count"
+    rows = [ln for ln in text.splitlines() if ln.startswith(name + "{")]
+    assert rows, "no admission histogram"
+    plugins = {ln.split('name="')[1].split('"')[0] for ln in rows}
+    assert len(plugins) >= 2, plugins
+    creates = [ln for ln in rows if 'operation="CREATE"' in ln and 'type="admit"' in ln and 'rejected="false"' in ln]
+    assert creates and max(float(ln.split()[-1]) for ln in creates) >= 1
+    assert "# TYPE apiserver_admission_controller_admission_duration_seconds histogram" in text

@@ -115,6 +115,13 @@ def test_pvcviewer_webhook_over_rest(split):
         cl.client.create({"apiVersion": "kubeflow.org/v1alpha1", "kind": "PVCViewer", "metadata": {"name": "v", "namespace": "remote"},
                           "spec": {"pvc": "", "rwoScheduling": False}})
     assert "PVC name must be specified" in str(e.value.body)
+    # the API server timed the AdmissionReview round trips, the rejection labelled so
+    with urllib.request.urlopen(cl.url + "/metrics", timeout=5) as r:
+        text = r.read().decode()
+    rows = [ln for ln in text.splitlines()
+            if ln.startswith("apiserver_admission_webhook_admission_duration_seconds_count{")]
+    assert any('rejected="true"' in ln and 'operation="CREATE"' in ln for ln in rows), rows
+    assert any('rejected="false"' in ln for ln in rows), rows
 
 
 def test_kfam_over_rest(split):
