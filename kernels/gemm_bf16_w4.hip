@@ -273,6 +273,13 @@ void gemm_nt_256w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, _
   if (DIAG) t_loop1 = stamp();
   // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  // pin every accumulator behind the padding: the MFMAs are asm, so the compiler treats their AGPR
+  // results as ready at issue and would otherwise hoist v_accvgpr_read of the last writes above the
+  // s_nops (it did in the bias build of w4d: stale sums). The empty asm "redefines" each one here.
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) asm volatile("" : "+a"(acc[i][n]));
 
   // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
   // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
