@@ -6,6 +6,8 @@ Webhook cases port pvcviewer_controller_test.go:69-138.
 """
 import json
 import os
+import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -25,9 +27,21 @@ def c(cluster):
     return cl
 
 
-def _get(url):
-    with urllib.request.urlopen(url, timeout=5) as r:
-        return json.loads(r.read())
+def _get(url, timeout=15.0):
+    """GET through the gateway. The pods carry no readiness probe (as in the reference manifests),
+    so Ready can precede the server's bind by a few ms: a 502/503 or refused connection is retried."""
+    deadline = time.time() + timeout
+    while True:
+        try:
+            with urllib.request.urlopen(url, timeout=5) as r:
+                return json.loads(r.read())
+        except urllib.error.HTTPError as e:
+            if e.code not in (502, 503) or time.time() > deadline:
+                raise
+        except urllib.error.URLError:
+            if time.time() > deadline:
+                raise
+        time.sleep(0.1)
 
 
 def test_tensorboard_serves_pvc_logs(c, cluster):
