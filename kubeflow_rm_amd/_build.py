@@ -89,8 +89,29 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     if force or not _newer(KERNEL_LIB, objs):
         tmp = KERNEL_LIB.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)])
+        check_kernel_library(tmp)
         os.replace(tmp, KERNEL_LIB)
     return KERNEL_LIB
+
+
+# kernel families every production library must carry (kernel-descriptor symbols of the embedded
+# gfx950 code object). A host compile that drops a template's kernel stubs still links and still
+# exits 0, leaving a library whose launches fail at run time: refuse to install it.
+REQUIRED_KERNELS = ("gemm_nt_256w4", "gemm_nt_256p", "gemm_nt_128", "norm_fwd_wave", "ln_bwd_dx_wave",
+                    "allreduce_oneshot")
+
+
+def kernel_descriptors(lib: Path) -> set[str]:
+    import re
+    data = Path(lib).read_bytes()
+    return {m.group(1).decode() for m in re.finditer(rb"([A-Za-z0-9_]+)\.kd\x00", data)}
+
+
+def check_kernel_library(lib: Path) -> None:
+    names = kernel_descriptors(lib)
+    missing = [k for k in REQUIRED_KERNELS if not any(k in n for n in names)]
+    if missing:
+        raise RuntimeError(f"{lib}: no gfx950 kernel descriptors for {missing} ({len(names)} kernels found)")
 
 
 SANITIZER_CXX = "/opt/rocm/lib/llvm/bin/clang++"
