@@ -1284,7 +1284,11 @@ void Kubelet::register_telemetry_metrics() {
       std::vector<std::string>{"gpu", "cause"}, [rows]() {
         std::vector<std::pair<Labels, double>> out;
         for (const auto& r : rows()) {
-          if (!r.has_prev || r.t.accumulation_counter <= r.prev.accumulation_counter) continue;
+          // counters restart with the driver: only a forward step of every accumulator is a sample
+          if (!r.has_prev || r.t.accumulation_counter <= r.prev.accumulation_counter ||
+              r.t.ppt_residency_acc < r.prev.ppt_residency_acc ||
+              r.t.thermal_residency_acc < r.prev.thermal_residency_acc)
+            continue;
           const double dt = static_cast<double>(r.t.accumulation_counter - r.prev.accumulation_counter);
           out.push_back({{std::to_string(r.gpu), "power"},
                          static_cast<double>(r.t.ppt_residency_acc - r.prev.ppt_residency_acc) / dt});
