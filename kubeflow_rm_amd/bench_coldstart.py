@@ -59,6 +59,37 @@ SERVERS = {
 }
 
 
+def _wait_ready(c, name: str, namespace: str, timeout: float) -> dict:
+    """Poll the Notebook every 5 ms until readyReplicas == 1. Every ~100 ms also look at the pod: an
+    init container (the GPU readiness op) that terminated non-zero, or a main container that exited,
+    fails the run at once with its termination message instead of after the whole timeout."""
+    deadline = time.time() + timeout
+    next_pod_check = time.time() + 0.1
+    while True:
+        try:
+            o = c.get("kubeflow.org/v1", "Notebook", name, namespace)
+            if (o.get("status") or {}).get("readyReplicas") == 1:
+                return o
+        except Exception:  # noqa: BLE001 - not created yet / transient
+            pass
+        now = time.time()
+        if now >= next_pod_check:
+            next_pod_check = now + 0.1
+            try:
+                pod = c.get("v1", "Pod", f"{name}-0", namespace)
+            except Exception:  # noqa: BLE001
+                pod = None
+            st = (pod or {}).get("status") or {}
+            for cs in (st.get("initContainerStatuses") or []) + (st.get("containerStatuses") or []):
+                term = (cs.get("state") or {}).get("terminated") or {}
+                if term and term.get("exitCode", 0) != 0:
+                    raise RuntimeError(f"{name}: container {cs.get('name')} exited {term.get('exitCode')}: "
+                                       f"{(term.get('message') or '')[:400]}")
+        if now > deadline:
+            raise TimeoutError(f"{name}: not Ready within {timeout:.0f} s")
+        time.sleep(0.005)
+
+
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
                        readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
                        settle_s: float = 0.5, server: str = "stub") -> dict:
@@ -90,9 +121,7 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                   "spec": {"template": {"spec": {"containers": [ctr]}}}}
             t0 = time.time()
             c.create(nb)
-            obj = c.wait_for("kubeflow.org/v1", "Notebook", name, namespace,
-                             lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout,
-                             interval=0.005)
+            obj = _wait_ready(c, name, namespace, timeout)
             t1 = time.time()
             pod = c.get("v1", "Pod", f"{name}-0", namespace)
             t_sched = _cond(pod, "PodScheduled")
