@@ -18,7 +18,9 @@ Cold start (rank 0, after the timed region, while the other ranks wait on a CPU-
 their GPU memory released): ``--coldstart-runs`` (default 10) Notebook CREATE -> Ready runs of ONE
 notebook requesting all N GPUs, through the native control plane (process pods: no container
 runtime), with the in-pod readiness op on the allocated GPUs (N >= 2: one-shot peer all-reduce over
-xGMI). Reported with p50 / p90 and the per-phase p50 breakdown.
+xGMI). Reported with p50 / p90 and the per-phase p50 breakdown. Then the control-plane latencies of
+BASELINE configs 3 and 5 (Profile with GPU quota ready; TensorBoard and PVCViewer ready) on the same
+native control plane.
 """
 from __future__ import annotations
 
@@ -172,6 +174,11 @@ def main() -> int:
                     extra["cold_start_torch_ready_phases_p50_s"] = ct.get("phases_p50_s")
             except Exception as e:  # reported, never fatal for the GEMM number
                 extra["cold_start_error"] = f"{type(e).__name__}: {e}"
+            try:  # BASELINE configs 3 and 5: Profile with GPU quota, TensorBoard + PVCViewer on a PVC
+                from kubeflow_rm_amd.bench_coldstart import measure_control_plane
+                extra["control_plane"] = measure_control_plane(runs=5)
+            except Exception as e:  # reported, never fatal for the GEMM number
+                extra["control_plane_error"] = f"{type(e).__name__}: {e}"
         if world > 1:
             dist.barrier(group=cpu_group)
 

@@ -181,6 +181,53 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     return res
 
 
+def measure_control_plane(runs: int = 5, gpus: int | None = None, timeout: float = 30.0) -> dict:
+    """BASELINE configs 3 and 5 on the same native control plane (process pods), p50 over ``runs``:
+
+    * profile_ready_s: Profile CREATE (owner + ``amd.com/gpu`` / HBM quota) -> namespace, owner
+      RoleBinding, editor/viewer ServiceAccounts, AuthorizationPolicy and ResourceQuota all present.
+    * tensorboard_ready_s: Tensorboard CREATE (pvc:// logspath) -> ``status.readyReplicas == 1``.
+    * pvcviewer_ready_s: PVCViewer CREATE on the same PVC -> ``status.ready``.
+    """
+    def p50(xs):
+        return _pct(xs, 0.5) if xs else None
+
+    prof, tb, pv = [], [], []
+    with LocalCluster(gpus=gpus) as cl:
+        c = cl.client
+        for i in range(runs):
+            name = f"cp-{i}"
+            t0 = time.time()
+            c.create({"apiVersion": "kubeflow.org/v1", "kind": "Profile", "metadata": {"name": name},
+                      "spec": {"owner": {"kind": "User", "name": f"{name}@example.com"},
+                               "resourceQuotaSpec": {"hard": {"amd.com/gpu": "8", "amd.com/gpu-memory": "2304Gi"}}}})
+            for av, kind, obj in [("v1", "Namespace", None), ("rbac.authorization.k8s.io/v1", "RoleBinding", "namespaceAdmin"),
+                                  ("v1", "ServiceAccount", "default-editor"), ("v1", "ServiceAccount", "default-viewer"),
+                                  ("security.istio.io/v1beta1", "AuthorizationPolicy", "ns-owner-access-istio"),
+                                  ("v1", "ResourceQuota", "kf-resource-quota")]:
+                if obj is None:
+                    c.wait_for(av, kind, name, None, lambda o: True, timeout=timeout, interval=0.005)
+                else:
+                    c.wait_for(av, kind, obj, name, lambda o: True, timeout=timeout, interval=0.005)
+            prof.append(time.time() - t0)
+            c.create({"apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": "logs", "namespace": name},
+                      "spec": {"accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}})
+            t0 = time.time()
+            c.create({"apiVersion": "tensorboard.kubeflow.org/v1alpha1", "kind": "Tensorboard",
+                      "metadata": {"name": "tb", "namespace": name}, "spec": {"logspath": "pvc://logs/"}})
+            c.wait_for("tensorboard.kubeflow.org/v1alpha1", "Tensorboard", "tb", name,
+                       lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout, interval=0.005)
+            tb.append(time.time() - t0)
+            t0 = time.time()
+            c.create({"apiVersion": "kubeflow.org/v1alpha1", "kind": "PVCViewer", "metadata": {"name": "viewer", "namespace": name},
+                      "spec": {"pvc": "logs", "rwoScheduling": True}})
+            c.wait_for("kubeflow.org/v1alpha1", "PVCViewer", "viewer", name,
+                       lambda o: (o.get("status") or {}).get("ready") is True, timeout=timeout, interval=0.005)
+            pv.append(time.time() - t0)
+    return {"runs": runs, "profile_ready_p50_s": p50(prof), "tensorboard_ready_p50_s": p50(tb),
+            "pvcviewer_ready_p50_s": p50(pv), "note": "process pods (no container runtime)"}
+
+
 def main() -> int:
     p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     p.add_argument("--runs", type=int, default=5)

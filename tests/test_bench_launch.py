@@ -59,3 +59,13 @@ def test_launch_cli_runs_program_per_rank(tmp_path):
     ranks = [json.loads((tmp_path / f"rank{r}").read_text()) for r in range(3)]
     # the pod's injected rendezvous is used as is
     assert all(x["MASTER_ADDR"] == "127.0.0.9" and x["MASTER_PORT"] == "29999" for x in ranks)
+
+
+def test_control_plane_latencies_measured():
+    """BASELINE configs 3 / 5 (bench.py extra): Profile with GPU quota, TensorBoard, PVCViewer ready."""
+    from tests.conftest import _ensure_native
+    _ensure_native()
+    from kubeflow_rm_amd.bench_coldstart import measure_control_plane
+    r = measure_control_plane(runs=2)
+    for k in ("profile_ready_p50_s", "tensorboard_ready_p50_s", "pvcviewer_ready_p50_s"):
+        assert r[k] is not None and 0 < r[k] < 30, r
