@@ -8,6 +8,9 @@
 #include <spawn.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/syscall.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -306,6 +309,61 @@ void Kubelet::start() {
     set_thread_name("kubelet-hb");
     heartbeat_loop();
   });
+  epfd_ = ::epoll_create1(EPOLL_CLOEXEC);
+  wake_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  if (epfd_ >= 0 && wake_fd_ >= 0) {
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = wake_fd_;
+    ::epoll_ctl(epfd_, EPOLL_CTL_ADD, wake_fd_, &ev);
+    exit_watch_ = std::thread([this] {
+      set_thread_name("kubelet-exits");
+      exit_watch_loop();
+    });
+  }
+}
+
+void Kubelet::watch_exit(pid_t pid, const std::string& ns, const std::string& name) {
+  if (epfd_ < 0 || pid <= 0) return;
+#ifdef SYS_pidfd_open
+  const int pfd = static_cast<int>(::syscall(SYS_pidfd_open, pid, 0));
+#else
+  const int pfd = -1;
+#endif
+  if (pfd < 0) return;  // no pidfd (old kernel): the startup re-sync still notices the exit
+  ::fcntl(pfd, F_SETFD, FD_CLOEXEC);
+  std::lock_guard<std::mutex> g(watch_mu_);
+  watched_[pfd] = {ns, name};
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.fd = pfd;
+  if (::epoll_ctl(epfd_, EPOLL_CTL_ADD, pfd, &ev) != 0) {
+    watched_.erase(pfd);
+    ::close(pfd);
+  }
+}
+
+void Kubelet::exit_watch_loop() {
+  epoll_event evs[32];
+  while (running_) {
+    const int n = ::epoll_wait(epfd_, evs, 32, 1000);
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == wake_fd_) continue;
+      std::pair<std::string, std::string> key;
+      {
+        std::lock_guard<std::mutex> g(watch_mu_);
+        auto it = watched_.find(fd);
+        if (it == watched_.end()) continue;
+        key = it->second;
+        watched_.erase(it);
+        ::epoll_ctl(epfd_, EPOLL_CTL_DEL, fd, nullptr);
+        ::close(fd);
+      }
+      // the pidfd is readable once the process has exited (not reaped: reconcile's waitpid does)
+      if (ctl_) ctl_->enqueue(Request{key.first, key.second});
+    }
+  }
 }
 
 void Kubelet::heartbeat_loop() {
@@ -335,6 +393,19 @@ void Kubelet::stop() {
   }
   if (!running_.exchange(false)) return;
   if (hb_.joinable()) hb_.join();
+  if (wake_fd_ >= 0) {
+    const uint64_t one = 1;
+    (void)!::write(wake_fd_, &one, sizeof one);
+  }
+  if (exit_watch_.joinable()) exit_watch_.join();
+  {
+    std::lock_guard<std::mutex> g(watch_mu_);
+    for (auto& kv : watched_) ::close(kv.first);
+    watched_.clear();
+  }
+  if (epfd_ >= 0) ::close(epfd_);
+  if (wake_fd_ >= 0) ::close(wake_fd_);
+  epfd_ = wake_fd_ = -1;
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : pods_) terminate_pod(*kv.second, 0);
 }
@@ -798,6 +869,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     cr.state = "running";
     cr.reason = "";
     cr.started_at = ms_now();
+    watch_exit(pid, r.ns, r.name);
     cr.run_started = now_seconds();
     cr.ready = false;
     cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
@@ -984,6 +1056,12 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       if (cr.state == "waiting") {
         if (now_seconds() >= cr.backoff_until) {
           start_container(cr);
+          // no startup / readiness probe: Ready as soon as it runs (Kubernetes' default Success),
+          // in this pass rather than the next re-sync
+          if (cr.state == "running" && !c["startupProbe"].is_object() && !c["readinessProbe"].is_object()) {
+            cr.started_probe_ok = true;
+            cr.ready = true;
+          }
           next_wake = std::min(next_wake, kStartupPoll);
         } else {
           next_wake = std::min(next_wake, cr.backoff_until - now_seconds());

@@ -120,6 +120,15 @@ class Kubelet {
   std::shared_ptr<Controller> ctl_;
   std::atomic<bool> running_{false};
   std::thread hb_;
+  // container exits wake the pod's reconcile at once (pidfd + epoll; PLEG without the relist
+  // latency): the init container's exit gates Initialized, a crash needs a restart
+  void watch_exit(pid_t pid, const std::string& ns, const std::string& name);
+  void exit_watch_loop();
+  int epfd_ = -1;
+  int wake_fd_ = -1;
+  std::mutex watch_mu_;
+  std::map<int, std::pair<std::string, std::string>> watched_;  // pidfd -> pod ns/name
+  std::thread exit_watch_;
 };
 
 class Gateway {
