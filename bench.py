@@ -39,6 +39,9 @@ def parse_args():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--prewarm-s", type=float, default=float(os.environ.get("KFAMD_BENCH_PREWARM_S", "1.0")),
+                   help="untimed GEMM time before the W warmup steps, so the timed steps run at the "
+                        "sustained clock rather than on the DVFS ramp from idle (0 disables)")
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--n", type=int, default=8192)
     p.add_argument("--k", type=int, default=8192)
@@ -96,6 +99,13 @@ def main() -> int:
     def step():
         ops.gemm_nt(a, b, out=c)
 
+    # DVFS: an idle MI355X needs a few hundred ms of load to settle its GFX clock; without this a
+    # short K measures the ramp (20 steps = 16 ms), not the kernel
+    t_pre = time.perf_counter()
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
 
@@ -190,6 +200,7 @@ def main() -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm_s": args.prewarm_s,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
