@@ -159,11 +159,13 @@ def test_ipc_oneshot_timeout_is_fatal_not_silent():
     assert r0["raised"] is True and r0["nan"] is True and r0.get("refuses_after") is True, r0
 
 
-def test_ipc_oneshot_two_ranks_as_processes():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_oneshot_ranks_as_processes(world):
     """torch.distributed ranks (separate processes) over HIP IPC-mapped buffers; on the 1-GPU box
-    both processes share the device, exercising registration, handle exchange and the barrier."""
+    all processes share the device, exercising registration, handle exchange and the barrier."""
     from kubeflow_rm_amd.parallel.launch import spawn
-    res = spawn(_ipc_worker, 2, timeout=180)
+    res = spawn(_ipc_worker, world, timeout=180)
+    assert len(res) == world
     for r in res:
         assert r["timed_out"] is False, r
         assert r["worst"] == 0.0, r
