@@ -147,6 +147,9 @@ struct Kubelet::PodRuntime {
   bool terminating = false;
   double kill_deadline = 0;
   bool announced_kill = false;
+  // held by a reconcile pass for this pod, and by stop() around terminate_pod: the workqueue keeps
+  // one worker per key, stop() comes from outside it
+  std::mutex op_mu;
 };
 
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)), cfg_(std::move(cfg)) {
@@ -163,6 +166,15 @@ Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)
       for (const auto& r : recipes_.as_array()) merged.push_back(r);
       recipes_ = merged;
     }
+  }
+  for (const auto& r : recipes_.as_array()) recipe_re_.emplace_back(r["match"].as_string(), std::regex::icase);
+  epfd_ = ::epoll_create1(EPOLL_CLOEXEC);
+  wake_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  if (epfd_ >= 0 && wake_fd_ >= 0) {
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = wake_fd_;
+    ::epoll_ctl(epfd_, EPOLL_CTL_ADD, wake_fd_, &ev);
   }
   if (cfg_.root_dir.empty()) cfg_.root_dir = "/tmp/kflite-" + random_hex(4);
   make_dirs(cfg_.root_dir + "/pods");
@@ -197,7 +209,12 @@ int Kubelet::alloc_rdzv_port() {
   return 29500;  // nothing free in the range: fall back to torch's default and let it report
 }
 
-Kubelet::~Kubelet() { stop(); }
+Kubelet::~Kubelet() {
+  stop();
+  for (auto& kv : watched_) ::close(kv.first);
+  if (epfd_ >= 0) ::close(epfd_);
+  if (wake_fd_ >= 0) ::close(wake_fd_);
+}
 
 std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::string* why) const {
   std::vector<std::string> cmd, args;
@@ -216,9 +233,10 @@ std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::strin
   }
   keys.push_back(container["image"].as_string());
   for (const auto& key : keys) {
-    for (const auto& r : recipes_.as_array()) {
-      std::regex re(r["match"].as_string(), std::regex::icase);
-      if (!std::regex_search(key, re)) continue;
+    const auto& recipes = recipes_.as_array();
+    for (size_t i = 0; i < recipes.size(); ++i) {
+      const Json& r = recipes[i];
+      if (!std::regex_search(key, recipe_re_[i])) continue;
       std::vector<std::string> out;
       for (const auto& a : r["argv"].as_array()) {
         std::string s = replace_all(a.as_string(), "{python}", cfg_.python);
@@ -309,13 +327,7 @@ void Kubelet::start() {
     set_thread_name("kubelet-hb");
     heartbeat_loop();
   });
-  epfd_ = ::epoll_create1(EPOLL_CLOEXEC);
-  wake_fd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
   if (epfd_ >= 0 && wake_fd_ >= 0) {
-    epoll_event ev{};
-    ev.events = EPOLLIN;
-    ev.data.fd = wake_fd_;
-    ::epoll_ctl(epfd_, EPOLL_CTL_ADD, wake_fd_, &ev);
     exit_watch_ = std::thread([this] {
       set_thread_name("kubelet-exits");
       exit_watch_loop();
@@ -392,22 +404,24 @@ void Kubelet::stop() {
     metrics_registered_ = false;
   }
   if (!running_.exchange(false)) return;
+  stopping_ = true;
   if (hb_.joinable()) hb_.join();
   if (wake_fd_ >= 0) {
     const uint64_t one = 1;
     (void)!::write(wake_fd_, &one, sizeof one);
   }
   if (exit_watch_.joinable()) exit_watch_.join();
+  // the epoll set and eventfd stay open until the destructor: a reconcile still in flight may
+  // register one more pidfd
+  std::vector<std::shared_ptr<PodRuntime>> all;
   {
-    std::lock_guard<std::mutex> g(watch_mu_);
-    for (auto& kv : watched_) ::close(kv.first);
-    watched_.clear();
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : pods_) all.push_back(kv.second);
   }
-  if (epfd_ >= 0) ::close(epfd_);
-  if (wake_fd_ >= 0) ::close(wake_fd_);
-  epfd_ = wake_fd_ = -1;
-  std::lock_guard<std::mutex> g(mu_);
-  for (auto& kv : pods_) terminate_pod(*kv.second, 0);
+  for (auto& rt : all) {
+    std::lock_guard<std::mutex> pl(rt->op_mu);
+    terminate_pod(*rt, 0);
+  }
 }
 
 // ---- process management ---------------------------------------------------------------------------
@@ -553,6 +567,7 @@ bool Kubelet::read_logs(const std::string& ns, const std::string& pod, const std
 
 // ---- reconcile ---------------------------------------------------------------------------------
 Result Kubelet::reconcile(const Request& r, std::string* err) {
+  if (stopping_) return {};
   Json pod;
   ApiError e = c_->get("v1", "Pod", r.ns, r.name, pod);
   std::shared_ptr<PodRuntime> rt;
@@ -565,6 +580,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       if (e.code == 404 || (!e && pod.str_at({"metadata", "uid"}) != k->second)) {
         // pod object is gone (or replaced by a new incarnation): tear the old sandbox down
         if (rt) {
+          std::lock_guard<std::mutex> pl(rt->op_mu);
           terminate_pod(*rt, 0);
           alloc_->release(rt->uid);
           rdzv_ports_.erase(rt->rdzv_port);
@@ -582,6 +598,11 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     return {};
   }
   if (pod.at_path({"spec", "nodeName"}).as_string() != cfg_.node_name) return {};
+  std::unique_lock<std::mutex> pod_lock;
+  if (rt) {
+    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
+    if (stopping_) return {};
+  }
   const std::string uid = pod.str_at({"metadata", "uid"});
   const std::string restart_policy = pod.at_path({"spec", "restartPolicy"}).as_string_or("Always");
 
@@ -701,6 +722,10 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     std::lock_guard<std::mutex> g(mu_);
     pods_[uid] = rt;
     key_to_uid_[r.ns + "/" + r.name] = uid;
+  }
+  if (!pod_lock.owns_lock()) {
+    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
+    if (stopping_) return {};
   }
 
   if (!rt->gpu_ok) {

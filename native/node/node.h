@@ -24,6 +24,7 @@
 #include <set>
 #include <memory>
 #include <mutex>
+#include <regex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -110,6 +111,7 @@ class Kubelet {
   KubeletConfig cfg_;
   std::unique_ptr<GpuAllocator> alloc_;
   Json recipes_;
+  std::vector<std::regex> recipe_re_;  // recipes_[i]["match"], compiled once (std::regex construction is not thread-safe)
   std::mutex mu_;
   std::map<std::string, std::shared_ptr<PodRuntime>> pods_;  // uid -> runtime
   std::map<std::string, std::string> key_to_uid_;            // ns/name -> uid
@@ -119,6 +121,7 @@ class Kubelet {
   std::unique_ptr<EventRecorder> rec_;
   std::shared_ptr<Controller> ctl_;
   std::atomic<bool> running_{false};
+  std::atomic<bool> stopping_{false};
   std::thread hb_;
   // container exits wake the pod's reconcile at once (pidfd + epoll; PLEG without the relist
   // latency): the init container's exit gates Initialized, a crash needs a restart

@@ -42,9 +42,11 @@ def test_notebook_to_statefulset_service_and_ready(c, cluster):
     sts = c.wait_for("apps/v1", "StatefulSet", "nb1", "e2e", lambda o: True, timeout=10)
     ref = sts["metadata"]["ownerReferences"][0]
     assert ref["kind"] == "Notebook" and ref["name"] == "nb1" and ref["controller"] is True
-    svc = c.get("v1", "Service", "nb1", "e2e")
+    # the reconciler creates the StatefulSet, then the Service, then the VirtualService
+    svc = c.wait_for("v1", "Service", "nb1", "e2e", lambda o: True, timeout=10)
     assert svc["spec"]["ports"][0]["targetPort"] == 8888
-    vs = c.get("networking.istio.io/v1alpha3", "VirtualService", "notebook-e2e-nb1", "e2e")
+    vs = c.wait_for("networking.istio.io/v1alpha3", "VirtualService", "notebook-e2e-nb1", "e2e", lambda o: True,
+                    timeout=10)
     assert vs["spec"]["http"][0]["match"][0]["uri"]["prefix"] == "/notebook/e2e/nb1/"
     nb = c.wait_for(NB, "Notebook", "nb1", "e2e", _ready, timeout=30)
     assert "running" in nb["status"]["containerState"]
