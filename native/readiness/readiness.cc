@@ -180,6 +180,7 @@ bool gemm_check(int dev, const Args& a, DevBuffers& buf, Json& out) {
   HIP_OK(hipSetDevice(dev));
   HIP_OK(hipStreamCreate(&buf.s));
   hipStream_t s = buf.s;
+  lap("stream_ms");
   const size_t na = (size_t)a.m * a.k, nb = (size_t)a.n * a.k, nc = (size_t)a.m * a.n;
   buf.na = na;
   buf.nb = nb;
@@ -187,10 +188,11 @@ bool gemm_check(int dev, const Args& a, DevBuffers& buf, Json& out) {
   HIP_OK(hipMalloc(&buf.A, na * 2));
   HIP_OK(hipMalloc(&buf.B, nb * 2));
   HIP_OK(hipMalloc(&buf.C, nc * 2));
+  lap("alloc_ms");
   __bf16 *A = buf.A, *B = buf.B, *C = buf.C;
   hipLaunchKernelGGL(fill_uniform, dim3(1024), dim3(256), 0, s, A, na, 1234u + dev);
   hipLaunchKernelGGL(fill_uniform, dim3(1024), dim3(256), 0, s, B, nb, 4321u + dev);
-  lap("alloc_fill_ms");
+  lap("fill_ms");
   auto run = [&]() {
     return kfamd_gemm_nt_bf16(A, B, C, nullptr, nullptr, a.m, a.n, a.k, 1, a.k, a.k, a.n, 0, 0, 0, 0, 0, 1.0f, 0, s);
   };
@@ -299,13 +301,23 @@ bool ln_check(int dev, const Args& a, DevBuffers& buf, Json& out) {
     std::memcpy(&r, &bits, 4);
     return r;
   };
+  // copies on the op's own stream: the first synchronous hipMemcpy would bring up the null
+  // stream's queue as well (about 8 ms of a cold start)
+  std::vector<uint16_t> hx1(a.ln_hidden), hy1(a.ln_hidden);
+  const size_t last = (size_t)(a.ln_rows - 1) * a.ln_hidden, rb = (size_t)a.ln_hidden * 2;
+  HIP_OK(hipMemcpyAsync(hg.data(), g, rb, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(hb.data(), b, rb, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(hx.data(), x, rb, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(hy.data(), y, rb, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(hx1.data(), x + last, rb, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(hy1.data(), y + last, rb, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
-  HIP_OK(hipMemcpy(hg.data(), g, a.ln_hidden * 2, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(hb.data(), b, a.ln_hidden * 2, hipMemcpyDeviceToHost));
   double max_err = 0;
-  for (int row : {0, a.ln_rows - 1}) {
-    HIP_OK(hipMemcpy(hx.data(), x + (size_t)row * a.ln_hidden, a.ln_hidden * 2, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(hy.data(), y + (size_t)row * a.ln_hidden, a.ln_hidden * 2, hipMemcpyDeviceToHost));
+  for (int which = 0; which < 2; ++which) {
+    if (which == 1) {
+      hx.swap(hx1);
+      hy.swap(hy1);
+    }
     double mean = 0, var = 0;
     for (int i = 0; i < a.ln_hidden; ++i) mean += f(hx[i]);
     mean /= a.ln_hidden;
