@@ -2,10 +2,12 @@
 // backend calls with the CSRF double-submit header, exponential-backoff poller (1 s -> 8 s, reset
 // when the data changes), namespace selection bound to the central dashboard's iframe protocol
 // (library.js: parent-connected / iframe-connected / namespace-selected / all-namespaces), and the
-// library's components: resource table (sortable, filterable, per-row actions, the same data-cy
-// hooks as kubeflow-common-lib's resource-table), status icons (lib-status-icon semantics),
-// conditions table, logs viewer, form validators (DNS-1123 names, CPU / memory quantities, limit
-// >= request), snack bar, details dialog with tabs, YAML view.
+// library's components: resource table (sortable; chip filter: every term must match, "text"
+// against any column, "column:value" against one; paginated 10 / 20 / 50; per-row actions; the
+// same data-cy hooks as kubeflow-common-lib's resource-table; date-time and memory cells),
+// status icons (lib-status-icon semantics), conditions table, logs viewer, form validators
+// (DNS-1123 names, CPU / memory quantities, limit >= request), confirm dialog with its applying /
+// error states, snack bar, details dialog with tabs, YAML view.
 //
 // Every component has a pure render function (string in, string out) so node can unit-test it
 // without a DOM; the DOM classes only bind those strings to elements and events.
@@ -148,7 +150,37 @@
   // escaped value), sortable (default true)}]; cfg.actions: [{name, label, enabled(row)}]
   // state: {sortCol, sortDir: 1|-1, filter}. Default order: the "Name" column ascending (the
   // reference tables' default sort).
+  // column kinds: "date" (lib DateTimeValue: "5 minutes ago", full time on hover, sorted by time)
+  // and "memory" (MemoryValue: a quantity shown in binary units, sorted by bytes)
   function colValue(c, row) { return c.value ? c.value(row) : row[c.field || c.title.toLowerCase()]; }
+  function sortKey(c, row) {
+    const v = colValue(c, row);
+    if (c.kind === "date") { const t = Date.parse(v); return isNaN(t) ? -Infinity : t; }
+    if (c.kind === "memory") { try { return quantityToScalar(v); } catch (e) { return NaN; } }
+    return v;
+  }
+  function viewText(c, row) {
+    const v = colValue(c, row);
+    if (c.kind === "memory") { try { return formatBytes(quantityToScalar(v)); } catch (e) { return String(v); } }
+    return v == null ? "" : String(v);
+  }
+  // the filter box holds comma-separated chips: "ready" matches any column, "status:ready" only
+  // the Status column (table.component.ts filterPredicate: all chips AND-ed)
+  function parseFilter(text) {
+    return String(text || "").split(",").map((t) => t.trim().toLowerCase()).filter(Boolean).map((t) => {
+      const i = t.indexOf(":");
+      return i > 0 && i < t.length - 1 ? { column: t.slice(0, i), value: t.slice(i + 1) } : t;
+    });
+  }
+  function cellMatches(c, row, needle) {
+    if (viewText(c, row).toLowerCase().includes(needle)) return true;
+    return c.kind === "date" && !!colValue(c, row) && timeAgo(colValue(c, row)).toLowerCase().includes(needle);
+  }
+  function rowMatches(cols, row, terms) {
+    return terms.every((t) => (typeof t === "string"
+      ? cols.some((c) => cellMatches(c, row, t))
+      : cols.some((c) => c.title.toLowerCase() === t.column && cellMatches(c, row, t.value))));
+  }
   function sortedRows(cfg, rows, state) {
     state = state || {};
     const cols = cfg.columns;
@@ -156,12 +188,12 @@
     if (idx === undefined || idx === null) idx = cols.findIndex((c) => c.title === "Name");
     const dir = state.sortDir || 1;
     let out = rows.slice();
-    const f = (state.filter || "").trim().toLowerCase();
-    if (f) out = out.filter((r) => cols.some((c) => String(colValue(c, r) == null ? "" : colValue(c, r)).toLowerCase().includes(f)));
+    const terms = parseFilter(state.filter);
+    if (terms.length) out = out.filter((r) => rowMatches(cols, r, terms));
     if (idx >= 0 && cols[idx] && cols[idx].sortable !== false) {
       const c = cols[idx];
       out.sort((a, b) => {
-        const x = colValue(c, a), y = colValue(c, b);
+        const x = sortKey(c, a), y = sortKey(c, b);
         const nx = typeof x === "number" ? x : NaN, ny = typeof y === "number" ? y : NaN;
         const r = !isNaN(nx) && !isNaN(ny) ? nx - ny : String(x == null ? "" : x).localeCompare(String(y == null ? "" : y));
         return r * dir;
@@ -169,9 +201,25 @@
     }
     return out;
   }
+  // mat-paginator: page sizes 10 / 20 / 50 (default 50), "1 – 10 of 23"
+  const PAGE_SIZES = [10, 20, 50];
+  function paginate(total, page, size) {
+    size = PAGE_SIZES.includes(size) ? size : 50;
+    const pages = Math.max(1, Math.ceil(total / size));
+    page = Math.min(Math.max(0, page || 0), pages - 1);
+    const start = page * size, end = Math.min(total, start + size);
+    return { page, size, pages, start, end, label: total ? `${start + 1} – ${end} of ${total}` : "0 of 0" };
+  }
+  function renderCell(c, r) {
+    if (c.html) return c.html(r);
+    if (c.kind === "date") return dateTimeHtml(colValue(c, r));
+    return esc(viewText(c, r));
+  }
   function renderTable(cfg, rows, state) {
     state = state || {};
-    const view = sortedRows(cfg, rows, state);
+    const all = sortedRows(cfg, rows, state);
+    const pg = paginate(all.length, state.page, state.pageSize);
+    const view = all.slice(pg.start, pg.end);
     const sortIdx = state.sortCol === undefined || state.sortCol === null ? cfg.columns.findIndex((c) => c.title === "Name") : state.sortCol;
     const head = cfg.columns.map((c, i) => {
       const arrow = i === sortIdx ? ((state.sortDir || 1) > 0 ? " &#9650;" : " &#9660;") : "";
@@ -179,7 +227,7 @@
     }).join("") + (cfg.actions && cfg.actions.length ? "<th></th>" : "");
     const body = view.map((r) => {
       const key = esc(cfg.key ? cfg.key(r) : (r.namespace ? r.namespace + "/" : "") + r.name);
-      const cells = cfg.columns.map((c) => `<td data-cy-resource-table-row="${esc(c.title)}">${c.html ? c.html(r) : esc(colValue(c, r))}</td>`).join("");
+      const cells = cfg.columns.map((c) => `<td data-cy-resource-table-row="${esc(c.title)}">${renderCell(c, r)}</td>`).join("");
       const acts = (cfg.actions || []).map((a) => {
         const on = a.enabled ? a.enabled(r) : true;
         return `<button data-action="${esc(a.name)}" data-key="${key}"${on ? "" : " disabled"}>${esc(typeof a.label === "function" ? a.label(r) : a.label)}</button>`;
@@ -187,13 +235,30 @@
       return `<tr data-key="${key}">${cells}${cfg.actions && cfg.actions.length ? `<td class="actions">${acts}</td>` : ""}</tr>`;
     }).join("");
     const empty = view.length ? "" : `<tr><td colspan="${cfg.columns.length + 1}" class="muted">${esc(cfg.empty || "No resources.")}</td></tr>`;
-    return `<table class="rt"><thead><tr>${head}</tr></thead><tbody>${body}${empty}</tbody></table>`;
+    const pager = all.length > PAGE_SIZES[0] ? `<div class="paginator" data-cy-paginator>` +
+      `<label>Items per page <select data-page-size>${PAGE_SIZES.map((n) => `<option${n === pg.size ? " selected" : ""}>${n}</option>`).join("")}</select></label>` +
+      `<span class="range">${pg.label}</span>` +
+      `<button data-page="prev"${pg.page > 0 ? "" : " disabled"}>&lsaquo;</button><button data-page="next"${pg.page < pg.pages - 1 ? "" : " disabled"}>&rsaquo;</button></div>` : "";
+    return `<table class="rt"><thead><tr>${head}</tr></thead><tbody>${body}${empty}</tbody></table>${pager}`;
   }
   // DOM binding: header click sorts (again: reverse), filter box, action buttons -> cfg.onAction
   class ResourceTable {
     constructor(el, cfg) {
-      this.el = el; this.cfg = cfg; this.rows = []; this.state = { sortCol: null, sortDir: 1, filter: "" };
+      this.el = el; this.cfg = cfg; this.rows = []; this.state = { sortCol: null, sortDir: 1, filter: "", page: 0, pageSize: 50 };
+      el.addEventListener("change", (ev) => {
+        if (ev.target.matches && ev.target.matches("select[data-page-size]")) {
+          this.state.pageSize = Number(ev.target.value);
+          this.state.page = 0;
+          this.render();
+        }
+      });
       el.addEventListener("click", (ev) => {
+        const pb = ev.target.closest("button[data-page]");
+        if (pb) {
+          this.state.page += pb.dataset.page === "next" ? 1 : -1;
+          this.render();
+          return;
+        }
         const th = ev.target.closest("th[data-col]");
         if (th) {
           const i = Number(th.dataset.col);
@@ -216,7 +281,7 @@
         }
       });
     }
-    setFilter(f) { this.state.filter = f; this.render(); }
+    setFilter(f) { this.state.filter = f; this.state.page = 0; this.render(); }
     setRows(rows) { this.rows = rows || []; this.render(); }
     render() { this.el.innerHTML = renderTable(this.cfg, this.rows, this.state); }
   }
@@ -284,6 +349,100 @@
     },
   };
 
+  // ---- quantities and bytes (resource-table MemoryValue) ----------------------------------------
+  // Kubernetes quantity -> number ("500m" -> 0.5, "1Gi" -> 1073741824); unknown suffix throws
+  const QTY_SCALE = { n: 1e-9, u: 1e-6, m: 1e-3, "": 1, k: 1e3, M: 1e6, G: 1e9, T: 1e12, P: 1e15, E: 1e18,
+                      Ki: 2 ** 10, Mi: 2 ** 20, Gi: 2 ** 30, Ti: 2 ** 40, Pi: 2 ** 50, Ei: 2 ** 60 };
+  function quantityToScalar(q) {
+    if (q === undefined || q === null || q === "") return 0;
+    const m = String(q).trim().match(/^([+-]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?)([a-zA-Z]*)$/);
+    if (!m || !(m[2] in QTY_SCALE)) throw new Error(`Unknown quantity ${q}`);
+    return Number(m[1]) * QTY_SCALE[m[2]];
+  }
+  // bytes -> "1.5 Gi" (binary units, one decimal) or "1.6 GB" with si
+  function formatBytes(bytes, si, decimals) {
+    const base = si ? 1000 : 1024, d = decimals === undefined ? 1 : decimals;
+    if (Math.abs(bytes) < base) return `${bytes} B`;
+    const units = si ? ["kB", "MB", "GB", "TB", "PB", "EB"] : ["Ki", "Mi", "Gi", "Ti", "Pi", "Ei"];
+    let u = -1, v = bytes;
+    const r = 10 ** d;
+    do { v /= base; u++; } while (Math.round(Math.abs(v) * r) / r >= base && u < units.length - 1);
+    return `${v.toFixed(d)} ${units[u]}`;
+  }
+
+  // ---- date-time (lib-date-time: distance in words with a suffix, "about" / "almost" dropped) --
+  function timeAgo(date, now) {
+    const t = date instanceof Date ? date.getTime() : Date.parse(date);
+    if (!date || isNaN(t)) return "-";
+    const ref = now === undefined ? Date.now() : typeof now === "number" ? now : now instanceof Date ? now.getTime() : Date.parse(now);
+    const secs = Math.abs(ref - t) / 1000, mins = Math.round(secs / 60);
+    const plural = (n, w) => `${n} ${w}${n === 1 ? "" : "s"}`;
+    let words;
+    if (mins < 1) words = "less than a minute";
+    else if (mins < 45) words = plural(mins, "minute");
+    else if (mins < 90) words = "1 hour";
+    else if (mins < 1440) words = plural(Math.round(mins / 60), "hour");
+    else if (mins < 2520) words = "1 day";
+    else if (mins < 43200) words = plural(Math.round(mins / 1440), "day");
+    else if (mins < 86400) words = plural(Math.round(mins / 43200), "month");
+    else {
+      const a = new Date(Math.min(t, ref)), b = new Date(Math.max(t, ref));
+      let months = (b.getUTCFullYear() - a.getUTCFullYear()) * 12 + b.getUTCMonth() - a.getUTCMonth();
+      if (b.getUTCDate() < a.getUTCDate()) months -= 1;
+      if (months < 12) words = plural(Math.round(mins / 43200), "month");
+      else {
+        const years = Math.floor(months / 12), rest = months % 12;
+        words = rest < 3 ? plural(years, "year") : rest < 9 ? `over ${plural(years, "year")}` : plural(years + 1, "year");
+      }
+    }
+    return ref >= t ? `${words} ago` : `in ${words}`;
+  }
+  // a date cell: relative time, the local and UTC time on hover (the component's popover)
+  function dateTimeHtml(date) {
+    if (!date) return "-";
+    const t = Date.parse(date);
+    const local = isNaN(t) ? String(date) : new Date(t).toString();
+    return `<span class="date-time" data-date="${esc(date)}" title="Local: ${esc(local)}&#10;UTC: ${esc(date)}">${esc(timeAgo(date))}</span>`;
+  }
+
+  // ---- confirm dialog (lib-confirm-dialog) -------------------------------------------------------
+  // cfg: {title, message, accept, cancel, applying, confirmColor, error}. The accept button turns
+  // into a disabled "applying" button while onAccept runs; a failure keeps the dialog open with
+  // the error under the message (the apps' delete / stop / close-viewer flows).
+  function renderConfirm(cfg, applying) {
+    return `<h2 class="dialog-title">${esc(cfg.title)}</h2><div class="dialog-content"><p>${esc(cfg.message || "")}</p>` +
+      `<p class="error" data-cy-dialog-error>${esc(cfg.error || "")}</p></div><div class="dialog-actions">` +
+      `<button data-resp="cancel">${esc(String(cfg.cancel || "cancel").toUpperCase())}</button>` +
+      (applying
+        ? `<button disabled class="applying"><span class="spinner"></span> ${esc(String(cfg.applying || "").toUpperCase())}</button>`
+        : `<button data-resp="accept" class="${esc(cfg.confirmColor || "primary")}">${esc(String(cfg.accept || "ok").toUpperCase())}</button>`) +
+      "</div>";
+  }
+  function confirmDialog(cfg, onAccept) {
+    return new Promise((resolve) => {
+      const dlg = document.createElement("dialog");
+      dlg.className = "confirm";
+      if (cfg.width) dlg.style.width = cfg.width;
+      document.body.append(dlg);
+      const state = Object.assign({}, cfg);
+      const done = (resp) => { dlg.close(); dlg.remove(); resolve(resp); };
+      const draw = (applying) => {
+        dlg.innerHTML = renderConfirm(state, applying);
+        const cancel = dlg.querySelector('button[data-resp="cancel"]');
+        cancel.onclick = () => done("cancel");
+        const ok = dlg.querySelector('button[data-resp="accept"]');
+        if (ok) ok.onclick = async () => {
+          draw(true);
+          try { if (onAccept) await onAccept(); done("accept"); }
+          catch (e) { state.error = e.message || String(e); draw(false); }
+        };
+      };
+      dlg.addEventListener("cancel", () => done("cancel"));
+      draw(false);
+      dlg.showModal();
+    });
+  }
+
   // ---- snack bar ------------------------------------------------------------------------------
   function snack(message, status) {
     let el = document.getElementById("kf-snack");
@@ -304,6 +463,7 @@
   }
   global.kf = { call, Poller, cookie, setNamespace, onNamespace, namespace: () => currentNs, statusCell, h,
                 esc, toYaml, eventsTable, kvTable, details, statusIcon, renderTable, sortedRows, ResourceTable, nameLink,
-                conditionsTable, renderLogs, LogsViewer, validators, parseQuantity, snack };
+                conditionsTable, renderLogs, LogsViewer, validators, parseQuantity, snack, parseFilter, rowMatches,
+                paginate, PAGE_SIZES, quantityToScalar, formatBytes, timeAgo, dateTimeHtml, renderConfirm, confirmDialog };
   if (typeof module !== "undefined" && module.exports) module.exports = global.kf;  // node unit tests
 })(typeof window !== "undefined" ? window : globalThis);

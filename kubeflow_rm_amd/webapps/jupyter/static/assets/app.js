@@ -25,16 +25,26 @@
         { title: "Name", value: (r) => r.name, html: (r) => kf.nameLink(r) },
       ];
       if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
+      // index-default/config.ts: Created at / Last activity are DateTimeValues, Memory a MemoryValue
       cols.push(
         { title: "Type", value: (r) => r.serverType },
-        { title: "Age", value: (r) => r.age },
+        { title: "Created at", kind: "date", value: (r) => r.age },
+        { title: "Last activity", kind: "date", value: (r) => r.last_activity },
         { title: "Image", value: (r) => r.shortImage, html: (r) => `<span title="${e(r.image)}">${e(r.shortImage)}</span>` },
         { title: "GPUs", value: (r) => (r.gpus || {}).count || 0, html: (r) => `<span title="${e((r.gpus || {}).message || "")}">${e((r.gpus || {}).count || 0)}</span>` },
         { title: "CPUs", value: (r) => r.cpu },
-        { title: "Memory", value: (r) => r.memory },
-        { title: "Volumes", value: (r) => (r.volumes || []).join(", "), sortable: false },
+        { title: "Memory", kind: "memory", value: (r) => r.memory },
       );
       return cols;
+    },
+    // confirm dialogs (services/config.ts)
+    dialogs: {
+      delete: (name) => ({ title: `Are you sure you want to delete this notebook server? ${name}`,
+                           message: "Warning: Your data might be lost if the notebook server is not backed by persistent storage",
+                           accept: "DELETE", confirmColor: "warn", cancel: "CANCEL", error: "", applying: "DELETING", width: "600px" }),
+      stop: (name) => ({ title: `Are you sure you want to stop this notebook server? ${name}`,
+                         message: "Warning: Your data might be lost if the notebook server is not backed by persistent storage.",
+                         accept: "STOP", confirmColor: "primary", cancel: "CANCEL", error: "", applying: "STOPPING", width: "600px" }),
     },
     // "{notebook-name}-workspace" -> "<name>-workspace" ("-workspace" while the name is empty)
     volumeName(template, notebookName) { return String(template || "").split("{notebook-name}").join(notebookName || ""); },
@@ -171,8 +181,12 @@
         onOpen: (r) => showDetails(r.namespace, r.name),
         onAction: (name, r) => {
           if (name === "connect") window.open(`/notebook/${r.namespace}/${r.name}/`);
-          if (name === "toggle") act("PATCH", r.namespace, r.name, { stopped: r.status.phase !== "stopped" });
-          if (name === "delete" && confirm(`Delete notebook ${r.name}?`)) act("DELETE", r.namespace, r.name);
+          const url = `/api/namespaces/${r.namespace}/notebooks/${r.name}`;
+          // starting needs no confirmation; stopping and deleting go through the confirm dialog,
+          // which stays open with the backend's error if the call fails
+          if (name === "toggle" && r.status.phase === "stopped") act("PATCH", r.namespace, r.name, { stopped: false });
+          else if (name === "toggle") kf.confirmDialog(JWA.dialogs.stop(r.name), () => kf.call("PATCH", url, { stopped: true })).then(() => poller.reset());
+          if (name === "delete") kf.confirmDialog(JWA.dialogs.delete(r.name), () => kf.call("DELETE", url)).then(() => poller.reset());
         },
       };
     }

@@ -7,13 +7,19 @@
   const kf = global.kf || (typeof require !== "undefined" ? require("../../../crud_backend/static/kf.js") : null);
 
   const TWA = {
+    // confirm dialog (pages/index/index.component.ts)
+    dialogs: {
+      delete: (name) => ({ title: `Are you sure you want to delete this Tensorboard : ${name} ?`, message: "",
+                           accept: "DELETE", confirmColor: "warn", cancel: "CANCEL", error: "", applying: "DELETING",
+                           width: "600px" }),
+    },
     columns(allNamespaces) {
       const cols = [
         { title: "Status", value: (r) => r.status.phase, html: (r) => kf.statusIcon(r.status) },
         { title: "Name", value: (r) => r.name },
       ];
       if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
-      cols.push({ title: "Logspath", value: (r) => r.logspath }, { title: "Created at", value: (r) => r.age });
+      cols.push({ title: "Logspath", value: (r) => r.logspath }, { title: "Created at", kind: "date", value: (r) => r.age });
       return cols;
     },
     logspath(kind, pvc, path) {
@@ -47,8 +53,8 @@
         actions: [{ name: "connect", label: "Connect", enabled: (r) => r.status.phase === "ready" }, { name: "delete", label: "Delete" }],
         onAction: async (name, r) => {
           if (name === "connect") window.open(`/tensorboard/${r.namespace}/${r.name}/`);
-          if (name === "delete" && confirm(`Delete TensorBoard ${r.name}?`)) {
-            try { await kf.call("DELETE", `/api/namespaces/${r.namespace}/tensorboards/${r.name}`); } catch (e) { kf.snack(e.message, "ERROR"); }
+          if (name === "delete") {
+            await kf.confirmDialog(TWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${r.namespace}/tensorboards/${r.name}`));
             poller.reset();
           }
         },

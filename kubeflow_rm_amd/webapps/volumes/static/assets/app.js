@@ -8,6 +8,15 @@
   const kf = global.kf || (typeof require !== "undefined" ? require("../../../crud_backend/static/kf.js") : null);
 
   const VWA = {
+    // confirm dialogs (services/actions.service.ts, index-default.component.ts)
+    dialogs: {
+      delete: (name) => ({ title: `Are you sure you want to delete this volume? ${name}`,
+                           message: "Warning: All data in this volume will be lost.", accept: "DELETE",
+                           confirmColor: "warn", cancel: "CANCEL", error: "", applying: "DELETING", width: "600px" }),
+      closeViewer: (name) => ({ title: `Are you sure you want to close this viewer? ${name}`,
+                                message: "Warning: Any running processes will terminate.", accept: "CLOSE",
+                                confirmColor: "warn", cancel: "CANCEL", error: "", applying: "CLOSING", width: "600px" }),
+    },
     columns(allNamespaces) {
       const cols = [
         { title: "Status", value: (r) => r.status.phase, html: (r) => kf.statusIcon(r.status) },
@@ -15,8 +24,8 @@
       ];
       if (allNamespaces) cols.push({ title: "Namespace", value: (r) => r.namespace });
       cols.push(
-        { title: "Created at", value: (r) => r.age },
-        { title: "Size", value: (r) => r.capacity },
+        { title: "Created at", kind: "date", value: (r) => r.age },
+        { title: "Size", kind: "memory", value: (r) => r.capacity },
         { title: "Access Mode", value: (r) => (r.modes || []).join(", ") },
         { title: "Storage Class", value: (r) => r.class || "" },
         { title: "Used by", value: (r) => (r.notebooks || []).join(", "), sortable: false },
@@ -98,8 +107,10 @@
             if (v.status === "ready" && v.url) window.open(v.url);
             else if (v.status === "uninitialized") act("POST", `/api/namespaces/${ns}/viewers`, { name: r.name });
           }
-          if (name === "close") act("DELETE", `/api/namespaces/${ns}/viewers/${r.name}`);
-          if (name === "delete" && confirm(`Delete volume ${r.name}?`)) act("DELETE", `/api/namespaces/${ns}/pvcs/${r.name}`);
+          if (name === "close")
+            kf.confirmDialog(VWA.dialogs.closeViewer(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/viewers/${r.name}`)).then(() => poller.reset());
+          if (name === "delete")
+            kf.confirmDialog(VWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/pvcs/${r.name}`)).then(() => poller.reset());
         },
       };
     }

@@ -196,6 +196,103 @@ test("conditions table, logs viewer, quantities, name validator", () => {
   assert.strictEqual(kf.validators.limitAtLeastRequest("2Gi", "2048Mi", "Memory"), "");
 });
 
+test("resource table: filter chips (any column / column:value, AND-ed) and date / memory columns", () => {
+  const nbs = fixture("jupyter", "notebooks").notebooks;
+  const cols = JWA.columns(false);
+  const terms = kf.parseFilter("Status:ready, rstudio,");
+  assert.deepStrictEqual(terms, [{ column: "status", value: "ready" }, "rstudio"]);
+  const names = (filter) => kf.sortedRows({ columns: cols }, nbs, { filter }).map((r) => r.name);
+  assert.deepStrictEqual(names("terminating"), nbs.filter((n) => n.status.phase === "terminating").map((n) => n.name).sort());
+  assert.deepStrictEqual(names("status:stopped"), nbs.filter((n) => n.status.phase === "stopped").map((n) => n.name).sort());
+  // every chip must match: a name chip AND a phase chip
+  const one = nbs.find((n) => n.status.phase === "ready");
+  assert.deepStrictEqual(names(`${one.name}, status:ready`), [one.name]);
+  assert.deepStrictEqual(names(`${one.name},status:stopped`), []);
+  // Memory is a MemoryValue: "1073741824m" (a milli-byte quantity) shows as 1.0 Mi, "1Gi" as 1.0 Gi
+  const html = kf.renderTable({ columns: cols }, nbs);
+  const mem = column(html, "Memory");
+  nbs.slice().sort((a, b) => a.name.localeCompare(b.name)).forEach((n, i) =>
+    assert.strictEqual(mem[i], kf.formatBytes(kf.quantityToScalar(n.memory))));
+  assert.ok(mem.includes("1.0 Mi") && mem.includes("1.0 Gi"), mem);
+  // Created at / Last activity: relative time with the UTC time on hover; "-" when unset
+  const created = column(html, "Created at");
+  assert.ok(created.every((c) => /ago<\/span>$/.test(c) && c.includes("UTC: 20")), created[0]);
+  assert.ok(column(html, "Last activity").includes("-"));
+  // a date column filters on its words too ("... days ago" / "... years ago")
+  assert.strictEqual(names("created at:ago").length, nbs.length);
+  // sorting a date column sorts by time, a memory column by bytes
+  const byAge = kf.sortedRows({ columns: cols }, nbs, { sortCol: cols.findIndex((c) => c.title === "Created at"), sortDir: 1 });
+  assert.deepStrictEqual(byAge.map((r) => r.age), nbs.map((r) => r.age).sort());
+  const byMem = kf.sortedRows({ columns: cols }, nbs, { sortCol: cols.findIndex((c) => c.title === "Memory"), sortDir: 1 });
+  assert.strictEqual(byMem[0].memory, "1073741824m");
+});
+
+test("resource table paginator: 10 / 20 / 50 per page, range label, buttons", () => {
+  const cols = [{ title: "Name", value: (r) => r.name }];
+  const rows = Array.from({ length: 23 }, (_, i) => ({ name: `nb-${String(i).padStart(2, "0")}` }));
+  assert.deepStrictEqual(kf.PAGE_SIZES, [10, 20, 50]);
+  assert.deepStrictEqual(kf.paginate(23, 2, 10), { page: 2, size: 10, pages: 3, start: 20, end: 23, label: "21 – 23 of 23" });
+  assert.strictEqual(kf.paginate(23, 9, 10).page, 2);       // clamped to the last page
+  assert.strictEqual(kf.paginate(23, 0, 7).size, 50);       // unknown size -> default 50
+  assert.strictEqual(kf.paginate(0, 0, 10).label, "0 of 0");
+  const page1 = kf.renderTable({ columns: cols }, rows, { page: 1, pageSize: 10 });
+  assert.deepStrictEqual(column(page1, "Name"), rows.slice(10, 20).map((r) => r.name));
+  assert.ok(page1.includes("11 – 20 of 23") && page1.includes("data-cy-paginator"));
+  assert.ok(!/data-page="prev" disabled/.test(page1) && !/data-page="next" disabled/.test(page1));
+  const first = kf.renderTable({ columns: cols }, rows, { page: 0, pageSize: 20 });
+  assert.ok(/data-page="prev" disabled/.test(first) && first.includes("1 – 20 of 23"));
+  assert.ok(!kf.renderTable({ columns: cols }, rows.slice(0, 5)).includes("data-cy-paginator"));
+});
+
+test("quantities, bytes and relative time (resource-table utils, lib-date-time)", () => {
+  assert.strictEqual(kf.quantityToScalar("500m"), 0.5);
+  assert.strictEqual(kf.quantityToScalar("2Gi"), 2 * 2 ** 30);
+  assert.strictEqual(kf.quantityToScalar("1.5k"), 1500);
+  assert.strictEqual(kf.quantityToScalar("10"), 10);
+  assert.strictEqual(kf.quantityToScalar(""), 0);
+  assert.throws(() => kf.quantityToScalar("3 bananas"));
+  assert.strictEqual(kf.formatBytes(512), "512 B");
+  assert.strictEqual(kf.formatBytes(1536), "1.5 Ki");
+  assert.strictEqual(kf.formatBytes(20 * 2 ** 30), "20.0 Gi");
+  assert.strictEqual(kf.formatBytes(1023.99 * 2 ** 20), "1.0 Gi");  // rounds up into the next unit
+  assert.strictEqual(kf.formatBytes(1.5e9, true), "1.5 GB");
+  const now = Date.parse("2024-03-10T12:00:00Z");
+  const ago = (ms) => kf.timeAgo(new Date(now - ms).toISOString(), now);
+  const M = 60e3, H = 60 * M, D = 24 * H;
+  assert.strictEqual(ago(10e3), "less than a minute ago");
+  assert.strictEqual(ago(1 * M), "1 minute ago");
+  assert.strictEqual(ago(44 * M), "44 minutes ago");
+  assert.strictEqual(ago(50 * M), "1 hour ago");
+  assert.strictEqual(ago(5 * H), "5 hours ago");
+  assert.strictEqual(ago(30 * H), "1 day ago");
+  assert.strictEqual(ago(12 * D), "12 days ago");
+  assert.strictEqual(ago(40 * D), "1 month ago");
+  assert.strictEqual(ago(200 * D), "7 months ago");
+  assert.strictEqual(kf.timeAgo("2023-02-01T12:00:00Z", now), "1 year ago");
+  assert.strictEqual(kf.timeAgo("2022-09-10T12:00:00Z", now), "over 1 year ago");
+  assert.strictEqual(kf.timeAgo("2021-04-10T12:00:00Z", now), "3 years ago");
+  assert.strictEqual(kf.timeAgo(new Date(now + 3 * H).toISOString(), now), "in 3 hours");
+  assert.strictEqual(kf.timeAgo("", now), "-");
+  assert.strictEqual(kf.dateTimeHtml(""), "-");
+});
+
+test("confirm dialogs: the reference texts, applying state, error kept in the dialog", () => {
+  const d = JWA.dialogs.delete("nb1");
+  assert.strictEqual(d.title, "Are you sure you want to delete this notebook server? nb1");
+  assert.strictEqual(d.accept, "DELETE");
+  assert.strictEqual(d.applying, "DELETING");
+  assert.strictEqual(JWA.dialogs.stop("nb1").confirmColor, "primary");
+  assert.strictEqual(VWA.dialogs.delete("v").message, "Warning: All data in this volume will be lost.");
+  assert.strictEqual(VWA.dialogs.closeViewer("v").accept, "CLOSE");
+  assert.strictEqual(TWA.dialogs.delete("t").title, "Are you sure you want to delete this Tensorboard : t ?");
+  const idle = kf.renderConfirm(d, false);
+  assert.ok(idle.includes('data-resp="accept" class="warn">DELETE</button>') && idle.includes(">CANCEL</button>"));
+  const busy = kf.renderConfirm(d, true);
+  assert.ok(!busy.includes('data-resp="accept"') && busy.includes("DELETING") && busy.includes("disabled"));
+  const failed = kf.renderConfirm(Object.assign({}, d, { error: "<forbidden>" }), false);
+  assert.ok(failed.includes("&lt;forbidden&gt;") && failed.includes('data-resp="accept"'));
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {
