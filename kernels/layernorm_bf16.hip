@@ -46,29 +46,34 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;  // wave-uniform; no barriers below
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)row * H);
-  float v[VPL][8];
+  // hidden 8192: the row stays resident as packed bf16 (64 data VGPRs instead of 128 fp32), so 4
+  // waves per SIMD instead of 2 keep more rows in flight: +6-8 % at 8192 / 32768 x 8192. At
+  // hidden <= 4096 the fp32 copy already allows 4+ waves and re-widening measured 0-8 % slower
+  // (profiles/r2_ln_occupancy), so there the compiler keeps the widened values.
+  constexpr bool kRepack = VPL >= 16;
+  bf16x8 v[VPL];
 #pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    // streamed once: non-temporal (no L2/MALL allocation for data nobody re-reads)
-    const bf16x8 t = __builtin_nontemporal_load(&xr[j * 64 + lane]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[j][e] = (float)t[e];
-  }
+  for (int j = 0; j < VPL; ++j) v[j] = __builtin_nontemporal_load(&xr[j * 64 + lane]);  // streamed once
   float mean = 0.f;
   if (!RMS) {
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[j][e];
+      for (int e = 0; e < 8; ++e) s += (float)v[j][e];
     mean = wave_sum(s) * (1.f / H);
   }
+  // an empty asm "redefines" the packed row before each later pass, so the compiler widens it again
+  // instead of keeping the first pass's fp32 copies live (which is what costs the registers)
+  if constexpr (kRepack)
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float d = v[j][e] - mean;
+      const float d = (float)v[j][e] - mean;
       ss += d * d;
     }
   const float rstd = rsqrtf(wave_sum(ss) * (1.f / H) + eps);
@@ -76,6 +81,9 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
   }
+  if constexpr (kRepack)
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
   const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
   const bf16x8* b8 = reinterpret_cast<const bf16x8*>(beta);
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (long long)row * H);
@@ -87,7 +95,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float r = (v[j][e] - mean) * rstd * (float)g[e];
+      float r = ((float)v[j][e] - mean) * rstd * (float)g[e];
       if (!RMS && beta) r += (float)b[e];
       o[e] = (__bf16)r;
     }
@@ -144,27 +152,68 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
   const bf16x8* dyr = reinterpret_cast<const bf16x8*>(dy + (long long)row * H);
   const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
   const float mu = mean[row], rs = rstd[row];
-  float xh[VPL][8], gd[VPL][8];
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    const bf16x8 xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      xh[j][e] = ((float)xv[e] - mu) * rs;
-      gd[j][e] = (float)dv[e] * (float)gv[e];
-      s1 += gd[j][e] * xh[j][e];
-      s2 += gd[j][e];
-    }
-  }
-  const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
   bf16x8* dxr = reinterpret_cast<bf16x8*>(dx + (long long)row * H);
+  if constexpr (VPL < 16) {
+    // the widened row (xhat, gamma * dy) stays in registers between the passes
+    float xh[VPL][8], gd[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    bf16x8 o;
+    for (int j = 0; j < VPL; ++j) {
+      const bf16x8 xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
-    dxr[j * 64 + lane] = o;
+      for (int e = 0; e < 8; ++e) {
+        xh[j][e] = ((float)xv[e] - mu) * rs;
+        gd[j][e] = (float)dv[e] * (float)gv[e];
+        s1 += gd[j][e] * xh[j][e];
+        s2 += gd[j][e];
+      }
+    }
+    const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
+      dxr[j * 64 + lane] = o;
+    }
+  } else {
+    // hidden 8192: x and dy stay packed bf16 between the two passes (8 VGPRs per 8 columns
+    // instead of 16 fp32: 2 waves per SIMD instead of 1); the second pass widens them again and
+    // re-reads gamma, which every row shares (L2-resident)
+    bf16x8 xv[VPL], dv[VPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      xv[j] = xr[j * 64 + lane];
+      dv[j] = dyr[j * 64 + lane];
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const bf16x8 gv = g8[j * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = ((float)xv[j][e] - mu) * rs, gd = (float)dv[j][e] * (float)gv[e];
+        s1 += gd * xh;
+        s2 += gd;
+      }
+    }
+    const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      asm volatile("" : "+v"(xv[j]));  // widen again below rather than keep pass one's fp32 values
+      asm volatile("" : "+v"(dv[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const bf16x8 gv = g8[j * 64 + lane];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = ((float)xv[j][e] - mu) * rs, gd = (float)dv[j][e] * (float)gv[e];
+        o[e] = (__bf16)(rs * (gd - xh * c1 - c2));
+      }
+      dxr[j * 64 + lane] = o;
+    }
   }
 }
 
