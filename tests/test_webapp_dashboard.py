@@ -1,6 +1,7 @@
 """Central dashboard backend.
 
-Ports the reference's app tests (api_test.ts: metrics 405 / series / intervals;
+Ports the reference's app tests (api_test.ts: metrics 405 / series / intervals; k8s_service_test.ts:
+namespaces / events / nodes, empty on error, platform info known / other / unknown / defaults;
 attach_user_middleware_test.ts; api_workgroup_test.ts: env-info, exists, create, contributors,
 KFAM failure surfacing) with a fake KFAM + metrics service, then runs the whole workgroup flow
 against the real native KFAM and kube-lite (registration -> owner namespace -> contributor add /
@@ -249,3 +250,57 @@ def test_workgroup_flow_against_kfam(cluster, monkeypatch):
     svc.stop()
     assert tc.delete("/api/workgroup/nuke-self", headers=carol).status_code == 200
     cluster.client.wait_gone("kubeflow.org/v1", "Profile", "carol", None, timeout=20)
+
+
+# ---- KubernetesService (ports of k8s_service_test.ts) ------------------------------------------
+class ScriptedK8s:
+    """list() answers from a {kind: items | exception} table (the reference's mocked CoreV1Api)."""
+
+    def __init__(self, table):
+        self.table = table
+
+    def list(self, av, kind, ns=None, **kw):
+        v = self.table.get(kind, [])
+        if isinstance(v, Exception):
+            raise v
+        return {"items": v}
+
+
+def _node(provider=None):
+    spec = {"podCIDR": "10.44.1.0/24"}
+    if provider:
+        spec["providerID"] = provider
+    return {"apiVersion": "v1", "kind": "Node", "spec": spec}
+
+
+GCE = "gce://kubeflow-dev/us-east1-d/gke-kubeflow-default-pool-59885f2c-08tm"
+KF_APP = {"apiVersion": "app.k8s.io/v1beta1", "kind": "Application", "spec": {"descriptor": {"type": "kubeflow", "version": "1.0.0"}}}
+
+
+def test_k8s_service_namespaces_events_nodes_and_errors():
+    from kubeflow_rm_amd.client import ApiException
+    ok = dashboard.KubernetesService(ScriptedK8s({
+        "Namespace": [{"metadata": {"name": "default"}}, {"metadata": {"name": "kubeflow"}}],
+        "Event": [{"metadata": {"name": "e1"}, "reason": "Scheduled"}],
+        "Node": [_node(GCE), _node(GCE.replace("08tm", "r72s"))]}))
+    assert [n["metadata"]["name"] for n in ok.get_namespaces()] == ["default", "kubeflow"]   # Returns all namespaces
+    assert ok.get_events("kubeflow")[0]["reason"] == "Scheduled"                             # Returns events
+    assert len(ok.get_nodes()) == 2                                                          # Returns all Nodes
+    err = ApiException(500, "testing-error", None)
+    bad = dashboard.KubernetesService(ScriptedK8s({"Namespace": err, "Event": err, "Node": err}))
+    assert bad.get_namespaces() == [] and bad.get_events("kubeflow") == [] and bad.get_nodes() == []  # empty on error
+
+
+@pytest.mark.parametrize("nodes,apps,want", [
+    ([_node(GCE), _node(GCE)], [KF_APP], {"provider": GCE, "providerName": "gce", "kubeflowVersion": "1.0.0"}),
+    ([_node(), _node()], [KF_APP], {"provider": "other://", "providerName": "other", "kubeflowVersion": "1.0.0"}),
+    ([_node(GCE)], [], {"provider": GCE, "providerName": "gce", "kubeflowVersion": "unknown"}),
+    ("error", "error", {"provider": "other://", "providerName": "other", "kubeflowVersion": "unknown"}),
+], ids=["known provider and version", "no providerID -> other", "no Application -> unknown", "defaults on error"])
+def test_k8s_service_platform_info(nodes, apps, want, monkeypatch):
+    from kubeflow_rm_amd.client import ApiException
+    monkeypatch.delenv("LOGOUT_URL", raising=False)
+    err = ApiException(500, "testing-error", None)
+    svc = dashboard.KubernetesService(ScriptedK8s({"Node": err if nodes == "error" else nodes,
+                                                  "Application": err if apps == "error" else apps}))
+    assert svc.get_platform_info() == {**want, "logoutUrl": "/logout"}
