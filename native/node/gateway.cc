@@ -2,6 +2,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "core/util.h"
 #include "node/node.h"
@@ -12,7 +13,10 @@ Gateway::Gateway(std::shared_ptr<Client> c, std::string gateway_name)
     : c_(std::move(c)),
       gw_(std::move(gateway_name)),
       upgrades_(Registry::global().counter("gateway_upgraded_connections_total", "connections tunnelled after an HTTP Upgrade (WebSocket)")),
-      streams_(Registry::global().counter("gateway_streamed_responses_total", "responses relayed incrementally (chunked / unframed / large)")) {}
+      streams_(Registry::global().counter("gateway_streamed_responses_total", "responses relayed incrementally (chunked / unframed / large)")) {
+  const char* d = std::getenv("KFAMD_ROUTE_DOMAIN");
+  route_domain_ = d && *d ? d : "apps.kube-lite";
+}
 Gateway::~Gateway() { stop(); }
 
 void Gateway::setup(Manager& mgr) {
@@ -99,7 +103,9 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   } else if (routes_) {
     // OpenShift Route (host based)
     for (const auto& r : routes_->list()) {
-      if (r.at_path({"spec", "host"}).as_string() != host.substr(0, host.find(':'))) continue;
+      std::string rhost = r.at_path({"spec", "host"}).as_string();
+      if (rhost.empty()) rhost = r.str_at({"metadata", "name"}) + "-" + r.str_at({"metadata", "namespace"}) + "." + route_domain_;
+      if (rhost != host.substr(0, host.find(':'))) continue;
       const std::string svc = r.at_path({"spec", "to", "name"}).as_string();
       rt.dest_host = svc + "." + r.str_at({"metadata", "namespace"}) + ".svc";
       const Json& tp = r.at_path({"spec", "port", "targetPort"});

@@ -162,6 +162,9 @@ class Gateway {
   Informer* routes_ = nullptr;
   std::unique_ptr<HttpServer> srv_;
   std::shared_ptr<CounterVec> upgrades_, streams_;
+  // host an OpenShift router gives a Route without spec.host: <name>-<namespace>.<domain>
+  // (KFAMD_ROUTE_DOMAIN, default apps.kube-lite)
+  std::string route_domain_;
 };
 
 }  // namespace kf

@@ -259,3 +259,52 @@ def test_service_mesh_notebook(c):
         c.create(_nb("both", "odh", annotations={"opendatahub.io/service-mesh": "true",
                                                  "notebooks.opendatahub.io/inject-oauth": "true"}))
     assert "Pick one" in str(e.value.body)
+
+
+# ---- e2e lifecycle (ports of odh-notebook-controller/e2e: creation, traffic, update, deletion) -----
+def _via_route(cluster, host, path):
+    import urllib.request
+    req = urllib.request.Request(cluster.gateway + path, headers={"Host": host})
+    with urllib.request.urlopen(req, timeout=5) as r:
+        return r.status, r.read()
+
+
+def test_e2e_lifecycle_creation_traffic_update_deletion(cluster, c):
+    # creation (notebook_creation_test.go): instance, Route, NetworkPolicies, StatefulSet
+    c.create(_nb("life", "odh"))
+    c.wait_for(NB, "Notebook", "life", "odh", lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=30)
+    route = _exists(c, "route.openshift.io/v1", "Route", "life")
+    for np in ("life-ctrl-np", "life-oauth-np"):
+        _exists(c, "networking.k8s.io/v1", "NetworkPolicy", np)
+    sts = _exists(c, "apps/v1", "StatefulSet", "life")
+    assert sts["spec"]["template"]["spec"]["containers"][0]["image"] == "jupyter:1"
+    # traffic (testNotebookTraffic): the Route's host reaches the notebook server through the gateway
+    # a Route without spec.host gets the router's default host <name>-<namespace>.<domain>
+    host = route["spec"].get("host") or "life-odh.apps.kube-lite"
+    deadline = time.time() + 15
+    while True:
+        try:
+            status, _ = _via_route(cluster, host, "/notebook/odh/life/api/status")
+            break
+        except Exception:
+            if time.time() > deadline:
+                raise
+            time.sleep(0.2)
+    assert status == 200
+    # update (notebook_update_test.go): a new image reaches the StatefulSet and its pod
+    nb = c.get(NB, "Notebook", "life", "odh")
+    nb["spec"]["template"]["spec"]["containers"][0]["image"] = "jupyter-minimal:2"
+    c.update(nb)
+    c.wait_for("apps/v1", "StatefulSet", "life", "odh",
+               lambda o: o["spec"]["template"]["spec"]["containers"][0]["image"] == "jupyter-minimal:2", timeout=15)
+    c.wait_for("v1", "Pod", "life-0", "odh",
+               lambda o: o["spec"]["containers"][0]["image"] == "jupyter-minimal:2"
+               and any(cd["type"] == "Ready" and cd["status"] == "True" for cd in (o.get("status") or {}).get("conditions", [])),
+               timeout=30)
+    assert _exists(c, "route.openshift.io/v1", "Route", "life")["spec"]["to"]["name"] == "life"
+    # deletion (notebook_deletion_test.go): the owned StatefulSet, NetworkPolicies and Route go with it
+    c.delete(NB, "Notebook", "life", "odh")
+    c.wait_gone(NB, "Notebook", "life", "odh", timeout=20)
+    for av, kind, name in (("apps/v1", "StatefulSet", "life"), ("networking.k8s.io/v1", "NetworkPolicy", "life-ctrl-np"),
+                           ("networking.k8s.io/v1", "NetworkPolicy", "life-oauth-np"), ("route.openshift.io/v1", "Route", "life")):
+        c.wait_gone(av, kind, name, "odh", timeout=20)
