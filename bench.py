@@ -49,7 +49,9 @@ def parse_args():
                    help="cold-start runs of one N-GPU notebook through the native control plane (rank 0)")
     p.add_argument("--coldstart-torch-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_TORCH_RUNS", "5")),
                    help="cold-start runs with the torch-ready notebook server (torch import + GEMM before Ready)")
-    p.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt)")
+    p.add_argument("--compare-torch", action=argparse.BooleanOptionalAction, default=True,
+                   help="also time torch.matmul (hipBLASLt) on the same operands, after the timed region "
+                        "(rank 0; reported as torch_matmul_tflops_per_gpu, never as the value)")
     p.add_argument("--no-allreduce-sweep", action="store_true",
                    help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
     return p.parse_args()
