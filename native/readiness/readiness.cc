@@ -26,8 +26,8 @@
 //
 // Flags: --m/--n/--k GEMM size (default 4096^3), --iters, --ln-rows/--ln-hidden,
 //        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
-//        --oneshot-sim N, --rccl (RCCL sweep on >= 2 GPUs), --rccl-single (RCCL stage with one
-//        device), --serial (devices one after another).
+//        --oneshot-sim N, --full-sweep (one-shot at every size, not 3), --rccl (RCCL sweep on >= 2
+//        GPUs), --rccl-single (RCCL stage with one device), --serial (devices one after another).
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <rccl/rccl.h>
@@ -146,6 +146,7 @@ struct Args {
   bool rccl = false;        // --rccl: RCCL communicator + busbw sweep on >= 2 GPUs (opt-in)
   bool serial = false;      // --serial: check devices one after another
   int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
+  bool full_sweep = false;  // --full-sweep: one-shot at every 4x size 16 B..256 KiB, 50 timed calls each
   std::string inject_fault;  // fault injection: fail the op at this stage
 };
 
@@ -500,7 +501,7 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
 }
 
 // K3 fast path: one-shot peer all-reduce. sim_ranks > 0: that many ranks on device 0, one launch.
-bool oneshot_check(int ndev, int sim_ranks, Json& out) {
+bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<hipStream_t>& dev_streams, Json& out) {
   g_stage = "allreduce-oneshot";
   const bool sim = sim_ranks > 0;
   const int nranks = sim ? sim_ranks : ndev;
@@ -511,6 +512,13 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
   const size_t max_bytes = 256 << 10;
   const int max_blocks = 64;
   const long long fbytes = kfamd_allreduce_oneshot_flag_bytes(nranks, max_blocks);
+  Json stages = Json::object();
+  auto tp = std::chrono::steady_clock::now();
+  auto lap = [&](const char* name) {
+    const auto now = std::chrono::steady_clock::now();
+    stages[name] = std::chrono::duration<double, std::milli>(now - tp).count();
+    tp = now;
+  };
   if (!sim) {
     for (int i = 0; i < nranks; ++i) {
       HIP_OK(hipSetDevice(i));
@@ -524,11 +532,26 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
       }
     }
   }
+  lap("peer_access_ms");
   auto dev_of = [&](int r) { return sim ? 0 : r; };
   std::vector<void*> in(8, nullptr), outb(8, nullptr);
   std::vector<uint32_t*> flags(8, nullptr);
   std::vector<unsigned*> tmo(nranks, nullptr);
-  std::vector<hipStream_t> st(sim ? 1 : nranks);
+  // each device's stream from the GEMM / LayerNorm stages: every new stream (and the null stream's
+  // first use) brings up another HW queue, about 20 ms each on the cold-start path
+  std::vector<hipStream_t> st(sim ? 1 : nranks, nullptr);
+  std::vector<bool> own(st.size(), false);
+  for (size_t i = 0; i < st.size(); ++i) {
+    const int d = sim ? 0 : (int)i;
+    if (d < (int)dev_streams.size() && dev_streams[d]) {
+      st[i] = dev_streams[d];
+    } else {
+      HIP_OK(hipSetDevice(d));
+      HIP_OK(hipStreamCreate(&st[i]));
+      own[i] = true;
+    }
+  }
+  auto stream_of = [&](int r) { return st[sim ? 0 : r]; };
   for (int r = 0; r < nranks; ++r) {
     HIP_OK(hipSetDevice(dev_of(r)));
     HIP_OK(hipMalloc(&in[r], max_bytes));
@@ -536,11 +559,15 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
     // flags are polled across devices: uncached so a peer's atomic store is seen without a flush
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags[r]), fbytes, hipDeviceMallocUncached) != hipSuccess)
       HIP_OK(hipMalloc(&flags[r], fbytes));
-    HIP_OK(hipMemset(flags[r], 0, fbytes));
+    HIP_OK(hipMemsetAsync(flags[r], 0, fbytes, stream_of(r)));
     HIP_OK(hipMalloc(&tmo[r], sizeof(unsigned)));
-    HIP_OK(hipMemset(tmo[r], 0, sizeof(unsigned)));
-    if (!sim || r == 0) HIP_OK(hipStreamCreate(&st[r]));
+    HIP_OK(hipMemsetAsync(tmo[r], 0, sizeof(unsigned), stream_of(r)));
   }
+  for (size_t i = 0; i < st.size(); ++i) {
+    HIP_OK(hipSetDevice(sim ? 0 : (int)i));
+    HIP_OK(hipStreamSynchronize(st[i]));  // flags zeroed on every device before any rank launches
+  }
+  lap("alloc_ms");
   unsigned epoch = 0;
   bool ok = true;
   auto launch_all = [&](size_t n) -> bool {
@@ -562,7 +589,15 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
     return true;
   };
   Json sweep = Json::array();
-  for (size_t bytes = 16; bytes <= max_bytes; bytes *= 4) {
+  // on the cold-start path (an N-GPU pod's init container) three sizes verify the small, mid and
+  // largest one-shot shapes; every launch syncs all N devices, so the full sweep costs tens of ms
+  std::vector<size_t> sizes;
+  if (full_sweep)
+    for (size_t b = 16; b <= max_bytes; b *= 4) sizes.push_back(b);
+  else
+    sizes = {16, 16 << 10, max_bytes};
+  const int iters = full_sweep ? 50 : 10;
+  for (size_t bytes : sizes) {
     const size_t n = bytes / 4;
     for (int r = 0; r < nranks; ++r) {
       HIP_OK(hipSetDevice(dev_of(r)));
@@ -574,20 +609,21 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
     std::vector<float> h(n);
     for (int r = 0; r < nranks; ++r) {
       HIP_OK(hipSetDevice(dev_of(r)));
-      HIP_OK(hipMemcpy(h.data(), outb[r], bytes, hipMemcpyDeviceToHost));
+      unsigned t = 0;
+      HIP_OK(hipMemcpyAsync(h.data(), outb[r], bytes, hipMemcpyDeviceToHost, stream_of(r)));
+      HIP_OK(hipMemcpyAsync(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost, stream_of(r)));
+      HIP_OK(hipStreamSynchronize(stream_of(r)));
       for (size_t i = 0; i < n; ++i)
         if (h[i] != want) ok = false;
-      unsigned t = 0;
-      HIP_OK(hipMemcpy(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost));
       if (t) ok = false;
     }
-    const int iters = 50;
     auto t1 = std::chrono::steady_clock::now();
     for (int it = 0; it < iters; ++it)
       if (!launch_all(n)) return false;
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / iters;
     sweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}});
   }
+  lap("sweep_ms");
   for (int r = 0; r < nranks; ++r) {
     (void)hipSetDevice(dev_of(r));
     (void)hipFree(in[r]);
@@ -595,8 +631,10 @@ bool oneshot_check(int ndev, int sim_ranks, Json& out) {
     (void)hipFree(flags[r]);
     (void)hipFree(tmo[r]);
   }
-  for (auto s : st) (void)hipStreamDestroy(s);
-  out = Json{{"mode", sim ? "simulated-on-device-0" : "peer"}, {"ranks", nranks}, {"sweep", sweep}, {"correct", ok},
+  for (size_t i = 0; i < st.size(); ++i)
+    if (own[i]) (void)hipStreamDestroy(st[i]);
+  lap("free_ms");
+  out = Json{{"mode", sim ? "simulated-on-device-0" : "peer"}, {"ranks", nranks}, {"sweep", sweep}, {"correct", ok}, {"stages", stages},
              {"note", "us = host wall per call incl. launch + stream sync"}};
   if (!ok) fail("one-shot all-reduce mismatch or peer timeout");
   return ok;
@@ -821,6 +859,7 @@ int readiness_main(int argc, char** argv) {
     else if (s == "--rccl-single") a.force_rccl = true;
     else if (s == "--rccl") a.rccl = true;
     else if (s == "--fast-exit") g_fast_exit = true;
+    else if (s == "--full-sweep") a.full_sweep = true;
     else if (s == "--no-fast-exit") g_fast_exit = false;
     else if (s == "--serial") a.serial = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
@@ -864,6 +903,8 @@ int readiness_main(int argc, char** argv) {
       double query_ms = 0, gemm_ms = 0, ln_ms = 0;
     };
     std::vector<DevResult> res(ndev);
+    // each device's buffers and stream live until the multi-GPU stages are done (they reuse the stream)
+    std::vector<DevBuffers> bufs(ndev);
     auto lap = [](std::chrono::steady_clock::time_point& t) {
       auto now = std::chrono::steady_clock::now();
       double ms = std::chrono::duration<double, std::milli>(now - t).count();
@@ -879,7 +920,7 @@ int readiness_main(int argc, char** argv) {
         r.dev = Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
                      {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}};
       r.query_ms = lap(ts);
-      DevBuffers buf;
+      DevBuffers& buf = bufs[d];
       Json g;
       if (gemm_check(d, a, buf, g)) r.gemm = g;
       else r.gemm = Json{{"device", d}, {"error", first_error()}};
@@ -928,7 +969,9 @@ int readiness_main(int argc, char** argv) {
     if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
       Json os;
       auto ts = std::chrono::steady_clock::now();
-      oneshot_check(ndev, a.oneshot_sim, os);
+      std::vector<hipStream_t> streams;
+      for (const auto& b : bufs) streams.push_back(b.s);
+      oneshot_check(ndev, a.oneshot_sim, a.full_sweep, streams, os);
       g_result["allreduce_oneshot"] = os;
       g_result["stages_ms"]["allreduce_oneshot"] = lap(ts);
     }
