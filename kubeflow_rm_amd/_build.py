@@ -12,6 +12,7 @@ Everything is built in-tree so that the artefacts travel with a ``gpurun`` snaps
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -78,14 +79,23 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     obj_dir.mkdir(parents=True, exist_ok=True)
     LIB_DIR.mkdir(parents=True, exist_ok=True)
 
+    # kfamd_build_info() names the kernel sources it was built from (content hash), so a loaded
+    # library identifies itself even when only other translation units were recompiled
+    src_hash = hashlib.sha256(b"".join(p.read_bytes() for p in [*srcs, *headers])).hexdigest()[:12]
+    stamp = obj_dir / "src_hash"
+    hash_changed = not stamp.exists() or stamp.read_text().strip() != src_hash
+
     def compile_one(src: Path) -> Path:
         obj = obj_dir / (src.stem + ".o")
-        if force or not _newer(obj, [src, *headers]):
-            _run([HIPCC, *HIP_FLAGS, "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
+        info = src.name == "kfamd_info.hip"
+        if force or not _newer(obj, [src, *headers]) or (info and hash_changed):
+            extra = [f'-DKFAMD_SRC_HASH="{src_hash}"'] if info else []
+            _run([HIPCC, *HIP_FLAGS, *extra, "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
         objs = list(ex.map(compile_one, srcs))
+    stamp.write_text(src_hash)
     if force or not _newer(KERNEL_LIB, objs):
         tmp = KERNEL_LIB.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)])
