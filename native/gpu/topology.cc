@@ -400,7 +400,13 @@ Json gpu_env_for(const Placement& p, const GpuTopology& t, bool multi_gpu, const
     auto pos = std::find(p.devices.begin(), p.devices.end(), d) - p.devices.begin();
     ring.push_back(std::to_string(pos));
   }
-  add("HIP_VISIBLE_DEVICES", join(ids, ","));
+  // the container view of a device-plugin allocation: ROCr brings up only these agents (a process
+  // pod otherwise initialises, and at exit tears down, every GPU of the node), renumbered 0..n-1
+  // for HIP; KFAMD_GPU_IDS keeps the node-level ids
+  std::vector<std::string> local;
+  for (size_t i = 0; i < ids.size(); ++i) local.push_back(std::to_string(i));
+  add("ROCR_VISIBLE_DEVICES", join(ids, ","));
+  add("HIP_VISIBLE_DEVICES", join(local, ","));
   add("KFAMD_GPU_IDS", join(ids, ","));
   add("KFAMD_XGMI_RING", join(ring, ","));
   add("KFAMD_GPU_TOPOLOGY", t.describe());

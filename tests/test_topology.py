@@ -107,6 +107,20 @@ def _wait(cond, timeout=30):
 
 
 @pytest.mark.skipif(len(os.sched_getaffinity(0)) < 8, reason="needs 8 schedulable CPUs")
+def test_pod_env_exposes_only_the_allocated_gpus(native):
+    """Device-plugin Allocate semantics for process pods: ROCr sees only the allocated GPUs (it would
+    otherwise bring up and tear down every GPU of the node per process), HIP numbers them 0..n-1,
+    the ring is in those pod-local ordinals and KFAMD_GPU_IDS keeps the node ids."""
+    env = {e["name"]: e["value"] for e in native.call("gpu_env_for", gpus=8, devices=[5, 4])}
+    assert env["ROCR_VISIBLE_DEVICES"] == "5,4"
+    assert env["HIP_VISIBLE_DEVICES"] == "0,1"
+    assert env["KFAMD_GPU_IDS"] == "5,4"
+    assert sorted(env["KFAMD_XGMI_RING"].split(",")) == ["0", "1"]
+    assert env["WORLD_SIZE"] == env["LOCAL_WORLD_SIZE"] == "2"
+    one = {e["name"]: e["value"] for e in native.call("gpu_env_for", gpus=8, devices=[3])}
+    assert one["ROCR_VISIBLE_DEVICES"] == "3" and one["HIP_VISIBLE_DEVICES"] == "0" and "WORLD_SIZE" not in one
+
+
 def test_gpu_pod_pinned_to_numa_local_cpus_and_partition_hbm_quota(tmp_path):
     """e2e: a kubelet on the fake CPX/NPS2 node advertises 16 devices x 36 GiB, a 1-GPU notebook
     lands on package 1's NUMA node and runs on exactly that node's CPUs, and quota charges 36 GiB."""
