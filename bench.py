@@ -137,12 +137,16 @@ def main() -> int:
     if world > 1 and not args.no_allreduce_sweep:
         # BASELINE §3 "RCCL all-reduce busbw over xGMI" on the same N GPUs, outside the timed GEMM
         # region (every rank participates; rank 0 reports)
+        # 8 B .. 1 GiB, fp32 and bf16, algbw and busbw = algbw * 2(n-1)/n
         try:
             from kubeflow_rm_amd.parallel.collectives import allreduce_sweep
-            sw = allreduce_sweep(max_bytes=256 << 20, min_bytes=8 << 10, step=16, iters_small=20, iters_large=5,
-                                 device=dev)
-            extra["rccl_allreduce_fp32"] = [{"bytes": r["bytes"], "us": round(r["us"], 1),
-                                             "busbw_GBps": round(r["busbw_GBps"], 1)} for r in sw]
+            for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+                sw = allreduce_sweep(max_bytes=1 << 30, min_bytes=8, step=8, iters_small=20, iters_large=5,
+                                     dtype=dt, device=dev)
+                extra[f"rccl_allreduce_{name}"] = [{"bytes": r["bytes"], "us": round(r["us"], 1),
+                                                    "algbw_GBps": round(r["algbw_GBps"], 1),
+                                                    "busbw_GBps": round(r["busbw_GBps"], 1)} for r in sw]
+                torch.cuda.empty_cache()
         except Exception as e:  # reported, never fatal for the GEMM number
             extra["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
     if args.compare_torch and rank == 0:
