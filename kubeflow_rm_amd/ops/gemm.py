@@ -28,6 +28,35 @@ def _check_operand(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name} must have a contiguous last dimension")
 
 
+# Shapes off the MFMA tiles (M, N % 128, K % 64) would run on the generic kernel at a third to a
+# half of the tiled kernels' rate (profiles/r2_gemm_unaligned). Above this size the operands are
+# zero-padded up to the tiles instead: the copies cost a few percent of the GEMM.
+_PAD_MIN_FLOPS = 2.0 * 1024 ** 3
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K):
+    """Zero-pad to the tile grid, run the tiled kernel, copy the [M, N] corner into ``out``."""
+    big = -(-M // 256) * -(-N // 256) * batch > 128  # the auto dispatch's 256-tile threshold
+    tm = 256 if big else 128
+    Mp, Np, Kp = _round_up(M, tm), _round_up(N, tm), _round_up(K, 64)
+    F = torch.nn.functional
+    ap = F.pad(a3, (0, Kp - K, 0, Mp - M))
+    bp = F.pad(b, (0, Kp - K, 0, Np - N))
+    bias_p = F.pad(bias, (0, Np - N)) if bias is not None else None
+    res_p = None
+    if residual is not None:
+        r3 = residual.view(batch, M, N) if batched else residual.reshape(M, N)
+        res_p = F.pad(r3, (0, Np - N, 0, Mp - M))
+    cp = gemm_nt(ap, bp, bias=bias_p, residual=res_p, alpha=alpha, act=act)
+    c3 = out.view(batch, M, N) if batched else out.view(M, N)
+    c3.copy_(cp[..., :M, :N])
+    return out
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = None,
             residual: torch.Tensor | None = None, alpha: float = 1.0, act: str = "none",
             out: torch.Tensor | None = None, variant: str = "auto") -> torch.Tensor:
@@ -71,6 +100,9 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
         _check_operand(bias, "bias")
         if bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous [N] tensor")
+    if (variant == "auto" and (M % 128 or N % 128 or K % 64)
+            and flops(M, N, K, batch) >= _PAD_MIN_FLOPS):
+        return _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K)
     r_ptr, ldr, sr = None, 0, 0
     if residual is not None:
         _check_operand(residual, "residual")

@@ -70,6 +70,22 @@ def test_gemm_generic_path(M, N, K):
     _assert_close(out, _ref_gemm(a, b), K)
 
 
+@pytest.mark.parametrize("M,N,K", [(3000, 2900, 1000), (4000, 4000, 4000), (1030, 4100, 1000), (2000, 2000, 2000)])
+def test_gemm_unaligned_shapes_on_padded_tiles(M, N, K):
+    """Off-tile shapes above the padding threshold run zero-padded on the tiled kernels; the fused
+    epilogue (bias, activation) and the residual are padded with them and the corner copied out."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    a, b, bias = _rand(M, K, seed=21), _rand(N, K, seed=22), _rand(N, seed=23)
+    out = gemm_nt(a, b, bias=bias, act="silu", alpha=0.5)
+    _assert_close(out, _ref_gemm(a, b, bias, "silu", alpha=0.5), K)
+    r = _rand(M, N, seed=24)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert gemm_nt(a, b, residual=r, out=out) is out
+    _assert_close(out, _ref_gemm(a, b, residual=r), K)
+    a3, b3 = _rand(2, 1500, 1000, seed=25), _rand(2, 1700, 1000, seed=26)  # batched, above the threshold
+    _assert_close(gemm_nt(a3, b3), _ref_gemm(a3, b3), 1000)
+
+
 @pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4", "w4s"])
 @pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
 def test_gemm_epilogue(variant, act):
