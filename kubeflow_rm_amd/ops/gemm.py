@@ -44,15 +44,22 @@ def _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N
     tm = 256 if big else 128
     Mp, Np, Kp = _round_up(M, tm), _round_up(N, tm), _round_up(K, 64)
     F = torch.nn.functional
-    ap = F.pad(a3, (0, Kp - K, 0, Mp - M))
-    bp = F.pad(b, (0, Kp - K, 0, Np - N))
-    bias_p = F.pad(bias, (0, Np - N)) if bias is not None else None
+
+    def pad(t, cols, rows):  # copy only an operand that is off the grid (e.g. just B for an odd N)
+        return t if cols == 0 and rows == 0 else F.pad(t, (0, cols, 0, rows))
+
+    ap = pad(a3, Kp - K, Mp - M)
+    bp = pad(b, Kp - K, Np - N)
+    bias_p = F.pad(bias, (0, Np - N)) if bias is not None and Np != N else bias
     res_p = None
     if residual is not None:
         r3 = residual.view(batch, M, N) if batched else residual.reshape(M, N)
-        res_p = F.pad(r3, (0, Np - N, 0, Mp - M))
-    cp = gemm_nt(ap, bp, bias=bias_p, residual=res_p, alpha=alpha, act=act)
+        res_p = pad(r3, Np - N, Mp - M)
     c3 = out.view(batch, M, N) if batched else out.view(M, N)
+    if Mp == M and Np == N:  # only K was off the grid: write straight into out
+        gemm_nt(ap, bp, bias=bias_p, residual=res_p, alpha=alpha, act=act, out=c3)
+        return out
+    cp = gemm_nt(ap, bp, bias=bias_p, residual=res_p, alpha=alpha, act=act)
     c3.copy_(cp[..., :M, :N])
     return out
 

@@ -84,6 +84,12 @@ def test_gemm_unaligned_shapes_on_padded_tiles(M, N, K):
     _assert_close(out, _ref_gemm(a, b, residual=r), K)
     a3, b3 = _rand(2, 1500, 1000, seed=25), _rand(2, 1700, 1000, seed=26)  # batched, above the threshold
     _assert_close(gemm_nt(a3, b3), _ref_gemm(a3, b3), 1000)
+    # only N off the grid (an lm_head with an odd vocabulary): A is used in place
+    a2, b2 = _rand(2048, 768, seed=27), _rand(5003, 768, seed=28)
+    _assert_close(gemm_nt(a2, b2), _ref_gemm(a2, b2), 768)
+    # only K off the grid: the tiled kernel writes straight into the output
+    a4, b4 = _rand(2048, 1000, seed=29), _rand(2048, 1000, seed=30)
+    _assert_close(gemm_nt(a4, b4, bias=bias[:0].new_zeros(2048)), _ref_gemm(a4, b4), 1000)
 
 
 @pytest.mark.parametrize("variant", ["fast", "pipe", "generic", "w4", "w4s"])
