@@ -8,8 +8,10 @@ WORLD_SIZE in the env) it launches the N ranks itself (kubeflow_rm_amd.parallel.
 child processes started before this process touches the GPU, private rendezvous port, one failing
 rank stops the rest and fails the run). Each rank is one notebook pod's GPU running
 the K1 readiness op: a bf16 GEMM C = A @ B^T (8192^3 by default) on the hand-written gfx950 MFMA
-kernel. A "step" = one such GEMM on every GPU. W untimed warmup steps, then exactly K timed steps
-bracketed by barrier + device sync on both sides; the slowest rank's time is used. ``value`` is
+kernel. A "step" = one such GEMM on every GPU. ``--prewarm-s`` (default 1 s) of untimed GEMMs settle
+the GPU clock, then W untimed warmup steps, then exactly K timed steps bracketed by barrier + device
+sync on both sides; the slowest rank's time is used. After the timed region rank 0 times
+torch.matmul (hipBLASLt) on the same operands (``torch_matmul_tflops_per_gpu``, never the value). ``value`` is
 the whole-job aggregate TFLOPS (N x per-GEMM FLOPs / max-rank time). Weak scaling: per-GPU work
 is fixed as N grows. Data: synthetic uniform [-1, 1) bf16 operands (random data, not zeros:
 zero operands inflate MFMA clocks — cdna_hip_programming.md §5.4 rule 25).
