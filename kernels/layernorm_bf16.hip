@@ -2,7 +2,7 @@
 //
 // SURVEY.md §2.7.2 K2. Memory-bound: the target is the HBM3E roof (~6.3 TB/s achievable).
 //  * Fast path: one 64-lane wave per row, the whole row resident in VGPRs (hidden = 512*VPL,
-//    VPL in {1,2,4,8,16} -> hidden 512..8192), 16-byte bf16x8 loads/stores (Guideline 13),
+//    VPL in {1,2,3,4,5,6,8,10,12,16} -> hidden 512..8192), 16-byte bf16x8 loads/stores,
 //    exact two-pass mean/variance from registers (no re-read of HBM), wave-only reductions
 //    (no LDS, no barriers), 4 rows per 256-thread workgroup -> rows/4 workgroups (>>256 CUs).
 //  * Generic path: one workgroup per row, any hidden size, LDS block reduction.
@@ -298,16 +298,17 @@ __global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restri
 
 inline bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// wave-per-row widths: hidden = 512 * VPL, the powers of two plus the common model widths
+// 1536 / 2560 / 3072 / 5120 / 6144 (VPL 3, 5, 6, 10, 12); anything else takes the block kernel
 inline int vpl_for(int hidden) {
-  switch (hidden) {
-    case 512: return 1;
-    case 1024: return 2;
-    case 2048: return 4;
-    case 4096: return 8;
-    case 8192: return 16;
+  if (hidden % 512) return 0;
+  switch (hidden / 512) {
+    case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 10: case 12: case 16: return hidden / 512;
     default: return 0;
   }
 }
+
+#define KFAMD_FOR_EACH_VPL(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16)
 
 template <bool RMS>
 int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
@@ -323,11 +324,10 @@ int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float*
   if (vec) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (vpl) {
-      case 1: hipLaunchKernelGGL((norm_fwd_wave<1, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
-      case 2: hipLaunchKernelGGL((norm_fwd_wave<2, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
-      case 4: hipLaunchKernelGGL((norm_fwd_wave<4, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
-      case 8: hipLaunchKernelGGL((norm_fwd_wave<8, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
-      case 16: hipLaunchKernelGGL((norm_fwd_wave<16, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+#define KFAMD_NORM_FWD_CASE(V) \
+  case V: hipLaunchKernelGGL((norm_fwd_wave<V, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      KFAMD_FOR_EACH_VPL(KFAMD_NORM_FWD_CASE)
+#undef KFAMD_NORM_FWD_CASE
     }
   } else {
     hipLaunchKernelGGL((norm_fwd_block<RMS>), dim3(rows), dim3(256), 0, s, xp, gp, bp, yp, mean, rstd, hidden, eps);
@@ -370,11 +370,10 @@ extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const voi
   if (vec) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (vpl) {
-      case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 2: hipLaunchKernelGGL((ln_bwd_dx_wave<2>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 4: hipLaunchKernelGGL((ln_bwd_dx_wave<4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 8: hipLaunchKernelGGL((ln_bwd_dx_wave<8>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 16: hipLaunchKernelGGL((ln_bwd_dx_wave<16>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+#define KFAMD_LN_BWD_CASE(V) \
+  case V: hipLaunchKernelGGL((ln_bwd_dx_wave<V>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      KFAMD_FOR_EACH_VPL(KFAMD_LN_BWD_CASE)
+#undef KFAMD_LN_BWD_CASE
     }
   } else {
     hipLaunchKernelGGL(ln_bwd_dx_block, dim3(rows), dim3(256), 0, s, dyp, xp, gp, mean, rstd, dxp, hidden);
