@@ -35,23 +35,26 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-template <int VPL, bool RMS>
+// W bf16 per lane per unit: 8 (16-byte loads, hidden = 512 * VPL) or 4 (8-byte loads, hidden =
+// 256 * VPL for the widths 256 / 768 / 1280 that are not multiples of 512)
+template <int VPL, bool RMS, int W = 8>
 __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ x,
                                                     const __bf16* __restrict__ gamma,
                                                     const __bf16* __restrict__ beta,
                                                     __bf16* __restrict__ y, float* __restrict__ mean_out,
                                                     float* __restrict__ rstd_out, int rows, float eps) {
-  constexpr int H = VPL * 512;
+  using vec_t = __bf16 __attribute__((ext_vector_type(W)));
+  constexpr int H = VPL * 64 * W;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;  // wave-uniform; no barriers below
-  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)row * H);
+  const vec_t* xr = reinterpret_cast<const vec_t*>(x + (long long)row * H);
   // hidden 8192: the row stays resident as packed bf16 (64 data VGPRs instead of 128 fp32), so 4
   // waves per SIMD instead of 2 keep more rows in flight: +6-8 % at 8192 / 32768 x 8192. At
   // hidden <= 4096 the fp32 copy already allows 4+ waves and re-widening measured 0-8 % slower
   // (profiles/r2_ln_occupancy), so there the compiler keeps the widened values.
   constexpr bool kRepack = VPL >= 16;
-  bf16x8 v[VPL];
+  vec_t v[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) v[j] = __builtin_nontemporal_load(&xr[j * 64 + lane]);  // streamed once
   float mean = 0.f;
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < VPL; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += (float)v[j][e];
+      for (int e = 0; e < W; ++e) s += (float)v[j][e];
     mean = wave_sum(s) * (1.f / H);
   }
   // an empty asm "redefines" the packed row before each later pass, so the compiler widens it again
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
 #pragma unroll
   for (int j = 0; j < VPL; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < W; ++e) {
       const float d = (float)v[j][e] - mean;
       ss += d * d;
     }
@@ -84,17 +87,17 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   if constexpr (kRepack)
 #pragma unroll
     for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
-  const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
-  const bf16x8* b8 = reinterpret_cast<const bf16x8*>(beta);
-  bf16x8* yr = reinterpret_cast<bf16x8*>(y + (long long)row * H);
+  const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
+  const vec_t* b8 = reinterpret_cast<const vec_t*>(beta);
+  vec_t* yr = reinterpret_cast<vec_t*>(y + (long long)row * H);
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
-    const bf16x8 g = g8[j * 64 + lane];
-    bf16x8 b;
+    const vec_t g = g8[j * 64 + lane];
+    vec_t b;
     if (!RMS && beta) b = b8[j * 64 + lane];
-    bf16x8 o;
+    vec_t o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < W; ++e) {
       float r = ((float)v[j][e] - mean) * rstd * (float)g[e];
       if (!RMS && beta) r += (float)b[e];
       o[e] = (__bf16)r;
@@ -297,6 +300,7 @@ __global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restri
 }
 
 inline bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline bool a8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 
 // wave-per-row widths: hidden = 512 * VPL, the powers of two plus the common model widths
 // 1536 / 2560 / 3072 / 5120 / 6144 (VPL 3, 5, 6, 10, 12); anything else takes the block kernel
@@ -309,6 +313,13 @@ inline int vpl_for(int hidden) {
 }
 
 #define KFAMD_FOR_EACH_VPL(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16)
+
+// forward only: hidden = 256 * {1, 3, 5} with 8-byte rows (e.g. 768, the BERT-base / GPT-2 width)
+inline int vpl4_for(int hidden) {
+  if (hidden % 256 || hidden % 512 == 0) return 0;
+  const int v = hidden / 256;
+  return (v == 1 || v == 3 || v == 5) ? v : 0;
+}
 
 template <bool RMS>
 int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
@@ -328,6 +339,13 @@ int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float*
   case V: hipLaunchKernelGGL((norm_fwd_wave<V, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
       KFAMD_FOR_EACH_VPL(KFAMD_NORM_FWD_CASE)
 #undef KFAMD_NORM_FWD_CASE
+    }
+  } else if (const int v4 = vpl4_for(hidden); v4 && a8(x) && a8(gamma) && a8(y) && (!beta || a8(beta))) {
+    dim3 grid((rows + 3) / 4), block(256);
+    switch (v4) {
+      case 1: hipLaunchKernelGGL((norm_fwd_wave<1, RMS, 4>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 3: hipLaunchKernelGGL((norm_fwd_wave<3, RMS, 4>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+      case 5: hipLaunchKernelGGL((norm_fwd_wave<5, RMS, 4>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
     }
   } else {
     hipLaunchKernelGGL((norm_fwd_block<RMS>), dim3(rows), dim3(256), 0, s, xp, gp, bp, yp, mean, rstd, hidden, eps);

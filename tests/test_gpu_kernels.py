@@ -128,7 +128,7 @@ def test_linear_autograd():
 
 
 @pytest.mark.parametrize("rows,H", [(64, 512), (128, 4096), (33, 8192), (10, 1000), (7, 3), (65, 1536), (40, 2560),
-                                    (37, 3072), (19, 5120), (23, 6144)])
+                                    (37, 3072), (19, 5120), (23, 6144), (50, 768), (9, 256), (31, 1280)])
 def test_layernorm_fwd_bwd(rows, H):
     from kubeflow_rm_amd.ops import layer_norm
     x = (_rand(rows, H, seed=15, scale=3.0).float() + 1.5).to(torch.bfloat16).requires_grad_(True)
@@ -146,7 +146,7 @@ def test_layernorm_fwd_bwd(rows, H):
     assert (b.grad.float() - br.grad).abs().max().item() < 2e-2 * (br.grad.abs().max().item() + 1)
 
 
-@pytest.mark.parametrize("rows,H", [(64, 4096), (5, 777), (41, 3072), (9, 6144)])
+@pytest.mark.parametrize("rows,H", [(64, 4096), (5, 777), (41, 3072), (9, 6144), (26, 768)])
 def test_rmsnorm(rows, H):
     from kubeflow_rm_amd.ops import rms_norm
     x, w = _rand(rows, H, seed=19), _rand(H, seed=20)
