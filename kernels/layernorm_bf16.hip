@@ -140,31 +140,32 @@ __global__ __launch_bounds__(256) void norm_fwd_block(const __bf16* __restrict__
 }
 
 // ---- backward: dx ---------------------------------------------------------------------------
-template <int VPL>
+template <int VPL, int W = 8>  // W as in norm_fwd_wave
 __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__ dy,
                                                      const __bf16* __restrict__ x,
                                                      const __bf16* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
                                                      __bf16* __restrict__ dx, int rows) {
-  constexpr int H = VPL * 512;
+  using vec_t = __bf16 __attribute__((ext_vector_type(W)));
+  constexpr int H = VPL * 64 * W;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)row * H);
-  const bf16x8* dyr = reinterpret_cast<const bf16x8*>(dy + (long long)row * H);
-  const bf16x8* g8 = reinterpret_cast<const bf16x8*>(gamma);
+  const vec_t* xr = reinterpret_cast<const vec_t*>(x + (long long)row * H);
+  const vec_t* dyr = reinterpret_cast<const vec_t*>(dy + (long long)row * H);
+  const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
   const float mu = mean[row], rs = rstd[row];
-  bf16x8* dxr = reinterpret_cast<bf16x8*>(dx + (long long)row * H);
+  vec_t* dxr = reinterpret_cast<vec_t*>(dx + (long long)row * H);
   if constexpr (VPL < 16) {
     // the widened row (xhat, gamma * dy) stays in registers between the passes
-    float xh[VPL][8], gd[VPL][8];
+    float xh[VPL][W], gd[VPL][W];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-      const bf16x8 xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
+      const vec_t xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < W; ++e) {
         xh[j][e] = ((float)xv[e] - mu) * rs;
         gd[j][e] = (float)dv[e] * (float)gv[e];
         s1 += gd[j][e] * xh[j][e];
@@ -174,16 +175,16 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
     const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-      bf16x8 o;
+      vec_t o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
+      for (int e = 0; e < W; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
       dxr[j * 64 + lane] = o;
     }
   } else {
     // hidden 8192: x and dy stay packed bf16 between the two passes (8 VGPRs per 8 columns
     // instead of 16 fp32: 2 waves per SIMD instead of 1); the second pass widens them again and
     // re-reads gamma, which every row shares (L2-resident)
-    bf16x8 xv[VPL], dv[VPL];
+    vec_t xv[VPL], dv[VPL];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
@@ -192,9 +193,9 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-      const bf16x8 gv = g8[j * 64 + lane];
+      const vec_t gv = g8[j * 64 + lane];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < W; ++e) {
         const float xh = ((float)xv[j][e] - mu) * rs, gd = (float)dv[j][e] * (float)gv[e];
         s1 += gd * xh;
         s2 += gd;
@@ -208,10 +209,10 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-      const bf16x8 gv = g8[j * 64 + lane];
-      bf16x8 o;
+      const vec_t gv = g8[j * 64 + lane];
+      vec_t o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < W; ++e) {
         const float xh = ((float)xv[j][e] - mu) * rs, gd = (float)dv[j][e] * (float)gv[e];
         o[e] = (__bf16)(rs * (gd - xh * c1 - c2));
       }
@@ -314,7 +315,7 @@ inline int vpl_for(int hidden) {
 
 #define KFAMD_FOR_EACH_VPL(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16)
 
-// forward only: hidden = 256 * {1, 3, 5} with 8-byte rows (e.g. 768, the BERT-base / GPT-2 width)
+// hidden = 256 * {1, 3, 5} with 8-byte rows (e.g. 768, the BERT-base / GPT-2 width)
 inline int vpl4_for(int hidden) {
   if (hidden % 256 || hidden % 512 == 0) return 0;
   const int v = hidden / 256;
@@ -392,6 +393,13 @@ extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const voi
   case V: hipLaunchKernelGGL((ln_bwd_dx_wave<V>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
       KFAMD_FOR_EACH_VPL(KFAMD_LN_BWD_CASE)
 #undef KFAMD_LN_BWD_CASE
+    }
+  } else if (const int v4 = vpl4_for(hidden); v4 && a8(dy) && a8(x) && a8(gamma) && a8(dx)) {
+    dim3 grid((rows + 3) / 4), block(256);
+    switch (v4) {
+      case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 3: hipLaunchKernelGGL((ln_bwd_dx_wave<3, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 5: hipLaunchKernelGGL((ln_bwd_dx_wave<5, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
     }
   } else {
     hipLaunchKernelGGL(ln_bwd_dx_block, dim3(rows), dim3(256), 0, s, dyp, xp, gp, mean, rstd, dxp, hidden);
