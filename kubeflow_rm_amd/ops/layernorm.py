@@ -28,15 +28,46 @@ def layer_norm_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | N
     return y.view(x.shape), mean, rstd
 
 
-def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+def rms_norm_fwd(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6, save_stats: bool = False):
     _check_operand(x, "x")
     H = x.shape[-1]
     x2 = x.reshape(-1, H).contiguous()
     y = torch.empty_like(x2)
+    rstd = torch.empty(x2.shape[0], dtype=torch.float32, device=x.device) if save_stats else None
     rc = _lib.lib().kfamd_rmsnorm_fwd_bf16(x2.data_ptr(), weight.contiguous().data_ptr(), y.data_ptr(),
-                                           None, x2.shape[0], H, float(eps), _stream_ptr(x))
+                                           rstd.data_ptr() if rstd is not None else None, x2.shape[0], H,
+                                           float(eps), _stream_ptr(x))
     _lib.check(rc, f"rmsnorm_fwd[{x2.shape[0]}x{H}]")
-    return y.view(x.shape)
+    return y.view(x.shape), rstd
+
+
+class _RMSNorm(torch.autograd.Function):
+    """Forward on the HIP kernel (fp32 rstd saved); backward from the saved rstd:
+    dx = rstd * (w*dy - xhat * mean(w*dy*xhat)), dw = sum(dy * xhat), xhat = x * rstd."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        y, rstd = rms_norm_fwd(x, weight, eps, save_stats=True)
+        ctx.save_for_backward(x, weight, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, rstd = ctx.saved_tensors
+        H = x.shape[-1]
+        xf = x.reshape(-1, H).float()
+        r = rstd.unsqueeze(-1)
+        xhat = xf * r
+        gyf = gy.reshape(-1, H).float()
+        gdy = gyf * weight.float()
+        dx = r * (gdy - xhat * (gdy * xhat).mean(-1, keepdim=True))
+        dw = (gyf * xhat).sum(0)
+        return dx.to(x.dtype).view(x.shape), dw.to(weight.dtype), None
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    """Autograd-aware RMSNorm over the last dim (bf16 I/O, fp32 statistics)."""
+    return _RMSNorm.apply(x, weight, eps)
 
 
 class _LayerNorm(torch.autograd.Function):

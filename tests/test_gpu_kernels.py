@@ -154,6 +154,14 @@ def test_rmsnorm(rows, H):
     xf = x.float()
     ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * w.float()
     assert (y.float() - ref).abs().max().item() < 3e-2
+    # backward (dx, dw) against fp32 autograd
+    xg, wg = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    gy = _rand(rows, H, seed=31)
+    rms_norm(xg, wg, 1e-6).backward(gy)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr).backward(gy.float())
+    assert (xg.grad.float() - xr.grad).abs().max().item() <= 2e-2 * xr.grad.abs().max().item() + 1e-2
+    assert (wg.grad.float() - wr.grad).abs().max().item() <= 2e-2 * wr.grad.abs().max().item() + 1e-2
 
 
 def test_gemm_w4_needs_16b_output_rows():
