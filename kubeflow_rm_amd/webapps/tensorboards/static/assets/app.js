@@ -26,10 +26,29 @@
       const p = String(path || "").trim();
       return kind === "pvc" ? `pvc://${pvc}/${p.replace(/^\/+/, "")}` : p;
     },
-    validate(name, kind, pvc, path) {
+    // pages/index/index.component.ts processIncomingData: per-row action states (delete is held while
+    // the object terminates, connect only once the server is ready) and the age cell's tooltip.
+    process(rows) {
+      return rows.map((t) => {
+        const r = JSON.parse(JSON.stringify(t));
+        r.deleteAction = r.status.phase === "terminating" ? "terminating" : "ready";
+        r.connectAction = r.status.phase === "ready" ? "ready" : "unavailable";
+        if (r.age && typeof r.age === "object") { r.ageValue = r.age.uptime; r.ageTooltip = r.age.timestamp; }
+        return r;
+      });
+    },
+    // Optimistic row state after an accepted DELETE, until the next poll sees the object go.
+    markDeleting(r) {
+      r.status = Object.assign({}, r.status, { phase: "terminating", message: "Preparing to delete the Tensorboard object..." });
+      r.deleteAction = "unavailable";
+      return r;
+    },
+    // pages/form/form.component.ts: names already taken in the namespace are rejected client-side.
+    validate(name, kind, pvc, path, taken) {
       const errs = [];
       const n = kf.validators.name(name);
       if (n) errs.push(n);
+      else if (taken && taken.has(name)) errs.push(`TensorBoard ${name} already exists`);
       if (kind === "pvc" && !pvc) errs.push("Select a PVC");
       if (kind !== "pvc" && !/^(s3|gs):\/\/[^/]+/.test(String(path || "").trim())) errs.push("Object store paths look like s3://bucket/path or gs://bucket/path");
       return errs;
@@ -38,7 +57,7 @@
 
   function app() {
     const $ = (id) => document.getElementById(id);
-    let poller = null, table = null;
+    let poller = null, table = null, rows = [];
     async function namespaces() {
       let list = [];
       try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
@@ -50,11 +69,13 @@
     function tableConfig() {
       return {
         columns: TWA.columns(false), empty: "No TensorBoards in this namespace.",
-        actions: [{ name: "connect", label: "Connect", enabled: (r) => r.status.phase === "ready" }, { name: "delete", label: "Delete" }],
+        actions: [{ name: "connect", label: "Connect", enabled: (r) => r.connectAction === "ready" },
+                  { name: "delete", label: "Delete", enabled: (r) => r.deleteAction === "ready" }],
         onAction: async (name, r) => {
           if (name === "connect") window.open(`/tensorboard/${r.namespace}/${r.name}/`);
           if (name === "delete") {
-            await kf.confirmDialog(TWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${r.namespace}/tensorboards/${r.name}`));
+            const ok = await kf.confirmDialog(TWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${r.namespace}/tensorboards/${r.name}`));
+            if (ok === "accept") { TWA.markDeleting(r); table.setRows(rows); }
             poller.reset();
           }
         },
@@ -64,7 +85,8 @@
       const ns = kf.namespace();
       if (!ns) return null;
       const { tensorboards } = await kf.call("GET", `/api/namespaces/${ns}/tensorboards`);
-      table.setRows(tensorboards.map((t) => Object.assign({ namespace: ns }, t)));
+      rows = TWA.process(tensorboards.map((t) => Object.assign({ namespace: ns }, t)));
+      table.setRows(rows);
       return tensorboards.map((t) => [t.name, t.status.phase]);
     }
     async function open() {
@@ -80,7 +102,8 @@
       if (ev.submitter && ev.submitter.value !== "ok") return;
       ev.preventDefault();
       const ns = kf.namespace(), kind = $("f-kind").value;
-      const errs = TWA.validate($("f-name").value, kind, $("f-pvc").value, $("f-path").value);
+      const taken = new Set(rows.map((r) => r.name));
+      const errs = TWA.validate($("f-name").value, kind, $("f-pvc").value, $("f-path").value, taken);
       if (errs.length) { $("f-error").textContent = errs.join("; "); return; }
       const logspath = TWA.logspath(kind, $("f-pvc").value, $("f-path").value);
       const configurations = [...$("f-configs").querySelectorAll("input:checked")].map((i) => i.value);

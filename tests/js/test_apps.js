@@ -162,6 +162,17 @@ test("TWA index page: every TensorBoard name in name order with the reference st
   assert.strictEqual(TWA.logspath("object", "", " s3://b/run "), "s3://b/run");
   assert.deepStrictEqual(TWA.validate("tb", "object", "", "s3://bucket/x"), []);
   assert.strictEqual(TWA.validate("tb", "object", "", "/local").length, 1);
+  assert.deepStrictEqual(TWA.validate("tb", "object", "", "s3://bucket/x", new Set(["tb"])), ["TensorBoard tb already exists"]);
+  // index.component.ts processIncomingData: action states follow the phase; age split into value/tooltip
+  const [ready, term, wait] = TWA.process([
+    { name: "a", status: { phase: "ready" }, age: { uptime: "2 min", timestamp: "2024-01-01T00:00:00Z" } },
+    { name: "b", status: { phase: "terminating" } }, { name: "c", status: { phase: "waiting" } }]);
+  assert.deepStrictEqual([ready.connectAction, ready.deleteAction, ready.ageValue, ready.ageTooltip],
+                         ["ready", "ready", "2 min", "2024-01-01T00:00:00Z"]);
+  assert.deepStrictEqual([term.connectAction, term.deleteAction], ["unavailable", "terminating"]);
+  assert.deepStrictEqual([wait.connectAction, wait.deleteAction], ["unavailable", "ready"]);
+  const gone = TWA.markDeleting(ready);
+  assert.deepStrictEqual([gone.status.phase, gone.deleteAction], ["terminating", "unavailable"]);
 });
 
 test("resource table: header click order, numeric sort, filter, escaping", () => {
