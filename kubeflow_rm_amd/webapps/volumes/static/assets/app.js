@@ -41,6 +41,22 @@
       const v = VWA.viewerState(row);
       return v.status === "ready" ? "Open browser" : v.status === "uninitialized" ? "Browse" : `Browser ${v.status}`;
     },
+    // Button states of index-default.component.ts parseIncomingData. `waiting` is the set of claims
+    // whose viewer the user asked for; their window opens (autoOpen) once the viewer is ready.
+    actionStates(row, waiting) {
+      const v = VWA.viewerState(row), phase = row.status.phase;
+      const deleteAction = (row.notebooks || []).length ? "unavailable" : phase === "terminating" ? "terminating" : "ready";
+      // a claim that is only waiting for its first consumer may get the viewer as that consumer
+      const firstConsumer = phase === "unavailable" && row.status.state === "WaitForFirstConsumer";
+      let openAction = v.status, autoOpen = false;
+      if (phase !== "ready" && !firstConsumer) openAction = "unavailable";
+      else if (waiting && waiting.has(row.name)) {
+        if (v.status === "ready") { autoOpen = true; waiting.delete(row.name); }
+        else if (v.status === "uninitialized" || v.status === "waiting") openAction = "waiting";
+      }
+      const closeAction = v.status === "uninitialized" ? "unavailable" : v.status === "terminating" ? "waiting" : "ready";
+      return { deleteAction, openAction, closeAction, autoOpen };
+    },
     newPvcBody(name, size, mode, storageClass) {
       return { name, size: /[A-Za-z]$/.test(String(size)) ? String(size) : `${size}Gi`, mode, class: storageClass || "{empty}", type: "empty" };
     },
@@ -55,7 +71,9 @@
 
   function app() {
     const $ = (id) => document.getElementById(id);
-    let poller = null, table = null;
+    let poller = null, table = null, rows = [];
+    const waiting = new Set();
+    const openViewer = (r) => window.open(VWA.viewerState(r).url, `${r.name}: Volumes Viewer`, "height=600,width=800");
     async function namespaces() {
       let list = [];
       try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
@@ -96,21 +114,35 @@
       return {
         columns: VWA.columns(false), empty: "No volumes in this namespace.",
         actions: [
-          { name: "browse", label: (r) => VWA.browseLabel(r), enabled: (r) => ["ready", "uninitialized"].includes(VWA.viewerState(r).status) },
-          { name: "close", label: "Close browser", enabled: (r) => VWA.viewerState(r).status !== "uninitialized" },
-          { name: "delete", label: "Delete" },
+          { name: "browse", label: (r) => (r.openAction === "waiting" ? "Starting browser" : VWA.browseLabel(r)),
+            enabled: (r) => ["ready", "uninitialized"].includes(r.openAction) },
+          { name: "close", label: "Close browser", enabled: (r) => r.closeAction === "ready" },
+          { name: "delete", label: "Delete", enabled: (r) => r.deleteAction === "ready" },
         ],
-        onOpen: (r) => showDetails(r.namespace, r.name),
+        onOpen: (r) => (r.status.phase === "terminating" ? kf.snack("PVC is unavailable now.", "WARNING") : showDetails(r.namespace, r.name)),
         onAction: (name, r) => {
           const ns = r.namespace, v = VWA.viewerState(r);
           if (name === "browse") {
-            if (v.status === "ready" && v.url) window.open(v.url);
-            else if (v.status === "uninitialized") act("POST", `/api/namespaces/${ns}/viewers`, { name: r.name });
+            if (v.status === "ready" && v.url) openViewer(r);
+            else if (v.status === "uninitialized") {
+              waiting.add(r.name); r.openAction = "waiting"; table.setRows(rows);
+              kf.call("POST", `/api/namespaces/${ns}/viewers`, { name: r.name })
+                .catch((e) => { waiting.delete(r.name); kf.snack(e.message, "ERROR"); }).then(() => poller.reset());
+            }
           }
           if (name === "close")
-            kf.confirmDialog(VWA.dialogs.closeViewer(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/viewers/${r.name}`)).then(() => poller.reset());
+            kf.confirmDialog(VWA.dialogs.closeViewer(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/viewers/${r.name}`)).then((resp) => {
+              if (resp === "accept") { waiting.delete(r.name); r.closeAction = "waiting"; table.setRows(rows); }
+              poller.reset();
+            });
           if (name === "delete")
-            kf.confirmDialog(VWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/pvcs/${r.name}`)).then(() => poller.reset());
+            kf.confirmDialog(VWA.dialogs.delete(r.name), () => kf.call("DELETE", `/api/namespaces/${ns}/pvcs/${r.name}`)).then((resp) => {
+              if (resp === "accept") {
+                r.status = Object.assign({}, r.status, { phase: "terminating", message: "Preparing to delete the Volume..." });
+                r.deleteAction = "unavailable"; waiting.delete(r.name); table.setRows(rows);
+              }
+              poller.reset();
+            });
         },
       };
     }
@@ -118,7 +150,12 @@
       const ns = kf.namespace();
       if (!ns) return null;
       const { pvcs } = await kf.call("GET", `/api/namespaces/${ns}/pvcs`);
-      table.setRows(pvcs.map((p) => Object.assign({ namespace: ns }, p)));
+      rows = pvcs.map((p) => {
+        const r = Object.assign({ namespace: ns }, p), st = VWA.actionStates(r, waiting);
+        if (st.autoOpen) openViewer(r);
+        return Object.assign(r, st);
+      });
+      table.setRows(rows);
       return pvcs.map((p) => [p.name, p.status.phase, VWA.viewerState(p).status]);
     }
     async function open() {

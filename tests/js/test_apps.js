@@ -153,6 +153,22 @@ test("VWA index page: every PVC name in name order with the reference status ico
   assert.deepStrictEqual(VWA.newPvcBody("v1", "10", "ReadWriteOnce", ""), { name: "v1", size: "10Gi", mode: "ReadWriteOnce", class: "{empty}", type: "empty" });
   assert.deepStrictEqual(VWA.validate("ok-name", "5"), []);
   assert.strictEqual(VWA.validate("ok-name", "five").length, 1);
+  // index-default.component.ts button states: in-use claims cannot be deleted, a claim waiting for its
+  // first consumer may start a viewer, a requested viewer shows "waiting" and opens once ready
+  const row = (phase, viewer, extra) => Object.assign({ name: "v", status: { phase }, viewer, notebooks: [] }, extra || {});
+  assert.strictEqual(VWA.actionStates(row("ready", { status: "uninitialized" }, { notebooks: ["nb"] })).deleteAction, "unavailable");
+  assert.strictEqual(VWA.actionStates(row("terminating", { status: "uninitialized" })).deleteAction, "terminating");
+  assert.strictEqual(VWA.actionStates(row("waiting", { status: "uninitialized" })).openAction, "unavailable");
+  const wffc = row("unavailable", { status: "uninitialized" });
+  wffc.status.state = "WaitForFirstConsumer";
+  assert.strictEqual(VWA.actionStates(wffc).openAction, "uninitialized");
+  const w = new Set(["v"]);
+  assert.deepStrictEqual(VWA.actionStates(row("ready", { status: "waiting" }), w),
+                         { deleteAction: "ready", openAction: "waiting", closeAction: "ready", autoOpen: false });
+  assert.strictEqual(VWA.actionStates(row("ready", { status: "ready", url: "/u" }), w).autoOpen, true);
+  assert.strictEqual(w.has("v"), false);
+  assert.strictEqual(VWA.actionStates(row("ready", { status: "terminating" })).closeAction, "waiting");
+  assert.strictEqual(VWA.actionStates(row("ready", { status: "uninitialized" })).closeAction, "unavailable");
 });
 
 test("TWA index page: every TensorBoard name in name order with the reference status icons", () => {
