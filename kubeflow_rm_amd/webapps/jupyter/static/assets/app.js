@@ -147,12 +147,30 @@
     },
     // the union of several namespaces' notebook lists (all-namespaces view)
     merge(lists) { return [].concat(...lists); },
+    // index-default.component.ts updateNotebookFields: button states derived from the phase
+    // (start/stop "uninitialized" = the Stop form of the toggle, "ready" = Start).
+    actionStates(r) {
+      const p = r.status.phase;
+      return {
+        deleteAction: p === "terminating" ? "terminating" : "ready",
+        connectAction: p === "ready" ? "ready" : "unavailable",
+        startStopAction: p === "ready" ? "uninitialized" : p === "stopped" ? "ready" : p === "terminating" ? "unavailable" : "uninitialized",
+      };
+    },
+    // Optimistic row after an accepted action, until the next poll (startNotebook/stopNotebook/delete).
+    markPending(r, what) {
+      const next = { delete: ["terminating", "Preparing to delete the Notebook."],
+                     start: ["waiting", "Starting the Notebook Server."],
+                     stop: ["waiting", "Preparing to stop the Notebook Server."] }[what];
+      r.status = Object.assign({}, r.status, { phase: next[0], message: next[1] });
+      return Object.assign(r, JWA.actionStates(r));
+    },
   };
 
   // ---- DOM ------------------------------------------------------------------------------------
   function app() {
     const $ = (id) => document.getElementById(id);
-    let config = null, poller = null, table = null, namespaces = [], form = null;
+    let config = null, poller = null, table = null, namespaces = [], form = null, rows = [];
 
     async function loadNamespaces() {
       try { namespaces = (await kf.call("GET", "/api/namespaces")).namespaces; }
@@ -174,19 +192,23 @@
       return {
         columns: JWA.columns(allNs), empty: "No notebooks in this namespace.",
         actions: [
-          { name: "connect", label: "Connect", enabled: (r) => r.status.phase === "ready" },
-          { name: "toggle", label: (r) => (r.status.phase === "stopped" ? "Start" : "Stop") },
-          { name: "delete", label: "Delete" },
+          { name: "connect", label: "Connect", enabled: (r) => r.connectAction === "ready" },
+          { name: "toggle", label: (r) => (r.status.phase === "stopped" ? "Start" : "Stop"), enabled: (r) => r.startStopAction !== "unavailable" },
+          { name: "delete", label: "Delete", enabled: (r) => r.deleteAction === "ready" },
         ],
-        onOpen: (r) => showDetails(r.namespace, r.name),
+        onOpen: (r) => (r.status.phase === "terminating"
+          ? kf.snack("Notebook is being deleted, cannot show details.", "INFO") : showDetails(r.namespace, r.name)),
         onAction: (name, r) => {
           if (name === "connect") window.open(`/notebook/${r.namespace}/${r.name}/`);
           const url = `/api/namespaces/${r.namespace}/notebooks/${r.name}`;
           // starting needs no confirmation; stopping and deleting go through the confirm dialog,
           // which stays open with the backend's error if the call fails
-          if (name === "toggle" && r.status.phase === "stopped") act("PATCH", r.namespace, r.name, { stopped: false });
-          else if (name === "toggle") kf.confirmDialog(JWA.dialogs.stop(r.name), () => kf.call("PATCH", url, { stopped: true })).then(() => poller.reset());
-          if (name === "delete") kf.confirmDialog(JWA.dialogs.delete(r.name), () => kf.call("DELETE", url)).then(() => poller.reset());
+          const pending = (what) => (resp) => { if (resp === "accept") { JWA.markPending(r, what); table.setRows(rows); } poller.reset(); };
+          if (name === "toggle" && r.status.phase === "stopped") {
+            JWA.markPending(r, "start"); table.setRows(rows);
+            act("PATCH", r.namespace, r.name, { stopped: false });
+          } else if (name === "toggle") kf.confirmDialog(JWA.dialogs.stop(r.name), () => kf.call("PATCH", url, { stopped: true })).then(pending("stop"));
+          if (name === "delete") kf.confirmDialog(JWA.dialogs.delete(r.name), () => kf.call("DELETE", url)).then(pending("delete"));
         },
       };
     }
@@ -194,8 +216,9 @@
     async function refresh() {
       const list = allNs ? namespaces : [kf.namespace()].filter(Boolean);
       if (!list.length) return null;
-      const rows = JWA.merge(await Promise.all(list.map(async (ns) =>
-        (await kf.call("GET", `/api/namespaces/${ns}/notebooks`)).notebooks.map((r) => Object.assign({ namespace: ns }, r)))));
+      rows = JWA.merge(await Promise.all(list.map(async (ns) =>
+        (await kf.call("GET", `/api/namespaces/${ns}/notebooks`)).notebooks.map((r) => Object.assign({ namespace: ns }, r)))))
+        .map((r) => Object.assign(r, JWA.actionStates(r)));
       table.setRows(rows);
       return rows.map((r) => [r.namespace, r.name, r.status.phase]);
     }

@@ -171,6 +171,18 @@ test("VWA index page: every PVC name in name order with the reference status ico
   assert.strictEqual(VWA.actionStates(row("ready", { status: "uninitialized" })).closeAction, "unavailable");
 });
 
+test("JWA index page: reference action states and optimistic rows", () => {
+  const st = (phase) => JWA.actionStates({ status: { phase } });
+  assert.deepStrictEqual(st("ready"), { deleteAction: "ready", connectAction: "ready", startStopAction: "uninitialized" });
+  assert.deepStrictEqual(st("stopped"), { deleteAction: "ready", connectAction: "unavailable", startStopAction: "ready" });
+  assert.deepStrictEqual(st("terminating"), { deleteAction: "terminating", connectAction: "unavailable", startStopAction: "unavailable" });
+  assert.strictEqual(st("waiting").startStopAction, "uninitialized");
+  const r = JWA.markPending({ name: "nb", status: { phase: "ready" } }, "stop");
+  assert.deepStrictEqual([r.status.phase, r.status.message, r.connectAction], ["waiting", "Preparing to stop the Notebook Server.", "unavailable"]);
+  assert.strictEqual(JWA.markPending({ status: { phase: "ready" } }, "delete").deleteAction, "terminating");
+  assert.strictEqual(JWA.markPending({ status: { phase: "stopped" } }, "start").status.message, "Starting the Notebook Server.");
+});
+
 test("TWA index page: every TensorBoard name in name order with the reference status icons", () => {
   const tbs = fixture("tensorboards", "tensorboards").tensorboards;
   checkTable(tbs, TWA.columns(false));
