@@ -95,6 +95,9 @@
         kf.call("GET", `/api/namespaces/${ns}/poddefaults`)]);
       $("f-pvc").innerHTML = pvcs.map((p) => `<option>${kf.esc(p)}</option>`).join("");
       $("f-configs").innerHTML = poddefaults.map((pd) => `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"> ${kf.esc(pd.desc)}</label><br>`).join("");
+      // form.component.ts: object store is the default; the PVC picker shows only for PVC storage
+      const kind = () => { $("f-pvc-row").hidden = $("f-kind").value !== "pvc"; };
+      $("f-kind").onchange = kind; kind();
       $("f-error").textContent = "";
       $("dlg").showModal();
     }
