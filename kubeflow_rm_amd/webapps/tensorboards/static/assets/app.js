@@ -58,17 +58,26 @@
   function app() {
     const $ = (id) => document.getElementById(id);
     let poller = null, table = null, rows = [];
+    // "All namespaces" (index.component.ts polls getTensorBoards(ns) with an array): rows of every
+    // namespace, merged, with a Namespace column; creating still targets one namespace.
+    const ALL = "__all__";
+    let list = [], allNs = false;
     async function namespaces() {
-      let list = [];
       try { list = (await kf.call("GET", "/api/namespaces")).namespaces; } catch (e) { list = kf.namespace() ? [kf.namespace()] : []; }
-      $("ns").innerHTML = list.map((n) => `<option value="${kf.esc(n)}">${kf.esc(n)}</option>`).join("");
+      $("ns").innerHTML = list.map((n) => `<option value="${kf.esc(n)}">${kf.esc(n)}</option>`).join("") +
+        (list.length > 1 ? `<option value="${ALL}">All namespaces</option>` : "");
       if (!kf.namespace() && list.length) kf.setNamespace(list[0]);
       $("ns").value = kf.namespace();
-      $("ns").onchange = () => kf.setNamespace($("ns").value);
+      $("ns").onchange = () => {
+        allNs = $("ns").value === ALL;
+        table = new kf.ResourceTable($("rows"), tableConfig());
+        $("new").disabled = allNs;
+        if (allNs) poller.reset(); else kf.setNamespace($("ns").value);
+      };
     }
     function tableConfig() {
       return {
-        columns: TWA.columns(false), empty: "No TensorBoards in this namespace.",
+        columns: TWA.columns(allNs), empty: allNs ? "No TensorBoards in any namespace." : "No TensorBoards in this namespace.",
         actions: [{ name: "connect", label: "Connect", enabled: (r) => r.connectAction === "ready" },
                   { name: "delete", label: "Delete", enabled: (r) => r.deleteAction === "ready" }],
         onAction: async (name, r) => {
@@ -82,12 +91,13 @@
       };
     }
     async function refresh() {
-      const ns = kf.namespace();
-      if (!ns) return null;
-      const { tensorboards } = await kf.call("GET", `/api/namespaces/${ns}/tensorboards`);
-      rows = TWA.process(tensorboards.map((t) => Object.assign({ namespace: ns }, t)));
+      const nss = allNs ? list : [kf.namespace()].filter(Boolean);
+      if (!nss.length) return null;
+      const per = await Promise.all(nss.map(async (ns) =>
+        (await kf.call("GET", `/api/namespaces/${ns}/tensorboards`)).tensorboards.map((t) => Object.assign({ namespace: ns }, t))));
+      rows = TWA.process([].concat(...per));
       table.setRows(rows);
-      return tensorboards.map((t) => [t.name, t.status.phase]);
+      return rows.map((t) => [t.namespace, t.name, t.status.phase]);
     }
     async function open() {
       const ns = kf.namespace();
@@ -105,7 +115,7 @@
       if (ev.submitter && ev.submitter.value !== "ok") return;
       ev.preventDefault();
       const ns = kf.namespace(), kind = $("f-kind").value;
-      const taken = new Set(rows.map((r) => r.name));
+      const taken = new Set(rows.filter((r) => r.namespace === ns).map((r) => r.name));
       const errs = TWA.validate($("f-name").value, kind, $("f-pvc").value, $("f-path").value, taken);
       if (errs.length) { $("f-error").textContent = errs.join("; "); return; }
       const logspath = TWA.logspath(kind, $("f-pvc").value, $("f-path").value);
@@ -122,7 +132,7 @@
       await namespaces();
       $("new").onclick = open;
       $("form").addEventListener("submit", submit);
-      kf.onNamespace((ns) => { $("ns").value = ns; poller.reset(); });
+      kf.onNamespace((ns) => { if (!allNs) { $("ns").value = ns; poller.reset(); } });
       poller.start();
     })();
   }
