@@ -533,15 +533,23 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 }  // namespace
 
-extern "C" int kfamd_gemm_nt_bf16_w4_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
-                                            int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
-                                            long long ldr, long long sa, long long sb, long long sc, long long sr,
-                                            float alpha, int act, void* stream);
+extern "C" int kfamd_w4_launch_nt(int bm, const void* A, const void* B, void* C, const void* bias, const void* R,
+                                  void* Aux, int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
+                                  long long ldr, long long sa, long long sb, long long sc, long long sr, float alpha,
+                                  int act, void* stream);
+extern "C" int kfamd_w4_launch_t(int la, int lb, int bm, const void* A, const void* B, void* C, const void* R, int M,
+                                 int N, int K, int batch, long long lda, long long ldb, long long ldc, long long ldr,
+                                 long long sa, long long sb, long long sc, long long sr, float alpha, void* stream);
 
-extern "C" int kfamd_gemm_nt_bf16_w4s_launch(const void* A, const void* B, void* C, const void* bias, const void* R,
-                                             int M, int N, int K, int batch, long long lda, long long ldb,
-                                             long long ldc, long long ldr, long long sa, long long sb, long long sc,
-                                             long long sr, float alpha, int act, void* stream);
+namespace {
+// w4 tile choice: the 128x128 tile (two blocks per CU) when the problem has at most half as many
+// 256x256 tiles as MI355X has CUs, or a dimension below 256 (profiles/r1_gemm_w4s: 1024^3 92 -> 206
+// TF, 2048^3 430 -> 848; at 3072^3, 144 tiles, the 256 tile still wins 980 : 904).
+int w4_tile(int M, int N, int batch) {
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
+  return (t256 <= 128 || M < 256 || N < 256) ? 128 : 256;
+}
+}  // namespace
 
 extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* C,
                                           const void* bias, const void* R, int M, int N, int K,
@@ -559,6 +567,16 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   if (R && act != KFAMD_ACT_NONE) return KFAMD_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
+  // w4 / w4s (gemm_bf16_w4.hip): edge tiles in-kernel, so auto takes them for any M, N >= 128 with
+  // N % 8, K % 8 and 16-byte aligned rows; anything else falls through to the r1 kernels below.
+  if (variant == 6 || variant == 9)
+    return kfamd_w4_launch_nt(variant == 6 ? 256 : 128, A, B, C, bias, R, nullptr, M, N, K, batch, lda, ldb, ldc, ldr,
+                              stride_a, stride_b, stride_c, stride_r, alpha, act, stream);
+  if (variant == 0) {
+    const int rc = kfamd_w4_launch_nt(w4_tile(M, N, batch), A, B, C, bias, R, nullptr, M, N, K, batch, lda, ldb, ldc,
+                                      ldr, stride_a, stride_b, stride_c, stride_r, alpha, act, stream);
+    if (rc >= 0) return rc;  // launched (or a HIP launch error)
+  }
   const bool shapes_ok = (M % kBM == 0) && (N % kBN == 0) && (K % kBK == 0);
   const bool align_ok = aligned16(A) && aligned16(B) && aligned16(C) && (lda % 8 == 0) &&
                         (ldb % 8 == 0) && (ldc % 4 == 0) && (stride_a % 8 == 0) &&
@@ -566,21 +584,6 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
                         (!bias || (reinterpret_cast<uintptr_t>(bias) & 7) == 0) &&
                         (!R || ((reinterpret_cast<uintptr_t>(R) & 7) == 0 && ldr % 4 == 0 && stride_r % 4 == 0));
   bool fast = shapes_ok && align_ok;
-  // 128x128 w4 tiles: any M, N % 128 (K % 64) with the fast-path alignment. Auto picks them when the
-  // problem has at most half as many 256x256 tiles as MI355X has CUs (256): 2048^2 is 64 tiles of
-  // 256^2 (a quarter of the chip) but 256 of 128^2 at two blocks per CU (profiles/r1_gemm_w4s:
-  // 1024^3 92 -> 206 TF, 2048^3 430 -> 848; at 3072^3, 144 tiles, the 256 tile still wins 980 : 904).
-  const bool shapes128 = (M % 128 == 0) && (N % 128 == 0) && (K % kBK == 0);
-  const long long tiles256 = shapes_ok ? (long long)(M / kBM) * (N / kBN) * batch : 0;
-  const bool w4s_ok = (long long)128 * lda * 2 < (1LL << 31) && (long long)128 * ldb * 2 < (1LL << 31);
-  // the w4 epilogues store 16 B (8 columns) per lane: C rows must be 16-byte aligned
-  const bool c16 = (ldc % 8 == 0) && (stride_c % 8 == 0);
-  if (variant == 9 || (variant == 0 && align_ok && c16 && shapes128 && w4s_ok && tiles256 <= 128)) {
-    if (!shapes128) return KFAMD_EINVAL;
-    if (!align_ok || !c16) return KFAMD_EALIGN;
-    return kfamd_gemm_nt_bf16_w4s_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
-                                         stride_c, stride_r, alpha, act, stream);
-  }
   if (variant == 1 || variant >= 3) {
     if (!shapes_ok) return KFAMD_EINVAL;
     if (!align_ok) return KFAMD_EALIGN;
@@ -594,14 +597,6 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   __bf16* c = static_cast<__bf16*>(C);
   const __bf16* bs = static_cast<const __bf16*>(bias);
   const __bf16* r = static_cast<const __bf16*>(R);
-  // default fast path: the 4-wave w4 kernel (one wave per SIMD, 5-slot LDS ring; profiles/r1_gemm_w4c);
-  // the 8-wave pipe_sched kernel when a 256-row panel spans >= 2 GiB (w4's 32-bit buffer offsets)
-  const bool w4_ok = (long long)kBM * lda * 2 < (1LL << 31) && (long long)kBN * ldb * 2 < (1LL << 31);
-  if (fast && variant == 6 && !c16) return KFAMD_EALIGN;
-  if (fast && (variant == 6 || (variant == 0 && w4_ok && c16))) {  // 4 waves x 128x128 (gemm_bf16_w4.hip)
-    return kfamd_gemm_nt_bf16_w4_launch(A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
-                                        stride_c, stride_r, alpha, act, stream);
-  }
   if (fast) {
     dim3 grid((M / kBM) * (N / kBN), batch), block(kThreads);
     if (variant == 0 || variant == 4) {  // 8 waves: pipelined + pinned interleave
@@ -632,4 +627,25 @@ extern "C" int kfamd_gemm_nt_bf16(const void* A, const void* B, void* C, const v
                                   float alpha, int act, void* stream) {
   return kfamd_gemm_nt_bf16_variant(0, A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr,
                                     stride_a, stride_b, stride_c, stride_r, alpha, act, stream);
+}
+
+// Layout-general entry (kfamd_kernels.h): la/lb select K-contiguous (0) or k-major (1) operands;
+// Aux = pre-activation second output (NT only). Only the w4 template serves the transposed layouts:
+// an unsupported shape returns KFAMD_EINVAL / KFAMD_EALIGN (callers fall back, never silently).
+extern "C" int kfamd_gemm_bf16_ex(int la, int lb, const void* A, const void* B, void* C, const void* bias,
+                                  const void* R, void* Aux, int M, int N, int K, int batch, long long lda,
+                                  long long ldb, long long ldc, long long ldr, long long stride_a, long long stride_b,
+                                  long long stride_c, long long stride_r, float alpha, int act, void* stream) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return KFAMD_EINVAL;
+  if (la < 0 || la > 1 || lb < 0 || lb > 1 || act < KFAMD_ACT_NONE || act > KFAMD_ACT_SILU) return KFAMD_EINVAL;
+  if (la == 0 && lb == 0) {
+    if (!Aux)
+      return kfamd_gemm_nt_bf16_variant(0, A, B, C, bias, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a, stride_b,
+                                        stride_c, stride_r, alpha, act, stream);
+    return kfamd_w4_launch_nt(w4_tile(M, N, batch), A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr,
+                              stride_a, stride_b, stride_c, stride_r, alpha, act, stream);
+  }
+  if (bias || Aux || act != KFAMD_ACT_NONE) return KFAMD_EINVAL;
+  return kfamd_w4_launch_t(la, lb, w4_tile(M, N, batch), A, B, C, R, M, N, K, batch, lda, ldb, ldc, ldr, stride_a,
+                           stride_b, stride_c, stride_r, alpha, stream);
 }

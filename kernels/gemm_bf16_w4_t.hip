@@ -1,0 +1,54 @@
+// gemm_bf16_w4_t.hip — the w4 GEMM template (gemm_w4.h) in the operand layouts of a linear layer's
+// backward, so autograd never materialises a transposed copy:
+//   dgrad  dX[M][K]  = dY[M][N] · W[N][K]      -> LA = 0 (dY K-contiguous), LB = 1 (W k-major)
+//   wgrad  dW[N][K]  = dY[M][N]^T · X[M][K]    -> LA = 1 (dY k-major),      LB = 1 (X k-major)
+//   and LA = 1, LB = 0 for completeness (A^T B^T products).
+// Epilogue: alpha and an optional residual R (R may alias C: gradient accumulation, C += A·B).
+#include "gemm_w4.h"
+
+using namespace kfw4;
+
+namespace {
+
+template <int LA, int LB, int BM>
+int launch_t(const void* A, const void* B, void* C, const void* R, int M, int N, int K, int batch, long long lda,
+             long long ldb, long long ldc, long long ldr, long long sa, long long sb, long long sc, long long sr,
+             float alpha, void* stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(((M + BM - 1) / BM) * ((N + BM - 1) / BM), batch), block(kThreads);
+  const __bf16* a = static_cast<const __bf16*>(A);
+  const __bf16* b = static_cast<const __bf16*>(B);
+  __bf16* c = static_cast<__bf16*>(C);
+  const __bf16* r = static_cast<const __bf16*>(R);
+  if (R)
+    hipLaunchKernelGGL((gemm_w4<KFAMD_ACT_NONE, false, true, false, LA, LB, BM>), grid, block, 0, s, a, b, c, nullptr,
+                       r, nullptr, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, nullptr);
+  else
+    hipLaunchKernelGGL((gemm_w4<KFAMD_ACT_NONE, false, false, false, LA, LB, BM>), grid, block, 0, s, a, b, c,
+                       nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, nullptr);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+}  // namespace
+
+// la/lb: 0 = K-contiguous operand, 1 = k-major (see gemm_w4.h); (0, 0) is kfamd_w4_launch_nt.
+extern "C" int kfamd_w4_launch_t(int la, int lb, int bm, const void* A, const void* B, void* C, const void* R, int M,
+                                 int N, int K, int batch, long long lda, long long ldb, long long ldc, long long ldr,
+                                 long long sa, long long sb, long long sc, long long sr, float alpha, void* stream) {
+  const int rc = check_shape(la, lb, bm, A, B, C, nullptr, R, nullptr, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr);
+  if (rc != KFAMD_OK) return rc;
+#define W4T(LA_, LB_)                                                                                              \
+  if (la == LA_ && lb == LB_) {                                                                                    \
+    if (bm == 256) return launch_t<LA_, LB_, 256>(A, B, C, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr,  \
+                                                   alpha, stream);                                                 \
+    if (bm == 128) return launch_t<LA_, LB_, 128>(A, B, C, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr,  \
+                                                   alpha, stream);                                                 \
+    return KFAMD_EINVAL;                                                                                           \
+  }
+  W4T(0, 1)
+  W4T(1, 1)
+  W4T(1, 0)
+#undef W4T
+  return KFAMD_EINVAL;
+}

@@ -1,0 +1,519 @@
+// gemm_w4.h — the K1 "w4" MFMA GEMM template: 4 waves (2x2) per block, one wave per SIMD with the
+// full register file (accumulators pinned in AGPRs), LDS-DMA staging through a 5-slot ring.
+// Instantiated by gemm_bf16_w4.hip (forward "NT" layout) and gemm_bf16_w4_t.hip (the backward
+// layouts), so each translation unit compiles only the variants it launches
+// (cdna_hip_programming.md §5.4 rule 19: co-compiled template variants perturb each other).
+//
+// Why this shape (MI355X_MICROARCH.md 'DVFS give-back' + cdna_hip_programming.md §5.4 rule 28):
+// on random data a bf16 GEMM runs clock-limited (~1.9 GHz), and what raises the held clock for the
+// same MFMAs is less energy per MFMA — fewer LDS read bytes and fewer VALU. LDS fragment reads per
+// K-tile scale with sum over waves of (wave_M + wave_N): 4 waves of 128x128 read 128 KiB per CU per
+// K-tile against 192 KiB for 8 waves of 128x64, with the same MFMA count and DMA bytes.
+//
+// Operand layouts (template LA / LB), C[m][n] = sum_k Aop[m][k] * Bop[n][k]:
+//   LA = 0: A stored [M][K], K contiguous (row-major activations: the forward and dgrad A)
+//   LA = 1: A stored [K][M], M contiguous (dY read as dY^T by the wgrad GEMM)
+//   LB = 0: B stored [N][K] (F.linear weight);  LB = 1: B stored [K][N] (W in dgrad, X in wgrad)
+// A K-contiguous operand is staged as [rows][64 k] 128-B rows (XOR swizzle on the 16-B chunk, read
+// with ds_read_b128); a row-contiguous ("k-major") operand as [64 k][BM] rows of BM*2 bytes, read
+// with ds_read_b64_tr_b16 (cdna_hip_programming.md T10), which hands each lane 4 consecutive k of one
+// column: two reads make the 8-k MFMA fragment. The k-major image is XOR-swizzled on chunk bits 1-3
+// by f(row) = 2*((row&3) | ((row>>3)&1)<<2): the 8 rows one 32-lane half reads (q = 0..3, two lane
+// groups 8 rows apart) then land on 8 distinct 32-B bank slots — conflict-free. The swizzle goes on
+// the DMA SOURCE address (LDS stays lane-linear, §5.4 rule 21) and on the read address.
+//
+// Edges (no padding copies):
+//   * M / N: the last tile row/column is SHIFTED to end at M / N (m0 = min(tm*BM, M-BM)); it
+//     overlaps its neighbour, recomputes those outputs from the same data and does not store them
+//     (store mask m >= tm*BM, n >= tn*BN). Needs M, N >= BM.
+//   * K: the K tiling is shifted so the partial tile is the FIRST one (tile t covers k from
+//     koff + 64t, koff = K - 64*ceil(K/64) <= 0; the buffer base moves by koff). Only the prologue's
+//     tile 0 has out-of-range 16-B pieces (k < 0): they get a voffset past the buffer's num_records,
+//     so the LDS-DMA writes zeros (raw-buffer range check; valid pieces keep voffset + soffset inside
+//     the record, so this holds whether or not the check includes soffset). The K loop itself carries
+//     no edge code.
+// Pipeline (unchanged from r2): two LDS tiles live + one free slot, DMA of tile kt+2 spread over
+// the K-tile (1 per 8 MFMAs), fragments of the next k-substep read under the current substep's
+// MFMAs (two register sets), interleave pinned with sched_barrier.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include "kfamd_kernels.h"
+
+namespace kfw4 {
+namespace {  // internal linkage: each translation unit instantiates its own kernels
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define KFW4_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+#define KFW4_FENCE() asm volatile("" ::: "memory")
+#define KFW4_PIN() __builtin_amdgcn_sched_barrier(0)
+
+constexpr int kBK = 64, kThreads = 256;
+constexpr int kSlots = 5;                         // operand-tile slots (A or B each)
+constexpr int kRsrcWord3 = 0x00020000;            // gfx9 raw buffer: 32-bit dword format, no swizzle
+constexpr unsigned kOOB = 0x80000000u;            // voffset of a zero-filled (out-of-range) piece
+constexpr int kNumRecords = 0x7fffffff;
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  switch (act) {
+    case KFAMD_ACT_RELU: return v > 0.f ? v : 0.f;
+    case KFAMD_ACT_GELU_TANH: {
+      // 0.5 v (1 + tanh(u)) == v * sigmoid(2u): one v_exp + one v_rcp instead of libm tanhf (the
+      // tanhf epilogue cost ~25 % of an 8192x4096x4096 GEMM, profiles/r3_linear)
+      const float u2 = 1.5957691216057308f * (v + 0.044715f * v * v * v);
+      return v * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+    }
+    case KFAMD_ACT_SILU: return v * __builtin_amdgcn_rcpf(1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Per-operand staging geometry. One operand tile = 64 k x BM rows/cols = BM*128 bytes, DMA'd as
+// BM/32 one-KiB pieces per wave (4 waves).
+template <int L, int BM>
+struct Stage {
+  static constexpr int TILE = BM * kBK * 2;
+  static constexpr int PIECES = BM / 32;
+  // number of distinct per-lane voffsets over the wave's pieces (depends on the swizzle)
+  static constexpr int NV = L == 0 ? 2 : (BM == 256 ? 4 : 2);
+  static constexpr int RPP = 512 / BM;            // k-major: k rows per 1-KiB piece (2 or 4)
+  static constexpr int LPR = BM / 8;              // k-major: lanes per k row (32 or 16)
+
+  unsigned voff[NV];
+  int rowstep;   // bytes between consecutive pieces of a wave (wave-uniform)
+  int ktstep;    // bytes per K tile (wave-uniform)
+
+  __device__ __forceinline__ void init(int wid, int lane, long long ld) {
+    if constexpr (L == 0) {
+      // piece p = wid*PIECES + j covers rows 8p..8p+7; lane i lands at LDS p*1024 + 16*i (row
+      // 8p + (i>>3), swizzled chunk (i&7)) and fetches global chunk (i&7) ^ ((row>>1)&7)
+      const int lrow = wid * (BM / 4) + (lane >> 3);
+#pragma unroll
+      for (int par = 0; par < 2; ++par) {
+        const int chunk = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);
+        voff[par] = (unsigned)(((long long)lrow * ld + chunk * 8) * 2);
+      }
+      rowstep = (int)(8 * ld * 2);
+      ktstep = kBK * 2;
+    } else {
+      // piece j of wave w covers k rows 16w + RPP*j + rip (rip = lane / LPR), phys chunk lane % LPR;
+      // global chunk = phys ^ f(row), f = lane part (2*rip) ^ wave part (depends on j only)
+      const int rip = lane / LPR, phys = lane % LPR;
+      const unsigned v16 = (unsigned)((phys ^ (2 * (rip & 3))) * 16);
+      const unsigned vrow = (unsigned)((long long)(16 * wid + rip) * ld * 2);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) voff[v] = (v16 ^ (unsigned)(wave_f16_of_variant(v))) + vrow;
+      rowstep = (int)(RPP * ld * 2);
+      ktstep = (int)(kBK * ld * 2);
+    }
+  }
+  // k-major: XOR (in bytes) the wave part of f adds to the chunk offset, per voffset variant
+  static __device__ __forceinline__ int wave_f16_of_variant(int v) {
+    if constexpr (BM == 256) return ((v & 1) * 4 + ((v >> 1) & 1) * 8) * 16;
+    else return (v & 1) * 8 * 16;
+  }
+  static __device__ __forceinline__ constexpr int variant_of_piece(int j) {
+    if constexpr (L == 0) return j & 1;
+    else if constexpr (BM == 256) return (j & 1) | (((j >> 2) & 1) << 1);
+    else return (j >> 1) & 1;
+  }
+  // validity of this lane's 16-B piece j of the first (partial) K tile, koff = K - 64*nk <= 0
+  static __device__ __forceinline__ bool valid0(int j, int wid, int lane, int koff) {
+    if constexpr (L == 0) {
+      const int chunk = (lane & 7) ^ ((4 * (j & 1) + (lane >> 4)) & 7);
+      return koff + chunk * 8 >= 0;
+    } else {
+      return koff + 16 * wid + RPP * j + lane / LPR >= 0;
+    }
+  }
+};
+
+// LDS fragment reader for one operand: fragment q (16 rows/cols of the wave tile) of k-substep s.
+template <int L, int BM>
+struct Reader {
+  static constexpr int TILE = BM * kBK * 2;
+  static constexpr int ROWB = BM * 2;    // k-major LDS row bytes
+  int wbase;       // L=0: byte offset of the wave's first row; L=1: unused
+  int off[2];      // L=0: per-lane byte offset within a 2 KiB fragment block, per substep
+  unsigned vfw;    // L=1: (32*F) ^ (2*wave column base), F = (q4 | (g&1)<<2)
+  unsigned vl;     // L=1: lane part (8g+q4)*ROWB + 8p
+
+  __device__ __forceinline__ void init(int lane, int wpos) {
+    const int WT = BM / 2;
+    if constexpr (L == 0) {
+      const int lr = lane & 15, lh = lane >> 4;
+      const int sw = lh ^ (lr >> 1);
+      off[0] = lr * 128 + (sw << 4);
+      off[1] = lr * 128 + ((sw ^ 4) << 4);
+      wbase = (wpos * WT) * 128;
+    } else {
+      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p = i & 3;
+      const int F = q4 | ((g & 1) << 2);
+      vfw = (unsigned)((32 * F) ^ (2 * wpos * WT));
+      vl = (unsigned)((8 * g + q4) * ROWB + 8 * p);
+      wbase = 0;
+    }
+  }
+  template <int S>
+  __device__ __forceinline__ bf16x8 read(const char* smem, int slot, int q) const {
+    if constexpr (L == 0) {
+      return *reinterpret_cast<const bf16x8*>(smem + slot * TILE + wbase + q * 2048 + off[S]);
+    } else {
+      // inline asm, not __builtin_amdgcn_ds_read_tr16_b64: hipcc 7.2 puts an s_waitcnt vmcnt(0)
+      // before every builtin tr read that follows an LDS-DMA (draining the staging pipeline each
+      // substep). Ordering against the DMA comes from the K loop's counted vmcnt + barrier, and
+      // the results are covered by the loop's explicit lgkmcnt(0) before their MFMAs (as for the
+      // plain ds_read_b128 of the K-contiguous operand).
+      typedef short s16x4 __attribute__((ext_vector_type(4)));
+      const unsigned a = (vfw ^ (unsigned)(32 * q)) + vl + (unsigned)(slot * TILE) +
+                         (unsigned)(uintptr_t)KFW4_LDS_PTR(smem);
+      s16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(a), "i"((32 * S) * ROWB));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"((32 * S + 4) * ROWB));
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+// BM = 256: 256x256 tile (one 160 KiB block per CU). BM = 128 ("w4s"): the same pipeline on a 128x128
+// tile, 64x64 per wave, 80 KiB of LDS -> two blocks per CU (problems with fewer 256-tiles than CUs).
+// AUX (ACT != NONE only): also store the pre-activation act^-1 input, for the activation's backward.
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, bool DIAG = false,
+          int ABL = 0>
+__global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
+                          amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
+void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
+             const __bf16* __restrict__ bias, const __bf16* __restrict__ R, __bf16* __restrict__ Aux, int M, int N,
+             int K, long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
+             long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag) {
+  constexpr int BN = BM, WT = BM / 2, NR = WT / 16;    // wave tile WT x WT = NR x NR MFMA blocks
+  constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
+  constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
+  constexpr int MF = NR * NR;                          // MFMAs per wave per k32 substep
+  constexpr int DMA_EVERY = MF / PIECES;               // one DMA per DMA_EVERY MFMAs
+  constexpr int RG = 2;
+  static_assert(BM == 256 || BM == 128, "tile");
+  static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
+  __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  unsigned long long t_start = 0, rt_start = 0;
+  if (DIAG) {
+    t_start = __builtin_amdgcn_s_memtime();
+    rt_start = __builtin_amdgcn_s_memrealtime();
+  }
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  constexpr int kGroupM = 4;
+  const int per_group = kGroupM * tiles_n;
+  const int g = wg / per_group, first_m = g * kGroupM;
+  const int gm = min(tiles_m - first_m, kGroupM);
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const int m_lo = tm * BM, n_lo = tn * BN;            // first output row / column this block stores
+  const int m0 = min(m_lo, M - BM), n0 = min(n_lo, N - BN);  // edge tiles shifted inside
+
+  const int nk = (K + kBK - 1) / kBK;
+  const int koff = K - nk * kBK;                       // first K tile starts at k = koff (<= 0)
+  const long long bz = blockIdx.y;
+  A += bz * sa + (LA == 0 ? (long long)m0 * lda + koff : (long long)m0 + (long long)koff * lda);
+  B += bz * sb + (LB == 0 ? (long long)n0 * ldb + koff : (long long)n0 + (long long)koff * ldb);
+  C += bz * sc;
+  if (HAS_AUX) Aux += bz * sc;
+  if (HAS_RES) R += bz * sr;
+  // ABL (timing-only ablation builds, w4_diag): 1 = zero-record descriptors (every DMA dropped in
+  // the address unit, instruction stream kept), 2 = no K-loop ds_reads.
+  const int nrec = (DIAG && ABL == 1) ? 0 : kNumRecords;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, nrec, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, nrec, kRsrcWord3);
+
+  Stage<LA, BM> sta;
+  Stage<LB, BM> stb;
+  sta.init(wid, lane, lda);
+  stb.init(wid, lane, ldb);
+  // LDS = 5 slots, each holding ONE operand tile. With 4 slots live (tile t being read, tile t+1
+  // landing) the fifth lets A_{t+2} stream in during substep 0 of iteration t, B_{t+2} during
+  // substep 1 (into A_t's slot, free after the mid barrier); B_t's slot becomes the next free one.
+  // the soffset operands as plain locals: naming a struct member inside the builtin's soffset made
+  // hipcc 7.2's host pass drop the kernel's launch stub (and with it the whole device bundle of the
+  // translation unit) without a diagnostic; _build.check_object_kernels guards against a recurrence
+  const int rs_a = sta.rowstep, kts_a = sta.ktstep, rs_b = stb.rowstep, kts_b = stb.ktstep;
+  auto dma_a = [&](int kt, int slot, int j, bool first) {
+    unsigned v = sta.voff[Stage<LA, BM>::variant_of_piece(j)];
+    if (first && !Stage<LA, BM>::valid0(j, wid, lane_id(), koff)) v = kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, KFW4_LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
+                                             v, j * rs_a + kt * kts_a, 0, 0);
+  };
+  auto dma_b = [&](int kt, int slot, int j, bool first) {
+    unsigned v = stb.voff[Stage<LB, BM>::variant_of_piece(j)];
+    if (first && !Stage<LB, BM>::valid0(j, wid, lane_id(), koff)) v = kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, KFW4_LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
+                                             v, j * rs_b + kt * kts_b, 0, 0);
+  };
+
+  Reader<LA, BM> rda;
+  Reader<LB, BM> rdb;
+  rda.init(lane, wm);
+  rdb.init(lane, wn);
+
+  f32x4 acc[NR][NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[NR], b0[NR], a1[NR], b1[NR];
+  // fragment q of a set: q < NR -> B fragment q, q >= NR -> A fragment q-NR
+  auto read_frag0 = [&](int sa_slot, int sb_slot, bf16x8(&af)[NR], bf16x8(&bf)[NR], int q) {
+    if (q < NR) bf[q] = rdb.template read<0>(smem, sb_slot, q);
+    else af[q - NR] = rda.template read<0>(smem, sa_slot, q - NR);
+  };
+  auto read_frag1 = [&](int sa_slot, int sb_slot, bf16x8(&af)[NR], bf16x8(&bf)[NR], int q) {
+    if (q < NR) bf[q] = rdb.template read<1>(smem, sb_slot, q);
+    else af[q - NR] = rda.template read<1>(smem, sa_slot, q - NR);
+  };
+
+  // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
+  int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) {
+    dma_a(0, sa0, j, true);
+    dma_b(0, sb0, j, true);
+  }
+  if (nk > 1) {
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      dma_a(1, sa1, j, false);
+      dma_b(1, sb1, j, false);
+    }
+    if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  KFW4_FENCE();
+  __builtin_amdgcn_s_barrier();
+  KFW4_FENCE();
+#pragma unroll
+  for (int q = 0; q < 2 * NR; ++q) read_frag0(sa0, sb0, a0, b0, q);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  KFW4_PIN();
+  __builtin_amdgcn_s_setprio(1);
+
+  // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
+  // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
+  unsigned long long seg[4] = {0, 0, 0, 0};
+  unsigned long long t_loop0 = 0, t_loop1 = 0;
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (DIAG) {
+      KFW4_PIN();
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      KFW4_PIN();
+    }
+    return t;
+  };
+  auto body = [&](int kt, auto do_stage, auto do_next) {
+    constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
+    constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
+    const unsigned long long t0 = stamp();
+    // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
+#pragma unroll
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag1(sa0, sb0, a1, b1, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_a(kt + 2, sf, m / DMA_EVERY, false);
+      KFW4_PIN();
+      mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
+      KFW4_PIN();
+    }
+    const unsigned long long t1 = stamp();
+    // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
+    // after it tile kt's slots are free
+    if (kStage) {
+      if constexpr (BM == 256) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0074);                      // vmcnt(4) expcnt(7) lgkmcnt(0)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    }
+    KFW4_FENCE();
+    __builtin_amdgcn_s_barrier();
+    KFW4_FENCE();
+    KFW4_PIN();
+    const unsigned long long t2 = stamp();
+    // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
+#pragma unroll
+    for (int m = 0; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag0(sa1, sb1, a0, b0, m / RG);
+      if (kStage && m % DMA_EVERY == 2) dma_b(kt + 2, sa0, m / DMA_EVERY, false);
+      KFW4_PIN();
+      mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
+      KFW4_PIN();
+    }
+    const unsigned long long t3 = stamp();
+    if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
+    KFW4_PIN();
+    // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
+    const int na = sf, nb = sa0;
+    sf = sb0;
+    sa0 = sa1;
+    sb0 = sb1;
+    sa1 = na;
+    sb1 = nb;
+    if (DIAG) {
+      const unsigned long long t4 = stamp();
+      seg[0] += t1 - t0;
+      seg[1] += t2 - t1;
+      seg[2] += t3 - t2;
+      seg[3] += t4 - t3;
+    }
+  };
+  using T = std::integral_constant<bool, true>;
+  using F = std::integral_constant<bool, false>;
+  if (DIAG) t_loop0 = stamp();
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
+  if (kt + 1 < nk) {
+    body(kt, F{}, T{});
+    ++kt;
+  }
+  if (kt < nk) body(kt, F{}, F{});
+  __builtin_amdgcn_s_setprio(0);
+  if (DIAG) t_loop1 = stamp();
+  // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  // pin every accumulator behind the padding: the MFMAs are asm, so the compiler treats their AGPR
+  // results as ready at issue and would otherwise hoist v_accvgpr_read of the last writes above the
+  // s_nops (it did in the bias build of r2's w4d: stale sums). The empty asm "redefines" each one.
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) asm volatile("" : "+a"(acc[i][n]));
+
+  // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
+  // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
+  // groups (cdna_hip_programming.md T21, 16-lane form), after which every lane holds 8 contiguous
+  // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
+  // lh 3 -> block n+1 cols 8-15: one dwordx4 store per lane per pair. The lane id is re-derived
+  // here (v_mbcnt) so no lane-derived VGPR has to survive the K loop.
+  const int elane = lane_id();
+  const int elr = elane & 15, elh = elane >> 4;
+  auto finish = [&](int i, int n, int m, uint2& pre_out) -> uint2 {
+    const int col = n0 + wn * WT + n * 16 + elh * 4;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
+    if (HAS_BIAS) {
+      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+    }
+    if (HAS_AUX) {
+      bf16x4 p;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = (__bf16)v[r];
+      pre_out = __builtin_bit_cast(uint2, p);
+    }
+    if (ACT != KFAMD_ACT_NONE) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
+    }
+    if (HAS_RES) {
+      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+    return __builtin_bit_cast(uint2, o);
+  };
+  const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int m = m0 + wm * WT + i * 16 + elr;
+    const bool row_ok = m >= m_lo;
+    const long long roff = (long long)m * ldc + n0 + wn * WT + swap_col;
+#pragma unroll
+    for (int n = 0; n < NR; n += 2) {
+      uint2 pp{0, 0}, pq{0, 0};
+      uint2 p = finish(i, n, m, pp), q = finish(i, n + 1, m, pq);
+      const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
+      const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
+      const bool ok = row_ok && (n0 + wn * WT + n * 16 + swap_col >= n_lo);
+      if (ok) *reinterpret_cast<uint4*>(C + roff + n * 16) = uint4{sx[0], sy[0], sx[1], sy[1]};
+      if (HAS_AUX) {
+        const auto ax = __builtin_amdgcn_permlane16_swap(pp.x, pq.x, false, false);
+        const auto ay = __builtin_amdgcn_permlane16_swap(pp.y, pq.y, false, false);
+        if (ok) *reinterpret_cast<uint4*>(Aux + roff + n * 16) = uint4{ax[0], ay[0], ax[1], ay[1]};
+      }
+    }
+  }
+  if (DIAG) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores retired: the block's real end
+    const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+    unsigned hw_id, xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    if (lane == 0) {
+      unsigned long long* d = diag + ((long long)blockIdx.x * 4 + wid) * 16;
+      for (int j = 0; j < 4; ++j) d[j] = seg[j];
+      d[4] = t_loop0 - t_start;  // prologue (address setup, first two tiles, F0(0))
+      d[5] = t_end - t_loop1;    // epilogue (stores issued)
+      d[6] = t_loop1 - t_loop0;  // K loop
+      d[7] = t_end - t_start;    // shader clocks, whole block (to the last store issue)
+      d[8] = rt_start;           // 100 MHz realtime at block start / end (stores retired)
+      d[9] = rt_end;
+      d[10] = ((unsigned long long)(xcc_id & 0xf) << 32) | hw_id;  // which CU ran the block
+    }
+  }
+}
+
+// Shape/alignment contract shared by the launchers (returns KFAMD_OK or an error code):
+//  16-B aligned bases and leading dims / batch strides in multiples of 8 elements; N % 8 (16-B
+//  output stores, 8-column edge shift); a K-contiguous operand needs K % 8, a k-major A needs M % 8;
+//  M, N >= BM; the 32-bit buffer offsets must cover a block's operand span.
+inline int check_shape(int la, int lb, int BM, const void* A, const void* B, const void* C, const void* bias,
+                       const void* R, const void* Aux, int M, int N, int K, long long lda, long long ldb,
+                       long long ldc, long long ldr, long long sa, long long sb, long long sc, long long sr) {
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (M < BM || N < BM || K <= 0) return KFAMD_EINVAL;
+  if (N % 8) return KFAMD_EINVAL;
+  if ((la == 0 || lb == 0) && K % 8) return KFAMD_EINVAL;
+  if (la == 1 && M % 8) return KFAMD_EINVAL;
+  if (la == 0 ? lda < K : lda < M) return KFAMD_EINVAL;
+  if (lb == 0 ? ldb < K : ldb < N) return KFAMD_EINVAL;
+  if (ldc < N || (R && ldr < N)) return KFAMD_EINVAL;
+  if (!al16(A) || !al16(B) || !al16(C) || (Aux && !al16(Aux))) return KFAMD_EALIGN;
+  if (lda % 8 || ldb % 8 || ldc % 8 || sa % 8 || sb % 8 || sc % 8) return KFAMD_EALIGN;
+  if (bias && (reinterpret_cast<uintptr_t>(bias) & 7)) return KFAMD_EALIGN;
+  if (R && ((reinterpret_cast<uintptr_t>(R) & 7) || ldr % 4 || sr % 4)) return KFAMD_EALIGN;
+  // buffer offsets: L=0 spans BM rows of ld; L=1 spans K rows of ld (voffset + soffset < 2^31)
+  const long long span_a = la == 0 ? ((long long)BM * lda + kBK) * 2 : ((long long)K + kBK) * lda * 2;
+  const long long span_b = lb == 0 ? ((long long)BM * ldb + kBK) * 2 : ((long long)K + kBK) * ldb * 2;
+  if (span_a >= (1LL << 31) || span_b >= (1LL << 31)) return KFAMD_EINVAL;
+  return KFAMD_OK;
+}
+
+}  // namespace
+}  // namespace kfw4

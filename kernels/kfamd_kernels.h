@@ -51,6 +51,26 @@ int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void* B, void* 
                                long long stride_a, long long stride_b, long long stride_c,
                                long long stride_r, float alpha, int act, void* stream);
 
+// Layout-general GEMM on the w4 MFMA template: C[b][m][n] = act(alpha * sum_k Aop[m][k] Bop[n][k]
+// + bias[n]) (+ R), with
+//   la = 0: A stored [M][K] (K contiguous, lda >= K)   la = 1: A stored [K][M] (M contiguous, lda >= M)
+//   lb = 0: B stored [N][K] (K contiguous, ldb >= K)   lb = 1: B stored [K][N] (N contiguous, ldb >= N)
+// Aux (la = lb = 0, act = gelu/silu only): second output with the pre-activation (same layout as C).
+// Transposed layouts take only alpha and R (R may alias C: C += A.B). Edge tiles are handled in the
+// kernel (any M, N >= 128; N % 8; K % 8 when an operand is K-contiguous; M % 8 when la = 1). Other
+// shapes return KFAMD_EINVAL and the caller falls back.
+int kfamd_gemm_bf16_ex(int la, int lb, const void* A, const void* B, void* C, const void* bias, const void* R,
+                       void* Aux, int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
+                       long long ldr, long long stride_a, long long stride_b, long long stride_c, long long stride_r,
+                       float alpha, int act, void* stream);
+
+// Fused linear-backward tail: g = dy * act'(z) (bf16; z = the forward's Aux pre-activation, or its
+// output y for relu), db = column sums of g (fp32, optional). act == NONE: only db = sum over rows of
+// dy (g unused). [rows][cols], cols % 8 == 0, 16-B aligned. workspace: kfamd_act_grad_workspace bytes.
+long long kfamd_act_grad_workspace(int rows, int cols);
+int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows, int cols,
+                        int act, void* stream);
+
 // LayerNorm forward over the last dim (hidden). x,y: [rows][hidden] bf16 (row stride = hidden).
 // gamma/beta: [hidden] bf16 (beta may be null). mean/rstd: optional fp32 [rows] (saved for bwd).
 int kfamd_layernorm_fwd_bf16(const void* x, const void* gamma, const void* beta, void* y,

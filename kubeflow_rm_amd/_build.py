@@ -91,6 +91,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
         if force or not _newer(obj, [src, *headers]) or (info and hash_changed):
             extra = [f'-DKFAMD_SRC_HASH="{src_hash}"'] if info else []
             _run([HIPCC, *HIP_FLAGS, *extra, "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
+            check_object_kernels(src, obj)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
@@ -107,7 +108,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
 # kernel families every production library must carry (kernel-descriptor symbols of the embedded
 # gfx950 code object). A host compile that drops a template's kernel stubs still links and still
 # exits 0, leaving a library whose launches fail at run time: refuse to install it.
-REQUIRED_KERNELS = ("gemm_nt_256w4", "gemm_nt_256p", "gemm_nt_128", "norm_fwd_wave", "ln_bwd_dx_wave",
+REQUIRED_KERNELS = ("gemm_w4", "gemm_nt_256p", "gemm_nt_128", "norm_fwd_wave", "ln_bwd_dx_wave",
                     "allreduce_oneshot")
 
 
@@ -115,6 +116,19 @@ def kernel_descriptors(lib: Path) -> set[str]:
     import re
     data = Path(lib).read_bytes()
     return {m.group(1).decode() for m in re.finditer(rb"([A-Za-z0-9_]+)\.kd\x00", data)}
+
+
+def check_object_kernels(src: Path, obj: Path) -> None:
+    """A translation unit that defines __global__ kernels must carry their gfx950 descriptors.
+    hipcc 7.2 can drop a TU's launch stubs AND its whole device bundle with exit status 0 (seen with
+    a struct member as a buffer builtin's soffset, kernels/gemm_w4.h): catch it per object."""
+    import re
+    if not re.search(r"^\s*(template\s*<[^;{]*>\s*)?__global__", src.read_text(), re.M) and \
+            "gemm_w4<" not in src.read_text():
+        return
+    if not kernel_descriptors(obj):
+        raise RuntimeError(f"{obj}: compiled from {src.name} but holds no gfx950 kernel descriptors "
+                           "(device bundle dropped by the compiler)")
 
 
 def check_kernel_library(lib: Path) -> None:

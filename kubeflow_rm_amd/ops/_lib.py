@@ -27,6 +27,10 @@ _SIGNATURES = {
     "kfamd_gemm_nt_bf16_variant": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                                            c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
                                            c_float, c_int, c_vp]),
+    "kfamd_gemm_bf16_ex": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                   c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_int, c_vp]),
+    "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
+    "kfamd_act_grad_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "kfamd_layernorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),
     "kfamd_rmsnorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),
     "kfamd_layernorm_bwd_workspace": (c_ll, [c_int, c_int]),

@@ -28,10 +28,14 @@ def _check_operand(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name} must have a contiguous last dimension")
 
 
-# Shapes off the MFMA tiles (M, N % 128, K % 64) would run on the generic kernel at a third to a
-# half of the tiled kernels' rate (profiles/r2_gemm_unaligned). Above this size the operands are
-# zero-padded up to the tiles instead: the copies cost a few percent of the GEMM.
+# The w4 kernels handle edge tiles in-kernel (gemm_w4.h) for M, N >= 128 with N % 8 == 0 and
+# K % 8 == 0. Other large shapes would run on the generic kernel at a third to a half of the tiled
+# kernels' rate (profiles/r2_gemm_unaligned): above this size they are zero-padded up to the tiles.
 _PAD_MIN_FLOPS = 2.0 * 1024 ** 3
+
+
+def _w4_shape(M: int, N: int, K: int) -> bool:
+    return M >= 128 and N >= 128 and N % 8 == 0 and K % 8 == 0
 
 
 def _round_up(x: int, m: int) -> int:
@@ -40,9 +44,8 @@ def _round_up(x: int, m: int) -> int:
 
 def _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K):
     """Zero-pad to the tile grid, run the tiled kernel, copy the [M, N] corner into ``out``."""
-    big = -(-M // 256) * -(-N // 256) * batch > 128  # the auto dispatch's 256-tile threshold
-    tm = 256 if big else 128
-    Mp, Np, Kp = _round_up(M, tm), _round_up(N, tm), _round_up(K, 64)
+    # pad only up to the w4 contract (M, N >= 128, N % 8, K % 8): the kernel handles the rest
+    Mp, Np, Kp = max(M, 128), max(_round_up(N, 8), 128), _round_up(K, 8)
     F = torch.nn.functional
 
     def pad(t, cols, rows):  # copy only an operand that is off the grid (e.g. just B for an odd N)
@@ -107,7 +110,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
         _check_operand(bias, "bias")
         if bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous [N] tensor")
-    if (variant == "auto" and (M % 128 or N % 128 or K % 64)
+    if (variant == "auto" and not _w4_shape(M, N, K)
             and flops(M, N, K, batch) >= _PAD_MIN_FLOPS):
         return _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K)
     r_ptr, ldr, sr = None, 0, 0
@@ -125,48 +128,164 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
     return out
 
 
+def _ex(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, *, bias=None, residual=None, aux=None,
+        alpha=1.0, act="none") -> int:
+    """Raw kfamd_gemm_bf16_ex call; returns the status (0 = launched)."""
+    r_ptr, ldr, sr = None, 0, 0
+    if residual is not None:
+        r_ptr, ldr, sr = residual.data_ptr(), residual.stride(-2), (residual.stride(0) if residual.dim() == 3 else 0)
+    return _lib.lib().kfamd_gemm_bf16_ex(
+        la, lb, a.data_ptr(), b.data_ptr(), c.data_ptr(), bias.data_ptr() if bias is not None else None, r_ptr,
+        aux.data_ptr() if aux is not None else None, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr,
+        float(alpha), ACTS[act], _stream_ptr(a))
+
+
+def mm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
+       out: torch.Tensor | None = None, residual: torch.Tensor | None = None, alpha: float = 1.0) -> torch.Tensor:
+    """``alpha * op(a) @ op(b) (+ residual)`` for 2-D or batched 3-D bf16 operands, op = transpose when
+    the flag is set, on the w4 MFMA kernel in whichever operand layout the tensors already have: a
+    transposed operand is read k-major through ``ds_read_b64_tr_b16`` instead of being copied
+    (``kernels/gemm_bf16_w4_t.hip``). Shapes the tiled kernel does not take (a dimension < 128, an odd
+    inner extent) run ``gemm_nt`` on transposed copies. ``residual`` may be ``out`` itself
+    (accumulate)."""
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    if a.dim() != b.dim() or a.dim() not in (2, 3) or (a.dim() == 3 and a.shape[0] != b.shape[0]):
+        raise ValueError("mm needs two 2-D or two equally batched 3-D operands")
+    batched = a.dim() == 3
+    batch = a.shape[0] if batched else 1
+    M, K = (a.shape[-1], a.shape[-2]) if trans_a else (a.shape[-2], a.shape[-1])
+    Kb, N = (b.shape[-1], b.shape[-2]) if trans_b else (b.shape[-2], b.shape[-1])
+    if K != Kb:
+        raise ValueError(f"inner dims differ: {K} vs {Kb}")
+    out_shape = (batch, M, N) if batched else (M, N)
+    if out is None:
+        out = torch.empty(out_shape, dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out")
+        if tuple(out.shape) != out_shape or out.device != a.device:
+            raise ValueError(f"out must be a bf16 {out_shape} tensor on {a.device}")
+    if residual is not None:
+        _check_operand(residual, "residual")
+        if tuple(residual.shape) != out_shape:
+            raise ValueError(f"residual must be {out_shape}")
+    la = 1 if trans_a else 0          # kernel A operand [M][K]: K contiguous unless a is read transposed
+    lb = 0 if trans_b else 1          # kernel B operand [N][K]: b [K][N] is k-major
+    sa = a.stride(0) if batched else 0
+    sb = b.stride(0) if batched else 0
+    sc = out.stride(0) if batched else 0
+    rc = _ex(la, lb, a, b, out, M, N, K, batch, a.stride(-2), b.stride(-2), out.stride(-2), sa, sb, sc,
+             residual=residual, alpha=alpha)
+    if rc > 0:
+        _lib.check(rc, f"mm[{M}x{N}x{K}x{batch}]")
+    if rc == 0:
+        return out
+    # fallback: materialise the NT operands (shape outside the tiled kernel's contract)
+    a_nt = (a.transpose(-1, -2) if trans_a else a).contiguous()
+    b_nt = (b if trans_b else b.transpose(-1, -2)).contiguous()
+    res = residual.clone() if residual is not None and residual.data_ptr() == out.data_ptr() else residual
+    return gemm_nt(a_nt, b_nt, residual=res, alpha=alpha, out=out)
+
+
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b with b stored [K, N] (row-major). Transposes b once into the NT layout."""
+    """a @ b with b stored [K, N] (row-major): read k-major in place (no transposed copy)."""
+    if a.dim() == 2 and b.dim() == 2:
+        return mm(a, b)
     return gemm_nt(a, b.t().contiguous())
 
 
+def gemm_nt_preact(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, act: str):
+    """(y, z): y = act(x2 @ weight^T + bias) and the pre-activation z from ONE GEMM (the epilogue's
+    second output), for gelu/silu backward. Falls back to z from the kernel + torch's activation."""
+    M, K = x2.shape
+    N = weight.shape[0]
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    z = torch.empty_like(y)
+    if bias is not None:
+        _check_operand(bias, "bias")
+    rc = _ex(0, 0, x2, weight, y, M, N, K, 1, x2.stride(0), weight.stride(0), N, 0, 0, 0, bias=bias, aux=z,
+             act=act)
+    if rc > 0:
+        _lib.check(rc, f"gemm_nt_preact[{M}x{N}x{K}]")
+    if rc == 0:
+        return y, z
+    z = gemm_nt(x2, weight, bias=bias)
+    F = torch.nn.functional
+    yf = F.gelu(z.float(), approximate="tanh") if act in ("gelu", "gelu_tanh") else F.silu(z.float())
+    return yf.to(torch.bfloat16), z
+
+
+def act_grad(gy: torch.Tensor, z: torch.Tensor | None, act: str, need_bias_grad: bool):
+    """(g, db): g = gy * act'(z) (z = pre-activation; the output y for relu), db = column sums of g
+    (fp32) — one fused HIP pass (kernels/act_grad_bf16.hip). act == 'none': g = gy."""
+    rows, cols = gy.shape
+    L = _lib.lib()
+    if act == "none" and not need_bias_grad:
+        return gy, None
+    if cols % 8 or gy.stride(-1) != 1 or (z is not None and not z.is_contiguous()) or not gy.is_contiguous():
+        F = torch.nn.functional
+        if act == "none":
+            g = gy
+        elif act == "relu":
+            g = gy * (z > 0)
+        else:
+            with torch.enable_grad():
+                p = z.float().requires_grad_(True)
+                f = F.gelu(p, approximate="tanh") if act in ("gelu", "gelu_tanh") else F.silu(p)
+                (gf,) = torch.autograd.grad(f, p, gy.float())
+            g = gf.to(torch.bfloat16)
+        return g, (g.float().sum(0) if need_bias_grad else None)
+    g = gy if act == "none" else torch.empty_like(gy)
+    db = ws = None
+    if need_bias_grad:
+        db = torch.empty(cols, dtype=torch.float32, device=gy.device)
+        ws = torch.empty(L.kfamd_act_grad_workspace(rows, cols) // 4, dtype=torch.float32, device=gy.device)
+    rc = L.kfamd_act_grad_bf16(gy.data_ptr(), z.data_ptr() if z is not None else None,
+                               g.data_ptr() if act != "none" else None, db.data_ptr() if db is not None else None,
+                               ws.data_ptr() if ws is not None else None, rows, cols, ACTS[act], _stream_ptr(gy))
+    _lib.check(rc, f"act_grad[{rows}x{cols}]")
+    return g, db
+
+
 class _Linear(torch.autograd.Function):
+    """y = act(x W^T + b). Forward: one GEMM whose epilogue also stores the pre-activation for gelu /
+    silu. Backward: one fused act-grad + bias-grad pass, then dgrad (g·W, W read k-major) and wgrad
+    (g^T·X, both read k-major) on the w4 kernel: no transposed copies, no recomputed GEMM."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, act):
-        y = gemm_nt(x, weight, bias=bias, act=act if bias is not None or act != "none" else "none")
-        ctx.save_for_backward(x, weight, bias, y if act == "relu" else None)
-        ctx.act = act
-        if act not in ("none", "relu"):
-            # need pre-activation for gelu/silu backward: recompute cheaply in backward
-            ctx.needs_preact = True
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        z = None
+        if act in ("gelu", "gelu_tanh", "silu"):
+            y, z = gemm_nt_preact(x2, weight, bias, act)
+            y = y.view(*x.shape[:-1], weight.shape[0])
         else:
-            ctx.needs_preact = False
+            y = gemm_nt(x, weight, bias=bias, act=act)
+        ctx.save_for_backward(x2, weight, bias, y if act == "relu" else z)
+        ctx.act = act
+        ctx.xshape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight, bias, y = ctx.saved_tensors
-        K = x.shape[-1]
+        x2, weight, bias, zy = ctx.saved_tensors
         N = weight.shape[0]
-        x2 = x.reshape(-1, K)
-        gy2 = gy.reshape(-1, N).contiguous()
-        if ctx.act == "relu":
-            gy2 = gy2 * (y.reshape(-1, N) > 0)
-        elif ctx.needs_preact:
-            pre = gemm_nt(x2, weight, bias=bias).float()
-            with torch.enable_grad():
-                p = pre.detach().requires_grad_(True)
-                f = torch.nn.functional.gelu(p, approximate="tanh") if ctx.act in ("gelu", "gelu_tanh") \
-                    else torch.nn.functional.silu(p)
-                (g,) = torch.autograd.grad(f, p, gy2.float())
-            gy2 = g.to(torch.bfloat16)
+        gy2 = gy.reshape(-1, N)
+        if not gy2.is_contiguous():
+            gy2 = gy2.contiguous()
+        need_db = bias is not None and ctx.needs_input_grad[2]
+        zz = zy.reshape(-1, N) if zy is not None else None
+        g, db = act_grad(gy2, zz, ctx.act, need_db)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = gemm_nt(gy2, weight.t().contiguous()).reshape(x.shape)
+            gx = mm(g, weight).reshape(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            gw = gemm_nt(gy2.t().contiguous(), x2.t().contiguous())
-        if bias is not None and ctx.needs_input_grad[2]:
-            gb = gy2.float().sum(0).to(bias.dtype)
+            gw = mm(g, x2, trans_a=True)
+        if need_db:
+            gb = db.to(bias.dtype)
         return gx, gw, gb, None
 
 

@@ -195,3 +195,127 @@ def test_gemm_rejects_bad_out_tensor():
         ops.gemm_nt(a, b, out=torch.empty(256, 512, device="cuda", dtype=torch.bfloat16)[:, ::2])
     out = torch.empty(256, 256, device="cuda", dtype=torch.bfloat16)
     assert ops.gemm_nt(a, b, out=out) is out
+
+
+# ---- r3: in-kernel edge tiles, transposed operand layouts, pre-activation output, act-grad ----------
+
+@pytest.mark.parametrize("M,N,K", [(1500, 1500, 1500), (4000, 4000, 4000), (3000, 3000, 3000), (8000, 8000, 8000),
+                                   (257, 264, 72), (129, 136, 8), (130, 1000, 520), (640, 384, 1000),
+                                   (128, 128, 64), (300, 200, 4104)])
+def test_gemm_edge_tiles_in_kernel(M, N, K):
+    """Off-grid M / N (shifted last tile, masked stores) and K (zero-filled first K tile) on the w4
+    kernels, both tile sizes, with the fused epilogue."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    a, b, bias = _rand(M, K, seed=41), _rand(N, K, seed=42), _rand(N, seed=43)
+    from kubeflow_rm_amd.ops.gemm import _w4_shape
+    for v in ("w4", "w4s", "auto"):
+        if v != "auto" and (not _w4_shape(M, N, K) or (v == "w4" and (M < 256 or N < 256))):
+            continue  # outside the tiled contract: auto pads up to it
+        out = gemm_nt(a, b, bias=bias, act="gelu_tanh", alpha=0.5, variant=v)
+        _assert_close(out, _ref_gemm(a, b, bias, "gelu_tanh", alpha=0.5), K)
+    r = _rand(M, N, seed=44)
+    _assert_close(gemm_nt(a, b, residual=r), _ref_gemm(a, b, residual=r), K)
+
+
+def test_gemm_edge_store_mask_leaves_neighbours():
+    """The shifted edge tile recomputes rows/columns its neighbour owns: with an in-place residual
+    (out aliases R) a double store would add the residual twice."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    M, N, K = 300, 392, 200
+    a, b = _rand(M, K, seed=45), _rand(N, K, seed=46)
+    c = _rand(M, N, seed=47)
+    ref = _ref_gemm(a, b, residual=c)
+    gemm_nt(a, b, residual=c, out=c)
+    _assert_close(c, ref, K)
+
+
+def _ref_mm(a, b, ta, tb, alpha=1.0, residual=None):
+    af = a.float().transpose(-1, -2) if ta else a.float()
+    bf = b.float().transpose(-1, -2) if tb else b.float()
+    c = alpha * (af @ bf)
+    return c + residual.float() if residual is not None else c
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (True, True), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (4096, 4096, 4096), (1500, 1000, 776),
+                                   (136, 128, 100), (2048, 1024, 8192)])
+def test_mm_operand_layouts(M, N, K, ta, tb):
+    """k-major operands through ds_read_b64_tr_b16 (no transposed copies) vs fp32."""
+    from kubeflow_rm_amd.ops import mm
+    a = _rand(*((K, M) if ta else (M, K)), seed=51)
+    b = _rand(*((N, K) if tb else (K, N)), seed=52)
+    out = mm(a, b, trans_a=ta, trans_b=tb)
+    _assert_close(out, _ref_mm(a, b, ta, tb), K)
+    # accumulate in place (gradient accumulation): out += alpha * op(a) op(b)
+    ref = _ref_mm(a, b, ta, tb, alpha=0.25, residual=out)
+    mm(a, b, trans_a=ta, trans_b=tb, out=out, residual=out, alpha=0.25)
+    _assert_close(out, ref, K)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (True, True)])
+def test_mm_identity_asymmetric(ta, tb):
+    """A = I with an asymmetric B through each layout: catches a transposed fragment or C write."""
+    from kubeflow_rm_amd.ops import mm
+    n = 384
+    eye = torch.eye(n, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device="cuda", dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
+    out = mm(eye, b, trans_a=ta, trans_b=tb)
+    assert torch.equal(out.float(), (b.float().t() if tb else b.float()))
+    out2 = mm(b, eye, trans_a=ta, trans_b=tb)
+    assert torch.equal(out2.float(), (b.float().t() if ta else b.float()))
+
+
+def test_mm_batched_layouts():
+    from kubeflow_rm_amd.ops import mm
+    a, b = _rand(3, 512, 256, seed=53), _rand(3, 512, 384, seed=54)
+    _assert_close(mm(a, b, trans_a=True), _ref_mm(a, b, True, False), 512)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "silu"])
+def test_gemm_preactivation_output(act):
+    from kubeflow_rm_amd.ops import gemm_nt_preact
+    M, N, K = 1000, 1536, 520
+    x, w, bias = _rand(M, K, seed=55), _rand(N, K, seed=56), _rand(N, seed=57)
+    y, z = gemm_nt_preact(x, w, bias, act)
+    _assert_close(z, _ref_gemm(x, w, bias), K)
+    _assert_close(y, _ref_gemm(x, w, bias, act), K)
+
+
+@pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
+@pytest.mark.parametrize("rows,cols", [(8192, 4096), (100, 136), (1, 8)])
+def test_act_grad_fused(act, rows, cols):
+    from kubeflow_rm_amd.ops import act_grad
+    gy, z = _rand(rows, cols, seed=58), _rand(rows, cols, seed=59, scale=3.0)
+    g, db = act_grad(gy, z, act, True)
+    zf = z.float().requires_grad_(True)
+    F = torch.nn.functional
+    f = {"none": lambda t: t, "relu": torch.relu, "gelu_tanh": lambda t: F.gelu(t, approximate="tanh"),
+         "silu": F.silu}[act](zf)
+    (gr,) = torch.autograd.grad(f, zf, gy.float())
+    assert (g.float() - gr).abs().max().item() <= 1e-2 * (gr.abs().max().item() + 1e-3) + 1e-2
+    dbr = g.float().sum(0)
+    assert (db - dbr).abs().max().item() <= 1e-3 * (dbr.abs().max().item() + 1.0)
+
+
+@pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
+@pytest.mark.parametrize("shape", [(4, 256, 1024, 512), (1, 1000, 776, 1032)])
+def test_linear_backward_layouts(act, shape):
+    """Full linear fwd+bwd: pre-activation from the forward epilogue, fused act/bias grad, dgrad and
+    wgrad on the transposed-layout kernels — all vs fp32 autograd."""
+    from kubeflow_rm_amd.ops import linear
+    B, T, K, N = shape
+    x = _rand(B, T, K, seed=61).requires_grad_(True)
+    w = _rand(N, K, seed=62, scale=0.05).requires_grad_(True)
+    bias = _rand(N, seed=63).requires_grad_(True)
+    y = linear(x, w, bias, act=act)
+    g = _rand(*y.shape, seed=64)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, bias))
+    F = torch.nn.functional
+    pre = xr @ wr.t() + br
+    yr = {"none": lambda t: t, "relu": torch.relu, "gelu_tanh": lambda t: F.gelu(t, approximate="tanh"),
+          "silu": F.silu}[act](pre)
+    yr.backward(g.float())
+    for got, ref in ((y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (bias.grad, br.grad)):
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err

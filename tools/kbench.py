@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--variants", default="auto")
+    ap.add_argument("--layouts", default="", help="MxNxK list: mm() in all four operand layouts vs torch")
+    ap.add_argument("--linear", default="", help="TxKxN list: linear fwd+bwd (gelu, bias) vs torch autograd")
     args = ap.parse_args()
     import torch
     from kubeflow_rm_amd import ops
@@ -67,6 +69,58 @@ def main():
             d["torch_tflops"] = round(fl / min(theirs) / 1e12, 1)
         emit(d)
         del a, b, c
+        torch.cuda.empty_cache()
+
+    for spec in [x for x in args.layouts.split(",") if x]:
+        M, N, K = map(int, spec.split("x"))
+        fl = 2.0 * M * N * K
+        iters = max(3, min(200, int(2e12 / fl) + 1))
+        d = {"kind": "mm_layouts_bf16", "M": M, "N": N, "K": K}
+        for ta, tb in ((False, True), (False, False), (True, False), (True, True)):
+            a = (torch.rand(*((K, M) if ta else (M, K)), device=dev) * 2 - 1).to(torch.bfloat16)
+            b = (torch.rand(*((N, K) if tb else (K, N)), device=dev) * 2 - 1).to(torch.bfloat16)
+            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            fa = (lambda: a.t()) if ta else (lambda: a)
+            fb = (lambda: b.t()) if tb else (lambda: b)
+            for _ in range(3):
+                ops.mm(a, b, trans_a=ta, trans_b=tb, out=c)
+                torch.matmul(fa(), fb())
+            o, t = [], []
+            for _ in range(args.rounds):
+                o.append(timeit(lambda: ops.mm(a, b, trans_a=ta, trans_b=tb, out=c), iters, dev))
+                t.append(timeit(lambda: torch.matmul(fa(), fb()), iters, dev))
+            tag = ("T" if ta else "N") + ("T" if tb else "N")
+            d[f"{tag}_tflops"] = round(fl / min(o) / 1e12, 1)
+            d[f"{tag}_torch_tflops"] = round(fl / min(t) / 1e12, 1)
+            del a, b, c
+        emit(d)
+        torch.cuda.empty_cache()
+
+    for spec in [x for x in args.linear.split(",") if x]:
+        T, K, N = map(int, spec.split("x"))
+        x = ((torch.rand(T, K, device=dev) * 2 - 1).to(torch.bfloat16)).requires_grad_(True)
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.02).to(torch.bfloat16).requires_grad_(True)
+        bb = torch.zeros(N, device=dev, dtype=torch.bfloat16).requires_grad_(True)
+        gy = (torch.rand(T, N, device=dev) * 2 - 1).to(torch.bfloat16)
+        F = torch.nn.functional
+
+        def ours():
+            ops.linear(x, w, bb, act="gelu_tanh").backward(gy)
+
+        def theirs():
+            F.gelu(F.linear(x, w, bb), approximate="tanh").backward(gy)
+        for _ in range(3):
+            ours()
+            theirs()
+        o, t = [], []
+        for _ in range(args.rounds):
+            o.append(timeit(ours, 10, dev))
+            t.append(timeit(theirs, 10, dev))
+        fl = 3 * 2.0 * T * K * N
+        emit({"kind": "linear_gelu_fwd_bwd_bf16", "T": T, "K": K, "N": N, "ours_ms": round(min(o) * 1e3, 3),
+              "torch_ms": round(min(t) * 1e3, 3), "ours_tflops": round(fl / min(o) / 1e12, 1),
+              "torch_tflops": round(fl / min(t) / 1e12, 1)})
+        del x, w, bb, gy
         torch.cuda.empty_cache()
 
     for spec in [x for x in args.ln.split(",") if x]:
