@@ -151,6 +151,19 @@ def main() -> int:
                 torch.cuda.empty_cache()
         except Exception as e:  # reported, never fatal for the GEMM number
             extra["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
+        # the hand-written peer all-reduces (K3) on the same GPUs, and the per-link xGMI ceiling
+        # their busbw is judged against (153 GB/s x 7 links per GPU, spec)
+        try:
+            from kubeflow_rm_amd.parallel.collectives import fast_allreduce_sweep, xgmi_probe
+            extra["allreduce_oneshot_bf16"] = fast_allreduce_sweep([16 << s for s in range(0, 15, 2)], "oneshot")
+            extra["allreduce_twoshot_bf16"] = fast_allreduce_sweep([256 << 10 << s for s in range(0, 9, 2)],
+                                                                   "twoshot")
+            torch.cuda.empty_cache()
+            xg = xgmi_probe()
+            extra["xgmi_peer"] = xg
+            extra["xgmi_peer_GBps"] = xg["pair_GBps_median"]
+        except Exception as e:  # reported, never fatal for the GEMM number
+            extra["fast_allreduce_error"] = f"{type(e).__name__}: {e}"
     if args.compare_torch and rank == 0:
         for _ in range(5):
             torch.matmul(a, b.t())

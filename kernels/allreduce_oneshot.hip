@@ -116,6 +116,20 @@ struct Vec<__bf16> {
   __device__ static void store1(void* p, long long i, float v) { static_cast<__bf16*>(p)[i] = (__bf16)v; }
 };
 
+// NaN into this block's vector indices i = blockIdx.x*kThreads + t (+ k*stride) < nvec, and block 0's
+// scalar tail [nvec*kElems, n): the write set of the block in the reduce loops below.
+template <typename V>
+__device__ void poison(void* out, long long n, long long nvec, long long stride) {
+  float nan8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) nan8[k] = __builtin_nanf("");
+  const uint4 nv = V::pack(nan8);
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += stride)
+    static_cast<uint4*>(out)[i] = nv;
+  if (blockIdx.x == 0)
+    for (long long i = nvec * V::kElems + threadIdx.x; i < n; i += kThreads) V::store1(out, i, __builtin_nanf(""));
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long n, int nranks, int rank0,
                                                               uint32_t epoch, uint64_t timeout_ticks,
@@ -125,9 +139,10 @@ __global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long
   const long long nvec = n / V::kElems;
   const long long stride = (long long)gridDim.x * kThreads;
   if (barrier(P, me, nranks, 0, epoch, timeout_ticks, timeout)) {
-    // a peer's input may be stale: poison this block's share of the output, skip the exit barrier
-    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride)
-      V::store1(P.out[me], i, __builtin_nanf(""));
+    // a peer's input may be stale: poison exactly the share this block would have written (the same
+    // vector indices as the reduce loop below, plus block 0's tail), skip the exit barrier. Blocks
+    // that passed the barrier keep their (correct) sums; nothing here touches their indices.
+    poison<V>(P.out[me], n, nvec, stride);
     return;
   }
   // 16-byte vectors; rank r's vector i lives at in[r] + 16 i
@@ -153,6 +168,83 @@ __global__ __launch_bounds__(kThreads) void allreduce_oneshot(Peers P, long long
   barrier(P, me, nranks, 1, epoch, timeout_ticks, timeout);
 }
 
+// ---- two-shot (reduce-scatter + all-gather) over the same peer-visible buffers -------------------
+// For mid-size messages: the one-shot makes every rank read all N inputs in full
+// ((N-1) x n bytes over xGMI per rank); the two-shot reads 2 (N-1)/N x n, and every rank pulls from
+// all N-1 peers at once, so all 7 links of an 8-GPU hive carry traffic (a ring uses one).
+//   entry barrier (phase 0) -> inputs published
+//   phase A: rank r owns vector slice r; block b sums its portion of slice r over all N inputs and
+//            writes it to in[r] (in place: only rank r ever reads in[r]'s slice r, and it has) and to
+//            out[r]
+//   mid barrier (phase 1)   -> block b of every rank has finished its portion of its slice
+//   phase B: block b copies its portion of every other slice s from in[s] (peer) into out[r]
+//   exit barrier (phase 2)  -> no rank reuses in[] while a peer may still read it
+// Block b of every rank owns the same index pattern in every slice, so the per-block-pair barriers
+// order exactly the writes and reads that meet. The scalar tail (n % vector width) is summed
+// directly by block 0 of every rank. Outputs need not be peer-visible (only in[] is read remotely).
+// Timeout handling as for the one-shot: the block poisons its whole write set and stops.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void allreduce_twoshot(Peers P, long long n, int nranks, int rank0,
+                                                              uint32_t epoch, uint64_t timeout_ticks,
+                                                              unsigned* timeout) {
+  using V = Vec<T>;
+  const int me = rank0 + blockIdx.y;
+  const long long nvec = n / V::kElems;
+  const long long per = (nvec + nranks - 1) / nranks;  // vectors per rank slice
+  const long long stride = (long long)gridDim.x * kThreads;
+  const long long first = (long long)blockIdx.x * kThreads + threadIdx.x;
+  auto poison_all = [&]() {  // this block's write set: its portion of every slice, and block 0's tail
+    float nan8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nan8[k] = __builtin_nanf("");
+    const uint4 nv = V::pack(nan8);
+    for (int sl = 0; sl < nranks; ++sl) {
+      const long long s0 = (long long)sl * per, s1 = min(nvec, s0 + per);
+      for (long long i = s0 + first; i < s1; i += stride) static_cast<uint4*>(P.out[me])[i] = nv;
+    }
+    if (blockIdx.x == 0)
+      for (long long i = nvec * V::kElems + threadIdx.x; i < n; i += kThreads) V::store1(P.out[me], i, __builtin_nanf(""));
+  };
+  if (barrier(P, me, nranks, 0, epoch, timeout_ticks, timeout)) {
+    poison_all();
+    return;
+  }
+  {
+    const long long s0 = (long long)me * per, s1 = min(nvec, s0 + per);
+    for (long long i = s0 + first; i < s1; i += stride) {
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      uint4 v[kMaxRanks];
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r)
+        if (r < nranks) v[r] = static_cast<const uint4*>(P.in[r])[i];
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r)
+        if (r < nranks) V::acc(s, v[r]);
+      const uint4 o = V::pack(s);
+      static_cast<uint4*>(const_cast<void*>(P.in[me]))[i] = o;
+      static_cast<uint4*>(P.out[me])[i] = o;
+    }
+    if (blockIdx.x == 0) {
+      for (long long i = nvec * V::kElems + threadIdx.x; i < n; i += kThreads) {
+        float s = 0.f;
+        for (int r = 0; r < nranks; ++r) s += V::load1(P.in[r], i);
+        V::store1(P.out[me], i, s);
+      }
+    }
+  }
+  if (barrier(P, me, nranks, 1, epoch, timeout_ticks, timeout)) {
+    poison_all();
+    return;
+  }
+  for (int k = 1; k < nranks; ++k) {  // start at the next rank so the peers' reads spread over links
+    const int src = (me + k) % nranks;
+    const long long s0 = (long long)src * per, s1 = min(nvec, s0 + per);
+    for (long long i = s0 + first; i < s1; i += stride)
+      static_cast<uint4*>(P.out[me])[i] = static_cast<const uint4*>(P.in[src])[i];
+  }
+  barrier(P, me, nranks, 2, epoch, timeout_ticks, timeout);
+}
+
 uint64_t g_timeout_ticks = 5000 * kTicksPerMs;
 
 }  // namespace
@@ -161,8 +253,18 @@ extern "C" void kfamd_allreduce_oneshot_set_timeout_ms(int ms) {
   g_timeout_ticks = (uint64_t)(ms < 1 ? 1 : ms) * kTicksPerMs;
 }
 
+// Flag arrays are shared by the one-shot (phases 0-1) and the two-shot (phases 0-2): epochs
+// increase per call whichever kernel runs, and every wait compares for equality with its own call's
+// epoch, so a stale flag of an earlier call of either kind never releases a barrier.
 extern "C" long long kfamd_allreduce_oneshot_flag_bytes(int nranks, int nblocks) {
-  return (long long)2 * nranks * nblocks * (long long)sizeof(uint32_t);
+  return (long long)3 * nranks * nblocks * (long long)sizeof(uint32_t);
+}
+
+extern "C" int kfamd_allreduce_twoshot_blocks(long long n, int dtype, int nranks) {
+  const long long vec = dtype == KFAMD_DTYPE_BF16 ? 8 : 4;
+  const long long per = ((n + vec - 1) / vec + nranks - 1) / (nranks < 1 ? 1 : nranks);
+  long long b = (per + kThreads * 2 - 1) / (kThreads * 2);  // ~2 vectors per thread per slice
+  return (int)(b < 1 ? 1 : (b > 64 ? 64 : b));
 }
 
 extern "C" int kfamd_allreduce_oneshot_blocks(long long n, int dtype) {
@@ -197,6 +299,38 @@ extern "C" int kfamd_allreduce_oneshot(const void* const* inputs, void* const* o
                        g_timeout_ticks, timeout);
   else
     hipLaunchKernelGGL(allreduce_oneshot<float>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch,
+                       g_timeout_ticks, timeout);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+// Two-shot: inputs are peer-visible and are overwritten in place (slice r of rank r's input ends up
+// holding the reduced slice); outputs are per rank, need not be peer-visible and receive the full sum.
+extern "C" int kfamd_allreduce_twoshot(void* const* inputs, void* const* outputs, uint32_t* const* flags, int nranks,
+                                       int rank0, int launch_ranks, long long n, int dtype, unsigned epoch,
+                                       int nblocks, unsigned* timeout, void* stream) {
+  if (nranks < 1 || nranks > kMaxRanks || launch_ranks < 1 || rank0 < 0 || rank0 + launch_ranks > nranks ||
+      n < 0 || epoch == 0 || nblocks < 1 || !timeout || (dtype != KFAMD_DTYPE_F32 && dtype != KFAMD_DTYPE_BF16))
+    return KFAMD_EINVAL;
+  Peers P{};
+  for (int r = 0; r < nranks; ++r) {
+    if (!inputs[r] || !flags[r]) return KFAMD_EINVAL;
+    if (reinterpret_cast<uintptr_t>(inputs[r]) & 15) return KFAMD_EALIGN;
+    P.in[r] = inputs[r];
+    P.flags[r] = flags[r];
+  }
+  for (int r = rank0; r < rank0 + launch_ranks; ++r) {
+    if (!outputs[r]) return KFAMD_EINVAL;
+    if (reinterpret_cast<uintptr_t>(outputs[r]) & 15) return KFAMD_EALIGN;
+    P.out[r] = outputs[r];
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(nblocks, launch_ranks), block(kThreads);
+  if (dtype == KFAMD_DTYPE_BF16)
+    hipLaunchKernelGGL(allreduce_twoshot<__bf16>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch,
+                       g_timeout_ticks, timeout);
+  else
+    hipLaunchKernelGGL(allreduce_twoshot<float>, grid, block, 0, s, P, n, nranks, rank0, (uint32_t)epoch,
                        g_timeout_ticks, timeout);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);

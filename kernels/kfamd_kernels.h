@@ -103,6 +103,14 @@ int kfamd_allreduce_oneshot(const void* const* inputs, void* const* outputs, uin
                             int nranks, int rank0, int launch_ranks, long long n, int dtype,
                             unsigned epoch, int nblocks, unsigned* timeout, void* stream);
 
+// Two-shot (reduce-scatter + all-gather) for mid-size messages: inputs peer-visible
+// and overwritten in place (rank r's slice r becomes the reduced slice), outputs per rank (need not be
+// peer-visible). Same flags / epochs / timeout contract as the one-shot (flag arrays are shared).
+int kfamd_allreduce_twoshot_blocks(long long n, int dtype, int nranks);
+int kfamd_allreduce_twoshot(void* const* inputs, void* const* outputs, uint32_t* const* flags, int nranks, int rank0,
+                            int launch_ranks, long long n, int dtype, unsigned epoch, int nblocks, unsigned* timeout,
+                            void* stream);
+
 // HIP IPC registration for one-process-per-GPU ranks (64-byte handles exchanged by the caller).
 int kfamd_ipc_alloc(long long bytes, int uncached, void** ptr, void* handle64);
 int kfamd_ipc_open(const void* handle64, void** ptr);

@@ -41,6 +41,9 @@ _SIGNATURES = {
     "kfamd_allreduce_oneshot_set_timeout_ms": (None, [c_int]),
     "kfamd_allreduce_oneshot": (c_int, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_int, c_int,
                                         c_int, c_ll, c_int, ctypes.c_uint, c_int, c_vp, c_vp]),
+    "kfamd_allreduce_twoshot_blocks": (c_int, [c_ll, c_int, c_int]),
+    "kfamd_allreduce_twoshot": (c_int, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_int, c_int,
+                                        c_int, c_ll, c_int, ctypes.c_uint, c_int, c_vp, c_vp]),
     "kfamd_ipc_alloc": (c_int, [c_ll, c_int, ctypes.POINTER(c_vp), ctypes.c_char_p]),
     "kfamd_ipc_open": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_vp)]),
     "kfamd_ipc_close": (c_int, [c_vp]),

@@ -2,7 +2,10 @@
 
 One kernel per rank reads every peer's registered buffer over xGMI and sums it (fp32, rank order,
 so every rank's result is bit-identical); two block-pair flag barriers replace RCCL's 2(N-1) ring
-hops, which is what bounds a KB-sized all-reduce. Large messages stay on RCCL.
+hops, which is what bounds a KB-sized all-reduce. Mid-size messages take the two-shot kernel
+(reduce-scatter + all-gather in one launch: 2(N-1)/N of the bytes per rank instead of N-1, pulled
+from all peers at once so every xGMI link carries traffic). ``algo="auto"`` switches at
+``TWOSHOT_MIN_BYTES``.
 
 :class:`OneShotAllReduce` owns the registered buffers for a set of ranks that this process can
 address: several devices of one process (peer access, the readiness op's layout) or, for tests on
@@ -18,6 +21,13 @@ from . import _lib
 from .gemm import _stream_ptr
 
 _DTYPES = {torch.float32: 0, torch.bfloat16: 1}
+TWOSHOT_MIN_BYTES = 256 << 10
+
+
+def pick_algo(nbytes: int, nranks: int, algo: str = "auto") -> str:
+    if algo != "auto":
+        return algo
+    return "twoshot" if nranks > 2 and nbytes >= TWOSHOT_MIN_BYTES else "oneshot"
 
 
 class OneShotAllReduce:
@@ -50,8 +60,9 @@ class OneShotAllReduce:
         self._out = arr(*[t.data_ptr() for t in self.outputs])
         self._flags = arr(*[t.data_ptr() for t in self.flags])
 
-    def __call__(self, tensors: list[torch.Tensor]) -> list[torch.Tensor]:
-        """All-reduce ``tensors`` (one per rank, same numel); returns views of the outputs."""
+    def __call__(self, tensors: list[torch.Tensor], algo: str = "auto") -> list[torch.Tensor]:
+        """All-reduce ``tensors`` (one per rank, same numel); returns views of the outputs.
+        ``algo``: "oneshot", "twoshot" or "auto" (by message size)."""
         if len(tensors) != self.nranks:
             raise ValueError("one tensor per rank")
         n = tensors[0].numel()
@@ -62,20 +73,27 @@ class OneShotAllReduce:
         self.epoch += 1
         L = _lib.lib()
         dt = _DTYPES[self.dtype]
-        nb = min(self.max_blocks, L.kfamd_allreduce_oneshot_blocks(n, dt))
+        algo = pick_algo(n * tensors[0].element_size(), self.nranks, algo)
+        if algo == "twoshot":
+            fn, nb = L.kfamd_allreduce_twoshot, L.kfamd_allreduce_twoshot_blocks(n, dt, self.nranks)
+        elif algo == "oneshot":
+            fn, nb = L.kfamd_allreduce_oneshot, L.kfamd_allreduce_oneshot_blocks(n, dt)
+        else:
+            raise ValueError(f"algo {algo}")
+        nb = min(self.max_blocks, nb)
+        self.last_algo = algo
         if self.simulated:
-            rc = L.kfamd_allreduce_oneshot(self._in, self._out, self._flags, self.nranks, 0, self.nranks, n, dt,
-                                           self.epoch, nb, self.timeout[0].data_ptr(), _stream_ptr(tensors[0]))
-            _lib.check(rc, f"allreduce_oneshot[{self.nranks}x{n}]")
+            rc = fn(self._in, self._out, self._flags, self.nranks, 0, self.nranks, n, dt,
+                    self.epoch, nb, self.timeout[0].data_ptr(), _stream_ptr(tensors[0]))
+            _lib.check(rc, f"allreduce_{algo}[{self.nranks}x{n}]")
         else:
             # inputs are copied on each device's current stream; the kernels then run concurrently,
             # one per device, meeting at the flag barriers
             for r, d in enumerate(self.devices):
                 with torch.cuda.device(d):
-                    rc = L.kfamd_allreduce_oneshot(self._in, self._out, self._flags, self.nranks, r, 1, n, dt,
-                                                   self.epoch, nb, self.timeout[r].data_ptr(),
-                                                   torch.cuda.current_stream(d).cuda_stream)
-                _lib.check(rc, f"allreduce_oneshot[rank {r}/{self.nranks}x{n}]")
+                    rc = fn(self._in, self._out, self._flags, self.nranks, r, 1, n, dt,
+                            self.epoch, nb, self.timeout[r].data_ptr(), torch.cuda.current_stream(d).cuda_stream)
+                _lib.check(rc, f"allreduce_{algo}[rank {r}/{self.nranks}x{n}]")
         return [o[:n].view(tensors[r].shape) for r, o in enumerate(self.outputs)]
 
     def timed_out(self) -> bool:

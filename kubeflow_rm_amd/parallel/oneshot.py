@@ -5,8 +5,10 @@ are exchanged once over the process group, and every rank maps its peers' buffer
 (``kfamd_ipc_open``). A call then copies the tensor into the rank's own buffer and launches
 ``kernels/allreduce_oneshot.hip`` on the current stream: every rank reads all peers over xGMI and
 writes the sum into the tensor. For the latency-bound sizes of TP decode / small DP buckets this
-replaces RCCL's 2(N-1) ring steps with one kernel; :func:`all_reduce` routes larger tensors to
-``torch.distributed.all_reduce`` (RCCL).
+replaces RCCL's 2(N-1) ring steps with one kernel. Mid-size tensors (``TWOSHOT_MIN_BYTES`` up to the
+registered size) take the two-shot kernel: reduce-scatter + all-gather in one launch, every rank
+pulling its slice from all peers at once (all xGMI links busy; 2(N-1)/N of the bytes instead of
+N-1). :func:`all_reduce` routes larger tensors to ``torch.distributed.all_reduce`` (RCCL).
 
 Failure model: the kernel's barriers wait at most ``timeout_ms`` (wall clock) for a peer. A missed
 deadline NaN-poisons that call's output and sets a device flag; the flag protocol is then out of
@@ -24,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from kubeflow_rm_amd.ops import _lib
+from kubeflow_rm_amd.ops.allreduce import pick_algo
 
 _DTYPES = {torch.float32: 0, torch.bfloat16: 1}
 MAX_BLOCKS = 64
@@ -77,8 +80,9 @@ class IpcOneShotAllReduce:
         self.epoch = 0
         dist.barrier(group=group)  # every rank mapped its peers before the first call
 
-    def __call__(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum of ``t`` (contiguous fp32 / bf16 CUDA tensor) over the group."""
+    def __call__(self, t: torch.Tensor, algo: str = "auto") -> torch.Tensor:
+        """In-place sum of ``t`` (contiguous fp32 / bf16 CUDA tensor) over the group. ``algo``:
+        "oneshot", "twoshot" or "auto" (by size; every rank must pick the same one)."""
         if t.dtype not in _DTYPES or not t.is_cuda or not t.is_contiguous():
             raise ValueError("contiguous fp32/bf16 CUDA tensor expected")
         nbytes = t.numel() * t.element_size()
@@ -94,10 +98,15 @@ class IpcOneShotAllReduce:
         self.epoch += 1
         self._out[self.rank] = t.data_ptr()
         dt = _DTYPES[t.dtype]
-        nb = min(MAX_BLOCKS, L.kfamd_allreduce_oneshot_blocks(t.numel(), dt))
-        rc = L.kfamd_allreduce_oneshot(self._in, self._out, self._flags, self.world, self.rank, 1, t.numel(), dt,
-                                       self.epoch, nb, self.timeout.data_ptr(), stream)
-        _lib.check(rc, f"allreduce_oneshot[rank {self.rank}/{self.world}, {t.numel()}]")
+        algo = pick_algo(nbytes, self.world, algo)
+        if algo == "twoshot":  # reduces in place in the registered buffers, gathers into t
+            fn, nb = L.kfamd_allreduce_twoshot, L.kfamd_allreduce_twoshot_blocks(t.numel(), dt, self.world)
+        else:
+            fn, nb = L.kfamd_allreduce_oneshot, L.kfamd_allreduce_oneshot_blocks(t.numel(), dt)
+        nb = min(MAX_BLOCKS, nb)
+        rc = fn(self._in, self._out, self._flags, self.world, self.rank, 1, t.numel(), dt,
+                self.epoch, nb, self.timeout.data_ptr(), stream)
+        _lib.check(rc, f"allreduce_{algo}[rank {self.rank}/{self.world}, {t.numel()}]")
         if self.epoch % self.check_every == 0:
             self.check()
         return t

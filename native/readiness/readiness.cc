@@ -27,7 +27,8 @@
 // Flags: --m/--n/--k GEMM size (default 4096^3), --iters, --ln-rows/--ln-hidden,
 //        --ar-max-bytes (default 64 MiB), --min-tflops (fail below), --skip-ln, --skip-allreduce,
 //        --oneshot-sim N, --full-sweep (one-shot at every size, not 3), --rccl (RCCL sweep on >= 2
-//        GPUs), --rccl-single (RCCL stage with one device), --serial (devices one after another).
+//        GPUs), --rccl-single (RCCL stage with one device), --serial (devices one after another),
+//        --xgmi (peer-copy bandwidth probe: each link alone, then all links at once).
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <rccl/rccl.h>
@@ -41,6 +42,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -146,7 +148,9 @@ struct Args {
   bool rccl = false;        // --rccl: RCCL communicator + busbw sweep on >= 2 GPUs (opt-in)
   bool serial = false;      // --serial: check devices one after another
   int oneshot_sim = 0;  // > 0: one-shot all-reduce with this many ranks simulated on device 0
-  bool full_sweep = false;  // --full-sweep: one-shot at every 4x size 16 B..256 KiB, 50 timed calls each
+  bool full_sweep = false;  // --full-sweep: one-shot at every 4x size 16 B..256 KiB, 50 timed calls each,
+                            // two-shot 256 KiB..64 MiB, and the xGMI peer-copy probe
+  bool xgmi = false;        // --xgmi: peer-copy bandwidth probe (pairs, then all pairs at once)
   std::string inject_fault;  // fault injection: fail the op at this stage
 };
 
@@ -624,6 +628,77 @@ bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<h
     sweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}});
   }
   lap("sweep_ms");
+  // two-shot (reduce-scatter + all-gather over all peers at once) for the mid sizes: one size on the
+  // cold-start path (correctness of the kernel on this hive), 256 KiB..64 MiB with --full-sweep
+  Json tsweep = Json::array();
+  if (nranks > 2 || full_sweep) {
+    const size_t ts_max = full_sweep ? (64u << 20) : (1u << 20);
+    std::vector<void*> tin(8, nullptr), tout(8, nullptr);
+    for (int r = 0; r < nranks; ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      HIP_OK(hipMalloc(&tin[r], ts_max));
+      HIP_OK(hipMalloc(&tout[r], ts_max));
+    }
+    auto launch_ts = [&](size_t n) -> bool {
+      ++epoch;
+      const int nb = kfamd_allreduce_twoshot_blocks((long long)n, KFAMD_DTYPE_F32, nranks);
+      for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        int rc = kfamd_allreduce_twoshot(tin.data(), tout.data(), flags.data(), nranks, sim ? 0 : r,
+                                         sim ? nranks : 1, (long long)n, KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r]);
+        if (rc != 0) {
+          fail("kfamd_allreduce_twoshot rc=" + std::to_string(rc));
+          return false;
+        }
+      }
+      for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        HIP_OK(hipStreamSynchronize(st[r]));
+      }
+      return true;
+    };
+    std::vector<size_t> tsizes;
+    if (full_sweep)
+      for (size_t b = 256u << 10; b <= ts_max; b *= 4) tsizes.push_back(b);
+    else
+      tsizes = {ts_max};
+    for (size_t bytes : tsizes) {
+      const size_t n = bytes / 4;
+      for (int r = 0; r < nranks; ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        hipLaunchKernelGGL(fill_const, dim3(64), dim3(256), 0, st[sim ? 0 : r], static_cast<float*>(tin[r]), n,
+                           (float)(r + 1));
+        HIP_OK(hipStreamSynchronize(st[sim ? 0 : r]));
+      }
+      if (!launch_ts(n)) return false;
+      const float want = (float)nranks * (nranks + 1) / 2;
+      std::vector<float> h(n);
+      for (int r = 0; r < nranks; ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        unsigned t = 0;
+        HIP_OK(hipMemcpyAsync(h.data(), tout[r], bytes, hipMemcpyDeviceToHost, stream_of(r)));
+        HIP_OK(hipMemcpyAsync(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost, stream_of(r)));
+        HIP_OK(hipStreamSynchronize(stream_of(r)));
+        for (size_t i = 0; i < n; ++i)
+          if (h[i] != want) ok = false;
+        if (t) ok = false;
+      }
+      const int it = full_sweep ? 20 : 5;
+      auto t1 = std::chrono::steady_clock::now();
+      for (int k = 0; k < it; ++k)
+        if (!launch_ts(n)) return false;
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / it;
+      const double algbw = bytes / (us * 1e-6) / 1e9;
+      tsweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}, {"algbw_GBps", algbw},
+                            {"busbw_GBps", algbw * 2.0 * (nranks - 1) / nranks}});
+    }
+    for (int r = 0; r < nranks; ++r) {
+      (void)hipSetDevice(dev_of(r));
+      (void)hipFree(tin[r]);
+      (void)hipFree(tout[r]);
+    }
+    lap("twoshot_ms");
+  }
   for (int r = 0; r < nranks; ++r) {
     (void)hipSetDevice(dev_of(r));
     (void)hipFree(in[r]);
@@ -636,8 +711,90 @@ bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<h
   lap("free_ms");
   out = Json{{"mode", sim ? "simulated-on-device-0" : "peer"}, {"ranks", nranks}, {"sweep", sweep}, {"correct", ok}, {"stages", stages},
              {"note", "us = host wall per call incl. launch + stream sync"}};
+  if (tsweep.size()) out["twoshot_sweep"] = tsweep;
   if (!ok) fail("one-shot all-reduce mismatch or peer timeout");
   return ok;
+}
+
+// xGMI peer-copy probe (the per-link rate the collectives are judged against must be
+// measured — spec 153 GB/s per link, 7 links per GPU). Phase 1: one ordered pair at a time, 256 MiB
+// hipMemcpyPeerAsync x iters (the single-link rate). Phase 2: every device copies to every other at
+// once, one stream per destination (per-GPU egress with all links busy).
+bool xgmi_probe(int ndev, Json& out) {
+  g_stage = "xgmi-probe";
+  if (ndev < 2) {
+    out = Json{{"skipped", "needs >= 2 GPUs"}};
+    return true;
+  }
+  const size_t bytes = 256u << 20;
+  const int iters = 5;
+  std::vector<void*> buf(ndev, nullptr);
+  std::vector<std::vector<hipStream_t>> st(ndev, std::vector<hipStream_t>(ndev, nullptr));
+  for (int i = 0; i < ndev; ++i) {
+    HIP_OK(hipSetDevice(i));
+    for (int j = 0; j < ndev; ++j) {
+      if (i == j) continue;
+      hipError_t pe = hipDeviceEnablePeerAccess(j, 0);
+      if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+        fail(std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(pe));
+        return false;
+      }
+      HIP_OK(hipStreamCreate(&st[i][j]));
+    }
+    HIP_OK(hipMalloc(&buf[i], bytes));
+    HIP_OK(hipMemset(buf[i], i + 1, bytes));
+  }
+  Json matrix = Json::array();
+  std::vector<double> vals;
+  for (int s = 0; s < ndev; ++s) {
+    Json row = Json::array();
+    for (int d = 0; d < ndev; ++d) {
+      if (s == d) {
+        row.push_back(0.0);
+        continue;
+      }
+      HIP_OK(hipSetDevice(s));
+      HIP_OK(hipMemcpyPeerAsync(buf[d], d, buf[s], s, bytes, st[s][d]));  // warm the path
+      HIP_OK(hipStreamSynchronize(st[s][d]));
+      auto t0 = std::chrono::steady_clock::now();
+      for (int k = 0; k < iters; ++k) HIP_OK(hipMemcpyPeerAsync(buf[d], d, buf[s], s, bytes, st[s][d]));
+      HIP_OK(hipStreamSynchronize(st[s][d]));
+      const double gbps = (double)bytes * iters / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / 1e9;
+      row.push_back(gbps);
+      vals.push_back(gbps);
+    }
+    matrix.push_back(row);
+  }
+  // all pairs at once
+  auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0; k < iters; ++k)
+    for (int s = 0; s < ndev; ++s)
+      for (int d = 0; d < ndev; ++d)
+        if (s != d) {
+          HIP_OK(hipSetDevice(s));
+          HIP_OK(hipMemcpyPeerAsync(buf[d], d, buf[s], s, bytes / (ndev - 1), st[s][d]));
+        }
+  for (int s = 0; s < ndev; ++s)
+    for (int d = 0; d < ndev; ++d)
+      if (s != d) {
+        HIP_OK(hipSetDevice(s));
+        HIP_OK(hipStreamSynchronize(st[s][d]));
+      }
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const double egress = (double)bytes * iters / sec / 1e9;  // per GPU: bytes/(ndev-1) to each of ndev-1 peers
+  for (int i = 0; i < ndev; ++i) {
+    (void)hipSetDevice(i);
+    (void)hipFree(buf[i]);
+    for (int j = 0; j < ndev; ++j)
+      if (st[i][j]) (void)hipStreamDestroy(st[i][j]);
+  }
+  std::sort(vals.begin(), vals.end());
+  out = Json{{"bytes", (long long)bytes}, {"iters", iters}, {"pair_GBps", matrix},
+             {"pair_GBps_min", vals.front()}, {"pair_GBps_median", vals[vals.size() / 2]},
+             {"pair_GBps_max", vals.back()}, {"all_pairs_egress_GBps_per_gpu", egress},
+             {"spec_link_GBps", 153.0},
+             {"note", "hipMemcpyPeerAsync; pair = one link at a time, all-pairs = every GPU to every peer at once"}};
+  return true;
 }
 
 }  // namespace
@@ -860,6 +1017,7 @@ int readiness_main(int argc, char** argv) {
     else if (s == "--rccl") a.rccl = true;
     else if (s == "--fast-exit") g_fast_exit = true;
     else if (s == "--full-sweep") a.full_sweep = true;
+    else if (s == "--xgmi") a.xgmi = true;
     else if (s == "--no-fast-exit") g_fast_exit = false;
     else if (s == "--serial") a.serial = true;
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
@@ -974,6 +1132,13 @@ int readiness_main(int argc, char** argv) {
       oneshot_check(ndev, a.oneshot_sim, a.full_sweep, streams, os);
       g_result["allreduce_oneshot"] = os;
       g_result["stages_ms"]["allreduce_oneshot"] = lap(ts);
+    }
+    if (ndev >= 2 && (a.xgmi || a.full_sweep)) {
+      Json xg;
+      auto ts = std::chrono::steady_clock::now();
+      xgmi_probe(ndev, xg);
+      g_result["xgmi"] = xg;
+      g_result["stages_ms"]["xgmi"] = lap(ts);
     }
   }
   g_stage = "report";

@@ -199,3 +199,141 @@ def test_tp_forward_on_oneshot_matches_reference_all_reduce():
     for r in spawn(_tp_oneshot_worker, 2, timeout=180):
         assert r["timed_out"] is False and r["calls"] >= 4, r  # 2 row-parallel reduces per block
         assert r["max_diff"] == 0.0, r
+
+
+# ---- r3: two-shot all-reduce, partial-timeout poisoning ------------------------------------------
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("numel", [8, 1001, 65536, 300_007, 2_000_000])
+def test_twoshot_matches_fp32_reference(nranks, dtype, numel):
+    """Reduce-scatter + all-gather in one launch: each slice is summed in rank order by its owner,
+    so the result is bit-identical to the fp32 rank-order reference on every rank."""
+    from kubeflow_rm_amd.ops import OneShotAllReduce
+    ar = OneShotAllReduce(nranks, 1 << 21, dtype)
+    g = torch.Generator(device="cuda").manual_seed(7 * nranks + numel)
+    xs = [torch.randn(numel, device="cuda", generator=g).to(dtype) for _ in range(nranks)]
+    outs = ar(xs, algo="twoshot")
+    torch.cuda.synchronize()
+    assert not ar.timed_out()
+    ref = _ref(xs).to(dtype)
+    for o in outs:
+        torch.testing.assert_close(o, ref, rtol=0, atol=0)
+    # alternate kinds on the shared flags: epochs keep them in step
+    outs = ar(xs, algo="oneshot")
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, ref) for o in outs) and not ar.timed_out()
+
+
+@pytest.mark.parametrize("kind", ["oneshot", "twoshot"])
+def test_partial_timeout_poisons_exactly_the_late_blocks_share(kind):
+    """only SOME blocks miss the deadline (the late rank's blocks arrive one at a time).
+    Rank 1 never launches; its entry-barrier flags are pre-set for half of rank 0's blocks. Those
+    blocks pass and write correct sums, the others time out and must NaN exactly their own share:
+    no element may keep the sentinel from before the call, none may be a wrong number."""
+    from kubeflow_rm_amd.ops import _lib
+    L = _lib.lib()
+    n, nb, epoch = 40_000, 8, 1
+    ins = [torch.randn(n, device="cuda") for _ in range(2)]
+    outs = [torch.full((n,), 7.0, device="cuda") for _ in range(2)]
+    fl = L.kfamd_allreduce_oneshot_flag_bytes(2, nb) // 4
+    flags = [torch.zeros(fl, dtype=torch.int32, device="cuda") for _ in range(2)]
+    for b in range(0, nb, 2):  # flags[me=0][phase 0][peer 1][block b] = epoch
+        flags[0][(0 * 2 + 1) * nb + b] = epoch
+    tmo = torch.zeros(1, dtype=torch.int32, device="cuda")
+    arr = ctypes.c_void_p * 8
+    fn = L.kfamd_allreduce_oneshot if kind == "oneshot" else L.kfamd_allreduce_twoshot
+    L.kfamd_allreduce_oneshot_set_timeout_ms(150)
+    try:
+        rc = fn(arr(*[t.data_ptr() for t in ins]), arr(*[t.data_ptr() for t in outs]),
+                arr(*[t.data_ptr() for t in flags]), 2, 0, 1, n, 0, epoch, nb, tmo.data_ptr(),
+                torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+    finally:
+        L.kfamd_allreduce_oneshot_set_timeout_ms(5000)
+    assert tmo.item() == 1
+    o = outs[0]
+    nan = torch.isnan(o)
+    assert not (o == 7.0).any().item(), "a timed-out block left part of its share unwritten"
+    ref = ins[0] + ins[1]
+    ok = ~nan
+    if kind == "oneshot":  # passed blocks computed their share; two-shot blocks stop at the mid barrier
+        assert ok.any().item() and nan.any().item()
+    assert torch.equal(o[ok], ref[ok]), "a non-NaN element differs from the true sum"
+
+
+def _ipc_twoshot_worker(rank):
+    import torch.distributed as dist
+    from kubeflow_rm_amd.parallel.oneshot import IpcOneShotAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    world = dist.get_world_size()
+    ar = IpcOneShotAllReduce(max_bytes=8 << 20)
+    worst = 0.0
+    for dtype in (torch.float32, torch.bfloat16):
+        for it, n in enumerate((1001, 300_000, 1_000_003)):
+            def data(r):
+                g = torch.Generator(device="cuda").manual_seed(77 * r + it)
+                return torch.randn(n, device="cuda", generator=g).to(dtype)
+            t = data(rank)
+            ar(t, algo="twoshot")
+            torch.cuda.synchronize()
+            ref = torch.zeros(n, device="cuda")
+            for r in range(world):
+                ref += data(r).float()
+            worst = max(worst, (t.float() - ref.to(dtype).float()).abs().max().item())
+    out = {"timed_out": ar.timed_out(), "worst": worst}
+    ar.close()
+    dist.destroy_process_group()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_twoshot_ranks_as_processes(world):
+    from kubeflow_rm_amd.parallel.launch import spawn
+    for r in spawn(_ipc_twoshot_worker, world, timeout=180):
+        assert r["timed_out"] is False and r["worst"] == 0.0, r
+
+
+def _probe_worker(rank):
+    import torch.distributed as dist
+    from kubeflow_rm_amd.parallel.collectives import fast_allreduce_sweep, xgmi_probe
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    xg = xgmi_probe(nbytes=32 << 20, iters=2)
+    ts = fast_allreduce_sweep([256 << 10, 4 << 20], "twoshot", iters=3)
+    os_ = fast_allreduce_sweep([16, 64 << 10], "oneshot", iters=3)
+    dist.destroy_process_group()
+    return {"xgmi": xg, "twoshot": ts, "oneshot": os_}
+
+
+def test_bench_multi_gpu_probes_run_as_processes():
+    """bench.py N > 1 extras (xGMI pair / all-pairs copy probe, one-/two-shot busbw sweeps) on
+    processes sharing the one GPU of the test box: exercises IPC registration, the pair schedule
+    and the result checks end to end (the numbers are same-device copies, not xGMI)."""
+    from kubeflow_rm_amd.parallel.launch import spawn
+    res = spawn(_probe_worker, 2, timeout=240)
+    for r in res:
+        xg = r["xgmi"]
+        assert xg["pair_GBps"][0][1] > 0 and xg["pair_GBps"][1][0] > 0 and xg["pair_GBps"][0][0] == 0
+        assert all(v > 0 for v in xg["all_pairs_egress_GBps_per_gpu"])
+        assert all(row["correct"] for row in r["twoshot"] + r["oneshot"]), r
+
+
+def test_readiness_op_twoshot_stage_simulated():
+    """The in-pod readiness op's K3 stage with 4 simulated ranks and --full-sweep: one-shot sweep
+    plus the two-shot 256 KiB..64 MiB sweep, every size checked exactly, busbw reported."""
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "kubeflow_rm_amd" / "bin" / "kfamd-readiness"
+    p = subprocess.run([str(exe), "--oneshot-sim", "4", "--full-sweep", "--skip-ln", "--m", "1024", "--n", "1024",
+                        "--k", "1024"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    os_ = rep["allreduce_oneshot"]
+    assert os_["correct"] is True and os_["ranks"] == 4
+    ts = os_["twoshot_sweep"]
+    assert [r["bytes"] for r in ts] == [256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20]
+    assert all(r["busbw_GBps"] > 0 for r in ts)
