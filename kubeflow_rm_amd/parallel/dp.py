@@ -19,6 +19,11 @@ Design for MI355X (not a DDP transliteration):
   ``finish()`` launches every remaining bucket in order, zero-filling missing grads — including
   buckets that saw no gradient at all on this rank. So rank A can never issue b0,b2,b1 while
   rank B issues b0,b1,b2 (an RCCL hang or mismatched-size reduce).
+* Unused parameters keep ``grad = None`` like torch DDP: zero-filling a missing grad
+  happens only in the bucket's flat buffer, never on ``p.grad``, and each bucket carries one
+  "used" slot per parameter (1 if this rank produced the grad) that is reduced with the data. A
+  parameter no rank used is left with ``grad is None`` (AdamW then skips it: no weight decay or
+  momentum step on weights the step never touched); one some rank used gets the reduced gradient.
 """
 from __future__ import annotations
 
@@ -99,18 +104,21 @@ class GradBucketer:
 
     def _launch(self, bi: int) -> None:
         b = self.buckets[bi]
-        for p in b.params:
-            if p.grad is None:  # no grad on this rank this step: contribute zeros
-                p.grad = torch.zeros_like(p)
-        dev = b.params[0].grad.device
+        dev = b.params[0].device
         if b.buffer is None or b.buffer.device != dev:
-            b.buffer = torch.empty(b.numel, dtype=b.dtype, device=dev)
-        for p, off in zip(b.params, b.offsets):
-            b.buffer[off:off + p.numel()].copy_(p.grad.reshape(-1))
+            b.buffer = torch.empty(b.numel + len(b.params), dtype=b.dtype, device=dev)
+        used = b.buffer[b.numel:]
+        used.fill_(1)
+        for i, (p, off) in enumerate(zip(b.params, b.offsets)):
+            if p.grad is None:  # no grad on this rank this step: contribute zeros, flag unused
+                b.buffer[off:off + p.numel()].zero_()
+                used[i].zero_()
+            else:
+                b.buffer[off:off + p.numel()].copy_(p.grad.reshape(-1))
         if self.average:
             b.buffer.div_(self.world)
         b.work = dist.all_reduce(b.buffer, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        self.comm_bytes += b.buffer.numel() * b.buffer.element_size()
+        self.comm_bytes += b.numel * b.buffer.element_size()
         self.launch_order.append(bi)
 
     def finish(self) -> None:
@@ -125,8 +133,14 @@ class GradBucketer:
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
-                for p, off in zip(b.params, b.offsets):
-                    p.grad.copy_(b.buffer[off:off + p.numel()].view_as(p.grad))
+                used = b.buffer[b.numel:].float().cpu().tolist()  # one small D2H per bucket
+                for p, off, u in zip(b.params, b.offsets, used):
+                    red = b.buffer[off:off + p.numel()].view_as(p)
+                    if p.grad is not None:
+                        p.grad.copy_(red)
+                    elif u > 0:  # another rank used it: take the reduced gradient
+                        p.grad = red.to(p.dtype).clone()
+                    # else: unused on every rank, grad stays None (torch DDP semantics)
                 b.work = None
             b.pending = len(b.params)
             b.ready = False

@@ -1,5 +1,6 @@
 // quota.cc — ResourceQuota admission + status controller with MI355X GPU / HBM accounting (K7).
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <memory>
 #include <mutex>
@@ -94,19 +95,38 @@ std::string fmt_num(double v) {
 // request's completion hook fires (in-process API server: committed or not), when the pod shows
 // up in the namespace's pod list (webhook mode, where no completion hook exists), or after
 // kReservationTtl (a webhook-admitted create that the API server then failed).
+// Reservations are keyed by the admission request (AdmissionReview uid, or a ledger sequence number
+// in-process), never by pod name: kube-apiserver sends generateName creates (ReplicaSet / Job pods)
+// with an EMPTY name, so name keys made concurrent generateName creates overwrite each other
+// (ADVICE r2). Landing is matched by name when the request had one, otherwise by generateName: the
+// oldest open reservation of that prefix claims one landed pod of the prefix created no earlier than
+// the reservation (a landed pod claims at most one reservation, ever).
 // Reference quota semantics: profile-controller/controllers/profile_controller.go:559-589
 // (the Profile's ResourceQuota) enforced by kube-apiserver's quota admission.
 namespace {
 constexpr double kReservationTtl = 30.0;
 
+double wall_seconds() {  // creationTimestamps are wall-clock; now_seconds() is monotonic
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+struct LandedPod {
+  std::string name, generate_name;
+  double created = 0;  // creationTimestamp, seconds (RFC 3339 has 1 s resolution)
+};
+
 struct QuotaLedger {
   struct Reservation {
     std::map<std::string, double> use;
-    double expires;
+    double expires = 0, reserved_at = 0;
+    std::string name, generate_name;
+    uint64_t seq = 0;
   };
   std::mutex mu;
-  std::map<std::string, std::map<std::string, Reservation>> by_ns;  // ns -> pod name -> usage
+  std::map<std::string, std::map<std::string, Reservation>> by_ns;  // ns -> request key -> usage
+  std::map<std::string, std::set<std::string>> claimed;              // ns -> landed pods that ended one
   std::map<std::string, std::unique_ptr<std::mutex>> ns_locks;
+  uint64_t next_seq = 0;
 
   std::mutex& ns_lock(const std::string& ns) {
     std::lock_guard<std::mutex> g(mu);
@@ -114,31 +134,69 @@ struct QuotaLedger {
     if (!m) m = std::make_unique<std::mutex>();
     return *m;
   }
-  // live reservations of ns other than pods already in `committed`; drops expired / landed ones
-  std::vector<std::map<std::string, double>> live(const std::string& ns, const std::set<std::string>& committed) {
+  // usage of ns's live reservations whose pod has not landed; drops expired and landed ones
+  std::vector<std::map<std::string, double>> live(const std::string& ns, const std::vector<LandedPod>& pods) {
     std::lock_guard<std::mutex> g(mu);
     std::vector<std::map<std::string, double>> out;
+    auto& cl = claimed[ns];
+    {  // forget claims of pods that are gone (the set only needs the pods still listed)
+      std::set<std::string> present;
+      for (const auto& p : pods) present.insert(p.name);
+      for (auto it = cl.begin(); it != cl.end();) it = present.count(*it) ? std::next(it) : cl.erase(it);
+    }
     auto it = by_ns.find(ns);
     if (it == by_ns.end()) return out;
     const double now = now_seconds();
-    for (auto r = it->second.begin(); r != it->second.end();) {
-      if (r->second.expires < now || committed.count(r->first)) {
-        r = it->second.erase(r);
-      } else {
-        out.push_back(r->second.use);
-        ++r;
+    std::vector<std::pair<uint64_t, std::string>> order;  // oldest reservation first
+    for (const auto& r : it->second) order.push_back({r.second.seq, r.first});
+    std::sort(order.begin(), order.end());
+    for (const auto& o : order) {
+      Reservation& r = it->second[o.second];
+      bool landed = false;
+      if (!r.name.empty()) {
+        for (const auto& p : pods)
+          if (p.name == r.name && !cl.count(p.name)) {
+            landed = true;
+            cl.insert(p.name);
+            break;
+          }
+      } else if (!r.generate_name.empty()) {
+        for (const auto& p : pods)
+          if (p.generate_name == r.generate_name && !cl.count(p.name) && p.created + 1.0 >= r.reserved_at) {
+            landed = true;
+            cl.insert(p.name);
+            break;
+          }
       }
+      if (landed || r.expires < now) it->second.erase(o.second);
+      else out.push_back(r.use);
     }
     return out;
   }
-  void reserve(const std::string& ns, const std::string& name, std::map<std::string, double> use) {
+  std::string reserve(const std::string& ns, const std::string& key_hint, const std::string& name,
+                      const std::string& generate_name, std::map<std::string, double> use) {
     std::lock_guard<std::mutex> g(mu);
-    by_ns[ns][name] = Reservation{std::move(use), now_seconds() + kReservationTtl};
+    const uint64_t seq = ++next_seq;
+    const std::string key = key_hint.empty() ? "seq:" + std::to_string(seq) : "uid:" + key_hint;
+    Reservation r;
+    r.use = std::move(use);
+    r.reserved_at = wall_seconds();
+    r.expires = now_seconds() + kReservationTtl;
+    r.name = name;
+    r.generate_name = generate_name;
+    r.seq = seq;
+    by_ns[ns][key] = std::move(r);
+    return key;
   }
-  void release(const std::string& ns, const std::string& name) {
+  void release(const std::string& ns, const std::string& key) {
     std::lock_guard<std::mutex> g(mu);
     auto it = by_ns.find(ns);
-    if (it != by_ns.end()) it->second.erase(name);
+    if (it != by_ns.end()) it->second.erase(key);
+  }
+  size_t open(const std::string& ns) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = by_ns.find(ns);
+    return it == by_ns.end() ? 0 : it->second.size();
   }
 };
 }  // namespace
@@ -155,15 +213,20 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
     Json pods;
     c->list("v1", "Pod", a.ns, ListOptions(), pods);
     std::map<std::string, double> used;
-    std::set<std::string> committed;
+    std::vector<LandedPod> landed;
     for (const auto& p : pods["items"].as_array()) {
-      committed.insert(p.str_at({"metadata", "name"}));
+      LandedPod lp;
+      lp.name = p.str_at({"metadata", "name"});
+      lp.generate_name = p.str_at({"metadata", "generateName"});
+      if (auto t = parse_rfc3339_ms(p.str_at({"metadata", "creationTimestamp"}))) lp.created = *t / 1000.0;
+      landed.push_back(std::move(lp));
       if (pod_counts(p))
         for (auto& kv : pod_quota_usage(p, hbm_dev)) used[kv.first] += kv.second;
     }
-    for (const auto& r : ledger->live(a.ns, committed))
+    for (const auto& r : ledger->live(a.ns, landed))
       for (const auto& kv : r) used[kv.first] += kv.second;
     auto want = pod_quota_usage(*a.object, hbm_dev);
+    const std::string name = !a.name.empty() ? a.name : a.object->str_at({"metadata", "name"});
     for (const auto& q : quotas["items"].as_array()) {
       std::vector<std::string> exceeded;
       for (const auto& h : q.at_path({"spec", "hard"}).as_object()) {
@@ -175,14 +238,15 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
                              ", limited: " + h.first + "=" + fmt_num(hard));
       }
       if (!exceeded.empty())
-        return ApiError{403, "Forbidden", "pods \"" + a.name + "\" is forbidden: exceeded quota: " + q.str_at({"metadata", "name"}) +
+        return ApiError{403, "Forbidden", "pods \"" + name + "\" is forbidden: exceeded quota: " + q.str_at({"metadata", "name"}) +
                                               ", requested: " + join(exceeded, "; ")};
     }
     if (a.dry_run) return {};
-    ledger->reserve(a.ns, a.name, std::move(want));
-    const std::string ns = a.ns, name = a.name;
+    const std::string key = ledger->reserve(a.ns, a.uid, name, a.object->str_at({"metadata", "generateName"}),
+                                            std::move(want));
+    const std::string ns = a.ns;
     // in-process: the pod is in the store (its list entry replaces the reservation) or never will be
-    a.on_done.push_back([ledger, ns, name](bool) { ledger->release(ns, name); });
+    a.on_done.push_back([ledger, ns, key](bool) { ledger->release(ns, key); });
     return {};
   };
 }
@@ -246,6 +310,7 @@ Json AdmissionWebhookServer::review(const std::string& path, const Json& ar) {
     a.subresource = req["subResource"].as_string();
     a.ns = req["namespace"].as_string();
     a.name = req["name"].as_string();
+    a.uid = req["uid"].as_string();
     a.version = req.at_path({"kind", "version"}).as_string();
     Json obj = req["object"];
     Json old = req["oldObject"];

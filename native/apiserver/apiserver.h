@@ -121,6 +121,7 @@ struct AdmissionAttrs {
   std::string operation;  // CREATE UPDATE DELETE
   std::shared_ptr<const ResourceInfo> res;
   std::string subresource, ns, name, version;
+  std::string uid;                   // AdmissionReview request uid (webhook mode); "" in-process
   Json* object = nullptr;            // mutable during the mutating phase
   const Json* old_object = nullptr;  // UPDATE/DELETE
   const UserInfo* user = nullptr;

@@ -480,13 +480,35 @@ TlsClientOptions& tls_client_default() {
   static TlsClientOptions o;
   return o;
 }
+std::shared_ptr<SSL_CTX> build_client_ctx(const TlsClientOptions& o, std::string* err);
+
+// A file's identity for the cache key: a rotated service-account ca.crt or client certificate (same
+// path, new content) must build a fresh context, so mtime + size are part of the key.
+std::string file_stamp(const std::string& path) {
+  struct stat st {};
+  if (path.empty() || ::stat(path.c_str(), &st) != 0) return "-";
+  return std::to_string((long long)st.st_mtim.tv_sec) + "." + std::to_string((long long)st.st_mtim.tv_nsec) + ":" +
+         std::to_string((long long)st.st_size);
+}
+
 std::shared_ptr<SSL_CTX> client_ctx(const TlsClientOptions& o, std::string* err) {
-  static std::map<std::string, std::shared_ptr<SSL_CTX>> cache;
+  // keyed by the option set plus the files' current stamps; superseded entries (a rotated file, or
+  // a webhook caBundle that changed) are evicted so the cache cannot grow without bound
+  static std::map<std::string, std::pair<std::string, std::shared_ptr<SSL_CTX>>> cache;  // opts -> (stamps, ctx)
   const std::string key = o.ca_file + '\0' + o.ca_pem + '\0' + o.cert_file + '\0' + o.key_file + '\0' +
                           (o.insecure_skip_verify ? "1" : "0");
+  const std::string stamps = file_stamp(o.ca_file) + '|' + file_stamp(o.cert_file) + '|' + file_stamp(o.key_file);
   std::lock_guard<std::mutex> g(tls_client_mu());
   auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
+  if (it != cache.end() && it->second.first == stamps) return it->second.second;
+  if (it != cache.end()) cache.erase(it);
+  if (cache.size() >= 64) cache.clear();  // bounded: caBundle-keyed entries of deleted webhooks
+  auto made = build_client_ctx(o, err);
+  if (made) cache[key] = {stamps, made};
+  return made;
+}
+
+std::shared_ptr<SSL_CTX> build_client_ctx(const TlsClientOptions& o, std::string* err) {
   std::shared_ptr<SSL_CTX> ctx(SSL_CTX_new(TLS_client_method()), SSL_CTX_free);
   if (!ctx) {
     if (err) *err = tls_error("SSL_CTX_new");
@@ -531,7 +553,6 @@ std::shared_ptr<SSL_CTX> client_ctx(const TlsClientOptions& o, std::string* err)
       return nullptr;
     }
   }
-  cache[key] = ctx;
   return ctx;
 }
 

@@ -60,14 +60,30 @@ bool AmdSmi::load_locked() {
   err_ = "built without AMD SMI headers";
   return false;
 #else
-  for (const char* name : {"libamd_smi.so.26", "libamd_smi.so", "/opt/rocm/lib/libamd_smi.so"}) {
-    lib_ = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+  // Only the SONAME of the headers this file was compiled against: amdsmi_gpu_metrics_t / amdsmi_bdf_t
+  // are laid out by those headers, and a library of another major version could write a larger
+  // struct into our stack objects. The runtime version is checked as well.
+#define KFAMD_STR2(x) #x
+#define KFAMD_STR(x) KFAMD_STR2(x)
+  const std::string soname = "libamd_smi.so." KFAMD_STR(AMDSMI_LIB_VERSION_MAJOR);
+  for (const std::string& name : {soname, std::string("/opt/rocm/lib/") + soname}) {
+    lib_ = dlopen(name.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (lib_) break;
   }
+#undef KFAMD_STR
+#undef KFAMD_STR2
   if (!lib_) {
     const char* e = dlerror();
-    err_ = e ? e : "libamd_smi not found";
+    err_ = e ? e : (soname + " not found");
     return false;
+  }
+  if (auto ver = reinterpret_cast<amdsmi_status_t (*)(amdsmi_version_t*)>(dlsym(lib_, "amdsmi_get_lib_version"))) {
+    amdsmi_version_t v{};
+    if (ver(&v) == AMDSMI_STATUS_SUCCESS && v.major != AMDSMI_LIB_VERSION_MAJOR) {
+      err_ = "libamd_smi major version " + std::to_string(v.major) + " != headers' " +
+             std::to_string(AMDSMI_LIB_VERSION_MAJOR);
+      return false;
+    }
   }
   const char* names[] = {"amdsmi_init", "amdsmi_get_socket_handles", "amdsmi_get_processor_handles",
                          "amdsmi_get_gpu_device_bdf", "amdsmi_get_gpu_metrics_info", "amdsmi_shut_down"};

@@ -177,3 +177,30 @@ def test_dist_init_refuses_shared_default_port(monkeypatch):
     monkeypatch.setattr(kd, "_ENV", None)
     with pytest.raises(RuntimeError, match="MASTER_PORT"):
         kd.init(backend="gloo")
+
+
+def _dp_unused_worker(rank):
+    from kubeflow_rm_amd import parallel
+    parallel.init(backend="gloo")
+    torch.manual_seed(7)
+    net = _Branchy()
+    dp = parallel.DataParallel(net, bucket_mb=400 / 2**20)
+    opt = torch.optim.AdamW(net.parameters(), lr=0.1, weight_decay=0.5)
+    before = net.experts[3].weight.detach().clone()
+    # expert 3 is used by no rank; expert 1 only by rank 1
+    use = [0, 1] if rank == 1 else [0]
+    net.zero_grad(set_to_none=True)
+    dp(torch.randn(3, 8), use).sum().backward()
+    out = {"e3_none": all(p.grad is None for p in net.experts[3].parameters()),
+           "e1_has": all(p.grad is not None for p in net.experts[1].parameters())}
+    opt.step()
+    out["e3_untouched"] = bool(torch.equal(net.experts[3].weight, before))
+    parallel.shutdown()
+    return out
+
+
+def test_data_parallel_globally_unused_params_keep_grad_none():
+    """a parameter no rank used keeps grad None (torch DDP semantics), so AdamW applies
+    no weight decay / momentum to it; one used by another rank gets the reduced gradient."""
+    for r in spawn(_dp_unused_worker, 2, timeout=120):
+        assert r == {"e3_none": True, "e1_has": True, "e3_untouched": True}, r

@@ -137,3 +137,47 @@ def test_kfam_over_rest(split):
                 raise
             time.sleep(0.1)
     assert [b["user"]["name"] for b in body["bindings"]] == ["r@example.com"]
+
+
+def test_quota_webhook_concurrent_generate_name_creates(split):
+    """kube-apiserver sends generateName creates (ReplicaSet / Job pods) to the quota
+    webhook with an EMPTY name. Eight such AdmissionReviews at once against a 2-GPU quota must admit
+    exactly two: reservations are keyed by the request uid, not the (empty) pod name."""
+    import base64
+    import concurrent.futures as cf
+    import ssl
+    import uuid
+    cl, _ = split
+    c = cl.client
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "gen-quota"}})
+    c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q", "namespace": "gen-quota"},
+              "spec": {"hard": {"amd.com/gpu": "2"}}})
+    vwc = c.list("admissionregistration.k8s.io/v1", "ValidatingWebhookConfiguration")["items"]
+    hooks = [w for v in vwc for w in v["webhooks"] if w["clientConfig"].get("url", "").endswith("/quota")]
+    assert hooks, "admission-webhook registered no /quota hook"
+    url = hooks[0]["clientConfig"]["url"]
+    ctx = ssl.create_default_context()
+    ca = hooks[0]["clientConfig"].get("caBundle")
+    if ca:
+        ctx.load_verify_locations(cadata=base64.b64decode(ca).decode())
+        ctx.check_hostname = False
+    else:
+        ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE
+
+    def review(i):
+        body = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                "request": {"uid": str(uuid.uuid4()), "operation": "CREATE", "namespace": "gen-quota", "name": "",
+                            "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                            "resource": {"group": "", "version": "v1", "resource": "pods"},
+                            "userInfo": {"username": "system:serviceaccount:kube-system:replicaset-controller"},
+                            "object": {"apiVersion": "v1", "kind": "Pod",
+                                       "metadata": {"generateName": "job-", "namespace": "gen-quota"},
+                                       "spec": {"containers": [{"name": "x", "image": "x",
+                                                                "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}}
+        req = urllib.request.Request(url, data=json.dumps(body).encode(), headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=10, context=ctx if url.startswith("https") else None) as r:
+            return json.loads(r.read())["response"]["allowed"]
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        allowed = list(ex.map(review, range(8)))
+    assert sum(allowed) == 2, allowed
