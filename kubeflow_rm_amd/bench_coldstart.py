@@ -90,12 +90,37 @@ def _wait_ready(c, name: str, namespace: str, timeout: float) -> dict:
         time.sleep(0.005)
 
 
+def _reconcile_latency(url: str) -> dict:
+    """p50 / p99 of controller_runtime_reconcile_time_seconds and workqueue_queue_duration_seconds
+    per controller, scraped from the control plane's /metrics (PromQL histogram_quantile)."""
+    import urllib.request
+    from .loadtest import histogram_quantile, parse_histograms
+    with urllib.request.urlopen(url + "/metrics", timeout=10) as r:
+        text = r.read().decode()
+    out = {}
+    for fam, key in (("controller_runtime_reconcile_time_seconds", "reconcile"),
+                     ("workqueue_queue_duration_seconds", "queue")):
+        for labels, h in parse_histograms(text, fam).items():
+            name = dict(labels).get("controller") or dict(labels).get("name") or "?"
+            if not h["count"]:
+                continue
+            out.setdefault(name, {})[key] = {"count": int(h["count"]),
+                                             "p50_ms": round(1e3 * histogram_quantile(0.5, h["buckets"]), 3),
+                                             "p99_ms": round(1e3 * histogram_quantile(0.99, h["buckets"]), 3)}
+    return out
+
+
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
                        readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
-                       settle_s: float = 0.5, server: str = "stub") -> dict:
-    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...}}.
+                       settle_s: float = 0.5, server: str = "stub", odh_oauth: bool = False) -> dict:
+    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...},
+    "reconcile": {controller: {"reconcile": {p50_ms, p99_ms}, "queue": {...}}}}.
 
     ``server``: "stub" or "torch-ready" (see SERVERS). Both are process pods (no container runtime).
+    ``odh_oauth``: the ODH spawn path of SURVEY CS1 with OAuth: the ODH webhook injects the
+    oauth-proxy sidecar and the reconciliation lock; the odh-notebook-controller creates the OAuth
+    ServiceAccount / Service / Secret / Route and removes the lock once the SA has its image pull
+    secret (Q7), and only then does the notebook controller scale the StatefulSet to 1.
 
     ``settle_s``: pause after the previous run's pod is gone, so runs are independent cold starts.
     The amdgpu KFD tears a GPU process down asynchronously after it exits and the next open of
@@ -109,6 +134,8 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
         for i in range(runs):
             name = f"cs-{i}"
             ann = {} if readiness else {"kfamd.io/gpu-readiness-op": "false"}
+            if odh_oauth:
+                ann["notebooks.opendatahub.io/inject-oauth"] = "true"
             ctr = {"name": name, "image": image, "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}}}
             srv = SERVERS[server]
             if srv.get("env"):
@@ -137,11 +164,17 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
             if t_sched:
                 phases["create_to_scheduled_s"] = t_sched - t0
             stages = {}
-            for st in (pod.get("status") or {}).get("initContainerStatuses") or []:
-                msg = ((st.get("state") or {}).get("terminated") or {}).get("message") or ""
+            # the op's report: the sidecar's (published by the kubelet as a pod annotation) or the
+            # init container's termination message (gpu-readiness-mode: init)
+            msgs = [((pod.get("metadata") or {}).get("annotations") or {}).get("notebooks.kubeflow.org/gpu-readiness") or ""]
+            msgs += [((st.get("state") or {}).get("terminated") or {}).get("message") or ""
+                     for st in (pod.get("status") or {}).get("initContainerStatuses") or []]
+            for msg in msgs:
                 try:
                     rep = json.loads(msg)
                 except ValueError:
+                    continue
+                if not isinstance(rep, dict):
                     continue
                 stages = {"hip_init_ms": rep.get("hip_init_ms"), "total_ms": rep.get("total_ms"),
                           **{f"{k}_ms": v for k, v in (rep.get("stages_ms") or {}).items()},
@@ -167,9 +200,14 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                     break
                 time.sleep(0.02)
             time.sleep(settle_s)
+        try:
+            recon = _reconcile_latency(cl.url)
+        except Exception as e:  # noqa: BLE001 - reported, never fatal
+            recon = {"error": f"{type(e).__name__}: {e}"}
     xs = [r["cold_start_s"] for r in out_runs]
     phase_keys = sorted({k for r in out_runs for k in r["phases"]})
     res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs, "server": server,
+           "odh_oauth": odh_oauth, "reconcile": recon,
            "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
     stage_keys = sorted({k for r in out_runs for k, v in r["readiness_stages"].items() if v is not None})
     if stage_keys:
@@ -235,11 +273,12 @@ def main() -> int:
     p.add_argument("--gpus", type=int, default=None, help="node GPUs (default: discover; -> synthetic 8 without /dev/kfd)")
     p.add_argument("--no-readiness", action="store_true")
     p.add_argument("--settle", type=float, default=0.5, help="seconds between runs (0: back to back)")
+    p.add_argument("--odh-oauth", action="store_true", help="ODH spawn path with the OAuth proxy (CS1)")
     p.add_argument("--server", choices=sorted(SERVERS), default="stub",
                    help="notebook server recipe: stub (no torch) or torch-ready (torch import + GEMM before Ready)")
     a = p.parse_args()
     r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness,
-                           settle_s=a.settle, server=a.server)
+                           settle_s=a.settle, server=a.server, odh_oauth=a.odh_oauth)
     print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
     print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
     return 0

@@ -49,6 +49,13 @@ struct GpuReadinessOptions {
   std::string image = "kfamd/readiness:gfx950";
   std::vector<std::string> args = {"--m", "4096", "--n", "4096", "--k", "4096", "--iters", "10"};
   bool only_notebooks = true;  // pods carrying the notebook-name label
+  // "sidecar" (default): a native sidecar (init container, restartPolicy: Always) that shares the
+  // pod's GPUs (KFAMD_SHARE_POD_GPUS; on upstream Kubernetes the equivalent is one DRA ResourceClaim
+  // referenced by both containers) and gates Ready through /readyz — the op overlaps the notebook
+  // server's start. "init": the r1/r2 blocking init container (device-plugin-only clusters).
+  // Per pod: annotation kfamd.io/gpu-readiness-mode. Process-wide: env KFAMD_GPU_READINESS_MODE.
+  std::string mode = "sidecar";
+  int port = 8689;  // the sidecar's /readyz port
 };
 AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o = {});
 

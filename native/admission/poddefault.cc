@@ -221,16 +221,38 @@ AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o) {
     // kfamd.io/gpu-readiness-args: extra op flags, e.g. "--min-tflops 1200" (fail a notebook whose
     // GPU underperforms) or "--inject-fault gemm" (fault-injection drills)
     for (const auto& s : split(annotation(pod, "kfamd.io/gpu-readiness-args"), ' ', true)) args.push_back(s);
+    std::string mode = annotation(pod, "kfamd.io/gpu-readiness-mode");
+    if (mode.empty()) mode = o.mode;
+    if (const char* m = std::getenv("KFAMD_GPU_READINESS_MODE"); m && *m && annotation(pod, "kfamd.io/gpu-readiness-mode").empty())
+      mode = m;
+    const bool sidecar = mode != "init";
+    Json env = Json::array();
     Json ic{{"name", "gpu-readiness"},
             {"image", o.image},
             {"command", Json::array({"kfamd-readiness"})},
-            {"args", args},
-            {"resources", Json{{"limits", Json{{GPU_RESOURCE, std::to_string(gpus)}}}}},
             {"terminationMessagePolicy", "FallbackToLogsOnError"}};
+    if (sidecar) {
+      // native sidecar: started before the notebook container, not waited for; the pod is Ready
+      // when the server AND /readyz (the op's verdict, published before its GPU teardown) are
+      Json sargs = Json::array({"--sidecar", "--port", std::to_string(o.port)});
+      for (const auto& x : args.as_array()) sargs.push_back(x);
+      ic["args"] = sargs;
+      ic["restartPolicy"] = "Always";
+      ic["ports"] = Json::array({Json{{"name", "kfamd-ready"}, {"containerPort", o.port}}});
+      ic["readinessProbe"] = Json{{"httpGet", Json{{"path", "/readyz"}, {"port", o.port}}},
+                                  {"periodSeconds", 10}, {"failureThreshold", 1}};
+      // the notebook container holds the GPUs; the sidecar checks THOSE devices (no second
+      // allocation: requests of restartable init containers would add to the pod's)
+      env.push_back(Json{{"name", "KFAMD_SHARE_POD_GPUS"}, {"value", "true"}});
+    } else {
+      ic["args"] = args;
+      ic["resources"] = Json{{"limits", Json{{GPU_RESOURCE, std::to_string(gpus)}}}};
+    }
     // kfamd.io/gpu-readiness-profile: "true" -> the op runs itself under rocprofv3 and reports the
     // per-kernel stats with its result (Notebook status.gpuReadiness.rocprof_top)
     if (annotation(pod, "kfamd.io/gpu-readiness-profile") == "true")
-      ic["env"] = Json::array({Json{{"name", "KFAMD_READINESS_PROFILE"}, {"value", "1"}}});
+      env.push_back(Json{{"name", "KFAMD_READINESS_PROFILE"}, {"value", "1"}});
+    if (env.size()) ic["env"] = env;
     Json& ics = pod["spec"]["initContainers"];
     Json out = Json::array({ic});
     for (const auto& x : ics.as_array()) out.push_back(x);

@@ -34,6 +34,14 @@ std::string ms_now() { return rfc3339_ms_now(); }
 
 int64_t probe_i(const Json& probe, const char* key, int64_t def) { return probe[key].as_int(def); }
 
+// env KFAMD_SHARE_POD_GPUS=true: the container sees the pod's allocated GPUs without requesting its
+// own (what one DRA ResourceClaim shared by two containers gives on upstream Kubernetes)
+bool shares_pod_gpus(const Json& c) {
+  for (const auto& e : c["env"].as_array())
+    if (e["name"].as_string() == "KFAMD_SHARE_POD_GPUS") return e["value"].as_string() == "true";
+  return false;
+}
+
 bool tcp_connect(const std::string& ip, int port, int timeout_ms) {
   int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (fd < 0) return false;
@@ -120,6 +128,7 @@ const char* kDefaultRecipes = R"([
 struct ContainerRt {
   std::string name;
   bool init = false;
+  bool sidecar = false;  // native sidecar: an init container with restartPolicy: Always (K8s 1.29)
   pid_t pid = -1;
   std::string state = "waiting";  // waiting | running | terminated
   std::string reason = "ContainerCreating";
@@ -143,6 +152,7 @@ struct Kubelet::PodRuntime {
   std::vector<ContainerRt> init, main;
   size_t init_done = 0;
   bool init_failed = false;
+  bool readiness_published = false;  // gpu-readiness sidecar report copied to the pod annotation
   std::string start_time;
   bool terminating = false;
   double kill_deadline = 0;
@@ -694,6 +704,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         ContainerRt cr;
         cr.name = c["name"].as_string();
         cr.init = init;
+        cr.sidecar = init && c["restartPolicy"].as_string() == "Always";
         cr.log_path = rt->dir + "/" + cr.name + ".log";
         cr.term_path = rt->dir + "/" + cr.name + ".termination-log";
         for (const auto& vm : c["volumeMounts"].as_array()) {
@@ -793,8 +804,10 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       set("KUBERNETES_SERVICE_PORT", std::to_string(u.port));
       set("KFAMD_API_URL", cfg_.api_url);
     }
-    // GPU wiring from the device plugin allocation
-    const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0;
+    // GPU wiring from the device plugin allocation (and for a container that shares the pod's
+    // GPUs without a second allocation: the gpu-readiness sidecar)
+    const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 ||
+                           shares_pod_gpus(c);
     if (wants_gpu && !rt->gpus.devices.empty()) {
       const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1, rt->ip, rt->rdzv_port);
       for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
@@ -879,7 +892,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     // runs on the CPUs local to its GPUs (host<->HBM copies, RCCL proxy threads, data loaders)
     std::vector<int> cpus;
     if (cfg_.numa_pinning && !rt->gpus.devices.empty() &&
-        resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0)
+        (resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 || shares_pod_gpus(c)))
       cpus = alloc_->topology().local_cpus(rt->gpus.devices);
     pid_t pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
     if (pid < 0) {
@@ -965,7 +978,103 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   // Until a pod is Ready the kubelet re-syncs it every 10 ms (cold start is on the notebook's
   // critical path; a sync of an unchanged pod costs no API call), afterwards at the 1 s relist.
   constexpr double kStartupPoll = 0.01;
-  // init containers, sequentially
+  // Probes of one running container (startup gates readiness/liveness); keeps next_wake.
+  auto tick_probes = [&](ContainerRt& cr, const Json& c) {
+    const double now = now_seconds();
+    const Json& sp = c["startupProbe"];
+    if (!cr.started_probe_ok && now >= cr.next_startup_probe) {
+      if (run_probe(sp, c)) {
+        if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
+      } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
+        rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
+        ::kill(-cr.pid, SIGKILL);
+      }
+      cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
+    }
+    if (!cr.started_probe_ok) {
+      next_wake = std::min(next_wake, 0.1);
+      return;
+    }
+    const Json& rp = c["readinessProbe"];
+    if (!rp.is_object()) {
+      cr.ready = true;
+    } else if (now >= cr.next_ready_probe) {
+      bool ok = run_probe(rp, c);
+      if (ok) {
+        cr.ready_fail = 0;
+        if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
+      } else {
+        cr.ready_ok = 0;
+        if (++cr.ready_fail >= probe_i(rp, "failureThreshold", 3)) {
+          if (cr.ready) rec_->event(pod, "Warning", "Unhealthy", "Readiness probe failed");
+          cr.ready = false;
+        }
+      }
+      // probe fast until the first success (cold-start latency), then at periodSeconds
+      cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.02);
+    }
+    const Json& lp = c["livenessProbe"];
+    if (lp.is_object() && now >= cr.next_live_probe) {
+      if (run_probe(lp, c)) {
+        cr.live_fail = 0;
+      } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
+        rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
+        ::kill(-cr.pid, SIGKILL);
+      }
+      cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
+    }
+    if (!cr.ready) {
+      next_wake = std::min(next_wake, kStartupPoll);
+    } else {
+      // wake for the next due probe; a container without probes only needs the 1 s
+      // exit-detection relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
+      double due = 1e30;
+      if (rp.is_object()) due = std::min(due, cr.next_ready_probe);
+      if (lp.is_object()) due = std::min(due, cr.next_live_probe);
+      if (due < 1e30) next_wake = std::min(next_wake, std::max(0.2, due - now));
+    }
+  };
+  // a long-running container (main, or sidecar): exit -> restart per policy with back-off, probes
+  auto tick_long_running = [&](ContainerRt& cr, bool always_restart) {
+    const Json& c = container_spec(cr);
+    if (cr.state == "running") {
+      if (!handle_exit(cr)) {
+        tick_probes(cr, c);
+        return;
+      }
+    }
+    if (cr.state == "terminated") {
+      const bool restart = always_restart || restart_policy == "Always" ||
+                           (restart_policy == "OnFailure" && cr.exit_code != 0);
+      if (!restart) return;
+      cr.last_state = Json{{"terminated", Json{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at},
+                                               {"finishedAt", cr.finished_at}, {"message", cr.message}}}};
+      cr.restarts++;
+      cr.state = "waiting";
+      cr.reason = "CrashLoopBackOff";
+      double ran = now_seconds() - cr.run_started;
+      double backoff = ran > 600 ? cfg_.restart_backoff : std::min(300.0, cfg_.restart_backoff * (1 << std::min(cr.restarts - 1, 5)));
+      cr.backoff_until = now_seconds() + backoff;
+      rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + cr.name);
+    }
+    if (cr.state == "waiting") {
+      if (now_seconds() >= cr.backoff_until) {
+        start_container(cr);
+        // no startup / readiness probe: Ready as soon as it runs (Kubernetes' default Success),
+        // in this pass rather than the next re-sync
+        if (cr.state == "running" && !c["startupProbe"].is_object() && !c["readinessProbe"].is_object()) {
+          cr.started_probe_ok = true;
+          cr.ready = true;
+        }
+        next_wake = std::min(next_wake, kStartupPoll);
+      } else {
+        next_wake = std::min(next_wake, cr.backoff_until - now_seconds());
+      }
+    }
+  };
+  // init containers, sequentially. A native sidecar (restartPolicy: Always) counts as done once it
+  // is STARTED (running, startup probe passed): the next init container / the main containers
+  // start while it keeps running, and it is restarted whenever it exits (KEP-753 semantics).
   while (rt->init_done < rt->init.size() && !rt->init_failed) {
     ContainerRt& ic = rt->init[rt->init_done];
     if (ic.state == "waiting") {
@@ -975,19 +1084,31 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       }
       start_container(ic);
       next_wake = kStartupPoll;
+      if (ic.sidecar && ic.state == "running" && !container_spec(ic)["startupProbe"].is_object()) {
+        ic.started_probe_ok = true;
+        rt->init_done++;
+        continue;
+      }
       break;
     }
     if (ic.state == "running") {
       if (handle_exit(ic)) continue;
+      if (ic.sidecar) {
+        tick_probes(ic, container_spec(ic));
+        if (ic.started_probe_ok) {
+          rt->init_done++;
+          continue;
+        }
+      }
       next_wake = kStartupPoll;  // init containers gate the pod: notice their exit within ~10 ms
       break;
     }
     // terminated
-    if (ic.exit_code == 0) {
+    if (ic.exit_code == 0 && !ic.sidecar) {
       rt->init_done++;
       continue;
     }
-    if (restart_policy == "Never") {
+    if (restart_policy == "Never" && !ic.sidecar) {
       rt->init_failed = true;
       break;
     }
@@ -1001,98 +1122,24 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     break;
   }
   const bool initialized = rt->init_done == rt->init.size();
-  if (initialized) {
-    for (auto& cr : rt->main) {
-      const Json& c = container_spec(cr);
-      if (cr.state == "running") {
-        if (handle_exit(cr)) {
-          // fallthrough to restart handling below
-        } else {
-          const double now = now_seconds();
-          // startup probe gates readiness/liveness
-          const Json& sp = c["startupProbe"];
-          if (!cr.started_probe_ok && now >= cr.next_startup_probe) {
-            if (run_probe(sp, c)) {
-              if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
-            } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
-              rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
-              ::kill(-cr.pid, SIGKILL);
-            }
-            cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
-          }
-          if (cr.started_probe_ok) {
-            const Json& rp = c["readinessProbe"];
-            if (!rp.is_object()) {
-              cr.ready = true;
-            } else if (now >= cr.next_ready_probe) {
-              bool ok = run_probe(rp, c);
-              if (ok) {
-                cr.ready_fail = 0;
-                if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
-              } else {
-                cr.ready_ok = 0;
-                if (++cr.ready_fail >= probe_i(rp, "failureThreshold", 3)) {
-                  if (cr.ready) rec_->event(pod, "Warning", "Unhealthy", "Readiness probe failed");
-                  cr.ready = false;
-                }
-              }
-              // probe fast until the first success (cold-start latency), then at periodSeconds
-              cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.02);
-            }
-            const Json& lp = c["livenessProbe"];
-            if (lp.is_object() && now >= cr.next_live_probe) {
-              if (run_probe(lp, c)) {
-                cr.live_fail = 0;
-              } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
-                rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
-                ::kill(-cr.pid, SIGKILL);
-              }
-              cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
-            }
-            if (!cr.ready) {
-              next_wake = std::min(next_wake, kStartupPoll);
-            } else {
-              // wake for the next due probe; a container without probes only needs the 1 s
-              // exit-detection relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
-              double due = 1e30;
-              if (rp.is_object()) due = std::min(due, cr.next_ready_probe);
-              if (lp.is_object()) due = std::min(due, cr.next_live_probe);
-              if (due < 1e30) next_wake = std::min(next_wake, std::max(0.2, due - now));
-            }
-          } else {
-            next_wake = std::min(next_wake, 0.1);
-          }
-          continue;
-        }
-      }
-      if (cr.state == "terminated") {
-        const bool restart = restart_policy == "Always" || (restart_policy == "OnFailure" && cr.exit_code != 0);
-        if (!restart) continue;
-        cr.last_state = Json{{"terminated", Json{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at},
-                                                 {"finishedAt", cr.finished_at}, {"message", cr.message}}}};
-        cr.restarts++;
-        cr.state = "waiting";
-        cr.reason = "CrashLoopBackOff";
-        double ran = now_seconds() - cr.run_started;
-        double backoff = ran > 600 ? cfg_.restart_backoff : std::min(300.0, cfg_.restart_backoff * (1 << std::min(cr.restarts - 1, 5)));
-        cr.backoff_until = now_seconds() + backoff;
-        rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + cr.name);
-      }
-      if (cr.state == "waiting") {
-        if (now_seconds() >= cr.backoff_until) {
-          start_container(cr);
-          // no startup / readiness probe: Ready as soon as it runs (Kubernetes' default Success),
-          // in this pass rather than the next re-sync
-          if (cr.state == "running" && !c["startupProbe"].is_object() && !c["readinessProbe"].is_object()) {
-            cr.started_probe_ok = true;
-            cr.ready = true;
-          }
-          next_wake = std::min(next_wake, kStartupPoll);
-        } else {
-          next_wake = std::min(next_wake, cr.backoff_until - now_seconds());
-        }
-      }
-    }
+  // started sidecars run alongside everything after them
+  for (size_t i = 0; i < rt->init_done && i < rt->init.size(); ++i)
+    if (rt->init[i].sidecar) tick_long_running(rt->init[i], true);
+  if (initialized)
+    for (auto& cr : rt->main) tick_long_running(cr, false);
+  // the gpu-readiness sidecar's report (its termination-log file, written before it turns Ready)
+  // goes onto the pod as notebooks.kubeflow.org/gpu-readiness, where the notebook controller
+  // surfaces it as status.gpuReadiness; written before the status update that makes the pod Ready
+  for (const auto& cr : rt->init) {
+    if (!cr.sidecar || cr.name != "gpu-readiness" || !cr.ready || rt->readiness_published) continue;
+    std::string rep;
+    if (!read_file(cr.term_path, rep) || rep.empty()) continue;
+    rt->readiness_published = true;
+    c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
+      if (o.str_at({"metadata", "uid"}) != uid) return false;
+      o["metadata"]["annotations"][ANNOTATION_GPU_READINESS] = rep.substr(0, 4096);
+      return true;
+    });
   }
 
   // ---- status --------------------------------------------------------------------------------------
@@ -1122,6 +1169,8 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   for (const auto& cr : rt->main) main_st.push_back(cstatus(cr));
   bool all_ready = initialized && !rt->main.empty(), all_running = initialized, any_running = false, all_done = initialized,
        any_failed = rt->init_failed;
+  for (const auto& cr : rt->init)
+    if (cr.sidecar) all_ready = all_ready && cr.ready;  // sidecar readiness gates the pod's
   for (const auto& cr : rt->main) {
     all_ready = all_ready && cr.ready;
     all_running = all_running && cr.state == "running";

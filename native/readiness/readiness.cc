@@ -33,7 +33,11 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <arpa/inet.h>
 #include <dirent.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <execinfo.h>
 #include <signal.h>
 #include <spawn.h>
@@ -44,6 +48,7 @@
 #include <atomic>
 #include <algorithm>
 #include <chrono>
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -969,8 +974,116 @@ double realtime_ms() {
   return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
 }
 
+// ---- sidecar mode (--sidecar) ---------------------------------------------------------------------
+// The op as a native sidecar (an init container with restartPolicy: Always, injected by the GPU
+// readiness admission plugin): the notebook server starts while the GPU checks run, and the pod
+// turns Ready only when both are done — the cold start is max(op, server) instead of op + server.
+// This process never touches the GPU: it forks a child (before any HIP call) that runs the op and,
+// as soon as its report is written (termination log), signals the verdict through a pipe — BEFORE
+// the child's HIP / KFD teardown, which then overlaps everything else. The parent serves the verdict
+// on http://$POD_IP:<port>/readyz (the sidecar's readinessProbe: 503 until the report, then 200):
+// on success it stays up (the sidecar contract; it holds no GPU state), on failure it exits 1 so the
+// kubelet records the report as the container's termination message (-> Notebook
+// status.gpuReadiness) and restarts it with back-off.
+int g_report_fd = -1;
+
+void signal_sidecar(bool ok) {
+  if (g_report_fd < 0) return;
+  const char c = ok ? '1' : '0';
+  (void)!::write(g_report_fd, &c, 1);
+  ::close(g_report_fd);
+  g_report_fd = -1;
+}
+
+int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
+  int port = 8689;
+  std::vector<char*> child_argv;
+  for (int i = 0; i < argc; ++i) {
+    const std::string s = argv[i];
+    if (s == "--sidecar") continue;
+    if (s == "--port" && i + 1 < argc) {
+      port = std::atoi(argv[++i]);
+      continue;
+    }
+    child_argv.push_back(argv[i]);
+  }
+  child_argv.push_back(nullptr);
+  int fds[2];
+  if (::pipe(fds) != 0) return 2;
+  const pid_t pid = ::fork();
+  if (pid < 0) return 2;
+  if (pid == 0) {  // the op: HIP lives only in this process
+    ::close(fds[0]);
+    g_report_fd = fds[1];
+    const int rc = op((int)child_argv.size() - 1, child_argv.data());
+    signal_sidecar(rc == 0);
+    std::fflush(nullptr);
+    _exit(rc);
+  }
+  ::close(fds[1]);
+  const char* ip = std::getenv("POD_IP");
+  const int ls = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  int one = 1;
+  ::setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons(static_cast<uint16_t>(port));
+  if (::inet_pton(AF_INET, ip && *ip ? ip : "127.0.0.1", &sa.sin_addr) != 1) sa.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (ls < 0 || ::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0 || ::listen(ls, 16) != 0)
+    std::fprintf(stderr, "kfamd-readiness --sidecar: cannot listen on port %d: %s\n", port, std::strerror(errno));
+  int verdict = -1;  // -1 pending, 1 ok, 0 failed
+  bool child_reaped = false;
+  int child_rc = 1;
+  for (;;) {
+    pollfd pf[2] = {{ls, POLLIN, 0}, {verdict < 0 ? fds[0] : -1, POLLIN, 0}};
+    const int n = ::poll(pf, 2, verdict < 0 ? -1 : 1000);
+    if (n < 0 && errno != EINTR) break;
+    if (pf[1].revents & (POLLIN | POLLHUP)) {
+      char c = 0;
+      verdict = ::read(fds[0], &c, 1) == 1 && c == '1' ? 1 : 0;
+      ::close(fds[0]);
+    }
+    if (!child_reaped) {
+      int st = 0;
+      if (::waitpid(pid, &st, verdict == 0 ? 0 : WNOHANG) == pid) {
+        child_reaped = true;
+        child_rc = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
+        if (verdict < 0) verdict = 0;  // died without a verdict (crash): failed
+      }
+    }
+    if (verdict == 0) {
+      // the child wrote the termination log (the report); the container exits with it
+      std::fflush(nullptr);
+      return child_rc != 0 ? child_rc : 1;
+    }
+    if (ls >= 0 && (pf[0].revents & POLLIN)) {
+      const int cs = ::accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+      if (cs >= 0) {
+        char buf[1024];
+        (void)!::recv(cs, buf, sizeof buf, MSG_DONTWAIT);
+        const char* resp = verdict == 1 ? "HTTP/1.1 200 OK\r\nContent-Length: 3\r\nConnection: close\r\n\r\nok\n"
+                                        : "HTTP/1.1 503 Service Unavailable\r\nContent-Length: 8\r\nConnection: close\r\n\r\npending\n";
+        (void)!::send(cs, resp, std::strlen(resp), MSG_NOSIGNAL);
+        ::close(cs);
+      }
+    }
+  }
+  return 1;
+}
+
 int main(int argc, char** argv) {
   g_t_main_ms = realtime_ms();
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--sidecar")
+      return run_sidecar(argc, argv, [](int ac, char** av) -> int {
+        const char* prof = std::getenv("KFAMD_READINESS_PROFILE");
+        if (prof && std::string(prof) == "1" && !std::getenv("KFAMD_READINESS_CHILD")) {
+          const int rc = run_profiled(ac, av);
+          if (rc >= 0) return rc;
+        }
+        g_fast_exit = true;
+        return readiness_main(ac, av);
+      });
   // fast exit by default; not under a profiler (rocprofv3 writes its results from exit handlers)
   {
     const char* pre = std::getenv("LD_PRELOAD");
@@ -1187,6 +1300,7 @@ int readiness_main(int argc, char** argv) {
     }
   }
   const int rc = g_error.empty() ? 0 : 1;
+  signal_sidecar(rc == 0);  // sidecar mode: the verdict goes out before the HIP / KFD teardown
   if (g_fast_exit) {
     // the report is written and every stage synchronised: leave without the HIP runtime's static
     // teardown (report -> exit 75 -> 57 ms median on MI355X, profiles/r2_coldstart_exit); the
