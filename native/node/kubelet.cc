@@ -1138,6 +1138,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
       if (o.str_at({"metadata", "uid"}) != uid) return false;
       o["metadata"]["annotations"][ANNOTATION_GPU_READINESS] = rep.substr(0, 4096);
+      o["metadata"]["annotations"]["notebooks.kubeflow.org/gpu-readiness-at"] = ms_now();
       return true;
     });
   }

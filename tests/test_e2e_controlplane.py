@@ -110,6 +110,24 @@ def test_gpu_allocation_metrics(c, cluster):
     assert hbm and hbm[0] >= 4 * 288 * 2**30
 
 
+def test_gpu_readiness_sidecar_overlaps_server_start(c):
+    """The readiness op runs as a native sidecar: the notebook container is started while the op is
+    still running (Initialized does not wait for it), the sidecar stays running after its verdict,
+    its /readyz gates the pod's Ready, and its report reaches the Notebook status."""
+    c.create(_notebook("sc1", "e2e", gpus=1, annotations={"kfamd.io/gpu-readiness-args": "--iters 3"}))
+    nb = c.wait_for(NB, "Notebook", "sc1", "e2e", _ready, timeout=30)
+    assert nb["status"]["gpuReadiness"]["ok"] is True
+    pod = c.get("v1", "Pod", "sc1-0", "e2e")
+    side = pod["status"]["initContainerStatuses"][0]
+    assert side["name"] == "gpu-readiness" and "running" in side["state"] and side["ready"] is True
+    assert side["restartCount"] == 0
+    main = pod["status"]["containerStatuses"][0]
+    # the server was started before the op's verdict (no serial init wait)
+    assert main["state"]["running"]["startedAt"] <= pod["metadata"]["annotations"].get(
+        "notebooks.kubeflow.org/gpu-readiness-at", "9999")
+    c.delete(NB, "Notebook", "sc1", "e2e")
+
+
 def test_gpu_readiness_failure_surfaces_on_notebook(c):
     """a GPU-side fault in the readiness op -> pod not Ready -> the Notebook status
     carries the op's error (fault injected through kfamd.io/gpu-readiness-args)."""

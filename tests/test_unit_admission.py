@@ -115,10 +115,24 @@ def test_gpu_readiness_injected_for_gpu_notebooks(native):
     out = native.call("gpu_readiness_mutate", pod=pod)
     ic = out["spec"]["initContainers"][0]
     assert ic["name"] == "gpu-readiness" and ic["command"] == ["kfamd-readiness"]
-    assert ic["resources"]["limits"]["amd.com/gpu"] == "2"
-    assert "env" not in ic
+    # default: a native sidecar on the notebook's own GPUs (no second amd.com/gpu request: requests
+    # of restartable init containers add to the pod's), gating Ready through /readyz
+    assert ic["restartPolicy"] == "Always" and ic["args"][:3] == ["--sidecar", "--port", "8689"]
+    assert "resources" not in ic
+    assert {"name": "KFAMD_SHARE_POD_GPUS", "value": "true"} in ic["env"]
+    assert ic["readinessProbe"]["httpGet"] == {"path": "/readyz", "port": 8689}
     # idempotent
     assert native.call("gpu_readiness_mutate", pod=out)["spec"]["initContainers"] == out["spec"]["initContainers"]
+
+
+def test_gpu_readiness_init_mode_blocks_like_r2(native):
+    """kfamd.io/gpu-readiness-mode: init -> the blocking init container with its own GPU request
+    (device-plugin-only clusters, where a sidecar could not share the notebook's devices)."""
+    pod = {"metadata": {"labels": {"notebook-name": "nb"}, "annotations": {"kfamd.io/gpu-readiness-mode": "init"}},
+           "spec": {"containers": [{"name": "nb", "image": "x", "resources": {"limits": {"amd.com/gpu": "2"}}}]}}
+    ic = native.call("gpu_readiness_mutate", pod=pod)["spec"]["initContainers"][0]
+    assert ic["resources"]["limits"]["amd.com/gpu"] == "2"
+    assert "restartPolicy" not in ic and "env" not in ic and "--sidecar" not in ic["args"]
 
 
 def test_gpu_readiness_profile_annotation_enables_rocprof(native):
