@@ -6,6 +6,8 @@
     python -m kubeflow_rm_amd.kfctl crds [--out manifests/crds]         # regenerate CRD YAML from
                                                                         # the native registry
     python -m kubeflow_rm_amd.kfctl up [--data-dir DIR]                  # local kube-lite cluster
+    python -m kubeflow_rm_amd.kfctl apply -f notebook.yaml | -           # kubectl-style file apply
+    python -m kubeflow_rm_amd.kfctl get|describe|wait|rollout|logs ...   # kubectl subset (kubectl.py)
 
 Apply order follows kubectl's dependency order (Namespaces and CRDs first, webhooks last) so
 that every object's kind and namespace exist when it arrives; ``--dry-run`` sends every object
@@ -112,10 +114,14 @@ def main(argv: list[str] | None = None) -> int:
     b.add_argument("path")
     for name in ("apply", "delete"):
         s = sub.add_parser(name)
-        s.add_argument("path")
+        s.add_argument("path", nargs="*", help="kustomize dir (or, for delete, <resource> <name>)")
+        s.add_argument("-f", "--filename", default=None, help="YAML/JSON manifest file, '-' for stdin")
+        s.add_argument("-n", "--namespace", default=None)
         s.add_argument("--server", default=None)
         if name == "apply":
             s.add_argument("--dry-run", action="store_true")
+    from . import kubectl
+    kubectl.add_parsers(sub)
     c = sub.add_parser("crds")
     c.add_argument("--out", default=str(Path(__file__).resolve().parent.parent / "manifests" / "crds"))
     u = sub.add_parser("up")
@@ -124,13 +130,34 @@ def main(argv: list[str] | None = None) -> int:
     if args.cmd == "build":
         sys.stdout.write(kustomize.dump(kustomize.build(args.path)))
         return 0
+    if args.cmd in kubectl.VERBS:
+        return kubectl.run(args.cmd, args)
     if args.cmd in ("apply", "delete"):
         client = KubeClient(args.server)
-        objs = kustomize.build(args.path)
-        if args.cmd == "apply":
-            apply(client, objs, dry_run=args.dry_run)
-        else:
-            delete(client, objs)
+        try:
+            if args.filename:
+                objs = kubectl.load_docs(args.filename)
+                for o in objs:
+                    if args.namespace and "namespace" not in o.setdefault("metadata", {}):
+                        o["metadata"]["namespace"] = args.namespace
+            elif args.cmd == "delete" and len(args.path) == 2:  # delete <resource> <name>
+                res = kubectl.resolve(client, args.path[0])
+                client.delete(res.api_version, res.kind, args.path[1], (args.namespace or "default") if res.namespaced else None)
+                print(f'{res.kind.lower()}{"." + res.group if res.group else ""} "{args.path[1]}" deleted')
+                return 0
+            elif len(args.path) == 1:
+                objs = kustomize.build(args.path[0])
+            else:
+                print("error: must specify one of -f or a kustomize directory", file=sys.stderr)
+                return 1
+            if args.cmd == "apply":
+                apply(client, objs, dry_run=args.dry_run)
+            else:
+                delete(client, objs)
+        except (ApiException, kubectl.KubectlError) as e:
+            print(e if isinstance(e, kubectl.KubectlError) else f"Error from server ({e.reason or e.status}): {e.message}",
+                  file=sys.stderr)
+            return 1
         return 0
     if args.cmd == "crds":
         for p in write_crds(Path(args.out)):

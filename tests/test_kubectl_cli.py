@@ -1,0 +1,148 @@
+"""kfctl's kubectl subset (get / describe / wait / rollout status / logs / apply -f / delete) against
+kube-lite, driven as the reference's own acceptance flow drives kubectl:
+
+* ``.github/workflows/odh_notebook_controller_integration_test.yaml:233-289``: apply a Notebook,
+  wait for its StatefulSet, ``rollout status``, ``wait --for=jsonpath='{.spec.replicas}'=1``,
+  ``wait pods <nb>-0 --for=condition=Ready``, then the ``describe`` / ``logs`` dump;
+* ``notebook_controller_integration_test.yaml:106``: ``wait pods -l app=... --for=condition=Ready``.
+Every command runs as a subprocess of ``python -m kubeflow_rm_amd.kfctl`` (the user-facing CLI).
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from kubeflow_rm_amd.cluster import LocalCluster
+
+NB_YAML = """
+apiVersion: kubeflow.org/v1
+kind: Notebook
+metadata:
+  name: minimal-notebook
+  annotations:
+    notebooks.opendatahub.io/inject-oauth: "false"
+spec:
+  template:
+    spec:
+      containers:
+        - name: minimal-notebook
+          image: quay.io/thoth-station/s2i-minimal-notebook:v0.3.0
+          imagePullPolicy: Always
+          workingDir: /opt/app-root/src
+          env:
+            - name: JUPYTER_NOTEBOOK_PORT
+              value: "8888"
+          ports:
+            - name: notebook-port
+              containerPort: 8888
+              protocol: TCP
+          resources:
+            requests:
+              cpu: "1"
+              memory: 1m
+            limits:
+              cpu: "1"
+              memory: 1Gi
+          livenessProbe:
+            initialDelaySeconds: 10
+            periodSeconds: 5
+            timeoutSeconds: 1
+            successThreshold: 1
+            failureThreshold: 3
+            httpGet:
+              scheme: HTTP
+              path: /notebook/ci-ns/minimal-notebook/api
+              port: notebook-port
+"""
+
+
+@pytest.fixture(scope="module")
+def cl():
+    from tests.conftest import _ensure_native
+    _ensure_native()
+    with LocalCluster() as c:
+        c.client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "ci-ns"}})
+        yield c
+
+
+def kfctl(cl, *args, stdin=None, timeout=120):
+    env = dict(os.environ, KFAMD_API_URL=cl.url)
+    p = subprocess.run([sys.executable, "-m", "kubeflow_rm_amd.kfctl", *args, "--server", cl.url],
+                       input=stdin, capture_output=True, text=True, timeout=timeout, env=env)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_reference_ci_sequence(cl):
+    rc, out, err = kfctl(cl, "apply", "-f", "-", "-n", "ci-ns", stdin=NB_YAML)
+    assert rc == 0, err
+    # timeout 100 bash -c -- 'until kubectl get statefulset minimal-notebook; do sleep 1; done'
+    deadline = time.time() + 100
+    while True:
+        rc, out, err = kfctl(cl, "get", "statefulset", "minimal-notebook", "-n", "ci-ns")
+        if rc == 0:
+            break
+        assert "NotFound" in err, err
+        assert time.time() < deadline
+        time.sleep(0.2)
+    assert out.splitlines()[0].split() == ["NAME", "READY", "AGE"]
+    rc, out, err = kfctl(cl, "rollout", "status", "--watch", "statefulset", "minimal-notebook", "-n", "ci-ns")
+    assert rc == 0, err
+    rc, out, err = kfctl(cl, "wait", "statefulset", "minimal-notebook", "--for=jsonpath={.spec.replicas}=1",
+                         "--timeout=100s", "-n", "ci-ns")
+    assert rc == 0 and "statefulset.apps/minimal-notebook condition met" in out, (out, err)
+    rc, out, err = kfctl(cl, "rollout", "status", "--watch", "statefulset", "minimal-notebook", "--timeout=300s",
+                         "-n", "ci-ns")
+    assert rc == 0 and "roll out complete" in out, (out, err)
+    rc, out, err = kfctl(cl, "wait", "pods", "minimal-notebook-0", "--for=condition=Ready", "--timeout=100s",
+                         "-n", "ci-ns")
+    assert rc == 0 and "pod/minimal-notebook-0 condition met" in out, (out, err)
+    # Print notebook logs (the workflow's failure dump)
+    rc, out, err = kfctl(cl, "describe", "notebooks", "-n", "ci-ns")
+    assert rc == 0 and "Name:         minimal-notebook" in out and "Kind:         Notebook" in out, err
+    rc, out, err = kfctl(cl, "describe", "statefulsets", "-n", "ci-ns")
+    assert rc == 0 and "Controlled By:  Notebook/minimal-notebook" in out, out
+    rc, out, err = kfctl(cl, "describe", "pods", "-n", "ci-ns")
+    assert rc == 0 and "Conditions:" in out and "Ready" in out and "Events:" in out, out
+    rc, out, err = kfctl(cl, "logs", "minimal-notebook-0", "-n", "ci-ns")
+    assert rc == 0, err
+    rc, out, err = kfctl(cl, "describe", "routes", "-n", "ci-ns")
+    assert rc == 0, err
+
+
+def test_get_output_formats(cl):
+    rc, out, err = kfctl(cl, "get", "nb", "-n", "ci-ns", "-o", "json")
+    assert rc == 0
+    doc = json.loads(out)
+    assert doc["kind"] == "List" and doc["items"][0]["metadata"]["name"] == "minimal-notebook"
+    rc, out, _ = kfctl(cl, "get", "notebooks.kubeflow.org/minimal-notebook", "-n", "ci-ns", "-o", "yaml")
+    assert rc == 0 and "kind: Notebook" in out and "readyReplicas: 1" in out
+    rc, out, _ = kfctl(cl, "get", "po", "-n", "ci-ns", "-o", "name")
+    assert rc == 0 and out.strip() == "pod/minimal-notebook-0"
+    rc, out, _ = kfctl(cl, "get", "pods", "-n", "ci-ns", "-o", "jsonpath={.items[*].metadata.name}")
+    assert rc == 0 and out == "minimal-notebook-0"
+    rc, out, _ = kfctl(cl, "get", "pods", "-A", "-o", "wide")
+    hdr = out.splitlines()[0].split()
+    assert rc == 0 and hdr[:2] == ["NAMESPACE", "NAME"] and "IP" in hdr
+    rc, out, _ = kfctl(cl, "get", "notebook", "minimal-notebook", "-n", "ci-ns")
+    assert rc == 0 and out.splitlines()[1].split()[:3] == ["minimal-notebook", "1", "Ready"]
+    rc, out, _ = kfctl(cl, "get", "sts,svc", "-n", "ci-ns")
+    assert rc == 0 and out.count("NAME") == 2 and "ClusterIP" in out
+    rc, _, err = kfctl(cl, "get", "frobnicators")
+    assert rc == 1 and "doesn't have a resource type" in err
+
+
+def test_wait_by_label_timeout_and_delete(cl):
+    # notebook_controller_integration_test.yaml:106 form: wait pods -l ... --for=condition=Ready
+    rc, out, err = kfctl(cl, "wait", "pods", "-n", "ci-ns", "-l", "notebook-name=minimal-notebook",
+                         "--for=condition=Ready", "--timeout=30s")
+    assert rc == 0 and "condition met" in out, err
+    rc, out, err = kfctl(cl, "wait", "pod/minimal-notebook-0", "-n", "ci-ns", "--for=condition=Bogus",
+                         "--timeout=1s")
+    assert rc == 1 and "timed out waiting for the condition" in err
+    rc, out, err = kfctl(cl, "delete", "notebook", "minimal-notebook", "-n", "ci-ns")
+    assert rc == 0 and "deleted" in out, err
+    rc, out, err = kfctl(cl, "wait", "pods", "minimal-notebook-0", "-n", "ci-ns", "--for=delete", "--timeout=60s")
+    assert rc == 0, err
