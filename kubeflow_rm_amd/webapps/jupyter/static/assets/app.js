@@ -2,8 +2,9 @@
 // resource table, polled with backoff; "All namespaces" adds a Namespace column), connect / start /
 // stop / delete, notebook details (overview + conditions / events / logs viewer / YAML), and the
 // spawner built from /api/config: image groups, CPU and memory requests with their limits
-// (form-cpu-ram: the admin's limitFactor pre-fills the limit until the user edits it), MI355X GPU
-// counts on the amd.com/gpu vendor, workspace volume (name from the {notebook-name} template, size,
+// (form-cpu-ram: the admin's limitFactor pre-fills the limit until the user edits it), GPUs (count +
+// vendor from the admin's vendor list, /api/gpus marks the vendors installed in the cluster: the
+// form-gpus component), workspace volume (name from the {notebook-name} template, size,
 // access mode), data volumes (mount follows the volume name until edited), affinity / toleration
 // groups, PodDefault configurations, shared memory.
 //
@@ -75,7 +76,7 @@
         imagePullPolicy: ((c.imagePullPolicy || {}).value) || "IfNotPresent",
         cpu, cpuLimit: JWA.limitFrom(cpu, (c.cpu || {}).limitFactor, ""),
         memory: mem, memoryLimit: JWA.limitFrom(mem, (c.memory || {}).limitFactor, "Gi"),
-        gpus: { num: gpu.num || "none", vendor: gpu.vendor || ((gpu.vendors || [])[0] || {}).limitsKey || "" },
+        gpus: { num: gpu.num || "none", vendor: gpu.vendor || "" },  // form-new: config.gpus.value.vendor as is
         shm: !!((c.shm || {}).value),
         workspace: ws.newPvc || ws.existingSource ? {
           enabled: true, type: ws.existingSource ? "existing" : "new", template: (pvc.metadata || {}).name || "{notebook-name}-workspace",
@@ -100,6 +101,25 @@
       return out;
     },
     editMount(vol, mount) { return Object.assign({}, vol, { mount, mountDirty: true }); },
+    // form-gpus.component.ts: the admin's vendor list; a vendor /api/gpus does not report as
+    // installed keeps its option but carries the "no GPUs" tooltip; the vendor control is disabled
+    // while the count is "none", and a count needs a vendor (vendorWithNum -> vendorNullName)
+    gpuVendors(config) { return ((((config || {}).gpus || {}).value || {}).vendors) || []; },
+    vendorTooltip(vendor, installed) {
+      return installed && installed.has && installed.has(vendor.limitsKey) ? ""
+        : `There are currently no ${vendor.uiName} GPUs in your cluster.`;
+    },
+    vendorDisabled(gpus) { return !gpus || gpus.num === "none"; },
+    vendorError(gpus) {
+      return gpus && gpus.num !== "none" && !gpus.vendor ? "You must also specify the GPU Vendor for the assigned GPUs" : "";
+    },
+    vendorOptions(config, gpus, installed) {
+      const e = kf.esc;
+      const vendors = JWA.gpuVendors(config);
+      const empty = !gpus.vendor || !vendors.some((v) => v.limitsKey === gpus.vendor) ? '<option value=""></option>' : "";
+      return empty + vendors.map((v) => `<option value="${e(v.limitsKey)}" title="${e(JWA.vendorTooltip(v, installed))}"` +
+        `${v.limitsKey === gpus.vendor ? " selected" : ""}>${e(v.uiName)}</option>`).join("");
+    },
     validate(f) {
       const errs = [];
       const n = kf.validators.name(f.name, 52);  // StatefulSet pod names: <name>-0 within 63
@@ -112,6 +132,8 @@
           if (e2) errs.push(e2);
         }
       }
+      const ve = JWA.vendorError(f.gpus);
+      if (ve) errs.push(ve);
       (f.datavols || []).forEach((d) => {
         if (d.type === "new" && kf.validators.name(d.name)) errs.push(`Data volume: ${kf.validators.name(d.name)}`);
         if (!String(d.mount || "").startsWith("/")) errs.push(`Data volume mount must be an absolute path: ${d.mount}`);
@@ -171,6 +193,7 @@
   function app() {
     const $ = (id) => document.getElementById(id);
     let config = null, poller = null, table = null, namespaces = [], form = null, rows = [];
+    let installedVendors = new Set();
 
     async function loadNamespaces() {
       try { namespaces = (await kf.call("GET", "/api/namespaces")).namespaces; }
@@ -310,6 +333,7 @@
       $("f-custom-row").hidden = config.allowCustomImage === false;
       const counts = (config.gpus.value || {}).options || ["none", "1", "2", "4", "8"];
       $("f-gpus").innerHTML = counts.map((c) => `<option${c === form.gpus.num ? " selected" : ""}>${c}</option>`).join("");
+      renderVendor();
       $("f-cpu").value = form.cpu; $("f-cpu-limit").value = form.cpuLimit;
       $("f-mem").value = form.memory; $("f-mem-limit").value = form.memoryLimit;
       $("f-shm").checked = form.shm;
@@ -322,8 +346,18 @@
       renderWorkspace();
       renderDataVolumes();
     }
+    function renderVendor() {
+      $("f-gpu-vendor").innerHTML = JWA.vendorOptions(config, form.gpus, installedVendors);
+      $("f-gpu-vendor").disabled = JWA.vendorDisabled(form.gpus) || !!(config.gpus || {}).readOnly;
+      $("f-gpu-vendor-err").textContent = "";
+    }
     let cpuLimitDirty = false, memLimitDirty = false;
     function bindSpawner() {
+      $("f-gpus").onchange = (ev) => { form.gpus = { num: ev.target.value, vendor: form.gpus.vendor }; renderVendor(); };
+      $("f-gpu-vendor").onchange = (ev) => {
+        form.gpus = { num: form.gpus.num, vendor: ev.target.value };
+        $("f-gpu-vendor-err").textContent = JWA.vendorError(form.gpus);
+      };
       $("f-name").oninput = (ev) => {
         form.name = ev.target.value;
         if (form.workspace.enabled && form.workspace.type === "new") { form.workspace.name = JWA.volumeName(form.workspace.template, form.name); renderWorkspace(); }
@@ -356,6 +390,8 @@
           `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"${form.configurations.includes(pd.label) ? " checked" : ""}> ${kf.esc(pd.desc)}</label><br>`).join("") || '<span class="muted">none</span>';
       } catch (e) { $("f-configs").innerHTML = '<span class="muted">none</span>'; }
       try { form.pvcs = (await kf.call("GET", `/api/namespaces/${ns}/pvcs`)).pvcs; } catch (e) { form.pvcs = []; }
+      // backend.service.ts getGPUVendors: the configured vendors some node reports capacity for
+      try { installedVendors = new Set((await kf.call("GET", "/api/gpus")).vendors || []); } catch (e) { installedVendors = new Set(); }
       fillSpawner();
       $("f-error").textContent = "";
       $("spawner").showModal();
@@ -366,7 +402,8 @@
       ev.preventDefault();
       const ns = kf.namespace();
       form.customImage = $("f-custom").value.trim();
-      form.gpus = $("f-gpus").value === "none" ? { num: "none", vendor: form.gpus.vendor } : { num: $("f-gpus").value, vendor: form.gpus.vendor };
+      form.gpus = { num: $("f-gpus").value, vendor: $("f-gpu-vendor").value };
+      $("f-gpu-vendor-err").textContent = JWA.vendorError(form.gpus);
       form.shm = $("f-shm").checked;
       form.affinityConfig = $("f-affinity").value || "none";
       form.tolerationGroup = $("f-toleration").value || "none";

@@ -332,6 +332,34 @@ test("confirm dialogs: the reference texts, applying state, error kept in the di
   assert.ok(failed.includes("&lt;forbidden&gt;") && failed.includes('data-resp="accept"'));
 });
 
+test("JWA form-gpus: vendor list, 'not installed' tooltip, vendor-with-num (form-gpus.component.ts:25-77)", () => {
+  const cfg = fixture("jupyter", "config").config;  // vendors NVIDIA + AMD, vendor "", num "none"
+  const f = JWA.formDefaults(cfg, "nb");
+  assert.deepStrictEqual(f.gpus, { num: "none", vendor: "" });
+  // num "none": the vendor control is disabled, and no vendor is required
+  assert.strictEqual(JWA.vendorDisabled(f.gpus), true);
+  assert.strictEqual(JWA.vendorError(f.gpus), "");
+  // /api/gpus reported only amd.com/gpu: NVIDIA keeps its option with the tooltip
+  const installed = new Set(["amd.com/gpu"]);
+  const [nv, amd] = JWA.gpuVendors(cfg);
+  assert.strictEqual(JWA.vendorTooltip(nv, installed), "There are currently no NVIDIA GPUs in your cluster.");
+  assert.strictEqual(JWA.vendorTooltip(amd, installed), "");
+  const html = JWA.vendorOptions(cfg, f.gpus, installed);
+  assert.ok(html.startsWith('<option value=""></option>'), html);  // no vendor chosen yet
+  assert.ok(html.includes('value="nvidia.com/gpu" title="There are currently no NVIDIA GPUs in your cluster.">NVIDIA'));
+  assert.ok(html.includes('value="amd.com/gpu" title="">AMD'));
+  // a count without a vendor is the vendorNullName error, in validate() too
+  const g = { num: "2", vendor: "" };
+  assert.strictEqual(JWA.vendorDisabled(g), false);
+  assert.strictEqual(JWA.vendorError(g), "You must also specify the GPU Vendor for the assigned GPUs");
+  assert.ok(JWA.validate(Object.assign({}, f, { name: "nb", gpus: g })).includes("You must also specify the GPU Vendor for the assigned GPUs"));
+  const ok = { num: "2", vendor: "amd.com/gpu" };
+  assert.strictEqual(JWA.vendorError(ok), "");
+  assert.ok(JWA.vendorOptions(cfg, ok, installed).includes('value="amd.com/gpu" title="" selected>AMD'));
+  // nothing installed at all (CPU cluster): every vendor gets the tooltip
+  assert.ok(JWA.vendorOptions(cfg, ok, new Set()).includes("There are currently no AMD GPUs in your cluster."));
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {

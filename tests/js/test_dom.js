@@ -1,0 +1,195 @@
+// DOM-level tests of the JWA page (jupyter/static/index.html + assets/app.js + common kf.js) on the
+// fake DOM of fakedom.js: the page boots against a scripted backend, then the table's action
+// buttons and the spawner form are driven the way a user drives them (clicks, selects, typing) and
+// the HTTP calls the page makes are asserted. Ports the behaviour of the reference's
+// jupyter/frontend/src/app/pages/index/index-default (button wiring + confirm dialogs) and
+// pages/form/form-new/form-gpus/form-gpus.component.ts (vendor select, tooltip, vendorWithNum).
+// argv[2] = the reference crud-web-apps directory (its Cypress fixtures are the backend's data).
+"use strict";
+const assert = require("assert");
+const fs = require("fs");
+const path = require("path");
+const vm = require("vm");
+const { Document, Node, choose, type } = require("./fakedom.js");
+
+const WEB = path.join(__dirname, "../../kubeflow_rm_amd/webapps");
+const FIX = process.argv[2];
+const fixture = (name) => JSON.parse(fs.readFileSync(path.join(FIX, "jupyter/frontend/cypress/fixtures", name + ".json"), "utf8"));
+
+// ---- browser globals -----------------------------------------------------------------------------------
+global.window = global;
+global.Node = Node;
+global.document = new Document(fs.readFileSync(path.join(WEB, "jupyter/static/index.html"), "utf8"));
+global.location = { search: "?ns=team" };
+global.localStorage = { getItem: () => null, setItem: () => {} };
+global.addEventListener = () => {};
+global.parent = global;
+global.postMessage = () => {};
+const opened = [];
+global.open = (url) => opened.push(url);
+const realSetTimeout = setTimeout;
+global.setTimeout = (fn, ms) => (ms > 100 ? 0 : realSetTimeout(fn, ms));  // no background polling
+global.clearTimeout = () => {};
+
+// ---- scripted backend ----------------------------------------------------------------------------------
+const config = fixture("config").config;  // GPU vendors NVIDIA + AMD, no default vendor
+const notebooks = fixture("notebooks").notebooks;
+const calls = [];
+const overrides = {};
+global.fetch = async (url, opts) => {
+  const method = (opts && opts.method) || "GET";
+  const body = opts && opts.body ? JSON.parse(opts.body) : undefined;
+  calls.push({ method, url, body });
+  const key = `${method} ${url}`;
+  let data = { success: true };
+  if (overrides[key]) data = overrides[key];
+  else if (url === "api/config") data = { success: true, config };
+  else if (url === "api/namespaces") data = { success: true, namespaces: ["team"] };
+  else if (url === "api/namespaces/team/notebooks" && method === "GET") data = { success: true, notebooks };
+  else if (url === "api/namespaces/team/poddefaults") data = { success: true, poddefaults: [{ label: "add-gpu-env", desc: "GPU env" }] };
+  else if (url === "api/namespaces/team/pvcs") data = { success: true, pvcs: [{ name: "data" }] };
+  else if (url === "api/gpus") data = { success: true, vendors: ["amd.com/gpu"] };
+  const ok = data.success !== false;
+  return { ok, status: ok ? 200 : 403, statusText: ok ? "OK" : "Forbidden", json: async () => data };
+};
+
+const settle = async (n = 10) => { for (let i = 0; i < n; i++) await new Promise((r) => setImmediate(r)); };
+const $ = (id) => document.getElementById(id);
+const lastCall = (method) => calls.filter((c) => c.method === method).slice(-1)[0];
+
+vm.runInThisContext(fs.readFileSync(path.join(WEB, "crud_backend/static/kf.js"), "utf8"));
+vm.runInThisContext(fs.readFileSync(path.join(WEB, "jupyter/static/assets/app.js"), "utf8"));
+
+const tests = [];
+const test = (name, fn) => tests.push([name, fn]);
+const btn = (action, name) => document.querySelectorAll(`#notebooks button[data-action="${action}"]`)
+  .find((b) => b.getAttribute("data-key").split("/").pop() === name) || null;
+const nsOf = (r) => r.namespace || "team";
+const byPhase = (phase) => notebooks.find((r) => r.status.phase === phase);
+
+test("page boots: config, namespaces and the notebook table from the backend", async () => {
+  await settle();
+  assert.ok(calls.some((c) => c.url === "api/config"));
+  const rows = document.querySelectorAll("#notebooks tbody tr");
+  assert.strictEqual(rows.length, notebooks.length);
+});
+
+test("table: Stop on a ready notebook confirms, then PATCHes stopped=true and marks the row", async () => {
+  const nb = byPhase("ready");
+  btn("toggle", nb.name).click();
+  const dlg = document.querySelector("dialog.confirm");
+  assert.ok(dlg && dlg.open, "confirm dialog shown");
+  assert.ok(dlg.textContent.includes(`Are you sure you want to stop this notebook server? ${nb.name}`));
+  dlg.querySelector('button[data-resp="accept"]').click();
+  await settle();
+  const c = lastCall("PATCH");
+  assert.deepStrictEqual([c.url, c.body], [`api/namespaces/${nsOf(nb)}/notebooks/${nb.name}`, { stopped: true }]);
+  assert.strictEqual(document.querySelector("dialog.confirm"), null, "dialog closed after success");
+});
+
+test("table: a failing Stop keeps the dialog open with the backend's error", async () => {
+  // another row whose toggle is an enabled "Stop" (the warning-phase notebook)
+  const nb = byPhase("warning");
+  assert.ok(btn("toggle", nb.name) && !btn("toggle", nb.name).disabled && btn("toggle", nb.name).textContent === "Stop");
+  overrides[`PATCH api/namespaces/${nsOf(nb)}/notebooks/${nb.name}`] = { success: false, log: "forbidden: <stop>" };
+  // re-render with fresh rows (the previous test marked its row pending)
+  calls.length = 0;
+  btn("toggle", nb.name).click();
+  const dlg = document.querySelector("dialog.confirm");
+  dlg.querySelector('button[data-resp="accept"]').click();
+  await settle();
+  const again = document.querySelector("dialog.confirm");
+  assert.ok(again && again.textContent.includes("forbidden: <stop>"), "error shown in the dialog");
+  again.querySelector('button[data-resp="cancel"]').click();
+  await settle();
+  assert.strictEqual(document.querySelector("dialog.confirm"), null);
+  delete overrides[`PATCH api/namespaces/${nsOf(nb)}/notebooks/${nb.name}`];
+});
+
+test("table: Start on a stopped notebook PATCHes stopped=false without a dialog", async () => {
+  const nb = byPhase("stopped");
+  btn("toggle", nb.name).click();
+  await settle();
+  assert.strictEqual(document.querySelector("dialog.confirm"), null);
+  const c = lastCall("PATCH");
+  assert.deepStrictEqual([c.url, c.body], [`api/namespaces/${nsOf(nb)}/notebooks/${nb.name}`, { stopped: false }]);
+});
+
+test("table: Connect opens the notebook URL only when ready; Delete confirms then DELETEs", async () => {
+  const ready = notebooks.find((r) => r.status.phase === "ready" && btn("connect", r.name) && !btn("connect", r.name).disabled);
+  if (ready) {
+    btn("connect", ready.name).click();
+    assert.strictEqual(opened.pop(), `/notebook/${nsOf(ready)}/${ready.name}/`);
+  }
+  const stopped = byPhase("stopped");
+  const cb = btn("connect", stopped.name);
+  assert.ok(cb.disabled, "connect disabled for a stopped notebook");
+  cb.click();
+  assert.strictEqual(opened.length, 0);
+  const victim = notebooks.find((r) => btn("delete", r.name) && !btn("delete", r.name).disabled);
+  btn("delete", victim.name).click();
+  const dlg = document.querySelector("dialog.confirm");
+  assert.ok(dlg.textContent.includes(`Are you sure you want to delete this notebook server? ${victim.name}`));
+  dlg.querySelector('button[data-resp="accept"]').click();
+  await settle();
+  assert.strictEqual(lastCall("DELETE").url, `api/namespaces/${nsOf(victim)}/notebooks/${victim.name}`);
+});
+
+test("spawner: GPU vendor select from the config, 'not installed' tooltip, disabled while count is none", async () => {
+  $("new").click();
+  await settle();
+  assert.ok($("spawner").open, "spawner dialog open");
+  assert.ok(calls.some((c) => c.url === "api/gpus"), "installed vendors fetched");
+  const v = $("f-gpu-vendor");
+  const opts = v.options.map((o) => [o.value, o.textContent, o.getAttribute("title")]);
+  assert.deepStrictEqual(opts, [["", "", null],
+    ["nvidia.com/gpu", "NVIDIA", "There are currently no NVIDIA GPUs in your cluster."],
+    ["amd.com/gpu", "AMD", ""]]);
+  assert.strictEqual($("f-gpus").value, "none");
+  assert.ok(v.disabled, "vendor disabled while num is none");
+  choose($("f-gpus"), "2");
+  assert.ok(!$("f-gpu-vendor").disabled, "vendor enabled once a count is chosen");
+});
+
+test("spawner: a GPU count without a vendor is refused (vendorNullName), then the chosen vendor is POSTed", async () => {
+  type($("f-name"), "my-nb");
+  const posts = () => calls.filter((c) => c.method === "POST").length;
+  const before = posts();
+  $("f-submit").click();
+  await settle();
+  assert.strictEqual(posts(), before, "no POST while the vendor is missing");
+  assert.ok($("f-error").textContent.includes("You must also specify the GPU Vendor for the assigned GPUs"), $("f-error").textContent);
+  assert.ok($("f-gpu-vendor-err").textContent.includes("You must also specify the GPU Vendor"));
+  choose($("f-gpu-vendor"), "amd.com/gpu");
+  assert.strictEqual($("f-gpu-vendor-err").textContent, "");
+  $("f-submit").click();
+  await settle();
+  const c = lastCall("POST");
+  assert.strictEqual(c.url, "api/namespaces/team/notebooks");
+  assert.strictEqual(c.body.name, "my-nb");
+  assert.deepStrictEqual(c.body.gpus, { num: "2", vendor: "amd.com/gpu" });
+  assert.strictEqual(c.body.workspace.newPvc.metadata.name, "{notebook-name}-workspace");
+  assert.ok(!$("spawner").open, "spawner closed after a successful create");
+  assert.ok(document.getElementById("kf-snack").textContent.includes("Notebook my-nb created"));
+});
+
+test("spawner: count back to none sends no vendor requirement", async () => {
+  $("new").click();
+  await settle();
+  type($("f-name"), "cpu-nb");
+  choose($("f-gpus"), "none");
+  assert.ok($("f-gpu-vendor").disabled);
+  $("f-submit").click();
+  await settle();
+  const c = lastCall("POST");
+  assert.strictEqual(c.body.name, "cpu-nb");
+  assert.deepStrictEqual(c.body.gpus, { num: "none" });
+});
+
+(async () => {
+  let failed = 0;
+  for (const [name, fn] of tests) {
+    try { await fn(); console.log("ok -", name); } catch (e) { failed++; console.log("FAIL -", name, "\n", e && e.stack); }
+  }
+  process.exit(failed ? 1 : 0);
+})();

@@ -252,3 +252,33 @@ def test_dashboard_env_info_has_the_fixture_shape(monkeypatch):
     shell = app.test_client().get("/")
     assert b"/cdb.js" in shell.data
     assert app.test_client().get("/cdb.js").status_code == 200
+
+
+@needs_node
+def test_gpu_vendor_contract_with_backend(apps):
+    """T2: the spawner's vendor select is built from OUR /api/config vendor list and OUR /api/gpus
+    (configured vendors some node reports capacity for: the kube-lite node advertises amd.com/gpu),
+    so the MI355X vendor carries no "no GPUs in your cluster" tooltip, and a count without a vendor
+    is refused in JS before it reaches the backend."""
+    tc, _ = apps["jwa"]
+    cfg = tc.get("/api/config", headers=_h()).get_json()["config"]
+    vendors = tc.get("/api/gpus", headers=_h()).get_json()["vendors"]
+    assert vendors == ["amd.com/gpu"]
+    script = """
+      global.window = global; global.document = {cookie: ""}; global.location = {search: ""};
+      global.localStorage = {getItem: () => null, setItem: () => {}}; global.addEventListener = () => {}; global.parent = global;
+      const path = require("path"); const W = path.join(process.argv[1], "kubeflow_rm_amd/webapps");
+      global.kf = require(path.join(W, "crud_backend/static/kf.js"));
+      const JWA = require(path.join(W, "jupyter/static/assets/app.js"));
+      const cfg = JSON.parse(process.argv[2]), installed = new Set(JSON.parse(process.argv[3]));
+      const f = JWA.formDefaults(cfg, "g");
+      console.log(JSON.stringify({opts: JWA.vendorOptions(cfg, {num: "1", vendor: f.gpus.vendor}, installed),
+                                  err: JWA.vendorError({num: "1", vendor: ""}), vendor: f.gpus.vendor}));
+    """
+    r = subprocess.run([NODE, "-e", script, str(ROOT), json.dumps(cfg), json.dumps(vendors)], capture_output=True,
+                       text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["vendor"] == "amd.com/gpu"
+    assert 'value="amd.com/gpu" title="" selected>AMD Instinct MI355X' in out["opts"]
+    assert out["err"] == "You must also specify the GPU Vendor for the assigned GPUs"
