@@ -6,6 +6,7 @@ cases against kube-lite (routes, network policies, CA bundle, OAuth objects, ser
 reconciliation lock, update-pending). Runs with SET_PIPELINE_RBAC=true like the reference's
 RoleBinding cases.
 """
+import copy
 import time
 from pathlib import Path
 
@@ -243,6 +244,105 @@ def test_oauth_notebook(c):
     c.delete(NB, "Notebook", "secure", "odh")
     for av, kind, name in [("v1", "Secret", "secure-oauth-config"), ("v1", "Service", "secure-tls"),
                            ("route.openshift.io/v1", "Route", "secure"), ("networking.k8s.io/v1", "NetworkPolicy", "secure-ctrl-np")]:
+        c.wait_gone(av, kind, name, "odh", timeout=15)
+
+
+# ---- OAuth-mode envtest cases, one named test each (notebook_controller_test.go:575-898) ----------
+def _oauth_nb():
+    nb = _nb("oauth-env", "odh", annotations={"notebooks.opendatahub.io/inject-oauth": "true",
+                                              "notebooks.opendatahub.io/foo": "bar"})
+    nb["metadata"]["labels"] = {"app.kubernetes.io/instance": "oauth-env"}
+    spec = nb["spec"]["template"]["spec"]
+    spec["containers"][0]["image"] = "registry.redhat.io/ubi8/ubi:latest"
+    spec["volumes"] = [{"name": "notebook-data", "persistentVolumeClaim": {"claimName": "oauth-env-data"}}]
+    return nb
+
+
+def _oauth_spec_as_injected(nb):
+    spec = nb["spec"]["template"]["spec"]
+    proxy = [x for x in spec["containers"] if x["name"] == "oauth-proxy"][0]
+    vols = {v["name"]: v for v in spec["volumes"]}
+    return spec["serviceAccountName"], proxy["image"], vols["oauth-config"], vols["tls-certificates"]
+
+
+def test_oauth_envtest_inject_sidecar_and_remove_lock(c):
+    """It("Should inject the OAuth proxy as a sidecar container") / ("Should remove the
+    reconciliation lock annotation"): notebook_controller_test.go:660-681."""
+    nb = c.create(_oauth_nb())
+    spec = nb["spec"]["template"]["spec"]
+    assert [x["name"] for x in spec["containers"]] == ["oauth-env", "oauth-proxy"]
+    assert spec["serviceAccountName"] == "oauth-env"
+    vols = {v["name"]: v for v in spec["volumes"]}
+    assert vols["oauth-config"]["secret"] == {"secretName": "oauth-env-oauth-config", "defaultMode": 420}
+    assert vols["tls-certificates"]["secret"] == {"secretName": "oauth-env-tls", "defaultMode": 420}
+    assert nb["metadata"]["annotations"]["kubeflow-resource-stopped"] == LOCK
+    c.wait_for(NB, "Notebook", "oauth-env", "odh",
+               lambda o: "kubeflow-resource-stopped" not in (o["metadata"].get("annotations") or {}), timeout=10)
+
+
+def test_oauth_envtest_reconcile_notebook_when_modified(c):
+    """It("Should reconcile the Notebook when modified"), notebook_controller_test.go:684-698: a
+    hand edit of the SA name, the OAuth sidecar image and the oauth-config volume is undone by the
+    webhook on UPDATE — the spec comes back exactly as injected."""
+    for _ in range(50):  # the controllers write the Notebook too: retry the edit on a conflict
+        nb = c.get(NB, "Notebook", "oauth-env", "odh")
+        want = copy.deepcopy(_oauth_spec_as_injected(nb))
+        spec = nb["spec"]["template"]["spec"]
+        spec["serviceAccountName"] = "foo"
+        [x for x in spec["containers"] if x["name"] == "oauth-proxy"][0]["image"] = "bar"
+        for v in spec["volumes"]:
+            if v["name"] == "oauth-config":
+                v.pop("secret", None)
+        try:
+            out = c.update(nb)
+            break
+        except ApiException as e:
+            if e.status != 409:
+                raise
+            time.sleep(0.05)
+    assert _oauth_spec_as_injected(out) == want
+    time.sleep(0.2)
+    assert _oauth_spec_as_injected(c.get(NB, "Notebook", "oauth-env", "odh")) == want
+
+
+def test_oauth_envtest_route_recreated_when_deleted(c):
+    """It("Should recreate the Route when deleted"), notebook_controller_test.go:834-845."""
+    r = _exists(c, "route.openshift.io/v1", "Route", "oauth-env")
+    assert r["spec"]["to"] == {"kind": "Service", "name": "oauth-env-tls", "weight": 100}
+    assert r["spec"]["tls"] == {"termination": "reencrypt", "insecureEdgeTerminationPolicy": "Redirect"}
+    assert r["spec"]["port"]["targetPort"] == "oauth-proxy" and r["spec"]["wildcardPolicy"] == "None"
+    c.delete("route.openshift.io/v1", "Route", "oauth-env", "odh")
+    r2 = c.wait_for("route.openshift.io/v1", "Route", "oauth-env", "odh",
+                    lambda o: o["metadata"]["uid"] != r["metadata"]["uid"] and not o["metadata"].get("deletionTimestamp"),
+                    timeout=10)
+    assert r2["spec"]["to"]["name"] == "oauth-env-tls" and r2["spec"]["tls"]["termination"] == "reencrypt"
+
+
+def test_oauth_envtest_route_reconciled_when_modified(c):
+    """It("Should reconcile the Route when modified"), notebook_controller_test.go:847-863: a merge
+    patch of spec.to.name is reverted to the OAuth service."""
+    c.patch("route.openshift.io/v1", "Route", "oauth-env", {"spec": {"to": {"name": "foo"}}}, "odh", "merge")
+    r = c.wait_for("route.openshift.io/v1", "Route", "oauth-env", "odh",
+                   lambda o: o["spec"]["to"]["name"] == "oauth-env-tls", timeout=10)
+    assert r["spec"]["tls"]["termination"] == "reencrypt"
+
+
+def test_oauth_envtest_delete_oauth_proxy_objects(c):
+    """It("Should delete the OAuth proxy objects"), notebook_controller_test.go:865-898: the
+    Notebook controller-owns the ServiceAccount, Service, Secret and Route (controller +
+    blockOwnerDeletion); deleting it removes them (kube-lite runs the garbage collector that envtest
+    lacks, so existence is asserted too)."""
+    nb = c.get(NB, "Notebook", "oauth-env", "odh")
+    want = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook", "name": "oauth-env", "uid": nb["metadata"]["uid"],
+            "controller": True, "blockOwnerDeletion": True}
+    objs = [("v1", "ServiceAccount", "oauth-env"), ("v1", "Service", "oauth-env-tls"),
+            ("v1", "Secret", "oauth-env-oauth-config"), ("route.openshift.io/v1", "Route", "oauth-env")]
+    for av, kind, name in objs:
+        o = _exists(c, av, kind, name)
+        assert want in o["metadata"].get("ownerReferences", []), (kind, o["metadata"].get("ownerReferences"))
+    c.delete(NB, "Notebook", "oauth-env", "odh")
+    c.wait_gone(NB, "Notebook", "oauth-env", "odh", timeout=15)
+    for av, kind, name in objs:
         c.wait_gone(av, kind, name, "odh", timeout=15)
 
 
