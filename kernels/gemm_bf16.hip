@@ -568,7 +568,8 @@ extern "C" int kfamd_gemm_nt_bf16_variant(int variant, const void* A, const void
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
   // w4 / w4s (gemm_bf16_w4.hip): edge tiles in-kernel, so auto takes them for any M, N >= 128 with
-  // N % 8, K % 8 and 16-byte aligned rows; anything else falls through to the r1 kernels below.
+  // K % 8 and 16-byte aligned operand rows (any N / output alignment: the epilogue's odd path);
+  // anything else falls through to the r1 kernels below.
   if (variant == 6 || variant == 9)
     return kfamd_w4_launch_nt(variant == 6 ? 256 : 128, A, B, C, bias, R, nullptr, M, N, K, batch, lda, ldb, ldc, ldr,
                               stride_a, stride_b, stride_c, stride_r, alpha, act, stream);

@@ -32,6 +32,33 @@ int launch_t(const void* A, const void* B, void* C, const void* R, int M, int N,
 
 }  // namespace
 
+// Split-K partials of the transposed layouts on the 128x128 tile (see kfamd_w4_splitk_nt).
+extern "C" int kfamd_w4_splitk_t(int la, int lb, const void* A, const void* B, float* W, int M, int N, int K,
+                                 int batch, int splits, int kper, long long lda, long long ldb, long long sa,
+                                 long long sb, void* stream) {
+  const int rc = check_shape(la, lb, 128, A, B, W, nullptr, nullptr, nullptr, M, N, K, lda, ldb, N, 0, sa, sb, 0, 0);
+  if (rc != KFAMD_OK) return rc;
+  if (splits < 1 || kper < kBK || kper % kBK || (long long)kper * (splits - 1) >= K || !W || N % 8) return KFAMD_EINVAL;
+  if (reinterpret_cast<uintptr_t>(W) & 15) return KFAMD_EALIGN;
+  dim3 grid(((M + 127) / 128) * ((N + 127) / 128), batch, splits), block(kThreads);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* a = static_cast<const __bf16*>(A);
+  const __bf16* b = static_cast<const __bf16*>(B);
+#define W4S(LA_, LB_)                                                                                             \
+  if (la == LA_ && lb == LB_) {                                                                                   \
+    hipLaunchKernelGGL((gemm_w4<KFAMD_ACT_NONE, false, false, false, LA_, LB_, 128, true>), grid, block, 0, s, a, b, \
+                       nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, 0LL, 0LL, sa, sb, 0LL, 0LL, 1.0f,     \
+                       nullptr, W, kper);                                                                         \
+    const hipError_t e = hipGetLastError();                                                                       \
+    return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);                                                      \
+  }
+  W4S(0, 1)
+  W4S(1, 1)
+  W4S(1, 0)
+#undef W4S
+  return KFAMD_EINVAL;
+}
+
 // la/lb: 0 = K-contiguous operand, 1 = k-major (see gemm_w4.h); (0, 0) is kfamd_w4_launch_nt.
 extern "C" int kfamd_w4_launch_t(int la, int lb, int bm, const void* A, const void* B, void* C, const void* R, int M,
                                  int N, int K, int batch, long long lda, long long ldb, long long ldc, long long ldr,

@@ -82,6 +82,13 @@ __device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& 
 }
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// The same, opaque to CSE: the epilogue re-derives it after the K loop instead of the compiler
+// keeping a prologue copy (lane >> 4) alive - or spilled - across the loop.
+__device__ __forceinline__ int lane_id_fresh() {
+  int v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
+}
 
 // Per-operand staging geometry. One operand tile = 64 k x BM rows/cols = BM*128 bytes, DMA'd as
 // BM/32 one-KiB pieces per wave (4 waves).
@@ -195,14 +202,18 @@ struct Reader {
 // BM = 256: 256x256 tile (one 160 KiB block per CU). BM = 128 ("w4s"): the same pipeline on a 128x128
 // tile, 64x64 per wave, 80 KiB of LDS -> two blocks per CU (problems with fewer 256-tiles than CUs).
 // AUX (ACT != NONE only): also store the pre-activation act^-1 input, for the activation's backward.
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, bool DIAG = false,
-          int ABL = 0>
+// SPLIT (split-K, for problems with too few output tiles to fill 256 CUs): blockIdx.z takes the K
+// range [z*kper, (z+1)*kper) and the block stores its raw fp32 partial tile to W[z][M][N]; the
+// epilogue (alpha, bias, activation, Aux, residual) runs in splitk_reduce (gemm_bf16.hip).
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, bool SPLIT = false,
+          bool DIAG = false, int ABL = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
              const __bf16* __restrict__ bias, const __bf16* __restrict__ R, __bf16* __restrict__ Aux, int M, int N,
              int K, long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
-             long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag) {
+             long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag,
+             float* __restrict__ W = nullptr, int kper = 0) {
   constexpr int BN = BM, WT = BM / 2, NR = WT / 16;    // wave tile WT x WT = NR x NR MFMA blocks
   constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
   constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
@@ -211,6 +222,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   constexpr int RG = 2;
   static_assert(BM == 256 || BM == 128, "tile");
   static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
+  static_assert(!SPLIT || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
   __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -233,11 +245,17 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const int m_lo = tm * BM, n_lo = tn * BN;            // first output row / column this block stores
   const int m0 = min(m_lo, M - BM), n0 = min(n_lo, N - BN);  // edge tiles shifted inside
 
+  long long kbeg = 0;
+  if (SPLIT) {  // this block's K range; only the last split can be partial (kper % 64 == 0)
+    kbeg = (long long)blockIdx.z * kper;
+    K = min((long long)kper, (long long)K - kbeg);
+  }
   const int nk = (K + kBK - 1) / kBK;
   const int koff = K - nk * kBK;                       // first K tile starts at k = koff (<= 0)
   const long long bz = blockIdx.y;
-  A += bz * sa + (LA == 0 ? (long long)m0 * lda + koff : (long long)m0 + (long long)koff * lda);
-  B += bz * sb + (LB == 0 ? (long long)n0 * ldb + koff : (long long)n0 + (long long)koff * ldb);
+  const long long ka = kbeg + koff;
+  A += bz * sa + (LA == 0 ? (long long)m0 * lda + ka : (long long)m0 + ka * lda);
+  B += bz * sb + (LB == 0 ? (long long)n0 * ldb + ka : (long long)n0 + ka * ldb);
   C += bz * sc;
   if (HAS_AUX) Aux += bz * sc;
   if (HAS_RES) R += bz * sr;
@@ -415,17 +433,33 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
   // lh 3 -> block n+1 cols 8-15: one dwordx4 store per lane per pair. The lane id is re-derived
   // here (v_mbcnt) so no lane-derived VGPR has to survive the K loop.
-  const int elane = lane_id();
+  const int elane = lane_id_fresh();
   const int elr = elane & 15, elh = elane >> 4;
+  // Output granularity og (elements, uniform): the widest store every lane's 8-column run allows,
+  // from the alignment of C / Aux, ldc, the batch stride and N (n0 = min(n_lo, N - BN) is then a
+  // multiple of og too, so the per-og-group edge mask is exact). og = 8 is the 16-B fast path; an odd
+  // output (e.g. a 1500-wide C, or a column slice of a wider buffer) stores 8, 4 or 2 bytes.
+  const unsigned gbits = (unsigned)(reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(HAS_AUX ? Aux : C)) |
+                         (unsigned)(2 * (ldc | sc | N)) | 16u;
+  const int og = (gbits & -gbits) / 2;  // 1, 2, 4 or 8
+  // bias / residual fragments (4 columns at col = ... + 4 lh) as 8-B vectors when aligned for it
+  const bool vec_in = og >= 4 && !((reinterpret_cast<uintptr_t>(HAS_BIAS ? bias : nullptr) |
+                                   reinterpret_cast<uintptr_t>(HAS_RES ? R : nullptr)) & 7) &&
+                      !(HAS_RES && ((ldr | sr) & 3));
   auto finish = [&](int i, int n, int m, uint2& pre_out) -> uint2 {
     const int col = n0 + wn * WT + n * 16 + elh * 4;
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
     if (HAS_BIAS) {
-      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+      if (vec_in) {
+        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+        for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)bias[col + r];
+      }
     }
     if (HAS_AUX) {
       bf16x4 p;
@@ -438,14 +472,54 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
     }
     if (HAS_RES) {
-      const bf16x4 rr = *reinterpret_cast<const bf16x4*>(R + (long long)m * ldr + col);
+      const __bf16* rp = R + (long long)m * ldr + col;
+      if (vec_in) {
+        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rp);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+        for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
+      }
     }
     bf16x4 o;
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
     return __builtin_bit_cast(uint2, o);
+  };
+  if constexpr (SPLIT) {
+    // raw fp32 partials, 4 consecutive columns per lane per block: W[z][m][n], ld N
+    float* Wz = W + ((long long)blockIdx.z * gridDim.y + blockIdx.y) * (long long)M * N;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = m0 + wm * WT + i * 16 + elr;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        const int col = n0 + wn * WT + n * 16 + elh * 4;
+        if (m >= m_lo && col >= n_lo)
+          *reinterpret_cast<f32x4*>(Wz + (long long)m * N + col) = acc[i][n];
+      }
+    }
+    return;
+  }
+  // 8 contiguous bf16 (4 dwords after the swap) at element offset o, column c0: store in og-groups
+  auto store8 = [&](__bf16* base, long long o, int c0, bool row_ok, uint4 d) {
+    if (og == 8) {
+      if (row_ok && c0 >= n_lo) *reinterpret_cast<uint4*>(base + o) = d;
+    } else if (og == 4) {
+      if (row_ok && c0 >= n_lo) *reinterpret_cast<uint2*>(base + o) = uint2{d.x, d.y};
+      if (row_ok && c0 + 4 >= n_lo) *reinterpret_cast<uint2*>(base + o + 4) = uint2{d.z, d.w};
+    } else if (og == 2) {
+      const unsigned w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (row_ok && c0 + 2 * q >= n_lo) *reinterpret_cast<unsigned*>(base + o + 2 * q) = w[q];
+    } else {
+      const bf16x8 e = __builtin_bit_cast(bf16x8, d);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (row_ok && c0 + q >= n_lo) base[o + q] = e[q];
+    }
   };
   const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
 #pragma unroll
@@ -459,12 +533,12 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       uint2 p = finish(i, n, m, pp), q = finish(i, n + 1, m, pq);
       const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
       const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
-      const bool ok = row_ok && (n0 + wn * WT + n * 16 + swap_col >= n_lo);
-      if (ok) *reinterpret_cast<uint4*>(C + roff + n * 16) = uint4{sx[0], sy[0], sx[1], sy[1]};
+      const int c0 = n0 + wn * WT + n * 16 + swap_col;
+      store8(C, roff + n * 16, c0, row_ok, uint4{sx[0], sy[0], sx[1], sy[1]});
       if (HAS_AUX) {
         const auto ax = __builtin_amdgcn_permlane16_swap(pp.x, pq.x, false, false);
         const auto ay = __builtin_amdgcn_permlane16_swap(pp.y, pq.y, false, false);
-        if (ok) *reinterpret_cast<uint4*>(Aux + roff + n * 16) = uint4{ax[0], ay[0], ax[1], ay[1]};
+        store8(Aux, roff + n * 16, c0, row_ok, uint4{ax[0], ay[0], ax[1], ay[1]});
       }
     }
   }
@@ -490,24 +564,25 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 }
 
 // Shape/alignment contract shared by the launchers (returns KFAMD_OK or an error code):
-//  16-B aligned bases and leading dims / batch strides in multiples of 8 elements; N % 8 (16-B
-//  output stores, 8-column edge shift); a K-contiguous operand needs K % 8, a k-major A needs M % 8;
-//  M, N >= BM; the 32-bit buffer offsets must cover a block's operand span.
+//  A/B: 16-B aligned bases, leading dims / batch strides in multiples of 8 elements; a K-contiguous
+//  operand needs K % 8, a k-major A needs M % 8, a k-major B needs N % 8; M, N >= BM; the 32-bit
+//  buffer offsets must cover a block's operand span. C/Aux/bias/R: bf16-aligned, any N and ldc (the
+//  epilogue takes its element-wise path when they are off the 16-B grid).
 inline int check_shape(int la, int lb, int BM, const void* A, const void* B, const void* C, const void* bias,
                        const void* R, const void* Aux, int M, int N, int K, long long lda, long long ldb,
                        long long ldc, long long ldr, long long sa, long long sb, long long sc, long long sr) {
   auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (M < BM || N < BM || K <= 0) return KFAMD_EINVAL;
-  if (N % 8) return KFAMD_EINVAL;
+  if (lb == 1 && N % 8) return KFAMD_EINVAL;
   if ((la == 0 || lb == 0) && K % 8) return KFAMD_EINVAL;
   if (la == 1 && M % 8) return KFAMD_EINVAL;
   if (la == 0 ? lda < K : lda < M) return KFAMD_EINVAL;
   if (lb == 0 ? ldb < K : ldb < N) return KFAMD_EINVAL;
   if (ldc < N || (R && ldr < N)) return KFAMD_EINVAL;
-  if (!al16(A) || !al16(B) || !al16(C) || (Aux && !al16(Aux))) return KFAMD_EALIGN;
-  if (lda % 8 || ldb % 8 || ldc % 8 || sa % 8 || sb % 8 || sc % 8) return KFAMD_EALIGN;
-  if (bias && (reinterpret_cast<uintptr_t>(bias) & 7)) return KFAMD_EALIGN;
-  if (R && ((reinterpret_cast<uintptr_t>(R) & 7) || ldr % 4 || sr % 4)) return KFAMD_EALIGN;
+  auto al2 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 1) == 0; };
+  if (!al16(A) || !al16(B) || !al2(C) || (Aux && !al2(Aux))) return KFAMD_EALIGN;
+  if (lda % 8 || ldb % 8 || sa % 8 || sb % 8) return KFAMD_EALIGN;
+  if ((bias && !al2(bias)) || (R && !al2(R))) return KFAMD_EALIGN;
   // buffer offsets: L=0 spans BM rows of ld; L=1 spans K rows of ld (voffset + soffset < 2^31)
   const long long span_a = la == 0 ? ((long long)BM * lda + kBK) * 2 : ((long long)K + kBK) * lda * 2;
   const long long span_b = lb == 0 ? ((long long)BM * ldb + kBK) * 2 : ((long long)K + kBK) * ldb * 2;

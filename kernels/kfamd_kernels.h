@@ -64,6 +64,23 @@ int kfamd_gemm_bf16_ex(int la, int lb, const void* A, const void* B, void* C, co
                        long long ldr, long long stride_a, long long stride_b, long long stride_c, long long stride_r,
                        float alpha, int act, void* stream);
 
+// Split-K for problems with too few 128x128 output tiles to fill the chip: the partial products
+// of K range [z*kper, (z+1)*kper) go to W[z][b][M][N] fp32 (kper % 64 == 0, splits*kper >= K),
+// then kfamd_splitk_reduce applies the epilogue into bf16 C. Same shape contract as _ex at bm=128.
+int kfamd_w4_splitk_nt(const void* A, const void* B, float* W, int M, int N, int K, int batch, int splits, int kper,
+                       long long lda, long long ldb, long long stride_a, long long stride_b, void* stream);
+int kfamd_w4_splitk_t(int la, int lb, const void* A, const void* B, float* W, int M, int N, int K, int batch,
+                      int splits, int kper, long long lda, long long ldb, long long stride_a, long long stride_b,
+                      void* stream);
+int kfamd_splitk_reduce(const float* W, void* C, const void* bias, const void* R, void* Aux, int M, int N, int batch,
+                        int splits, long long ldc, long long ldr, long long stride_c, long long stride_r, float alpha,
+                        int act, void* stream);
+
+// K-padding pack (pad_bf16.hip): dst_i[r][0:Kp] = src_i[r][0:K], zero tail, both GEMM operands in
+// one launch (rows1 = 0: one matrix). Kp % 8 == 0; dst dense and 16-B aligned.
+int kfamd_pad_k_bf16(const void* src0, void* dst0, long long rows0, long long ld0, const void* src1, void* dst1,
+                     long long rows1, long long ld1, int K, int Kp, void* stream);
+
 // Fused linear-backward tail: g = dy * act'(z) (bf16; z = the forward's Aux pre-activation, or its
 // output y for relu), db = column sums of g (fp32, optional). act == NONE: only db = sum over rows of
 // dy (g unused). [rows][cols], cols % 8 == 0, 16-B aligned. workspace: kfamd_act_grad_workspace bytes.

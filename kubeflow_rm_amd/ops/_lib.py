@@ -29,6 +29,13 @@ _SIGNATURES = {
                                            c_float, c_int, c_vp]),
     "kfamd_gemm_bf16_ex": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                    c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_int, c_vp]),
+    "kfamd_w4_splitk_nt": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_ll,
+                                   c_ll, c_ll, c_vp]),
+    "kfamd_w4_splitk_t": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll,
+                                  c_ll, c_ll, c_ll, c_vp]),
+    "kfamd_splitk_reduce": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll,
+                                    c_ll, c_float, c_int, c_vp]),
+    "kfamd_pad_k_bf16": (c_int, [c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_vp]),
     "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
     "kfamd_act_grad_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "kfamd_layernorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),

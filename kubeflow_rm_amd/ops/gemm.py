@@ -28,14 +28,40 @@ def _check_operand(t: torch.Tensor, name: str) -> None:
         raise ValueError(f"{name} must have a contiguous last dimension")
 
 
-# The w4 kernels handle edge tiles in-kernel (gemm_w4.h) for M, N >= 128 with N % 8 == 0 and
-# K % 8 == 0. Other large shapes would run on the generic kernel at a third to a half of the tiled
-# kernels' rate (profiles/r2_gemm_unaligned): above this size they are zero-padded up to the tiles.
+# The w4 kernels handle edge tiles in-kernel (gemm_w4.h) for M, N >= 128 with K % 8 == 0, any N
+# and output alignment (NT layout). K off the 8-grid costs one fused pack of both operands
+# (kfamd_pad_k_bf16); M or N below the tile would run on the generic kernel at a third to a half
+# of the tiled kernels' rate (profiles/r2_gemm_unaligned): above this size they are zero-padded.
 _PAD_MIN_FLOPS = 2.0 * 1024 ** 3
 
 
 def _w4_shape(M: int, N: int, K: int) -> bool:
+    """Every w4 layout and split-K (16-B rows along N too)."""
     return M >= 128 and N >= 128 and N % 8 == 0 and K % 8 == 0
+
+
+def _w4_nt_shape(M: int, N: int, K: int) -> bool:
+    """The NT w4 kernel (any N: the epilogue stores odd widths element-wise)."""
+    return M >= 128 and N >= 128 and K % 8 == 0
+
+
+def pad_k(x: torch.Tensor, y: torch.Tensor | None, Kp: int):
+    """Zero-pad the last dim of one or two bf16 operands to Kp (% 8) in one kernel launch."""
+    outs = []
+    jobs = []
+    for t in (x, y):
+        if t is None:
+            continue
+        t2 = t.reshape(-1, t.shape[-1]) if t.dim() != 2 else t
+        if t2.stride(-1) != 1 or (t.dim() == 3 and t.stride(0) != t.shape[1] * t.stride(1)):
+            t2 = t.contiguous().reshape(-1, t.shape[-1])
+        d = torch.empty(*t.shape[:-1], Kp, dtype=torch.bfloat16, device=t.device)
+        outs.append(d)
+        jobs.append((t2.data_ptr(), d.data_ptr(), t2.shape[0], t2.stride(0)))
+    j1 = jobs[1] if len(jobs) > 1 else (None, None, 0, 0)
+    rc = _lib.lib().kfamd_pad_k_bf16(*jobs[0], *j1, x.shape[-1], Kp, _stream_ptr(x))
+    _lib.check(rc, f"pad_k[{x.shape[-1]}->{Kp}]")
+    return outs[0], (outs[1] if y is not None else None)
 
 
 def _round_up(x: int, m: int) -> int:
@@ -44,8 +70,14 @@ def _round_up(x: int, m: int) -> int:
 
 def _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K):
     """Zero-pad to the tile grid, run the tiled kernel, copy the [M, N] corner into ``out``."""
-    # pad only up to the w4 contract (M, N >= 128, N % 8, K % 8): the kernel handles the rest
-    Mp, Np, Kp = max(M, 128), max(_round_up(N, 8), 128), _round_up(K, 8)
+    Kp = _round_up(K, 8)
+    if M >= 128 and N >= 128:  # only K is off the grid: pack both operands, write out directly
+        ap, bp = pad_k(a3, b, Kp)
+        c3 = out.view(batch, M, N) if batched else out.view(M, N)
+        gemm_nt(ap, bp, bias=bias, residual=residual, alpha=alpha, act=act, out=c3)
+        return out
+    # pad only up to the w4 contract (M, N >= 128, K % 8): the kernel handles the rest
+    Mp, Np = max(M, 128), max(N, 128)
     F = torch.nn.functional
 
     def pad(t, cols, rows):  # copy only an operand that is off the grid (e.g. just B for an odd N)
@@ -110,8 +142,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
         _check_operand(bias, "bias")
         if bias.numel() != N or not bias.is_contiguous():
             raise ValueError("bias must be a contiguous [N] tensor")
-    if (variant == "auto" and not _w4_shape(M, N, K)
-            and flops(M, N, K, batch) >= _PAD_MIN_FLOPS):
+    if (variant == "auto" and not _w4_nt_shape(M, N, K)
+            and ((M >= 128 and N >= 128) or flops(M, N, K, batch) >= _PAD_MIN_FLOPS)):
         return _gemm_nt_padded(a3, b, bias, residual, alpha, act, out, batched, batch, M, N, K)
     r_ptr, ldr, sr = None, 0, 0
     if residual is not None:
@@ -119,6 +151,10 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
         r3 = residual.view(batch, M, N) if batched else residual.reshape(M, N)
         r_ptr, ldr = r3.data_ptr(), r3.stride(-2)
         sr = r3.stride(0) if batched else M * ldr
+    plan = splitk_plan(M, N, K, batch) if variant == "auto" else None
+    if plan is not None and _splitk(0, 0, a3, b, c3, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, bias=bias,
+                                    r_ptr=r_ptr, ldr=ldr, sr=sr, aux=None, alpha=alpha, act=act) == 0:
+        return out
     rc = _lib.lib().kfamd_gemm_nt_bf16_variant(
         VARIANTS[variant], a3.data_ptr(), b.data_ptr(), c3.data_ptr(),
         bias.data_ptr() if bias is not None else None, r_ptr,
@@ -128,12 +164,62 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
     return out
 
 
+# Split-K (kfamd_w4_splitk_*): a w4s block holds a CU (160 KB LDS ring), so a problem with fewer
+# 128x128 output tiles than CUs leaves most of the chip idle. It is split along K until it has about
+# one block per CU, each split at least _SPLITK_MIN_K deep (a shorter K loop is all prologue). Below
+# _SPLITK_MIN_TOTAL_K the unsplit kernel finishes in ~10 us and the extra reduce launch + fp32
+# round trip costs more than it saves (profiles/r3_splitk: 1000^3 10.7 us unsplit vs 15.9 split).
+_NUM_CUS = 256
+_SPLITK_MIN_K = 512
+_SPLITK_MIN_TOTAL_K = 2048
+SPLITK = True  # kill switch (benchmarks/tests compare against the unsplit kernel)
+
+
+def splitk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
+    """(splits, kper) for a w4-shaped problem that under-fills the chip, else None."""
+    if not SPLITK or K < _SPLITK_MIN_TOTAL_K or not _w4_shape(M, N, K):
+        return None
+    tiles = -(-M // 128) * -(-N // 128) * batch
+    want = min(_NUM_CUS // tiles if tiles else 0, K // _SPLITK_MIN_K, 8)
+    if want < 2:
+        return None
+    kper = _round_up(-(-K // want), 64)
+    splits = -(-K // kper)
+    return (splits, kper) if splits >= 2 else None
+
+
+def _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *, bias, r_ptr, ldr, sr, aux,
+            alpha, act) -> int:
+    splits, kper = plan
+    L = _lib.lib()
+    w = torch.empty(splits * batch * M * N, dtype=torch.float32, device=a.device)
+    st = _stream_ptr(a)
+    if la == 0 and lb == 0:
+        rc = L.kfamd_w4_splitk_nt(a.data_ptr(), b.data_ptr(), w.data_ptr(), M, N, K, batch, splits, kper,
+                                  lda, ldb, sa, sb, st)
+    else:
+        rc = L.kfamd_w4_splitk_t(la, lb, a.data_ptr(), b.data_ptr(), w.data_ptr(), M, N, K, batch, splits, kper,
+                                 lda, ldb, sa, sb, st)
+    if rc != 0:
+        return rc
+    return L.kfamd_splitk_reduce(w.data_ptr(), c.data_ptr(), bias.data_ptr() if bias is not None else None, r_ptr,
+                                 aux.data_ptr() if aux is not None else None, M, N, batch, splits, ldc, ldr, sc, sr,
+                                 float(alpha), ACTS[act], st)
+
+
 def _ex(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, *, bias=None, residual=None, aux=None,
         alpha=1.0, act="none") -> int:
-    """Raw kfamd_gemm_bf16_ex call; returns the status (0 = launched)."""
+    """Raw kfamd_gemm_bf16_ex call (split-K when the problem under-fills the chip); returns the status
+    (0 = launched)."""
     r_ptr, ldr, sr = None, 0, 0
     if residual is not None:
         r_ptr, ldr, sr = residual.data_ptr(), residual.stride(-2), (residual.stride(0) if residual.dim() == 3 else 0)
+    plan = splitk_plan(M, N, K, batch)
+    if plan is not None:
+        rc = _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, bias=bias, r_ptr=r_ptr,
+                     ldr=ldr, sr=sr, aux=aux, alpha=alpha, act=act)
+        if rc == 0:
+            return 0
     return _lib.lib().kfamd_gemm_bf16_ex(
         la, lb, a.data_ptr(), b.data_ptr(), c.data_ptr(), bias.data_ptr() if bias is not None else None, r_ptr,
         aux.data_ptr() if aux is not None else None, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr,

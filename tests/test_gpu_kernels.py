@@ -164,21 +164,20 @@ def test_rmsnorm(rows, H):
     assert (wg.grad.float() - wr.grad).abs().max().item() <= 2e-2 * wr.grad.abs().max().item() + 1e-2
 
 
-def test_gemm_w4_needs_16b_output_rows():
-    """The w4 / w4s epilogues store 16 B per lane: an output with ldc % 8 != 0 is refused by the
-    explicit variants and routed to an 8-byte-store kernel by auto (same result)."""
-    from kubeflow_rm_amd.ops import NativeLibraryError, gemm_nt
+def test_gemm_w4_output_rows_off_16b():
+    """An output with ldc % 8 != 0 (rows off the 16-B grid) takes the w4 epilogue's element-wise
+    path on the explicit variants and auto alike (same result, nothing written past the row)."""
+    from kubeflow_rm_amd.ops import gemm_nt
     M = N = K = 512
     a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
     big = torch.zeros(M, N + 4, device="cuda", dtype=torch.bfloat16)
     out = big[:, :N]
-    for v in ("w4", "w4s"):
-        with pytest.raises(NativeLibraryError):
-            gemm_nt(a, b, out=out, variant=v)
-    gemm_nt(a, b, out=out, variant="auto")
     ref = (a.float() @ b.float().t())
-    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
+    for v in ("w4", "w4s", "auto"):
+        out.zero_()
+        gemm_nt(a, b, out=out, variant=v)
+        torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-1)
     assert torch.all(big[:, N:] == 0)  # nothing written past the row
 
 
@@ -207,9 +206,9 @@ def test_gemm_edge_tiles_in_kernel(M, N, K):
     kernels, both tile sizes, with the fused epilogue."""
     from kubeflow_rm_amd.ops import gemm_nt
     a, b, bias = _rand(M, K, seed=41), _rand(N, K, seed=42), _rand(N, seed=43)
-    from kubeflow_rm_amd.ops.gemm import _w4_shape
+    from kubeflow_rm_amd.ops.gemm import _w4_nt_shape
     for v in ("w4", "w4s", "auto"):
-        if v != "auto" and (not _w4_shape(M, N, K) or (v == "w4" and (M < 256 or N < 256))):
+        if v != "auto" and (not _w4_nt_shape(M, N, K) or (v == "w4" and (M < 256 or N < 256))):
             continue  # outside the tiled contract: auto pads up to it
         out = gemm_nt(a, b, bias=bias, act="gelu_tanh", alpha=0.5, variant=v)
         _assert_close(out, _ref_gemm(a, b, bias, "gelu_tanh", alpha=0.5), K)
@@ -319,3 +318,105 @@ def test_linear_backward_layouts(act, shape):
     for got, ref in ((y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (bias.grad, br.grad)):
         err = (got.float() - ref).abs().max().item()
         assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1000, 2056), (1024, 1024, 4096), (1000, 1504, 3080), (136, 128, 2120),
+                                   (512, 768, 8192)])
+def test_splitk_plan_and_numerics(M, N, K):
+    """Split-K (fp32 partials + reduce) for under-filled problems: the plan splits, the result
+    matches fp32 and the last (partial) split is zero-filled, through every operand layout."""
+    from kubeflow_rm_amd.ops import gemm_nt, mm
+    from kubeflow_rm_amd.ops.gemm import splitk_plan
+    splits, kper = splitk_plan(M, N, K)
+    assert splits >= 2 and kper % 64 == 0 and (splits - 1) * kper < K <= splits * kper
+    a, b = _rand(M, K, seed=71), _rand(N, K, seed=72)
+    _assert_close(gemm_nt(a, b), _ref_gemm(a, b), K)
+    for ta, tb in ((True, False), (True, True), (False, True)):
+        aa = a.t().contiguous() if ta else a
+        bb = b if tb else b.t().contiguous()
+        out = mm(aa, bb, trans_a=ta, trans_b=tb)
+        _assert_close(out, _ref_mm(aa, bb, ta, tb), K)
+        ref = _ref_mm(aa, bb, ta, tb, alpha=0.5, residual=out)
+        mm(aa, bb, trans_a=ta, trans_b=tb, out=out, residual=out, alpha=0.5)
+        _assert_close(out, ref, K)
+
+
+@pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
+def test_splitk_epilogues(act):
+    """bias / activation / residual / pre-activation output run in the split-K reduce."""
+    from kubeflow_rm_amd.ops import gemm_nt, gemm_nt_preact
+    from kubeflow_rm_amd.ops.gemm import splitk_plan
+    M, N, K = 384, 512, 2056
+    assert splitk_plan(M, N, K) is not None
+    a, b, bias = _rand(M, K, seed=73), _rand(N, K, seed=74, scale=0.1), _rand(N, seed=75)
+    _assert_close(gemm_nt(a, b, bias=bias, act=act, alpha=0.5), _ref_gemm(a, b, bias, act, alpha=0.5), K)
+    if act == "none":
+        r = _rand(M, N, seed=76)
+        _assert_close(gemm_nt(a, b, bias=bias, residual=r), _ref_gemm(a, b, bias, residual=r), K)
+    if act in ("gelu_tanh", "silu"):
+        y, z = gemm_nt_preact(a, b, bias, act)
+        _assert_close(z, _ref_gemm(a, b, bias), K)
+        _assert_close(y, _ref_gemm(a, b, bias, act), K)
+
+
+def test_splitk_batched_matches_unsplit():
+    from kubeflow_rm_amd.ops import gemm, gemm_nt
+    a, b = _rand(2, 256, 4096, seed=77), _rand(2, 256, 4096, seed=78)
+    assert gemm.splitk_plan(256, 256, 4096, 2) is not None
+    split = gemm_nt(a, b)
+    gemm.SPLITK = False
+    try:
+        whole = gemm_nt(a, b)
+    finally:
+        gemm.SPLITK = True
+    ref = _ref_gemm(a, b)
+    _assert_close(split, ref, 4096)
+    _assert_close(whole, ref, 4096)
+
+
+@pytest.mark.parametrize("M,N,K", [(1500, 1500, 1504), (1000, 1001, 512), (300, 130, 2048), (2000, 1499, 1000)])
+@pytest.mark.parametrize("v", ["w4", "w4s"])
+def test_gemm_odd_output_width(M, N, K, v):
+    """N (and so the shifted edge tile's n0) off the 8-column grid: the element-wise epilogue path,
+    every epilogue (bias, activation, pre-activation output, in-place residual)."""
+    from kubeflow_rm_amd.ops import gemm_nt, gemm_nt_preact
+    if v == "w4" and (M < 256 or N < 256):
+        pytest.skip("256 tile needs M, N >= 256")
+    a, b, bias = _rand(M, K, seed=81), _rand(N, K, seed=82, scale=0.2), _rand(N, seed=83)
+    for act in ("none", "relu", "silu"):
+        _assert_close(gemm_nt(a, b, bias=bias, act=act, alpha=0.5, variant=v),
+                      _ref_gemm(a, b, bias, act, alpha=0.5), K)
+    c = _rand(M, N, seed=84)
+    ref = _ref_gemm(a, b, bias, residual=c)
+    gemm_nt(a, b, bias=bias, residual=c, out=c, variant=v)
+    _assert_close(c, ref, K)
+    y, z = gemm_nt_preact(a, b, bias, "gelu_tanh")
+    _assert_close(z, _ref_gemm(a, b, bias), K)
+    _assert_close(y, _ref_gemm(a, b, bias, "gelu_tanh"), K)
+
+
+def test_gemm_odd_output_stride_leaves_padding():
+    """C as a column slice of a wider buffer (ldc = 1503, rows off 16 B): the odd path writes exactly
+    the [M, N] window."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    M, N, K = 640, 1496, 256
+    a, b = _rand(M, K, seed=85), _rand(N, K, seed=86)
+    big = torch.full((M, 1503), 7.0, device="cuda", dtype=torch.bfloat16)
+    out = big[:, 3:3 + N]
+    gemm_nt(a, b, out=out, variant="w4")
+    _assert_close(out, _ref_gemm(a, b), K)
+    assert torch.all(big[:, :3] == 7.0) and torch.all(big[:, 3 + N:] == 7.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1500, 1500, 1500), (1000, 1000, 1001), (257, 300, 77), (4000, 4000, 3998)])
+def test_gemm_k_off_grid_packed(M, N, K):
+    """K % 8 != 0: both operands packed (zero tail) by one kfamd_pad_k_bf16 launch, then the tiled
+    kernel; also batched."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    from kubeflow_rm_amd.ops.gemm import pad_k
+    a, b, bias = _rand(M, K, seed=87), _rand(N, K, seed=88), _rand(N, seed=89)
+    ap, bp = pad_k(a, b, (K + 7) // 8 * 8)
+    assert torch.equal(ap[:, :K], a) and torch.all(ap[:, K:] == 0) and torch.equal(bp[:, :K], b)
+    _assert_close(gemm_nt(a, b, bias=bias, act="gelu_tanh"), _ref_gemm(a, b, bias, "gelu_tanh"), K)
+    a3, b3 = _rand(2, 256, K, seed=90), _rand(2, 384, K, seed=91)
+    _assert_close(gemm_nt(a3, b3), _ref_gemm(a3, b3), K)

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--variants", default="auto")
     ap.add_argument("--layouts", default="", help="MxNxK list: mm() in all four operand layouts vs torch")
+    ap.add_argument("--splitk", default="", help="MxNxK list: gemm_nt with and without split-K vs torch")
     ap.add_argument("--linear", default="", help="TxKxN list: linear fwd+bwd (gelu, bias) vs torch autograd")
     args = ap.parse_args()
     import torch
@@ -67,6 +68,32 @@ def main():
             d[f"{v}_tflops_median"] = round(fl / sorted(ours[v])[len(ours[v]) // 2] / 1e12, 1)
         if theirs:
             d["torch_tflops"] = round(fl / min(theirs) / 1e12, 1)
+        emit(d)
+        del a, b, c
+        torch.cuda.empty_cache()
+
+    for spec in [x for x in args.splitk.split(",") if x]:
+        from kubeflow_rm_amd.ops import gemm as G
+        M, N, K = map(int, spec.split("x"))
+        fl = 2.0 * M * N * K
+        iters = max(10, min(200, int(2e12 / fl) + 1))
+        a = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        res = {}
+        for tag, on in (("split", True), ("nosplit", False)):
+            G.SPLITK = on
+            for _ in range(3):
+                ops.gemm_nt(a, b, out=c)
+            res[tag] = min(timeit(lambda: ops.gemm_nt(a, b, out=c), iters, dev) for _ in range(args.rounds))
+        G.SPLITK = True
+        for _ in range(3):
+            torch.matmul(a, b.t())
+        res["torch"] = min(timeit(lambda: torch.matmul(a, b.t()), iters, dev) for _ in range(args.rounds))
+        d = {"kind": "gemm_splitk_bf16", "M": M, "N": N, "K": K, "plan": G.splitk_plan(M, N, K)}
+        for k, v in res.items():
+            d[f"{k}_us"] = round(v * 1e6, 1)
+            d[f"{k}_tflops"] = round(fl / v / 1e12, 1)
         emit(d)
         del a, b, c
         torch.cuda.empty_cache()
