@@ -72,7 +72,7 @@
     if (v === null || v === undefined) return "null";
     if (typeof v === "number" || typeof v === "boolean") return String(v);
     const s = String(v);
-    if (s === "" || /^[\s\-?:,\[\]{}#&*!|>'"%@`]|[:#]\s|\s$|^(true|false|null|yes|no|on|off|~)$|^[-+]?[0-9.]+([eE][-+]?[0-9]+)?$/i.test(s) || s.includes("\n"))
+    if (s === "" || /^[\s\-?:,\[\]{}#&*!|>'"%@`]|[:#]\s|\s#|\s$|^(true|false|null|yes|no|on|off|~)$|^[-+]?[0-9.]+([eE][-+]?[0-9]+)?$/i.test(s) || s.includes("\n"))
       return JSON.stringify(s);
     return s;
   }
@@ -98,6 +98,283 @@
       }).join("\n");
     }
     return ind + yamlScalar(v);
+  }
+  // ---- YAML editor (lib-monaco-editor, language "yaml") and loader (js-yaml load as used by the
+  // apps' shared/utils/yaml.ts parseYAML) ---------------------------------------------------------
+  // parseYaml covers the block YAML the apps exchange: mappings, sequences (also compact "- k: v"
+  // items and sequences at their key's indent), plain scalars with the core-schema types, quoted
+  // scalars, one-line flow collections, | and > block scalars, comments and "---". It returns
+  // [value, ""] or [{}, "<reason> (line:column)"]; empty text is [{}, ""] (the reference contract).
+  function yamlError(msg, line, col) { return new Error(`${msg} (${line + 1}:${(col || 0) + 1})`); }
+  function stripComment(s) {
+    let q = null;
+    for (let i = 0; i < s.length; i++) {
+      const c = s[i];
+      if (q) {
+        if (q === '"' && c === "\\") i++;
+        else if (q === "'" && c === "'" && s[i + 1] === "'") i++;
+        else if (c === q) q = null;
+      } else if ((c === '"' || c === "'") && (i === 0 || /[\s[{,:]/.test(s[i - 1]))) q = c;
+      else if (c === "#" && (i === 0 || /\s/.test(s[i - 1]))) return s.slice(0, i).replace(/\s+$/, "");
+    }
+    return s.replace(/\s+$/, "");
+  }
+  function plainScalar(s) {
+    if (s === "" || s === "~" || /^(null|Null|NULL)$/.test(s)) return null;
+    if (/^(true|True|TRUE)$/.test(s)) return true;
+    if (/^(false|False|FALSE)$/.test(s)) return false;
+    if (/^[-+]?[0-9]+$/.test(s)) return parseInt(s, 10);
+    if (/^0x[0-9a-fA-F]+$/.test(s)) return parseInt(s.slice(2), 16);
+    if (/^0o[0-7]+$/.test(s)) return parseInt(s.slice(2), 8);
+    if (/^[-+]?(\.[0-9]+|[0-9]+(\.[0-9]*)?)([eE][-+]?[0-9]+)?$/.test(s)) return parseFloat(s);
+    if (/^[-+]?\.(inf|Inf|INF)$/.test(s)) return s[0] === "-" ? -Infinity : Infinity;
+    if (/^\.(nan|NaN|NAN)$/.test(s)) return NaN;
+    return s;
+  }
+  // a quoted scalar that must span all of s
+  function quotedScalar(s, line, col) {
+    if (s[0] === '"') {
+      const m = s.match(/^"((?:[^"\\]|\\.)*)"$/);
+      if (m) { try { return JSON.parse(`"${m[1].replace(/\\'/g, "'")}"`); } catch (e) { /* below */ } }
+      throw yamlError("bad double-quoted scalar", line, col);
+    }
+    const m = s.match(/^'((?:[^']|'')*)'$/);
+    if (!m) throw yamlError("bad single-quoted scalar", line, col);
+    return m[1].replace(/''/g, "'");
+  }
+  // one-line flow collection: [a, "b", {c: 1}]
+  function flowValue(s, line, col) {
+    let i = 0;
+    const ws = () => { while (i < s.length && /\s/.test(s[i])) i++; };
+    const fail = (what) => yamlError(what, line, col + i);
+    function token(isKey) {
+      ws();
+      if (s[i] === '"' || s[i] === "'") {
+        const q = s[i];
+        let j = i + 1;
+        for (; j < s.length; j++) {
+          if (q === '"' && s[j] === "\\") j++;
+          else if (q === "'" && s[j] === "'" && s[j + 1] === "'") j++;
+          else if (s[j] === q) break;
+        }
+        if (j >= s.length) throw fail("unterminated quoted scalar");
+        const t = s.slice(i, j + 1);
+        i = j + 1;
+        return quotedScalar(t, line, col);
+      }
+      let j = i;
+      while (j < s.length && !/[,\]}]/.test(s[j]) && !(isKey && s[j] === ":")) j++;
+      const t = s.slice(i, j).trim();
+      i = j;
+      return isKey ? t : plainScalar(t);
+    }
+    function value() {
+      ws();
+      if (s[i] === "[" || s[i] === "{") {
+        const seq = s[i] === "[", close = seq ? "]" : "}", out = seq ? [] : {};
+        i++;
+        for (;;) {
+          ws();
+          if (s[i] === close) { i++; return out; }
+          if (seq) out.push(value());
+          else {
+            const k = token(true);
+            ws();
+            let v = null;
+            if (s[i] === ":") { i++; v = value(); }
+            out[k] = v;
+          }
+          ws();
+          if (s[i] === ",") { i++; continue; }
+          if (s[i] === close) { i++; return out; }
+          throw fail(`missed comma between flow collection entries`);
+        }
+      }
+      return token(false);
+    }
+    const v = value();
+    ws();
+    if (i < s.length) throw fail("unexpected characters after a flow collection");
+    return v;
+  }
+  function loadYaml(text) {
+    const raw = String(text).replace(/\r\n?/g, "\n").split("\n");
+    const L = [];
+    raw.forEach((r, n) => {
+      const lead = r.match(/^[ \t]*/)[0];
+      const t = stripComment(r);
+      if (!t.trim() || /^(---|\.\.\.)(\s|$)/.test(t)) return;
+      if (lead.includes("\t")) throw yamlError("tab characters must not be used in indentation", n, lead.indexOf("\t"));
+      L.push({ n, ind: lead.length, t: t.trim() });
+    });
+    if (!L.length) return null;
+    let i = 0;
+    const isSeq = (t) => t === "-" || t.startsWith("- ");
+    const isHeader = (t) => /^[|>][-+]?[0-9]?$/.test(t);
+    // "key: rest" -> [key, rest] (rest "" for a nested node), null when t is no mapping entry
+    function splitKey(t, ln) {
+      let k, j;
+      if (t[0] === '"' || t[0] === "'") {
+        const q = t[0];
+        for (j = 1; j < t.length; j++) {
+          if (q === '"' && t[j] === "\\") j++;
+          else if (q === "'" && t[j] === "'" && t[j + 1] === "'") j++;
+          else if (t[j] === q) break;
+        }
+        const rest = t.slice(j + 1).match(/^\s*:(\s+|$)/);
+        if (!rest) return null;
+        k = quotedScalar(t.slice(0, j + 1), ln.n, ln.ind);
+        return [k, t.slice(j + 1 + rest[0].length).trim()];
+      }
+      if (/^[[{]/.test(t) || isSeq(t)) return null;
+      const m = t.match(/^(.*?):(\s+|$)/);
+      if (!m) return null;
+      return [m[1].trim(), t.slice(m[0].length).trim()];
+    }
+    function scalar(t, ln, col) {
+      if (t[0] === '"' || t[0] === "'") return quotedScalar(t, ln.n, col);
+      if (t[0] === "[" || t[0] === "{") return flowValue(t, ln.n, col);
+      return plainScalar(t);
+    }
+    // | and > content: the raw lines after ln deeper than the parent's indent
+    function blockScalar(header, parentInd, ln) {
+      const lines = [];
+      let last = ln.n, contentInd = -1;
+      for (let n = ln.n + 1; n < raw.length; n++) {
+        const r = raw[n];
+        if (!r.trim()) { lines.push(""); continue; }
+        const ind = r.match(/^ */)[0].length;
+        if (ind <= parentInd) break;
+        if (contentInd < 0) contentInd = ind;
+        if (ind < contentInd) throw yamlError("bad indentation of a block scalar line", n, ind);
+        lines.push(r.slice(contentInd));
+        last = n;
+      }
+      lines.length = Math.max(0, last - ln.n);  // trailing blank lines belong to chomping, not content
+      while (i < L.length && L[i].n <= last) i++;
+      let body;
+      if (header[0] === "|") body = lines.join("\n");
+      else {
+        body = "";
+        lines.forEach((l, k) => {
+          if (k === 0) body = l;
+          else if (l === "") body += "\n";
+          else body += (body.endsWith("\n") || body === "" ? "" : " ") + l;
+        });
+      }
+      const chomp = header.includes("-") ? "" : "\n";
+      return body === "" ? "" : body + chomp;
+    }
+    function node(minInd) {
+      const ln = L[i];
+      if (ln.ind < minInd) return null;
+      if (isSeq(ln.t)) return seq(ln.ind);
+      if (splitKey(ln.t, ln)) return map(ln.ind);
+      i++;
+      return scalar(ln.t, ln, ln.ind);
+    }
+    function child(ind, ln) {  // the nested node of an entry with no inline value
+      if (i < L.length && L[i].ind > ind) return node(L[i].ind);
+      return null;
+    }
+    function seq(ind) {
+      const out = [];
+      while (i < L.length && L[i].ind === ind && isSeq(L[i].t)) {
+        const ln = L[i];
+        const rest = ln.t === "-" ? "" : ln.t.slice(1).trimStart();
+        const col = ind + ln.t.length - rest.length;
+        if (!rest) { i++; out.push(child(ind, ln)); }
+        else if (isSeq(rest) || splitKey(rest, ln)) { L[i] = { n: ln.n, ind: col, t: rest }; out.push(node(col)); }
+        else if (isHeader(rest)) { i++; out.push(blockScalar(rest, ind, ln)); }
+        else { i++; out.push(scalar(rest, ln, col)); }
+      }
+      if (i < L.length && L[i].ind > ind) throw yamlError("bad indentation of a sequence entry", L[i].n, L[i].ind);
+      return out;
+    }
+    function map(ind) {
+      const out = {};
+      while (i < L.length && L[i].ind === ind) {
+        const ln = L[i];
+        const kv = splitKey(ln.t, ln);
+        if (!kv) throw yamlError(isSeq(ln.t) ? "bad indentation of a sequence entry" : "can not read a block mapping entry", ln.n, ln.ind);
+        const [k, rest] = kv;
+        if (Object.prototype.hasOwnProperty.call(out, k)) throw yamlError("duplicated mapping key", ln.n, ln.ind);
+        i++;
+        if (!rest) out[k] = i < L.length && L[i].ind === ind && isSeq(L[i].t) ? seq(ind) : child(ind, ln);
+        else if (isHeader(rest)) out[k] = blockScalar(rest, ind, ln);
+        else out[k] = scalar(rest, ln, ind + ln.t.length - rest.length);
+      }
+      if (i < L.length && L[i].ind > ind) throw yamlError("bad indentation of a mapping entry", L[i].n, L[i].ind);
+      return out;
+    }
+    const v = node(0);
+    if (i < L.length) throw yamlError("end of the stream or a document separator is expected", L[i].n, L[i].ind);
+    return v;
+  }
+  function parseYaml(text) {
+    if (!text) return [{}, ""];
+    try { return [loadYaml(text), ""]; } catch (e) { return [{}, e.message]; }
+  }
+  // token-coloured HTML of YAML text (keys, strings, numbers / booleans / null, comments, dashes)
+  function highlightYaml(text) {
+    return String(text).split("\n").map((line) => {
+      const body = stripComment(line), comment = line.slice(body.length);
+      const m = body.match(/^(\s*(?:- +)*)(.*)$/);
+      let out = esc(m[1]).replace(/-/g, '<span class="y-p">-</span>');
+      let rest = m[2];
+      const kv = rest.match(/^((?:"(?:[^"\\]|\\.)*"|'(?:[^']|'')*'|[^\s"'[{#][^:]*?))(\s*:)(\s+|$)(.*)$/);
+      if (kv) { out += `<span class="y-k">${esc(kv[1])}</span>${esc(kv[2] + kv[3])}`; rest = kv[4]; }
+      const v = rest.trim();
+      if (v) {
+        const cls = /^["']/.test(v) ? "y-s" : /^[[{|>]/.test(v) ? "y-f"
+          : (typeof plainScalar(v) !== "string" ? "y-n" : "y-v");
+        out += `<span class="${cls}">${esc(rest)}</span>`;
+      }
+      return out + (comment.trim() ? `${esc(comment.slice(0, comment.indexOf("#")))}<span class="y-c">${esc(comment.slice(comment.indexOf("#")))}</span>` : esc(comment));
+    }).join("\n");
+  }
+  // static read-only editor markup (gutter + highlight) for tabs that need no interaction
+  function yamlHtml(text, height) {
+    const t = String(text == null ? "" : text);
+    const gutter = Array.from({ length: t.split("\n").length }, (_, k) => k + 1).join("\n");
+    return `<div class="yaml-editor ro" style="height:${Number(height) || 490}px"><pre class="gutter">${gutter}</pre>` +
+      `<div class="code"><pre class="hl">${highlightYaml(t)}\n</pre></div></div>`;
+  }
+  // Editor over a host element: line-number gutter + highlighted text; editable (a textarea laid
+  // over the highlight) unless readOnly. onChange(text, value, error) on every edit; the parse
+  // error shows under the editor (the apps' mat-error "errorParsingYaml").
+  class YamlEditor {
+    constructor(el, opts) {
+      this.el = el;
+      this.opts = opts || {};
+      const ro = !!this.opts.readOnly;
+      el.innerHTML = `<div class="yaml-editor${ro ? " ro" : ""}" style="height:${Number(this.opts.height) || 250}px">` +
+        `<pre class="gutter"></pre><div class="code"><pre class="hl"></pre>${ro ? "" : '<textarea spellcheck="false" wrap="off"></textarea>'}</div></div>` +
+        '<p class="yaml-error err" data-cy="yaml-error"></p>';
+      this.ta = el.querySelector("textarea");
+      if (this.ta) {
+        this.ta.addEventListener("input", () => this.setText(this.ta.value, true));
+        this.ta.addEventListener("keydown", (ev) => {  // Tab indents by two spaces instead of leaving the field
+          if (ev.key !== "Tab" || typeof this.ta.selectionStart !== "number") return;
+          ev.preventDefault();
+          const a = this.ta.selectionStart, b = this.ta.selectionEnd, v = this.ta.value;
+          this.ta.value = v.slice(0, a) + "  " + v.slice(b);
+          this.ta.selectionStart = this.ta.selectionEnd = a + 2;
+          this.setText(this.ta.value, true);
+        });
+      }
+      this.setText(this.opts.text || "", false);
+    }
+    setText(text, fromUser) {
+      this.text = String(text == null ? "" : text);
+      [this.value, this.error] = parseYaml(this.text);
+      const n = this.text.split("\n").length;
+      this.el.querySelector(".gutter").textContent = Array.from({ length: n }, (_, k) => k + 1).join("\n");
+      this.el.querySelector(".hl").innerHTML = highlightYaml(this.text) + "\n";
+      this.el.querySelector(".yaml-error").textContent = this.error;
+      if (this.ta && this.ta.value !== this.text) this.ta.value = this.text;
+      if (fromUser && this.opts.onChange) this.opts.onChange(this.text, this.value, this.error);
+    }
   }
   function eventsTable(events) {
     if (!events || !events.length) return '<p class="muted">No events.</p>';
@@ -464,6 +741,7 @@
   global.kf = { call, Poller, cookie, setNamespace, onNamespace, namespace: () => currentNs, statusCell, h,
                 esc, toYaml, eventsTable, kvTable, details, statusIcon, renderTable, sortedRows, ResourceTable, nameLink,
                 conditionsTable, renderLogs, LogsViewer, validators, parseQuantity, snack, parseFilter, rowMatches,
-                paginate, PAGE_SIZES, quantityToScalar, formatBytes, timeAgo, dateTimeHtml, renderConfirm, confirmDialog };
+                paginate, PAGE_SIZES, quantityToScalar, formatBytes, timeAgo, dateTimeHtml, renderConfirm, confirmDialog,
+                parseYaml, highlightYaml, yamlHtml, YamlEditor };
   if (typeof module !== "undefined" && module.exports) module.exports = global.kf;  // node unit tests
 })(typeof window !== "undefined" ? window : globalThis);

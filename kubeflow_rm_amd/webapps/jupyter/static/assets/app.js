@@ -6,7 +6,9 @@
 // vendor from the admin's vendor list, /api/gpus marks the vendors installed in the cluster: the
 // form-gpus component), workspace volume (name from the {notebook-name} template, size,
 // access mode), data volumes (mount follows the volume name until edited), affinity / toleration
-// groups, PodDefault configurations, shared memory.
+// groups, PodDefault configurations, shared memory. Volumes have the "Custom (Advanced)" type of
+// form-new/volume/{new,existing}: the PVC (or volume source) is edited as YAML in kf.YamlEditor,
+// and the notebook page's YAML tab shows the Notebook or its Pod (pages/notebook-page/yaml).
 //
 // The `JWA` object holds the pure parts (form defaults, limits, volume naming, request body,
 // validation, table columns): node unit-tests them against the reference's Cypress fixtures.
@@ -101,6 +103,34 @@
       return out;
     },
     editMount(vol, mount) { return Object.assign({}, vol, { mount, mountDirty: true }); },
+    // the newPvc / existingSource a volume row describes (what "Custom (Advanced)" starts from)
+    volumeSpec(v) {
+      return v.type === "existing" ? { persistentVolumeClaim: { claimName: v.existing } }
+        : { metadata: { name: v.template || v.name },
+            spec: { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] } };
+    },
+    // typeChanged(CUSTOM): dump the current spec into the editor; back to the plain form drops it
+    toCustom(v) { const spec = JWA.volumeSpec(v); return Object.assign({}, v, { custom: true, yaml: kf.toYaml(spec), spec, yamlError: "" }); },
+    fromCustom(v) { return Object.assign({}, v, { custom: false, yaml: "", spec: undefined, yamlError: "" }); },
+    // set yaml(text): a parse error is shown and keeps the last good spec (the form also refuses
+    // to submit while it is shown, where the reference would send the stale spec)
+    editCustom(v, text) {
+      const [parsed, error] = kf.parseYaml(text);
+      return Object.assign({}, v, { yaml: text, yamlError: error, spec: error ? v.spec : parsed });
+    },
+    kindOptions(v) {
+      const opts = v.type === "existing" ? [["pvc", "Kubernetes Volume"], ["custom", "Custom (Advanced)"]]
+        : [["empty", "Empty volume"], ["custom", "Custom (Advanced)"]];
+      return opts.map(([val, label]) => `<option value="${val}"${(val === "custom") === !!v.custom ? " selected" : ""}>${label}</option>`).join("");
+    },
+    // notebook-page/yaml: the Notebook or its Pod, with the component's placeholder texts
+    yamlTabText(selection, notebook, pod, podRequestCompleted) {
+      if (selection === "pod") {
+        if (pod) return kf.toYaml(pod);
+        return podRequestCompleted ? "No pod available for this notebook." : "Pod information is still being loaded.";
+      }
+      return notebook ? kf.toYaml(notebook) : "No data has been found...";
+    },
     // form-gpus.component.ts: the admin's vendor list; a vendor /api/gpus does not report as
     // installed keeps its option but carries the "no GPUs" tooltip; the vendor control is disabled
     // while the count is "none", and a count needs a vendor (vendorWithNum -> vendorNullName)
@@ -134,8 +164,10 @@
       }
       const ve = JWA.vendorError(f.gpus);
       if (ve) errs.push(ve);
+      if (f.workspace && f.workspace.enabled && f.workspace.custom && f.workspace.yamlError) errs.push(`Workspace volume: ${f.workspace.yamlError}`);
       (f.datavols || []).forEach((d) => {
-        if (d.type === "new" && kf.validators.name(d.name)) errs.push(`Data volume: ${kf.validators.name(d.name)}`);
+        if (d.custom && d.yamlError) errs.push(`Data volume: ${d.yamlError}`);
+        if (d.type === "new" && !d.custom && kf.validators.name(d.name)) errs.push(`Data volume: ${kf.validators.name(d.name)}`);
         if (!String(d.mount || "").startsWith("/")) errs.push(`Data volume mount must be an absolute path: ${d.mount}`);
       });
       return errs;
@@ -143,7 +175,8 @@
     // POST /api/namespaces/<ns>/notebooks body (backend form.py contract)
     buildBody(f, config, namespace) {
       const image = f.serverType === "group-one" ? f.imageGroupOne : f.serverType === "group-two" ? f.imageGroupTwo : f.image;
-      const vol = (v) => (v.type === "existing"
+      const vol = (v) => (v.custom ? (v.type === "existing" ? { mount: v.mount, existingSource: v.spec } : { mount: v.mount, newPvc: v.spec })
+        : v.type === "existing"
         ? { mount: v.mount, existingSource: { persistentVolumeClaim: { claimName: v.existing } } }
         : { mount: v.mount, newPvc: { metadata: { name: v.template || v.name },
                                       spec: { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] } } });
@@ -272,7 +305,7 @@
             ["Last activity", ann["notebooks.kubeflow.org/last-activity"] || "-"],
             ["Cold start (ms)", ann["notebooks.kubeflow.org/cold-start-phases"] || "-"],
             ["Stopped", ann["kubeflow-resource-stopped"] || "no"],
-          ]) + (st.gpuReadiness ? `<h3>GPU readiness op</h3><pre class="yaml">${e(kf.toYaml(st.gpuReadiness))}</pre>` : "") +
+          ]) + (st.gpuReadiness ? `<h3>GPU readiness op</h3>${kf.yamlHtml(kf.toYaml(st.gpuReadiness), 200)}` : "") +
             `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
         } },
         { name: "Events", render: async () => { if (logs) logs.stop(); return kf.eventsTable((await kf.call("GET", `${base}/events`)).events); } },
@@ -285,7 +318,23 @@
           }, 0);
           return `<p class="muted">Pod ${e(pod.metadata.name)} (following)</p><div class="logs-host"></div>`;
         } },
-        { name: "YAML", render: async () => { if (logs) logs.stop(); return `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).notebook))}</pre>`; } },
+        { name: "YAML", render: async () => {
+          if (logs) logs.stop();
+          const nb = (await kf.call("GET", base)).notebook;
+          let pod = null, podDone = false;
+          const podReq = kf.call("GET", `${base}/pod`).then((r) => { pod = r.pod; }, () => {}).then(() => { podDone = true; });
+          setTimeout(() => {
+            const host = document.querySelector("#kf-details .tab-body .yaml-host");
+            const sel = document.querySelector("#kf-details .tab-body select.yaml-which");
+            if (!host || !sel) return;
+            const ed = new kf.YamlEditor(host, { readOnly: true, height: 490, text: JWA.yamlTabText("notebook", nb) });
+            const show = () => ed.setText(JWA.yamlTabText(sel.value, nb, pod, podDone));
+            sel.onchange = show;
+            podReq.then(() => { if (sel.value === "pod") show(); });
+          }, 0);
+          return '<div class="yaml-tab"><p class="message">Show the full YAML of the <select class="yaml-which">' +
+            '<option value="notebook">Notebook</option><option value="pod">Pod</option></select></p><div class="yaml-host"></div></div>';
+        } },
       ]);
     }
 
@@ -298,16 +347,25 @@
     // ---- spawner ----
     function renderDataVolumes() {
       const host = $("f-datavols");
+      const hide = (d, when) => (when || d.custom ? " hidden" : "");
       host.innerHTML = form.datavols.map((d, i) => `<div class="datavol${i === form.datavols.length - 1 ? " last" : ""}" data-cy="data volumes" data-i="${i}">
         <select class="dv-type"><option value="new"${d.type === "new" ? " selected" : ""}>new</option><option value="existing"${d.type === "existing" ? " selected" : ""}>existing</option></select>
-        <input class="dv-name" data-cy="volume name input" value="${kf.esc(d.name)}" size="16"${d.type === "existing" ? " hidden" : ""}>
-        <select class="dv-existing"${d.type === "existing" ? "" : " hidden"}>${(form.pvcs || []).map((p) => `<option${p.name === d.existing ? " selected" : ""}>${kf.esc(p.name)}</option>`).join("")}</select>
-        <input class="dv-size" value="${kf.esc(d.size)}" size="4"${d.type === "existing" ? " hidden" : ""}><span class="muted"${d.type === "existing" ? " hidden" : ""}>Gi</span>
-        <select class="dv-mode"${d.type === "existing" ? " hidden" : ""}>${["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map((m) => `<option${m === d.accessMode ? " selected" : ""}>${m}</option>`).join("")}</select>
-        <input class="dv-mount" data-cy="mount path" value="${kf.esc(d.mount)}" size="20"><button type="button" class="dv-rm">&times;</button></div>`).join("");
+        <select class="dv-kind" title="Custom (Advanced): edit the K8s ${d.type === "existing" ? "volume" : "PVC full"} spec">${JWA.kindOptions(d)}</select>
+        <input class="dv-name" data-cy="volume name input" value="${kf.esc(d.name)}" size="16"${hide(d, d.type === "existing")}>
+        <select class="dv-existing"${hide(d, d.type !== "existing")}>${(form.pvcs || []).map((p) => `<option${p.name === d.existing ? " selected" : ""}>${kf.esc(p.name)}</option>`).join("")}</select>
+        <input class="dv-size" value="${kf.esc(d.size)}" size="4"${hide(d, d.type === "existing")}><span class="muted"${hide(d, d.type === "existing")}>Gi</span>
+        <select class="dv-mode"${hide(d, d.type === "existing")}>${["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map((m) => `<option${m === d.accessMode ? " selected" : ""}>${m}</option>`).join("")}</select>
+        <input class="dv-mount" data-cy="mount path" value="${kf.esc(d.mount)}" size="20"><button type="button" class="dv-rm">&times;</button>
+        ${d.custom ? `<div class="dv-custom"><p class="muted">Check the K8s docs for the supported volumes and their specs</p><div class="dv-yaml"></div></div>` : ""}</div>`).join("");
       host.querySelectorAll(".datavol").forEach((row) => {
         const i = Number(row.dataset.i);
-        row.querySelector(".dv-type").onchange = (ev) => { form.datavols[i].type = ev.target.value; if (ev.target.value === "existing" && form.pvcs && form.pvcs[0]) form.datavols[i].existing = form.pvcs[0].name; renderDataVolumes(); };
+        const yhost = row.querySelector(".dv-yaml");
+        if (yhost) new kf.YamlEditor(yhost, { text: form.datavols[i].yaml, height: 250, onChange: (t) => { form.datavols[i] = JWA.editCustom(form.datavols[i], t); } });
+        row.querySelector(".dv-kind").onchange = (ev) => {
+          form.datavols[i] = ev.target.value === "custom" ? JWA.toCustom(form.datavols[i]) : JWA.fromCustom(form.datavols[i]);
+          renderDataVolumes();
+        };
+        row.querySelector(".dv-type").onchange = (ev) => { form.datavols[i] = JWA.fromCustom(Object.assign(form.datavols[i], { type: ev.target.value })); if (ev.target.value === "existing" && form.pvcs && form.pvcs[0]) form.datavols[i].existing = form.pvcs[0].name; renderDataVolumes(); };
         row.querySelector(".dv-name").oninput = (ev) => { form.datavols[i] = JWA.renameDataVolume(form.datavols[i], ev.target.value); row.querySelector(".dv-mount").value = form.datavols[i].mount; };
         row.querySelector(".dv-existing").onchange = (ev) => { form.datavols[i].existing = ev.target.value; };
         row.querySelector(".dv-size").oninput = (ev) => { form.datavols[i].size = ev.target.value; };
@@ -320,7 +378,11 @@
       const w = form.workspace;
       $("f-ws").checked = !!w.enabled;
       $("f-ws-panel").hidden = !w.enabled;
-      $("f-ws-header").textContent = w.enabled ? (w.type === "existing" ? w.existing : w.name) : "none";
+      $("f-ws-header").textContent = w.enabled ? (w.custom ? "custom" : w.type === "existing" ? w.existing : w.name) : "none";
+      $("f-ws-kind").innerHTML = JWA.kindOptions(w);
+      $("f-ws-fields").hidden = !!w.custom;
+      $("f-ws-custom").hidden = !w.custom;
+      if (w.custom) new kf.YamlEditor($("f-ws-yaml"), { text: w.yaml, height: 250, onChange: (t) => { form.workspace = JWA.editCustom(form.workspace, t); } });
       $("f-ws-name").value = w.name || "";
       $("f-ws-size").value = w.size || "";
       document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.checked = r.value === w.accessMode; });
@@ -373,6 +435,7 @@
       $("f-cpu-limit").oninput = (ev) => { cpuLimitDirty = true; form.cpuLimit = ev.target.value; };
       $("f-mem-limit").oninput = (ev) => { memLimitDirty = true; form.memoryLimit = ev.target.value; };
       $("f-ws").onchange = (ev) => { form.workspace.enabled = ev.target.checked; renderWorkspace(); };
+      $("f-ws-kind").onchange = (ev) => { form.workspace = ev.target.value === "custom" ? JWA.toCustom(form.workspace) : JWA.fromCustom(form.workspace); renderWorkspace(); };
       $("f-ws-name").oninput = (ev) => { form.workspace.name = ev.target.value; form.workspace.template = ev.target.value; $("f-ws-header").textContent = ev.target.value; };
       $("f-ws-size").oninput = (ev) => { form.workspace.size = ev.target.value; };
       document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.onchange = () => { form.workspace.accessMode = r.value; }; });

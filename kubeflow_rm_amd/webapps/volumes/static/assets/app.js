@@ -107,7 +107,7 @@
           if (!pods.length) return '<p class="muted">Not mounted by any pod.</p>';
           return kf.kvTable(pods.map((p) => [p.metadata.name, `${(p.status || {}).phase || ""} on ${(p.spec || {}).nodeName || "-"}`]));
         } },
-        { name: "YAML", render: async () => `<pre class="yaml">${e(kf.toYaml((await kf.call("GET", base)).pvc))}</pre>` },
+        { name: "YAML", render: async () => kf.yamlHtml(kf.toYaml((await kf.call("GET", base)).pvc)) },
       ]);
     }
     function tableConfig() {

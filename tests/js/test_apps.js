@@ -143,6 +143,42 @@ test("JWA form: request body and validation", () => {
   assert.ok(!("shm" in b2) && !("cpu" in b2) && !("cpuLimit" in b2));
 });
 
+test("JWA form: Custom (Advanced) volumes edit the newPvc / existingSource as YAML (form-new/volume)", () => {
+  const cfg = fixture("jupyter", "config").config;
+  const f = JWA.formDefaults(cfg, "my-nb");
+  // typeChanged(CUSTOM) dumps the current PVC into the editor
+  f.workspace = JWA.toCustom(f.workspace);
+  assert.strictEqual(f.workspace.yaml, kf.toYaml(JWA.volumeSpec(JWA.formDefaults(cfg, "my-nb").workspace)));
+  assert.ok(f.workspace.yaml.includes("storage: 20Gi"), f.workspace.yaml);
+  f.workspace = JWA.editCustom(f.workspace, f.workspace.yaml.replace("20Gi", "50Gi") + "\n  storageClassName: fast");
+  const dv = JWA.toCustom(Object.assign(JWA.newDataVolume("my-nb", 1), { type: "existing", existing: "data" }));
+  assert.deepStrictEqual(dv.spec, { persistentVolumeClaim: { claimName: "data" } });
+  f.datavols = [JWA.editCustom(dv, "nfs:\n  server: 10.0.0.1\n  path: /exports")];
+  let b = JWA.buildBody(f, cfg, "team");
+  assert.strictEqual(b.workspace.newPvc.spec.resources.requests.storage, "50Gi");
+  assert.strictEqual(b.workspace.newPvc.spec.storageClassName, "fast");
+  assert.deepStrictEqual(b.datavols[0], { mount: dv.mount, existingSource: { nfs: { server: "10.0.0.1", path: "/exports" } } });
+  assert.deepStrictEqual(JWA.validate(f), []);
+  // a parse error keeps the last good spec and is reported; back to the plain form drops the YAML
+  const broken = JWA.editCustom(f.datavols[0], "nfs:\n  server: a\n   path: b");
+  assert.deepStrictEqual(broken.spec, f.datavols[0].spec);
+  assert.ok(broken.yamlError.startsWith("bad indentation"), broken.yamlError);
+  assert.ok(JWA.validate(Object.assign({}, f, { datavols: [broken] })).some((e) => e.startsWith("Data volume: bad indentation")));
+  const plain = JWA.fromCustom(broken);
+  b = JWA.buildBody(Object.assign({}, f, { datavols: [plain] }), cfg, "team");
+  assert.deepStrictEqual(b.datavols[0].existingSource, { persistentVolumeClaim: { claimName: "data" } });
+  assert.ok(JWA.kindOptions(plain).includes('value="pvc" selected') && JWA.kindOptions(dv).includes('value="custom" selected'));
+});
+
+test("JWA notebook page YAML tab: Notebook or Pod, with the component's placeholder texts", () => {
+  const nb = { metadata: { name: "a" } }, pod = { metadata: { name: "a-0" } };
+  assert.strictEqual(JWA.yamlTabText("notebook", nb), kf.toYaml(nb));
+  assert.strictEqual(JWA.yamlTabText("notebook", null), "No data has been found...");
+  assert.strictEqual(JWA.yamlTabText("pod", nb, null, false), "Pod information is still being loaded.");
+  assert.strictEqual(JWA.yamlTabText("pod", nb, null, true), "No pod available for this notebook.");
+  assert.strictEqual(JWA.yamlTabText("pod", nb, pod, true), kf.toYaml(pod));
+});
+
 test("VWA index page: every PVC name in name order with the reference status icons", () => {
   const pvcs = fixture("volumes", "pvcs").pvcs;
   checkTable(pvcs, VWA.columns(false));

@@ -186,6 +186,82 @@ test("spawner: count back to none sends no vendor requirement", async () => {
   assert.deepStrictEqual(c.body.gpus, { num: "none" });
 });
 
+test("spawner: a Custom (Advanced) data volume is edited as YAML; a parse error blocks the POST", async () => {
+  $("new").click();
+  await settle();
+  type($("f-name"), "yaml-nb");
+  $("f-add-vol").click();
+  const row = () => document.querySelector("#f-datavols .datavol");
+  choose(row().querySelector(".dv-kind"), "custom");
+  const ta = () => row().querySelector(".dv-yaml textarea");
+  assert.ok(ta(), "YAML editor shown for the custom volume");
+  assert.ok(ta().value.includes("name: yaml-nb-datavol-1"), ta().value);  // typeChanged dumps the current PVC
+  assert.ok(row().querySelector(".dv-name").hidden && row().querySelector(".dv-size").hidden);
+  const posts = () => calls.filter((c) => c.method === "POST").length;
+  const text = (ind) => `metadata:\n  name: big\nspec:\n  resources:\n    requests:\n      storage: 100Gi\n${ind}accessModes: [ReadWriteOnce]`;
+  type(ta(), text("   "));
+  assert.ok(row().querySelector(".yaml-error").textContent.startsWith("bad indentation of a mapping entry (7:4)"),
+    row().querySelector(".yaml-error").textContent);
+  const before = posts();
+  $("f-submit").click();
+  await settle();
+  assert.strictEqual(posts(), before, "no POST while the YAML does not parse");
+  assert.ok($("f-error").textContent.includes("Data volume: bad indentation"), $("f-error").textContent);
+  type(ta(), text("  "));
+  assert.strictEqual(row().querySelector(".yaml-error").textContent, "");
+  assert.strictEqual(row().querySelector(".gutter").textContent, "1\n2\n3\n4\n5\n6\n7");
+  assert.ok(row().querySelector(".hl").innerHTML.includes('<span class="y-k">storage</span>'));
+  $("f-submit").click();
+  await settle();
+  const c = lastCall("POST");
+  assert.strictEqual(c.body.name, "yaml-nb");
+  assert.deepStrictEqual(c.body.datavols[0].newPvc,
+    { metadata: { name: "big" }, spec: { resources: { requests: { storage: "100Gi" } }, accessModes: ["ReadWriteOnce"] } });
+});
+
+test("spawner: the workspace volume's Custom (Advanced) type sends the edited PVC", async () => {
+  $("new").click();
+  await settle();
+  type($("f-name"), "ws-nb");
+  choose($("f-ws-kind"), "custom");
+  assert.ok($("f-ws-fields").hidden && !$("f-ws-custom").hidden);
+  const ta = $("f-ws-yaml").querySelector("textarea");
+  assert.ok(ta.value.includes("storage: 20Gi"), ta.value);
+  type(ta, ta.value.replace("20Gi", "64Gi"));
+  $("f-submit").click();
+  await settle();
+  const c = lastCall("POST");
+  assert.strictEqual(c.body.name, "ws-nb");
+  assert.strictEqual(c.body.workspace.newPvc.spec.resources.requests.storage, "64Gi");
+  choose($("f-ws-kind"), "empty");
+  assert.ok(!$("f-ws-fields").hidden && $("f-ws-custom").hidden);
+});
+
+test("notebook page YAML tab: Notebook / Pod select over a read-only editor (notebook-page/yaml)", async () => {
+  const nb = byPhase("ready");
+  const base = `api/namespaces/${nsOf(nb)}/notebooks/${nb.name}`;
+  overrides[`GET ${base}`] = { success: true, notebook: { apiVersion: "kubeflow.org/v1", kind: "Notebook", metadata: { name: nb.name } } };
+  overrides[`GET ${base}/pod`] = { success: true, pod: { kind: "Pod", metadata: { name: `${nb.name}-0` } } };
+  const link = document.querySelectorAll("#notebooks a.name").find((a) => a.getAttribute("data-open").split("/").pop() === nb.name);
+  link.click();
+  await settle();
+  const dlg = $("kf-details");
+  assert.ok(dlg && dlg.open, "details open");
+  dlg.querySelectorAll("nav.tabs button[data-tab]").find((b) => b.textContent === "YAML").click();
+  await settle();
+  await new Promise((r) => realSetTimeout(r, 5));
+  await settle();
+  const body = dlg.querySelector(".tab-body");
+  assert.ok(body.textContent.includes("Show the full YAML of the"));
+  assert.ok(body.querySelector(".yaml-editor.ro") && !body.querySelector("textarea"), "read-only editor");
+  assert.ok(body.querySelector(".hl").textContent.includes("kind: Notebook"), body.querySelector(".hl").textContent);
+  choose(body.querySelector("select.yaml-which"), "pod");
+  assert.ok(body.querySelector(".hl").textContent.includes(`name: ${nb.name}-0`));
+  choose(body.querySelector("select.yaml-which"), "notebook");
+  assert.ok(body.querySelector(".hl").textContent.includes("kind: Notebook"));
+  dlg.querySelector("button[data-close]").click();
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {

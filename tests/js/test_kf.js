@@ -82,6 +82,71 @@ test("events table sorts newest first", () => {
   assert.ok(kf.eventsTable([]).includes("No events"));
 });
 
+test("parseYaml: the block YAML the apps exchange (js-yaml load semantics)", () => {
+  const [v, err] = kf.parseYaml([
+    "apiVersion: v1",
+    "kind: PersistentVolumeClaim   # trailing comment",
+    "metadata:",
+    '  name: "{notebook-name}-data"',
+    "  labels: {app: x, n: 3, 'q': [a, \"b\"]}",
+    "spec:",
+    "  accessModes:",
+    "  - ReadWriteOnce",       // sequence at its key's indent
+    "  resources:",
+    "    requests:",
+    "      storage: 20Gi",
+    "  items:",
+    "    - name: a",          // compact mapping items
+    "      value: 1.5",
+    "    -",
+    "      - nested",
+    "  script: |",
+    "    echo hi",
+    "",
+    "    exit 0",
+    "  folded: >-",
+    "    a b",
+    "    c",
+    "  empty:",
+    "  quoted: 'it''s # not a comment'",
+    "  flags: [true, false, null, ~, 0x1f, -3, .inf]",
+    "---",
+  ].join("\n"));
+  assert.strictEqual(err, "");
+  assert.deepStrictEqual(v, {
+    apiVersion: "v1", kind: "PersistentVolumeClaim",
+    metadata: { name: "{notebook-name}-data", labels: { app: "x", n: 3, q: ["a", "b"] } },
+    spec: { accessModes: ["ReadWriteOnce"], resources: { requests: { storage: "20Gi" } },
+            items: [{ name: "a", value: 1.5 }, ["nested"]], script: "echo hi\n\nexit 0\n", folded: "a b c",
+            empty: null, quoted: "it's # not a comment", flags: [true, false, null, null, 31, -3, Infinity] },
+  });
+  assert.deepStrictEqual(kf.parseYaml(""), [{}, ""]);
+  assert.deepStrictEqual(kf.parseYaml("- a\n- b: 1\n  c: 2"), [["a", { b: 1, c: 2 }], ""]);
+});
+
+test("parseYaml: errors carry the reason and line:column, value {} (parseYAML contract)", () => {
+  assert.deepStrictEqual(kf.parseYaml("a: 1\n  b: 2"), [{}, "bad indentation of a mapping entry (2:3)"]);
+  assert.deepStrictEqual(kf.parseYaml("a: 1\na: 2"), [{}, "duplicated mapping key (2:1)"]);
+  assert.deepStrictEqual(kf.parseYaml("a:\n\t- x"), [{}, "tab characters must not be used in indentation (2:1)"]);
+  assert.ok(kf.parseYaml("a: [1, 2").at === undefined && kf.parseYaml("a: [1, 2")[1].startsWith("missed comma"));
+  assert.ok(kf.parseYaml('a: "x\\q').at === undefined && kf.parseYaml('a: "x')[1].startsWith("bad double-quoted scalar"));
+  assert.ok(kf.parseYaml("a: 1\n- b")[1].startsWith("bad indentation of a sequence entry"));
+});
+
+test("toYaml -> parseYaml round-trips API objects (quoting of numeric / boolean strings)", () => {
+  const o = { metadata: { name: "nb", annotations: { "notebooks.kubeflow.org/last-activity": "2024-01-01T00:00:00Z", b: "true", n: "1.0", e: "" } },
+              spec: { template: { spec: { containers: [{ name: "c", args: ["--port", "8888"], env: [], resources: { limits: { "amd.com/gpu": 2 } } }] } } },
+              status: { conditions: [], readyReplicas: 1, msg: "two\nlines", colon: "a: b", hash: "x #y" } };
+  assert.deepStrictEqual(kf.parseYaml(kf.toYaml(o)), [o, ""]);
+});
+
+test("highlightYaml: keys, strings, numbers, comments and dashes as token spans", () => {
+  const h = kf.highlightYaml('a: "x" # c\n- 3\nb: <tag>');
+  assert.ok(h.includes('<span class="y-k">a</span>: <span class="y-s">&quot;x&quot;</span> <span class="y-c"># c</span>'), h);
+  assert.ok(h.includes('<span class="y-p">-</span> <span class="y-n">3</span>'), h);
+  assert.ok(h.includes('<span class="y-v">&lt;tag&gt;</span>'), h);  // escaped
+});
+
 (async () => {
   let failed = 0;
   for (const [name, fn] of tests) {
