@@ -720,6 +720,21 @@
     });
   }
 
+  // an information dialog: heading (+ sub-heading), arbitrary content, one CLOSE button
+  function infoDialog(heading, subHeading, html, width) {
+    const dlg = document.createElement("dialog");
+    dlg.className = "info";
+    if (width) dlg.style.width = width;
+    document.body.append(dlg);
+    dlg.innerHTML = `<h2 class="dialog-title">${esc(heading)} <span class="muted">${esc(subHeading || "")}</span></h2>` +
+      `<div class="dialog-content">${html}</div><div class="dialog-actions"><button data-resp="close">CLOSE</button></div>`;
+    const done = () => { dlg.close(); dlg.remove(); };
+    dlg.querySelector('button[data-resp="close"]').onclick = done;
+    dlg.addEventListener("cancel", done);
+    dlg.showModal();
+    return dlg;
+  }
+
   // ---- snack bar ------------------------------------------------------------------------------
   function snack(message, status) {
     let el = document.getElementById("kf-snack");
@@ -741,7 +756,7 @@
   global.kf = { call, Poller, cookie, setNamespace, onNamespace, namespace: () => currentNs, statusCell, h,
                 esc, toYaml, eventsTable, kvTable, details, statusIcon, renderTable, sortedRows, ResourceTable, nameLink,
                 conditionsTable, renderLogs, LogsViewer, validators, parseQuantity, snack, parseFilter, rowMatches,
-                paginate, PAGE_SIZES, quantityToScalar, formatBytes, timeAgo, dateTimeHtml, renderConfirm, confirmDialog,
+                paginate, PAGE_SIZES, quantityToScalar, formatBytes, timeAgo, dateTimeHtml, renderConfirm, confirmDialog, infoDialog,
                 parseYaml, highlightYaml, yamlHtml, YamlEditor };
   if (typeof module !== "undefined" && module.exports) module.exports = global.kf;  // node unit tests
 })(typeof window !== "undefined" ? window : globalThis);

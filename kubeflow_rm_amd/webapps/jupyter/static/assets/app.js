@@ -84,6 +84,8 @@
           enabled: true, type: ws.existingSource ? "existing" : "new", template: (pvc.metadata || {}).name || "{notebook-name}-workspace",
           name: JWA.volumeName((pvc.metadata || {}).name || "{notebook-name}-workspace", notebookName),
           size: size.size, unit: size.unit, accessMode: ((pvc.spec || {}).accessModes || ["ReadWriteOnce"])[0],
+          // volume/new/storage-class: "Use default class" unless the admin's PVC names a class
+          useDefaultSC: !("storageClassName" in (pvc.spec || {})), storageClass: (pvc.spec || {}).storageClassName || "",
           mount: ws.mount || HOME, existing: ((ws.existingSource || {}).persistentVolumeClaim || {}).claimName || "",
         } : { enabled: false },
         datavols: [],
@@ -95,7 +97,8 @@
     // a new data volume row; its mount tracks the name until the user types in the mount field
     newDataVolume(notebookName, index) {
       const name = `${notebookName || ""}-datavol-${index}`;
-      return { type: "new", name, size: "5", unit: "Gi", accessMode: "ReadWriteOnce", mount: JWA.mountFor(name), mountDirty: false, existing: "" };
+      return { type: "new", name, size: "5", unit: "Gi", accessMode: "ReadWriteOnce", mount: JWA.mountFor(name), mountDirty: false, existing: "",
+               useDefaultSC: true, storageClass: "" };
     },
     renameDataVolume(vol, name) {
       const out = Object.assign({}, vol, { name });
@@ -105,9 +108,18 @@
     editMount(vol, mount) { return Object.assign({}, vol, { mount, mountDirty: true }); },
     // the newPvc / existingSource a volume row describes (what "Custom (Advanced)" starts from)
     volumeSpec(v) {
-      return v.type === "existing" ? { persistentVolumeClaim: { claimName: v.existing } }
-        : { metadata: { name: v.template || v.name },
-            spec: { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] } };
+      if (v.type === "existing") return { persistentVolumeClaim: { claimName: v.existing } };
+      const spec = { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] };
+      // a disabled storage-class control (use the default) leaves the field out of the PVC
+      if (v.useDefaultSC === false) spec.storageClassName = v.storageClass || "";
+      return { metadata: { name: v.template || v.name }, spec };
+    },
+    // the class select: "Empty storage class" (value "") and the cluster's classes; while "Use
+    // default class" is ticked it is disabled and shows the default
+    storageClassOptions(classes, v, defaultClass) {
+      const cur = v.useDefaultSC === false ? (v.storageClass || "") : (defaultClass || "");
+      return [`<option value=""${cur === "" ? " selected" : ""}>Empty storage class</option>`]
+        .concat((classes || []).map((c) => `<option value="${kf.esc(c)}"${c === cur ? " selected" : ""}>${kf.esc(c)}</option>`)).join("");
     },
     // typeChanged(CUSTOM): dump the current spec into the editor; back to the plain form drops it
     toCustom(v) { const spec = JWA.volumeSpec(v); return Object.assign({}, v, { custom: true, yaml: kf.toYaml(spec), spec, yamlError: "" }); },
@@ -176,10 +188,7 @@
     buildBody(f, config, namespace) {
       const image = f.serverType === "group-one" ? f.imageGroupOne : f.serverType === "group-two" ? f.imageGroupTwo : f.image;
       const vol = (v) => (v.custom ? (v.type === "existing" ? { mount: v.mount, existingSource: v.spec } : { mount: v.mount, newPvc: v.spec })
-        : v.type === "existing"
-        ? { mount: v.mount, existingSource: { persistentVolumeClaim: { claimName: v.existing } } }
-        : { mount: v.mount, newPvc: { metadata: { name: v.template || v.name },
-                                      spec: { resources: { requests: { storage: `${v.size}${v.unit}` } }, accessModes: [v.accessMode] } } });
+        : v.type === "existing" ? { mount: v.mount, existingSource: JWA.volumeSpec(v) } : { mount: v.mount, newPvc: JWA.volumeSpec(v) });
       const body = {
         name: f.name, namespace, serverType: f.serverType,
         image: f.customImage ? f.customImage.trim() : image, customImage: !!f.customImage,
@@ -199,6 +208,113 @@
       if (((config || {}).cpu || {}).readOnly) delete body.cpuLimit;
       if (((config || {}).memory || {}).readOnly) delete body.memoryLimit;
       return body;
+    },
+    // ---- notebook page overview (notebook-page/overview): the main container's requests and
+    // limits, type, creator, shared memory, volumes grouped by kind, the PodDefault
+    // "configurations" the notebook's labels select, and the env grouped by where it came from
+    mainContainer(nb) {
+      const cs = ((((nb || {}).spec || {}).template || {}).spec || {}).containers || [];
+      return cs.find((c) => c.name === ((nb || {}).metadata || {}).name) || null;
+    },
+    overview(nb) {
+      const ann = ((nb || {}).metadata || {}).annotations || {};
+      const c = JWA.mainContainer(nb);
+      const res = (c || {}).resources || {};
+      const vols = ((((nb || {}).spec || {}).template || {}).spec || {}).volumes;
+      const type = ann["notebooks.kubeflow.org/server-type"];
+      return {
+        notebookType: !type ? "empty" : ({ "group-two": "RStudio", "group-one": "VSCode", jupyter: "JupyterLab" }[type] || type),
+        sharedMemory: !vols ? "null" : vols.some((v) => v.name === "dshm") ? "Yes" : "No",
+        notebookCreator: ann["notebooks.kubeflow.org/creator"] || null,
+        cpuRequests: (res.requests || {}).cpu || null, cpuLimits: (res.limits || {}).cpu || null,
+        memoryRequests: (res.requests || {}).memory || null, memoryLimits: (res.limits || {}).memory || null,
+        dockerImage: (c || {}).image || null,
+      };
+    },
+    VOLUME_GROUPS: {
+      PersistentVolumeClaims: ["Storage claimed from a PersistentVolume: it outlives the pod, with a requested size and access mode.",
+        "https://kubernetes.io/docs/concepts/storage/persistent-volumes/"],
+      "Memory-backed Volumes": ["An emptyDir on tmpfs: fast, counted against the container's memory limit, gone with the pod.",
+        "https://kubernetes.io/docs/concepts/storage/volumes/#emptydir"],
+      Ephemerals: ["An emptyDir: scratch space created empty with the pod on its node and deleted with it.",
+        "https://kubernetes.io/docs/concepts/storage/volumes/#emptydir"],
+      ConfigMaps: ["Configuration data from a ConfigMap, mounted as files.", "https://kubernetes.io/docs/concepts/storage/volumes/#configmap"],
+      Secrets: ["Sensitive data from a Secret, mounted as files on tmpfs.", "https://kubernetes.io/docs/concepts/storage/volumes/#secret"],
+      "Other Volumes": ["", "https://kubernetes.io/docs/concepts/storage/volumes"],
+    },
+    classifyVolume(v) {
+      if (v.persistentVolumeClaim) return "PersistentVolumeClaims";
+      if (v.emptyDir && v.emptyDir.medium === "Memory") return "Memory-backed Volumes";
+      if (v.emptyDir) return "Ephemerals";
+      if (v.configMap) return "ConfigMaps";
+      if (v.secret) return "Secrets";
+      return "Other Volumes";
+    },
+    // [{name, info, url, items: [{name, url?}]}], PVCs first (links to the volumes app's details)
+    volGroups(nb) {
+      const groups = [];
+      const ns = ((nb || {}).metadata || {}).namespace;
+      (((((nb || {}).spec || {}).template || {}).spec || {}).volumes || []).forEach((v) => {
+        const name = JWA.classifyVolume(v);
+        const item = name === "PersistentVolumeClaims" ? { name: v.name, url: `/volumes/volume/details/${ns}/${v.name}` } : { name: v.name };
+        let g = groups.find((x) => x.name === name);
+        if (!g) {
+          const [info, url] = JWA.VOLUME_GROUPS[name];
+          g = { name, info, url, items: [] };
+          if (name === "PersistentVolumeClaims") groups.unshift(g); else groups.push(g);
+        }
+        g.items.push(item);
+      });
+      return groups;
+    },
+    // PodDefaults whose (first) selector label the notebook carries
+    configurations(nb, podDefaults) {
+      const labels = Object.keys(((nb || {}).metadata || {}).labels || {});
+      return (podDefaults || []).filter((pd) => labels.includes(Object.keys((((pd.spec || {}).selector || {}).matchLabels) || {})[0]))
+        .map((pd) => ({ name: pd.metadata.name, Description: pd.spec.desc, Selector: pd.spec.selector, Env: pd.spec.env,
+                        Volumes: pd.spec.volumes, VolumeMounts: pd.spec.volumeMounts, ServiceAccountName: pd.spec.serviceAccountName }));
+    },
+    podDefaultsMessage(podRequestCompleted, configurations) {
+      return podRequestCompleted === true && !(configurations || []).length ? "No configurations available for this notebook." : "";
+    },
+    // configuration-info-dialog: the configuration minus its name, as YAML
+    configurationYaml(config) {
+      if (!config) return "No information available about the configuration";
+      const c = Object.assign({}, config);
+      delete c.name;
+      Object.keys(c).forEach((k) => { if (c[k] === undefined) delete c[k]; });
+      return kf.toYaml(c);
+    },
+    // env chips: "Notebook CR" (the CR's own env), then per PodDefault "(Configuration)" and "Other"
+    // for what the pod has beyond the CR; valueFrom.fieldRef resolves against the pod
+    envGroups(nb, pod, podDefaults) {
+      const chip = (e, obj) => {
+        if (e.value) return `${e.name}: ${e.value}`;
+        if (e.valueFrom && e.valueFrom.fieldRef) {
+          const v = e.valueFrom.fieldRef.fieldPath.split(".").reduce((o, k) => (o == null ? undefined : o[k]), obj);
+          return `${e.name}: ${v}`;
+        }
+        return `${e.name}: undefined`;
+      };
+      const groups = [];
+      const c = JWA.mainContainer(nb);
+      const crChips = c && c.env ? c.env.map((e) => chip(e, pod)) : [];
+      if (c && c.env) groups.push({ name: "Notebook CR", chips: crChips });
+      if (pod && podDefaults) {
+        const pc = ((pod.spec || {}).containers || []).find((x) => x.name === ((pod.metadata || {}).labels || {})["notebook-name"]);
+        if (pc && pc.env) {
+          const pdGroups = podDefaults.map((pd) => ({ name: `${pd.metadata.name} (Configuration)`, pd, chips: [] }));
+          const other = { name: "Other", chips: [] };
+          pc.env.forEach((e) => {
+            const v = chip(e, pod);
+            if (crChips.includes(v)) return;
+            const g = pdGroups.find((x) => (((x.pd.spec || {}).env) || []).some((pe) => pe.name === e.name)) || other;
+            if (!g.chips.includes(v)) g.chips.push(v);
+          });
+          pdGroups.concat([other]).forEach((g) => { if (g.chips.length) groups.push({ name: g.name, chips: g.chips }); });
+        }
+      }
+      return groups;
     },
     // the union of several namespaces' notebook lists (all-namespaces view)
     merge(lists) { return [].concat(...lists); },
@@ -288,24 +404,44 @@
         { name: "Overview", render: async () => {
           if (logs) logs.stop();
           const nb = (await kf.call("GET", base)).notebook;
+          let pod = null, podDone = false, pds = null;
+          try { pod = (await kf.call("GET", `${base}/pod`)).pod; } catch (err) { /* no pod (stopped or starting) */ }
+          podDone = true;
+          try { pds = (await kf.call("GET", `/api/namespaces/${ns}/poddefaults`)).poddefaults; } catch (err) { pds = []; }
+          const ov = JWA.overview(nb);
           const spec = ((nb.spec || {}).template || {}).spec || {};
-          const c = (spec.containers || [])[0] || {};
-          const lim = (c.resources || {}).limits || {}, req = (c.resources || {}).requests || {};
+          const lim = ((JWA.mainContainer(nb) || {}).resources || {}).limits || {};
           const ann = (nb.metadata || {}).annotations || {};
           const st = nb.status || {};
-          return kf.kvTable([
-            ["Name", nb.metadata.name], ["Namespace", nb.metadata.namespace],
-            ["Created", nb.metadata.creationTimestamp], ["Image", c.image],
-            ["Server type", ann["notebooks.kubeflow.org/server-type"] || "jupyter"],
-            ["CPU (request / limit)", `${req.cpu || "-"} / ${lim.cpu || "-"}`],
-            ["Memory (request / limit)", `${req.memory || "-"} / ${lim.memory || "-"}`],
-            ["MI355X GPUs", lim["amd.com/gpu"] || "0"], ["Allocated GPU ids", st.gpus || "-"],
-            ["Volumes", (spec.volumes || []).map((v) => v.name).join(", ")],
-            ["Ready replicas", st.readyReplicas || 0],
-            ["Last activity", ann["notebooks.kubeflow.org/last-activity"] || "-"],
-            ["Cold start (ms)", ann["notebooks.kubeflow.org/cold-start-phases"] || "-"],
-            ["Stopped", ann["kubeflow-resource-stopped"] || "no"],
-          ]) + (st.gpuReadiness ? `<h3>GPU readiness op</h3>${kf.yamlHtml(kf.toYaml(st.gpuReadiness), 200)}` : "") +
+          const configs = JWA.configurations(nb, pds);
+          setTimeout(() => {
+            document.querySelectorAll("#kf-details .tab-body button.config-link").forEach((b) => {
+              b.onclick = () => {  // configuration-info-dialog
+                const cfg = configs[Number(b.dataset.i)];
+                kf.infoDialog(`${cfg.name}: `, cfg.Description, kf.yamlHtml(JWA.configurationYaml(cfg), 280), "600px");
+              };
+            });
+          }, 0);
+          const rows = [["Name", nb.metadata.name], ["Namespace", nb.metadata.namespace], ["Created", nb.metadata.creationTimestamp],
+            ["Type", ov.notebookType], ["Shared memory enabled", ov.sharedMemory]];
+          if (ov.notebookCreator) rows.push(["Notebook creator", ov.notebookCreator]);
+          for (const [k, v] of [["Minimum CPU", ov.cpuRequests], ["Maximum CPU", ov.cpuLimits], ["Minimum memory", ov.memoryRequests], ["Maximum memory", ov.memoryLimits]])
+            if (v) rows.push([k, v]);
+          rows.push(["Image", ov.dockerImage], ["MI355X GPUs", lim["amd.com/gpu"] || "0"], ["Allocated GPU ids", st.gpus || "-"],
+            ["Ready replicas", st.readyReplicas || 0], ["Last activity", ann["notebooks.kubeflow.org/last-activity"] || "-"],
+            ["Cold start (ms)", ann["notebooks.kubeflow.org/cold-start-phases"] || "-"], ["Stopped", ann["kubeflow-resource-stopped"] || "no"]);
+          const groups = JWA.volGroups(nb);
+          const volHtml = groups.length ? groups.map((g) => `<div class="vol-group"><b title="${e(g.info + (g.info ? " " : "") + "Read more at " + g.url)}">${e(g.name)}</b> ` +
+            g.items.map((i) => (i.url ? `<a class="vol-link" href="${e(i.url)}">${e(i.name)}</a>` : `<span class="chip">${e(i.name)}</span>`)).join(" ") + "</div>").join("")
+            : '<p class="muted">No volumes available for this notebook.</p>';
+          const cfgHtml = configs.map((c, i) => `<button type="button" class="config-link lib-link" data-i="${i}">${e(c.name)}</button>`).join(" ") +
+            `<span class="muted">${e(JWA.podDefaultsMessage(podDone, configs))}</span>`;
+          const env = JWA.envGroups(nb, pod, pds);
+          const envHtml = env.length ? env.map((g) => `<div class="env-group"><b>${e(g.name)}</b> ${g.chips.map((c) => `<span class="chip">${e(c)}</span>`).join(" ")}</div>`).join("")
+            : '<p class="muted">No environment variables available for this notebook.</p>';
+          return kf.kvTable(rows) + `<h3>Volumes</h3>${volHtml}<h3>Configurations</h3><div class="configurations">${cfgHtml}</div>` +
+            `<h3>Environment</h3>${envHtml}` +
+            (st.gpuReadiness ? `<h3>GPU readiness op</h3>${kf.yamlHtml(kf.toYaml(st.gpuReadiness), 200)}` : "") +
             `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
         } },
         { name: "Events", render: async () => { if (logs) logs.stop(); return kf.eventsTable((await kf.call("GET", `${base}/events`)).events); } },
@@ -355,6 +491,8 @@
         <select class="dv-existing"${hide(d, d.type !== "existing")}>${(form.pvcs || []).map((p) => `<option${p.name === d.existing ? " selected" : ""}>${kf.esc(p.name)}</option>`).join("")}</select>
         <input class="dv-size" value="${kf.esc(d.size)}" size="4"${hide(d, d.type === "existing")}><span class="muted"${hide(d, d.type === "existing")}>Gi</span>
         <select class="dv-mode"${hide(d, d.type === "existing")}>${["ReadWriteOnce", "ReadWriteMany", "ReadOnlyMany"].map((m) => `<option${m === d.accessMode ? " selected" : ""}>${m}</option>`).join("")}</select>
+        <label class="muted"${hide(d, d.type === "existing")}><input type="checkbox" class="dv-sc-default"${d.useDefaultSC !== false ? " checked" : ""}> Use default class</label>
+        <select class="dv-sc" title="Storage class"${hide(d, d.type === "existing")}${d.useDefaultSC !== false ? " disabled" : ""}>${JWA.storageClassOptions(form.storageClasses, d, form.defaultStorageClass)}</select>
         <input class="dv-mount" data-cy="mount path" value="${kf.esc(d.mount)}" size="20"><button type="button" class="dv-rm">&times;</button>
         ${d.custom ? `<div class="dv-custom"><p class="muted">Check the K8s docs for the supported volumes and their specs</p><div class="dv-yaml"></div></div>` : ""}</div>`).join("");
       host.querySelectorAll(".datavol").forEach((row) => {
@@ -370,6 +508,8 @@
         row.querySelector(".dv-existing").onchange = (ev) => { form.datavols[i].existing = ev.target.value; };
         row.querySelector(".dv-size").oninput = (ev) => { form.datavols[i].size = ev.target.value; };
         row.querySelector(".dv-mode").onchange = (ev) => { form.datavols[i].accessMode = ev.target.value; };
+        row.querySelector(".dv-sc-default").onchange = (ev) => { form.datavols[i].useDefaultSC = ev.target.checked; renderDataVolumes(); };
+        row.querySelector(".dv-sc").onchange = (ev) => { form.datavols[i].storageClass = ev.target.value; };
         row.querySelector(".dv-mount").oninput = (ev) => { form.datavols[i] = JWA.editMount(form.datavols[i], ev.target.value); };
         row.querySelector(".dv-rm").onclick = () => { form.datavols.splice(i, 1); renderDataVolumes(); };
       });
@@ -385,6 +525,9 @@
       if (w.custom) new kf.YamlEditor($("f-ws-yaml"), { text: w.yaml, height: 250, onChange: (t) => { form.workspace = JWA.editCustom(form.workspace, t); } });
       $("f-ws-name").value = w.name || "";
       $("f-ws-size").value = w.size || "";
+      $("f-ws-sc-default").checked = w.useDefaultSC !== false;
+      $("f-ws-sc").innerHTML = JWA.storageClassOptions(form.storageClasses, w, form.defaultStorageClass);
+      $("f-ws-sc").disabled = w.useDefaultSC !== false;
       document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.checked = r.value === w.accessMode; });
     }
     function fillSpawner() {
@@ -438,6 +581,8 @@
       $("f-ws-kind").onchange = (ev) => { form.workspace = ev.target.value === "custom" ? JWA.toCustom(form.workspace) : JWA.fromCustom(form.workspace); renderWorkspace(); };
       $("f-ws-name").oninput = (ev) => { form.workspace.name = ev.target.value; form.workspace.template = ev.target.value; $("f-ws-header").textContent = ev.target.value; };
       $("f-ws-size").oninput = (ev) => { form.workspace.size = ev.target.value; };
+      $("f-ws-sc-default").onchange = (ev) => { form.workspace.useDefaultSC = ev.target.checked; if (!ev.target.checked) form.workspace.storageClass = $("f-ws-sc").value; renderWorkspace(); };
+      $("f-ws-sc").onchange = (ev) => { form.workspace.storageClass = ev.target.value; };
       document.querySelectorAll('input[name="f-ws-mode"]').forEach((r) => { r.onchange = () => { form.workspace.accessMode = r.value; }; });
       $("f-add-vol").onclick = () => { form.datavols.push(JWA.newDataVolume(form.name, form.datavols.length + 1)); renderDataVolumes(); };
     }
@@ -453,6 +598,9 @@
           `<label class="muted"><input type="checkbox" value="${kf.esc(pd.label)}"${form.configurations.includes(pd.label) ? " checked" : ""}> ${kf.esc(pd.desc)}</label><br>`).join("") || '<span class="muted">none</span>';
       } catch (e) { $("f-configs").innerHTML = '<span class="muted">none</span>'; }
       try { form.pvcs = (await kf.call("GET", `/api/namespaces/${ns}/pvcs`)).pvcs; } catch (e) { form.pvcs = []; }
+      // storage-class.component.ts: the cluster's classes and the default one
+      try { form.storageClasses = (await kf.call("GET", "/api/storageclasses")).storageClasses; } catch (e) { form.storageClasses = []; }
+      try { form.defaultStorageClass = (await kf.call("GET", "/api/storageclasses/default")).defaultStorageClass; } catch (e) { form.defaultStorageClass = ""; }
       // backend.service.ts getGPUVendors: the configured vendors some node reports capacity for
       try { installedVendors = new Set((await kf.call("GET", "/api/gpus")).vendors || []); } catch (e) { installedVendors = new Set(); }
       fillSpawner();

@@ -179,6 +179,61 @@ test("JWA notebook page YAML tab: Notebook or Pod, with the component's placehol
   assert.strictEqual(JWA.yamlTabText("pod", nb, pod, true), kf.toYaml(pod));
 });
 
+test("JWA notebook overview: resources, type, volumes by kind, configurations, env groups (notebook-page/overview)", () => {
+  const nb = {
+    metadata: { name: "nb", namespace: "team", labels: { "access-ml-pipeline": "true", app: "nb" },
+                annotations: { "notebooks.kubeflow.org/server-type": "group-one", "notebooks.kubeflow.org/creator": "user@x" } },
+    spec: { template: { spec: {
+      containers: [{ name: "sidecar" }, { name: "nb", image: "img:1", env: [{ name: "A", value: "1" }],
+                     resources: { requests: { cpu: "500m", memory: "1Gi" }, limits: { cpu: "1" } } }],
+      volumes: [{ name: "cm", configMap: { name: "c" } }, { name: "ws", persistentVolumeClaim: { claimName: "ws" } },
+                { name: "dshm", emptyDir: { medium: "Memory" } }, { name: "tmp", emptyDir: {} }, { name: "s", secret: {} },
+                { name: "data", persistentVolumeClaim: { claimName: "data" } }, { name: "x", nfs: {} }] } } },
+  };
+  const ov = JWA.overview(nb);
+  assert.deepStrictEqual(ov, { notebookType: "VSCode", sharedMemory: "Yes", notebookCreator: "user@x", cpuRequests: "500m",
+                               cpuLimits: "1", memoryRequests: "1Gi", memoryLimits: null, dockerImage: "img:1" });
+  assert.strictEqual(JWA.overview({ metadata: { annotations: {} } }).notebookType, "empty");
+  assert.strictEqual(JWA.overview({ metadata: {}, spec: { template: { spec: {} } } }).sharedMemory, "null");
+  const g = JWA.volGroups(nb);
+  assert.deepStrictEqual(g.map((x) => x.name), ["PersistentVolumeClaims", "ConfigMaps", "Memory-backed Volumes", "Ephemerals", "Secrets", "Other Volumes"]);
+  assert.deepStrictEqual(g[0].items, [{ name: "ws", url: "/volumes/volume/details/team/ws" }, { name: "data", url: "/volumes/volume/details/team/data" }]);
+  const pds = [
+    { metadata: { name: "add-ml-pipeline" }, spec: { desc: "Allow access", selector: { matchLabels: { "access-ml-pipeline": "true" } },
+      env: [{ name: "KF_PIPELINES_SA_TOKEN_PATH", value: "/var/run/secrets/token" }], volumes: [{ name: "tok" }] } },
+    { metadata: { name: "other" }, spec: { selector: { matchLabels: { nope: "true" } }, env: [{ name: "B", value: "2" }] } },
+  ];
+  const cfgs = JWA.configurations(nb, pds);
+  assert.deepStrictEqual(cfgs.map((c) => c.name), ["add-ml-pipeline"]);
+  assert.ok(!JWA.configurationYaml(cfgs[0]).includes("name: add-ml-pipeline") && JWA.configurationYaml(cfgs[0]).includes("Description: Allow access"));
+  assert.strictEqual(JWA.configurationYaml(null), "No information available about the configuration");
+  assert.strictEqual(JWA.podDefaultsMessage(true, []), "No configurations available for this notebook.");
+  assert.strictEqual(JWA.podDefaultsMessage(false, []), "");
+  const pod = { metadata: { name: "nb-0", labels: { "notebook-name": "nb" } }, status: { podIP: "10.0.0.7" },
+                spec: { containers: [{ name: "nb", env: [{ name: "A", value: "1" }, { name: "KF_PIPELINES_SA_TOKEN_PATH", value: "/var/run/secrets/token" },
+                                                        { name: "IP", valueFrom: { fieldRef: { fieldPath: "status.podIP" } } }] }] } };
+  assert.deepStrictEqual(JWA.envGroups(nb, pod, pds), [
+    { name: "Notebook CR", chips: ["A: 1"] },
+    { name: "add-ml-pipeline (Configuration)", chips: ["KF_PIPELINES_SA_TOKEN_PATH: /var/run/secrets/token"] },
+    { name: "Other", chips: ["IP: 10.0.0.7"] }]);
+  assert.deepStrictEqual(JWA.envGroups(nb, null, pds), [{ name: "Notebook CR", chips: ["A: 1"] }]);
+});
+
+test("JWA form storage class: default class leaves storageClassName out; an explicit or empty class is sent", () => {
+  const v = JWA.newDataVolume("nb", 1);
+  assert.ok(!("storageClassName" in JWA.volumeSpec(v).spec));
+  assert.strictEqual(JWA.volumeSpec(Object.assign({}, v, { useDefaultSC: false, storageClass: "fast" })).spec.storageClassName, "fast");
+  assert.strictEqual(JWA.volumeSpec(Object.assign({}, v, { useDefaultSC: false, storageClass: "" })).spec.storageClassName, "");
+  const opts = JWA.storageClassOptions(["fast", "slow"], v, "slow");
+  assert.ok(opts.startsWith('<option value="">Empty storage class</option>') && opts.includes('<option value="slow" selected>'), opts);
+  const cfg = JSON.parse(JSON.stringify(fixture("jupyter", "config").config));
+  assert.strictEqual(JWA.formDefaults(cfg, "nb").workspace.useDefaultSC, true);
+  cfg.workspaceVolume.value.newPvc.spec.storageClassName = "fast";
+  const ws = JWA.formDefaults(cfg, "nb").workspace;
+  assert.deepStrictEqual([ws.useDefaultSC, ws.storageClass], [false, "fast"]);
+  assert.strictEqual(JWA.buildBody(JWA.formDefaults(cfg, "nb"), cfg, "team").workspace.newPvc.spec.storageClassName, "fast");
+});
+
 test("VWA index page: every PVC name in name order with the reference status icons", () => {
   const pvcs = fixture("volumes", "pvcs").pvcs;
   checkTable(pvcs, VWA.columns(false));

@@ -49,6 +49,8 @@ global.fetch = async (url, opts) => {
   else if (url === "api/namespaces/team/poddefaults") data = { success: true, poddefaults: [{ label: "add-gpu-env", desc: "GPU env" }] };
   else if (url === "api/namespaces/team/pvcs") data = { success: true, pvcs: [{ name: "data" }] };
   else if (url === "api/gpus") data = { success: true, vendors: ["amd.com/gpu"] };
+  else if (url === "api/storageclasses") data = { success: true, storageClasses: ["standard", "fast-nvme"] };
+  else if (url === "api/storageclasses/default") data = { success: true, defaultStorageClass: "standard" };
   const ok = data.success !== false;
   return { ok, status: ok ? 200 : 403, statusText: ok ? "OK" : "Forbidden", json: async () => data };
 };
@@ -235,6 +237,60 @@ test("spawner: the workspace volume's Custom (Advanced) type sends the edited PV
   assert.strictEqual(c.body.workspace.newPvc.spec.resources.requests.storage, "64Gi");
   choose($("f-ws-kind"), "empty");
   assert.ok(!$("f-ws-fields").hidden && $("f-ws-custom").hidden);
+});
+
+test("spawner: storage class — default ticked sends none, an explicit class is POSTed (storage-class component)", async () => {
+  $("new").click();
+  await settle();
+  type($("f-name"), "sc-nb");
+  assert.ok($("f-ws-sc-default").checked && $("f-ws-sc").disabled);
+  assert.strictEqual($("f-ws-sc").value, "standard", "disabled select shows the default class");
+  $("f-add-vol").click();
+  const row = document.querySelector("#f-datavols .datavol");
+  const cb = row.querySelector(".dv-sc-default");
+  cb.checked = false;
+  cb.dispatchEvent({ type: "change" });
+  const sel = document.querySelector("#f-datavols .datavol .dv-sc");
+  assert.ok(!sel.disabled);
+  assert.deepStrictEqual(sel.options.map((o) => o.textContent), ["Empty storage class", "standard", "fast-nvme"]);
+  choose(sel, "fast-nvme");
+  $("f-submit").click();
+  await settle();
+  const c = lastCall("POST");
+  assert.strictEqual(c.body.name, "sc-nb");
+  assert.ok(!("storageClassName" in c.body.workspace.newPvc.spec));
+  assert.strictEqual(c.body.datavols[0].newPvc.spec.storageClassName, "fast-nvme");
+});
+
+test("notebook overview: volumes by kind, configuration dialog with the PodDefault as YAML, env groups", async () => {
+  const nb = byPhase("ready");
+  const ns = nsOf(nb);
+  const base = `api/namespaces/${ns}/notebooks/${nb.name}`;
+  overrides[`GET ${base}`] = { success: true, notebook: {
+    metadata: { name: nb.name, namespace: ns, labels: { "add-gpu-env": "true" }, annotations: {} },
+    spec: { template: { spec: { containers: [{ name: nb.name, image: "img", env: [{ name: "A", value: "1" }], resources: {} }],
+                                volumes: [{ name: "ws", persistentVolumeClaim: { claimName: "ws" } }, { name: "dshm", emptyDir: { medium: "Memory" } }] } } },
+    status: { conditions: [] } } };
+  overrides[`GET ${base}/pod`] = { success: true, pod: { metadata: { name: `${nb.name}-0`, labels: { "notebook-name": nb.name } },
+    spec: { containers: [{ name: nb.name, env: [{ name: "A", value: "1" }, { name: "HIP_VISIBLE_DEVICES", value: "0" }] }] } } };
+  overrides[`GET api/namespaces/${ns}/poddefaults`] = { success: true, poddefaults: [{ label: "add-gpu-env", desc: "GPU env",
+    metadata: { name: "gpu-env" }, spec: { desc: "GPU env", selector: { matchLabels: { "add-gpu-env": "true" } }, env: [{ name: "HIP_VISIBLE_DEVICES", value: "0" }] } }] };
+  document.querySelectorAll("#notebooks a.name").find((a) => a.getAttribute("data-open").split("/").pop() === nb.name).click();
+  await settle();
+  await new Promise((r) => realSetTimeout(r, 5));
+  const body = $("kf-details").querySelector(".tab-body");
+  assert.ok(body.textContent.includes("Shared memory enabled"), body.textContent.slice(0, 200));
+  assert.ok(body.querySelector(`a.vol-link[href="/volumes/volume/details/${ns}/ws"]`), "PVC links to the volumes app");
+  assert.ok(body.textContent.includes("Memory-backed Volumes"));
+  assert.ok(body.textContent.includes("gpu-env (Configuration)") && body.textContent.includes("HIP_VISIBLE_DEVICES: 0"));
+  body.querySelector("button.config-link").click();
+  const info = document.querySelector("dialog.info");
+  assert.ok(info && info.open && info.textContent.includes("gpu-env:"));
+  assert.ok(info.querySelector(".hl").textContent.includes("Description: GPU env") && !info.querySelector(".hl").textContent.includes("name: gpu-env"));
+  info.querySelector('button[data-resp="close"]').click();
+  assert.strictEqual(document.querySelector("dialog.info"), null);
+  $("kf-details").querySelector("button[data-close]").click();
+  for (const k of [`GET ${base}`, `GET ${base}/pod`, `GET api/namespaces/${ns}/poddefaults`]) delete overrides[k];
 });
 
 test("notebook page YAML tab: Notebook / Pod select over a read-only editor (notebook-page/yaml)", async () => {

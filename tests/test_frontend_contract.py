@@ -205,6 +205,44 @@ def test_spawner_body_built_in_js_is_accepted_by_the_backend(apps):
     assert c.get("v1", "PersistentVolumeClaim", "jsform-workspace", NS)["spec"]["accessModes"] == ["ReadWriteOnce"]
 
 
+@needs_node
+def test_custom_yaml_volumes_and_storage_class_accepted_by_the_backend(apps):
+    """Custom (Advanced) volumes: the PVC / volume source the user typed as YAML (parsed by kf.parseYaml
+    in node) and an explicit storage class reach the backend, which creates the PVC and mounts the
+    source as written."""
+    tc, token = apps["jwa"]
+    c = apps["c"]
+    cfg = tc.get("/api/config", headers=_h()).get_json()["config"]
+    script = """
+      global.window = global; global.document = {cookie: ""}; global.location = {search: ""};
+      global.localStorage = {getItem: () => null, setItem: () => {}}; global.addEventListener = () => {}; global.parent = global;
+      const path = require("path"); const W = path.join(process.argv[1], "kubeflow_rm_amd/webapps");
+      global.kf = require(path.join(W, "crud_backend/static/kf.js"));
+      const JWA = require(path.join(W, "jupyter/static/assets/app.js"));
+      const cfg = JSON.parse(process.argv[2]);
+      const f = JWA.formDefaults(cfg, "yamlform");
+      f.workspace = Object.assign(f.workspace, {size: "1", accessMode: "ReadWriteOnce", useDefaultSC: false, storageClass: "standard"});
+      let custom = JWA.toCustom(JWA.renameDataVolume(JWA.newDataVolume("yamlform", 1), "x"));
+      custom = JWA.editCustom(custom, "metadata:\\n  name: yamlform-big\\nspec:\\n  accessModes: [ReadWriteOnce]\\n" +
+                                      "  resources:\\n    requests:\\n      storage: 2Gi  # typed by hand\\n");
+      let src = JWA.toCustom(Object.assign(JWA.newDataVolume("yamlform", 2), {type: "existing", existing: "x", mount: "/data/cfg"}));
+      src = JWA.editCustom(src, "configMap:\\n  name: team-config\\n");
+      f.datavols = [custom, src];
+      const errs = JWA.validate(f);
+      if (errs.length) { console.error(errs.join("; ")); process.exit(2); }
+      console.log(JSON.stringify(JWA.buildBody(f, cfg, process.argv[3])));
+    """
+    r = subprocess.run([NODE, "-e", script, str(ROOT), json.dumps(cfg), NS], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    body = json.loads(r.stdout)
+    resp = tc.post(f"/api/namespaces/{NS}/notebooks", json=body, headers=_h(token))
+    assert resp.status_code == 200, resp.get_json()
+    assert c.get("v1", "PersistentVolumeClaim", "yamlform-big", NS)["spec"]["resources"]["requests"]["storage"] == "2Gi"
+    assert c.get("v1", "PersistentVolumeClaim", "yamlform-workspace", NS)["spec"]["storageClassName"] == "standard"
+    vols = c.get("kubeflow.org/v1beta1", "Notebook", "yamlform", NS)["spec"]["template"]["spec"]["volumes"]
+    assert any(v.get("configMap") == {"name": "team-config"} for v in vols), vols
+
+
 DASH_FIXTURES = Path("/root/reference/components/centraldashboard-angular/frontend/cypress/fixtures")
 
 
