@@ -46,7 +46,9 @@ CONFIGS = {
 def _layer_norm(x, w, b, eps=1e-5):
     if x.is_cuda:
         from kubeflow_rm_amd import ops
-        return ops.layer_norm(x, w, b, eps)
+        if ops.native_enabled():
+            return ops.layer_norm(x, w, b, eps)
+        return F.layer_norm(x, (x.shape[-1],), w, b, eps)
     return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
 
 
@@ -94,17 +96,18 @@ class Block(torch.nn.Module):
                                             device=device, seed=seed + 3)
         self.fc2 = tpl.RowParallelLinear(cfg.d_ff, cfg.d_model, group=tp_group, dtype=cfg.dtype, device=device, seed=seed + 4)
 
-    def attention(self, x):
+    def attention(self, x, residual=None):
         B, T, _ = x.shape
         h, hd = self.local_heads, self.cfg.head_dim
         qkv = self.qkv(x)  # [B, T, 3 * h * hd] — the column shard is [q_h | k_h | v_h] per rank
         q, k, v = qkv.view(B, T, 3, h, hd).permute(2, 0, 3, 1, 4)
         y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return self.proj(y.transpose(1, 2).reshape(B, T, h * hd))
+        return self.proj(y.transpose(1, 2).reshape(B, T, h * hd), residual=residual)
 
     def forward(self, x):
-        x = x + self.attention(self.ln1(x))
-        return x + self.fc2(self.fc1(self.ln2(x)))
+        # both residual adds ride in the output projections' GEMM epilogues (without TP)
+        x = self.attention(self.ln1(x), residual=x)
+        return self.fc2(self.fc1(self.ln2(x)), residual=x)
 
 
 class GPT(torch.nn.Module):

@@ -4,3 +4,25 @@ from .gemm import act_grad, flops, gemm_nt, gemm_nt_preact, linear, matmul, mm  
 from .layernorm import layer_norm, layer_norm_fwd, rms_norm, rms_norm_fwd  # noqa: F401
 from .allreduce import OneShotAllReduce  # noqa: F401
 from .graph import GraphedCallable  # noqa: F401
+
+
+# A/B switch for the model layers (kubeflow_rm_amd.models / parallel.tp): inside torch_reference()
+# GPU tensors run torch's F.linear / F.layer_norm instead of these kernels. Benchmarks use it to
+# compare the two on the same model; nothing in the framework switches it on by itself.
+import contextlib as _contextlib
+
+_native = True
+
+
+def native_enabled() -> bool:
+    return _native
+
+
+@_contextlib.contextmanager
+def torch_reference():
+    global _native
+    prev, _native = _native, False
+    try:
+        yield
+    finally:
+        _native = prev

@@ -339,7 +339,7 @@ class _Linear(torch.autograd.Function):
     (g^T·X, both read k-major) on the w4 kernel: no transposed copies, no recomputed GEMM."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, act):
+    def forward(ctx, x, weight, bias, act, residual):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
         if x2.stride(-1) != 1:
@@ -348,8 +348,15 @@ class _Linear(torch.autograd.Function):
         if act in ("gelu", "gelu_tanh", "silu"):
             y, z = gemm_nt_preact(x2, weight, bias, act)
             y = y.view(*x.shape[:-1], weight.shape[0])
+            if residual is not None:
+                y = y + residual
+        elif residual is not None and act == "none":
+            # the residual add of a transformer block's output projection, in the GEMM epilogue
+            y = gemm_nt(x, weight, bias=bias, residual=residual.contiguous())
         else:
             y = gemm_nt(x, weight, bias=bias, act=act)
+            if residual is not None:
+                y = y + residual
         ctx.save_for_backward(x2, weight, bias, y if act == "relu" else z)
         ctx.act = act
         ctx.xshape = x.shape
@@ -372,13 +379,16 @@ class _Linear(torch.autograd.Function):
             gw = mm(g, x2, trans_a=True)
         if need_db:
             gb = db.to(bias.dtype)
-        return gx, gw, gb, None
+        # y = ... + residual: the residual's gradient is gy itself
+        gr = gy if ctx.needs_input_grad[4] else None
+        return gx, gw, gb, None, gr
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
-           act: str = "none") -> torch.Tensor:
-    """Autograd-aware ``act(F.linear(x, weight, bias))`` on the MFMA kernel."""
-    return _Linear.apply(x, weight, bias, act)
+           act: str = "none", residual: torch.Tensor | None = None) -> torch.Tensor:
+    """Autograd-aware ``act(F.linear(x, weight, bias)) (+ residual)`` on the MFMA kernel (the
+    residual rides in the GEMM epilogue when there is no activation)."""
+    return _Linear.apply(x, weight, bias, act, residual)
 
 
 def flops(M: int, N: int, K: int, batch: int = 1) -> float:

@@ -7,8 +7,10 @@ block) rather than capacity. Layers:
 * ``ColumnParallelLinear``: weight [out/tp, in]; input replicated (identity fwd, all-reduce of
   the input gradient in bwd); output stays sharded unless ``gather_output``.
 * ``RowParallelLinear``: weight [out, in/tp]; input sharded along the feature dim; the partial
-  products are all-reduced in fwd (identity in bwd); bias added once after the reduce, and an
-  optional residual is fused into the GEMM epilogue on rank 0 only.
+  products are all-reduced in fwd (identity in bwd); bias and an optional residual are added once
+  after the reduce — or, without TP, both ride in the GEMM epilogue. (Adding them on rank 0's
+  partial would be cheaper, but then only rank 0's copy of the replicated residual stream would
+  get its gradient.)
 
 GPU tensors run on the hand-written gfx950 GEMM (kubeflow_rm_amd.ops.linear, fused bias +
 activation epilogue). CPU tensors (gloo tests) use torch's linear — they are not a fallback for
@@ -23,18 +25,19 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 
-def _linear(x, w, b=None, act="none"):
+def _linear(x, w, b=None, act="none", residual=None):
     if x.is_cuda:
         from kubeflow_rm_amd import ops
-        return ops.linear(x, w, b, act=act)
+        if ops.native_enabled():
+            return ops.linear(x, w, b, act=act, residual=residual)
     y = F.linear(x, w, b)
     if act == "relu":
-        return F.relu(y)
-    if act in ("gelu", "gelu_tanh"):
-        return F.gelu(y, approximate="tanh")
-    if act == "silu":
-        return F.silu(y)
-    return y
+        y = F.relu(y)
+    elif act in ("gelu", "gelu_tanh"):
+        y = F.gelu(y, approximate="tanh")
+    elif act == "silu":
+        y = F.silu(y)
+    return y + residual if residual is not None else y
 
 
 # Optional K3 fast path per TP group (kubeflow_rm_amd.parallel.oneshot): the row-parallel forward
@@ -186,8 +189,12 @@ class RowParallelLinear(torch.nn.Module):
         self.weight = torch.nn.Parameter(_init_shard((out_features, in_features), 1, group, dtype, device, seed))
         self.bias = torch.nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device)) if bias else None
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
         if not self.input_is_parallel:
             x = scatter_to_tp(x, self.group)
+        if _world(self.group) == 1:
+            return _linear(x, self.weight, self.bias, residual=residual)
         y = reduce_from_tp(_linear(x, self.weight), self.group)
-        return y + self.bias if self.bias is not None else y
+        if self.bias is not None:
+            y = y + self.bias
+        return y + residual if residual is not None else y

@@ -420,3 +420,24 @@ def test_gemm_k_off_grid_packed(M, N, K):
     _assert_close(gemm_nt(a, b, bias=bias, act="gelu_tanh"), _ref_gemm(a, b, bias, "gelu_tanh"), K)
     a3, b3 = _rand(2, 256, K, seed=90), _rand(2, 384, K, seed=91)
     _assert_close(gemm_nt(a3, b3), _ref_gemm(a3, b3), K)
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_linear_residual_in_epilogue(bias):
+    """y = x W^T + b + r with r in the GEMM epilogue; dr = dy, the other grads as without r."""
+    from kubeflow_rm_amd.ops import linear
+    x = _rand(2, 300, 512, seed=92).requires_grad_(True)
+    w = _rand(768, 512, seed=93, scale=0.05).requires_grad_(True)
+    b = _rand(768, seed=94).requires_grad_(True) if bias else None
+    r = _rand(2, 300, 768, seed=95).requires_grad_(True)
+    y = linear(x, w, b, residual=r)
+    g = _rand(*y.shape, seed=96)
+    y.backward(g)
+    xr, wr, rr = (t.detach().float().requires_grad_(True) for t in (x, w, r))
+    br = b.detach().float().requires_grad_(True) if bias else None
+    yr = xr @ wr.t() + (br if bias else 0) + rr
+    yr.backward(g.float())
+    pairs = [(y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (r.grad, rr.grad)] + ([(b.grad, br.grad)] if bias else [])
+    for got, ref in pairs:
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err

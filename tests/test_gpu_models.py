@@ -78,3 +78,21 @@ def test_gpt_forward_hipgraph_replay_matches_eager():
     eager, graphed = timed(fwd), timed(g)
     print(f"gpt-tiny fwd, 64 tokens: eager {eager * 1e6:.0f} us, hipGraph replay {graphed * 1e6:.0f} us")
     assert graphed < eager
+
+
+def test_gpt_native_matches_torch_reference_ops():
+    """The same GPT step on the framework's kernels and inside ops.torch_reference() (F.linear /
+    F.layer_norm): logits and the loss agree, and the reference switch restores the native path."""
+    import torch
+    from kubeflow_rm_amd import ops
+    from kubeflow_rm_amd.models import gpt
+    dev = torch.device("cuda", 0)
+    m = gpt.build("gpt-tiny", device=dev)
+    idx = torch.randint(0, m.cfg.vocab_size, (2, 64), device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    logits, loss = m(idx, idx)
+    with ops.torch_reference():
+        assert not ops.native_enabled()
+        logits_t, loss_t = m(idx, idx)
+    assert ops.native_enabled()
+    assert abs(loss.item() - loss_t.item()) < 2e-2 * abs(loss_t.item())
+    assert (logits.float() - logits_t.float()).abs().max().item() < 5e-2 * logits_t.float().abs().max().item() + 5e-2

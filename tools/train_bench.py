@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""GPT training step on one MI355X: the framework's kernels vs plain torch ops on the same model.
+
+One step = forward + backward + AdamW update of kubeflow_rm_amd.models.gpt (bf16 weights and
+activations, fused AdamW), on synthetic tokens. ``--backend native`` runs the projections on the
+w4 MFMA GEMM (bias / GELU / residual epilogues, pre-activation output, fused act-grad, transposed
+backward layouts) and LayerNorm on the wave-per-row kernel; ``--backend torch`` runs the same model
+inside ``ops.torch_reference()`` (F.linear / F.layer_norm: hipBLASLt + torch's LayerNorm). Both use
+torch's scaled_dot_product_attention, embedding and cross-entropy. Rounds alternate between the two
+backends so clock drift hits both.
+
+python tools/train_bench.py --model gpt-small --batch 8 --seq 1024 --steps 10 --rounds 3
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt-small")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--backends", default="native,torch")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    import torch
+    from kubeflow_rm_amd import ops
+    from kubeflow_rm_amd.models import gpt
+
+    dev = torch.device("cuda", 0)
+    model = gpt.build(args.model, device=dev)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)
+    g = torch.Generator(device=dev).manual_seed(0)
+    V = model.cfg.vocab_size
+    idx = torch.randint(0, V, (args.batch, args.seq), generator=g, device=dev)
+    tgt = torch.randint(0, V, (args.batch, args.seq), generator=g, device=dev)
+    tokens = args.batch * args.seq
+    fpt = model.flops_per_token(args.seq)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        _, loss = model(idx, tgt)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def run(backend, n):
+        ctx = ops.torch_reference() if backend == "torch" else _null()
+        with ctx:
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                loss = step()
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) / n, float(loss.item())
+
+    backends = [b for b in args.backends.split(",") if b]
+    best = {b: float("inf") for b in backends}
+    last_loss = {}
+    for _ in range(args.rounds):
+        for b in backends:
+            dt, loss = run(b, args.steps)
+            best[b] = min(best[b], dt)
+            last_loss[b] = loss
+    out = {"kind": "gpt_train_step_bf16", "model": args.model, "params_M": round(gpt.num_params(model) / 1e6, 1),
+           "batch": args.batch, "seq": args.seq, "tokens_per_step": tokens}
+    for b in backends:
+        out[f"{b}_ms"] = round(best[b] * 1e3, 2)
+        out[f"{b}_tokens_per_s"] = round(tokens / best[b])
+        out[f"{b}_model_tflops"] = round(fpt * tokens / best[b] / 1e12, 1)
+        out[f"{b}_loss"] = round(last_loss[b], 4)
+    if "native" in best and "torch" in best:
+        out["speedup_native_vs_torch"] = round(best["torch"] / best["native"], 3)
+    print(json.dumps(out), flush=True)
+    if args.out:
+        with open(args.out, "a") as f:
+            f.write(json.dumps(out) + "\n")
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+if __name__ == "__main__":
+    main()
