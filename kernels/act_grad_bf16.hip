@@ -103,7 +103,41 @@ __global__ __launch_bounds__(256) void colsum_finalize(const float* __restrict__
   if (sl == 0 && c < cols) db[c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
+// Forward activation as its own HBM pass: y = act(z), n elements (n % 8 == 0, 16-B aligned). For
+// large linears this beats applying gelu / silu in the GEMM epilogue: there the exp / rcp run at one
+// wave per SIMD with the MFMA pipe idle, after every CU's tile finishes at the same moment
+// (profiles/r3_train_step); here they run at full occupancy under the memory stream.
+__global__ __launch_bounds__(256) void act_fwd(const __bf16* __restrict__ z, __bf16* __restrict__ y, long long n8, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const bf16x8 v = reinterpret_cast<const bf16x8*>(z)[i];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float x = (float)v[k];
+      float r;
+      if (act == KFAMD_ACT_GELU_TANH) r = x * sigm(1.5957691216057308f * (x + 0.044715f * x * x * x));
+      else if (act == KFAMD_ACT_SILU) r = x * sigm(x);
+      else if (act == KFAMD_ACT_RELU) r = x > 0.f ? x : 0.f;
+      else r = x;
+      o[k] = (__bf16)r;
+    }
+    reinterpret_cast<bf16x8*>(y)[i] = o;
+  }
+}
+
 }  // namespace
+
+extern "C" int kfamd_act_fwd_bf16(const void* z, void* y, long long n, int act, void* stream) {
+  if (!z || !y || n <= 0 || n % 8 || act < KFAMD_ACT_NONE || act > KFAMD_ACT_SILU) return KFAMD_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(z) | reinterpret_cast<uintptr_t>(y)) & 15) return KFAMD_EALIGN;
+  const long long n8 = n / 8;
+  const long long want = (n8 + 255) / 256;
+  dim3 grid((unsigned)(want < 256 * 16 ? want : 256 * 16)), block(256);
+  hipLaunchKernelGGL(act_fwd, grid, block, 0, reinterpret_cast<hipStream_t>(stream), static_cast<const __bf16*>(z),
+                     static_cast<__bf16*>(y), n8, act);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
 
 extern "C" long long kfamd_act_grad_workspace(int rows, int cols) {
   return (long long)((rows + kRowsPerBlock - 1) / kRowsPerBlock) * cols * (long long)sizeof(float);

@@ -446,13 +446,21 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const bool vec_in = og >= 4 && !((reinterpret_cast<uintptr_t>(HAS_BIAS ? bias : nullptr) |
                                    reinterpret_cast<uintptr_t>(HAS_RES ? R : nullptr)) & 7) &&
                       !(HAS_RES && ((ldr | sr) & 3));
-  auto finish = [&](int i, int n, int m, uint2& pre_out) -> uint2 {
+  // VEC (compile time): bias / residual as 8-B vector loads (the fast path) or element loads
+  auto finish = [&](auto VEC, int i, int n, int m, uint2& pre_out) -> uint2 {
+    constexpr bool vec = decltype(VEC)::value;
     const int col = n0 + wn * WT + n * 16 + elh * 4;
     float v[4];
+    // the accumulator reads as volatile asm, so each path streams them next to their use instead of
+    // the compiler hoisting all 256 reads above the path branch (256 extra live VGPRs + moves)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = acc[i][n][r] * alpha;
+    for (int r = 0; r < 4; ++r) {
+      float a;
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][n][r]));
+      v[r] = a * alpha;
+    }
     if (HAS_BIAS) {
-      if (vec_in) {
+      if constexpr (vec) {
         const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
@@ -473,7 +481,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
     if (HAS_RES) {
       const __bf16* rp = R + (long long)m * ldr + col;
-      if (vec_in) {
+      if constexpr (vec) {
         const bf16x4 rr = *reinterpret_cast<const bf16x4*>(rp);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
@@ -482,10 +490,12 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
         for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
       }
     }
-    bf16x4 o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
-    return __builtin_bit_cast(uint2, o);
+    // two v_cvt_pk_bf16_f32 (RNE), no per-element insert / perm shuffling
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 lo = __builtin_convertvector((f32x2{v[0], v[1]}), bf16x2);
+    const bf16x2 hi = __builtin_convertvector((f32x2{v[2], v[3]}), bf16x2);
+    return uint2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
   };
   if constexpr (SPLIT) {
     // raw fp32 partials, 4 consecutive columns per lane per block: W[z][m][n], ld N
@@ -502,8 +512,14 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
     return;
   }
-  // 8 contiguous bf16 (4 dwords after the swap) at element offset o, column c0: store in og-groups
-  auto store8 = [&](__bf16* base, long long o, int c0, bool row_ok, uint4 d) {
+  // 8 contiguous bf16 (4 dwords after the swap) at element offset o, column c0: one 16-B store (the
+  // fast path), or og-groups for an odd output
+  auto store16 = [&](__bf16* base, long long o, int c0, bool row_ok, uint4 d) {
+    if (row_ok && c0 >= n_lo) *reinterpret_cast<uint4*>(base + o) = d;
+  };
+  // interior tile (not shifted at an M or N edge): every lane stores, no mask
+  auto store_all = [&](__bf16* base, long long o, int, bool, uint4 d) { *reinterpret_cast<uint4*>(base + o) = d; };
+  auto store_og = [&](__bf16* base, long long o, int c0, bool row_ok, uint4 d) {
     if (og == 8) {
       if (row_ok && c0 >= n_lo) *reinterpret_cast<uint4*>(base + o) = d;
     } else if (og == 4) {
@@ -522,25 +538,37 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
   };
   const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
+  auto emit = [&](auto VEC, auto store) {
 #pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int m = m0 + wm * WT + i * 16 + elr;
-    const bool row_ok = m >= m_lo;
-    const long long roff = (long long)m * ldc + n0 + wn * WT + swap_col;
+    for (int i = 0; i < NR; ++i) {
+      const int m = m0 + wm * WT + i * 16 + elr;
+      const bool row_ok = m >= m_lo;
+      // one row pointer per i; the n blocks are immediate offsets from it
+      __bf16* crow = C + ((long long)m * ldc + n0 + wn * WT + swap_col);
+      __bf16* xrow = HAS_AUX ? Aux + ((long long)m * ldc + n0 + wn * WT + swap_col) : nullptr;
 #pragma unroll
-    for (int n = 0; n < NR; n += 2) {
-      uint2 pp{0, 0}, pq{0, 0};
-      uint2 p = finish(i, n, m, pp), q = finish(i, n + 1, m, pq);
-      const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
-      const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
-      const int c0 = n0 + wn * WT + n * 16 + swap_col;
-      store8(C, roff + n * 16, c0, row_ok, uint4{sx[0], sy[0], sx[1], sy[1]});
-      if (HAS_AUX) {
-        const auto ax = __builtin_amdgcn_permlane16_swap(pp.x, pq.x, false, false);
-        const auto ay = __builtin_amdgcn_permlane16_swap(pp.y, pq.y, false, false);
-        store8(Aux, roff + n * 16, c0, row_ok, uint4{ax[0], ay[0], ax[1], ay[1]});
+      for (int n = 0; n < NR; n += 2) {
+        uint2 pp{0, 0}, pq{0, 0};
+        uint2 p = finish(VEC, i, n, m, pp), q = finish(VEC, i, n + 1, m, pq);
+        const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
+        const int c0 = n0 + wn * WT + n * 16 + swap_col;
+        store(crow, n * 16, c0, row_ok, uint4{sx[0], sy[0], sx[1], sy[1]});
+        if (HAS_AUX) {
+          const auto ax = __builtin_amdgcn_permlane16_swap(pp.x, pq.x, false, false);
+          const auto ay = __builtin_amdgcn_permlane16_swap(pp.y, pq.y, false, false);
+          store(xrow, n * 16, c0, row_ok, uint4{ax[0], ay[0], ax[1], ay[1]});
+        }
       }
     }
+  };
+  // uniform branches: interior tiles store unmasked straight-line 16-B stores, shifted edge tiles
+  // mask per lane, an odd output takes the og path; only the path that runs is fetched
+  if (og == 8 && vec_in) {
+    if (m0 == m_lo && n0 == n_lo) emit(T{}, store_all);
+    else emit(T{}, store16);
+  } else {
+    emit(F{}, store_og);
   }
   if (DIAG) {
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();

@@ -85,6 +85,8 @@ int kfamd_pad_k_bf16(const void* src0, void* dst0, long long rows0, long long ld
 // output y for relu), db = column sums of g (fp32, optional). act == NONE: only db = sum over rows of
 // dy (g unused). [rows][cols], cols % 8 == 0, 16-B aligned. workspace: kfamd_act_grad_workspace bytes.
 long long kfamd_act_grad_workspace(int rows, int cols);
+// y = act(z) elementwise (n % 8 == 0, 16-B aligned): the forward activation as its own pass
+int kfamd_act_fwd_bf16(const void* z, void* y, long long n, int act, void* stream);
 int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows, int cols,
                         int act, void* stream);
 

@@ -280,15 +280,35 @@ def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return gemm_nt(a, b.t().contiguous())
 
 
+# gelu / silu forward: in the GEMM epilogue (second output z) or as GEMM -> z, then one elementwise
+# y = act(z) pass. The epilogue's exp / rcp run at one wave per SIMD with the MFMA pipe idle and
+# every CU's tile finishes at once, so once the grid covers the chip the separate pass is faster
+# (profiles/r3_train_step: gpt-1b fc1 8192x8192x2048 289 us fused vs ~240 GEMM + pass).
+PREACT_MODE = "auto"      # "fused" | "split" | "auto"
+_PREACT_SPLIT_TILES = 256  # 256x256 output tiles from which "auto" splits
+
+
+def _preact_split(M: int, N: int) -> bool:
+    if PREACT_MODE != "auto":
+        return PREACT_MODE == "split"
+    return N % 8 == 0 and -(-M // 256) * -(-N // 256) >= _PREACT_SPLIT_TILES
+
+
 def gemm_nt_preact(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, act: str):
-    """(y, z): y = act(x2 @ weight^T + bias) and the pre-activation z from ONE GEMM (the epilogue's
-    second output), for gelu/silu backward. Falls back to z from the kernel + torch's activation."""
+    """(y, z): y = act(x2 @ weight^T + bias) and the pre-activation z (for gelu/silu backward),
+    either both from ONE GEMM (the epilogue's second output) or z from the GEMM and y from one
+    elementwise pass (large grids, see PREACT_MODE)."""
     M, K = x2.shape
     N = weight.shape[0]
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
     z = torch.empty_like(y)
     if bias is not None:
         _check_operand(bias, "bias")
+    if _preact_split(M, N):
+        gemm_nt(x2, weight, bias=bias, out=z)
+        _lib.check(_lib.lib().kfamd_act_fwd_bf16(z.data_ptr(), y.data_ptr(), M * N, ACTS[act], _stream_ptr(z)),
+                   f"act_fwd[{M}x{N}]")
+        return y, z
     rc = _ex(0, 0, x2, weight, y, M, N, K, 1, x2.stride(0), weight.stride(0), N, 0, 0, 0, bias=bias, aux=z,
              act=act)
     if rc > 0:

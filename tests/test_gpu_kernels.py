@@ -441,3 +441,19 @@ def test_linear_residual_in_epilogue(bias):
     for got, ref in pairs:
         err = (got.float() - ref).abs().max().item()
         assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "silu"])
+@pytest.mark.parametrize("mode", ["fused", "split"])
+def test_preact_modes_agree(act, mode):
+    """gelu / silu forward in the GEMM epilogue or as GEMM + one elementwise pass: same y and z."""
+    from kubeflow_rm_amd.ops import gemm as G
+    M, N, K = 1024, 2048, 512
+    x, w, bias = _rand(M, K, seed=97), _rand(N, K, seed=98, scale=0.1), _rand(N, seed=99)
+    G.PREACT_MODE = mode
+    try:
+        y, z = G.gemm_nt_preact(x, w, bias, act)
+    finally:
+        G.PREACT_MODE = "auto"
+    _assert_close(z, _ref_gemm(x, w, bias), K)
+    _assert_close(y, _ref_gemm(x, w, bias, act), K)

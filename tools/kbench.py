@@ -131,22 +131,40 @@ def main():
         gy = (torch.rand(T, N, device=dev) * 2 - 1).to(torch.bfloat16)
         F = torch.nn.functional
 
+        from kubeflow_rm_amd.ops import gemm as G
+
         def ours():
             ops.linear(x, w, bb, act="gelu_tanh").backward(gy)
 
+        def ours_fwd():
+            with torch.no_grad():
+                ops.linear(x, w, bb, act="gelu_tanh")
+
         def theirs():
             F.gelu(F.linear(x, w, bb), approximate="tanh").backward(gy)
+
+        def theirs_fwd():
+            with torch.no_grad():
+                F.gelu(F.linear(x, w, bb), approximate="tanh")
+        res = {}
+        for mode in ("fused", "split"):
+            G.PREACT_MODE = mode
+            for _ in range(3):
+                ours()
+            res[mode] = min(timeit(ours, 10, dev) for _ in range(args.rounds))
+            res[mode + "_fwd"] = min(timeit(ours_fwd, 10, dev) for _ in range(args.rounds))
+        G.PREACT_MODE = "auto"
         for _ in range(3):
-            ours()
             theirs()
-        o, t = [], []
-        for _ in range(args.rounds):
-            o.append(timeit(ours, 10, dev))
-            t.append(timeit(theirs, 10, dev))
+        t = min(timeit(theirs, 10, dev) for _ in range(args.rounds))
+        tf = min(timeit(theirs_fwd, 10, dev) for _ in range(args.rounds))
         fl = 3 * 2.0 * T * K * N
-        emit({"kind": "linear_gelu_fwd_bwd_bf16", "T": T, "K": K, "N": N, "ours_ms": round(min(o) * 1e3, 3),
-              "torch_ms": round(min(t) * 1e3, 3), "ours_tflops": round(fl / min(o) / 1e12, 1),
-              "torch_tflops": round(fl / min(t) / 1e12, 1)})
+        best = min(res["fused"], res["split"])
+        emit({"kind": "linear_gelu_fwd_bwd_bf16", "T": T, "K": K, "N": N, "ours_ms": round(best * 1e3, 3),
+              "fused_ms": round(res["fused"] * 1e3, 3), "split_ms": round(res["split"] * 1e3, 3),
+              "fused_fwd_ms": round(res["fused_fwd"] * 1e3, 3), "split_fwd_ms": round(res["split_fwd"] * 1e3, 3),
+              "torch_ms": round(t * 1e3, 3), "torch_fwd_ms": round(tf * 1e3, 3),
+              "ours_tflops": round(fl / best / 1e12, 1), "torch_tflops": round(fl / t / 1e12, 1)})
         del x, w, bb, gy
         torch.cuda.empty_cache()
 

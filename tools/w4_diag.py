@@ -16,25 +16,30 @@ def main():
     from kubeflow_rm_amd import _build, ops
     # the stamped / ablation kernels live in their own library (never in libkfamd_kernels.so);
     # build it on the host first: python -c "from kubeflow_rm_amd import _build; _build.build_diag_kernels()"
-    if not _build.DIAG_LIB.exists():
-        raise SystemExit(f"{_build.DIAG_LIB} missing: build it with _build.build_diag_kernels()")
-    L = ctypes.CDLL(str(_build.DIAG_LIB))
+    import os
+    lib = Path(os.environ.get("KFAMD_DIAG_LIB", str(_build.DIAG_LIB)))  # A/B: another diag build
+    if not lib.exists():
+        raise SystemExit(f"{lib} missing: build it with _build.build_diag_kernels()")
+    L = ctypes.CDLL(str(lib))
     f = L.kfamd_gemm_nt_bf16_w4_diag
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     dev = torch.device("cuda", 0)
-    for s in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4096,8192,16384").split(",")]:
-        a = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
-        b = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
-        c = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
-        nblk = (s // 256) ** 2
+    for spec in (sys.argv[1] if len(sys.argv) > 1 else "4096,8192,16384").split(","):
+        # a size s (s^3) or MxNxK (multiples of 256 / 256 / 64)
+        M, N, K = (int(v) for v in spec.split("x")) if "x" in spec else (int(spec),) * 3
+        s = K
+        a = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        nblk = (M // 256) * (N // 256)
         diag = torch.zeros(nblk * 4 * 16, dtype=torch.int64, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
         abl_cycles = {}
         for abl in (1, 2, 0):
             for _ in range(3):
-                rc = f(a.data_ptr(), b.data_ptr(), c.data_ptr(), s, s, s, diag.data_ptr(), abl, stream)
+                rc = f(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, diag.data_ptr(), abl, stream)
                 assert rc == 0, rc
             torch.cuda.synchronize()
             d8 = diag.view(nblk, 4, 16).double()
@@ -77,9 +82,9 @@ def main():
             ops.gemm_nt(a, b, out=c, variant="w4")
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / n
-        print(json.dumps({"size": s, "segments": ["substep0_issue+F1_land", "dma_wait+barrier", "substep1_issue",
+        print(json.dumps({"size": spec, "segments": ["substep0_issue+F1_land", "dma_wait+barrier", "substep1_issue",
                                                    "F0_land"], "share": [round(x, 4) for x in share],
-                          "mean_cycles_per_wave": [round(x) for x in cyc], "w4_tflops": round(2 * s ** 3 / dt / 1e12, 1),
+                          "mean_cycles_per_wave": [round(x) for x in cyc], "w4_tflops": round(2 * M * N * K / dt / 1e12, 1),
                           "loop_cycles_per_ktile": round(sum(cyc) / (s // 64)),
                           "prologue_cycles": round(d8[..., 4].mean().item()), "epilogue_issue_cycles": round(d8[..., 5].mean().item()),
                           "kloop_cycles": round(d8[..., 6].mean().item()),
