@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void colsum_finalize(const float* __restrict__
 // Forward activation as its own HBM pass: y = act(z), n elements (n % 8 == 0, 16-B aligned). For
 // large linears this beats applying gelu / silu in the GEMM epilogue: there the exp / rcp run at one
 // wave per SIMD with the MFMA pipe idle, after every CU's tile finishes at the same moment
-// (profiles/r3_train_step); here they run at full occupancy under the memory stream.
+// (profiles/r3_train_step); here they run at full occupancy under the memory stream. Used by
+// ops.gemm_nt_preact in its "split" mode (A/B runs; the fused epilogue is the default).
 __global__ __launch_bounds__(256) void act_fwd(const __bf16* __restrict__ z, __bf16* __restrict__ y, long long n8, int act) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     const bf16x8 v = reinterpret_cast<const bf16x8*>(z)[i];

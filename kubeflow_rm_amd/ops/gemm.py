@@ -280,18 +280,15 @@ def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return gemm_nt(a, b.t().contiguous())
 
 
-# gelu / silu forward: in the GEMM epilogue (second output z) or as GEMM -> z, then one elementwise
-# y = act(z) pass. The epilogue's exp / rcp run at one wave per SIMD with the MFMA pipe idle and
-# every CU's tile finishes at once, so once the grid covers the chip the separate pass is faster
-# (profiles/r3_train_step: gpt-1b fc1 8192x8192x2048 289 us fused vs ~240 GEMM + pass).
-PREACT_MODE = "auto"      # "fused" | "split" | "auto"
-_PREACT_SPLIT_TILES = 256  # 256x256 output tiles from which "auto" splits
+# gelu / silu forward: in the GEMM epilogue (second output z, the default) or as GEMM -> z, then one
+# elementwise y = act(z) pass ("split"). With the 8 k-cycle epilogue the fused form wins or ties at
+# every measured shape (profiles/r3_train_step: 8192x2048x8192 fwd 0.257 ms fused, 0.275 split,
+# torch 0.261); the split form stays selectable for A/B runs.
+PREACT_MODE = "auto"      # "fused" | "split" | "auto" (= fused)
 
 
 def _preact_split(M: int, N: int) -> bool:
-    if PREACT_MODE != "auto":
-        return PREACT_MODE == "split"
-    return N % 8 == 0 and -(-M // 256) * -(-N // 256) >= _PREACT_SPLIT_TILES
+    return PREACT_MODE == "split" and N % 8 == 0
 
 
 def gemm_nt_preact(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None, act: str):

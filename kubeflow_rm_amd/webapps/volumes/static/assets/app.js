@@ -1,6 +1,6 @@
 // Volumes web app frontend (reference crud-web-apps/volumes/frontend): PVC table (common resource
-// table, polled) with the notebooks using each claim, create / delete, volume details (overview +
-// conditions / events / pods using it / YAML) and the PVCViewer (file browser) lifecycle: browse
+// table, polled) with the notebooks using each claim, create / delete, volume details (overview with
+// the pods mounting it and conditions / events / YAML) and the PVCViewer (file browser) lifecycle: browse
 // -> viewer created -> open its URL when ready -> close.
 // `VWA` holds the pure parts (columns, viewer button state, request body) for the node tests.
 (function (global) {
@@ -57,6 +57,42 @@
       const closeAction = v.status === "uninitialized" ? "unavailable" : v.status === "terminating" ? "waiting" : "ready";
       return { deleteAction, openAction, closeAction, autoOpen };
     },
+    // volume-details-page/overview: the PVC's facts ("null" where unset, as the component shows),
+    // owner chips, and the pods mounting it grouped into Notebooks / InferenceService links
+    overview(pvc) {
+      const spec = (pvc || {}).spec || {}, st = (pvc || {}).status || {};
+      const owners = ((pvc || {}).metadata || {}).ownerReferences || [];
+      return {
+        accessModes: (st.accessModes || spec.accessModes || []).filter(Boolean),
+        size: (st.capacity || {}).storage || ((spec.resources || {}).requests || {}).storage || "null",
+        storageClass: spec.storageClassName || "null", volumeMode: spec.volumeMode || "null",
+        volumeName: spec.volumeName || "null", ownerRefs: owners.map((r) => `${r.kind}: ${r.name}`),
+      };
+    },
+    podGroups(pods, viewerUrl) {
+      const groups = [];
+      (pods || []).forEach((pod) => {
+        const labels = (pod.metadata || {}).labels || {}, ns = (pod.metadata || {}).namespace;
+        let name, group, url;
+        if ("serving.kubeflow.org/inferenceservice" in labels) {
+          const svc = labels["serving.kubeflow.org/inferenceservice"];
+          name = `${svc} (${labels.component})`;
+          group = "InferenceService";
+          url = `${viewerUrl || ""}/models/details/${ns}/${svc}/`;
+        } else if ("notebook-name" in labels) {
+          name = labels["notebook-name"];
+          group = "Notebooks";
+          url = `${viewerUrl || ""}/jupyter/notebook/details/${ns}/${name}/`;
+        } else return;
+        let g = groups.find((x) => x.name === group);
+        if (!g) groups.push(g = { name: group, links: [] });
+        g.links.push({ name, url });
+      });
+      return groups;
+    },
+    podsMountedMessage(error) {
+      return error ? `Failed to fetch mounted pods with error: ${error}` : "No pods are using this PVC.";
+    },
     newPvcBody(name, size, mode, storageClass) {
       return { name, size: /[A-Za-z]$/.test(String(size)) ? String(size) : `${size}Gi`, mode, class: storageClass || "{empty}", type: "empty" };
     },
@@ -86,27 +122,33 @@
       try { await kf.call(method, path, body); } catch (e) { kf.snack(e.message, "ERROR"); }
       poller.reset();
     }
-    // volume page: overview + conditions / events / pods / YAML (VWA pages/volume-details-page)
+    const spec_has = (pvc, k) => !!((pvc || {}).spec || {})[k];
+    // volume page: overview (+ pods mounted, conditions) / events / YAML (VWA pages/volume-details-page)
     function showDetails(ns, name) {
       const base = `/api/namespaces/${ns}/pvcs/${name}`;
       const e = kf.esc;
       return kf.details(`Volume ${ns}/${name}`, [
         { name: "Overview", render: async () => {
           const pvc = (await kf.call("GET", base)).pvc;
-          const spec = pvc.spec || {}, st = pvc.status || {};
-          return kf.kvTable([
-            ["Name", pvc.metadata.name], ["Namespace", pvc.metadata.namespace], ["Created", pvc.metadata.creationTimestamp],
-            ["Phase", st.phase || "-"], ["Requested", ((spec.resources || {}).requests || {}).storage || "-"],
-            ["Capacity", (st.capacity || {}).storage || "-"], ["Access modes", (spec.accessModes || []).join(", ")],
-            ["Storage class", spec.storageClassName || "(default)"], ["Volume", spec.volumeName || "-"],
-          ]) + `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
+          const st = pvc.status || {};
+          const ov = VWA.overview(pvc);
+          let pods = [], err = "";
+          try { pods = (await kf.call("GET", `${base}/pods`)).pods; } catch (x) { err = x.message; }
+          const groups = VWA.podGroups(pods, "");
+          const chips = (xs) => xs.map((x) => `<span class="chip">${e(x)}</span>`).join(" ");
+          const rows = [["Name", pvc.metadata.name], ["Namespace", pvc.metadata.namespace], ["Created", pvc.metadata.creationTimestamp],
+            ["Phase", st.phase || "-"], ["Size", ov.size], ["Storage class", ov.storageClass], ["Volume mode", ov.volumeMode]];
+          if (spec_has(pvc, "volumeName")) rows.push(["Volume name", ov.volumeName]);
+          return kf.kvTable(rows) +
+            `<table class="kv"><tr><th>Access modes</th><td>${chips(ov.accessModes)}</td></tr>` +
+            (ov.ownerRefs.length ? `<tr><th title="The PVC is deleted with the objects that own it">Owned by</th><td>${chips(ov.ownerRefs)}</td></tr>` : "") +
+            "</table><h3>Pods Mounted</h3>" +
+            (groups.length ? groups.map((g) => `<div class="vol-group"><b>${e(g.name)}</b> ` +
+              g.links.map((l) => `<a class="pod-link" href="${e(l.url)}">${e(l.name)}</a>`).join(" ") + "</div>").join("")
+              : `<p class="muted">${e(VWA.podsMountedMessage(err))}</p>`) +
+            `<h3>Conditions</h3>${kf.conditionsTable(st.conditions)}`;
         } },
         { name: "Events", render: async () => kf.eventsTable((await kf.call("GET", `${base}/events`)).events) },
-        { name: "Pods", render: async () => {
-          const pods = (await kf.call("GET", `${base}/pods`)).pods;
-          if (!pods.length) return '<p class="muted">Not mounted by any pod.</p>';
-          return kf.kvTable(pods.map((p) => [p.metadata.name, `${(p.status || {}).phase || ""} on ${(p.spec || {}).nodeName || "-"}`]));
-        } },
         { name: "YAML", render: async () => kf.yamlHtml(kf.toYaml((await kf.call("GET", base)).pvc)) },
       ]);
     }

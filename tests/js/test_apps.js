@@ -234,6 +234,25 @@ test("JWA form storage class: default class leaves storageClassName out; an expl
   assert.strictEqual(JWA.buildBody(JWA.formDefaults(cfg, "nb"), cfg, "team").workspace.newPvc.spec.storageClassName, "fast");
 });
 
+test("VWA volume overview: facts, owner chips, pods mounted grouped into links (volume-details-page/overview)", () => {
+  const pvc = { metadata: { name: "data", ownerReferences: [{ kind: "Notebook", name: "nb" }] },
+                spec: { accessModes: ["ReadWriteOnce"], resources: { requests: { storage: "5Gi" } }, storageClassName: "fast" },
+                status: { capacity: { storage: "8Gi" }, accessModes: ["ReadWriteMany"] } };
+  assert.deepStrictEqual(VWA.overview(pvc), { accessModes: ["ReadWriteMany"], size: "8Gi", storageClass: "fast", volumeMode: "null",
+                                              volumeName: "null", ownerRefs: ["Notebook: nb"] });
+  assert.strictEqual(VWA.overview({ spec: { resources: { requests: { storage: "5Gi" } } } }).size, "5Gi");
+  const pods = [
+    { metadata: { namespace: "team", labels: { "notebook-name": "nb1" } } },
+    { metadata: { namespace: "team", labels: { "serving.kubeflow.org/inferenceservice": "svc", component: "predictor" } } },
+    { metadata: { namespace: "team", labels: { app: "other" } } },
+    { metadata: { namespace: "team", labels: { "notebook-name": "nb2" } } }];
+  assert.deepStrictEqual(VWA.podGroups(pods, "/x"), [
+    { name: "Notebooks", links: [{ name: "nb1", url: "/x/jupyter/notebook/details/team/nb1/" }, { name: "nb2", url: "/x/jupyter/notebook/details/team/nb2/" }] },
+    { name: "InferenceService", links: [{ name: "svc (predictor)", url: "/x/models/details/team/svc/" }] }]);
+  assert.strictEqual(VWA.podsMountedMessage(""), "No pods are using this PVC.");
+  assert.strictEqual(VWA.podsMountedMessage("boom"), "Failed to fetch mounted pods with error: boom");
+});
+
 test("VWA index page: every PVC name in name order with the reference status icons", () => {
   const pvcs = fixture("volumes", "pvcs").pvcs;
   checkTable(pvcs, VWA.columns(false));
