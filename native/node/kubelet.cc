@@ -975,9 +975,9 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     return true;
   };
   double next_wake = 1.0;
-  // Until a pod is Ready the kubelet re-syncs it every 10 ms (cold start is on the notebook's
+  // Until a pod is Ready the kubelet re-syncs it every 5 ms (cold start is on the notebook's
   // critical path; a sync of an unchanged pod costs no API call), afterwards at the 1 s relist.
-  constexpr double kStartupPoll = 0.01;
+  constexpr double kStartupPoll = 0.005;
   // Probes of one running container (startup gates readiness/liveness); keeps next_wake.
   auto tick_probes = [&](ContainerRt& cr, const Json& c) {
     const double now = now_seconds();
@@ -1010,8 +1010,9 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
           cr.ready = false;
         }
       }
-      // probe fast until the first success (cold-start latency), then at periodSeconds
-      cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : 0.02);
+      // probe fast until the first success (cold-start latency: the readiness sidecar's verdict or
+      // the server's first answer is seen within ~5 ms), then at periodSeconds
+      cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : kStartupPoll);
     }
     const Json& lp = c["livenessProbe"];
     if (lp.is_object() && now >= cr.next_live_probe) {
@@ -1224,7 +1225,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       },
       true);
   if (ue && ue.code != 404) *err = ue.message;
-  return Result::after(std::max(0.02, next_wake));
+  return Result::after(std::max(kStartupPoll, next_wake));
 }
 
 // GPU metrics (SURVEY §5.5 build additions), scraped from the kubelet's registry: which pod holds
