@@ -236,7 +236,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  constexpr int kGroupM = 4;
+#ifndef KFW4_GROUP_M
+#define KFW4_GROUP_M 4  // tile-row group of the grouped raster (A/B runs build other values)
+#endif
+  constexpr int kGroupM = KFW4_GROUP_M;
   const int per_group = kGroupM * tiles_n;
   const int g = wg / per_group, first_m = g * kGroupM;
   const int gm = min(tiles_m - first_m, kGroupM);
