@@ -274,10 +274,17 @@ def mm(a: torch.Tensor, b: torch.Tensor, *, trans_a: bool = False, trans_b: bool
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b with b stored [K, N] (row-major): read k-major in place (no transposed copy)."""
-    if a.dim() == 2 and b.dim() == 2:
+    """a @ b with b stored [K, N] (row-major), read k-major in place (no transposed copy):
+    [M, K] @ [K, N], [..., M, K] @ [K, N] (leading dims folded into M) and batched
+    [B, M, K] @ [B, K, N]."""
+    if b.dim() == 2:
+        if a.dim() == 2:
+            return mm(a, b)
+        a2 = a.reshape(-1, a.shape[-1])
+        return mm(a2, b).view(*a.shape[:-1], b.shape[-1])
+    if a.dim() == 3 and b.dim() == 3:
         return mm(a, b)
-    return gemm_nt(a, b.t().contiguous())
+    return gemm_nt(a, b.transpose(-1, -2).contiguous())
 
 
 # gelu / silu forward: in the GEMM epilogue (second output z, the default) or as GEMM -> z, then one

@@ -457,3 +457,13 @@ def test_preact_modes_agree(act, mode):
         G.PREACT_MODE = "auto"
     _assert_close(z, _ref_gemm(x, w, bias), K)
     _assert_close(y, _ref_gemm(x, w, bias, act), K)
+
+
+def test_matmul_shapes_without_copies():
+    """matmul: 2-D, leading dims folded into M, and batched, all vs fp32."""
+    from kubeflow_rm_amd.ops import matmul
+    a, b = _rand(3, 200, 256, seed=100), _rand(256, 384, seed=101)
+    _assert_close(matmul(a, b), a.float() @ b.float(), 256)
+    a3, b3 = _rand(2, 256, 512, seed=102), _rand(2, 512, 384, seed=103)
+    _assert_close(matmul(a3, b3), a3.float() @ b3.float(), 512)
+    _assert_close(matmul(a3[0], b3[0]), a3[0].float() @ b3[0].float(), 512)
