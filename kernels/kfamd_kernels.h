@@ -76,6 +76,14 @@ int kfamd_splitk_reduce(const float* W, void* C, const void* bias, const void* R
                         int splits, long long ldc, long long ldr, long long stride_c, long long stride_r, float alpha,
                         int act, void* stream);
 
+// Softmax cross-entropy (xent_bf16.hip): forward -> per-row loss and log-sum-exp (fp32); backward ->
+// dlogits = (softmax - onehot) * (*g / *count) in bf16 (device scalars: no host sync).
+int kfamd_xent_fwd_bf16(const void* logits, long long ld, const long long* target, float* loss, float* lse, int rows,
+                        int V, long long ignore_index, void* stream);
+int kfamd_xent_bwd_bf16(const void* logits, long long ld, const long long* target, const float* lse, void* grad,
+                        long long ldg, int rows, int V, long long ignore_index, const float* g, const float* count,
+                        void* stream);
+
 // K-padding pack (pad_bf16.hip): dst_i[r][0:Kp] = src_i[r][0:K], zero tail, both GEMM operands in
 // one launch (rows1 = 0: one matrix). Kp % 8 == 0; dst dense and 16-B aligned.
 int kfamd_pad_k_bf16(const void* src0, void* dst0, long long rows0, long long ld0, const void* src1, void* dst1,

@@ -3,7 +3,8 @@
 Used by the multi-GPU notebook smoke (BASELINE config 4: DP/TP over RCCL inside a pod), the
 examples and ``smoke()``. Every projection runs on the hand-written MFMA GEMM with its fused
 epilogue (bias + GELU for the MLP up-projection; residual for the down-projection), LayerNorm
-on the wave-per-row kernel, attention on ``scaled_dot_product_attention`` (ROCm flash path).
+on the wave-per-row kernel, the LM-head loss on the bf16 cross-entropy kernel, attention on
+``scaled_dot_product_attention`` (ROCm flash path).
 With a tensor-parallel group the attention heads and the MLP are split Megatron-style
 (QKV / fc1 column-parallel, out-proj / fc2 row-parallel: one all-reduce per sub-block).
 
@@ -50,6 +51,14 @@ def _layer_norm(x, w, b, eps=1e-5):
             return ops.layer_norm(x, w, b, eps)
         return F.layer_norm(x, (x.shape[-1],), w, b, eps)
     return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def _cross_entropy(logits, targets):
+    if logits.is_cuda:
+        from kubeflow_rm_amd import ops
+        if ops.native_enabled():
+            return ops.cross_entropy(logits, targets)  # bf16 logits, no fp32 copy
+    return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
 
 
 class LayerNorm(torch.nn.Module):
@@ -131,8 +140,7 @@ class GPT(torch.nn.Module):
         logits = tpl._linear(x, self.tok)  # tied output head [B, T, vocab]
         if targets is None:
             return logits
-        loss = F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1))
-        return logits, loss
+        return logits, _cross_entropy(logits, targets)
 
     def flops_per_token(self, seq: int) -> float:
         """Training FLOPs/token (fwd+bwd = 3x fwd): dense matmuls + attention scores."""

@@ -38,6 +38,8 @@ _SIGNATURES = {
     "kfamd_pad_k_bf16": (c_int, [c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_vp]),
     "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
     "kfamd_act_fwd_bf16": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp]),
+    "kfamd_xent_fwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp]),
+    "kfamd_xent_bwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp]),
     "kfamd_act_grad_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "kfamd_layernorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),
     "kfamd_rmsnorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),

@@ -467,3 +467,21 @@ def test_matmul_shapes_without_copies():
     a3, b3 = _rand(2, 256, 512, seed=102), _rand(2, 512, 384, seed=103)
     _assert_close(matmul(a3, b3), a3.float() @ b3.float(), 512)
     _assert_close(matmul(a3[0], b3[0]), a3[0].float() @ b3[0].float(), 512)
+
+
+@pytest.mark.parametrize("rows,V", [(512, 32000), (37, 1000), (8, 50257)])
+def test_cross_entropy_matches_fp32(rows, V):
+    """bf16 softmax cross-entropy (fwd: loss via log-sum-exp; bwd: softmax - onehot scaled by the
+    upstream gradient / counted rows) vs torch's fp32 cross-entropy, with ignored targets."""
+    from kubeflow_rm_amd.ops import cross_entropy
+    x = (torch.randn(rows, V, device="cuda") * 3).to(torch.bfloat16).requires_grad_(True)
+    t = torch.randint(0, V, (rows,), device="cuda")
+    t[::5] = -100
+    loss = cross_entropy(x, t)
+    (loss * 0.5).backward()
+    xr = x.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xr, t, ignore_index=-100)
+    (ref * 0.5).backward()
+    assert abs(loss.item() - ref.item()) <= 1e-3 * abs(ref.item()) + 1e-3, (loss.item(), ref.item())
+    err = (x.grad.float() - xr.grad).abs().max().item()
+    assert err <= 1e-2 * xr.grad.abs().max().item() + 1e-6, err
