@@ -63,7 +63,16 @@ def _preinit_hip() -> threading.Thread | None:
         try:
             hip = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
             if hip.hipInit(0) == 0 and hip.hipSetDevice(0) == 0:
-                hip.hipFree(None)  # creates the device context (and its first queue) now
+                hip.hipFree(None)  # creates the device context now
+                # the first GPU operation of the process pays ~90 ms more (the null stream's HW queue,
+                # the runtime's blit kernels): a memset + sync here, under the import. Only HIP's
+                # own entry points (ctypes drops the GIL for each); loading another HIP library on
+                # this thread while torch registers its kernels on the main one can deadlock.
+                buf = ctypes.c_void_p()
+                if hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(4096)) == 0:
+                    hip.hipMemset(buf, 0, ctypes.c_size_t(4096))
+                    hip.hipDeviceSynchronize()
+                    hip.hipFree(buf)
         except OSError:
             pass  # torch initialises on first use as usual
 
@@ -83,15 +92,23 @@ def warmup_torch() -> dict:
     from kubeflow_rm_amd import ops
     t2 = time.perf_counter()
     dev = torch.device("cuda", 0)
-    a = torch.randn(1024, 1024, device=dev).to(torch.bfloat16)
-    b = torch.randn(1024, 1024, device=dev).to(torch.bfloat16)
-    c = ops.gemm_nt(a, b)
-    torch.cuda.synchronize(dev)
+    # operands made on the host and copied in (DMA), the GEMM on the framework's MFMA kernel on torch's
+    # stream and caching allocator, the result copied back and spot-checked on the host: proves torch's
+    # GPU runtime and the pod's GPU work without launching (and so code-object loading) any of torch's
+    # own kernels before Ready — the first of those costs ~100 ms and lands in the user's first cell
+    g = torch.Generator().manual_seed(0)
+    ha = (torch.rand(1024, 1024, generator=g) * 2 - 1).to(torch.bfloat16)
+    hb = (torch.rand(1024, 1024, generator=g) * 2 - 1).to(torch.bfloat16)
+    c = ops.gemm_nt(ha.to(dev), hb.to(dev))
+    hc = c.cpu()
     t3 = time.perf_counter()
-    ok = bool(torch.isfinite(c.float()).all().item())
+    rows = [0, 511, 1023]
+    ref = ha[rows].float() @ hb.float().t()
+    err = (hc[rows].float() - ref).abs().max().item()
+    ok = bool(torch.isfinite(hc[rows].float()).all().item()) and err <= 1e-2 * ref.abs().max().item() + 1e-2
     return {"ok": ok, "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
             "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1), "hip_preinit": pre is not None,
-            "device": torch.cuda.get_device_name(dev)}
+            "max_abs_err": err, "device": torch.cuda.get_device_name(dev)}
 
 
 def _now() -> str:
