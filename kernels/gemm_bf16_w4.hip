@@ -82,6 +82,64 @@ extern "C" int kfamd_w4_launch_nt(int bm, const void* A, const void* B, void* C,
   return KFAMD_EINVAL;
 }
 
+// Stream-K on the 256x256 tile (NT layout, batch 1): a persistent grid of `grid` blocks (one per CU)
+// runs the whole waves of tiles, then the remaining rem = tiles % grid tiles in `splits` K-splits
+// each, round-robin over all blocks (gemm_w4.h SK). W: (splits - 1) * rem partial tiles of 256 x 256
+// fp32; flags: splits * rem words, never holding `epoch` from an earlier call (the caller keeps one
+// buffer per stream and a strictly increasing epoch). Negative `splits`: every owner recomputes its
+// producers' splits after the deadline (tests of that path).
+extern "C" int kfamd_w4_streamk_nt(const void* A, const void* B, void* C, const void* bias, const void* R, void* Aux,
+                                   int M, int N, int K, long long lda, long long ldb, long long ldc, long long ldr,
+                                   float alpha, int act, float* W, unsigned* flags, unsigned epoch, int grid,
+                                   int splits, void* stream) {
+  const int rc = check_shape(0, 0, 256, A, B, C, bias, R, Aux, M, N, K, lda, ldb, ldc, ldr, 0, 0, 0, 0);
+  if (rc != KFAMD_OK) return rc;
+  if (!W || !flags || epoch == 0 || grid < 8 || grid > 4096) return KFAMD_EINVAL;
+  // no pre-activation output: the second output's registers push the persistent loop's accumulators
+  // into scratch (the Aux forward runs on the plain kernel)
+  if (Aux) return KFAMD_EINVAL;
+  if (R && act != KFAMD_ACT_NONE) return KFAMD_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(flags) & 3)) return KFAMD_EALIGN;
+  // an owner tracks its producers in a 64-bit mask; every split holds at least one K-tile
+  const int KT = (K + kBK - 1) / kBK;
+  // (splits < 0: the deadline path's test mode, see gemm_w4.h)
+  const int S = splits < 0 ? -splits : splits;
+  if (S < 1 || S > 64 || S > KT) return KFAMD_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 g(grid), block(kThreads);
+  const __bf16* a = static_cast<const __bf16*>(A);
+  const __bf16* b = static_cast<const __bf16*>(B);
+  __bf16* c = static_cast<__bf16*>(C);
+  const __bf16* bs = static_cast<const __bf16*>(bias);
+  const __bf16* r = static_cast<const __bf16*>(R);
+  const bool hb = bias != nullptr, hr = R != nullptr;
+#define SK_LAUNCH(ACTV, HB, HR, HX)                                                                                  \
+  hipLaunchKernelGGL((gemm_w4<ACTV, HB, HR, HX, 0, 0, 256, false, false, 0, true>), g, block, 0, s, a, b, c, bs, r, \
+                     nullptr, M, N, K, lda, ldb, ldc, ldr, 0LL, 0LL, 0LL, 0LL, alpha, nullptr, W, splits, flags, epoch)
+  switch (act) {
+    case KFAMD_ACT_NONE:
+      if (hb && hr) SK_LAUNCH(KFAMD_ACT_NONE, true, true, false);
+      else if (hb) SK_LAUNCH(KFAMD_ACT_NONE, true, false, false);
+      else if (hr) SK_LAUNCH(KFAMD_ACT_NONE, false, true, false);
+      else SK_LAUNCH(KFAMD_ACT_NONE, false, false, false);
+      break;
+#define SK_ACT(ACTV)                                   \
+  case ACTV:                                           \
+    if (hb) SK_LAUNCH(ACTV, true, false, false);       \
+    else SK_LAUNCH(ACTV, false, false, false);         \
+    break;
+    SK_ACT(KFAMD_ACT_RELU)
+    SK_ACT(KFAMD_ACT_GELU_TANH)
+    SK_ACT(KFAMD_ACT_SILU)
+    default:
+      return KFAMD_EINVAL;
+  }
+#undef SK_ACT
+#undef SK_LAUNCH
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
 // Split-K partials on the 128x128 w4s tile (NT layout): W[splits][batch][M][N] fp32, K range
 // [z*kper, (z+1)*kper) per split (kper % 64 == 0); the epilogue runs in kfamd_splitk_reduce.
 extern "C" int kfamd_w4_splitk_nt(const void* A, const void* B, float* W, int M, int N, int K, int batch, int splits,

@@ -57,6 +57,7 @@ constexpr int kSlots = 5;                         // operand-tile slots (A or B 
 constexpr int kRsrcWord3 = 0x00020000;            // gfx9 raw buffer: 32-bit dword format, no swizzle
 constexpr unsigned kOOB = 0x80000000u;            // voffset of a zero-filled (out-of-range) piece
 constexpr int kNumRecords = 0x7fffffff;
+constexpr unsigned long long kSkTimeoutTicks = 5000000;  // stream-K partial wait: 50 ms of s_memrealtime
 
 __device__ __forceinline__ float act_fn(float v, int act) {
   switch (act) {
@@ -205,15 +206,23 @@ struct Reader {
 // SPLIT (split-K, for problems with too few output tiles to fill 256 CUs): blockIdx.z takes the K
 // range [z*kper, (z+1)*kper) and the block stores its raw fp32 partial tile to W[z][M][N]; the
 // epilogue (alpha, bias, activation, Aux, residual) runs in splitk_reduce (gemm_bf16.hip).
+// SK (stream-K, for grids that leave part of the last wave of 256 CUs idle): a persistent grid of
+// G = gridDim.x blocks (one per CU) first runs the whole data-parallel waves (tiles [0, T - T % G)),
+// then the remaining tiles in kper K-splits each, spread round-robin over all G blocks. The block
+// running a tile's last split owns it: it adds the other splits' fp32 partials (W[unit][BM][BN],
+// released with an agent-scope flag = epoch) and runs the epilogue; a partial that does not arrive
+// within the deadline is recomputed by the owner itself, so a non-co-resident grid is slow, never
+// hung or wrong.
 template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, bool SPLIT = false,
-          bool DIAG = false, int ABL = 0>
+          bool DIAG = false, int ABL = 0, bool SK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
              const __bf16* __restrict__ bias, const __bf16* __restrict__ R, __bf16* __restrict__ Aux, int M, int N,
              int K, long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
              long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag,
-             float* __restrict__ W = nullptr, int kper = 0) {
+             float* __restrict__ W = nullptr, int kper = 0, unsigned* __restrict__ sk_flags = nullptr,
+             unsigned sk_epoch = 0) {
   constexpr int BN = BM, WT = BM / 2, NR = WT / 16;    // wave tile WT x WT = NR x NR MFMA blocks
   constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
   constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
@@ -223,6 +232,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(BM == 256 || BM == 128, "tile");
   static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
   static_assert(!SPLIT || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
+  static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
   __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -236,6 +246,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
   const int wg = xcd_remap(blockIdx.x, nwg);
+#ifndef KFW4_SK_AB
+#define KFW4_SK_AB 0  // stream-K timing ablations (tools/sk_ab.py builds): 1 no partial traffic, 2 no owner wait
+#endif
 #ifndef KFW4_GROUP_M
 #define KFW4_GROUP_M 4  // tile-row group of the grouped raster (A/B runs build other values)
 #endif
@@ -245,18 +258,20 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const int gm = min(tiles_m - first_m, kGroupM);
   const int tm = first_m + (wg % per_group) % gm;
   const int tn = (wg % per_group) / gm;
-  const int m_lo = tm * BM, n_lo = tn * BN;            // first output row / column this block stores
-  const int m0 = min(m_lo, M - BM), n0 = min(n_lo, N - BN);  // edge tiles shifted inside
+  int m_lo = tm * BM, n_lo = tn * BN;                  // first output row / column this block stores
+  int m0 = min(m_lo, M - BM), n0 = min(n_lo, N - BN);  // edge tiles shifted inside
 
   long long kbeg = 0;
   if (SPLIT) {  // this block's K range; only the last split can be partial (kper % 64 == 0)
     kbeg = (long long)blockIdx.z * kper;
     K = min((long long)kper, (long long)K - kbeg);
   }
-  const int nk = (K + kBK - 1) / kBK;
-  const int koff = K - nk * kBK;                       // first K tile starts at k = koff (<= 0)
+  int nk = (K + kBK - 1) / kBK;
+  int koff = K - nk * kBK;                             // first K tile starts at k = koff (<= 0)
   const long long bz = blockIdx.y;
   const long long ka = kbeg + koff;
+  const __bf16* const A_in = A;
+  const __bf16* const B_in = B;
   A += bz * sa + (LA == 0 ? (long long)m0 * lda + ka : (long long)m0 + ka * lda);
   B += bz * sb + (LB == 0 ? (long long)n0 * ldb + ka : (long long)n0 + ka * ldb);
   C += bz * sc;
@@ -265,8 +280,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // ABL (timing-only ablation builds, w4_diag): 1 = zero-record descriptors (every DMA dropped in
   // the address unit, instruction stream kept), 2 = no K-loop ds_reads.
   const int nrec = (DIAG && ABL == 1) ? 0 : kNumRecords;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, nrec, kRsrcWord3);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, nrec, kRsrcWord3);
+  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, nrec, kRsrcWord3);
+  __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, nrec, kRsrcWord3);
 
   Stage<LA, BM> sta;
   Stage<LB, BM> stb;
@@ -314,6 +329,25 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     else af[q - NR] = rda.template read<1>(smem, sa_slot, q - NR);
   };
 
+  // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
+  // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
+  unsigned long long seg[4] = {0, 0, 0, 0};
+  unsigned long long t_loop0 = 0, t_loop1 = 0;
+  auto stamp = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (DIAG) {
+      KFW4_PIN();
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      KFW4_PIN();
+    }
+    return t;
+  };
+  using T = std::integral_constant<bool, true>;
+  using F = std::integral_constant<bool, false>;
+  unsigned long long sk_mask = 0;  // stream-K owner: which producer splits' partials the epilogue adds
+  int sk_base = 0, sk_stride = 0;  // ... split j's partial is slot sk_base + j * sk_stride
+  // prologue + K loop over the current (ra, rb, nk, koff): adds into acc
+  auto run_k = [&]() __attribute__((always_inline)) {
   // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
   int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
 #pragma unroll
@@ -341,19 +375,6 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   KFW4_PIN();
   __builtin_amdgcn_s_setprio(1);
 
-  // DIAG build only (cdna_hip_programming.md §7 'In-kernel stamps'): per-wave shader-clock sums of
-  // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
-  unsigned long long seg[4] = {0, 0, 0, 0};
-  unsigned long long t_loop0 = 0, t_loop1 = 0;
-  auto stamp = [&]() -> unsigned long long {
-    unsigned long long t = 0;
-    if (DIAG) {
-      KFW4_PIN();
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-      KFW4_PIN();
-    }
-    return t;
-  };
   auto body = [&](int kt, auto do_stage, auto do_next) {
     constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
     constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
@@ -408,8 +429,6 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       seg[3] += t4 - t3;
     }
   };
-  using T = std::integral_constant<bool, true>;
-  using F = std::integral_constant<bool, false>;
   if (DIAG) t_loop0 = stamp();
   int kt = 0;
   for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
@@ -429,6 +448,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   for (int i = 0; i < NR; ++i)
 #pragma unroll
     for (int n = 0; n < NR; ++n) asm volatile("" : "+a"(acc[i][n]));
+  };  // run_k
 
   // Epilogue. Lane (lr, lh) holds row lr, columns 4lh..4lh+3 of every 16x16 block n. For each pair
   // of blocks (n, n+1) one v_permlane16_swap per dword trades rows 1<->0 and 3<->2 of the lane
@@ -436,6 +456,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // columns: lh 0 -> block n cols 0-7, lh 1 -> block n+1 cols 0-7, lh 2 -> block n cols 8-15,
   // lh 3 -> block n+1 cols 8-15: one dwordx4 store per lane per pair. The lane id is re-derived
   // here (v_mbcnt) so no lane-derived VGPR has to survive the K loop.
+  auto epilogue = [&]() __attribute__((always_inline)) {
   const int elane = lane_id_fresh();
   const int elr = elane & 15, elh = elane >> 4;
   // Output granularity og (elements, uniform): the widest store every lane's 8-column run allows,
@@ -460,8 +481,26 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     for (int r = 0; r < 4; ++r) {
       float a;
       asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][n][r]));
-      v[r] = a * alpha;
+      v[r] = a;
     }
+    if constexpr (SK) {
+      // stream-K owner: add the producers' fp32 partials (same fragment layout as acc)
+      for (unsigned long long mk = (KFW4_SK_AB & 1) ? 0ull : sk_mask; mk; mk &= mk - 1) {
+        const int slot = sk_base + __builtin_ctzll(mk) * sk_stride;
+        // agent-coherent (sc1) loads: a producer on another XCD wrote them through its L2
+        unsigned long long* pp = reinterpret_cast<unsigned long long*>(
+            W + (long long)slot * BM * BN + (long long)(wm * WT + i * 16 + elr) * BN + wn * WT + n * 16 + elh * 4);
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 lo = __builtin_bit_cast(f32x2, __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const f32x2 hi = __builtin_bit_cast(f32x2, __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        v[0] += lo[0];
+        v[1] += lo[1];
+        v[2] += hi[0];
+        v[3] += hi[1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= alpha;
     if (HAS_BIAS) {
       if constexpr (vec) {
         const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
@@ -573,6 +612,187 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   } else {
     emit(F{}, store_og);
   }
+  };  // epilogue
+
+  if constexpr (SK) {
+    // ---- stream-K persistent schedule (batch 1) -------------------------------------------------
+    const int G = gridDim.x, KT = nk, koff_full = koff;
+    const int T_dp = nwg - nwg % G;
+    auto set_tile = [&](int w) __attribute__((always_inline)) {
+      const int gg = w / per_group, fm = gg * kGroupM;
+      const int gmm = min(tiles_m - fm, kGroupM);
+      const int tm_ = fm + (w % per_group) % gmm, tn_ = (w % per_group) / gmm;
+      m_lo = tm_ * BM;
+      n_lo = tn_ * BN;
+      m0 = min(m_lo, M - BM);
+      n0 = min(n_lo, N - BN);
+    };
+    auto set_k = [&](int k0, int k1) __attribute__((always_inline)) {  // K-tiles [k0, k1) of the current tile
+      const long long kofs = koff_full + (long long)kBK * k0;
+      const __bf16* a = A_in + (LA == 0 ? (long long)m0 * lda + kofs : (long long)m0 + kofs * lda);
+      const __bf16* b = B_in + (LB == 0 ? (long long)n0 * ldb + kofs : (long long)n0 + kofs * ldb);
+      ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, (short)0, nrec, kRsrcWord3);
+      rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, nrec, kRsrcWord3);
+      nk = k1 - k0;
+      koff = k0 == 0 ? koff_full : 0;  // only the tile's first K tile is partial
+    };
+    // zero the accumulators when `zero` is set, in place: an MFMA of zero fragments with C = 0 writes
+    // the AGPRs. The branch sits inside the asm, so every accumulator has one unconditional def per
+    // work item: a def under a branch gives the accumulators a phi at the join, which the allocator
+    // resolves through VGPR copies of all 256 (and spills). Each asm pads its MFMAs' write latency
+    // itself: the hazard recognizer cannot see into it, and a compiler copy of an accumulator
+    // placed right after it read the previous tile's value (stale r = 0 elements, r3 sk_diag).
+    static_assert(NR % 4 == 0, "zero_acc_if: 4 accumulators per asm");
+    auto zero_acc_if = [&](int zero) __attribute__((always_inline)) {
+      const bf16x8 z = {};
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int n = 0; n < NR; n += 4)
+          asm volatile(
+              "s_cmp_eq_u32 %4, 0\n\ts_cbranch_scc1 1f\n\t"
+              "v_mfma_f32_16x16x32_bf16 %0, %5, %5, 0\n\tv_mfma_f32_16x16x32_bf16 %1, %5, %5, 0\n\t"
+              "v_mfma_f32_16x16x32_bf16 %2, %5, %5, 0\n\tv_mfma_f32_16x16x32_bf16 %3, %5, %5, 0\n\t"
+              "s_nop 7\n\ts_nop 7\n\ts_nop 7\n1:"
+              : "+a"(acc[i][n]), "+a"(acc[i][n + 1]), "+a"(acc[i][n + 2]), "+a"(acc[i][n + 3])
+              : "s"(zero), "v"(z)
+              : "scc");
+    };
+    // one fp32 partial tile per producer unit, lane layout = the accumulator fragments
+    auto partial_at = [&](int slot, int i, int n) __attribute__((always_inline)) -> float* {
+      const int el = lane_id_fresh();
+      return W + (long long)slot * BM * BN + (long long)(wm * WT + i * 16 + (el & 15)) * BN + wn * WT + n * 16 +
+             (el >> 4) * 4;
+    };
+    // Schedule. The rem = T % G tiles past the whole waves are cut into S = kper K-splits each; in a
+    // partition (below) unit u = j * n + t (split j of its t-th tile, split-major) goes to the
+    // partition's block u % Gx, round u / Gx. Split-major keeps a round's blocks on the same K range
+    // of their tiles, so they share A / B panels in L2 like the data-parallel waves. The last split's
+    // block owns the tile; splits 0..S-2 store fp32 partials (slot u) and raise
+    // flag[u]. An owner waits only for smaller units (same or earlier rounds, whose producers never
+    // wait), so a co-resident grid cannot deadlock; a partial that misses the deadline is recomputed
+    // by the owner on top of its accumulators.
+    // One work loop, one unconditional run_k per item (the K loop and the epilogue are inlined once).
+    // kper < 0: test mode, producers publish a flag value no owner accepts (every owner takes the
+    // deadline path and recomputes the producers' splits)
+    const int rem = nwg - T_dp, S = kper < 0 ? -kper : kper;
+    const unsigned pub = kper < 0 ? ~sk_epoch : sk_epoch;
+    // XCD-aware: the leftover tiles are cut into P = 8 contiguous ranges (neighbours in the grouped
+    // raster share A / B panels) and range x is run by the blocks b % 8 == x, which the dispatcher
+    // places on one XCD (one L2). Round-robin over all blocks spread a tile's panel-sharing
+    // neighbours over all 8 L2s and ran HBM-bound. Only locality rests on the placement: every unit
+    // still runs exactly once, on whichever CU its block lands.
+    const int P = (G % 8 == 0 && rem >= 8) ? 8 : 1;
+    const int part = blockIdx.x % P, Gx = G / P;
+    const int t_begin = (int)((long long)part * rem / P);
+    const int nx = (int)((long long)(part + 1) * rem / P) - t_begin;
+    const int units = nx * S;
+    int dp_j = blockIdx.x, u = blockIdx.x / P;
+    int coll_j = S, coll_t = 0;  // an owner's next producer split to collect
+    int fb_j = -1;               // a producer split to recompute (deadline missed)
+    int cur_u = 0;
+    auto split_k = [&](int j) __attribute__((always_inline)) { set_k((int)((long long)j * KT / S), (int)((long long)(j + 1) * KT / S)); };
+    sk_stride = rem;
+    while (true) {
+      int role;  // 0: epilogue now, 1: producer, 2: owner (collect, then epilogue)
+      int zero = 1;
+      if (fb_j >= 0) {
+        split_k(fb_j);
+        fb_j = -1;
+        zero = 0;
+        role = 2;
+      } else if (dp_j < T_dp) {  // whole waves: plain tiles
+        sk_mask = 0;
+        set_tile(xcd_remap(dp_j, T_dp));
+        set_k(0, KT);
+        role = 0;
+        dp_j += G;
+      } else if (u < units) {
+        const int jj = u / nx, t = t_begin + (u - jj * nx);
+        sk_mask = 0;
+        set_tile(T_dp + t);
+        split_k(jj);
+        cur_u = jj * rem + t;  // partial slot / flag word
+        if (S == 1) {
+          role = 0;
+        } else if (jj < S - 1) {
+          role = 1;
+        } else {
+          role = 2;
+          coll_j = 0;
+          coll_t = t;
+          sk_base = t;
+        }
+        u += Gx;
+      } else {
+        break;
+      }
+      zero_acc_if(zero);
+      __syncthreads();  // the previous item's fragment reads are done before the ring refills
+      run_k();
+      if (role == 1) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+          for (int n = 0; n < NR; ++n) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v[r]) : "a"(acc[i][n][r]));
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            unsigned long long* pp = reinterpret_cast<unsigned long long*>(partial_at(cur_u, i, n));
+            if (!(KFW4_SK_AB & 1)) {
+              __hip_atomic_store(pp, __builtin_bit_cast(unsigned long long, (f32x2{v[0], v[1]})), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(pp + 1, __builtin_bit_cast(unsigned long long, (f32x2{v[2], v[3]})), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+        // The partials and flags move as agent-scope relaxed atomics (sc1: written through / read past
+        // the XCD's L2), so no agent-scope fence is needed: a release / acquire fence writes back /
+        // invalidates the whole L2 of the XCD, evicting the A / B panels every other block on it is
+        // streaming (that made each split cost about a whole tile). Completion of this wave's stores,
+        // then the barrier, orders them before the flag.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(sk_flags + cur_u, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      if (role == 2) {
+        while (coll_j < S - 1) {
+          const int ob = coll_j * rem + coll_t;
+          __syncthreads();
+          if (tid == 0) {
+            int ok = 0;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (true) {
+              if ((KFW4_SK_AB & 2) ||
+                  __hip_atomic_load(sk_flags + ob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sk_epoch) {
+                ok = 1;
+                break;
+              }
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kSkTimeoutTicks) break;
+              __builtin_amdgcn_s_sleep(4);
+            }
+            *reinterpret_cast<volatile __attribute__((address_space(3))) int*>(KFW4_LDS_PTR(smem)) = ok;  // ring idle
+          }
+          __syncthreads();
+          const int ok = __builtin_amdgcn_readfirstlane(
+              *reinterpret_cast<volatile __attribute__((address_space(3))) int*>(KFW4_LDS_PTR(smem)));
+          if (!ok) {  // producer not (yet) resident: its split becomes this block's next item
+            fb_j = coll_j++;
+            break;
+          }
+          sk_mask |= 1ull << coll_j;
+          ++coll_j;
+        }
+        if (fb_j >= 0) continue;
+      }
+      epilogue();
+    }
+    return;
+  }
+  run_k();
+  epilogue();
   if (DIAG) {
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores retired: the block's real end

@@ -72,6 +72,13 @@ int kfamd_w4_splitk_nt(const void* A, const void* B, float* W, int M, int N, int
 int kfamd_w4_splitk_t(int la, int lb, const void* A, const void* B, float* W, int M, int N, int K, int batch,
                       int splits, int kper, long long lda, long long ldb, long long stride_a, long long stride_b,
                       void* stream);
+// Stream-K (256 tile, NT, batch 1) for grids whose last wave would leave CUs idle: `grid` persistent
+// blocks (one per CU), the rem = tiles % grid leftover tiles in `splits` K-splits each; W = (splits -
+// 1) * rem x 256 x 256 fp32, flags = splits * rem words owned by the calling stream with a strictly
+// increasing non-zero epoch per call. Epilogues as kfamd_w4_launch_nt without the Aux output.
+int kfamd_w4_streamk_nt(const void* A, const void* B, void* C, const void* bias, const void* R, void* Aux, int M,
+                        int N, int K, long long lda, long long ldb, long long ldc, long long ldr, float alpha, int act,
+                        float* W, unsigned* flags, unsigned epoch, int grid, int splits, void* stream);
 int kfamd_splitk_reduce(const float* W, void* C, const void* bias, const void* R, void* Aux, int M, int N, int batch,
                         int splits, long long ldc, long long ldr, long long stride_c, long long stride_r, float alpha,
                         int act, void* stream);

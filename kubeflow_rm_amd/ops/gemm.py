@@ -155,6 +155,10 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
     if plan is not None and _splitk(0, 0, a3, b, c3, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, bias=bias,
                                     r_ptr=r_ptr, ldr=ldr, sr=sr, aux=None, alpha=alpha, act=act) == 0:
         return out
+    skp = streamk_plan(M, N, K, batch) if variant == "auto" and plan is None else None
+    if skp is not None and _streamk(a3, b, c3, M, N, K, lda, ldb, ldc, skp, bias=bias, r_ptr=r_ptr, ldr=ldr,
+                                     aux=None, alpha=alpha, act=act) == 0:
+        return out
     rc = _lib.lib().kfamd_gemm_nt_bf16_variant(
         VARIANTS[variant], a3.data_ptr(), b.data_ptr(), c3.data_ptr(),
         bias.data_ptr() if bias is not None else None, r_ptr,
@@ -207,6 +211,66 @@ def _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *,
                                  float(alpha), ACTS[act], st)
 
 
+# Stream-K (kfamd_w4_streamk_nt, gemm_w4.h SK): a 256x256-tile problem whose tile count leaves the
+# last wave of 256 CUs partly idle (e.g. 144 tiles of 3072^2: 56 % of one wave) runs as a persistent
+# grid of one block per CU: the whole waves as plain tiles, then the leftover tiles in S K-splits
+# each, round-robin over all blocks; the block with a tile's last split adds the others' fp32
+# partials in its epilogue (no reduce launch).
+# Off by default: correct (tests/test_gpu_kernels.py) but slower than the plain kernel on every
+# measured shape. Each split moves a 256 KB fp32 partial tile through HBM twice, which costs more
+# than the idle CUs it fills (profiles/r3_streamk: 3072^2 x 8192 at 3 splits 189 us vs 144 plain,
+# 120 us with the partial traffic ablated).
+STREAMK = False
+_STREAMK_MIN_KT = 16        # K-tiles (x64) per tile: shallower problems are prologue / epilogue bound
+_STREAMK_MAX_WAVES = 4      # beyond this the partial last wave costs < 1/8 of the run
+_STREAMK_UNIT_COST = 3      # per-split overhead in K-tiles (prologue, partial store / add, epilogue)
+_streamk_ws: dict = {}      # (device, stream) -> [W fp32 partials, flags u32, epoch]
+
+
+def streamk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
+    """(grid, splits) for a stream-K run of an NT problem that leaves the last wave under-filled, else None."""
+    if not STREAMK or batch != 1 or not _w4_nt_shape(M, N, K) or M < 256 or N < 256:
+        return None
+    tiles = -(-M // 256) * -(-N // 256)
+    kt = -(-K // 64)
+    G = _NUM_CUS
+    rem = tiles % G
+    if kt < _STREAMK_MIN_KT or rem == 0 or tiles > _STREAMK_MAX_WAVES * G or rem > G * 7 // 8:
+        return None
+
+    P = 8 if rem >= 8 else 1  # XCD partitions of the leftover tiles (gemm_w4.h SK)
+
+    def cost(S):  # leftover part: rounds of units, each ceil(KT / S) K-tiles + the per-unit overhead
+        return -(-S * -(-rem // P) // (G // P)) * (-(-kt // S) + (_STREAMK_UNIT_COST if S > 1 else 0))
+
+    best = min(range(1, min(64, kt // 4) + 1), key=lambda S: (cost(S), S))
+    if best == 1 or cost(best) >= 0.9 * cost(1):
+        return None
+    return G, best
+
+
+def _streamk(a, b, c, M, N, K, lda, ldb, ldc, plan, *, bias, r_ptr, ldr, aux, alpha, act,
+             _force_deadline: bool = False) -> int:
+    grid, splits = plan
+    rem = (-(-M // 256) * -(-N // 256)) % grid
+    key = (a.device, _stream_ptr(a))
+    ws = _streamk_ws.get(key)
+    need_w, need_f = max(1, (splits - 1) * rem) * 256 * 256, splits * rem
+    if ws is None or ws[0].numel() < need_w or ws[1].numel() < need_f:
+        old = (ws[0].numel(), ws[1].numel()) if ws is not None else (0, 0)
+        ws = [torch.empty(max(need_w, old[0]), dtype=torch.float32, device=a.device),
+              torch.zeros(max(need_f, old[1], 1024), dtype=torch.int32, device=a.device), 0]
+        _streamk_ws[key] = ws
+    ws[2] += 1
+    if ws[2] >= 2 ** 32 - 1:  # epochs never repeat a value a flag may still hold
+        ws[1].zero_()
+        ws[2] = 1
+    return _lib.lib().kfamd_w4_streamk_nt(
+        a.data_ptr(), b.data_ptr(), c.data_ptr(), bias.data_ptr() if bias is not None else None, r_ptr,
+        aux.data_ptr() if aux is not None else None, M, N, K, lda, ldb, ldc, ldr, float(alpha), ACTS[act],
+        ws[0].data_ptr(), ws[1].data_ptr(), ws[2], grid, -splits if _force_deadline else splits, _stream_ptr(a))
+
+
 def _ex(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, *, bias=None, residual=None, aux=None,
         alpha=1.0, act="none") -> int:
     """Raw kfamd_gemm_bf16_ex call (split-K when the problem under-fills the chip); returns the status
@@ -220,6 +284,11 @@ def _ex(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, *, bias=None
                      ldr=ldr, sr=sr, aux=aux, alpha=alpha, act=act)
         if rc == 0:
             return 0
+    # (the pre-activation output runs on the plain kernel: see kfamd_w4_streamk_nt)
+    skp = streamk_plan(M, N, K, batch) if la == 0 and lb == 0 and plan is None and aux is None else None
+    if skp is not None and _streamk(a, b, c, M, N, K, lda, ldb, ldc, skp, bias=bias, r_ptr=r_ptr, ldr=ldr,
+                                     aux=aux, alpha=alpha, act=act) == 0:
+        return 0
     return _lib.lib().kfamd_gemm_bf16_ex(
         la, lb, a.data_ptr(), b.data_ptr(), c.data_ptr(), bias.data_ptr() if bias is not None else None, r_ptr,
         aux.data_ptr() if aux is not None else None, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr,

@@ -374,6 +374,69 @@ def test_splitk_batched_matches_unsplit():
     _assert_close(whole, ref, 4096)
 
 
+@pytest.fixture
+def streamk_on():
+    from kubeflow_rm_amd.ops import gemm
+    old = gemm.STREAMK
+    gemm.STREAMK = True
+    yield
+    gemm.STREAMK = old
+
+
+@pytest.mark.parametrize("M,N,K", [(3072, 3072, 8192), (3000, 3000, 3000), (6144, 2048, 4096), (1000, 5000, 3000),
+                                   (2304, 2304, 1024), (1024, 8192, 8200)])
+def test_streamk_plan_and_numerics(M, N, K, streamk_on):
+    """Stream-K (persistent grid, the last partial wave's K-tiles shared over all CUs): the plan
+    picks it, the result matches fp32 (edge tiles, K tails, segments crossing tiles) and the plain
+    kernel's output."""
+    from kubeflow_rm_amd.ops import gemm, gemm_nt
+    grid, splits = gemm.streamk_plan(M, N, K)
+    assert grid == 256 and splits >= 2
+    a, b = _rand(M, K, seed=81), _rand(N, K, seed=82)
+    sk = gemm_nt(a, b)
+    _assert_close(sk, _ref_gemm(a, b), K)
+    gemm.STREAMK = False
+    dp = gemm_nt(a, b)
+    err = (sk.float() - dp.float()).abs().max().item()
+    assert err <= 1e-2 * (dp.float().abs().max().item() + 1e-3), err
+
+
+@pytest.mark.parametrize("act", ["none", "gelu_tanh", "silu", "relu"])
+def test_streamk_epilogues(act, streamk_on):
+    """bias / activation / residual on the stream-K owner's epilogue (adds the producers' fp32
+    partials first); the pre-activation output (plain kernel) next to it."""
+    from kubeflow_rm_amd.ops import gemm, gemm_nt, gemm_nt_preact
+    M, N, K = 3072, 3072, 4096
+    assert gemm.streamk_plan(M, N, K) is not None
+    a, b, bias = _rand(M, K, seed=83), _rand(N, K, seed=84, scale=0.1), _rand(N, seed=85)
+    _assert_close(gemm_nt(a, b, bias=bias, act=act, alpha=0.5), _ref_gemm(a, b, bias, act, alpha=0.5), K)
+    if act == "none":
+        r = _rand(M, N, seed=86)
+        _assert_close(gemm_nt(a, b, bias=bias, residual=r), _ref_gemm(a, b, bias, residual=r), K)
+    if act in ("gelu_tanh", "silu"):
+        y, z = gemm_nt_preact(a, b, bias, act)
+        _assert_close(z, _ref_gemm(a, b, bias), K)
+        _assert_close(y, _ref_gemm(a, b, bias, act), K)
+
+
+def test_streamk_deadline_path_and_epochs():
+    """Owners whose producers' partials never arrive (test mode: producers publish a flag value no
+    owner accepts) recompute those splits after the deadline, and the result is still exact; a
+    grid of 4x the CUs (not co-resident) and repeated calls (new epochs over the same flag words)
+    stay correct."""
+    from kubeflow_rm_amd.ops import gemm
+    M, N, K = 2304, 2304, 2048  # 81 tiles, 32 K-tiles each
+    a, b = _rand(M, K, seed=87), _rand(N, K, seed=88)
+    ref = _ref_gemm(a, b)
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    for plan, force in (((256, 3), True), ((256, 3), False), ((1024, 8), False), ((256, 4), False), ((256, 3), False)):
+        c.zero_()
+        rc = gemm._streamk(a, b, c, M, N, K, K, K, N, plan, bias=None, r_ptr=None, ldr=0, aux=None, alpha=1.0,
+                           act="none", _force_deadline=force)
+        assert rc == 0
+        _assert_close(c, ref, K)
+
+
 @pytest.mark.parametrize("M,N,K", [(1500, 1500, 1504), (1000, 1001, 512), (300, 130, 2048), (2000, 1499, 1000)])
 @pytest.mark.parametrize("v", ["w4", "w4s"])
 def test_gemm_odd_output_width(M, N, K, v):

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--variants", default="auto")
     ap.add_argument("--layouts", default="", help="MxNxK list: mm() in all four operand layouts vs torch")
     ap.add_argument("--splitk", default="", help="MxNxK list: gemm_nt with and without split-K vs torch")
+    ap.add_argument("--streamk", default="", help="MxNxK list: gemm_nt with and without stream-K vs torch")
     ap.add_argument("--linear", default="", help="TxKxN list: linear fwd+bwd (gelu, bias) vs torch autograd")
     args = ap.parse_args()
     import torch
@@ -96,6 +97,38 @@ def main():
             d[f"{k}_tflops"] = round(fl / v / 1e12, 1)
         emit(d)
         del a, b, c
+        torch.cuda.empty_cache()
+
+    for spec in [x for x in args.streamk.split(",") if x]:
+        from kubeflow_rm_amd.ops import gemm as G
+        M, N, K = map(int, spec.split("x"))
+        fl = 2.0 * M * N * K
+        iters = max(10, min(200, int(2e12 / fl) + 1))
+        a = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ref = torch.matmul(a, b.t())
+        res, err = {}, {}
+        for tag, on in (("sk", True), ("dp", False)):
+            G.STREAMK = on
+            for _ in range(3):
+                ops.gemm_nt(a, b, out=c)
+            err[tag] = float((c.float() - ref.float()).abs().max())
+            res[tag] = []
+        for _ in range(args.rounds):  # interleaved rounds
+            for tag, on in (("sk", True), ("dp", False)):
+                G.STREAMK = on
+                res[tag].append(timeit(lambda: ops.gemm_nt(a, b, out=c), iters, dev))
+            res.setdefault("torch", []).append(timeit(lambda: torch.matmul(a, b.t()), iters, dev))
+        G.STREAMK = True  # (for the plan below; restored after)
+        d = {"kind": "gemm_streamk_bf16", "M": M, "N": N, "K": K, "plan": G.streamk_plan(M, N, K),
+             "max_err_vs_torch": err}
+        for k, v in res.items():
+            d[f"{k}_us"] = round(min(v) * 1e6, 1)
+            d[f"{k}_tflops"] = round(fl / min(v) / 1e12, 1)
+        G.STREAMK = False
+        emit(d)
+        del a, b, c, ref
         torch.cuda.empty_cache()
 
     for spec in [x for x in args.layouts.split(",") if x]:
