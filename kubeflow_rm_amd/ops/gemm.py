@@ -168,15 +168,32 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
     return out
 
 
-# Split-K (kfamd_w4_splitk_*): a w4s block holds a CU (160 KB LDS ring), so a problem with fewer
-# 128x128 output tiles than CUs leaves most of the chip idle. It is split along K until it has about
-# one block per CU, each split at least _SPLITK_MIN_K deep (a shorter K loop is all prologue). Below
-# _SPLITK_MIN_TOTAL_K the unsplit kernel finishes in ~10 us and the extra reduce launch + fp32
-# round trip costs more than it saves (profiles/r3_splitk: 1000^3 10.7 us unsplit vs 15.9 split).
+# Split-K (kfamd_w4_splitk_*): a problem with too few 128x128 output tiles leaves CUs idle, so it is
+# split along K (fp32 partials + one reduce launch carrying the epilogue). The split count minimises a
+# small cost model: the busiest CU's share of MFMA work (a w4s block takes 80 KB of LDS, so two run
+# per CU, and a second resident block adds ~15 % throughput by hiding the other's latency), plus the
+# partials' HBM round trip and the reduce launch. Each split is at least _SPLITK_MIN_K deep. Below
+# _SPLITK_MIN_TOTAL_K the unsplit kernel finishes in ~10 us and the extra launch costs more than it
+# saves (profiles/r3_splitk: 1000^3 10.7 us unsplit vs 15.9 split). Measured against the one-block-
+# per-CU plan on the gpt-small weight-gradient shapes (profiles/r3_splitk_slots): 3072x768x32768
+# 256 -> 184 us, 768x3072x32768 259 -> 170, 2304x768x32768 146 -> 124.
 _NUM_CUS = 256
 _SPLITK_MIN_K = 512
 _SPLITK_MIN_TOTAL_K = 2048
+_SPLITK_MAX = 8
 SPLITK = True  # kill switch (benchmarks/tests compare against the unsplit kernel)
+_CU_TFLOPS = 5.1e12        # one w4s block alone on a CU (~1.3 PF/s over 256 CUs)
+_HBM_BPS = 5.0e12          # partial write + read in the split path
+_REDUCE_LAUNCH_S = 5e-6
+
+
+def _splitk_cost(M: int, N: int, K: int, batch: int, s: int) -> float:
+    tiles = -(-M // 128) * -(-N // 128) * batch
+    per_cu = -(-tiles * s // _NUM_CUS)
+    gemm = per_cu * (2.0 * 128 * 128 * -(-K // s)) / _CU_TFLOPS * (0.85 if per_cu >= 2 else 1.0)
+    if s == 1:
+        return gemm
+    return gemm + s * M * N * batch * 8.0 / _HBM_BPS + _REDUCE_LAUNCH_S
 
 
 def splitk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
@@ -184,10 +201,16 @@ def splitk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | Non
     if not SPLITK or K < _SPLITK_MIN_TOTAL_K or not _w4_shape(M, N, K):
         return None
     tiles = -(-M // 128) * -(-N // 128) * batch
-    want = min(_NUM_CUS // tiles if tiles else 0, K // _SPLITK_MIN_K, 8)
-    if want < 2:
+    if tiles >= 2 * _NUM_CUS:
         return None
-    kper = _round_up(-(-K // want), 64)
+    best, best_cost = 1, _splitk_cost(M, N, K, batch, 1)
+    for s in range(2, min(_SPLITK_MAX, K // _SPLITK_MIN_K) + 1):
+        c = _splitk_cost(M, N, K, batch, s)
+        if c < 0.95 * best_cost:  # a finer split has to pay for its extra partials clearly
+            best, best_cost = s, c
+    if best < 2:
+        return None
+    kper = _round_up(-(-K // best), 64)
     splits = -(-K // kper)
     return (splits, kper) if splits >= 2 else None
 

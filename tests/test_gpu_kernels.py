@@ -320,8 +320,8 @@ def test_linear_backward_layouts(act, shape):
         assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 1000, 2056), (1024, 1024, 4096), (1000, 1504, 3080), (136, 128, 2120),
-                                   (512, 768, 8192)])
+@pytest.mark.parametrize("M,N,K", [(1000, 1000, 4104), (1024, 1024, 4096), (1000, 1504, 6152), (136, 128, 2120),
+                                   (512, 768, 8192), (768, 3072, 16384)])
 def test_splitk_plan_and_numerics(M, N, K):
     """Split-K (fp32 partials + reduce) for under-filled problems: the plan splits, the result
     matches fp32 and the last (partial) split is zero-filled, through every operand layout."""
