@@ -214,7 +214,9 @@ def main() -> int:
                                             "(no torch import); cold_start_torch_ready_* = same path with a server "
                                             "that imports torch + runs a GEMM on the GPU before Ready; the GPU "
                                             "readiness op runs as a native sidecar overlapping the server start; "
-                                            "cold_start_odh_* = ODH path with the OAuth proxy + reconciliation lock")
+                                            "cold_start_odh_* = ODH path with the OAuth proxy + reconciliation lock; "
+                                            "cold_start_torch_ready_zygote_* = torch-ready server forked from the "
+                                            "kubelet's pre-imported interpreter (torch imported once per node)")
                 if args.coldstart_torch_runs > 0:
                     ct = measure_cold_start(runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready",
                                             namespace="bench-torch")
@@ -222,6 +224,16 @@ def main() -> int:
                     extra["cold_start_torch_ready_p50_s"] = ct["p50_s"]
                     extra["cold_start_torch_ready_p90_s"] = ct["p90_s"]
                     extra["cold_start_torch_ready_phases_p50_s"] = ct.get("phases_p50_s")
+                    extra["cold_start_torch_ready_server_p50_ms"] = ct.get("server_warmup_p50_ms")
+                    # the same server forked from the node's pre-imported interpreter (kubelet
+                    # --pod-zygote: torch imported once per node, GPU untouched before the fork)
+                    cz = measure_cold_start(runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready",
+                                            namespace="bench-zygote", zygote=True)
+                    extra["cold_start_torch_ready_zygote_runs"] = len(cz["runs"])
+                    extra["cold_start_torch_ready_zygote_p50_s"] = cz["p50_s"]
+                    extra["cold_start_torch_ready_zygote_p90_s"] = cz["p90_s"]
+                    extra["cold_start_torch_ready_zygote_phases_p50_s"] = cz.get("phases_p50_s")
+                    extra["cold_start_torch_ready_zygote_server_p50_ms"] = cz.get("server_warmup_p50_ms")
             except Exception as e:  # reported, never fatal for the GEMM number
                 extra["cold_start_error"] = f"{type(e).__name__}: {e}"
             try:  # BASELINE configs 3 and 5: Profile with GPU quota, TensorBoard + PVCViewer on a PVC

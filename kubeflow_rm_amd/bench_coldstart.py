@@ -112,7 +112,8 @@ def _reconcile_latency(url: str) -> dict:
 
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
                        readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
-                       settle_s: float = 0.5, server: str = "stub", odh_oauth: bool = False) -> dict:
+                       settle_s: float = 0.5, server: str = "stub", odh_oauth: bool = False,
+                       zygote: bool = False) -> dict:
     """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...},
     "reconcile": {controller: {"reconcile": {p50_ms, p99_ms}, "queue": {...}}}}.
 
@@ -122,13 +123,19 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     ServiceAccount / Service / Secret / Route and removes the lock once the SA has its image pull
     secret (Q7), and only then does the notebook controller scale the StatefulSet to 1.
 
+    ``zygote``: the kubelet forks the notebook server from a pre-imported interpreter (torch already
+    imported, GPU untouched: kubeflow_rm_amd/images/zygote.py) instead of starting a fresh one; the
+    runs start once the node's zygote serves (like a node with the image pre-pulled).
+
     ``settle_s``: pause after the previous run's pod is gone, so runs are independent cold starts.
     The amdgpu KFD tears a GPU process down asynchronously after it exits and the next open of
     /dev/kfd waits for that (100-130 ms right after an exit, 0.1 ms after >= 0.25 s:
     ``profiles/r1_coldstart2/kfd_gap.txt``); back to back, run i+1 would pay run i's teardown.
     """
     out_runs = []
-    with LocalCluster(gpus=gpus) as cl:
+    with LocalCluster(gpus=gpus, zygote=zygote) as cl:
+        if zygote:
+            cl.wait_zygotes(timeout=300)
         c = cl.client
         c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": namespace}})
         for i in range(runs):
@@ -185,7 +192,27 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                                          or {}).get("notebooks.kubeflow.org/cold-start-phases", "null"))
             except Exception:
                 pass
-            out_runs.append({"cold_start_s": t1 - t0, "phases": phases, "readiness_stages": stages,
+            warm = None
+            if server == "torch-ready":  # the server's own warmup timings (import / first GEMM)
+                try:
+                    import urllib.request
+                    ip = (pod.get("status") or {}).get("podIP")
+                    with urllib.request.urlopen(f"http://{ip}:8888/notebook/{namespace}/{name}/api/gpu", timeout=5) as r:
+                        warm = json.loads(r.read()).get("warmup")
+                    # container start -> server main -> listening -> pod Ready (wall clock, one host)
+                    st = next((cs for cs in (pod.get("status") or {}).get("containerStatuses") or []
+                               if cs.get("name") == name), {})
+                    t_cs = _ts(((st.get("state") or {}).get("running") or {}).get("startedAt"))
+                    if warm and t_cs and warm.get("main_ts") and warm.get("listen_ts"):
+                        warm["start_to_main_ms"] = round((warm["main_ts"] - t_cs) * 1e3, 1)
+                        warm["main_to_listen_ms"] = round((warm["listen_ts"] - warm["main_ts"]) * 1e3, 1)
+                        if t_ready:
+                            warm["listen_to_pod_ready_ms"] = round((t_ready - warm["listen_ts"]) * 1e3, 1)
+                        if t_init:
+                            warm["initialized_to_start_ms"] = round((t_cs - t_init) * 1e3, 1)
+                except Exception:  # noqa: BLE001 - diagnostics only
+                    pass
+            out_runs.append({"cold_start_s": t1 - t0, "phases": phases, "readiness_stages": stages, "server_warmup": warm,
                              "controller_phases_ms": ctl_phases,
                              "gpus": (obj.get("status") or {}).get("gpus"),
                              "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
@@ -207,12 +234,17 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     xs = [r["cold_start_s"] for r in out_runs]
     phase_keys = sorted({k for r in out_runs for k in r["phases"]})
     res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs, "server": server,
-           "odh_oauth": odh_oauth, "reconcile": recon,
+           "odh_oauth": odh_oauth, "zygote": zygote, "reconcile": recon,
            "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
     stage_keys = sorted({k for r in out_runs for k, v in r["readiness_stages"].items() if v is not None})
     if stage_keys:
         res["readiness_stages_p50_ms"] = {k: _pct([r["readiness_stages"][k] for r in out_runs
                                                     if r["readiness_stages"].get(k) is not None], 0.5) for k in stage_keys}
+    wk = sorted({k for r in out_runs for k, v in (r.get("server_warmup") or {}).items() if isinstance(v, (int, float))
+                 and not isinstance(v, bool)})
+    if wk:
+        res["server_warmup_p50_ms"] = {k: _pct([r["server_warmup"][k] for r in out_runs if (r.get("server_warmup") or {}).get(k)
+                                                is not None], 0.5) for k in wk if k.endswith("_ms")}
     rd = [r["gpuReadiness"] for r in out_runs if r.get("gpuReadiness")]
     if rd:
         res["readiness"] = rd[-1]
@@ -274,13 +306,16 @@ def main() -> int:
     p.add_argument("--no-readiness", action="store_true")
     p.add_argument("--settle", type=float, default=0.5, help="seconds between runs (0: back to back)")
     p.add_argument("--odh-oauth", action="store_true", help="ODH spawn path with the OAuth proxy (CS1)")
+    p.add_argument("--zygote", action="store_true", help="kubelet --pod-zygote (pre-imported interpreter)")
     p.add_argument("--server", choices=sorted(SERVERS), default="stub",
                    help="notebook server recipe: stub (no torch) or torch-ready (torch import + GEMM before Ready)")
     a = p.parse_args()
     r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness,
-                           settle_s=a.settle, server=a.server, odh_oauth=a.odh_oauth)
+                           settle_s=a.settle, server=a.server, odh_oauth=a.odh_oauth, zygote=a.zygote)
     print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
     print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
+    for x in r["runs"]:
+        print(json.dumps({"run_s": round(x["cold_start_s"], 4), "server_warmup": x.get("server_warmup")}))
     return 0
 
 

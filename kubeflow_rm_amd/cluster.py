@@ -33,8 +33,9 @@ def kflite_binary() -> Path:
 class LocalCluster:
     def __init__(self, data_dir: str | None = None, env: dict | None = None, args: list[str] | None = None,
                  controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0,
-                 ca_file: str | None = None):
+                 ca_file: str | None = None, zygote: bool = False):
         self._tmp = None
+        self.zygote = zygote  # kubelet --pod-zygote: Python containers fork from a pre-imported interpreter
         if data_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="kflite-")
             data_dir = self._tmp.name
@@ -69,6 +70,8 @@ class LocalCluster:
             # explicit: a kflite built elsewhere (sanitizer builds under build/) cannot derive the
             # package root from its own path, and pod image recipes run `python -m kubeflow_rm_amd...`
             cmd += ["--repo-root", str(ROOT)]
+        if self.zygote and "--pod-zygote" not in self.args:
+            cmd += ["--pod-zygote"]
         cmd += self.args
         self.log_path = Path(self.data_dir) / "kflite.log"
         self._log = open(self.log_path, "ab")
@@ -94,6 +97,24 @@ class LocalCluster:
             raise TimeoutError("kflite did not come up")
         self.client = KubeClient(self.url, ca_file=self.ca_file)
         return self
+
+    def wait_zygotes(self, timeout: float = 120.0) -> list[str]:
+        """Block until the kubelet's zygotes serve (their sockets exist), like waiting for a node's
+        image pre-pull; returns the socket paths. The first ``import torch`` on a fresh machine can
+        take a minute or two."""
+        root = Path(self.data_dir) / "kubelet"
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            socks = sorted(str(p) for p in root.glob("zygote-*.sock"))
+            logs = sorted(root.glob("zygote-*.log"))
+            if socks and len(socks) >= len(logs):
+                return socks
+            for lg in logs:
+                t = lg.read_text(errors="replace")
+                if "refusing to serve" in t or "Traceback" in t:
+                    raise RuntimeError(f"zygote failed: {t[-2000:]}")
+            time.sleep(0.05)
+        raise TimeoutError("zygote did not come up")
 
     def stop(self) -> None:
         if self.proc and self.proc.poll() is None:

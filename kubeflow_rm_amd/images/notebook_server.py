@@ -41,6 +41,7 @@ KERNELS: dict[str, dict] = {}
 TERMINALS: dict[str, dict] = {}
 STARTED = time.time()
 WARMUP: dict = {}
+PREINIT: dict = {}  # cumulative ms of the HIP pre-init thread's steps
 
 
 def _preinit_hip() -> threading.Thread | None:
@@ -61,9 +62,14 @@ def _preinit_hip() -> threading.Thread | None:
 
     def run():
         try:
+            t = time.perf_counter()
             hip = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
-            if hip.hipInit(0) == 0 and hip.hipSetDevice(0) == 0:
+            PREINIT["dlopen_ms"] = round((time.perf_counter() - t) * 1e3, 1)
+            ok = hip.hipInit(0) == 0
+            PREINIT["hip_init_ms"] = round((time.perf_counter() - t) * 1e3, 1)
+            if ok and hip.hipSetDevice(0) == 0:
                 hip.hipFree(None)  # creates the device context now
+                PREINIT["context_ms"] = round((time.perf_counter() - t) * 1e3, 1)
                 # the first GPU operation of the process pays ~90 ms more (the null stream's HW queue,
                 # the runtime's blit kernels): a memset + sync here, under the import. Only HIP's
                 # own entry points (ctypes drops the GIL for each); loading another HIP library on
@@ -73,6 +79,7 @@ def _preinit_hip() -> threading.Thread | None:
                     hip.hipMemset(buf, 0, ctypes.c_size_t(4096))
                     hip.hipDeviceSynchronize()
                     hip.hipFree(buf)
+                PREINIT["first_op_ms"] = round((time.perf_counter() - t) * 1e3, 1)
         except OSError:
             pass  # torch initialises on first use as usual
 
@@ -102,12 +109,19 @@ def warmup_torch() -> dict:
     c = ops.gemm_nt(ha.to(dev), hb.to(dev))
     hc = c.cpu()
     t3 = time.perf_counter()
-    rows = [0, 511, 1023]
-    ref = ha[rows].float() @ hb.float().t()
-    err = (hc[rows].float() - ref).abs().max().item()
-    ok = bool(torch.isfinite(hc[rows].float()).all().item()) and err <= 1e-2 * ref.abs().max().item() + 1e-2
-    return {"ok": ok, "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
+    # spot check: 3 rows x 16 columns against fp32 on the host. Small tensors (below the CPU kernels'
+    # parallel grain, so no OpenMP pool start) and index_select only:
+    # the full 3 x 1024 reference (a parallel 1M-element convert) and list indexing (the advanced-
+    # indexing path's first call) each cost 60-150 ms of CPU on the cold-start critical path
+    rows = torch.tensor([0, 511, 1023])
+    ref = ha.index_select(0, rows).float() @ hb[::64].float().t()
+    got = hc.index_select(0, rows)[:, ::64].float()
+    err = (got - ref).abs().max().item()
+    ok = bool(torch.isfinite(got).all().item()) and err <= 1e-2 * ref.abs().max().item() + 1e-2
+    t4 = time.perf_counter()
+    return {"ok": ok, "check_ms": round((t4 - t3) * 1e3, 1), "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
             "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1), "hip_preinit": pre is not None,
+            "preinit_ms": dict(PREINIT),
             "max_abs_err": err, "device": torch.cuda.get_device_name(dev)}
 
 
@@ -334,10 +348,14 @@ def make_handler(prefix: str):
 def main(argv=None) -> int:
     prefix = os.environ.get("NB_PREFIX", "")
     port = int(os.environ.get("NB_PORT", (os.environ.get("KFAMD_CONTAINER_PORTS") or "8888").split(",")[0] or 8888))
+    t_main = time.time()
     if os.environ.get("KFAMD_WARMUP") == "torch":
         WARMUP.update(warmup_torch())
         print(f"[kflite-notebook] warmup {json.dumps(WARMUP)}", flush=True)
     srv = serve(make_handler(prefix), port)
+    if WARMUP:  # wall-clock stamps for the cold-start breakdown (bench_coldstart)
+        WARMUP["main_ts"] = t_main
+        WARMUP["listen_ts"] = time.time()
     print(f"[kflite-notebook] serving {prefix or '/'} on {srv.server_address[0]}:{port} home={os.environ.get('HOME')}",
           flush=True)
     run_forever([srv])

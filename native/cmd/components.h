@@ -25,6 +25,7 @@ struct ComponentFlags {
   std::string pod_cidr_prefix = "127.20";
   std::string sysfs_root;  // GPU discovery root ("" = /sys)
   bool numa_pinning = true;
+  bool pod_zygote = false;
   // gateway (Istio ingress equivalent)
   std::string gateway_addr = "127.0.0.1";
   int64_t gateway_port = 0;

@@ -26,6 +26,8 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("pod-cidr-prefix", &pod_cidr_prefix, "127.20", "pod IPs are allocated as <prefix>.x.y (loopback)");
   f.add_string("sysfs-root", &sysfs_root, "", "sysfs root for GPU / PCI / NUMA discovery (default /sys)");
   f.add_bool("numa-pinning", &numa_pinning, true, "pin GPU pods to their GPUs' NUMA-local CPUs");
+  f.add_bool("pod-zygote", &pod_zygote, false,
+             "fork Python pod containers from a pre-imported interpreter per image recipe (torch preloaded)");
   f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
   f.add_int("gateway-port", &gateway_port, 0, "ingress gateway port (0 = ephemeral)");
   f.add_string("gateway-name", &gateway_name, "kubeflow/kubeflow-gateway", "VirtualService gateway served by the ingress");
@@ -207,6 +209,7 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     kc.gpus = static_cast<int>(I.f.gpus);
     kc.sysfs_root = I.f.sysfs_root;
     kc.numa_pinning = I.f.numa_pinning;
+    kc.pod_zygote = I.f.pod_zygote;
     I.kubelet = std::make_unique<Kubelet>(I.c, kc);
     I.kubelet->setup(mgr);
     if (I.api) {

@@ -11,10 +11,12 @@
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/syscall.h>
+#include <sys/un.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstring>
 #include <fstream>
 #include <regex>
@@ -111,7 +113,7 @@ const char* kDefaultRecipes = R"([
   {"match": "pvcviewer-controller", "argv": ["{bin}/pvcviewer-controller"], "passArgs": true},
   {"match": "admission-webhook|poddefaults-webhook", "argv": ["{bin}/admission-webhook"], "passArgs": true},
   {"match": "cmd:tensorboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
-  {"match": "cmd:jupyter|cmd:start-notebook.sh|cmd:start.sh", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
+  {"match": "cmd:jupyter|cmd:start-notebook.sh|cmd:start.sh", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"], "zygote": "torch,kubeflow_rm_amd.images.notebook_server"},
   {"match": "oauth-proxy|oauth_proxy", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.oauth_proxy"], "passArgs": true},
   {"match": "filebrowser", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.filebrowser"], "passArgs": true},
   {"match": "jupyter-web-app|crud-web-apps/jupyter", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.jupyter"]},
@@ -119,7 +121,7 @@ const char* kDefaultRecipes = R"([
   {"match": "volumes-web-app|crud-web-apps/volumes", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.volumes"]},
   {"match": "centraldashboard", "argv": ["{python}", "-m", "kubeflow_rm_amd.webapps.dashboard"]},
   {"match": "tensorboard|tensorflow/tensorflow", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.tensorboard_server"], "passArgs": true},
-  {"match": "jupyter|notebook|scipy|pytorch|tensorflow|codeserver|code-server|rstudio|workbench|s2i-", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"]},
+  {"match": "jupyter|notebook|scipy|pytorch|tensorflow|codeserver|code-server|rstudio|workbench|s2i-", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"], "zygote": "torch,kubeflow_rm_amd.images.notebook_server"},
   {"match": ".*", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.generic_server"], "passArgs": true}
 ])";
 }  // namespace
@@ -141,6 +143,10 @@ struct ContainerRt {
   double run_started = 0;
   Json last_state = Json::object();
   std::string log_path, term_path;
+  // forked by a zygote (not our child): the exit status arrives on this connection; -1 = our own
+  // child (waitpid). zorphan: the zygote went away first, exit is noticed by kill(pid, 0)
+  int zfd = -1;
+  bool zorphan = false;
 };
 
 struct Kubelet::PodRuntime {
@@ -226,7 +232,8 @@ Kubelet::~Kubelet() {
   if (wake_fd_ >= 0) ::close(wake_fd_);
 }
 
-std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::string* why) const {
+std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::string* why, std::string* zygote) const {
+  if (zygote) zygote->clear();
   std::vector<std::string> cmd, args;
   for (const auto& x : container["command"].as_array()) cmd.push_back(x.as_string());
   for (const auto& x : container["args"].as_array()) args.push_back(x.as_string());
@@ -258,6 +265,7 @@ std::vector<std::string> Kubelet::resolve_argv(const Json& container, std::strin
         out.insert(out.end(), args.begin(), args.end());
       }
       if (why) *why = "recipe:" + r["match"].as_string();
+      if (zygote) *zygote = r["zygote"].as_string();
       return out;
     }
   }
@@ -332,6 +340,7 @@ void Kubelet::start() {
     o["metadata"]["annotations"] = node.at_path({"metadata", "annotations"});
     return true;
   });
+  if (cfg_.pod_zygote) start_zygotes();
   running_ = true;
   hb_ = std::thread([this] {
     set_thread_name("kubelet-hb");
@@ -354,16 +363,27 @@ void Kubelet::watch_exit(pid_t pid, const std::string& ns, const std::string& na
 #endif
   if (pfd < 0) return;  // no pidfd (old kernel): the startup re-sync still notices the exit
   ::fcntl(pfd, F_SETFD, FD_CLOEXEC);
+  watch_fd(pfd, ns, name);
+}
+
+// fd readable = the container exited (a pidfd, or a zygote connection carrying the exit status);
+// the watch owns fd and closes it when it fires
+void Kubelet::watch_fd(int fd, const std::string& ns, const std::string& name) {
+  if (epfd_ < 0 || fd < 0) {
+    if (fd >= 0) ::close(fd);
+    return;
+  }
   std::lock_guard<std::mutex> g(watch_mu_);
-  watched_[pfd] = {ns, name};
+  watched_[fd] = {ns, name};
   epoll_event ev{};
   ev.events = EPOLLIN;
-  ev.data.fd = pfd;
-  if (::epoll_ctl(epfd_, EPOLL_CTL_ADD, pfd, &ev) != 0) {
-    watched_.erase(pfd);
-    ::close(pfd);
+  ev.data.fd = fd;
+  if (::epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev) != 0) {
+    watched_.erase(fd);
+    ::close(fd);
   }
 }
+
 
 void Kubelet::exit_watch_loop() {
   epoll_event evs[32];
@@ -432,6 +452,7 @@ void Kubelet::stop() {
     std::lock_guard<std::mutex> pl(rt->op_mu);
     terminate_pod(*rt, 0);
   }
+  stop_zygotes();
 }
 
 // ---- process management ---------------------------------------------------------------------------
@@ -508,7 +529,139 @@ bool reap(pid_t pid, int& exit_code, std::string& reason) {
   if (WIFSIGNALED(st) && WTERMSIG(st) == SIGKILL) reason = "Error";
   return true;
 }
+
+// Container start through a zygote (kubeflow_rm_amd/images/zygote.py): one connection per container,
+// request = the argv after the interpreter + env + cwd + log + CPU mask, reply {"pid": N}; the exit
+// status arrives later on the same connection (*zfd keeps it). Returns -1 when the zygote is not
+// there or refuses (the caller then spawns a fresh interpreter).
+pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv, const std::vector<std::string>& env,
+                   const std::string& cwd, const std::string& log_path, const std::vector<int>& cpus, int* zfd,
+                   std::string* err) {
+  const int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  sockaddr_un a{};
+  a.sun_family = AF_UNIX;
+  if (sock.size() >= sizeof a.sun_path) {
+    ::close(fd);
+    return -1;
+  }
+  std::memcpy(a.sun_path, sock.c_str(), sock.size() + 1);
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  Json req{{"argv", Json::array()}, {"env", Json::array()}, {"cwd", cwd}, {"log", log_path}, {"cpus", Json::array()}};
+  for (size_t i = 1; i < argv.size(); ++i) req["argv"].push_back(argv[i]);
+  for (const auto& e : env) req["env"].push_back(e);
+  for (int c : cpus) req["cpus"].push_back(static_cast<int64_t>(c));
+  const std::string line = req.dump() + "\n";
+  size_t off = 0;
+  while (off < line.size()) {
+    const ssize_t n = ::send(fd, line.data() + off, line.size() - off, MSG_NOSIGNAL);
+    if (n <= 0) {
+      ::close(fd);
+      return -1;
+    }
+    off += static_cast<size_t>(n);
+  }
+  // the reply line, byte by byte: a fast-exiting child's exit line may follow it in the same segment
+  std::string reply;
+  const double deadline = now_seconds() + 10;
+  while (reply.empty() || reply.back() != '\n') {
+    pollfd p{fd, POLLIN, 0};
+    const int left = static_cast<int>((deadline - now_seconds()) * 1000);
+    if (left <= 0 || ::poll(&p, 1, left) <= 0) break;
+    char ch;
+    if (::recv(fd, &ch, 1, 0) != 1) break;
+    reply += ch;
+  }
+  Json r;
+  if (!Json::try_parse(reply, r) || !r["pid"].is_number()) {
+    if (err) *err = "zygote: " + (r["error"].is_string() ? r["error"].as_string() : std::string("no reply"));
+    ::close(fd);
+    return -1;
+  }
+  *zfd = fd;
+  return static_cast<pid_t>(r["pid"].as_int());
+}
+
+// reap() for either kind of container process: our child (waitpid) or a zygote's (its status line)
+bool reap_container(pid_t pid, int& zfd, bool& zorphan, int& exit_code, std::string& reason) {
+  if (zorphan) {  // the zygote died before its child: no status to be had, only whether it is gone
+    if (::kill(pid, 0) == 0 || errno == EPERM) return false;
+    exit_code = 137;
+    reason = "Error";
+    zorphan = false;
+    return true;
+  }
+  if (zfd < 0) return reap(pid, exit_code, reason);
+  char buf[512];
+  const ssize_t n = ::recv(zfd, buf, sizeof buf - 1, MSG_DONTWAIT);
+  if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) return false;
+  ::close(zfd);
+  zfd = -1;
+  Json st;
+  if (n > 0 && Json::try_parse(std::string(buf, static_cast<size_t>(n)), st) && st["exit"].is_number()) {
+    exit_code = static_cast<int>(st["exit"].as_int());
+    const int sig = static_cast<int>(st["signal"].as_int());
+    reason = exit_code == 0 ? "Completed" : (exit_code == 137 ? "OOMKilled" : "Error");
+    if (sig == SIGKILL) reason = "Error";
+    return true;
+  }
+  zorphan = true;  // EOF without a status: the zygote is gone
+  return reap_container(pid, zfd, zorphan, exit_code, reason);
+}
 }  // namespace
+
+// One pre-imported interpreter per distinct recipe preload list. Started with the container base
+// env (PATH, LD_LIBRARY_PATH, HSA_*, KFAMD_*, PYTHONPATH = the framework): the forked containers
+// replace it with their own. A zygote that is not up yet (the first seconds after node start) or
+// that died is simply not used.
+void Kubelet::start_zygotes() {
+  std::vector<std::string> env;
+  for (char** e = environ; *e; ++e) {
+    std::string kv = *e;
+    const std::string k = kv.substr(0, kv.find('='));
+    if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || starts_with(k, "HSA_") ||
+        starts_with(k, "KFAMD_") || starts_with(k, "ROCM") || k == "OMP_NUM_THREADS" || k == "HOME")
+      env.push_back(kv);
+  }
+  env.push_back("PYTHONPATH=" + cfg_.repo_root);
+  env.push_back("PYTHONUNBUFFERED=1");
+  int i = 0;
+  for (const auto& r : recipes_.as_array()) {
+    const std::string pre = r["zygote"].as_string();
+    if (pre.empty() || zygotes_.count(pre)) continue;
+    Zygote z;
+    z.sock = cfg_.root_dir + "/zygote-" + std::to_string(i) + ".sock";
+    z.log = cfg_.root_dir + "/zygote-" + std::to_string(i) + ".log";
+    ++i;
+    std::string err;
+    z.pid = spawn({cfg_.python, "-m", "kubeflow_rm_amd.images.zygote", "--socket", z.sock, "--preload", pre}, env,
+                  cfg_.root_dir, z.log, &err);
+    if (z.pid < 0) continue;
+    zygotes_[pre] = z;
+  }
+}
+
+void Kubelet::stop_zygotes() {
+  for (auto& kv : zygotes_) {
+    if (kv.second.pid <= 0) continue;
+    ::kill(-kv.second.pid, SIGTERM);
+    int code = 0;
+    std::string reason;
+    const double deadline = now_seconds() + 5;
+    while (!reap(kv.second.pid, code, reason)) {
+      if (now_seconds() > deadline) {
+        ::kill(-kv.second.pid, SIGKILL);
+        ::waitpid(kv.second.pid, nullptr, 0);
+        break;
+      }
+      ::usleep(5000);
+    }
+    kv.second.pid = -1;
+  }
+}
 
 void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
   auto kill_all = [&](int sig) {
@@ -527,7 +680,7 @@ void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
       double deadline = now_seconds() + static_cast<double>(grace_s);
       int code = 0;
       std::string reason;
-      while (!reap(c.pid, code, reason)) {
+      while (!reap_container(c.pid, c.zfd, c.zorphan, code, reason)) {
         if (now_seconds() > deadline) {
           ::kill(-c.pid, SIGKILL);
           deadline = now_seconds() + 5;
@@ -869,8 +1022,8 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     std::vector<std::string> envv;
     std::map<std::string, std::string> envm;
     env_for(c, envv, envm);
-    std::string why;
-    std::vector<std::string> argv = resolve_argv(c, &why);
+    std::string why, zygote;
+    std::vector<std::string> argv = resolve_argv(c, &why, &zygote);
     for (auto& a : argv) a = expand_vars(a, envm);
     std::string wd = c["workingDir"].as_string();
     std::string cwd = rt->dir + "/rootfs";
@@ -894,7 +1047,24 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     if (cfg_.numa_pinning && !rt->gpus.devices.empty() &&
         (resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 || shares_pod_gpus(c)))
       cpus = alloc_->topology().local_cpus(rt->gpus.devices);
-    pid_t pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
+    pid_t pid = -1;
+    cr.zfd = -1;
+    cr.zorphan = false;
+    // a recipe with a zygote forks from the pre-imported interpreter when one serves it ('python -m'
+    // containers only); otherwise, or when it does not answer, a fresh interpreter as always
+    auto zy = zygote.empty() ? zygotes_.end() : zygotes_.find(zygote);
+    if (zy != zygotes_.end() && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
+      std::string zerr;
+      pid = zygote_spawn(zy->second.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
+      if (pid > 0) {
+        std::ofstream lf(cr.log_path, std::ios::app);
+        lf << "# kflite: forked from zygote " << zy->second.pid << " (preloaded " << zygote << ")\n";
+      } else if (!zerr.empty()) {
+        std::ofstream lf(cr.log_path, std::ios::app);
+        lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";
+      }
+    }
+    if (pid < 0) pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
     if (pid < 0) {
       cr.state = "waiting";
       cr.reason = "CreateContainerError";
@@ -907,7 +1077,12 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     cr.state = "running";
     cr.reason = "";
     cr.started_at = ms_now();
-    watch_exit(pid, r.ns, r.name);
+    if (cr.zfd >= 0) {
+      const int dfd = ::fcntl(cr.zfd, F_DUPFD_CLOEXEC, 0);  // the watch closes its own copy
+      if (dfd >= 0) watch_fd(dfd, r.ns, r.name);
+    } else {
+      watch_exit(pid, r.ns, r.name);
+    }
     cr.run_started = now_seconds();
     cr.ready = false;
     cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
@@ -962,7 +1137,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   auto handle_exit = [&](ContainerRt& cr) {
     int code = 0;
     std::string reason;
-    if (cr.pid <= 0 || cr.state != "running" || !reap(cr.pid, code, reason)) return false;
+    if (cr.pid <= 0 || cr.state != "running" || !reap_container(cr.pid, cr.zfd, cr.zorphan, code, reason)) return false;
     cr.pid = -1;
     cr.state = "terminated";
     cr.exit_code = code;

@@ -81,6 +81,9 @@ struct KubeletConfig {
   std::string recipes_file;  // optional JSON overriding the image recipes
   std::string sysfs_root;    // "" = /sys (tests: a fake tree with class/kfd, bus/pci, devices/system/node)
   bool numa_pinning = true;  // pin GPU pods' processes to their devices' NUMA-local CPUs
+  // start a pre-imported interpreter (kubeflow_rm_amd/images/zygote.py) per image recipe that names
+  // one, and fork Python containers from it instead of exec'ing a fresh interpreter
+  bool pod_zygote = false;
 };
 
 class Kubelet {
@@ -98,7 +101,9 @@ class Kubelet {
 
   struct PodRuntime;
   // image -> argv resolution (unit-tested)
-  std::vector<std::string> resolve_argv(const Json& container, std::string* why = nullptr) const;
+  // zygote (optional): the recipe's preload list when its containers may fork from a zygote
+  std::vector<std::string> resolve_argv(const Json& container, std::string* why = nullptr,
+                                        std::string* zygote = nullptr) const;
 
  private:
   Json node_object() const;
@@ -132,6 +137,15 @@ class Kubelet {
   std::mutex watch_mu_;
   std::map<int, std::pair<std::string, std::string>> watched_;  // pidfd -> pod ns/name
   std::thread exit_watch_;
+  void watch_fd(int fd, const std::string& ns, const std::string& name);
+  // pre-imported interpreters, keyed by preload list (cfg_.pod_zygote)
+  struct Zygote {
+    std::string sock, log;
+    pid_t pid = -1;
+  };
+  std::map<std::string, Zygote> zygotes_;
+  void start_zygotes();
+  void stop_zygotes();
 };
 
 class Gateway {

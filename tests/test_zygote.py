@@ -1,0 +1,125 @@
+"""Pod zygote (kubelet --pod-zygote, kubeflow_rm_amd/images/zygote.py): notebook containers fork
+from a pre-imported interpreter instead of exec'ing a fresh one.
+
+Checks the container contract survives the fork: the pod's own env, cwd, log and process session;
+readiness through the gateway; the exit status of a crashing container reaches the pod status
+(restartCount, terminated exit code) although the kubelet is not the process's parent; deletion
+kills the process; and a zygote that is gone falls back to a fresh interpreter.
+"""
+import json
+import os
+import signal
+import time
+import urllib.error
+import urllib.request
+from pathlib import Path
+
+import pytest
+
+from kubeflow_rm_amd.cluster import LocalCluster
+
+NB = "kubeflow.org/v1"
+
+
+def _notebook(name, ns, env=None):
+    c = {"name": name, "image": "jupyter-scipy:latest", "env": env or []}
+    return {"apiVersion": NB, "kind": "Notebook", "metadata": {"name": name, "namespace": ns},
+            "spec": {"template": {"spec": {"containers": [c]}}}}
+
+
+def _ready(o):
+    return (o.get("status") or {}).get("readyReplicas") == 1
+
+
+@pytest.fixture(scope="module")
+def zc():
+    with LocalCluster(gpus=0, zygote=True) as cl:
+        cl.wait_zygotes(timeout=300)
+        cl.client.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "zy"}})
+        yield cl
+
+
+def _get(url):
+    deadline = time.time() + 20
+    while True:
+        try:
+            with urllib.request.urlopen(url, timeout=5) as r:
+                return json.loads(r.read())
+        except (urllib.error.URLError, ConnectionError):
+            if time.time() > deadline:
+                raise
+            time.sleep(0.1)
+
+
+def _pid_of(c, pod, ns):
+    st = c.get("v1", "Pod", pod, ns)["status"]["containerStatuses"][0]
+    return int(st["containerID"].split("://")[1])
+
+
+def test_notebook_forks_from_zygote_with_its_own_env(zc):
+    c = zc.client
+    c.create(_notebook("z1", "zy", env=[{"name": "KFAMD_GPU_TOPOLOGY", "value": "zygote-env-test"}]))
+    c.wait_for(NB, "Notebook", "z1", "zy", _ready, timeout=60)
+    logs = c.pod_logs("z1-0", "zy")
+    assert "forked from zygote" in logs, logs
+    ip = c.get("v1", "Pod", "z1-0", "zy")["status"]["podIP"]
+    info = _get(f"http://{ip}:8888/notebook/zy/z1/api/gpu")
+    # the container's env (read by the server at run time; /proc/<pid>/environ shows the zygote's
+    # initial block, as for any process that changed its environment)
+    assert info["topology"] == "zygote-env-test" and "cpus_allowed" in info
+    assert "serving /notebook/zy/z1 on" in c.pod_logs("z1-0", "zy")
+    pid = _pid_of(c, "z1-0", "zy")
+    # its own session (the kubelet kills the process group) and the pod's working directory
+    assert os.getsid(pid) == pid
+    assert "/pods/zy_z1-0_" in os.readlink(f"/proc/{pid}/cwd")
+    # torch came preloaded: the container did not import it itself
+    assert "torch" in Path(f"/proc/{pid}/maps").read_text()
+
+
+def test_crash_exit_code_reaches_pod_status(zc):
+    c = zc.client
+    c.create(_notebook("z2", "zy", env=[{"name": "NB_PORT", "value": "not-a-port"}]))
+
+    def crashed(o):
+        for cs in (o.get("status") or {}).get("containerStatuses") or []:
+            last = (cs.get("lastState") or {}).get("terminated") or (cs.get("state") or {}).get("terminated")
+            if cs.get("restartCount", 0) >= 1 and last and last.get("exitCode") == 1:
+                return True
+        return False
+    c.wait_for("v1", "Pod", "z2-0", "zy", crashed, timeout=60)
+    assert "ValueError" in c.pod_logs("z2-0", "zy")
+    c.delete(NB, "Notebook", "z2", "zy")
+
+
+def test_delete_kills_forked_process(zc):
+    c = zc.client
+    pid = _pid_of(c, "z1-0", "zy")
+    c.delete(NB, "Notebook", "z1", "zy")
+    c.wait_gone("v1", "Pod", "z1-0", "zy", timeout=60)
+    deadline = time.time() + 10
+    while time.time() < deadline:
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.05)
+    else:
+        pytest.fail(f"forked container {pid} still alive after pod deletion")
+
+
+def test_fresh_interpreter_when_zygote_is_gone(zc):
+    c = zc.client
+    socks = zc.wait_zygotes()
+    zpid = None
+    for lg in (Path(zc.data_dir) / "kubelet").glob("zygote-*.log"):
+        for line in lg.read_text().splitlines():
+            if "ready on" in line:
+                zpid = int(line.split("pid ")[1].split()[0])
+    assert zpid
+    os.kill(zpid, signal.SIGKILL)  # its socket file stays behind: connect is refused
+    assert socks
+    c.create(_notebook("z3", "zy"))
+    c.wait_for(NB, "Notebook", "z3", "zy", _ready, timeout=60)
+    logs = c.pod_logs("z3-0", "zy")
+    assert "forked from zygote" not in logs
+    c.delete(NB, "Notebook", "z3", "zy")
