@@ -123,3 +123,18 @@ def test_fresh_interpreter_when_zygote_is_gone(zc):
     logs = c.pod_logs("z3-0", "zy")
     assert "forked from zygote" not in logs
     c.delete(NB, "Notebook", "z3", "zy")
+
+
+@pytest.mark.gpu
+def test_gpu_torch_ready_notebook_forked_from_zygote():
+    """On the GPU: the torch-ready server forked from the zygote creates its own HIP context on the
+    pod's GPU, runs the MFMA GEMM and passes the fp32 spot check; the GPU readiness sidecar passes."""
+    from kubeflow_rm_amd.bench_coldstart import measure_cold_start
+    r = measure_cold_start(runs=2, gpus_per_notebook=1, server="torch-ready", zygote=True, namespace="zy-gpu",
+                           settle_s=0.3, timeout=120)
+    assert len(r["runs"]) == 2
+    for run in r["runs"]:
+        w = run["server_warmup"] or {}
+        assert w.get("ok") is True, run
+        assert w.get("import_torch_ms", 1e9) < 50, w  # preloaded, not imported by the container
+    assert (r.get("readiness") or {}).get("ok", True) is not False
