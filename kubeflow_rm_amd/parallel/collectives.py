@@ -52,7 +52,7 @@ def fast_allreduce_sweep(sizes: list[int], algo: str, dtype=torch.bfloat16, iter
     """The hand-written IPC all-reduce (``algo`` = "oneshot" / "twoshot", kernels/allreduce_oneshot.hip)
     over the group's GPUs, one process per GPU; same algbw / busbw convention as ``allreduce_sweep``.
     Every result is checked against the exact rank-order sum of a known pattern."""
-    from .oneshot import IpcOneShotAllReduce
+    from .oneshot import IpcOneShotAllReduce, OneShotTimeout, agree
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -63,23 +63,35 @@ def fast_allreduce_sweep(sizes: list[int], algo: str, dtype=torch.bfloat16, iter
         for nbytes in sizes:
             n = max(nbytes // esz, 1)
             x = torch.full((n,), float(rank + 1), dtype=dtype, device=dev)
-            ar(x, algo=algo)
-            _sync(dev)
-            want = world * (world + 1) / 2
-            correct = bool(torch.all(x == want).item())
-            for _ in range(3):
+            err = None
+            try:
                 ar(x, algo=algo)
-            _sync(dev)
+                _sync(dev)
+                want = world * (world + 1) / 2
+                correct = bool(torch.all(x == want).item())
+                for _ in range(3):
+                    ar(x, algo=algo)
+                _sync(dev)
+                ar.check()
+            except OneShotTimeout as e:
+                err = e
+            # every rank leaves the sweep at the same size when any rank timed out (a rank raising
+            # alone would leave the others in the next barrier)
+            if not agree(err is None, group):
+                out.append({"bytes": n * esz, "error": f"{type(err).__name__}: {err}" if err else "timeout on a peer rank"})
+                break
             dist.barrier(group=group)
             t0 = time.perf_counter()
             for _ in range(iters):
                 ar(x, algo=algo)
             _sync(dev)
             dt = (time.perf_counter() - t0) / iters
+            ok_t = not ar.timed_out()
             algbw = n * esz / dt / 1e9
             out.append({"bytes": n * esz, "us": round(dt * 1e6, 1), "algbw_GBps": round(algbw, 1),
-                        "busbw_GBps": round(algbw * 2 * (world - 1) / world, 1), "correct": correct})
-        ar.check()
+                        "busbw_GBps": round(algbw * 2 * (world - 1) / world, 1), "correct": correct and ok_t})
+            if not agree(ok_t, group):
+                break
     finally:
         ar.close()
     return out
@@ -107,11 +119,18 @@ def xgmi_probe(nbytes: int = 256 << 20, iters: int = 5, group=None) -> dict:
     dist.all_gather_object(handles, h.raw, group=group)
     peers: dict[int, int] = {}
     try:
-        for r in range(world):
-            if r != rank:
-                p = ctypes.c_void_p()
-                _lib.check(L.kfamd_ipc_open(handles[r], ctypes.byref(p)), f"kfamd_ipc_open(rank {r})")
-                peers[r] = p.value
+        from .oneshot import agree
+        err = None
+        try:
+            for r in range(world):
+                if r != rank:
+                    p = ctypes.c_void_p()
+                    _lib.check(L.kfamd_ipc_open(handles[r], ctypes.byref(p)), f"kfamd_ipc_open(rank {r})")
+                    peers[r] = p.value
+        except RuntimeError as e:
+            err = e
+        if not agree(err is None, group):  # every rank gives up together (the finally's barrier matches)
+            raise err if err is not None else RuntimeError("xgmi_probe: a peer rank could not map the IPC buffers")
         src = torch.empty(nbytes, dtype=torch.uint8, device=dev).fill_(rank + 1)
         streams = {r: torch.cuda.Stream(dev) for r in peers}
         dist.barrier(group=group)

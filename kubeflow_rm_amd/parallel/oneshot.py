@@ -32,6 +32,16 @@ _DTYPES = {torch.float32: 0, torch.bfloat16: 1}
 MAX_BLOCKS = 64
 
 
+def agree(ok: bool, group=None) -> bool:
+    """True on every rank iff ``ok`` on every rank (one tiny all-reduce; on the device for RCCL)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return ok
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
 class OneShotTimeout(RuntimeError):
     """A peer missed the one-shot barrier deadline; this communicator is unusable."""
 
@@ -61,17 +71,28 @@ class IpcOneShotAllReduce:
         dist.all_gather_object(handles, mine, group=group)
         self._opened: list[int] = []
         bufs, flags = [], []
-        for r, (hb, hf) in enumerate(handles):
-            if r == self.rank:
-                bufs.append(self._own[0])
-                flags.append(self._own[1])
-                continue
-            pb, pf = ctypes.c_void_p(), ctypes.c_void_p()
-            _lib.check(L.kfamd_ipc_open(hb, ctypes.byref(pb)), f"kfamd_ipc_open(buffer of rank {r})")
-            _lib.check(L.kfamd_ipc_open(hf, ctypes.byref(pf)), f"kfamd_ipc_open(flags of rank {r})")
-            self._opened += [pb.value, pf.value]
-            bufs.append(pb.value)
-            flags.append(pf.value)
+        err = None
+        try:
+            for r, (hb, hf) in enumerate(handles):
+                if r == self.rank:
+                    bufs.append(self._own[0])
+                    flags.append(self._own[1])
+                    continue
+                pb, pf = ctypes.c_void_p(), ctypes.c_void_p()
+                _lib.check(L.kfamd_ipc_open(hb, ctypes.byref(pb)), f"kfamd_ipc_open(buffer of rank {r})")
+                self._opened.append(pb.value)
+                _lib.check(L.kfamd_ipc_open(hf, ctypes.byref(pf)), f"kfamd_ipc_open(flags of rank {r})")
+                self._opened.append(pf.value)
+                bufs.append(pb.value)
+                flags.append(pf.value)
+        except RuntimeError as e:
+            err = e
+        # collective outcome: a rank that could not map a peer must not leave the others waiting in
+        # the kernel's barrier or in the next collective; every rank raises together
+        if not agree(err is None, group):
+            self.close()
+            raise err if err is not None else RuntimeError(f"one-shot all-reduce: a peer of rank {self.rank} "
+                                                           "could not map the IPC buffers")
         arr = ctypes.c_void_p * 8
         self._in = arr(*bufs)
         self._flags = arr(*flags)
@@ -131,7 +152,7 @@ class IpcOneShotAllReduce:
     def close(self) -> None:
         L = _lib.lib()
         torch.cuda.synchronize()
-        if not self._own:
+        if not getattr(self, "_own", None):
             return
         for p in self._opened:
             L.kfamd_ipc_close(p)

@@ -204,3 +204,18 @@ def test_data_parallel_globally_unused_params_keep_grad_none():
     no weight decay / momentum to it; one used by another rank gets the reduced gradient."""
     for r in spawn(_dp_unused_worker, 2, timeout=120):
         assert r == {"e3_none": True, "e1_has": True, "e3_untouched": True}, r
+
+
+def _agree_worker(rank):
+    from kubeflow_rm_amd import parallel
+    from kubeflow_rm_amd.parallel.oneshot import agree
+    parallel.init(backend="gloo")
+    out = (agree(True), agree(rank != 2), agree(rank == 0 or True))
+    parallel.shutdown()
+    return out
+
+
+def test_ipc_setup_outcome_is_agreed_by_every_rank():
+    """oneshot.agree: the IPC all-reduce setup, the fast sweep and the xGMI probe fail on every rank
+    together (one rank unable to map a peer must not leave the others in the next collective)."""
+    assert spawn(_agree_worker, 4) == [(True, False, True)] * 4
