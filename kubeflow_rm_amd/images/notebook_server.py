@@ -122,7 +122,7 @@ def warmup_torch() -> dict:
     return {"ok": ok, "check_ms": round((t4 - t3) * 1e3, 1), "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
             "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1), "hip_preinit": pre is not None,
             "preinit_ms": dict(PREINIT),
-            "max_abs_err": err, "device": torch.cuda.get_device_name(dev)}
+            "max_abs_err": err}
 
 
 def _now() -> str:
@@ -294,6 +294,11 @@ def make_handler(prefix: str):
                     return self.send_json(200, [{"name": t["name"], "last_activity": t["last_activity"]}
                                                 for t in TERMINALS.values()])
             if p == "/api/gpu":
+                if WARMUP and "device" not in WARMUP:
+                    # looked up on the first request, not before Ready: torch's device-properties
+                    # query cost ~100 ms of the cold start
+                    import torch
+                    WARMUP["device"] = torch.cuda.get_device_name(0)
                 info = {"HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES"),
                         "ring": os.environ.get("KFAMD_XGMI_RING"),
                         "topology": os.environ.get("KFAMD_GPU_TOPOLOGY"), "warmup": WARMUP or None,

@@ -52,7 +52,44 @@ def _time_init() -> dict:
     return out
 
 
+def _time_steps() -> dict:
+    """First-use cost of each kind of first GPU operation, in order, after init + context."""
+    out = {}
+    hip = ctypes.CDLL(_lib(), mode=ctypes.RTLD_GLOBAL)
+    t = time.perf_counter()
+
+    def lap(name):
+        nonlocal t
+        hip.hipDeviceSynchronize()
+        now = time.perf_counter()
+        out[name] = round((now - t) * 1e3, 1)
+        t = now
+    hip.hipInit(0)
+    hip.hipSetDevice(0)
+    hip.hipFree(None)
+    lap("init_context_ms")
+    s = ctypes.c_void_p()
+    hip.hipStreamCreate(ctypes.byref(s))
+    lap("stream_create_ms")
+    buf = ctypes.c_void_p()
+    hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(1 << 20))
+    lap("malloc_ms")
+    host = ctypes.create_string_buffer(1 << 20)
+    hip.hipMemcpy(buf, host, ctypes.c_size_t(1 << 20), 1)  # H2D
+    lap("memcpy_h2d_ms")
+    hip.hipMemcpy(host, buf, ctypes.c_size_t(1 << 20), 2)  # D2H
+    lap("memcpy_d2h_ms")
+    hip.hipMemsetAsync(buf, 0, ctypes.c_size_t(4096), s)
+    lap("memset_ms")
+    hip.hipMemsetAsync(buf, 1, ctypes.c_size_t(4096), s)
+    lap("memset2_ms")
+    return out
+
+
 def child(mode: str) -> None:
+    if mode == "steps":
+        print(json.dumps({"mode": mode, "comgr_cache": os.environ.get("AMD_COMGR_CACHE_DIR"), **_time_steps()}), flush=True)
+        return
     if mode in ("torch", "forked", "forked_env"):
         t = time.perf_counter()
         import torch  # noqa: F401
@@ -87,6 +124,14 @@ def child(mode: str) -> None:
 def main() -> int:
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         child(sys.argv[2])
+        return 0
+    if len(sys.argv) > 1 and sys.argv[1] == "--steps":
+        import tempfile
+        cache = tempfile.mkdtemp(prefix="comgr-")
+        for rep in range(4):  # 1st run fills the comgr cache, later runs hit it
+            subprocess.run([sys.executable, __file__, "--child", "steps"], check=True, timeout=120,
+                           env={**os.environ, "AMD_COMGR_CACHE_DIR": cache})
+            time.sleep(0.3)
         return 0
     for rep in range(3):
         for mode in ("bare", "torch", "forked", "forked_env"):
