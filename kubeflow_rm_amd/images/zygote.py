@@ -143,7 +143,13 @@ def serve(sock_path: str, preload: list[str]) -> int:
     except FileNotFoundError:
         pass
     lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    try:
+        os.unlink(sock_path + ".tmp")
+    except FileNotFoundError:
+        pass
     lsock.bind(sock_path + ".tmp")
+    # only the kubelet's user may ask for a process (a request names the env, cwd and log file)
+    os.chmod(sock_path + ".tmp", 0o600)
     lsock.listen(64)
     os.rename(sock_path + ".tmp", sock_path)  # the socket appears only once the zygote accepts
     print(f"[zygote] pid {os.getpid()} ready on {sock_path}: preloaded {preload} in {import_s:.2f} s", flush=True)
