@@ -13,6 +13,8 @@
 //              gives every pod its own loopback IP (127.20.x.y) so every notebook listens on :8888,
 //              materialises volumes (emptyDir / PVC / configMap / secret) under the pod sandbox,
 //              runs init containers in order, HTTP/TCP/exec probes, restart policies with back-off,
+//              optionally forks Python containers from a per-recipe pre-imported interpreter
+//              (--pod-zygote: torch imported once per node, kubeflow_rm_amd/images/zygote.py),
 //              graceful termination, termination messages, container logs, and full pod status with
 //              millisecond timestamps (the cold-start phase breakdown of SURVEY §5.1).
 //   Gateway    HTTP reverse proxy that serves Istio VirtualServices (uri prefix match, rewrite,
