@@ -659,7 +659,7 @@ void Kubelet::stop_zygotes() {
       }
       ::usleep(5000);
     }
-    kv.second.pid = -1;
+    // the entry stays as it is (reconcile workers may still read it; a connect is simply refused)
   }
 }
 
