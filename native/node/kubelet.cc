@@ -629,6 +629,7 @@ void Kubelet::start_zygotes() {
   env.push_back("PYTHONPATH=" + cfg_.repo_root);
   env.push_back("PYTHONUNBUFFERED=1");
   int i = 0;
+  std::lock_guard<std::mutex> g(zy_mu_);
   for (const auto& r : recipes_.as_array()) {
     const std::string pre = r["zygote"].as_string();
     if (pre.empty() || zygotes_.count(pre)) continue;
@@ -645,7 +646,12 @@ void Kubelet::start_zygotes() {
 }
 
 void Kubelet::stop_zygotes() {
-  for (auto& kv : zygotes_) {
+  std::map<std::string, Zygote> zs;
+  {
+    std::lock_guard<std::mutex> g(zy_mu_);
+    zs = zygotes_;
+  }
+  for (auto& kv : zs) {
     if (kv.second.pid <= 0) continue;
     ::kill(-kv.second.pid, SIGTERM);
     int code = 0;
@@ -1052,13 +1058,18 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     cr.zorphan = false;
     // a recipe with a zygote forks from the pre-imported interpreter when one serves it ('python -m'
     // containers only); otherwise, or when it does not answer, a fresh interpreter as always
-    auto zy = zygote.empty() ? zygotes_.end() : zygotes_.find(zygote);
-    if (zy != zygotes_.end() && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
+    Zygote zy;
+    if (!zygote.empty()) {
+      std::lock_guard<std::mutex> g(zy_mu_);
+      auto it = zygotes_.find(zygote);
+      if (it != zygotes_.end()) zy = it->second;
+    }
+    if (zy.pid > 0 && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
       std::string zerr;
-      pid = zygote_spawn(zy->second.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
+      pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
       if (pid > 0) {
         std::ofstream lf(cr.log_path, std::ios::app);
-        lf << "# kflite: forked from zygote " << zy->second.pid << " (preloaded " << zygote << ")\n";
+        lf << "# kflite: forked from zygote " << zy.pid << " (preloaded " << zygote << ")\n";
       } else if (!zerr.empty()) {
         std::ofstream lf(cr.log_path, std::ios::app);
         lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";

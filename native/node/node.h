@@ -145,7 +145,8 @@ class Kubelet {
     std::string sock, log;
     pid_t pid = -1;
   };
-  std::map<std::string, Zygote> zygotes_;
+  std::map<std::string, Zygote> zygotes_;  // guarded by zy_mu_ (start() runs after the workers)
+  std::mutex zy_mu_;
   void start_zygotes();
   void stop_zygotes();
 };
