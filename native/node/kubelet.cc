@@ -410,7 +410,10 @@ void Kubelet::exit_watch_loop() {
 
 void Kubelet::heartbeat_loop() {
   while (running_) {
-    for (int i = 0; i < 100 && running_; ++i) ::usleep(100000);
+    for (int i = 0; i < 100 && running_; ++i) {
+      ::usleep(100000);
+      if (cfg_.pod_zygote && i % 10 == 9 && running_) supervise_zygotes();
+    }
     if (!running_) break;
     c_->update_with_retry(
         "v1", "Node", "", cfg_.node_name,
@@ -617,7 +620,7 @@ bool reap_container(pid_t pid, int& zfd, bool& zorphan, int& exit_code, std::str
 // env (PATH, LD_LIBRARY_PATH, HSA_*, KFAMD_*, PYTHONPATH = the framework): the forked containers
 // replace it with their own. A zygote that is not up yet (the first seconds after node start) or
 // that died is simply not used.
-void Kubelet::start_zygotes() {
+bool Kubelet::spawn_zygote(Zygote& z) {
   std::vector<std::string> env;
   for (char** e = environ; *e; ++e) {
     std::string kv = *e;
@@ -628,20 +631,46 @@ void Kubelet::start_zygotes() {
   }
   env.push_back("PYTHONPATH=" + cfg_.repo_root);
   env.push_back("PYTHONUNBUFFERED=1");
+  std::string err;
+  z.pid = spawn({cfg_.python, "-m", "kubeflow_rm_amd.images.zygote", "--socket", z.sock, "--preload", z.preload}, env,
+                cfg_.root_dir, z.log, &err);
+  z.started = now_seconds();
+  return z.pid > 0;
+}
+
+void Kubelet::start_zygotes() {
   int i = 0;
   std::lock_guard<std::mutex> g(zy_mu_);
   for (const auto& r : recipes_.as_array()) {
     const std::string pre = r["zygote"].as_string();
     if (pre.empty() || zygotes_.count(pre)) continue;
     Zygote z;
+    z.preload = pre;
     z.sock = cfg_.root_dir + "/zygote-" + std::to_string(i) + ".sock";
     z.log = cfg_.root_dir + "/zygote-" + std::to_string(i) + ".log";
     ++i;
-    std::string err;
-    z.pid = spawn({cfg_.python, "-m", "kubeflow_rm_amd.images.zygote", "--socket", z.sock, "--preload", pre}, env,
-                  cfg_.root_dir, z.log, &err);
-    if (z.pid < 0) continue;
-    zygotes_[pre] = z;
+    if (spawn_zygote(z)) zygotes_[pre] = z;
+  }
+}
+
+// A zygote that exited (killed, OOM, crashed) is started again; containers meanwhile start fresh
+// interpreters. One that keeps exiting right after its start (e.g. it refused to serve because its
+// preload opened the GPU driver) is given up after three tries.
+void Kubelet::supervise_zygotes() {
+  std::lock_guard<std::mutex> g(zy_mu_);
+  for (auto& kv : zygotes_) {
+    Zygote& z = kv.second;
+    int code = 0;
+    std::string reason;
+    if (z.pid <= 0 || !reap(z.pid, code, reason)) continue;
+    z.quick_exits = now_seconds() - z.started < 30 ? z.quick_exits + 1 : 0;
+    {
+      std::ofstream lf(z.log, std::ios::app);
+      lf << "# kflite: zygote " << z.pid << " exited (" << code << ")"
+         << (z.quick_exits >= 3 ? "; not restarted (exits right after start)" : "; restarting") << "\n";
+    }
+    z.pid = -1;
+    if (z.quick_exits < 3) spawn_zygote(z);
   }
 }
 

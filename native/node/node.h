@@ -142,13 +142,17 @@ class Kubelet {
   void watch_fd(int fd, const std::string& ns, const std::string& name);
   // pre-imported interpreters, keyed by preload list (cfg_.pod_zygote)
   struct Zygote {
-    std::string sock, log;
+    std::string preload, sock, log;
     pid_t pid = -1;
+    double started = 0;
+    int quick_exits = 0;  // exits within 30 s of a start, in a row: 3 and it is not restarted
   };
   std::map<std::string, Zygote> zygotes_;  // guarded by zy_mu_ (start() runs after the workers)
   std::mutex zy_mu_;
   void start_zygotes();
   void stop_zygotes();
+  void supervise_zygotes();  // heartbeat thread: restart a zygote that exited
+  bool spawn_zygote(Zygote& z);
 };
 
 class Gateway {

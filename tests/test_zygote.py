@@ -107,7 +107,7 @@ def test_delete_kills_forked_process(zc):
         pytest.fail(f"forked container {pid} still alive after pod deletion")
 
 
-def test_fresh_interpreter_when_zygote_is_gone(zc):
+def test_fresh_interpreter_when_zygote_is_gone_then_restarted(zc):
     c = zc.client
     socks = zc.wait_zygotes()
     zpid = None
@@ -123,6 +123,21 @@ def test_fresh_interpreter_when_zygote_is_gone(zc):
     logs = c.pod_logs("z3-0", "zy")
     assert "forked from zygote" not in logs
     c.delete(NB, "Notebook", "z3", "zy")
+    # the kubelet restarts the zygote (heartbeat-thread supervision), and containers fork from it again
+    deadline = time.time() + 120
+    new_pid = None
+    while time.time() < deadline and new_pid is None:
+        for lg in (Path(zc.data_dir) / "kubelet").glob("zygote-*.log"):
+            for line in lg.read_text().splitlines():
+                if "ready on" in line and int(line.split("pid ")[1].split()[0]) != zpid:
+                    new_pid = int(line.split("pid ")[1].split()[0])
+        time.sleep(0.2)
+    assert new_pid, "zygote not restarted"
+    c.wait_gone("v1", "Pod", "z3-0", "zy", timeout=60)
+    c.create(_notebook("z4", "zy"))
+    c.wait_for(NB, "Notebook", "z4", "zy", _ready, timeout=60)
+    assert f"forked from zygote {new_pid}" in c.pod_logs("z4-0", "zy")
+    c.delete(NB, "Notebook", "z4", "zy")
 
 
 @pytest.mark.gpu
