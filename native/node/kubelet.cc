@@ -670,7 +670,9 @@ void Kubelet::supervise_zygotes() {
          << (z.quick_exits >= 3 ? "; not restarted (exits right after start)" : "; restarting") << "\n";
     }
     z.pid = -1;
-    if (z.quick_exits < 3) spawn_zygote(z);
+    static const auto restarts =
+        Registry::global().counter("kubelet_zygote_restarts_total", "pre-imported interpreters restarted after an exit");
+    if (z.quick_exits < 3 && spawn_zygote(z)) restarts->inc();
   }
 }
 
@@ -1104,7 +1106,13 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";
       }
     }
-    if (pid < 0) pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
+    static const auto starts = Registry::global().counter(
+        "kubelet_container_starts_total", "container processes started, by how: zygote fork or fresh exec", {"mode"});
+    if (pid > 0) starts->inc({"zygote"});
+    if (pid < 0) {
+      pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
+      if (pid > 0) starts->inc({"fresh"});
+    }
     if (pid < 0) {
       cr.state = "waiting";
       cr.reason = "CreateContainerError";

@@ -137,6 +137,11 @@ def test_fresh_interpreter_when_zygote_is_gone_then_restarted(zc):
     c.create(_notebook("z4", "zy"))
     c.wait_for(NB, "Notebook", "z4", "zy", _ready, timeout=60)
     assert f"forked from zygote {new_pid}" in c.pod_logs("z4-0", "zy")
+    with urllib.request.urlopen(zc.url + "/metrics", timeout=10) as r:
+        metrics = r.read().decode()
+    assert 'kubelet_container_starts_total{mode="zygote"}' in metrics
+    assert 'kubelet_container_starts_total{mode="fresh"}' in metrics
+    assert "kubelet_zygote_restarts_total 1" in metrics
     c.delete(NB, "Notebook", "z4", "zy")
 
 
