@@ -548,6 +548,106 @@ def cmd_logs(client: KubeClient, a, out=sys.stdout) -> int:
             seen = len(text)
 
 
+_SAMPLE_RE = None
+
+
+def parse_samples(text: str) -> list[tuple[str, dict, float]]:
+    """Prometheus text exposition -> [(metric, {label: value}, sample value)] (no histograms needed)."""
+    import re
+    global _SAMPLE_RE
+    if _SAMPLE_RE is None:
+        _SAMPLE_RE = (re.compile(r'^([a-zA-Z_:][a-zA-Z0-9_:]*)(?:\{(.*)\})?\s+(\S+)'), re.compile(r'(\w+)="((?:[^"\\]|\\.)*)"'))
+    line_re, label_re = _SAMPLE_RE
+    out = []
+    for line in text.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        m = line_re.match(line)
+        if not m:
+            continue
+        try:
+            v = float(m.group(3))
+        except ValueError:
+            continue
+        out.append((m.group(1), dict(label_re.findall(m.group(2) or "")), v))
+    return out
+
+
+def _gib(b: float | None) -> str:
+    return "-" if b is None else f"{b / (1 << 30):.1f}Gi"
+
+
+def gpu_table(samples: list[tuple[str, dict, float]]) -> dict[str, dict]:
+    """Per-GPU view of the kubelet's device-plugin and AMD SMI series (node-level ``kfctl top``)."""
+    gpus: dict[str, dict] = {}
+    for name, lab, v in samples:
+        if not name.startswith("kfamd_gpu_") or "gpu" not in lab:
+            continue
+        g = gpus.setdefault(lab["gpu"], {"gpu": lab["gpu"]})
+        key = name[len("kfamd_gpu_"):]
+        if key == "allocated" and v >= 1:
+            g["pod"] = f"{lab.get('namespace', '')}/{lab.get('pod', '')}"
+        elif key == "temperature_celsius":
+            g[f"temp_{lab.get('sensor', '')}"] = v
+        elif key in ("gfx_activity_percent", "hbm_activity_percent", "busy_percent", "vram_used_bytes",
+                     "vram_total_bytes", "power_watts", "gfxclk_mhz"):
+            g[key] = v
+            if lab.get("pod"):
+                g.setdefault("pod", f"{lab.get('namespace', '')}/{lab['pod']}")
+    return gpus
+
+
+def cmd_top(client: KubeClient, a, out=sys.stdout) -> int:
+    """``top node``: one row per MI355X (holding pod, GFX / HBM activity, VRAM, power, clock, hotspot);
+    ``top pod``: per pod, its GPUs and their summed use. From the kubelet's /metrics series."""
+    text = client._req("GET", "/metrics", raw=True)
+    gpus = gpu_table(parse_samples(text))
+    if not gpus:
+        raise KubectlError("no GPU metrics from the node (kubelet metrics not registered)")
+    num = lambda k: (lambda g: g.get(k))  # noqa: E731
+    if a.what in ("node", "nodes", "no", "gpu", "gpus"):
+        rows = [["GPU", "POD", "GFX%", "HBM%", "VRAM", "POWER", "SCLK", "HOTSPOT"]]
+        for key in sorted(gpus, key=lambda x: int(x) if x.isdigit() else 0):
+            g = gpus[key]
+            act = g.get("gfx_activity_percent", g.get("busy_percent"))
+            rows.append([key, g.get("pod", "<none>"), "-" if act is None else f"{act:.0f}%",
+                         "-" if num("hbm_activity_percent")(g) is None else f"{g['hbm_activity_percent']:.0f}%",
+                         f"{_gib(g.get('vram_used_bytes'))}/{_gib(g.get('vram_total_bytes'))}",
+                         "-" if g.get("power_watts") is None else f"{g['power_watts']:.0f}W",
+                         "-" if g.get("gfxclk_mhz") is None else f"{g['gfxclk_mhz']:.0f}MHz",
+                         "-" if g.get("temp_hotspot") is None else f"{g['temp_hotspot']:.0f}C"])
+    elif a.what in ("pod", "pods", "po"):
+        pods: dict[str, dict] = {}
+        for g in gpus.values():
+            if "pod" not in g:
+                continue
+            ns, pod = g["pod"].split("/", 1)
+            if a.namespace and ns != a.namespace:
+                continue
+            p = pods.setdefault(g["pod"], {"ns": ns, "pod": pod, "gpus": [], "act": [], "vram": 0.0, "power": 0.0})
+            p["gpus"].append(g["gpu"])
+            act = g.get("gfx_activity_percent", g.get("busy_percent"))
+            if act is not None:
+                p["act"].append(act)
+            p["vram"] += g.get("vram_used_bytes") or 0.0
+            p["power"] += g.get("power_watts") or 0.0
+        rows = [["NAMESPACE", "POD", "GPUS", "GFX%", "VRAM", "POWER"]]
+        for key in sorted(pods):
+            p = pods[key]
+            rows.append([p["ns"], p["pod"], ",".join(sorted(p["gpus"], key=lambda x: int(x) if x.isdigit() else 0)),
+                         f"{sum(p['act']) / len(p['act']):.0f}%" if p["act"] else "-", _gib(p["vram"]),
+                         f"{p['power']:.0f}W" if p["power"] else "-"])
+        if len(rows) == 1:
+            out.write("No GPU pods found" + (f" in {a.namespace} namespace.\n" if a.namespace else ".\n"))
+            return 0
+    else:
+        raise KubectlError(f'error: unknown resource for top: "{a.what}" (node | pod)')
+    widths = [max(len(r[i]) for r in rows) for i in range(len(rows[0]))]
+    for r in rows:
+        out.write("   ".join(c.ljust(w) for c, w in zip(r, widths)).rstrip() + "\n")
+    return 0
+
+
 def load_docs(path: str) -> list[dict]:
     import yaml
     text = sys.stdin.read() if path == "-" else open(path).read()
@@ -588,9 +688,13 @@ def add_parsers(sub) -> None:
     lg.add_argument("--tail", type=int, default=None)
     lg.add_argument("-n", "--namespace", default=None)
     lg.add_argument("--server", default=None)
+    t = sub.add_parser("top", help="GPU use per MI355X (top node) or per pod (top pod), from the kubelet metrics")
+    t.add_argument("what", choices=["node", "nodes", "no", "gpu", "gpus", "pod", "pods", "po"])
+    common(t, selector=False)
 
 
-VERBS = {"get": cmd_get, "describe": cmd_describe, "wait": cmd_wait, "rollout": cmd_rollout, "logs": cmd_logs}
+VERBS = {"get": cmd_get, "describe": cmd_describe, "wait": cmd_wait, "rollout": cmd_rollout, "logs": cmd_logs,
+         "top": cmd_top}
 
 
 def run(verb: str, args, client: KubeClient | None = None) -> int:

@@ -146,3 +146,60 @@ def test_wait_by_label_timeout_and_delete(cl):
     assert rc == 0 and "deleted" in out, err
     rc, out, err = kfctl(cl, "wait", "pods", "minimal-notebook-0", "-n", "ci-ns", "--for=delete", "--timeout=60s")
     assert rc == 0, err
+
+
+METRICS = """# HELP kfamd_gpu_allocated 1 for every MI355X allocated to a pod by the device plugin
+kfamd_gpu_allocated{gpu="0",namespace="team-a",pod="nb-0"} 1
+kfamd_gpu_allocated{gpu="1",namespace="team-a",pod="nb-0"} 1
+kfamd_gpu_gfx_activity_percent{gpu="0",namespace="team-a",pod="nb-0"} 90
+kfamd_gpu_gfx_activity_percent{gpu="1",namespace="team-a",pod="nb-0"} 70
+kfamd_gpu_gfx_activity_percent{gpu="2",namespace="",pod=""} 0
+kfamd_gpu_vram_used_bytes{gpu="0"} 10737418240
+kfamd_gpu_vram_used_bytes{gpu="1"} 5368709120
+kfamd_gpu_vram_total_bytes{gpu="0"} 309237645312
+kfamd_gpu_power_watts{gpu="0"} 1320
+kfamd_gpu_gfxclk_mhz{gpu="0"} 1850
+kfamd_gpu_temperature_celsius{gpu="0",sensor="hotspot"} 81
+kfamd_gpu_temperature_celsius{gpu="0",sensor="hbm"} 70
+"""
+
+
+def test_top_tables_from_kubelet_metrics():
+    from types import SimpleNamespace
+    import io
+    from kubeflow_rm_amd import kubectl
+
+    class FakeClient:
+        def _req(self, method, path, raw=False, **kw):
+            assert (method, path, raw) == ("GET", "/metrics", True)
+            return METRICS
+    out = io.StringIO()
+    assert kubectl.cmd_top(FakeClient(), SimpleNamespace(what="node", namespace=None), out) == 0
+    lines = out.getvalue().splitlines()
+    assert lines[0].split() == ["GPU", "POD", "GFX%", "HBM%", "VRAM", "POWER", "SCLK", "HOTSPOT"]
+    row0 = lines[1].split()
+    assert row0[:3] == ["0", "team-a/nb-0", "90%"] and row0[4] == "10.0Gi/288.0Gi" and row0[5:] == ["1320W", "1850MHz", "81C"]
+    assert lines[3].split()[:2] == ["2", "<none>"]
+    out = io.StringIO()
+    assert kubectl.cmd_top(FakeClient(), SimpleNamespace(what="pod", namespace="team-a"), out) == 0
+    rows = [r.split() for r in out.getvalue().splitlines()]
+    assert rows[1] == ["team-a", "nb-0", "0,1", "80%", "15.0Gi", "1320W"]
+
+
+def test_top_pod_on_the_cluster(cl):
+    """kfctl top against kube-lite: a 2-GPU notebook shows up on its two devices (synthetic node:
+    allocation series only, no AMD SMI telemetry)."""
+    nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook",
+          "metadata": {"name": "topnb", "namespace": "ci-ns", "annotations": {"kfamd.io/gpu-readiness-op": "false"}},
+          "spec": {"template": {"spec": {"containers": [{"name": "topnb", "image": "jupyter-scipy:latest",
+                                                          "resources": {"limits": {"amd.com/gpu": "2"}}}]}}}}
+    cl.client.create(nb)
+    cl.client.wait_for("v1", "Pod", "topnb-0", "ci-ns", lambda o: (o.get("spec") or {}).get("nodeName"), timeout=30)
+    rc, out, err = kfctl(cl, "top", "pod", "-n", "ci-ns")
+    assert rc == 0, err
+    row = [r.split() for r in out.splitlines() if "topnb-0" in r][0]
+    assert row[0] == "ci-ns" and len(row[2].split(",")) == 2
+    rc, out, err = kfctl(cl, "top", "node")
+    assert rc == 0, err
+    assert sum("ci-ns/topnb-0" in r for r in out.splitlines()) == 2
+    cl.client.delete("kubeflow.org/v1", "Notebook", "topnb", "ci-ns")
