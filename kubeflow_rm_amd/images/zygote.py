@@ -65,6 +65,23 @@ def _set_pdeathsig() -> None:
         pass
 
 
+def _size_thread_pools(env: dict) -> None:
+    """The OpenMP runtime read OMP_NUM_THREADS and the CPU mask when the zygote loaded it, so a
+    forked container would inherit the zygote's thread count (every node CPU) instead of what a
+    fresh process pinned to its NUMA-local CPUs gets. Apply the container's own setting."""
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return
+    n = 0
+    try:
+        n = int(env.get("OMP_NUM_THREADS") or 0)
+    except ValueError:
+        n = 0
+    if n <= 0:
+        n = len(os.sched_getaffinity(0))
+    torch.set_num_threads(max(1, n))
+
+
 def _child(req: dict, closefds: list[int]) -> None:
     """Runs in the forked process: become the container, run its module, never return."""
     code = 1
@@ -99,6 +116,7 @@ def _child(req: dict, closefds: list[int]) -> None:
         os.environ.update(env)
         pp = [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p]
         sys.path[:0] = [p for p in pp if p not in sys.path]
+        _size_thread_pools(env)
         argv = list(req["argv"])
         if len(argv) < 2 or argv[0] != "-m":
             raise ValueError(f"zygote runs 'python -m module' containers only, got {argv!r}")

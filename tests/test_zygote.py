@@ -158,3 +158,47 @@ def test_gpu_torch_ready_notebook_forked_from_zygote():
         assert w.get("ok") is True, run
         assert w.get("import_torch_ms", 1e9) < 50, w  # preloaded, not imported by the container
     assert (r.get("readiness") or {}).get("ok", True) is not False
+
+
+def test_zygote_protocol_thread_pool_env_argv_exit(tmp_path):
+    """The protocol directly: a forked container gets its own CPU mask with a torch/OpenMP pool sized
+    to it (not the zygote's), its env, argv and cwd; the exit status comes back on the connection."""
+    import socket
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    sock = str(tmp_path / "z.sock")
+    env = dict(os.environ, PYTHONPATH=str(root))
+    env.pop("OMP_NUM_THREADS", None)
+    z = subprocess.Popen([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock, "--preload", "torch"],
+                         env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 120
+        while not os.path.exists(sock):
+            assert z.poll() is None and time.time() < deadline
+            time.sleep(0.05)
+        assert oct(os.stat(sock).st_mode & 0o777) == "0o600"
+        cpus = sorted(os.sched_getaffinity(0))[:2]
+
+        def run(extra_env, exit_code):
+            log = tmp_path / f"c{exit_code}.log"
+            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            s.connect(sock)
+            req = {"argv": ["-m", "tests.zygote_probe_mod", "a1", "a2"], "cwd": str(tmp_path), "log": str(log),
+                   "cpus": cpus, "env": [f"PYTHONPATH={root}", "PROBE_VAR=v", f"PROBE_EXIT={exit_code}", *extra_env]}
+            s.sendall((json.dumps(req) + "\n").encode())
+            f = s.makefile("r")
+            pid = json.loads(f.readline())["pid"]
+            st = json.loads(f.readline())
+            s.close()
+            probe = json.loads([ln for ln in log.read_text().splitlines() if ln.startswith("PROBE ")][0][6:])
+            return pid, st, probe
+        pid, st, probe = run([], 0)
+        assert st == {"exit": 0, "signal": 0}
+        assert probe["cpus"] == cpus and probe["threads"] == len(cpus)
+        assert probe["env"] == "v" and probe["argv"] == ["a1", "a2"] and probe["cwd"] == str(tmp_path)
+        pid, st, probe = run(["OMP_NUM_THREADS=1"], 3)
+        assert st["exit"] == 3 and probe["threads"] == 1
+    finally:
+        z.terminate()
+        z.wait(timeout=10)
