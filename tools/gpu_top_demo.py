@@ -4,12 +4,14 @@ notebook forked from the zygote, a GEMM load in it for a few seconds, and the to
 while it runs (AMD SMI telemetry: activity, VRAM, power, clock, hotspot)."""
 from __future__ import annotations
 
+import os
 import subprocess
 import sys
 import threading
 import time
 
-from kubeflow_rm_amd.cluster import LocalCluster
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kubeflow_rm_amd.cluster import LocalCluster  # noqa: E402
 
 
 def kfctl(url: str, *args: str) -> str:
