@@ -128,10 +128,16 @@ def main() -> int:
     if len(sys.argv) > 1 and sys.argv[1] == "--steps":
         import tempfile
         cache = tempfile.mkdtemp(prefix="comgr-")
-        for rep in range(4):  # 1st run fills the comgr cache, later runs hit it
-            subprocess.run([sys.executable, __file__, "--child", "steps"], check=True, timeout=120,
-                           env={**os.environ, "AMD_COMGR_CACHE_DIR": cache})
-            time.sleep(0.3)
+        # env variants of the HIP runtime's first-queue path (after one warm-up run fills the cache)
+        variants = [{}] + [dict([kv.split("=", 1)]) for kv in sys.argv[2:]]
+        subprocess.run([sys.executable, __file__, "--child", "steps"], check=True, timeout=120,
+                       env={**os.environ, "AMD_COMGR_CACHE_DIR": cache})
+        for rep in range(3):
+            for v in variants:
+                time.sleep(0.3)
+                print(json.dumps({"variant": v}), flush=True)
+                subprocess.run([sys.executable, __file__, "--child", "steps"], check=True, timeout=120,
+                               env={**os.environ, "AMD_COMGR_CACHE_DIR": cache, **v})
         return 0
     for rep in range(3):
         for mode in ("bare", "torch", "forked", "forked_env"):
