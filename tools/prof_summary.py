@@ -11,7 +11,7 @@ for f in sorted(base.glob("pmc*/run_counter_collection.csv")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        k = "hipBLASLt" if "Cijk" in k else ("w4" if "256w4" in k else ("pipe_sched" if "256p" in k else None))
+        k = "hipBLASLt" if "Cijk" in k else ("w4" if ("256w4" in k or "gemm_w4" in k) else ("pipe_sched" if "256p" in k else None))
         if k is None:
             continue
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -25,7 +25,7 @@ for f in sorted(base.glob("pmc*/run_counter_collection.csv")):
             res[k]["pmc_dispatch_us"] = round(sum(ds) / len(ds), 1)
 for r in csv.DictReader(open(base / "trace/run_kernel_stats.csv")):
     k = r["Name"]
-    k = "hipBLASLt" if "Cijk" in k else ("w4" if "256w4" in k else ("pipe_sched" if "256p" in k else None))
+    k = "hipBLASLt" if "Cijk" in k else ("w4" if ("256w4" in k or "gemm_w4" in k) else ("pipe_sched" if "256p" in k else None))
     if k:
         res[k]["trace_mean_us"] = round(float(r["AverageNs"]) / 1e3, 1)
         res[k]["trace_TFLOPs"] = round(2 * 8192 ** 3 / (float(r["AverageNs"]) * 1e-9) / 1e12, 1)
