@@ -20,7 +20,9 @@ Cold start (rank 0, after the timed region, while the other ranks wait on a CPU-
 their GPU memory released): ``--coldstart-runs`` (default 10) Notebook CREATE -> Ready runs of ONE
 notebook requesting all N GPUs, through the native control plane (process pods: no container
 runtime), with the in-pod readiness op on the allocated GPUs (N >= 2: one-shot peer all-reduce over
-xGMI). Reported with p50 / p90 and the per-phase p50 breakdown. Then the control-plane latencies of
+xGMI). Reported with p50 / p90 and the per-phase p50 breakdown; the same for the ODH OAuth spawn path,
+the torch-ready server (imports torch + runs a GEMM before Ready) and that server forked from the
+kubelet's pre-imported interpreter (``--pod-zygote``). Then the control-plane latencies of
 BASELINE configs 3 and 5 (Profile with GPU quota ready; TensorBoard and PVCViewer ready) on the same
 native control plane.
 """
