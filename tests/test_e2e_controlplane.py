@@ -61,7 +61,7 @@ def test_notebook_to_statefulset_service_and_ready(c, cluster):
                 assert "started" in json.loads(r.read())
                 break
         except urllib.error.HTTPError as e:
-            if e.code != 503 or time.time() > deadline:
+            if e.code not in (404, 502, 503) or time.time() > deadline:  # route / server not up yet
                 raise
             time.sleep(0.1)
 

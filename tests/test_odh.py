@@ -205,16 +205,27 @@ def test_update_pending_blocks_webhook_restart(c):
 
 
 def test_workbench_bundle_deleted_unmounts(c):
-    c.delete("v1", "ConfigMap", "odh-trusted-ca-bundle", "odh")
-    try:  # the reconciler may already have removed the workbench bundle derived from it
-        c.delete("v1", "ConfigMap", "workbench-trusted-ca-bundle", "odh")
-    except ApiException as e:
-        assert e.status == 404, e
+    def delete_if_there(name):
+        try:
+            c.delete("v1", "ConfigMap", name, "odh")
+        except ApiException as e:
+            assert e.status == 404, e
+    delete_if_there("odh-trusted-ca-bundle")
+    # the reconciler may already have removed the workbench bundle derived from it, or (one pass
+    # still working from the old source) re-create it once more: delete until the source is gone
+    # from its view too
 
     def unmounted(o):
         return not any(v.get("configMap", {}).get("name") == "workbench-trusted-ca-bundle"
                        for v in o["spec"]["template"]["spec"].get("volumes", []))
-    nb = c.wait_for(NB, "Notebook", "withca", "odh", unmounted, timeout=15)
+    deadline = time.time() + 30
+    while True:
+        delete_if_there("workbench-trusted-ca-bundle")
+        nb = c.get(NB, "Notebook", "withca", "odh")
+        if unmounted(nb):
+            break
+        assert time.time() < deadline, "workbench bundle still mounted"
+        time.sleep(0.2)
     env = {e["name"] for e in nb["spec"]["template"]["spec"]["containers"][0].get("env", [])}
     assert "REQUESTS_CA_BUNDLE" not in env
 

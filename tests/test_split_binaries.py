@@ -103,7 +103,7 @@ def test_profile_notebook_poddefault_over_rest(split):
                 assert r.status == 200
                 break
         except urllib.error.HTTPError as e:
-            if e.code != 503 or time.time() > deadline:
+            if e.code not in (404, 502, 503) or time.time() > deadline:  # route / server not up yet
                 raise
             time.sleep(0.1)
 
