@@ -218,6 +218,16 @@ class KubeClient:
             params["tailLines"] = str(tail_lines)
         return self._req("GET", f"/api/v1/namespaces/{namespace}/pods/{name}/log", params=params, raw=True)
 
+    def pod_exec(self, name: str, namespace: str, command: list[str], container: str | None = None,
+                 timeout: float = 30.0) -> dict:
+        """Non-interactive exec: {"exitCode": n, "output": stdout+stderr}."""
+        params = [("command", c) for c in command]
+        if container:
+            params.append(("container", container))
+        params.append(("timeoutSeconds", str(int(max(1, timeout)))))
+        return self._req("POST", f"/api/v1/namespaces/{namespace}/pods/{name}/exec", params=params,
+                         timeout=timeout + 10)
+
     def subject_access_review(self, user: str, verb: str, group: str, resource: str, namespace: str | None = None,
                               name: str | None = None, subresource: str | None = None, groups: list[str] | None = None) -> dict:
         body = {"apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",

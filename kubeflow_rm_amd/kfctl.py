@@ -7,7 +7,7 @@
                                                                         # the native registry
     python -m kubeflow_rm_amd.kfctl up [--data-dir DIR]                  # local kube-lite cluster
     python -m kubeflow_rm_amd.kfctl apply -f notebook.yaml | -           # kubectl-style file apply
-    python -m kubeflow_rm_amd.kfctl get|describe|wait|rollout|logs|top ...   # kubectl subset (kubectl.py)
+    python -m kubeflow_rm_amd.kfctl get|describe|wait|rollout|logs|exec|top ...   # kubectl subset (kubectl.py)
 
 Apply order follows kubectl's dependency order (Namespaces and CRDs first, webhooks last) so
 that every object's kind and namespace exist when it arrives; ``--dry-run`` sends every object

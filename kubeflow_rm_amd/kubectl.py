@@ -17,6 +17,7 @@ success, 1 on an error or a wait that timed out.
 """
 from __future__ import annotations
 
+import argparse
 import datetime as _dt
 import json
 import re
@@ -548,6 +549,26 @@ def cmd_logs(client: KubeClient, a, out=sys.stdout) -> int:
             seen = len(text)
 
 
+def cmd_exec(client: KubeClient, a, out=sys.stdout) -> int:
+    """kubectl exec POD [-c C] -- CMD...: runs in the container's env / working directory / CPU mask
+    (no TTY, no stdin); prints the combined output and exits with the command's status."""
+    cmd = list(a.command)
+    if not cmd:
+        raise KubectlError("error: you must specify at least one command for the container")
+    name = a.pod.split("/", 1)[1] if a.pod.startswith(("pod/", "pods/")) else a.pod
+    try:
+        r = client.pod_exec(name, a.namespace or "default", cmd, container=a.container,
+                            timeout=parse_duration(a.timeout))
+    except ApiException as e:
+        raise KubectlError(f"Error from server ({e.reason or e.status}): {e.message}")
+    out.write(r.get("output", ""))
+    out.flush()
+    code = int(r.get("exitCode", 1))
+    if code:
+        sys.stderr.write(f"command terminated with exit code {code}\n")
+    return code
+
+
 _SAMPLE_RE = None
 
 
@@ -688,18 +709,50 @@ def add_parsers(sub) -> None:
     lg.add_argument("--tail", type=int, default=None)
     lg.add_argument("-n", "--namespace", default=None)
     lg.add_argument("--server", default=None)
+    ex = sub.add_parser("exec", help="run a command in a pod's container (no TTY / stdin)")
+    ex.add_argument("pod")
+    ex.add_argument("-c", "--container", default=None)
+    ex.add_argument("-n", "--namespace", default=None)
+    ex.add_argument("--timeout", default="30s")
+    ex.add_argument("--server", default=None)
+    ex.add_argument("command", nargs=argparse.REMAINDER)
     t = sub.add_parser("top", help="GPU use per MI355X (top node) or per pod (top pod), from the kubelet metrics")
     t.add_argument("what", choices=["node", "nodes", "no", "gpu", "gpus", "pod", "pods", "po"])
     common(t, selector=False)
 
 
 VERBS = {"get": cmd_get, "describe": cmd_describe, "wait": cmd_wait, "rollout": cmd_rollout, "logs": cmd_logs,
-         "top": cmd_top}
+         "top": cmd_top, "exec": cmd_exec}
+
+
+def _exec_split(a) -> None:
+    """kubectl accepts exec's flags after the pod name; argparse's REMAINDER took them with the
+    command: move everything before ``--`` back onto the namespace."""
+    cmd = list(a.command)
+    if "--" not in cmd:
+        a.command = cmd
+        return
+    i = cmd.index("--")
+    pre, a.command = cmd[:i], cmd[i + 1:]
+    flags = {"-n": "namespace", "--namespace": "namespace", "-c": "container", "--container": "container",
+             "--timeout": "timeout", "--server": "server"}
+    it = iter(pre)
+    for tok in it:
+        key, _, val = tok.partition("=")
+        if key not in flags:
+            raise KubectlError(f"error: unknown flag: {tok}")
+        setattr(a, flags[key], val if val else next(it, ""))
 
 
 def run(verb: str, args, client: KubeClient | None = None) -> int:
+    if verb == "exec":
+        try:
+            _exec_split(args)
+        except KubectlError as e:
+            sys.stderr.write(str(e) + "\n")
+            return 1
     client = client or KubeClient(getattr(args, "server", None))
-    if getattr(args, "namespace", None) is None and verb != "logs":
+    if getattr(args, "namespace", None) is None and verb not in ("logs", "exec"):
         args.namespace = None if getattr(args, "all_namespaces", False) else "default"
     try:
         return VERBS[verb](client, args)

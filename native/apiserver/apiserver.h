@@ -133,6 +133,11 @@ struct AdmissionAttrs {
 using AdmissionFn = std::function<ApiError(AdmissionAttrs&)>;
 using LogProvider = std::function<bool(const std::string& ns, const std::string& pod, const std::string& container,
                                        int64_t tail_lines, std::string& out)>;
+// pods/exec (non-interactive): run argv in the container's environment, wait up to timeout_s;
+// returns false when the pod / container is not running here (err says why)
+using ExecProvider = std::function<bool(const std::string& ns, const std::string& pod, const std::string& container,
+                                        const std::vector<std::string>& argv, double timeout_s, int& exit_code,
+                                        std::string& output, std::string& err)>;
 
 class ApiServer {
  public:
@@ -191,6 +196,7 @@ class ApiServer {
   void add_mutating_plugin(const std::string& name, AdmissionFn fn);
   void add_validating_plugin(const std::string& name, AdmissionFn fn);
   void set_log_provider(LogProvider p) { log_provider_ = std::move(p); }
+  void set_exec_provider(ExecProvider p) { exec_provider_ = std::move(p); }
   bool authorize(const UserInfo& u, const std::string& verb, const std::string& group, const std::string& resource,
                  const std::string& subresource, const std::string& ns, const std::string& name,
                  std::string* reason = nullptr);
@@ -260,6 +266,7 @@ class ApiServer {
   std::list<std::weak_ptr<Watch>> watchers_;
   std::vector<std::pair<std::string, AdmissionFn>> mutating_, validating_;
   LogProvider log_provider_;
+  ExecProvider exec_provider_;
   std::ofstream wal_;
   std::mutex wal_mu_;
   size_t wal_records_ = 0;

@@ -310,6 +310,33 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
     resp.text(200, out);
     return;
   }
+  if (res->group.empty() && plural == "pods" && sub == "exec") {
+    // kubectl exec without a TTY or stdin: ?command=a&command=b[&container=c][&timeoutSeconds=n];
+    // reply {"exitCode": n, "output": "<stdout+stderr>"} (authorized above as create pods/exec)
+    if (req.method != "POST" && req.method != "GET") {
+      resp.json(405, ApiError{405, "MethodNotAllowed", "exec takes POST"}.status_json().dump());
+      return;
+    }
+    auto it = req.query.find("command");
+    if (it == req.query.end() || it->second.empty()) {
+      resp.json(400, ApiError::BadRequest("you must specify at least one command for the container").status_json().dump());
+      return;
+    }
+    Json p;
+    if (ApiError e = r_get(res, version, ns, name, p)) {
+      send_error(resp, e, "Pod", name);
+      return;
+    }
+    int code = 0;
+    std::string out, err;
+    const double timeout = std::max(1.0, std::atof(req.q("timeoutSeconds", "30").c_str()));
+    if (!exec_provider_ || !exec_provider_(ns, name, req.q("container"), it->second, timeout, code, out, err)) {
+      resp.json(400, ApiError::BadRequest(err.empty() ? "exec is not available for pod " + name : err).status_json().dump());
+      return;
+    }
+    resp.json(200, Json{{"exitCode", static_cast<int64_t>(code)}, {"output", out}}.dump());
+    return;
+  }
   if (res->group.empty() && plural == "services" && sub == "proxy") {
     std::string r;
     for (size_t k = 3; k < rest.size(); ++k) r += (k > 3 ? "/" : "") + rest[k];

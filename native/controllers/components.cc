@@ -216,6 +216,9 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
       Kubelet* k = I.kubelet.get();
       I.api->set_log_provider([k](const std::string& ns, const std::string& pod, const std::string& cont, int64_t tail,
                                   std::string& out) { return k->read_logs(ns, pod, cont, tail, out); });
+      I.api->set_exec_provider([k](const std::string& ns, const std::string& pod, const std::string& cont,
+                                   const std::vector<std::string>& argv, double timeout, int& code, std::string& out,
+                                   std::string& err) { return k->exec(ns, pod, cont, argv, timeout, code, out, err); });
     }
     I.starters.push_back([&I] { I.kubelet->start(); });
     I.stoppers.push_back([&I] { I.kubelet->stop(); });

@@ -147,6 +147,10 @@ struct ContainerRt {
   // child (waitpid). zorphan: the zygote went away first, exit is noticed by kill(pid, 0)
   int zfd = -1;
   bool zorphan = false;
+  // what the running process was started with (pods/exec runs commands in the same environment)
+  std::vector<std::string> envv;
+  std::string cwd;
+  std::vector<int> cpus;
 };
 
 struct Kubelet::PodRuntime {
@@ -732,6 +736,70 @@ void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
     }
 }
 
+bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::string& container,
+                   const std::vector<std::string>& argv, double timeout_s, int& exit_code, std::string& output,
+                   std::string& err) {
+  std::shared_ptr<PodRuntime> rt;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto k = key_to_uid_.find(ns + "/" + pod);
+    if (k != key_to_uid_.end()) {
+      auto it = pods_.find(k->second);
+      if (it != pods_.end()) rt = it->second;
+    }
+  }
+  if (!rt) {
+    err = "pod " + pod + " is not running on this node";
+    return false;
+  }
+  std::vector<std::string> envv;
+  std::string cwd, dir;
+  std::vector<int> cpus;
+  {
+    std::lock_guard<std::mutex> pl(rt->op_mu);
+    const ContainerRt* found = nullptr;
+    for (const auto& c : rt->main)
+      if (!found && (container.empty() || c.name == container)) found = &c;
+    for (const auto& c : rt->init)  // a named native sidecar
+      if (!found && !container.empty() && c.name == container) found = &c;
+    if (!found) {
+      err = "container " + container + " is not valid for pod " + pod;
+      return false;
+    }
+    if (found->state != "running" || found->pid <= 0) {
+      err = "container " + found->name + " is not running";
+      return false;
+    }
+    envv = found->envv;
+    cwd = found->cwd;
+    cpus = found->cpus;
+    dir = rt->dir;
+  }
+  const std::string out_path = dir + "/exec-" + random_hex(6) + ".out";
+  std::string serr;
+  const pid_t pid = spawn(argv, envv, cwd, out_path, &serr, cpus);
+  if (pid < 0) {
+    err = serr;
+    ::unlink(out_path.c_str());
+    return false;
+  }
+  std::string reason;
+  double deadline = now_seconds() + timeout_s;
+  bool killed = false;
+  while (!reap(pid, exit_code, reason)) {
+    if (now_seconds() > deadline) {
+      ::kill(-pid, SIGKILL);
+      killed = true;
+      deadline = now_seconds() + 5;
+    }
+    ::usleep(2000);
+  }
+  if (!read_file(out_path, output)) output.clear();
+  ::unlink(out_path.c_str());
+  if (killed) output += "\ncommand terminated: timeout after " + std::to_string(static_cast<int>(timeout_s)) + " s\n";
+  return true;
+}
+
 bool Kubelet::read_logs(const std::string& ns, const std::string& pod, const std::string& container, int64_t tail,
                         std::string& out) {
   std::shared_ptr<PodRuntime> rt;
@@ -1124,6 +1192,9 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     cr.pid = pid;
     cr.state = "running";
     cr.reason = "";
+    cr.envv = envv;
+    cr.cwd = cwd;
+    cr.cpus = cpus;
     cr.started_at = ms_now();
     if (cr.zfd >= 0) {
       const int dfd = ::fcntl(cr.zfd, F_DUPFD_CLOEXEC, 0);  // the watch closes its own copy

@@ -98,6 +98,10 @@ class Kubelet {
   Result reconcile(const Request& r, std::string* err);
   bool read_logs(const std::string& ns, const std::string& pod, const std::string& container, int64_t tail,
                  std::string& out);
+  // pods/exec: argv in a running container's env, working directory and CPU mask (a new process in
+  // the container's place; output = stdout + stderr); false + err when it cannot run
+  bool exec(const std::string& ns, const std::string& pod, const std::string& container,
+            const std::vector<std::string>& argv, double timeout_s, int& exit_code, std::string& output, std::string& err);
   GpuAllocator& gpus() { return *alloc_; }
   const std::string& node_name() const { return cfg_.node_name; }
 

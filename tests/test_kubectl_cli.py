@@ -203,3 +203,30 @@ def test_top_pod_on_the_cluster(cl):
     assert rc == 0, err
     assert sum("ci-ns/topnb-0" in r for r in out.splitlines()) == 2
     cl.client.delete("kubeflow.org/v1", "Notebook", "topnb", "ci-ns")
+
+
+def test_exec_runs_in_the_container_environment(cl):
+    """kfctl exec (pods/exec, no TTY): the command runs with the container's env and working directory,
+    output comes back, and the exit status is the CLI's."""
+    nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook", "metadata": {"name": "exnb", "namespace": "ci-ns"},
+          "spec": {"template": {"spec": {"containers": [{"name": "exnb", "image": "jupyter-scipy:latest",
+                                                          "env": [{"name": "GREETING", "value": "hi from the pod"}]}]}}}}
+    cl.client.create(nb)
+    cl.client.wait_for("kubeflow.org/v1", "Notebook", "exnb", "ci-ns",
+                       lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=60)
+    env = dict(os.environ, KFAMD_API_URL=cl.url)
+
+    def run(*args):
+        p = subprocess.run([sys.executable, "-m", "kubeflow_rm_amd.kfctl", "exec", *args], capture_output=True, text=True,
+                           timeout=60, env=env)
+        return p.returncode, p.stdout, p.stderr
+    rc, out, err = run("exnb-0", "-n", "ci-ns", "--", "sh", "-c", 'echo "$GREETING"; echo "$POD_NAME"; pwd; exit 3')
+    assert rc == 3, err
+    lines = out.splitlines()
+    assert lines[0] == "hi from the pod" and lines[1] == "exnb-0" and "/pods/ci-ns_exnb-0_" in lines[2]
+    assert "command terminated with exit code 3" in err
+    rc, out, err = run("exnb-0", "-n", "ci-ns", "-c", "nope", "--", "true")
+    assert rc == 1 and "not valid" in err
+    rc, out, err = run("exnb-0", "-n", "ci-ns", "--timeout", "1s", "--", "sleep", "30")
+    assert rc != 0 and "timeout" in out
+    cl.client.delete("kubeflow.org/v1", "Notebook", "exnb", "ci-ns")
