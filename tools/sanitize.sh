@@ -9,7 +9,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-profiles/r1_sanitizers}
 mkdir -p "$OUT"
-SUITES="tests/test_zygote.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py"
+SUITES="tests/test_zygote.py tests/test_kubectl_cli.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py"
 rc=0
 for san in thread address; do
   python -c "from kubeflow_rm_amd import _build; _build.build_native(sanitize='$san', build_type='RelWithDebInfo')" \
