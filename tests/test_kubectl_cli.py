@@ -230,3 +230,21 @@ def test_exec_runs_in_the_container_environment(cl):
     rc, out, err = run("exnb-0", "-n", "ci-ns", "--timeout", "1s", "--", "sleep", "30")
     assert rc != 0 and "timeout" in out
     cl.client.delete("kubeflow.org/v1", "Notebook", "exnb", "ci-ns")
+
+
+def test_exec_sees_the_pods_gpu_allocation(cl):
+    """exec in a GPU notebook: the command gets the device plugin's HIP/ROCR visibility and the
+    NUMA-local CPU mask the container process got."""
+    nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook",
+          "metadata": {"name": "gpunb", "namespace": "ci-ns", "annotations": {"kfamd.io/gpu-readiness-op": "false"}},
+          "spec": {"template": {"spec": {"containers": [{"name": "gpunb", "image": "jupyter-scipy:latest",
+                                                          "resources": {"limits": {"amd.com/gpu": "2"}}}]}}}}
+    cl.client.create(nb)
+    o = cl.client.wait_for("kubeflow.org/v1", "Notebook", "gpunb", "ci-ns",
+                           lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=60)
+    r = cl.client.pod_exec("gpunb-0", "ci-ns", ["sh", "-c", 'echo "$HIP_VISIBLE_DEVICES|$ROCR_VISIBLE_DEVICES|$WORLD_SIZE"'])
+    assert r["exitCode"] == 0
+    hip, rocr, world = r["output"].strip().split("|")
+    assert len(hip.split(",")) == 2 and len(rocr.split(",")) == 2 and world == "2"
+    del o
+    cl.client.delete("kubeflow.org/v1", "Notebook", "gpunb", "ci-ns")
