@@ -202,3 +202,24 @@ def test_zygote_protocol_thread_pool_env_argv_exit(tmp_path):
     finally:
         z.terminate()
         z.wait(timeout=10)
+
+
+@pytest.mark.gpu
+def test_gpu_exec_into_torch_ready_notebook():
+    """On the GPU: kfctl-style exec into a GPU notebook (forked from the zygote) runs a torch op on the
+    pod's GPU from the container's environment."""
+    with LocalCluster(gpus=None, zygote=True) as cl:
+        cl.wait_zygotes(timeout=300)
+        c = cl.client
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "zx"}})
+        c.create({"apiVersion": NB, "kind": "Notebook", "metadata": {"name": "g", "namespace": "zx"},
+                  "spec": {"template": {"spec": {"containers": [{
+                      "name": "g", "image": "kfamd/jupyter-pytorch-rocm:latest",
+                      "env": [{"name": "KFAMD_WARMUP", "value": "torch"}],
+                      "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}})
+        c.wait_for(NB, "Notebook", "g", "zx", _ready, timeout=120)
+        r = c.pod_exec("g-0", "zx", ["python3", "-c", "import torch; print(float(torch.ones(4, device='cuda').sum()), "
+                                     "torch.cuda.device_count())"], timeout=120)
+        assert r["exitCode"] == 0, r
+        assert r["output"].strip().splitlines()[-1] == "4.0 1"
+        c.delete(NB, "Notebook", "g", "zx")
