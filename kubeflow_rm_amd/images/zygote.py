@@ -213,6 +213,11 @@ def serve(sock_path: str, preload: list[str]) -> int:
                     break
                 buf += chunk
             req = json.loads(buf)
+            argv = req.get("argv") if isinstance(req, dict) else None
+            if not (isinstance(argv, list) and len(argv) >= 2 and argv[0] == "-m" and
+                    all(isinstance(x, str) for x in argv) and isinstance(req.get("cwd"), str) and
+                    isinstance(req.get("log"), str) and isinstance(req.get("env", []), list)):
+                raise ValueError("want {argv: ['-m', module, ...], cwd, log, env, cpus}")
         except (OSError, ValueError) as e:
             try:
                 conn.sendall((json.dumps({"error": f"bad request: {e}"}) + "\n").encode())

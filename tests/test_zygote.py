@@ -223,3 +223,30 @@ def test_gpu_exec_into_torch_ready_notebook():
         assert r["exitCode"] == 0, r
         assert r["output"].strip().splitlines()[-1] == "4.0 1"
         c.delete(NB, "Notebook", "g", "zx")
+
+
+def test_zygote_rejects_malformed_requests(tmp_path):
+    import socket
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    sock = str(tmp_path / "z.sock")
+    z = subprocess.Popen([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock],
+                         env=dict(os.environ, PYTHONPATH=str(root)), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 60
+        while not os.path.exists(sock):
+            assert z.poll() is None and time.time() < deadline
+            time.sleep(0.05)
+        for bad in (b"not json\n", b'{"argv": ["python", "x.py"], "cwd": "/", "log": "/dev/null"}\n',
+                    b'{"argv": ["-m", "x"], "log": "/dev/null"}\n'):
+            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            s.connect(sock)
+            s.sendall(bad)
+            reply = json.loads(s.makefile("r").readline())
+            s.close()
+            assert "error" in reply and "pid" not in reply, reply
+        assert z.poll() is None  # still serving
+    finally:
+        z.terminate()
+        z.wait(timeout=10)
