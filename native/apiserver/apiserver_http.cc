@@ -329,7 +329,8 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
     }
     int code = 0;
     std::string out, err;
-    const double timeout = std::max(1.0, std::atof(req.q("timeoutSeconds", "30").c_str()));
+    // bounded: the request holds one API server worker for its duration
+    const double timeout = std::min(3600.0, std::max(1.0, std::atof(req.q("timeoutSeconds", "30").c_str())));
     if (!exec_provider_ || !exec_provider_(ns, name, req.q("container"), it->second, timeout, code, out, err)) {
       resp.json(400, ApiError::BadRequest(err.empty() ? "exec is not available for pod " + name : err).status_json().dump());
       return;

@@ -796,6 +796,8 @@ bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::str
   }
   if (!read_file(out_path, output)) output.clear();
   ::unlink(out_path.c_str());
+  constexpr size_t kMaxOut = 16u << 20;  // the reply carries at most the last 16 MiB
+  if (output.size() > kMaxOut) output = "[... output truncated ...]\n" + output.substr(output.size() - kMaxOut);
   if (killed) output += "\ncommand terminated: timeout after " + std::to_string(static_cast<int>(timeout_s)) + " s\n";
   return true;
 }
