@@ -621,7 +621,13 @@ def gpu_table(samples: list[tuple[str, dict, float]]) -> dict[str, dict]:
 def cmd_top(client: KubeClient, a, out=sys.stdout) -> int:
     """``top node``: one row per MI355X (holding pod, GFX / HBM activity, VRAM, power, clock, hotspot);
     ``top pod``: per pod, its GPUs and their summed use. From the kubelet's /metrics series."""
-    text = client._req("GET", "/metrics", raw=True)
+    if getattr(a, "metrics_url", None):  # split deployment: the node agent serves its own /metrics
+        import requests
+        r = requests.get(a.metrics_url, timeout=10)
+        r.raise_for_status()
+        text = r.text
+    else:
+        text = client._req("GET", "/metrics", raw=True)
     gpus = gpu_table(parse_samples(text))
     if not gpus:
         raise KubectlError("no GPU metrics from the node (kubelet metrics not registered)")
@@ -718,6 +724,8 @@ def add_parsers(sub) -> None:
     ex.add_argument("command", nargs=argparse.REMAINDER)
     t = sub.add_parser("top", help="GPU use per MI355X (top node) or per pod (top pod), from the kubelet metrics")
     t.add_argument("what", choices=["node", "nodes", "no", "gpu", "gpus", "pod", "pods", "po"])
+    t.add_argument("--metrics-url", default=None,
+                   help="the node agent's /metrics when it runs apart from the API server (kfamd-node)")
     common(t, selector=False)
 
 
