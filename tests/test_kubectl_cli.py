@@ -248,3 +248,31 @@ def test_exec_sees_the_pods_gpu_allocation(cl):
     assert len(hip.split(",")) == 2 and len(rocr.split(",")) == 2 and world == "2"
     del o
     cl.client.delete("kubeflow.org/v1", "Notebook", "gpunb", "ci-ns")
+
+
+def test_top_from_a_separate_node_agent_metrics_url():
+    import http.server
+    import io
+    import threading
+    from types import SimpleNamespace
+    from kubeflow_rm_amd import kubectl
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            body = METRICS.encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        out = io.StringIO()
+        a = SimpleNamespace(what="gpus", namespace=None, metrics_url=f"http://127.0.0.1:{srv.server_address[1]}/metrics")
+        assert kubectl.cmd_top(None, a, out) == 0
+        assert "team-a/nb-0" in out.getvalue()
+    finally:
+        srv.shutdown()
