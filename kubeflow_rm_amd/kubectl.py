@@ -338,6 +338,21 @@ def describe_one(client: KubeClient, res: Resource, o: dict) -> str:
         ready, status, restarts = _pod_status(o)
         st = o.get("status") or {}
         s += f"{'Status:':<14}{status}\n{'IP:':<14}{st.get('podIP', '')}\n{'Node:':<14}{(o.get('spec') or {}).get('nodeName', '')}\n"
+        ann = (o.get("metadata") or {}).get("annotations") or {}
+        if ann.get("amd.com/gpu-ids"):  # the device plugin's allocation (kubelet annotations)
+            s += f"{'GPUs:':<14}{ann['amd.com/gpu-ids']}"
+            if ann.get("amd.com/xgmi-ring"):
+                s += f"  (xGMI ring {ann['amd.com/xgmi-ring']})"
+            if ann.get("amd.com/gpu-placement"):
+                s += f"\n{'Placement:':<14}{ann['amd.com/gpu-placement']}"
+            s += "\n"
+        if ann.get("notebooks.kubeflow.org/gpu-readiness"):
+            try:
+                rep = json.loads(ann["notebooks.kubeflow.org/gpu-readiness"])
+                verdict = "ok" if rep.get("ok") else f"FAILED ({rep.get('error') or rep.get('stage') or '?'})"
+                s += f"{'GPU Check:':<14}{verdict}, {rep.get('total_ms', '?')} ms\n"
+            except (ValueError, AttributeError):
+                pass
         for title, key in (("Init Containers:", "initContainerStatuses"), ("Containers:", "containerStatuses")):
             cs = st.get(key) or []
             if cs:

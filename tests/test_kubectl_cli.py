@@ -246,6 +246,10 @@ def test_exec_sees_the_pods_gpu_allocation(cl):
     assert r["exitCode"] == 0
     hip, rocr, world = r["output"].strip().split("|")
     assert len(hip.split(",")) == 2 and len(rocr.split(",")) == 2 and world == "2"
+    rc, out, err = kfctl(cl, "describe", "pod", "gpunb-0", "-n", "ci-ns")
+    assert rc == 0, err
+    gpus_line = [ln for ln in out.splitlines() if ln.startswith("GPUs:")]
+    assert gpus_line and "xGMI ring" in gpus_line[0], out
     del o
     cl.client.delete("kubeflow.org/v1", "Notebook", "gpunb", "ci-ns")
 
