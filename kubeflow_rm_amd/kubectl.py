@@ -179,7 +179,8 @@ def _columns(kind: str, wide: bool) -> list[tuple[str, Callable[[dict], str]]]:
         cols = [("READY", lambda o: _pod_status(o)[0]), ("STATUS", lambda o: _pod_status(o)[1]),
                 ("RESTARTS", lambda o: str(_pod_status(o)[2])), age]
         if wide:
-            cols += [("IP", lambda o: st(o).get("podIP") or "<none>"), ("NODE", lambda o: sp(o).get("nodeName") or "<none>")]
+            cols += [("IP", lambda o: st(o).get("podIP") or "<none>"), ("NODE", lambda o: sp(o).get("nodeName") or "<none>"),
+                     ("GPUS", lambda o: (md(o).get("annotations") or {}).get("amd.com/gpu-ids") or "<none>")]
         return cols
     if kind == "StatefulSet":
         return [("READY", lambda o: f"{st(o).get('readyReplicas') or 0}/{sp(o).get('replicas', 1)}"), age]

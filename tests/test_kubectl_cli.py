@@ -250,6 +250,10 @@ def test_exec_sees_the_pods_gpu_allocation(cl):
     assert rc == 0, err
     gpus_line = [ln for ln in out.splitlines() if ln.startswith("GPUs:")]
     assert gpus_line and "xGMI ring" in gpus_line[0], out
+    rc, out, err = kfctl(cl, "get", "pods", "-n", "ci-ns", "-o", "wide")
+    assert rc == 0, err
+    hdr, row = out.splitlines()[0].split(), [r.split() for r in out.splitlines() if r.startswith("gpunb-0")][0]
+    assert hdr[-1] == "GPUS" and len(row[-1].split(",")) == 2
     del o
     cl.client.delete("kubeflow.org/v1", "Notebook", "gpunb", "ci-ns")
 
