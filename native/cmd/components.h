@@ -26,6 +26,7 @@ struct ComponentFlags {
   std::string sysfs_root;  // GPU discovery root ("" = /sys)
   bool numa_pinning = true;
   bool pod_zygote = false;
+  std::string image_recipes;
   // gateway (Istio ingress equivalent)
   std::string gateway_addr = "127.0.0.1";
   int64_t gateway_port = 0;

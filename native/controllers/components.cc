@@ -26,6 +26,8 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("pod-cidr-prefix", &pod_cidr_prefix, "127.20", "pod IPs are allocated as <prefix>.x.y (loopback)");
   f.add_string("sysfs-root", &sysfs_root, "", "sysfs root for GPU / PCI / NUMA discovery (default /sys)");
   f.add_bool("numa-pinning", &numa_pinning, true, "pin GPU pods to their GPUs' NUMA-local CPUs");
+  f.add_string("image-recipes", &image_recipes, "",
+               "JSON list of extra image recipes ({match, argv, passArgs, zygote}) tried before the built-in ones");
   f.add_bool("pod-zygote", &pod_zygote, false,
              "fork Python pod containers from a pre-imported interpreter per image recipe (torch preloaded)");
   f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
@@ -210,6 +212,7 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     kc.sysfs_root = I.f.sysfs_root;
     kc.numa_pinning = I.f.numa_pinning;
     kc.pod_zygote = I.f.pod_zygote;
+    kc.recipes_file = I.f.image_recipes;
     I.kubelet = std::make_unique<Kubelet>(I.c, kc);
     I.kubelet->setup(mgr);
     if (I.api) {

@@ -250,3 +250,21 @@ def test_zygote_rejects_malformed_requests(tmp_path):
     finally:
         z.terminate()
         z.wait(timeout=10)
+
+
+def test_operator_image_recipe_with_its_own_zygote(tmp_path):
+    """--image-recipes: an operator maps an image to a command and opts it into a zygote with its own
+    preload list; containers of that image fork from it."""
+    recipes = tmp_path / "recipes.json"
+    recipes.write_text(json.dumps([{"match": "acme/lab", "argv": ["{python}", "-m", "kubeflow_rm_amd.images.notebook_server"],
+                                    "zygote": "json,kubeflow_rm_amd.images.notebook_server"}]))
+    with LocalCluster(gpus=0, zygote=True, args=["--image-recipes", str(recipes)]) as cl:
+        socks = cl.wait_zygotes(timeout=300)
+        assert len(socks) == 2  # the built-in notebook zygote + the operator's
+        c = cl.client
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "op"}})
+        c.create({"apiVersion": NB, "kind": "Notebook", "metadata": {"name": "a", "namespace": "op"},
+                  "spec": {"template": {"spec": {"containers": [{"name": "a", "image": "acme/lab:1"}]}}}})
+        c.wait_for(NB, "Notebook", "a", "op", _ready, timeout=60)
+        logs = c.pod_logs("a-0", "op")
+        assert "recipe:acme/lab" in logs and "preloaded json,kubeflow_rm_amd.images.notebook_server" in logs, logs
