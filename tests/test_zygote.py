@@ -268,3 +268,13 @@ def test_operator_image_recipe_with_its_own_zygote(tmp_path):
         c.wait_for(NB, "Notebook", "a", "op", _ready, timeout=60)
         logs = c.pod_logs("a-0", "op")
         assert "recipe:acme/lab" in logs and "preloaded json,kubeflow_rm_amd.images.notebook_server" in logs, logs
+
+
+def test_cold_start_bench_zygote_path_on_cpu():
+    """bench_coldstart's zygote path end to end on the CPU (synthetic GPUs, no readiness op): the
+    cluster waits for its zygote, the runs complete and their phases are recorded."""
+    from kubeflow_rm_amd.bench_coldstart import measure_cold_start
+    r = measure_cold_start(runs=2, gpus_per_notebook=1, gpus=2, readiness=False, zygote=True, namespace="zy-cpu",
+                           settle_s=0.0, timeout=60)
+    assert len(r["runs"]) == 2 and r["zygote"] is True
+    assert r["p50_s"] < 30 and "create_to_pod_ready_s" in r["phases_p50_s"]
