@@ -31,10 +31,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import statistics
 import sys
 import time
 
+T_START = time.time()
 METRIC = "notebook pod cold-start p50 (s) + in-pod bf16 matmul TFLOPS at 1/2/4/8 MI355X"
 
 
@@ -58,7 +58,74 @@ def parse_args():
                         "(rank 0; reported as torch_matmul_tflops_per_gpu, never as the value)")
     p.add_argument("--no-allreduce-sweep", action="store_true",
                    help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
+    p.add_argument("--budget-s", type=float, default=float(os.environ.get("KFAMD_BENCH_BUDGET_S", "450")),
+                   help="wall-clock budget from process start for everything after the timed region: extras "
+                        "that do not fit are reported as skipped, one that hangs as timeout (bench_extras.py)")
     return p.parse_args()
+
+
+COLD_START_NOTE = ("process pods (no container runtime); notebook server = stub recipe (no torch import); "
+                   "cold_start_torch_ready_* = same path with a server that imports torch + runs a GEMM on the GPU "
+                   "before Ready (fresh interpreter); cold_start_torch_ready_zygote_* = that server forked from the "
+                   "kubelet's pre-imported interpreter (torch imported once per node); cold_start_odh_* = ODH path "
+                   "with the OAuth proxy + reconciliation lock; the GPU readiness op runs as a native sidecar "
+                   "overlapping the server start. *_failures = runs not Ready within the per-run timeout, with "
+                   "pod diagnostics in cold_start_failures")
+
+
+def _cs_keys(prefix: str, cs: dict) -> dict:
+    out = {f"{prefix}_runs": len(cs["runs"]), f"{prefix}_p50_s": cs["p50_s"], f"{prefix}_p90_s": cs["p90_s"],
+           f"{prefix}_phases_p50_s": cs.get("phases_p50_s"), f"{prefix}_failures": len(cs.get("failures") or [])}
+    if cs.get("server_warmup_p50_ms"):
+        out[f"{prefix}_server_p50_ms"] = cs["server_warmup_p50_ms"]
+    if cs.get("truncated"):
+        out[f"{prefix}_truncated"] = True
+    if cs.get("failures"):
+        out.setdefault("cold_start_failures", {})[prefix] = cs["failures"]
+    return out
+
+
+def run_cold_starts(ex, args, world: int) -> None:
+    """Rank 0: the four cold-start variants and the control-plane latencies, each its own extra."""
+    from kubeflow_rm_amd.bench_coldstart import measure_cold_start, measure_control_plane
+
+    def stub(e):
+        cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world, timeout=30, deadline=e.deadline())
+        out = _cs_keys("cold_start", cs)
+        out.update({"cold_start_gpus_per_notebook": world, "cold_start_readiness": cs.get("readiness"),
+                    "cold_start_note": COLD_START_NOTE})
+        # BASELINE §3 north-star #2: controller reconcile latency, from the control plane's own
+        # controller_runtime_reconcile_time_seconds histogram over these runs
+        nbr = (cs.get("reconcile") or {}).get("notebook-controller") or {}
+        out["reconcile_p50_ms"] = (nbr.get("reconcile") or {}).get("p50_ms")
+        out["reconcile_p99_ms"] = (nbr.get("reconcile") or {}).get("p99_ms")
+        out["reconcile_queue_p50_ms"] = (nbr.get("queue") or {}).get("p50_ms")
+        out["reconcile_by_controller"] = cs.get("reconcile")
+        return out
+
+    def merge_failures(e, out):
+        f = out.pop("cold_start_failures", None)
+        if f:
+            e.data.setdefault("cold_start_failures", {}).update(f)
+        return out
+
+    ex.run("cold_start_stub", lambda e: merge_failures(e, stub(e)), est_s=10, timeout_s=90)
+    if args.coldstart_torch_runs > 0:
+        # the torch-ready server, fresh interpreter (the jupyter-pytorch-rocm image's cold start)
+        ex.run("cold_start_torch_ready", lambda e: merge_failures(e, _cs_keys("cold_start_torch_ready", measure_cold_start(
+            runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready", namespace="bench-torch",
+            timeout=30, deadline=e.deadline()))), est_s=15, timeout_s=120)
+        # the same server forked from the node's pre-imported interpreter (kubelet --pod-zygote)
+        ex.run("cold_start_torch_ready_zygote", lambda e: merge_failures(e, _cs_keys(
+            "cold_start_torch_ready_zygote", measure_cold_start(
+                runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready", namespace="bench-zygote",
+                zygote=True, timeout=30, deadline=e.deadline()))), est_s=20, timeout_s=120)
+    # the fork's own spawn path (SURVEY CS1): ODH webhook lock + OAuth proxy + two reconciles
+    ex.run("cold_start_odh", lambda e: merge_failures(e, _cs_keys("cold_start_odh", measure_cold_start(
+        runs=max(3, args.coldstart_runs // 2), gpus_per_notebook=world, odh_oauth=True, namespace="bench-odh",
+        timeout=30, deadline=e.deadline()))), est_s=25, timeout_s=90)
+    # BASELINE configs 3 and 5: Profile with GPU quota, TensorBoard + PVCViewer on a PVC
+    ex.run("control_plane", lambda e: {"control_plane": measure_control_plane(runs=5)}, est_s=5, timeout_s=60)
 
 
 def self_launch(args) -> int:
@@ -140,44 +207,91 @@ def main() -> int:
     per_gpu_tflops = flops / (ms_per_step * 1e-3) / 1e12
     value = per_gpu_tflops * world
 
-    extra = {}
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "TFLOPS (bf16 GEMM, aggregate over GPUs)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "prewarm_s": args.prewarm_s,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform [-1,1) bf16 operands, random-init)",
+        "config": {
+            "model": f"in-pod bf16 matmul HIP smoke (K1 readiness op), C=A@B^T {M}x{N}x{K}",
+            "global_batch": world,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+        },
+        "per_gpu_tflops": round(per_gpu_tflops, 2),
+        "kernel": "kfamd gemm_w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring, XCD remap, in-kernel edge tiles)",
+        "check_rows": int(rows.numel()),
+        "correct": bool(ok),
+        "max_abs_err_vs_fp32": err,
+    }
+
+    # everything after the timed region is an extra: own try, own deadline, overall budget, and a
+    # watchdog that prints the line with what was measured if one of them hangs (bench_extras.py)
+    from kubeflow_rm_amd.bench_extras import Extras, print_line
+    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+
+    def agree(flag: bool) -> bool:
+        if world == 1:
+            return flag
+        f = torch.tensor([1 if flag else 0], dtype=torch.int32)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN, group=cpu_group)
+        return bool(f.item())
+
+    ex = Extras(args.budget_s, t_start=T_START, rank=rank, agree=agree, exit_code=0 if ok else 1,
+                emit=lambda rep: print_line({**line, **rep}))
+
     if world > 1 and not args.no_allreduce_sweep:
         # BASELINE §3 "RCCL all-reduce busbw over xGMI" on the same N GPUs, outside the timed GEMM
         # region (every rank participates; rank 0 reports)
         # 8 B .. 1 GiB, fp32 and bf16, algbw and busbw = algbw * 2(n-1)/n
-        try:
+        def rccl(_ex):
             from kubeflow_rm_amd.parallel.collectives import allreduce_sweep
+            out = {}
             for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
                 sw = allreduce_sweep(max_bytes=1 << 30, min_bytes=8, step=8, iters_small=20, iters_large=5,
                                      dtype=dt, device=dev)
-                extra[f"rccl_allreduce_{name}"] = [{"bytes": r["bytes"], "us": round(r["us"], 1),
-                                                    "algbw_GBps": round(r["algbw_GBps"], 1),
-                                                    "busbw_GBps": round(r["busbw_GBps"], 1)} for r in sw]
+                out[f"rccl_allreduce_{name}"] = [{"bytes": r["bytes"], "us": round(r["us"], 1),
+                                                  "algbw_GBps": round(r["algbw_GBps"], 1),
+                                                  "busbw_GBps": round(r["busbw_GBps"], 1)} for r in sw]
                 torch.cuda.empty_cache()
-        except Exception as e:  # reported, never fatal for the GEMM number
-            extra["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
+            return out
+        ex.run("rccl_allreduce", rccl, est_s=20, timeout_s=90, collective=True)
+
         # the hand-written peer all-reduces (K3) on the same GPUs, and the per-link xGMI ceiling
         # their busbw is judged against (153 GB/s x 7 links per GPU, spec)
-        try:
-            from kubeflow_rm_amd.parallel.collectives import fast_allreduce_sweep, xgmi_probe
-            extra["allreduce_oneshot_bf16"] = fast_allreduce_sweep([16 << s for s in range(0, 15, 2)], "oneshot")
-            extra["allreduce_twoshot_bf16"] = fast_allreduce_sweep([256 << 10 << s for s in range(0, 9, 2)],
-                                                                   "twoshot")
+        def peer(_ex):
+            from kubeflow_rm_amd.parallel.collectives import fast_allreduce_sweep
+            return {"allreduce_oneshot_bf16": fast_allreduce_sweep([16 << s for s in range(0, 15, 2)], "oneshot"),
+                    "allreduce_twoshot_bf16": fast_allreduce_sweep([256 << 10 << s for s in range(0, 9, 2)], "twoshot")}
+        ex.run("peer_allreduce", peer, est_s=15, timeout_s=60, collective=True)
+
+        def xgmi(_ex):
+            from kubeflow_rm_amd.parallel.collectives import xgmi_probe
             torch.cuda.empty_cache()
             xg = xgmi_probe()
-            extra["xgmi_peer"] = xg
-            extra["xgmi_peer_GBps"] = xg["pair_GBps_median"]
-        except Exception as e:  # reported, never fatal for the GEMM number
-            extra["fast_allreduce_error"] = f"{type(e).__name__}: {e}"
+            return {"xgmi_peer": xg, "xgmi_peer_GBps": xg["pair_GBps_median"]}
+        ex.run("xgmi_probe", xgmi, est_s=10, timeout_s=60, collective=True)
+
     if args.compare_torch and rank == 0:
-        for _ in range(5):
-            torch.matmul(a, b.t())
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            torch.matmul(a, b.t())
-        torch.cuda.synchronize(dev)
-        extra["torch_matmul_tflops_per_gpu"] = round(flops * args.steps / (time.perf_counter() - t1) / 1e12, 1)
+        def hipblaslt(_ex):
+            for _ in range(5):
+                torch.matmul(a, b.t())
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                torch.matmul(a, b.t())
+            torch.cuda.synchronize(dev)
+            return {"torch_matmul_tflops_per_gpu": round(flops * args.steps / (time.perf_counter() - t1) / 1e12, 1)}
+        ex.run("torch_matmul", hipblaslt, est_s=2, timeout_s=30)
 
     if args.coldstart_runs > 0:
         # the N-GPU notebook needs every GPU: free this rank's memory, park ranks != 0 on a CPU
@@ -185,96 +299,17 @@ def main() -> int:
         del a, b, c
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
-        cpu_group = dist.new_group(backend="gloo") if world > 1 else None
         if world > 1:
             dist.barrier(group=cpu_group)
         if rank == 0:
-            try:
-                from kubeflow_rm_amd.bench_coldstart import measure_cold_start
-                cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world)
-                extra["cold_start_gpus_per_notebook"] = world
-                extra["cold_start_runs"] = len(cs["runs"])
-                extra["cold_start_p50_s"] = cs["p50_s"]
-                extra["cold_start_p90_s"] = cs["p90_s"]
-                extra["cold_start_phases_p50_s"] = cs.get("phases_p50_s")
-                extra["cold_start_readiness"] = cs.get("readiness")
-                # BASELINE §3 north-star #2: controller reconcile latency, from the control plane's own
-                # controller_runtime_reconcile_time_seconds histogram over these runs
-                nbr = (cs.get("reconcile") or {}).get("notebook-controller") or {}
-                extra["reconcile_p50_ms"] = (nbr.get("reconcile") or {}).get("p50_ms")
-                extra["reconcile_p99_ms"] = (nbr.get("reconcile") or {}).get("p99_ms")
-                extra["reconcile_queue_p50_ms"] = (nbr.get("queue") or {}).get("p50_ms")
-                extra["reconcile_by_controller"] = cs.get("reconcile")
-                # the fork's own spawn path: ODH webhook lock + OAuth proxy + two reconciles
-                co = measure_cold_start(runs=max(3, args.coldstart_runs // 2), gpus_per_notebook=world,
-                                        odh_oauth=True, namespace="bench-odh")
-                extra["cold_start_odh_runs"] = len(co["runs"])
-                extra["cold_start_odh_p50_s"] = co["p50_s"]
-                extra["cold_start_odh_p90_s"] = co["p90_s"]
-                extra["cold_start_odh_phases_p50_s"] = co.get("phases_p50_s")
-                extra["cold_start_note"] = ("process pods (no container runtime); notebook server = stub recipe "
-                                            "(no torch import); cold_start_torch_ready_* = same path with a server "
-                                            "that imports torch + runs a GEMM on the GPU before Ready; the GPU "
-                                            "readiness op runs as a native sidecar overlapping the server start; "
-                                            "cold_start_odh_* = ODH path with the OAuth proxy + reconciliation lock; "
-                                            "cold_start_torch_ready_zygote_* = torch-ready server forked from the "
-                                            "kubelet's pre-imported interpreter (torch imported once per node)")
-                if args.coldstart_torch_runs > 0:
-                    ct = measure_cold_start(runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready",
-                                            namespace="bench-torch")
-                    extra["cold_start_torch_ready_runs"] = len(ct["runs"])
-                    extra["cold_start_torch_ready_p50_s"] = ct["p50_s"]
-                    extra["cold_start_torch_ready_p90_s"] = ct["p90_s"]
-                    extra["cold_start_torch_ready_phases_p50_s"] = ct.get("phases_p50_s")
-                    extra["cold_start_torch_ready_server_p50_ms"] = ct.get("server_warmup_p50_ms")
-                    # the same server forked from the node's pre-imported interpreter (kubelet
-                    # --pod-zygote: torch imported once per node, GPU untouched before the fork)
-                    cz = measure_cold_start(runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready",
-                                            namespace="bench-zygote", zygote=True)
-                    extra["cold_start_torch_ready_zygote_runs"] = len(cz["runs"])
-                    extra["cold_start_torch_ready_zygote_p50_s"] = cz["p50_s"]
-                    extra["cold_start_torch_ready_zygote_p90_s"] = cz["p90_s"]
-                    extra["cold_start_torch_ready_zygote_phases_p50_s"] = cz.get("phases_p50_s")
-                    extra["cold_start_torch_ready_zygote_server_p50_ms"] = cz.get("server_warmup_p50_ms")
-            except Exception as e:  # reported, never fatal for the GEMM number
-                extra["cold_start_error"] = f"{type(e).__name__}: {e}"
-            try:  # BASELINE configs 3 and 5: Profile with GPU quota, TensorBoard + PVCViewer on a PVC
-                from kubeflow_rm_amd.bench_coldstart import measure_control_plane
-                extra["control_plane"] = measure_control_plane(runs=5)
-            except Exception as e:  # reported, never fatal for the GEMM number
-                extra["control_plane_error"] = f"{type(e).__name__}: {e}"
+            run_cold_starts(ex, args, world)
         if world > 1:
+            # ranks != 0 wait here for rank 0's cold starts; the watchdog bounds the wait
             dist.barrier(group=cpu_group)
 
+    line.update(ex.finish())
     if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "TFLOPS (bf16 GEMM, aggregate over GPUs)",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "prewarm_s": args.prewarm_s,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (uniform [-1,1) bf16 operands, random-init)",
-            "config": {
-                "model": f"in-pod bf16 matmul HIP smoke (K1 readiness op), C=A@B^T {M}x{N}x{K}",
-                "global_batch": world,
-                "seq_len": None,
-                "parallelism": f"dp{world}",
-            },
-            "per_gpu_tflops": round(per_gpu_tflops, 2),
-            "kernel": "kfamd gemm_w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring, XCD remap, in-kernel edge tiles)",
-            "check_rows": int(rows.numel()),
-            "correct": bool(ok),
-            "max_abs_err_vs_fp32": err,
-            **extra,
-        }
-        print(json.dumps(line), flush=True)
+        ex.emit_once()
     if world > 1:
         dist.destroy_process_group()
     return 0 if ok else 1

@@ -59,10 +59,44 @@ SERVERS = {
 }
 
 
+def _diagnose(c, name: str, namespace: str, log_bytes: int = 2048) -> dict:
+    """What a failed run leaves behind: the pod's phase, conditions and container states, and the last
+    ``log_bytes`` of every container's log (the torch-ready server dumps its threads' stacks there
+    every few seconds while it warms up)."""
+    out: dict = {"pod": f"{name}-0"}
+    try:
+        pod = c.get("v1", "Pod", f"{name}-0", namespace)
+    except Exception as e:  # noqa: BLE001
+        out["pod_error"] = f"{type(e).__name__}: {e}"
+        return out
+    st = pod.get("status") or {}
+    out["phase"] = st.get("phase")
+    out["conditions"] = [{k: cnd.get(k) for k in ("type", "status", "reason")} for cnd in st.get("conditions") or []]
+    logs = {}
+    for cs in (st.get("initContainerStatuses") or []) + (st.get("containerStatuses") or []):
+        out.setdefault("containers", []).append({"name": cs.get("name"), "ready": cs.get("ready"),
+                                                 "restartCount": cs.get("restartCount"), "state": cs.get("state")})
+        try:
+            logs[cs.get("name")] = c.pod_logs(f"{name}-0", namespace, container=cs.get("name"))[-log_bytes:]
+        except Exception as e:  # noqa: BLE001
+            logs[cs.get("name")] = f"<logs unavailable: {type(e).__name__}: {e}>"
+    out["logs_tail"] = logs
+    return out
+
+
+class ColdStartFailure(RuntimeError):
+    """A run that did not become Ready; ``diag`` is _diagnose()'s record."""
+
+    def __init__(self, msg: str, diag: dict | None = None):
+        super().__init__(msg)
+        self.diag = diag or {}
+
+
 def _wait_ready(c, name: str, namespace: str, timeout: float) -> dict:
     """Poll the Notebook every 5 ms until readyReplicas == 1. Every ~100 ms also look at the pod: an
     init container (the GPU readiness op) that terminated non-zero, or a main container that exited,
-    fails the run at once with its termination message instead of after the whole timeout."""
+    fails the run at once with its termination message instead of after the whole timeout. Either
+    failure carries the pod's diagnostics (ColdStartFailure.diag)."""
     deadline = time.time() + timeout
     next_pod_check = time.time() + 0.1
     while True:
@@ -83,11 +117,29 @@ def _wait_ready(c, name: str, namespace: str, timeout: float) -> dict:
             for cs in (st.get("initContainerStatuses") or []) + (st.get("containerStatuses") or []):
                 term = (cs.get("state") or {}).get("terminated") or {}
                 if term and term.get("exitCode", 0) != 0:
-                    raise RuntimeError(f"{name}: container {cs.get('name')} exited {term.get('exitCode')}: "
-                                       f"{(term.get('message') or '')[:400]}")
+                    raise ColdStartFailure(f"{name}: container {cs.get('name')} exited {term.get('exitCode')}: "
+                                           f"{(term.get('message') or '')[:400]}", _diagnose(c, name, namespace))
         if now > deadline:
-            raise TimeoutError(f"{name}: not Ready within {timeout:.0f} s")
+            raise ColdStartFailure(f"{name}: not Ready within {timeout:.0f} s", _diagnose(c, name, namespace))
         time.sleep(0.005)
+
+
+def _teardown(c, name: str, namespace: str, settle_s: float) -> None:
+    """Delete the run's Notebook and wait for its pod to go (the GPU is free again), then settle."""
+    try:
+        c.delete("kubeflow.org/v1", "Notebook", name, namespace)
+        c.wait_gone("kubeflow.org/v1", "Notebook", name, namespace, timeout=60)
+    except Exception:  # noqa: BLE001 - already gone
+        pass
+    # the StatefulSet / pod are garbage collected asynchronously; wait for the GPU to free up
+    end = time.time() + 60
+    while time.time() < end:
+        try:
+            c.get("v1", "Pod", f"{name}-0", namespace)
+        except Exception:  # noqa: BLE001
+            break
+        time.sleep(0.02)
+    time.sleep(settle_s)
 
 
 def _reconcile_latency(url: str) -> dict:
@@ -113,9 +165,17 @@ def _reconcile_latency(url: str) -> dict:
 def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | None = None, image: str = "kfamd/jupyter-pytorch-rocm:latest",
                        readiness: bool = True, timeout: float = 120.0, namespace: str = "bench",
                        settle_s: float = 0.5, server: str = "stub", odh_oauth: bool = False,
-                       zygote: bool = False) -> dict:
-    """Returns {"p50_s", "p90_s", "runs": [...], "phases_p50_s": {...}, "readiness": {...},
+                       zygote: bool = False, env: dict | None = None, deadline: float | None = None,
+                       max_failures: int = 2) -> dict:
+    """Returns {"p50_s", "p90_s", "runs": [...], "failures": [...], "phases_p50_s": {...}, "readiness": {...},
     "reconcile": {controller: {"reconcile": {p50_ms, p99_ms}, "queue": {...}}}}.
+
+    A run that is not Ready within ``timeout`` (or whose container exits non-zero) is recorded in
+    ``failures`` with the pod's phase, container states and log tails (``_diagnose``) and the next
+    run goes on; after ``max_failures`` of them the measurement stops. ``deadline`` (wall-clock
+    ``time.time()``) stops starting new runs, so a caller with a total budget gets a partial result
+    (``"truncated": true``) instead of none. ``env``: extra container env (e.g. an A/B knob).
+    p50/p90 are over the runs that became Ready; ``failures`` says how many did not.
 
     ``server``: "stub" or "torch-ready" (see SERVERS). Both are process pods (no container runtime).
     ``odh_oauth``: the ODH spawn path of SURVEY CS1 with OAuth: the ODH webhook injects the
@@ -132,21 +192,29 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     /dev/kfd waits for that (100-130 ms right after an exit, 0.1 ms after >= 0.25 s:
     ``profiles/r1_coldstart2/kfd_gap.txt``); back to back, run i+1 would pay run i's teardown.
     """
-    out_runs = []
+    out_runs: list[dict] = []
+    failures: list[dict] = []
+    truncated = False
     with LocalCluster(gpus=gpus, zygote=zygote) as cl:
         if zygote:
-            cl.wait_zygotes(timeout=300)
+            cl.wait_zygotes(timeout=300 if deadline is None else max(1.0, min(300.0, deadline - time.time())))
         c = cl.client
         c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": namespace}})
         for i in range(runs):
+            if deadline is not None and time.time() + 1.0 > deadline:
+                truncated = True
+                break
+            if len(failures) >= max_failures:
+                truncated = True
+                break
             name = f"cs-{i}"
             ann = {} if readiness else {"kfamd.io/gpu-readiness-op": "false"}
             if odh_oauth:
                 ann["notebooks.opendatahub.io/inject-oauth"] = "true"
             ctr = {"name": name, "image": image, "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}}}
             srv = SERVERS[server]
-            if srv.get("env"):
-                ctr["env"] = list(srv["env"])
+            if srv.get("env") or env:
+                ctr["env"] = list(srv.get("env") or []) + [{"name": k, "value": str(v)} for k, v in (env or {}).items()]
             if srv.get("probe"):
                 ctr["readinessProbe"] = {"httpGet": {"path": f"/notebook/{namespace}/{name}/api/status", "port": 8888},
                                          "periodSeconds": 5}
@@ -155,7 +223,13 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                   "spec": {"template": {"spec": {"containers": [ctr]}}}}
             t0 = time.time()
             c.create(nb)
-            obj = _wait_ready(c, name, namespace, timeout)
+            run_timeout = timeout if deadline is None else max(1.0, min(timeout, deadline - time.time()))
+            try:
+                obj = _wait_ready(c, name, namespace, run_timeout)
+            except ColdStartFailure as e:
+                failures.append({"run": i, "error": str(e), "after_s": round(time.time() - t0, 3), **e.diag})
+                _teardown(c, name, namespace, settle_s)
+                continue
             t1 = time.time()
             pod = c.get("v1", "Pod", f"{name}-0", namespace)
             t_sched = _cond(pod, "PodScheduled")
@@ -216,17 +290,7 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                              "controller_phases_ms": ctl_phases,
                              "gpus": (obj.get("status") or {}).get("gpus"),
                              "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
-            c.delete("kubeflow.org/v1", "Notebook", name, namespace)
-            c.wait_gone("kubeflow.org/v1", "Notebook", name, namespace, timeout=60)
-            # the StatefulSet / pod are garbage collected asynchronously; wait for the GPU to free up
-            deadline = time.time() + 60
-            while time.time() < deadline:
-                try:
-                    c.get("v1", "Pod", f"{name}-0", namespace)
-                except Exception:
-                    break
-                time.sleep(0.02)
-            time.sleep(settle_s)
+            _teardown(c, name, namespace, settle_s)
         try:
             recon = _reconcile_latency(cl.url)
         except Exception as e:  # noqa: BLE001 - reported, never fatal
@@ -234,6 +298,7 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     xs = [r["cold_start_s"] for r in out_runs]
     phase_keys = sorted({k for r in out_runs for k in r["phases"]})
     res = {"p50_s": _pct(xs, 0.5), "p90_s": _pct(xs, 0.9), "settle_s": settle_s, "runs": out_runs, "server": server,
+           "failures": failures, "truncated": truncated, "env": env or None,
            "odh_oauth": odh_oauth, "zygote": zygote, "reconcile": recon,
            "phases_p50_s": {k: _pct([r["phases"][k] for r in out_runs if k in r["phases"]], 0.5) for k in phase_keys}}
     stage_keys = sorted({k for r in out_runs for k, v in r["readiness_stages"].items() if v is not None})
@@ -309,14 +374,22 @@ def main() -> int:
     p.add_argument("--zygote", action="store_true", help="kubelet --pod-zygote (pre-imported interpreter)")
     p.add_argument("--server", choices=sorted(SERVERS), default="stub",
                    help="notebook server recipe: stub (no torch) or torch-ready (torch import + GEMM before Ready)")
+    p.add_argument("--env", action="append", default=[], metavar="K=V", help="extra notebook container env (repeatable)")
+    p.add_argument("--timeout", type=float, default=120.0, help="per-run Ready deadline, seconds")
+    p.add_argument("--max-failures", type=int, default=2)
     a = p.parse_args()
+    env = dict(kv.split("=", 1) for kv in a.env) or None
     r = measure_cold_start(runs=a.runs, gpus_per_notebook=a.gpus_per_notebook, gpus=a.gpus, readiness=not a.no_readiness,
-                           settle_s=a.settle, server=a.server, odh_oauth=a.odh_oauth, zygote=a.zygote)
-    print(json.dumps({k: v for k, v in r.items() if k != "runs"}))
-    print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
+                           settle_s=a.settle, server=a.server, odh_oauth=a.odh_oauth, zygote=a.zygote, env=env,
+                           timeout=a.timeout, max_failures=a.max_failures)
+    print(json.dumps({k: v for k, v in r.items() if k not in ("runs", "failures")}))
+    for f in r["failures"]:
+        print(json.dumps({"failure": f}))
+    if r["runs"]:
+        print(json.dumps({"median_run": statistics.median(x["cold_start_s"] for x in r["runs"])}))
     for x in r["runs"]:
         print(json.dumps({"run_s": round(x["cold_start_s"], 4), "server_warmup": x.get("server_warmup")}))
-    return 0
+    return 1 if r["failures"] else 0
 
 
 if __name__ == "__main__":

@@ -44,58 +44,161 @@ WARMUP: dict = {}
 PREINIT: dict = {}  # cumulative ms of the HIP pre-init thread's steps
 
 
-def _preinit_hip() -> threading.Thread | None:
-    """Bring up the HIP runtime and this process's device context on a side thread while the main
-    thread imports torch (1.5-1.8 s). The thread loads torch's own bundled libamdhip64 (same SONAME
-    torch links, so torch reuses the initialised runtime) without importing torch; ctypes drops
-    the GIL for each call, so the two overlap. KFAMD_HIP_PREINIT=0 disables it."""
-    if os.environ.get("KFAMD_HIP_PREINIT", "1") == "0":
-        return None
-    import ctypes
+def _hip_lib() -> str | None:
+    """torch's bundled libamdhip64 (same SONAME torch links, so torch reuses the initialised runtime)."""
     import importlib.util
     spec = importlib.util.find_spec("torch")
     locs = list(spec.submodule_search_locations or []) if spec else []
-    lib = next((os.path.join(d, "lib", "libamdhip64.so") for d in locs
-                if os.path.exists(os.path.join(d, "lib", "libamdhip64.so"))), None)
+    return next((os.path.join(d, "lib", "libamdhip64.so") for d in locs
+                 if os.path.exists(os.path.join(d, "lib", "libamdhip64.so"))), None)
+
+
+def _hip_preinit_run(lib: str) -> None:
+    """HIP runtime + this process's device context + the first GPU operation (the null stream's HW
+    queue, the runtime's blit kernels: ~90 ms), through HIP's own entry points only (ctypes drops the
+    GIL for each call). Every step stamps PREINIT (ms since the thread started) so a stall names its step."""
+    import ctypes
+    t = time.perf_counter()
+
+    def stamp(k):
+        PREINIT[k] = round((time.perf_counter() - t) * 1e3, 1)
+
+    try:
+        PREINIT["step"] = "dlopen"
+        hip = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
+        stamp("dlopen_ms")
+        PREINIT["step"] = "hipInit"
+        ok = hip.hipInit(0) == 0
+        stamp("hip_init_ms")
+        PREINIT["step"] = "context"
+        if ok and hip.hipSetDevice(0) == 0:
+            hip.hipFree(None)  # creates the device context now
+            stamp("context_ms")
+            PREINIT["step"] = "first_op"
+            buf = ctypes.c_void_p()
+            if hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(4096)) == 0:
+                hip.hipMemset(buf, 0, ctypes.c_size_t(4096))
+                hip.hipDeviceSynchronize()
+                hip.hipFree(buf)
+            stamp("first_op_ms")
+        PREINIT["step"] = "done"
+    except OSError as e:
+        PREINIT["step"] = f"error: {e}"  # torch initialises on first use as usual
+
+
+class _AfterTorchC:
+    """sys.meta_path hook: runs ``callback`` right after the extension module ``torch._C`` has been
+    created, i.e. after libtorch / libtorch_hip are loaded and every static constructor that registers
+    torch's HIP fat binaries has run. The rest of ``import torch`` (~1 s of pure-Python module imports)
+    then overlaps the HIP pre-init thread, and no HIP call on that thread can race a dlopen whose
+    constructors call into HIP (the loader-lock / registration interleaving of the old
+    whole-import overlap)."""
+
+    def __init__(self, callback):
+        self.callback = callback
+        self.fired = False
+
+    def find_spec(self, fullname, path=None, target=None):
+        if fullname != "torch._C" or self.fired:
+            return None
+        import importlib.machinery
+        spec = importlib.machinery.PathFinder.find_spec(fullname, path)
+        if spec is None or spec.loader is None:
+            return None
+        inner, hook = spec.loader, self
+
+        class _Loader:
+            def create_module(self, s):
+                m = inner.create_module(s)
+                hook._fire()
+                return m
+
+            def exec_module(self, m):
+                inner.exec_module(m)
+
+        spec.loader = _Loader()
+        return spec
+
+    def _fire(self):
+        if not self.fired:
+            self.fired = True
+            try:
+                sys.meta_path.remove(self)
+            except ValueError:
+                pass
+            self.callback()
+
+
+def _preinit_hip() -> dict | None:
+    """Bring up the HIP runtime and this process's device context on a side thread while the main
+    thread finishes ``import torch``. KFAMD_HIP_PREINIT selects when the thread starts:
+
+    * ``after-c`` (default): once ``torch._C`` exists (torch's HIP code objects registered); overlaps
+      the Python half of the import.
+    * ``thread``: before the import starts (overlaps the whole import, including the dlopen of
+      libtorch_hip whose constructors register fat binaries while hipInit runs on the side thread —
+      kept only for the A/B in profiles/r4_coldstart).
+    * ``0``: off; torch initialises HIP on first use.
+
+    Returns {"mode", "thread"} (thread may still be None while waiting for torch._C)."""
+    mode = os.environ.get("KFAMD_HIP_PREINIT", "after-c")
+    if mode in ("0", "off", ""):
+        return None
+    lib = _hip_lib()
     if lib is None:
         return None
+    st: dict = {"mode": mode, "thread": None}
 
-    def run():
-        try:
-            t = time.perf_counter()
-            hip = ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
-            PREINIT["dlopen_ms"] = round((time.perf_counter() - t) * 1e3, 1)
-            ok = hip.hipInit(0) == 0
-            PREINIT["hip_init_ms"] = round((time.perf_counter() - t) * 1e3, 1)
-            if ok and hip.hipSetDevice(0) == 0:
-                hip.hipFree(None)  # creates the device context now
-                PREINIT["context_ms"] = round((time.perf_counter() - t) * 1e3, 1)
-                # the first GPU operation of the process pays ~90 ms more (the null stream's HW queue,
-                # the runtime's blit kernels): a memset + sync here, under the import. Only HIP's
-                # own entry points (ctypes drops the GIL for each); loading another HIP library on
-                # this thread while torch registers its kernels on the main one can deadlock.
-                buf = ctypes.c_void_p()
-                if hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(4096)) == 0:
-                    hip.hipMemset(buf, 0, ctypes.c_size_t(4096))
-                    hip.hipDeviceSynchronize()
-                    hip.hipFree(buf)
-                PREINIT["first_op_ms"] = round((time.perf_counter() - t) * 1e3, 1)
-        except OSError:
-            pass  # torch initialises on first use as usual
+    def start():
+        PREINIT["start_ms"] = round((time.perf_counter() - _T_WARMUP[0]) * 1e3, 1)
+        th = threading.Thread(target=_hip_preinit_run, args=(lib,), name="hip-preinit", daemon=True)
+        st["thread"] = th
+        th.start()
 
-    t = threading.Thread(target=run, name="hip-preinit", daemon=True)
-    t.start()
-    return t
+    if mode == "thread" or "torch._C" in sys.modules:
+        start()
+    else:
+        st["hook"] = _AfterTorchC(start)
+        sys.meta_path.insert(0, st["hook"])
+    return st
+
+
+_T_WARMUP = [time.perf_counter()]
 
 
 def warmup_torch() -> dict:
-    """import torch + the framework's kernels and run one GEMM on cuda:0 (the pod's first GPU)."""
-    t0 = time.perf_counter()
+    """import torch + the framework's kernels and run one GEMM on cuda:0 (the pod's first GPU).
+
+    While it runs, ``faulthandler`` dumps every thread's Python stack to the container log every
+    KFAMD_WARMUP_TRACE_S seconds (default 5; 0 disables), so a slow or stuck warmup leaves the
+    evidence of where it is in the pod log the cold-start bench collects on failure."""
+    import faulthandler
+    trace_s = float(os.environ.get("KFAMD_WARMUP_TRACE_S", "5") or 0)
+    if trace_s > 0:
+        faulthandler.dump_traceback_later(trace_s, repeat=True, file=sys.stderr)
+    try:
+        return _warmup_torch()
+    finally:
+        if trace_s > 0:
+            faulthandler.cancel_dump_traceback_later()
+
+
+def _warmup_torch() -> dict:
+    t0 = _T_WARMUP[0] = time.perf_counter()
     pre = _preinit_hip()
     import torch
     t1 = time.perf_counter()
-    if pre is not None:
-        pre.join()
+    if pre is not None and pre.get("hook") is not None and not pre["hook"].fired:
+        try:  # torch._C came from somewhere the hook did not see (already imported): start now
+            sys.meta_path.remove(pre["hook"])
+        except ValueError:
+            pass
+        pre["hook"]._fire()
+    if pre is not None and pre["thread"] is not None:
+        pre["thread"].join(timeout=30)
+        if pre["thread"].is_alive():
+            PREINIT["joined"] = False  # reported; torch goes on and initialises HIP itself
+    t_join = time.perf_counter()
     from kubeflow_rm_amd import ops
     t2 = time.perf_counter()
     dev = torch.device("cuda", 0)
@@ -120,7 +223,7 @@ def warmup_torch() -> dict:
     ok = bool(torch.isfinite(got).all().item()) and err <= 1e-2 * ref.abs().max().item() + 1e-2
     t4 = time.perf_counter()
     return {"ok": ok, "check_ms": round((t4 - t3) * 1e3, 1), "import_torch_ms": round((t1 - t0) * 1e3, 1), "import_ops_ms": round((t2 - t1) * 1e3, 1),
-            "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1), "hip_preinit": pre is not None,
+            "first_gemm_ms": round((t3 - t2) * 1e3, 1), "total_ms": round((t3 - t0) * 1e3, 1), "hip_preinit": (pre or {}).get("mode"), "preinit_join_ms": round((t_join - t1) * 1e3, 1),
             "preinit_ms": dict(PREINIT),
             "max_abs_err": err}
 

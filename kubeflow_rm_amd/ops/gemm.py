@@ -471,9 +471,11 @@ class _Linear(torch.autograd.Function):
             y = gemm_nt(x, weight, bias=bias, residual=residual.contiguous())
         else:
             y = gemm_nt(x, weight, bias=bias, act=act)
+            if act == "relu":
+                z = y  # relu' is read from the activation output BEFORE the residual add
             if residual is not None:
                 y = y + residual
-        ctx.save_for_backward(x2, weight, bias, y if act == "relu" else z)
+        ctx.save_for_backward(x2, weight, bias, z)
         ctx.act = act
         ctx.xshape = x.shape
         return y

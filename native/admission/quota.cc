@@ -99,27 +99,25 @@ std::string fmt_num(double v) {
 // in-process), never by pod name: kube-apiserver sends generateName creates (ReplicaSet / Job pods)
 // with an EMPTY name, so name keys made concurrent generateName creates overwrite each other
 // (ADVICE r2). Landing is matched by name when the request had one, otherwise by generateName: the
-// oldest open reservation of that prefix claims one landed pod of the prefix created no earlier than
-// the reservation (a landed pod claims at most one reservation, ever).
+// oldest open reservation of that prefix claims one landed pod of the prefix that was NOT listed when
+// the reservation was made (a landed pod claims at most one reservation, ever). Name sets rather than
+// creationTimestamps (1 s resolution): a pod that landed just before the reservation, and was never
+// claimed, could otherwise claim it and drop an in-flight pod's usage from the total.
 // Reference quota semantics: profile-controller/controllers/profile_controller.go:559-589
 // (the Profile's ResourceQuota) enforced by kube-apiserver's quota admission.
 namespace {
 constexpr double kReservationTtl = 30.0;
 
-double wall_seconds() {  // creationTimestamps are wall-clock; now_seconds() is monotonic
-  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
-}
-
 struct LandedPod {
   std::string name, generate_name;
-  double created = 0;  // creationTimestamp, seconds (RFC 3339 has 1 s resolution)
 };
 
 struct QuotaLedger {
   struct Reservation {
     std::map<std::string, double> use;
-    double expires = 0, reserved_at = 0;
+    double expires = 0;
     std::string name, generate_name;
+    std::set<std::string> existed;  // pods of generate_name listed at reserve time: never claim this one
     uint64_t seq = 0;
   };
   std::mutex mu;
@@ -162,7 +160,7 @@ struct QuotaLedger {
           }
       } else if (!r.generate_name.empty()) {
         for (const auto& p : pods)
-          if (p.generate_name == r.generate_name && !cl.count(p.name) && p.created + 1.0 >= r.reserved_at) {
+          if (p.generate_name == r.generate_name && !cl.count(p.name) && !r.existed.count(p.name)) {
             landed = true;
             cl.insert(p.name);
             break;
@@ -174,16 +172,19 @@ struct QuotaLedger {
     return out;
   }
   std::string reserve(const std::string& ns, const std::string& key_hint, const std::string& name,
-                      const std::string& generate_name, std::map<std::string, double> use) {
+                      const std::string& generate_name, std::map<std::string, double> use,
+                      const std::vector<LandedPod>& listed) {
     std::lock_guard<std::mutex> g(mu);
     const uint64_t seq = ++next_seq;
     const std::string key = key_hint.empty() ? "seq:" + std::to_string(seq) : "uid:" + key_hint;
     Reservation r;
     r.use = std::move(use);
-    r.reserved_at = wall_seconds();
     r.expires = now_seconds() + kReservationTtl;
     r.name = name;
     r.generate_name = generate_name;
+    if (!generate_name.empty())
+      for (const auto& p : listed)
+        if (p.generate_name == generate_name) r.existed.insert(p.name);
     r.seq = seq;
     by_ns[ns][key] = std::move(r);
     return key;
@@ -218,7 +219,6 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
       LandedPod lp;
       lp.name = p.str_at({"metadata", "name"});
       lp.generate_name = p.str_at({"metadata", "generateName"});
-      if (auto t = parse_rfc3339_ms(p.str_at({"metadata", "creationTimestamp"}))) lp.created = *t / 1000.0;
       landed.push_back(std::move(lp));
       if (pod_counts(p))
         for (auto& kv : pod_quota_usage(p, hbm_dev)) used[kv.first] += kv.second;
@@ -243,7 +243,7 @@ AdmissionFn make_quota_plugin(std::shared_ptr<Client> c, int64_t hbm) {
     }
     if (a.dry_run) return {};
     const std::string key = ledger->reserve(a.ns, a.uid, name, a.object->str_at({"metadata", "generateName"}),
-                                            std::move(want));
+                                            std::move(want), landed);
     const std::string ns = a.ns;
     // in-process: the pod is in the store (its list entry replaces the reservation) or never will be
     a.on_done.push_back([ledger, ns, key](bool) { ledger->release(ns, key); });

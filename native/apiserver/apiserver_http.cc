@@ -5,6 +5,7 @@
 // DELETE (single + collection), discovery (/api, /apis, /apis/{g}/{v}), /version, /healthz,
 // /readyz, /livez, /metrics, pod logs, the services/{name}:{port}/proxy subresource (used by the
 // culler in DEV mode like `kubectl proxy`), and /debug/faults for fault injection.
+#include <atomic>
 #include <algorithm>
 #include <chrono>
 
@@ -270,6 +271,10 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
   }
   bool watch = req.q("watch") == "true" || req.q("watch") == "1";
   std::string verb = verb_for(req.method, !name.empty(), watch);
+  // pods/exec runs a command in the container whatever the HTTP method (kubectl upgrades a GET to a
+  // stream): authorize it as "create", as Kubernetes does since CVE-2018-1002105's follow-ups, so a role
+  // with only get on pods/* cannot run commands
+  if (group.empty() && plural == "pods" && (sub == "exec" || sub == "attach")) verb = "create";
   std::string authz_sub = sub;
   if (cfg_.authz_rbac) {
     std::string reason;
@@ -327,6 +332,19 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
       send_error(resp, e, "Pod", name);
       return;
     }
+    // each exec holds an API server worker for its duration: at most kMaxConcurrentExec at once, so
+    // long execs can never starve controllers and watches of workers
+    static std::atomic<int> active_exec{0};
+    constexpr int kMaxConcurrentExec = 4;
+    if (active_exec.fetch_add(1) >= kMaxConcurrentExec) {
+      active_exec.fetch_sub(1);
+      resp.json(429, ApiError{429, "TooManyRequests", "too many concurrent exec sessions, retry later"}.status_json().dump());
+      return;
+    }
+    struct ExecSlot {
+      std::atomic<int>& n;
+      ~ExecSlot() { n.fetch_sub(1); }
+    } exec_slot{active_exec};
     int code = 0;
     std::string out, err;
     // bounded: the request holds one API server worker for its duration

@@ -1,4 +1,5 @@
 // kubelet.cc — process-pod kubelet with the MI355X device plugin (see node.h).
+#include <cstdio>
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -785,20 +786,46 @@ bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::str
   }
   std::string reason;
   double deadline = now_seconds() + timeout_s;
-  bool killed = false;
+  bool killed = false, too_big = false;
+  constexpr size_t kMaxOut = 16u << 20;       // the reply carries at most the last 16 MiB
+  constexpr off_t kMaxFile = 64ll << 20;      // a command that writes more is killed (disk + RAM bound)
+  double next_size_check = 0;
   while (!reap(pid, exit_code, reason)) {
-    if (now_seconds() > deadline) {
+    const double now = now_seconds();
+    if (!killed && now > deadline) {
       ::kill(-pid, SIGKILL);
       killed = true;
-      deadline = now_seconds() + 5;
+      deadline = now + 5;
+    }
+    if (!killed && now >= next_size_check) {  // bounded output: e.g. `yes` fills 64 MiB in well under a second
+      next_size_check = now + 0.01;
+      struct stat st{};
+      if (::stat(out_path.c_str(), &st) == 0 && st.st_size > kMaxFile) {
+        ::kill(-pid, SIGKILL);
+        killed = too_big = true;
+        deadline = now + 5;
+      }
     }
     ::usleep(2000);
   }
-  if (!read_file(out_path, output)) output.clear();
+  // read only the tail: seek to the last kMaxOut bytes
+  output.clear();
+  bool truncated = false;
+  if (FILE* f = std::fopen(out_path.c_str(), "rb")) {
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+      const long size = std::ftell(f);
+      const long from = size > static_cast<long>(kMaxOut) ? size - static_cast<long>(kMaxOut) : 0;
+      truncated = from > 0;
+      std::fseek(f, from, SEEK_SET);
+      output.resize(static_cast<size_t>(size - from));
+      output.resize(std::fread(output.data(), 1, output.size(), f));
+    }
+    std::fclose(f);
+  }
   ::unlink(out_path.c_str());
-  constexpr size_t kMaxOut = 16u << 20;  // the reply carries at most the last 16 MiB
-  if (output.size() > kMaxOut) output = "[... output truncated ...]\n" + output.substr(output.size() - kMaxOut);
-  if (killed) output += "\ncommand terminated: timeout after " + std::to_string(static_cast<int>(timeout_s)) + " s\n";
+  if (truncated) output = "[... output truncated ...]\n" + output;
+  if (too_big) output += "\ncommand terminated: output exceeded " + std::to_string(kMaxFile >> 20) + " MiB\n";
+  else if (killed) output += "\ncommand terminated: timeout after " + std::to_string(static_cast<int>(timeout_s)) + " s\n";
   return true;
 }
 

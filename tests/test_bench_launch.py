@@ -69,3 +69,58 @@ def test_control_plane_latencies_measured():
     r = measure_control_plane(runs=2)
     for k in ("profile_ready_p50_s", "tensorboard_ready_p50_s", "pvcviewer_ready_p50_s"):
         assert r[k] is not None and 0 < r[k] < 30, r
+
+
+_HANG_STUB = r"""
+import json, os, sys, time
+sys.path.insert(0, sys.argv[2])
+from kubeflow_rm_amd.bench_extras import Extras, print_line
+r = int(os.environ["RANK"])
+line = {"metric": "stub", "n_gpus": int(os.environ["WORLD_SIZE"])}
+ex = Extras(float(sys.argv[3]), rank=r, grace_s=1.0, nonzero_rank_delay_s=1.0,
+            emit=lambda rep: print_line({**line, **rep}))
+ex.run("quick", lambda e: {"quick_value": 1}, est_s=0.1, timeout_s=5)
+ex.run("broken", lambda e: 1 / 0, est_s=0.1, timeout_s=5)
+ex.run("hang", lambda e: time.sleep(3600), est_s=0.1, timeout_s=2)
+ex.run("never", lambda e: {"never": 1})
+line.update(ex.finish())
+ex.emit_once()
+"""
+
+
+def test_bench_extra_that_hangs_still_yields_the_line(tmp_path):
+    """one extra hangs on every rank; the self-launched job still ends well inside
+    the budget with exactly one JSON line, the hung extra marked ``timeout``, the finished ones kept."""
+    import time
+    stub = tmp_path / "hang.py"
+    stub.write_text(_HANG_STUB)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    env["KFAMD_BENCH_RANK_ARGV"] = json.dumps([sys.executable, str(stub), str(tmp_path), str(ROOT), "60"])
+    t0 = time.time()
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    took = time.time() - t0
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    st = d["extras_status"]
+    assert st["quick"]["status"] == "ok" and d["quick_value"] == 1
+    assert st["broken"]["status"] == "error" and "ZeroDivisionError" in st["broken"]["error"]
+    assert st["hang"]["status"] == "timeout"
+    assert "never" not in st and "never" not in d
+    assert took < 40, took
+
+
+def test_bench_extras_skip_what_does_not_fit_the_budget():
+    from kubeflow_rm_amd.bench_extras import Extras
+    ex = Extras(5.0)
+    assert ex.run("fits", lambda e: {"x": 1}, est_s=1)
+    assert not ex.run("too_big", lambda e: {"y": 1}, est_s=30)
+    # collective extras follow the agreement, not the local view
+    ex.agree = lambda ok: False
+    assert not ex.run("peer_says_no", lambda e: {"z": 1}, est_s=0, collective=True)
+    rep = ex.finish()
+    assert rep["x"] == 1 and "y" not in rep and "z" not in rep
+    assert rep["extras_status"]["too_big"]["status"] == "skipped"
+    assert rep["extras_status"]["peer_says_no"]["status"] == "skipped"

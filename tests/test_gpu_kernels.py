@@ -506,6 +506,30 @@ def test_linear_residual_in_epilogue(bias):
         assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, err
 
 
+@pytest.mark.parametrize("act", ["relu", "gelu_tanh", "silu"])
+def test_linear_activation_with_residual_grads(act):
+    """y = act(x W^T + b) + r. The activation's derivative must come from the
+    pre-residual values: the residual (here offset by +2, so y > 0 almost everywhere) must not leak
+    into relu's mask. Every gradient against F.linear + act + add in fp32."""
+    from kubeflow_rm_amd.ops import linear
+    F = torch.nn.functional
+    x = _rand(2, 256, 512, seed=101).requires_grad_(True)
+    w = _rand(768, 512, seed=102, scale=0.05).requires_grad_(True)
+    b = _rand(768, seed=103).requires_grad_(True)
+    r = (_rand(2, 256, 768, seed=104).float() + 2.0).to(torch.bfloat16).requires_grad_(True)
+    y = linear(x, w, b, act=act, residual=r)
+    g = _rand(*y.shape, seed=105)
+    y.backward(g)
+    xr, wr, br, rr = (t.detach().float().requires_grad_(True) for t in (x, w, b, r))
+    zr = F.linear(xr, wr, br)
+    ar = torch.relu(zr) if act == "relu" else (F.gelu(zr, approximate="tanh") if act == "gelu_tanh" else F.silu(zr))
+    yr = ar + rr
+    yr.backward(g.float())
+    for got, ref in [(y, yr), (x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad), (r.grad, rr.grad)]:
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 2e-2 * (ref.abs().max().item() + 1e-3) + 2e-2, (act, err)
+
+
 @pytest.mark.parametrize("act", ["gelu_tanh", "silu"])
 @pytest.mark.parametrize("mode", ["fused", "split"])
 def test_preact_modes_agree(act, mode):

@@ -284,3 +284,54 @@ def test_top_from_a_separate_node_agent_metrics_url():
         assert "team-a/nb-0" in out.getvalue()
     finally:
         srv.shutdown()
+
+
+def test_exec_output_is_bounded(cl):
+    """a command that floods stdout (``yes``) is killed once its output passes 64 MiB and the
+    reply carries at most the last 16 MiB, instead of filling the pod directory and the kubelet's RAM."""
+    nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook", "metadata": {"name": "floodnb", "namespace": "ci-ns"},
+          "spec": {"template": {"spec": {"containers": [{"name": "floodnb", "image": "jupyter-scipy:latest"}]}}}}
+    cl.client.create(nb)
+    cl.client.wait_for("kubeflow.org/v1", "Notebook", "floodnb", "ci-ns",
+                       lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=60)
+    t0 = time.time()
+    r = cl.client.pod_exec("floodnb-0", "ci-ns", ["yes"], timeout=120)
+    assert time.time() - t0 < 60
+    out = r["output"]
+    assert "output exceeded 64 MiB" in out
+    assert len(out) <= (16 << 20) + 200
+    assert out.startswith("[... output truncated ...]")
+    cl.client.delete("kubeflow.org/v1", "Notebook", "floodnb", "ci-ns")
+
+
+def test_exec_needs_create_on_pods_exec():
+    """pods/exec is authorized as ``create``, whatever the HTTP method. A user whose
+    role grants get/list on pods and every pods/* subresource gets 403 from exec (GET and POST); with
+    ``create pods/exec`` the request gets past authorization (404: no such pod)."""
+    from tests.conftest import _ensure_native
+    _ensure_native()
+    from kubeflow_rm_amd.client import ApiException, KubeClient
+    with LocalCluster(args=["--authorization-mode", "RBAC"], controllers="builtin") as c:
+        admin = c.client
+        admin.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "rb"}})
+        admin.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "reader", "namespace": "rb"},
+                      "rules": [{"apiGroups": [""], "resources": ["pods", "pods/*"], "verbs": ["get", "list", "watch"]}]})
+        admin.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding", "metadata": {"name": "eve-reads", "namespace": "rb"},
+                      "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": "reader"},
+                      "subjects": [{"kind": "User", "name": "eve", "apiGroup": "rbac.authorization.k8s.io"}]})
+        eve = KubeClient(c.url, impersonate="eve")
+        for method in ("GET", "POST"):
+            with pytest.raises(ApiException) as e:
+                eve._req(method, "/api/v1/namespaces/rb/pods/p-0/exec", params={"command": "id"})
+            assert e.value.status == 403, (method, e.value.status)
+        with pytest.raises(ApiException) as e:
+            eve.get("v1", "Pod", "p-0", "rb")
+        assert e.value.status == 404  # get itself is allowed
+        admin.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role", "metadata": {"name": "execer", "namespace": "rb"},
+                      "rules": [{"apiGroups": [""], "resources": ["pods/exec"], "verbs": ["create"]}]})
+        admin.create({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding", "metadata": {"name": "eve-execs", "namespace": "rb"},
+                      "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": "execer"},
+                      "subjects": [{"kind": "User", "name": "eve", "apiGroup": "rbac.authorization.k8s.io"}]})
+        with pytest.raises(ApiException) as e:
+            eve._req("POST", "/api/v1/namespaces/rb/pods/p-0/exec", params={"command": "id"})
+        assert e.value.status == 404

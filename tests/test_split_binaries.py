@@ -181,3 +181,30 @@ def test_quota_webhook_concurrent_generate_name_creates(split):
     with cf.ThreadPoolExecutor(8) as ex:
         allowed = list(ex.map(review, range(8)))
     assert sum(allowed) == 2, allowed
+
+    # a pod of the same prefix that landed just before a reservation and was never
+    # claimed (here: created before the quota existed, so it never had one) must not claim the
+    # in-flight reservation; 1 landed + 1 reserved = 2, so the next create is denied
+    c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "gen-quota2"}})
+    c.create({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "job2-early", "generateName": "job2-",
+                                                              "namespace": "gen-quota2"},
+              "spec": {"nodeName": "none", "containers": [{"name": "x", "image": "x",
+                                                           "resources": {"limits": {"amd.com/gpu": "1"}}}]}})
+    c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q", "namespace": "gen-quota2"},
+              "spec": {"hard": {"amd.com/gpu": "2"}}})
+
+    def review2(_):
+        body = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                "request": {"uid": str(uuid.uuid4()), "operation": "CREATE", "namespace": "gen-quota2", "name": "",
+                            "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                            "resource": {"group": "", "version": "v1", "resource": "pods"},
+                            "userInfo": {"username": "system:serviceaccount:kube-system:job-controller"},
+                            "object": {"apiVersion": "v1", "kind": "Pod",
+                                       "metadata": {"generateName": "job2-", "namespace": "gen-quota2"},
+                                       "spec": {"containers": [{"name": "x", "image": "x",
+                                                                "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}}
+        req = urllib.request.Request(url, data=json.dumps(body).encode(), headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=10, context=ctx if url.startswith("https") else None) as r:
+            return json.loads(r.read())["response"]["allowed"]
+
+    assert [review2(i) for i in range(3)] == [True, False, False]
