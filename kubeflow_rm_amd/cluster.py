@@ -9,6 +9,7 @@ The process is started in its own session; stop() terminates exactly that proces
 from __future__ import annotations
 
 import json
+import secrets
 import os
 import random
 import signal
@@ -33,8 +34,13 @@ def kflite_binary() -> Path:
 class LocalCluster:
     def __init__(self, data_dir: str | None = None, env: dict | None = None, args: list[str] | None = None,
                  controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0,
-                 ca_file: str | None = None, zygote: bool = False):
+                 ca_file: str | None = None, zygote: bool = False, users: list[str] | dict | None = None):
         self._tmp = None
+        # end users with bearer tokens (kflite --token-auth-file): the gateway authenticates them and
+        # sets the userid header from the token (never from the client); ``user_headers(name)``
+        self.users: dict[str, str] = {}
+        for u in (users or []):
+            self.users[u] = (users[u] if isinstance(users, dict) else "") or "tok-" + secrets.token_hex(16)
         self.zygote = zygote  # kubelet --pod-zygote: Python containers fork from a pre-imported interpreter
         if data_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="kflite-")
@@ -51,6 +57,7 @@ class LocalCluster:
         self.url = ""
         self.gateway = ""
         self.kfam = ""
+        self.mesh = ""
         self.client: KubeClient | None = None
 
     def start(self) -> "LocalCluster":
@@ -70,6 +77,11 @@ class LocalCluster:
             # explicit: a kflite built elsewhere (sanitizer builds under build/) cannot derive the
             # package root from its own path, and pod image recipes run `python -m kubeflow_rm_amd...`
             cmd += ["--repo-root", str(ROOT)]
+        if self.users and not any(a.startswith("--token-auth-file") for a in self.args):
+            tf = Path(self.data_dir) / "tokens.json"
+            tf.write_text(json.dumps({t: {"username": u, "groups": ["system:authenticated"]} for u, t in self.users.items()}))
+            os.chmod(tf, 0o600)
+            cmd += ["--token-auth-file", str(tf)]
         if self.zygote and "--pod-zygote" not in self.args:
             cmd += ["--pod-zygote"]
         cmd += self.args
@@ -90,6 +102,7 @@ class LocalCluster:
                     self.url = d["server"]
                     self.gateway = d.get("gateway", "")
                     self.kfam = d.get("kfam", "")
+                    self.mesh = d.get("mesh", "")
                     break
             time.sleep(0.02)
         else:
@@ -133,6 +146,10 @@ class LocalCluster:
         if self._tmp:
             self._tmp.cleanup()
             self._tmp = None
+
+    def user_headers(self, user: str) -> dict:
+        """Request headers that authenticate ``user`` at the gateway (bearer token)."""
+        return {"Authorization": f"Bearer {self.users[user]}"}
 
     def logs(self) -> str:
         try:

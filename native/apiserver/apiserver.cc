@@ -634,6 +634,18 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
   if (res->virtual_only) {
     // SubjectAccessReview & friends: evaluate, never store
     Json& spec = obj["spec"];
+    if (res->kind == "TokenReview") {
+      UserInfo tu;
+      if (authenticate_token(spec["token"].as_string(), tu)) {
+        Json groups = Json::array();
+        for (const auto& g : tu.groups) groups.push_back(g);
+        obj["status"] = Json{{"authenticated", true}, {"user", Json{{"username", tu.username}, {"groups", groups}}}};
+      } else {
+        obj["status"] = Json{{"authenticated", false}, {"error", "invalid bearer token"}};
+      }
+      spec.erase("token");  // never echo a credential back
+      return {};
+    }
     UserInfo u;
     if (res->kind == "SelfSubjectAccessReview") {
       u = o.user;

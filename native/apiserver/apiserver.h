@@ -201,6 +201,13 @@ class ApiServer {
                  const std::string& subresource, const std::string& ns, const std::string& name,
                  std::string* reason = nullptr);
   bool authenticate(const HttpRequest& req, UserInfo& out) const;
+  // A bearer token: the static token file's, or one issued by TokenRequest for a ServiceAccount
+  // that still exists (same uid) and has not expired.
+  bool authenticate_token(const std::string& token, UserInfo& out) const;
+  // TokenRequest (POST serviceaccounts/<name>/token): a random bound token for the ServiceAccount,
+  // valid for expiration_s (clamped to [600 s, 48 h]); false when the ServiceAccount does not exist.
+  ApiError issue_sa_token(const std::string& ns, const std::string& sa, int64_t expiration_s, std::string& token,
+                          double& expires_unix);
   int64_t current_rv() const;
   // Fault injection: "<kind>:<plural|*>:<count>[:<arg>]", kinds: conflict, error, delay, dropwatch.
   std::string inject_fault(const std::string& spec);
@@ -278,6 +285,12 @@ class ApiServer {
   std::condition_variable bg_cv_;
   bool bg_kick_ = false;
   uint32_t next_ip_ = 1;
+  struct SaToken {
+    std::string ns, name, uid;
+    double expires = 0;  // unix seconds
+  };
+  mutable std::mutex tok_mu_;
+  std::map<std::string, SaToken> sa_tokens_;  // issued token -> service account
 };
 
 }  // namespace kf

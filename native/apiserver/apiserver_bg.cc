@@ -394,12 +394,49 @@ void ApiServer::bootstrap_rbac() {
 }
 
 // ---- authentication ---------------------------------------------------------------------------
+bool ApiServer::authenticate_token(const std::string& token, UserInfo& out) const {
+  auto it = cfg_.tokens.find(token);
+  if (it != cfg_.tokens.end()) {
+    out = it->second;
+    return true;
+  }
+  SaToken t;
+  {
+    std::lock_guard<std::mutex> g(tok_mu_);
+    auto st = sa_tokens_.find(token);
+    if (st == sa_tokens_.end()) return false;
+    t = st->second;
+  }
+  if (t.expires < static_cast<double>(now_unix_ms()) / 1000.0) return false;
+  Json sa;
+  // bound to the ServiceAccount object: deleting (or re-creating) it invalidates the token
+  if (!const_cast<ApiServer*>(this)->get("v1", "ServiceAccount", t.ns, t.name, sa).ok() ||
+      sa.str_at({"metadata", "uid"}) != t.uid)
+    return false;
+  out.username = "system:serviceaccount:" + t.ns + ":" + t.name;
+  out.groups = {"system:serviceaccounts", "system:serviceaccounts:" + t.ns, "system:authenticated"};
+  return true;
+}
+
+ApiError ApiServer::issue_sa_token(const std::string& ns, const std::string& sa_name, int64_t expiration_s,
+                                   std::string& token, double& expires_unix) {
+  Json sa;
+  ApiError e = get("v1", "ServiceAccount", ns, sa_name, sa);
+  if (e) return e;
+  expiration_s = std::min<int64_t>(std::max<int64_t>(expiration_s, 600), 48 * 3600);
+  token = "kfsa." + secure_random_hex(24);
+  expires_unix = static_cast<double>(now_unix_ms()) / 1000.0 + static_cast<double>(expiration_s);
+  std::lock_guard<std::mutex> g(tok_mu_);
+  const double now = static_cast<double>(now_unix_ms()) / 1000.0;
+  for (auto it = sa_tokens_.begin(); it != sa_tokens_.end();) it = it->second.expires < now ? sa_tokens_.erase(it) : std::next(it);
+  sa_tokens_[token] = SaToken{ns, sa_name, sa.str_at({"metadata", "uid"}), expires_unix};
+  return {};
+}
+
 bool ApiServer::authenticate(const HttpRequest& req, UserInfo& out) const {
   std::string auth = req.header("Authorization");
   if (starts_with(auth, "Bearer ")) {
-    auto it = cfg_.tokens.find(auth.substr(7));
-    if (it == cfg_.tokens.end()) return false;
-    out = it->second;
+    if (!authenticate_token(auth.substr(7), out)) return false;
   } else if (!cfg_.tokens.empty() && cfg_.authz_rbac) {
     out = UserInfo{"system:anonymous", {"system:unauthenticated"}};
   } else {

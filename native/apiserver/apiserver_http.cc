@@ -315,6 +315,32 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
     resp.text(200, out);
     return;
   }
+  if (res->group.empty() && plural == "serviceaccounts" && sub == "token") {
+    // TokenRequest (authentication.k8s.io/v1): a bound token for the ServiceAccount; authorized
+    // above as "create serviceaccounts/token"
+    if (req.method != "POST") {
+      resp.json(405, ApiError{405, "MethodNotAllowed", "TokenRequest takes POST"}.status_json().dump());
+      return;
+    }
+    Json body;
+    if (!req.body.empty() && !Json::try_parse(req.body, body)) {
+      resp.json(400, ApiError::BadRequest("invalid TokenRequest body").status_json().dump());
+      return;
+    }
+    std::string token;
+    double exp = 0;
+    if (ApiError e = issue_sa_token(ns, name, body.at_path({"spec", "expirationSeconds"}).as_int(3600), token, exp)) {
+      send_error(resp, e, "ServiceAccount", name);
+      return;
+    }
+    Json spec = body["spec"].is_object() ? body["spec"] : Json::object();
+    resp.json(201, Json{{"apiVersion", "authentication.k8s.io/v1"}, {"kind", "TokenRequest"},
+                        {"metadata", Json{{"name", name}, {"namespace", ns}}}, {"spec", spec},
+                        {"status", Json{{"token", token},
+                                        {"expirationTimestamp", rfc3339_from_ms(static_cast<int64_t>(exp * 1000))}}}}
+                       .dump());
+    return;
+  }
   if (res->group.empty() && plural == "pods" && sub == "exec") {
     // kubectl exec without a TTY or stdin: ?command=a&command=b[&container=c][&timeoutSeconds=n];
     // reply {"exitCode": n, "output": "<stdout+stderr>"} (authorized above as create pods/exec)

@@ -31,6 +31,9 @@ struct ComponentFlags {
   std::string gateway_addr = "127.0.0.1";
   int64_t gateway_port = 0;
   std::string gateway_name = "kubeflow/kubeflow-gateway";
+  bool gateway_authz = true;                  // enforce AuthorizationPolicies at the gateway
+  std::string gateway_trusted_proxy_secret_file;  // authn proxy in front of the ingress (see GatewayOptions)
+  int64_t mesh_port = 0;                      // in-cluster (mesh) listener: -1 off, 0 ephemeral
   // KFAM
   int64_t kfam_port = -1;  // -1 = disabled unless "kfam" is enabled (then ephemeral)
   std::string userid_header = "kubeflow-userid";
@@ -62,6 +65,7 @@ class Components {
   void start();
   void stop();
   int gateway_port() const;
+  int mesh_port() const;
   int kfam_port() const;
   int webhook_port() const;
 

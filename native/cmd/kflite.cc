@@ -131,6 +131,7 @@ int main(int argc, char** argv) {
   if (!data_dir.empty())
     write_file(data_dir + "/kflite.json", Json{{"server", url}, {"pid", static_cast<int64_t>(::getpid())},
                                                {"gateway", comps.gateway_port() ? "http://" + cf.gateway_addr + ":" + std::to_string(comps.gateway_port()) : ""},
+                                               {"mesh", comps.mesh_port() ? "http://" + cf.gateway_addr + ":" + std::to_string(comps.mesh_port()) : ""},
                                                {"kfam", comps.kfam_port() ? "http://127.0.0.1:" + std::to_string(comps.kfam_port()) : ""}}
                                                   .dump() + "\n");
   std::printf("kflite: controllers running: %s\n", join(std::vector<std::string>(enabled.begin(), enabled.end()), ",").c_str());

@@ -33,6 +33,12 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
   f.add_int("gateway-port", &gateway_port, 0, "ingress gateway port (0 = ephemeral)");
   f.add_string("gateway-name", &gateway_name, "kubeflow/kubeflow-gateway", "VirtualService gateway served by the ingress");
+  f.add_bool("gateway-authz", &gateway_authz, true,
+             "enforce Istio AuthorizationPolicies (ALLOW/DENY) on the ingress and mesh listeners");
+  f.add_string("gateway-trusted-proxy-secret-file", &gateway_trusted_proxy_secret_file, "",
+               "secret an authenticating proxy in front of the ingress presents (X-Kfamd-Auth-Proxy-Secret) "
+               "to assert the userid header");
+  f.add_int("mesh-port", &mesh_port, 0, "in-cluster mesh listener port (-1 = off, 0 = ephemeral)");
   f.add_int("kfam-port", &kfam_port, -1, "KFAM port (-1 = ephemeral when kfam is enabled)");
   f.add_string("userid-header", &userid_header, "kubeflow-userid", "user id header (KFAM / profile controller)");
   f.add_string("userid-prefix", &userid_prefix, "", "user id prefix (KFAM / profile controller)");
@@ -93,7 +99,38 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.notebook->setup(mgr, workers);
   }
   if (enabled.count("culler") && getenv_or("ENABLE_CULLING", "false") == "true") {
-    I.culler = std::make_unique<CullingReconciler>(I.c, CullingOptions::from_env(), I.nb_metrics);
+    CullingOptions co = CullingOptions::from_env();
+    if (enabled.count("gateway") && I.api && I.f.mesh_port >= 0 && co.mesh_url.empty()) {
+      // in-process: the kernels GETs go through this node's mesh listener as the notebook
+      // controller's ServiceAccount (NOTEBOOK_CONTROLLER_PRINCIPAL, profile_controller.go:420-422)
+      Impl* ip = &I;
+      co.mesh_url_fn = [ip]() -> std::string {
+        return ip->gateway && ip->gateway->mesh_port() ? "http://127.0.0.1:" + std::to_string(ip->gateway->mesh_port()) : "";
+      };
+      const std::string principal = getenv_or("NOTEBOOK_CONTROLLER_PRINCIPAL",
+                                              "cluster.local/ns/kubeflow/sa/notebook-controller-service-account");
+      auto parts = split(principal, '/', false);  // <domain>/ns/<ns>/sa/<name>
+      const std::string sa_ns = parts.size() == 5 ? parts[2] : "kubeflow";
+      const std::string sa = parts.size() == 5 ? parts[4] : "notebook-controller-service-account";
+      auto cache = std::make_shared<std::pair<std::string, double>>();
+      auto mu = std::make_shared<std::mutex>();
+      co.peer_token_fn = [ip, sa_ns, sa, cache, mu]() -> std::string {
+        std::lock_guard<std::mutex> g(*mu);
+        const double now = static_cast<double>(now_unix_ms()) / 1000.0;
+        if (!cache->first.empty() && cache->second - 60 > now) return cache->first;
+        WriteOptions sys;
+        Json nsobj{{"apiVersion", "v1"}, {"kind", "Namespace"}, {"metadata", Json{{"name", sa_ns}}}};
+        ip->api->create(nsobj, sys);  // exists: 409, fine
+        Json saobj{{"apiVersion", "v1"}, {"kind", "ServiceAccount"}, {"metadata", Json{{"name", sa}, {"namespace", sa_ns}}}};
+        ip->api->create(saobj, sys);
+        std::string tok;
+        double exp = 0;
+        if (ip->api->issue_sa_token(sa_ns, sa, 3600, tok, exp)) return "";
+        *cache = {tok, exp};
+        return tok;
+      };
+    }
+    I.culler = std::make_unique<CullingReconciler>(I.c, co, I.nb_metrics);
     I.culler->setup(mgr);
   }
   if (enabled.count("profile")) {
@@ -227,7 +264,22 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     I.stoppers.push_back([&I] { I.kubelet->stop(); });
   }
   if (enabled.count("gateway")) {
-    I.gateway = std::make_unique<Gateway>(I.c, I.f.gateway_name);
+    GatewayOptions go;
+    go.gateway_name = I.f.gateway_name;
+    go.userid_header = I.f.userid_header;
+    go.userid_prefix = I.f.userid_prefix;
+    go.ingress_principal = getenv_or("ISTIO_INGRESS_GATEWAY_PRINCIPAL", go.ingress_principal);
+    go.cluster_domain = getenv_or("CLUSTER_DOMAIN", go.cluster_domain);
+    go.enforce = I.f.gateway_authz;
+    go.mesh_port = static_cast<int>(I.f.mesh_port);
+    if (!I.f.gateway_trusted_proxy_secret_file.empty()) {
+      if (!read_file(I.f.gateway_trusted_proxy_secret_file, go.trusted_proxy_secret)) {
+        *err = "cannot read " + I.f.gateway_trusted_proxy_secret_file;
+        return false;
+      }
+      go.trusted_proxy_secret = trim(go.trusted_proxy_secret);
+    }
+    I.gateway = std::make_unique<Gateway>(I.c, go);
     I.gateway->setup(mgr);
     if (!I.gateway->start(I.f.gateway_addr, static_cast<int>(I.f.gateway_port), err)) return false;
     I.stoppers.push_back([&I] { I.gateway->stop(); });
@@ -290,6 +342,7 @@ void Components::stop() {
 }
 
 int Components::gateway_port() const { return impl_->gateway ? impl_->gateway->port() : 0; }
+int Components::mesh_port() const { return impl_->gateway ? impl_->gateway->mesh_port() : 0; }
 int Components::kfam_port() const { return impl_->kfam ? impl_->kfam->port() : 0; }
 int Components::webhook_port() const { return impl_->webhooks ? impl_->webhooks->port() : 0; }
 

@@ -25,6 +25,8 @@ CullingOptions CullingOptions::from_env() {
   o.dev = getenv_or("DEV", "false") != "false";
   o.proxy_url = getenv_or("KUBE_PROXY_URL", "http://localhost:8001");
   o.cluster_domain = getenv_or("CLUSTER_DOMAIN", "cluster.local");
+  o.mesh_url = getenv_or("MESH_URL", "");
+  o.mesh_token_file = getenv_or("MESH_TOKEN_FILE", "/var/run/secrets/kubernetes.io/serviceaccount/token");
   const std::string ps = getenv_or("IDLENESS_CHECK_PERIOD_SECONDS", "");
   if (!ps.empty()) o.period_seconds_override = std::atof(ps.c_str());
   return o;
@@ -116,7 +118,17 @@ bool CullingReconciler::fetch(const std::string& nm, const std::string& ns, cons
   if (o_.dev)
     url = o_.proxy_url + "/api/v1/namespaces/" + ns + "/services/" + nm + ":http-" + nm + "/proxy/notebook/" + ns + "/" + nm +
           "/api/" + what;
-  HttpResult r = http_request("GET", url, "", {}, 10000);
+  Headers h;
+  const std::string mesh = o_.mesh_url_fn ? o_.mesh_url_fn() : o_.mesh_url;
+  if (!o_.dev && !mesh.empty()) {
+    h["Host"] = nm + "." + ns + ".svc." + o_.cluster_domain;
+    std::string token;
+    if (o_.peer_token_fn) token = o_.peer_token_fn();
+    else if (read_file(o_.mesh_token_file, token)) token = trim(token);
+    if (!token.empty()) h["X-Kfamd-Peer-Token"] = token;
+    url = mesh + "/notebook/" + ns + "/" + nm + "/api/" + what;
+  }
+  HttpResult r = http_request("GET", url, "", h, 10000);
   if (r.status != 200) {
     KF_INFO("culler", "Warning: GET to " + url + ": " + (r.status ? std::to_string(r.status) : r.error));
     return false;

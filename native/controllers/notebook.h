@@ -2,6 +2,7 @@
 // components/notebook-controller/controllers/{notebook_controller.go,culling_controller.go}).
 #pragma once
 
+#include <functional>
 #include <map>
 #include <mutex>
 
@@ -66,6 +67,14 @@ struct CullingOptions {
   std::string proxy_url = "http://localhost:8001";  // KUBE_PROXY_URL (DEV mode)
   std::string cluster_domain = "cluster.local";
   double period_seconds_override = -1;  // tests: sub-minute periods
+  // Through the mesh (the gateway's in-cluster listener, node/node.h): the kernels GET goes to
+  // mesh_url with Host <nb>.<ns>.svc.<domain> and the culler's ServiceAccount token, so the
+  // profile's ns-owner-access-istio policy admits it as the notebook-controller principal
+  // (profile_controller.go:419-556, the "*/api/kernels" rule). MESH_URL / MESH_TOKEN_FILE in split
+  // mode; kflite wires both in-process.
+  std::string mesh_url;
+  std::string mesh_token_file;
+  std::function<std::string()> mesh_url_fn, peer_token_fn;
   static CullingOptions from_env();
   double period_seconds() const { return period_seconds_override > 0 ? period_seconds_override : check_period_minutes * 60.0; }
 };

@@ -342,7 +342,7 @@ Json odh_oauth_service(const Json& nb) {
 Json odh_oauth_secret(const Json& nb) {
   // cookie secret: base64(base64(16 random bytes)) like NewNotebookOAuthSecret
   std::string seed;
-  const std::string hex = random_hex(16);
+  const std::string hex = secure_random_hex(16);
   for (size_t i = 0; i + 1 < hex.size(); i += 2) seed += static_cast<char>(std::stoi(hex.substr(i, 2), nullptr, 16));
   return Json{{"apiVersion", "v1"},
               {"kind", "Secret"},

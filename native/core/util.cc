@@ -1,4 +1,6 @@
 // util.cc — see util.h.
+#include <sys/random.h>
+#include <cerrno>
 #include <pthread.h>
 #include "core/util.h"
 
@@ -167,6 +169,26 @@ std::string random_hex(size_t nbytes) {
   std::string out;
   for (size_t i = 0; i < nbytes; ++i) {
     unsigned v = static_cast<unsigned>(rng()() & 0xFF);
+    out += hex[v >> 4];
+    out += hex[v & 15];
+  }
+  return out;
+}
+
+std::string secure_random_hex(size_t nbytes) {
+  static const char* hex = "0123456789abcdef";
+  std::string raw(nbytes, '\0');
+  size_t got = 0;
+  while (got < nbytes) {
+    const ssize_t n = ::getrandom(raw.data() + got, nbytes - got, 0);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      std::abort();  // no entropy source: never hand out a predictable credential
+    }
+    got += static_cast<size_t>(n);
+  }
+  std::string out;
+  for (unsigned char v : raw) {
     out += hex[v >> 4];
     out += hex[v & 15];
   }

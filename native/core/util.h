@@ -30,6 +30,8 @@ std::string url_encode(const std::string& s);
 std::string base64_encode(const std::string& in);
 std::string base64_decode(const std::string& in);
 std::string random_hex(size_t nbytes);
+// credentials (tokens, cookie secrets): getrandom(2), never the PRNG behind random_hex
+std::string secure_random_hex(size_t nbytes);
 std::string random_alnum(size_t n);
 std::string uuid4();
 // Kubernetes resource quantities ("500m", "1Gi", "2", "1e3") -> value in base units

@@ -1,19 +1,46 @@
-// gateway.cc — Istio-ingress-equivalent HTTP gateway (see node.h).
+// gateway.cc — Istio-ingress-equivalent HTTP gateway and policy enforcement point (see node.h).
 #include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
 
 #include "core/util.h"
+#include "node/authz.h"
 #include "node/node.h"
 
 namespace kf {
 
-Gateway::Gateway(std::shared_ptr<Client> c, std::string gateway_name)
+namespace {
+constexpr const char* kPeerTokenHeader = "X-Kfamd-Peer-Token";
+constexpr const char* kProxySecretHeader = "X-Kfamd-Auth-Proxy-Secret";
+
+// "<svc>.<ns>.svc[.<domain>]" (or "<svc>.<ns>") -> (svc, ns); false for anything else
+bool split_service_host(const std::string& host_port, std::string& svc, std::string& ns) {
+  const std::string host = host_port.substr(0, host_port.find(':'));
+  auto parts = split(host, '.', true);
+  if (parts.size() < 2) return false;
+  if (parts.size() > 2 && parts[2] != "svc") return false;
+  svc = parts[0];
+  ns = parts[1];
+  return true;
+}
+
+std::string cookie_value(const std::string& cookies, const std::string& name) {
+  for (const auto& c : split(cookies, ';', true)) {
+    const std::string kv = trim(c);
+    if (starts_with(kv, name + "=")) return kv.substr(name.size() + 1);
+  }
+  return "";
+}
+}  // namespace
+
+Gateway::Gateway(std::shared_ptr<Client> c, GatewayOptions o)
     : c_(std::move(c)),
-      gw_(std::move(gateway_name)),
+      o_(std::move(o)),
       upgrades_(Registry::global().counter("gateway_upgraded_connections_total", "connections tunnelled after an HTTP Upgrade (WebSocket)")),
-      streams_(Registry::global().counter("gateway_streamed_responses_total", "responses relayed incrementally (chunked / unframed / large)")) {
+      streams_(Registry::global().counter("gateway_streamed_responses_total", "responses relayed incrementally (chunked / unframed / large)")),
+      decisions_(Registry::global().counter("gateway_authz_decisions_total",
+                                            "AuthorizationPolicy decisions by listener and result", {"listener", "result"})) {
   const char* d = std::getenv("KFAMD_ROUTE_DOMAIN");
   route_domain_ = d && *d ? d : "apps.kube-lite";
 }
@@ -22,6 +49,8 @@ Gateway::~Gateway() { stop(); }
 void Gateway::setup(Manager& mgr) {
   vs_ = &mgr.informer("networking.istio.io/v1alpha3", "VirtualService");
   routes_ = &mgr.informer("route.openshift.io/v1", "Route");
+  policies_ = &mgr.informer("security.istio.io/v1beta1", "AuthorizationPolicy");
+  services_ = &mgr.informer("v1", "Service");
 }
 
 bool Gateway::start(const std::string& addr, int port, std::string* err) {
@@ -29,11 +58,65 @@ bool Gateway::start(const std::string& addr, int port, std::string* err) {
   if (!srv_->listen(addr, port, err)) return false;
   srv_->set_handler([this](HttpRequest& req, HttpResponse& resp) { handle(req, resp); });
   srv_->start();
+  if (o_.mesh_port >= 0) {
+    mesh_ = std::make_unique<HttpServer>();
+    if (!mesh_->listen(addr, o_.mesh_port, err)) return false;
+    mesh_->set_handler([this](HttpRequest& req, HttpResponse& resp) { handle_mesh(req, resp); });
+    mesh_->start();
+  }
   return true;
 }
 
 void Gateway::stop() {
   if (srv_) srv_->stop();
+  if (mesh_) mesh_->stop();
+}
+
+Gateway::Identity Gateway::review_token(const std::string& token) {
+  Identity id;
+  if (token.empty()) return id;
+  const double now = now_seconds();
+  {
+    std::lock_guard<std::mutex> g(tok_mu_);
+    auto it = tok_cache_.find(token);
+    if (it != tok_cache_.end() && it->second.second > now) return it->second.first;
+  }
+  Json tr{{"apiVersion", "authentication.k8s.io/v1"}, {"kind", "TokenReview"}, {"spec", Json{{"token", token}}}};
+  const bool ok = !c_->create(tr);
+  if (ok && tr.at_path({"status", "authenticated"}).as_bool()) {
+    id.authenticated = true;
+    id.username = tr.at_path({"status", "user", "username"}).as_string();
+    for (const auto& g : tr.at_path({"status", "user", "groups"}).as_array()) id.groups.push_back(g.as_string());
+  }
+  std::lock_guard<std::mutex> g(tok_mu_);
+  if (tok_cache_.size() > 4096) tok_cache_.clear();
+  // an API server error is not cached: the next request asks again
+  if (ok) tok_cache_[token] = {id, now + (id.authenticated ? 10.0 : 2.0)};
+  return id;
+}
+
+bool Gateway::authorize(const std::string& dest_host, int dest_port, const HttpRequest& req, const std::string& path,
+                        const Headers& fwd, const std::string& principal, const std::string& source_ns, std::string* why) {
+  if (!o_.enforce || !policies_) return true;
+  std::string svc, ns;
+  if (!split_service_host(dest_host, svc, ns)) return true;  // not a Service destination
+  std::map<std::string, std::string> labels;  // the workload's labels: the Service's selector
+  Json s;
+  if (services_ && services_->get(ns, svc, s))
+    for (const auto& kv : s.at_path({"spec", "selector"}).as_object()) labels[kv.first] = kv.second.as_string();
+  AuthzRequest ar;
+  ar.principal = principal;
+  ar.source_namespace = source_ns;
+  ar.remote_ip = req.remote_addr.substr(0, req.remote_addr.rfind(':'));
+  ar.source_ip = ar.remote_ip;
+  ar.method = req.method;
+  ar.path = path;
+  ar.host = req.header("Host");
+  ar.port = dest_port;
+  for (const auto& kv : fwd) ar.headers[to_lower(kv.first)] = kv.second;
+  AuthzDecision d = evaluate_authz(policies_->list(), ar, ns, labels, o_.root_namespace);
+  if (!d.allowed && why) *why = d.reason + (d.policy.empty() ? "" : " (" + d.policy + ")");
+  return d.allowed;
 }
 
 bool Gateway::match(const std::vector<Json>& vss, const std::string& gateway, const std::string& host,
@@ -94,7 +177,8 @@ bool Gateway::match(const std::vector<Json>& vss, const std::string& gateway, co
 void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   const std::string host = req.header("Host");
   Route rt;
-  bool ok = vs_ && match(vs_->list(), gw_, host, req.path, rt);
+  bool ok = vs_ && match(vs_->list(), o_.gateway_name, host, req.path, rt);
+  bool routed_by_route = false;  // OpenShift Routes bypass the mesh (the ODH OAuth proxy guards them)
   std::string target_path;
   if (ok) {
     std::string rest = req.path.size() >= rt.prefix.size() ? req.path.substr(rt.prefix.size()) : "";
@@ -117,7 +201,7 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
             if (p["name"].as_string() == tp.as_string() || p["targetPort"] == tp) rt.dest_port = static_cast<int>(p["port"].as_int());
       }
       target_path = req.path;
-      ok = true;
+      ok = routed_by_route = true;
       break;
     }
   }
@@ -127,18 +211,86 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   }
   std::string url = "http://" + rt.dest_host + ":" + std::to_string(rt.dest_port) + target_path +
                     (req.raw_query.empty() ? "" : "?" + req.raw_query);
-  const bool upgrade = contains(to_lower(req.header("Connection")), "upgrade") && !req.header("Upgrade").empty();
+  // authentication: a trusted authn proxy's assertion, else a bearer token / session cookie
+  // (TokenReview); client-supplied identity headers never pass otherwise
+  const std::string uid_lc = to_lower(o_.userid_header);
+  const bool trusted_proxy = !o_.trusted_proxy_secret.empty() && req.header(kProxySecretHeader) == o_.trusted_proxy_secret;
+  Identity who;
+  if (!trusted_proxy) {
+    const std::string auth = req.header("Authorization");
+    std::string token = starts_with(auth, "Bearer ") ? trim(auth.substr(7)) : "";
+    if (token.empty()) token = cookie_value(req.header("Cookie"), o_.auth_cookie);
+    who = review_token(token);
+  }
   Headers h;
   for (const auto& kv : req.headers) {
     std::string k = to_lower(kv.first);
-    if (k == "content-length" || k == "transfer-encoding") continue;
-    if (k == "connection" && !upgrade) continue;
+    if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
+    if (k == to_lower(kPeerTokenHeader) || k == to_lower(kProxySecretHeader)) continue;
+    if (!trusted_proxy && (k == uid_lc || k == "kubeflow-groups")) continue;  // spoofed identity
     h[kv.first] = kv.second;
   }
+  if (who.authenticated && !who.service_account()) h[o_.userid_header] = o_.userid_prefix + who.username;
   for (const auto& m : rt.headers.as_object()) h[m.first] = m.second.as_string();
   h["X-Forwarded-Prefix"] = rt.prefix;
   h["X-Envoy-Original-Path"] = req.path;
-  const int timeout_ms = static_cast<int>(rt.timeout_s * 1000);
+  // authorization at the destination workload (what its Istio sidecar does in the reference): the
+  // request arrives from the ingress gateway's principal, with the path after the rewrite
+  std::string why;
+  if (!routed_by_route && !authorize(rt.dest_host, rt.dest_port, req, target_path, h, o_.ingress_principal,
+                                     o_.ingress_namespace, &why)) {
+    decisions_->inc({"ingress", "deny"});
+    resp.headers["X-Kfamd-Authz"] = why;
+    resp.text(403, "RBAC: access denied");
+    return;
+  }
+  if (!routed_by_route && o_.enforce) decisions_->inc({"ingress", "allow"});
+  forward(req, resp, url, std::move(h), static_cast<int>(rt.timeout_s * 1000));
+}
+
+void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
+  std::string svc, ns;
+  const std::string host = req.header("Host");
+  if (!split_service_host(host, svc, ns)) {
+    resp.text(404, "mesh: Host must name a Service (<svc>.<ns>.svc[.<domain>]), got " + host + "\n");
+    return;
+  }
+  // the caller's workload identity (Istio: the peer's mTLS certificate; here its ServiceAccount
+  // token); a caller without one is plaintext: no principal, no source namespace
+  Identity peer = review_token(req.header(kPeerTokenHeader));
+  std::string principal, source_ns;
+  if (peer.authenticated && peer.service_account()) {
+    auto parts = split(peer.username, ':', false);  // system:serviceaccount:<ns>:<name>
+    if (parts.size() == 4) {
+      source_ns = parts[2];
+      principal = o_.cluster_domain + "/ns/" + parts[2] + "/sa/" + parts[3];
+    }
+  }
+  Headers h;
+  for (const auto& kv : req.headers) {
+    std::string k = to_lower(kv.first);
+    if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
+    if (k == to_lower(kPeerTokenHeader)) continue;
+    h[kv.first] = kv.second;
+  }
+  const size_t colon = host.find(':');
+  const int port = colon == std::string::npos ? 80 : std::atoi(host.c_str() + colon + 1);
+  std::string why;
+  if (!authorize(host.substr(0, colon), port, req, req.path, h, principal, source_ns, &why)) {
+    decisions_->inc({"mesh", "deny"});
+    resp.headers["X-Kfamd-Authz"] = why;
+    resp.text(403, "RBAC: access denied");
+    return;
+  }
+  if (o_.enforce) decisions_->inc({"mesh", "allow"});
+  const std::string url = "http://" + svc + "." + ns + ".svc." + o_.cluster_domain + ":" + std::to_string(port) + req.path +
+                          (req.raw_query.empty() ? "" : "?" + req.raw_query);
+  forward(req, resp, url, std::move(h), 300000);
+}
+
+void Gateway::forward(HttpRequest& req, HttpResponse& resp, const std::string& url, Headers h, int timeout_ms) {
+  const bool upgrade = contains(to_lower(req.header("Connection")), "upgrade") && !req.header("Upgrade").empty();
+  if (upgrade) h["Connection"] = req.header("Connection");
   // Istio's default retry policy: 2 retries on connect-failure / refused-stream (a pod that is
   // Ready without a readiness probe may not be listening yet)
   auto with_retries = [](auto attempt) {

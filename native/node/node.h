@@ -18,7 +18,11 @@
 //              graceful termination, termination messages, container logs, and full pod status with
 //              millisecond timestamps (the cold-start phase breakdown of SURVEY §5.1).
 //   Gateway    HTTP reverse proxy that serves Istio VirtualServices (uri prefix match, rewrite,
-//              headers.request.set, timeout) and OpenShift Routes for the embedded cluster.
+//              headers.request.set, timeout) and OpenShift Routes for the embedded cluster, and the
+//              policy enforcement point Istio is in the reference: end-user authentication (bearer
+//              token / session cookie via TokenReview, or a trusted authn proxy), the userid header set
+//              only from that identity, and AuthorizationPolicy ALLOW/DENY evaluation (node/authz.h) on
+//              the ingress listener and on an in-cluster mesh listener (ServiceAccount principals).
 #pragma once
 
 #include <atomic>
@@ -159,15 +163,39 @@ class Kubelet {
   bool spawn_zygote(Zygote& z);
 };
 
+struct GatewayOptions {
+  std::string gateway_name = "kubeflow/kubeflow-gateway";  // VirtualService gateway served by the ingress
+  // identity: the header the ingress sets from the authenticated user (profile / KFAM policies and
+  // the web apps read it), minus nothing, plus userid_prefix
+  std::string userid_header = "kubeflow-userid";
+  std::string userid_prefix;
+  // the principals the profile's ns-owner-access-istio policy names
+  std::string ingress_principal = "cluster.local/ns/istio-system/sa/istio-ingressgateway-service-account";
+  std::string ingress_namespace = "istio-system";
+  std::string root_namespace = "istio-system";  // mesh-wide AuthorizationPolicies live here
+  std::string cluster_domain = "cluster.local";
+  // an authenticating proxy in front of the ingress (oauth2-proxy / dex) may assert the userid header
+  // when it presents this secret in X-Kfamd-Auth-Proxy-Secret (empty = no trusted proxy)
+  std::string trusted_proxy_secret;
+  std::string auth_cookie = "kfamd-token";  // browser sessions: the bearer token as a cookie
+  bool enforce = true;                      // evaluate AuthorizationPolicies (ALLOW/DENY)
+  int mesh_port = -1;                       // in-cluster listener (-1 = off, 0 = ephemeral)
+};
+
 class Gateway {
  public:
-  Gateway(std::shared_ptr<Client> c, std::string gateway_name);
+  Gateway(std::shared_ptr<Client> c, GatewayOptions o);
   ~Gateway();
   void setup(Manager& mgr);
   bool start(const std::string& addr, int port, std::string* err);
   void stop();
   int port() const { return srv_ ? srv_->port() : 0; }
+  int mesh_port() const { return mesh_ ? mesh_->port() : 0; }
+  // ingress: VirtualService / Route match, end-user authentication, policy check, proxy
   void handle(HttpRequest& req, HttpResponse& resp);
+  // mesh (the destination sidecars' job, done node-wide like Istio ambient's ztunnel): Host names a
+  // Service, the caller's identity is its ServiceAccount token in X-Kfamd-Peer-Token
+  void handle_mesh(HttpRequest& req, HttpResponse& resp);
 
   struct Route {
     std::string prefix, rewrite, dest_host;
@@ -180,16 +208,34 @@ class Gateway {
   static bool match(const std::vector<Json>& vss, const std::string& gateway, const std::string& host,
                     const std::string& path, Route& out);
 
+  struct Identity {
+    bool authenticated = false;
+    std::string username;
+    std::vector<std::string> groups;
+    bool service_account() const { return starts_with_sa(username); }
+    static bool starts_with_sa(const std::string& u) { return u.rfind("system:serviceaccount:", 0) == 0; }
+  };
+  // TokenReview through the API server, cached (positive 10 s, negative 2 s)
+  Identity review_token(const std::string& token);
+
  private:
+  bool authorize(const std::string& dest_host, int dest_port, const HttpRequest& req, const std::string& path,
+                 const Headers& fwd, const std::string& principal, const std::string& source_ns, std::string* why);
+  void forward(HttpRequest& req, HttpResponse& resp, const std::string& url, Headers h, int timeout_ms);
+
   std::shared_ptr<Client> c_;
-  std::string gw_;
+  GatewayOptions o_;
   Informer* vs_ = nullptr;
   Informer* routes_ = nullptr;
-  std::unique_ptr<HttpServer> srv_;
-  std::shared_ptr<CounterVec> upgrades_, streams_;
+  Informer* policies_ = nullptr;
+  Informer* services_ = nullptr;
+  std::unique_ptr<HttpServer> srv_, mesh_;
+  std::shared_ptr<CounterVec> upgrades_, streams_, decisions_;
   // host an OpenShift router gives a Route without spec.host: <name>-<namespace>.<domain>
   // (KFAMD_ROUTE_DOMAIN, default apps.kube-lite)
   std::string route_domain_;
+  std::mutex tok_mu_;
+  std::map<std::string, std::pair<Identity, double>> tok_cache_;  // token -> (identity, expiry)
 };
 
 }  // namespace kf

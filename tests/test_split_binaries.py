@@ -32,7 +32,7 @@ def _free_port():
 def split():
     from tests.conftest import _ensure_native
     _ensure_native()
-    cl = LocalCluster(controllers="builtin,scheduler,kubelet,gateway", env={"USE_ISTIO": "true"})
+    cl = LocalCluster(controllers="builtin,scheduler,kubelet,gateway", env={"USE_ISTIO": "true"}, users=["r@example.com"])
     cl.start()
     kfam_port = _free_port()
     procs = []
@@ -99,7 +99,8 @@ def test_profile_notebook_poddefault_over_rest(split):
     deadline = time.time() + 15
     while True:
         try:
-            with urllib.request.urlopen(cl.gateway + "/notebook/remote/nb/api/status", timeout=5) as r:
+            req = urllib.request.Request(cl.gateway + "/notebook/remote/nb/api/status", headers=cl.user_headers("r@example.com"))
+            with urllib.request.urlopen(req, timeout=5) as r:
                 assert r.status == 200
                 break
         except urllib.error.HTTPError as e:
