@@ -126,7 +126,14 @@ def main(argv: list[str] | None = None) -> int:
     c.add_argument("--out", default=str(Path(__file__).resolve().parent.parent / "manifests" / "crds"))
     u = sub.add_parser("up")
     u.add_argument("--data-dir", default=None)
-    args = ap.parse_args(argv)
+    argv = sys.argv[1:] if argv is None else list(argv)
+    if argv and argv[0] in kubectl.INTERMIXED:
+        # kubectl takes flags between positionals (`create secret tls -n NS NAME --cert=...`);
+        # argparse only allows that per sub-parser, via parse_intermixed_args
+        args = sub.choices[argv[0]].parse_intermixed_args(argv[1:])
+        args.cmd = argv[0]
+    else:
+        args = ap.parse_args(argv)
     if args.cmd == "build":
         sys.stdout.write(kustomize.dump(kustomize.build(args.path)))
         return 0

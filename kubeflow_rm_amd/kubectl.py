@@ -7,6 +7,7 @@
     kfctl rollout status [--watch] statefulset|deployment <name> [--timeout=300s] [-n NS]
     kfctl logs <pod> [-c CONTAINER] [-n NS] [--tail N] [-f]
     kfctl apply -f FILE|-     kfctl delete -f FILE|- | <resource> <name>
+    kfctl create / patch / annotate / label / scale          (kubectl_mutate.py)
 
 What the reference's own acceptance flow runs (``.github/workflows/odh_notebook_controller_integration_test.yaml:275-289``,
 ``notebook_controller_integration_test.yaml:106``) and what its load test drives
@@ -743,6 +744,8 @@ def add_parsers(sub) -> None:
     t.add_argument("--metrics-url", default=None,
                    help="the node agent's /metrics when it runs apart from the API server (kfamd-node)")
     common(t, selector=False)
+    from . import kubectl_mutate
+    kubectl_mutate.add_parsers(sub, common)
 
 
 VERBS = {"get": cmd_get, "describe": cmd_describe, "wait": cmd_wait, "rollout": cmd_rollout, "logs": cmd_logs,
@@ -786,3 +789,13 @@ def run(verb: str, args, client: KubeClient | None = None) -> int:
     except ApiException as e:
         sys.stderr.write(f"Error from server ({e.reason or e.status}): {e.message}\n")
         return 1
+    except OSError as e:  # -f / --cert / --from-file paths, as kubectl words it
+        sys.stderr.write(f"error: open {e.filename}: {(e.strerror or str(e)).lower()}\n")
+        return 1
+
+
+from . import kubectl_mutate as _mutate  # noqa: E402 - the writing verbs build on the helpers above
+
+VERBS.update(_mutate.VERBS)
+# verbs whose flags may sit between positionals (exec keeps argparse's plain form: its command follows `--`)
+INTERMIXED = frozenset(v for v in VERBS if v != "exec")

@@ -637,7 +637,9 @@ void add_ptr(Json& root, const std::vector<std::string>& toks, Json value, bool 
       arr.insert(arr.begin() + static_cast<long>(idx), std::move(value));
     }
   } else if (parent->is_object()) {
-    if (replace && !parent->has(last)) throw JsonError("json patch: replace of missing key " + last);
+    // kube-apiserver's json-patch (evanphx/json-patch v4) lets `replace` create a missing object
+    // member; the reference CI relies on it to set the webhook's absent caBundle
+    // (odh_notebook_controller_integration_test.yaml:207-212). Array indices stay strict.
     (*parent)[last] = std::move(value);
   } else {
     throw JsonError("json patch: parent is not a container");
