@@ -19,7 +19,12 @@ Protocol (one AF_UNIX stream connection per container start, JSON lines):
 The connection stays open for the life of the container: it is how the kubelet (which is not the
 process's parent) learns the exit status. The kubelet kills the process group (the child calls
 setsid). Safety: the zygote refuses to serve if its preload opened the GPU driver (/dev/kfd): a
-fork of a process with a live HIP context is undefined.
+fork of a process with a live HIP context is undefined. It also refuses if the preload left any
+native thread besides the main one: fork() copies only the calling thread, so a lock another thread
+held at that moment (malloc arenas, a BLAS server queue, the HIP runtime) would stay locked forever in
+every container. ``import numpy`` alone starts one OpenBLAS worker per CPU, so the zygote imports
+with the BLAS / OpenMP pools pinned to one thread and each container sizes its pools afterwards
+(OpenBLAS grows its pool on demand, OpenMP spawns on the first parallel region).
 
 Reference: the reference has no process runtime (L0 is Kubernetes); the cold-start path it
 exercises is notebook_controller.go Reconcile -> StatefulSet -> kubelet -> image ENTRYPOINT
@@ -65,21 +70,51 @@ def _set_pdeathsig() -> None:
         pass
 
 
-def _size_thread_pools(env: dict) -> None:
-    """The OpenMP runtime read OMP_NUM_THREADS and the CPU mask when the zygote loaded it, so a
-    forked container would inherit the zygote's thread count (every node CPU) instead of what a
-    fresh process pinned to its NUMA-local CPUs gets. Apply the container's own setting."""
-    torch = sys.modules.get("torch")
-    if torch is None:
-        return
-    n = 0
+# read at library load by OpenBLAS / OpenMP / MKL: the zygote imports with one-thread pools
+_POOL_ENV = ("OPENBLAS_NUM_THREADS", "GOTO_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS")
+
+
+def _native_threads() -> list[str]:
+    """Names of this process's OS threads (/proc/self/task/*/comm), the main thread first."""
+    out = []
     try:
-        n = int(env.get("OMP_NUM_THREADS") or 0)
-    except ValueError:
-        n = 0
-    if n <= 0:
-        n = len(os.sched_getaffinity(0))
-    torch.set_num_threads(max(1, n))
+        tids = sorted(os.listdir("/proc/self/task"), key=lambda t: (int(t) != os.getpid(), int(t)))
+    except OSError:
+        return ["?"]
+    for t in tids:
+        try:
+            with open(f"/proc/self/task/{t}/comm") as f:
+                out.append(f"{t}:{f.read().strip()}")
+        except OSError:
+            pass
+    return out
+
+
+def _env_threads(env: dict, *keys: str) -> int:
+    for k in keys:
+        try:
+            n = int(env.get(k) or 0)
+        except ValueError:
+            n = 0
+        if n > 0:
+            return n
+    return len(os.sched_getaffinity(0))
+
+
+def _size_thread_pools(env: dict) -> None:
+    """The OpenMP / OpenBLAS runtimes read their thread counts when the zygote loaded them (pinned to
+    one, see _POOL_ENV), so a forked container would keep that instead of what a fresh process pinned
+    to its NUMA-local CPUs gets. Apply the container's own settings, as a fresh process would read them."""
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        torch.set_num_threads(max(1, _env_threads(env, "OMP_NUM_THREADS")))
+    if "numpy" in sys.modules:
+        try:
+            from threadpoolctl import threadpool_limits
+            threadpool_limits(_env_threads(env, "OPENBLAS_NUM_THREADS", "GOTO_NUM_THREADS", "OMP_NUM_THREADS"),
+                              user_api="blas")
+        except Exception:  # noqa: BLE001 - no threadpoolctl in this image: BLAS stays single-threaded
+            pass
 
 
 def _child(req: dict, closefds: list[int]) -> None:
@@ -155,6 +190,11 @@ def serve(sock_path: str, preload: list[str]) -> int:
     if _gpu_driver_open():
         print(f"[zygote] refusing to serve: preloading {preload} opened the GPU driver", flush=True)
         return 3
+    threads = _native_threads()
+    if len(threads) > 1:
+        print(f"[zygote] refusing to serve: preloading {preload} left {len(threads)} threads {threads}; "
+              "a fork would copy only the main one", flush=True)
+        return 4
     _set_pdeathsig()
     try:
         os.unlink(sock_path)
@@ -170,7 +210,8 @@ def serve(sock_path: str, preload: list[str]) -> int:
     os.chmod(sock_path + ".tmp", 0o600)
     lsock.listen(64)
     os.rename(sock_path + ".tmp", sock_path)  # the socket appears only once the zygote accepts
-    print(f"[zygote] pid {os.getpid()} ready on {sock_path}: preloaded {preload} in {import_s:.2f} s", flush=True)
+    print(f"[zygote] pid {os.getpid()} ready on {sock_path}: preloaded {preload} in {import_s:.2f} s, "
+          f"threads {len(_native_threads())}", flush=True)
 
     rd, wr = os.pipe()
     os.set_blocking(rd, False)
@@ -227,6 +268,16 @@ def serve(sock_path: str, preload: list[str]) -> int:
             return
         sys.stdout.flush()
         sys.stderr.flush()
+        threads = _native_threads()
+        if len(threads) > 1:  # started since the preload check: never fork around it
+            print(f"[zygote] not forking: {len(threads)} threads {threads}", flush=True)
+            try:
+                conn.sendall((json.dumps({"error": f"zygote is multi-threaded ({len(threads)})"}) + "\n").encode())
+            except OSError:
+                pass
+            conn.close()
+            stop.append(1)
+            return
         pid = os.fork()
         if pid == 0:
             _child(req, [lsock.fileno(), rd, wr] + [c.fileno() for c in children.values()] + [conn.fileno()])
@@ -264,6 +315,8 @@ def main(argv=None) -> int:
     p.add_argument("--socket", required=True)
     p.add_argument("--preload", default="", help="comma-separated modules to import before serving")
     a = p.parse_args(argv)
+    for k in _POOL_ENV:  # the containers get their own env; these only shape the preload
+        os.environ[k] = "1"
     return serve(a.socket, [m for m in a.preload.split(",") if m])
 
 

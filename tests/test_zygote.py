@@ -188,14 +188,17 @@ def test_zygote_protocol_thread_pool_env_argv_exit(tmp_path):
     sock = str(tmp_path / "z.sock")
     env = dict(os.environ, PYTHONPATH=str(root))
     env.pop("OMP_NUM_THREADS", None)
-    z = subprocess.Popen([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock, "--preload", "torch"],
-                         env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    env.pop("OPENBLAS_NUM_THREADS", None)
+    z = subprocess.Popen([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock,
+                          "--preload", "numpy,torch"], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
         deadline = time.time() + 120
         while not os.path.exists(sock):
             assert z.poll() is None and time.time() < deadline
             time.sleep(0.05)
         assert oct(os.stat(sock).st_mode & 0o777) == "0o600"
+        # fork-safe: numpy (OpenBLAS) and torch preloaded, yet only the main thread exists
+        assert len(os.listdir(f"/proc/{z.pid}/task")) == 1
         cpus = sorted(os.sched_getaffinity(0))[:2]
 
         def run(extra_env, exit_code):
@@ -214,9 +217,11 @@ def test_zygote_protocol_thread_pool_env_argv_exit(tmp_path):
         pid, st, probe = run([], 0)
         assert st == {"exit": 0, "signal": 0}
         assert probe["cpus"] == cpus and probe["threads"] == len(cpus)
+        assert probe["blas_threads"] == [len(cpus)]  # grown back from the zygote's 1
         assert probe["env"] == "v" and probe["argv"] == ["a1", "a2"] and probe["cwd"] == str(tmp_path)
         pid, st, probe = run(["OMP_NUM_THREADS=1"], 3)
-        assert st["exit"] == 3 and probe["threads"] == 1
+        assert st["exit"] == 3 and probe["threads"] == 1 and probe["blas_threads"] == [1]
+        assert len(os.listdir(f"/proc/{z.pid}/task")) == 1
     finally:
         z.terminate()
         z.wait(timeout=10)
@@ -241,6 +246,21 @@ def test_gpu_exec_into_torch_ready_notebook():
         assert r["exitCode"] == 0, r
         assert r["output"].strip().splitlines()[-1] == "4.0 1"
         c.delete(NB, "Notebook", "g", "zx")
+
+
+def test_zygote_refuses_a_multithreaded_preload(tmp_path):
+    """A preload that leaves a native thread behind makes the zygote refuse to serve (exit 4), naming
+    the threads; the kubelet then starts containers as fresh interpreters."""
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    sock = str(tmp_path / "z.sock")
+    p = subprocess.run([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock,
+                        "--preload", "tests.zygote_thread_mod"], env=dict(os.environ, PYTHONPATH=str(root)),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 4, p.stdout + p.stderr
+    assert "refusing to serve" in p.stdout and "2 threads" in p.stdout, p.stdout
+    assert not os.path.exists(sock)
 
 
 def test_zygote_rejects_malformed_requests(tmp_path):
