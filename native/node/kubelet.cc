@@ -27,6 +27,7 @@
 #include "core/util.h"
 #include "gpu/smi.h"
 #include "node/node.h"
+#include "node/prober.h"
 
 extern char** environ;
 
@@ -142,6 +143,7 @@ struct ContainerRt {
   int ready_ok = 0, ready_fail = 0, live_fail = 0, startup_ok = 0, startup_fail = 0;
   double next_ready_probe = 0, next_live_probe = 0, next_startup_probe = 0, backoff_until = 0;
   double run_started = 0;
+  uint64_t probe_gen = 0;  // Prober generation of this run: verdicts of earlier runs are dropped
   Json last_state = Json::object();
   std::string log_path, term_path;
   // forked by a zygote (not our child): the exit status arrives on this connection; -1 = our own
@@ -201,6 +203,9 @@ Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)
   make_dirs(cfg_.root_dir + "/pods");
   make_dirs(cfg_.root_dir + "/pv");
   rec_ = std::make_unique<EventRecorder>(c_, "kubelet");
+  prober_ = std::make_unique<Prober>([this](const std::string& ns, const std::string& name) {
+    if (ctl_) ctl_->enqueue(Request{ns, name});
+  });
 }
 
 // Process pods share the host network namespace, and torch's TCPStore listens on the wildcard
@@ -232,6 +237,7 @@ int Kubelet::alloc_rdzv_port() {
 
 Kubelet::~Kubelet() {
   stop();
+  prober_->stop();  // also when start() never ran
   for (auto& kv : watched_) ::close(kv.first);
   if (epfd_ >= 0) ::close(epfd_);
   if (wake_fd_ >= 0) ::close(wake_fd_);
@@ -443,6 +449,7 @@ void Kubelet::stop() {
   }
   if (!running_.exchange(false)) return;
   stopping_ = true;
+  prober_->stop();  // waits for in-flight probes (each bounded by its timeoutSeconds)
   if (hb_.joinable()) hb_.join();
   if (wake_fd_ >= 0) {
     const uint64_t one = 1;
@@ -516,6 +523,41 @@ pid_t spawn(const std::vector<std::string>& argv, const std::vector<std::string>
     return -1;
   }
   return pid;
+}
+
+// An exec probe's process (on a Prober thread): wait up to timeout_ms for it (pidfd + poll, no
+// spinning), SIGKILL its group past that, reap it. Returns its exit code (non-zero on timeout).
+int wait_probe_process(pid_t pid, int timeout_ms) {
+  int st = 0;
+#ifdef SYS_pidfd_open
+  const int pfd = static_cast<int>(::syscall(SYS_pidfd_open, pid, 0));
+#else
+  const int pfd = -1;
+#endif
+  bool timed_out = false;
+  if (pfd >= 0) {
+    pollfd p{pfd, POLLIN, 0};
+    int rc;
+    do rc = ::poll(&p, 1, timeout_ms);
+    while (rc < 0 && errno == EINTR);
+    timed_out = rc == 0;
+    ::close(pfd);
+  } else {
+    const double deadline = now_seconds() + timeout_ms / 1000.0;
+    while (::waitpid(pid, &st, WNOHANG) == 0) {
+      if (now_seconds() > deadline) {
+        timed_out = true;
+        break;
+      }
+      ::usleep(5000);
+    }
+    if (!timed_out) return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+  }
+  if (timed_out) ::kill(-pid, SIGKILL);
+  while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+  }
+  if (timed_out) return 124;
+  return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
 }
 
 // returns true when the process has exited (fills status)
@@ -881,6 +923,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
           terminate_pod(*rt, 0);
           alloc_->release(rt->uid);
           rdzv_ports_.erase(rt->rdzv_port);
+          prober_->forget_pod(rt->uid);
           pods_.erase(rt->uid);
         }
         key_to_uid_.erase(k);
@@ -915,6 +958,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       alloc_->release(uid);
       std::lock_guard<std::mutex> g(mu_);
       rdzv_ports_.erase(rt->rdzv_port);
+      prober_->forget_pod(uid);
       pods_.erase(uid);
       key_to_uid_.erase(r.ns + "/" + r.name);
     }
@@ -1232,6 +1276,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       watch_exit(pid, r.ns, r.name);
     }
     cr.run_started = now_seconds();
+    cr.probe_gen = Prober::next_generation();
     cr.ready = false;
     cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
     const Json& sp = c["startupProbe"];
@@ -1241,7 +1286,9 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     cr.next_live_probe = now_seconds() + static_cast<double>(probe_i(c["livenessProbe"], "initialDelaySeconds", 0));
     rec_->event(pod, "Normal", "Started", "Started container " + cr.name);
   };
-  auto run_probe = [&](const Json& probe, const Json& c) -> bool {
+  // The probe as a self-contained closure (copies of the spec, the pod IP and the container env):
+  // it runs on a Prober thread, never on this reconcile worker.
+  auto make_probe = [&](const Json& probe, const Json& c) -> std::function<bool()> {
     const int timeout = static_cast<int>(probe_i(probe, "timeoutSeconds", 1)) * 1000;
     auto port_of = [&](const Json& p) -> int {
       if (p.is_number()) return static_cast<int>(p.as_int());
@@ -1251,36 +1298,42 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     };
     if (probe["httpGet"].is_object()) {
       const Json& hg = probe["httpGet"];
-      std::string host = hg["host"].as_string_or(rt->ip);
+      const std::string host = hg["host"].as_string_or(rt->ip);
       std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
       Headers h;
       for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
-      HttpResult res = http_request("GET", url, "", h, timeout);
-      return res.status >= 200 && res.status < 400;
+      return [url, h, timeout] {
+        HttpResult res = http_request("GET", url, "", h, timeout);
+        return res.status >= 200 && res.status < 400;
+      };
     }
-    if (probe["tcpSocket"].is_object()) return tcp_connect(rt->ip, port_of(probe.at_path({"tcpSocket", "port"})), timeout);
+    if (probe["tcpSocket"].is_object()) {
+      const std::string ip = rt->ip;
+      const int port = port_of(probe.at_path({"tcpSocket", "port"}));
+      return [ip, port, timeout] { return tcp_connect(ip, port, timeout); };
+    }
     if (probe["exec"].is_object()) {
       std::vector<std::string> argv;
       for (const auto& a : probe.at_path({"exec", "command"}).as_array()) argv.push_back(a.as_string());
-      if (argv.empty()) return false;
+      if (argv.empty()) return [] { return false; };
       std::vector<std::string> envv;
       std::map<std::string, std::string> envm;
       env_for(c, envv, envm);
-      pid_t pid = spawn(argv, envv, rt->dir + "/rootfs", rt->dir + "/probe.log", nullptr);
-      if (pid < 0) return false;
-      double deadline = now_seconds() + timeout / 1000.0;
-      int code = 0;
-      std::string reason;
-      while (!reap(pid, code, reason)) {
-        if (now_seconds() > deadline) {
-          ::kill(-pid, SIGKILL);
-          deadline = now_seconds() + 5;
-        }
-        ::usleep(2000);
-      }
-      return code == 0;
+      const std::string cwd = rt->dir + "/rootfs", log = rt->dir + "/probe.log";
+      return [argv, envv, cwd, log, timeout] {
+        pid_t pid = spawn(argv, envv, cwd, log, nullptr);
+        if (pid < 0) return false;
+        return wait_probe_process(pid, timeout) == 0;
+      };
     }
-    return true;
+    return [] { return true; };
+  };
+  // The verdict of this container's last `kind` probe, if one finished; starts one when `due`.
+  auto probe_verdict = [&](ContainerRt& cr, const char* kind, const Json& probe, const Json& c,
+                           bool due) -> std::optional<bool> {
+    const std::string key = rt->uid + "/" + (cr.init ? "init:" : "") + cr.name + "/" + kind;
+    const bool start = due && !prober_->in_flight(key);
+    return prober_->poll(key, cr.probe_gen, start, r.ns, r.name, start ? make_probe(probe, c) : nullptr);
   };
   auto handle_exit = [&](ContainerRt& cr) {
     int code = 0;
@@ -1305,14 +1358,16 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
   auto tick_probes = [&](ContainerRt& cr, const Json& c) {
     const double now = now_seconds();
     const Json& sp = c["startupProbe"];
-    if (!cr.started_probe_ok && now >= cr.next_startup_probe) {
-      if (run_probe(sp, c)) {
-        if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
-      } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
-        rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
-        ::kill(-cr.pid, SIGKILL);
+    if (!cr.started_probe_ok) {
+      if (auto v = probe_verdict(cr, "startup", sp, c, now >= cr.next_startup_probe)) {
+        if (*v) {
+          if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
+        } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
+          rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
+          ::kill(-cr.pid, SIGKILL);
+        }
+        cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
       }
-      cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
     }
     if (!cr.started_probe_ok) {
       next_wake = std::min(next_wake, 0.1);
@@ -1321,8 +1376,8 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     const Json& rp = c["readinessProbe"];
     if (!rp.is_object()) {
       cr.ready = true;
-    } else if (now >= cr.next_ready_probe) {
-      bool ok = run_probe(rp, c);
+    } else if (auto v = probe_verdict(cr, "readiness", rp, c, now >= cr.next_ready_probe)) {
+      const bool ok = *v;
       if (ok) {
         cr.ready_fail = 0;
         if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
@@ -1338,14 +1393,16 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
       cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : kStartupPoll);
     }
     const Json& lp = c["livenessProbe"];
-    if (lp.is_object() && now >= cr.next_live_probe) {
-      if (run_probe(lp, c)) {
-        cr.live_fail = 0;
-      } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
-        rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
-        ::kill(-cr.pid, SIGKILL);
+    if (lp.is_object()) {
+      if (auto v = probe_verdict(cr, "liveness", lp, c, now >= cr.next_live_probe)) {
+        if (*v) {
+          cr.live_fail = 0;
+        } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
+          rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
+          ::kill(-cr.pid, SIGKILL);
+        }
+        cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
       }
-      cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
     }
     if (!cr.ready) {
       next_wake = std::min(next_wake, kStartupPoll);

@@ -42,6 +42,8 @@
 
 namespace kf {
 
+class Prober;  // node/prober.h
+
 // Resource accounting helpers (shared with the quota admission plugin).
 // Effective pod request: max(sum(containers), max(initContainers)) per resource; extended
 // resources default their request to the limit.
@@ -134,6 +136,7 @@ class Kubelet {
   std::set<int> rdzv_ports_;  // MASTER_PORTs handed to running multi-GPU pods
   int alloc_rdzv_port();
   std::unique_ptr<EventRecorder> rec_;
+  std::unique_ptr<Prober> prober_;  // probes run on its threads, never on a reconcile worker
   std::shared_ptr<Controller> ctl_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stopping_{false};
