@@ -227,8 +227,29 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
   constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
   constexpr int MF = NR * NR;                          // MFMAs per wave per k32 substep
-  constexpr int DMA_EVERY = MF / PIECES;               // one DMA per DMA_EVERY MFMAs
-  constexpr int RG = 2;
+  // Schedule knobs (tools/w4_ab.py A/B builds; the defaults are the production schedule):
+  //   KFW4_RG: one fragment read per RG MFMAs; KFW4_DMA_EVERY / KFW4_DMA_PHASE: DMA piece j at
+  //   MFMA j * DMA_EVERY + DMA_PHASE of its substep; KFW4_PIN_MFMA: sched_barrier around every MFMA.
+#ifndef KFW4_DMA_EVERY
+#define KFW4_DMA_EVERY 0
+#endif
+#ifndef KFW4_DMA_PHASE
+#define KFW4_DMA_PHASE 2
+#endif
+#ifndef KFW4_RG
+#define KFW4_RG 2
+#endif
+#ifndef KFW4_PIN_MFMA
+#define KFW4_PIN_MFMA 1
+#endif
+#ifndef KFW4_PRIO
+#define KFW4_PRIO 1
+#endif
+  constexpr int DMA_EVERY = KFW4_DMA_EVERY > 0 ? KFW4_DMA_EVERY : MF / PIECES;  // one DMA per DMA_EVERY MFMAs
+  constexpr int DMA_PHASE = KFW4_DMA_PHASE;
+  static_assert(DMA_EVERY * (PIECES - 1) + DMA_PHASE < MF, "every DMA piece inside its substep");
+  constexpr int RG = KFW4_RG;
+  static_assert(RG * (2 * NR - 1) < MF, "every fragment read inside its substep");
   static_assert(BM == 256 || BM == 128, "tile");
   static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
   static_assert(!SPLIT || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
@@ -333,6 +354,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // the K-loop segments, read as SHARES (the stamps' lgkmcnt(0) forbids some overlap).
   unsigned long long seg[4] = {0, 0, 0, 0};
   unsigned long long t_loop0 = 0, t_loop1 = 0;
+#ifndef KFW4_CHEAP_STAMPS
+#define KFW4_CHEAP_STAMPS 0  // 1: s_memtime with no wait of its own; read after the loop's own lgkmcnt(0)
+#endif
   auto stamp = [&]() -> unsigned long long {
     unsigned long long t = 0;
     if (DIAG) {
@@ -342,6 +366,19 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
     return t;
   };
+  // K-loop stamps: with KFW4_CHEAP_STAMPS no wait of their own (valid after the loop's lgkmcnt(0))
+  auto stamp_k = [&]() -> unsigned long long {
+    unsigned long long t = 0;
+    if (DIAG && KFW4_CHEAP_STAMPS) {
+      KFW4_PIN();
+      asm volatile("s_memtime %0" : "=s"(t)::"memory");
+      KFW4_PIN();
+    } else if (DIAG) {
+      t = stamp();
+    }
+    return t;
+  };
+  unsigned long long prev_t3 = 0;  // cheap stamps: the previous iteration's end-of-MFMA stamp
   using T = std::integral_constant<bool, true>;
   using F = std::integral_constant<bool, false>;
   unsigned long long sk_mask = 0;  // stream-K owner: which producer splits' partials the epilogue adds
@@ -373,22 +410,22 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   for (int q = 0; q < 2 * NR; ++q) read_frag0(sa0, sb0, a0, b0, q);
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   KFW4_PIN();
-  __builtin_amdgcn_s_setprio(1);
+  if (KFW4_PRIO) __builtin_amdgcn_s_setprio(1);
 
   auto body = [&](int kt, auto do_stage, auto do_next) {
     constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
     constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
-    const unsigned long long t0 = stamp();
+    const unsigned long long t0 = stamp_k();
     // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag1(sa0, sb0, a1, b1, m / RG);
-      if (kStage && m % DMA_EVERY == 2) dma_a(kt + 2, sf, m / DMA_EVERY, false);
-      KFW4_PIN();
+      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) dma_a(kt + 2, sf, m / DMA_EVERY, false);
+      if (KFW4_PIN_MFMA) KFW4_PIN();
       mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
-      KFW4_PIN();
+      if (KFW4_PIN_MFMA) KFW4_PIN();
     }
-    const unsigned long long t1 = stamp();
+    const unsigned long long t1 = stamp_k();
     // tile kt+1 landed (only A_{kt+2} may still be in flight), F1(kt) in registers, then barrier:
     // after it tile kt's slots are free
     if (kStage) {
@@ -401,17 +438,17 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     __builtin_amdgcn_s_barrier();
     KFW4_FENCE();
     KFW4_PIN();
-    const unsigned long long t2 = stamp();
+    const unsigned long long t2 = stamp_k();
     // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag0(sa1, sb1, a0, b0, m / RG);
-      if (kStage && m % DMA_EVERY == 2) dma_b(kt + 2, sa0, m / DMA_EVERY, false);
-      KFW4_PIN();
+      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) dma_b(kt + 2, sa0, m / DMA_EVERY, false);
+      if (KFW4_PIN_MFMA) KFW4_PIN();
       mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
-      KFW4_PIN();
+      if (KFW4_PIN_MFMA) KFW4_PIN();
     }
-    const unsigned long long t3 = stamp();
+    const unsigned long long t3 = stamp_k();
     if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
     KFW4_PIN();
     // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
@@ -421,7 +458,18 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     sb0 = sb1;
     sa1 = na;
     sb1 = nb;
-    if (DIAG) {
+    if (DIAG && KFW4_CHEAP_STAMPS) {
+      // the stamps landed by this lgkmcnt(0) (the loop's own, except after the last tile); the empty
+      // asm re-defines them after it so no arithmetic on them is hoisted above the wait
+      if (!kNext) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned long long u0 = t0, u1 = t1, u2 = t2, u3 = t3;
+      asm volatile("" : "+s"(u0), "+s"(u1), "+s"(u2), "+s"(u3)::"memory");
+      seg[0] += u1 - u0;  // substep 0: MFMA issue + F1 reads + A DMAs
+      seg[1] += u2 - u1;  // mid wait (vmcnt / lgkmcnt) + barrier
+      seg[2] += u3 - u2;  // substep 1
+      if (prev_t3) seg[3] += u0 - prev_t3;  // end lgkmcnt(0) + slot rotation to the next tile
+      prev_t3 = u3;
+    } else if (DIAG) {
       const unsigned long long t4 = stamp();
       seg[0] += t1 - t0;
       seg[1] += t2 - t1;
@@ -437,7 +485,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     ++kt;
   }
   if (kt < nk) body(kt, F{}, F{});
-  __builtin_amdgcn_s_setprio(0);
+  if (KFW4_PRIO) __builtin_amdgcn_s_setprio(0);
   if (DIAG) t_loop1 = stamp();
   // the asm MFMAs are opaque to the hazard recognizer: cover the MFMA -> v_accvgpr_read latency
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");

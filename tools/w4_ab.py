@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""A/B of w4 GEMM K-loop schedules (tools/w4_ab.hip built once per knob set) on one GPU.
+
+  python tools/w4_ab.py --build            # on the host: compile every variant into kubeflow_rm_amd/lib/w4ab/
+  python tools/w4_ab.py --sizes 4096,8192   # on the GPU: bitwise check vs production, interleaved timing
+                                            # rounds vs the production kernel and torch.matmul, then the
+                                            # variants' cheap K-loop stamps (cycles per 64-k tile by segment)
+
+Prints one JSON line per measurement. Knobs: kernels/gemm_w4.h (KFW4_RG, KFW4_DMA_EVERY, KFW4_DMA_PHASE,
+KFW4_PIN_MFMA, KFW4_PRIO); every variant also carries KFW4_CHEAP_STAMPS=1, which only touches its diag
+kernel (s_memtime with no wait of its own, read after the loop's own lgkmcnt(0)).
+"""
+import argparse
+import ctypes
+import json
+import statistics
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+OUT = ROOT / "kubeflow_rm_amd" / "lib" / "w4ab"
+
+VARIANTS = {
+    "base": [],
+    "rg4": ["-DKFW4_RG=4"],
+    "dma_cluster": ["-DKFW4_DMA_EVERY=2", "-DKFW4_DMA_PHASE=1"],
+    "dma_spread6": ["-DKFW4_DMA_EVERY=6", "-DKFW4_DMA_PHASE=1"],
+    "nopin": ["-DKFW4_PIN_MFMA=0"],
+    "noprio": ["-DKFW4_PRIO=0"],
+}
+
+
+def build(names):
+    from concurrent.futures import ThreadPoolExecutor
+    OUT.mkdir(parents=True, exist_ok=True)
+
+    def one(name):
+        so = OUT / f"libw4ab_{name}.so"
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-mcode-object-version=5", f"-I{ROOT / 'kernels'}", "-DKFW4_CHEAP_STAMPS=1", *VARIANTS[name],
+               str(ROOT / "tools" / "w4_ab.hip"), "-o", str(so)]
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode:
+            raise SystemExit(f"{name}: {p.stderr[-2000:]}")
+        return name
+    with ThreadPoolExecutor(4) as ex:
+        for n in ex.map(one, names):
+            print("built", n, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--sizes", default="4096,8192,16384")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--diag", default="8192")
+    a = ap.parse_args()
+    names = [v for v in a.variants.split(",") if v]
+    if a.build:
+        build(names)
+        return
+    import torch
+    from kubeflow_rm_amd import ops
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    libs = {}
+    for n in names:
+        L = ctypes.CDLL(str(OUT / f"libw4ab_{n}.so"))
+        L.w4ab_nt.restype = i
+        L.w4ab_nt.argtypes = [vp, vp, vp, i, i, i, vp]
+        L.w4ab_diag.restype = i
+        L.w4ab_diag.argtypes = [vp, vp, vp, i, i, i, vp, vp]
+        libs[n] = L
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for s in [int(x) for x in a.sizes.split(",") if x]:
+        A = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        B = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        ref = ops.gemm_nt(A, B)
+        C = torch.empty_like(ref)
+        same = {}
+        for n, L in libs.items():
+            assert L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st) == 0
+            torch.cuda.synchronize()
+            same[n] = bool(torch.equal(C, ref))
+        iters = max(5, int(3e13 / (2 * s ** 3)))
+        fns = {"prod": lambda: ops.gemm_nt(A, B, out=C), "torch": lambda: torch.matmul(A, B.t())}
+        for n, L in libs.items():
+            fns[n] = (lambda L=L: L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st))
+        t_end = time.perf_counter() + 1.0
+        while time.perf_counter() < t_end:
+            fns["prod"]()
+        tf = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, fn in fns.items():
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+                tf[k].append(2 * s ** 3 * iters / (time.perf_counter() - t0) / 1e12)
+        print(json.dumps({"size": s, "bitwise_equal_to_prod": same,
+                          "median_tf": {k: round(statistics.median(v), 1) for k, v in tf.items()},
+                          "best_tf": {k: round(max(v), 1) for k, v in tf.items()}}), flush=True)
+        del A, B, C, ref
+    for s in [int(x) for x in a.diag.split(",") if x]:
+        A = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        B = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+        C = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
+        nblk = (s // 256) ** 2
+        diag = torch.zeros(nblk * 4 * 16, dtype=torch.int64, device=dev)
+        nk = s // 64
+        for n, L in libs.items():
+            for _ in range(3):
+                assert L.w4ab_diag(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, diag.data_ptr(), st) == 0
+            torch.cuda.synchronize()
+            d = diag.view(nblk, 4, 16).double()
+            seg = (d[..., :4].sum(dim=(0, 1)) / (nblk * 4 * (nk - 1))).tolist()  # cycles per 64-k tile
+            clk = ((d[:, 0, 7]) / (d[:, 0, 9] - d[:, 0, 8]).clamp(min=1) * 100).median().item()
+            print(json.dumps({"diag_size": s, "variant": n,
+                              "cycles_per_ktile": {"substep0": round(seg[0]), "mid_wait_barrier": round(seg[1]),
+                                                   "substep1": round(seg[2]), "end_wait_rotate": round(seg[3]),
+                                                   "total": round(sum(seg))},
+                              "prologue_cycles": round(d[..., 4].mean().item()),
+                              "epilogue_cycles": round(d[..., 5].mean().item()),
+                              "block_cycles": round(d[..., 7].mean().item()), "clock_mhz_median": round(clk)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
