@@ -248,7 +248,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   constexpr int DMA_EVERY = KFW4_DMA_EVERY > 0 ? KFW4_DMA_EVERY : MF / PIECES;  // one DMA per DMA_EVERY MFMAs
   constexpr int DMA_PHASE = KFW4_DMA_PHASE;
   static_assert(DMA_EVERY * (PIECES - 1) + DMA_PHASE < MF, "every DMA piece inside its substep");
-  constexpr int RG = KFW4_RG;
+  constexpr int RG = KFW4_RG < MF / (2 * NR) ? KFW4_RG : MF / (2 * NR);  // 128 tile: at most 2
   static_assert(RG * (2 * NR - 1) < MF, "every fragment read inside its substep");
   static_assert(BM == 256 || BM == 128, "tile");
   static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
@@ -327,6 +327,36 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, KFW4_LDS_PTR(smem + slot * TILE + (wid * PIECES + j) * 1024), 16,
                                              v, j * rs_b + kt * kts_b, 0, 0);
   };
+
+#ifndef KFW4_FASTK
+#define KFW4_FASTK 2  // 2: steady-state DMAs with a voffset register per piece and one soffset per K-tile
+#endif
+  // (a per-K-tile descriptor rebuild, tried as mode 1, made hipcc 7.2's host pass drop the launch stubs)
+#ifndef KFW4_UNROLL5
+#define KFW4_UNROLL5 1  // K loop unrolled over the 5-slot ring's period: every slot index a constant
+#endif
+#ifndef KFW4_ASM_DMA
+#define KFW4_ASM_DMA 0
+#endif
+  static_assert(!KFW4_ASM_DMA || (KFW4_FASTK == 2 && KFW4_DMA_PHASE >= 1), "asm DMA: voffset regs, M0 set one MFMA ahead");
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  // raw buffer descriptors as SGPR quads for the asm pieces (gfx9: base, base_hi | stride 0, records, word 3)
+  auto make_desc = [&](const void* p) __attribute__((always_inline)) -> i32x4 {
+    const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+    return i32x4{__builtin_amdgcn_readfirstlane((int)(unsigned)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+                 nrec, kRsrcWord3};
+  };
+  i32x4 dra = make_desc(A), drb = make_desc(B);
+  const unsigned lds_w = (unsigned)(uintptr_t)KFW4_LDS_PTR(smem) + (unsigned)(wid * PIECES * 1024);  // wave's pieces
+  // KFW4_FASTK == 2: piece j's full voffset (chunk swizzle + j rows) in a register of its own
+  unsigned vpa[PIECES], vpb[PIECES];
+  if (KFW4_FASTK == 2) {
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+      vpa[j] = sta.voff[Stage<LA, BM>::variant_of_piece(j)] + (unsigned)(j * rs_a);
+      vpb[j] = stb.voff[Stage<LB, BM>::variant_of_piece(j)] + (unsigned)(j * rs_b);
+    }
+  }
 
   Reader<LA, BM> rda;
   Reader<LB, BM> rdb;
@@ -412,15 +442,52 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   KFW4_PIN();
   if (KFW4_PRIO) __builtin_amdgcn_s_setprio(1);
 
-  auto body = [&](int kt, auto do_stage, auto do_next) {
+  // one K-tile; the slots come in as ints (rotating at run time) or integral constants (unrolled)
+  auto body_g = [&](int kt, auto do_stage, auto do_next, auto sa0, auto sb0, auto sa1, auto sb1, auto sf)
+      __attribute__((always_inline)) {
     constexpr bool kStage = decltype(do_stage)::value;  // tile kt+2 exists
     constexpr bool kNext = decltype(do_next)::value;    // tile kt+1 exists
+    // KFW4_ASM_DMA: the steady-state pieces as inline asm, M0 written one MFMA ahead (no s_nop for
+    // the M0 -> LDS-DMA hazard, no per-piece M0 copy); waits stay the loop's explicit ones
+    const unsigned lw = lds_w;  // (named here: a nested generic lambda does not capture it otherwise)
+    auto m0_set = [&](int slot, int j) __attribute__((always_inline)) {
+      const unsigned m0v = lw + (unsigned)(slot * TILE + j * 1024);
+      asm volatile("s_mov_b32 m0, %0" ::"s"(m0v) : "memory");
+    };
+    auto asm_dma = [&](const i32x4& r, unsigned v, int so) __attribute__((always_inline)) {
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(r), "s"(so) : "memory");
+    };
+    auto stage_a = [&](int j) __attribute__((always_inline)) {
+      if (KFW4_ASM_DMA) {
+        asm_dma(dra, vpa[j], (kt + 2) * kts_a);
+      } else if (KFW4_FASTK == 2) {  // per-piece voffset registers, one soffset per K-tile
+        // plain locals as the builtin's operands (see the soffset note above dma_a)
+        const unsigned v = vpa[j];
+        const int so = (kt + 2) * kts_a;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, KFW4_LDS_PTR(smem + sf * TILE + (wid * PIECES + j) * 1024), 16,
+                                                 v, so, 0, 0);
+      }
+      else dma_a(kt + 2, sf, j, false);
+    };
+    auto stage_b = [&](int j) __attribute__((always_inline)) {
+      if (KFW4_ASM_DMA) {
+        asm_dma(drb, vpb[j], (kt + 2) * kts_b);
+      } else if (KFW4_FASTK == 2) {
+        const unsigned v = vpb[j];
+        const int so = (kt + 2) * kts_b;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, KFW4_LDS_PTR(smem + sa0 * TILE + (wid * PIECES + j) * 1024), 16,
+                                                 v, so, 0, 0);
+      }
+      else dma_b(kt + 2, sa0, j, false);
+    };
     const unsigned long long t0 = stamp_k();
     // substep 0: MFMAs on F0(kt); read F1(kt); DMA A_{kt+2} -> free slot
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag1(sa0, sb0, a1, b1, m / RG);
-      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) dma_a(kt + 2, sf, m / DMA_EVERY, false);
+      if (KFW4_ASM_DMA && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
+        m0_set(sf, (m + 1) / DMA_EVERY);
+      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) stage_a(m / DMA_EVERY);
       if (KFW4_PIN_MFMA) KFW4_PIN();
       mfma(acc[m / NR][m % NR], b0[m % NR], a0[m / NR]);
       if (KFW4_PIN_MFMA) KFW4_PIN();
@@ -443,7 +510,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag0(sa1, sb1, a0, b0, m / RG);
-      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) dma_b(kt + 2, sa0, m / DMA_EVERY, false);
+      if (KFW4_ASM_DMA && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
+        m0_set(sa0, (m + 1) / DMA_EVERY);
+      if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) stage_b(m / DMA_EVERY);
       if (KFW4_PIN_MFMA) KFW4_PIN();
       mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
       if (KFW4_PIN_MFMA) KFW4_PIN();
@@ -451,13 +520,6 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     const unsigned long long t3 = stamp_k();
     if (kNext) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): F0(kt+1) in registers
     KFW4_PIN();
-    // rotate: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
-    const int na = sf, nb = sa0;
-    sf = sb0;
-    sa0 = sa1;
-    sb0 = sb1;
-    sa1 = na;
-    sb1 = nb;
     if (DIAG && KFW4_CHEAP_STAMPS) {
       // the stamps landed by this lgkmcnt(0) (the loop's own, except after the last tile); the empty
       // asm re-defines them after it so no arithmetic on them is hoisted above the wait
@@ -477,8 +539,34 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       seg[3] += t4 - t3;
     }
   };
+  // rotate after each tile: tile kt+1 -> current, tile kt+2 in (sf, sa0), B_kt's slot becomes free
+  auto body = [&](int kt, auto do_stage, auto do_next) __attribute__((always_inline)) {
+    body_g(kt, do_stage, do_next, sa0, sb0, sa1, sb1, sf);
+    const int na = sf, nb = sa0;
+    sf = sb0;
+    sa0 = sa1;
+    sb0 = sb1;
+    sa1 = na;
+    sb1 = nb;
+  };
   if (DIAG) t_loop0 = stamp();
   int kt = 0;
+  if (KFW4_UNROLL5) {
+    // the ring's period is 5 tiles: (sa0, sb0, sa1, sb1, sf) = (0,1,2,3,4) -> (2,3,4,0,1) -> (4,0,1,2,3)
+    // -> (1,2,3,4,0) -> (3,4,0,1,2) -> (0,1,2,3,4); state 0 again after each group of five
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using C2 = std::integral_constant<int, 2>;
+    using C3 = std::integral_constant<int, 3>;
+    using C4 = std::integral_constant<int, 4>;
+    for (; kt + 6 < nk; kt += 5) {
+      body_g(kt, T{}, T{}, C0{}, C1{}, C2{}, C3{}, C4{});
+      body_g(kt + 1, T{}, T{}, C2{}, C3{}, C4{}, C0{}, C1{});
+      body_g(kt + 2, T{}, T{}, C4{}, C0{}, C1{}, C2{}, C3{});
+      body_g(kt + 3, T{}, T{}, C1{}, C2{}, C3{}, C4{}, C0{});
+      body_g(kt + 4, T{}, T{}, C3{}, C4{}, C0{}, C1{}, C2{});
+    }
+  }
   for (; kt + 2 < nk; ++kt) body(kt, T{}, T{});
   if (kt + 1 < nk) {
     body(kt, F{}, T{});
@@ -681,6 +769,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       const __bf16* b = B_in + (LB == 0 ? (long long)n0 * ldb + kofs : (long long)n0 + kofs * ldb);
       ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, (short)0, nrec, kRsrcWord3);
       rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, nrec, kRsrcWord3);
+      if (KFW4_ASM_DMA) {
+        dra = make_desc(a);
+        drb = make_desc(b);
+      }
       nk = k1 - k0;
       koff = k0 == 0 ? koff_full : 0;  // only the tile's first K tile is partial
     };

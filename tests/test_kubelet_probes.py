@@ -11,7 +11,6 @@ its full ``timeoutSeconds: 5``) do not delay a probe-less pod's Ready by more th
 still decide readiness (an exec probe that exits 0 / non-zero / outlives its timeout).
 """
 import socket
-import statistics
 import time
 
 import pytest
@@ -48,7 +47,8 @@ def _time_to_ready(c, name, ns="pr"):
 
 def test_stalled_readiness_probes_do_not_hold_back_other_pods(cl):
     c = cl.client
-    base = statistics.median(_time_to_ready(c, f"base{i}") for i in range(5))
+    # min of 5: the test host's own load (pytest -n 8) only ever adds to a sample
+    base = min(_time_to_ready(c, f"base{i}") for i in range(5))
     stall = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
     stall.bind(("127.0.0.1", 0))
     stall.listen(256)  # never accept()ed: every HTTP probe connects, then waits out its timeout
@@ -65,7 +65,7 @@ def test_stalled_readiness_probes_do_not_hold_back_other_pods(cl):
             assert time.time() < deadline
             time.sleep(0.05)
         time.sleep(0.5)
-        loaded = statistics.median(_time_to_ready(c, f"late{i}") for i in range(5))
+        loaded = min(_time_to_ready(c, f"late{i}") for i in range(5))
         assert loaded <= base + 0.05, (base, loaded)
         assert not any(_ready(c.get("v1", "Pod", f"stalled{i}", "pr")) for i in range(8))
     finally:

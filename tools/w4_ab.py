@@ -24,7 +24,13 @@ sys.path.insert(0, str(ROOT))
 OUT = ROOT / "kubeflow_rm_amd" / "lib" / "w4ab"
 
 VARIANTS = {
-    "base": [],
+    "base": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=0"],  # the round-3 K loop
+    "unroll5": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1"],
+    "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1"],
+    "asmdma": ["-DKFW4_ASM_DMA=1"],
+    "f2u5_rg4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_RG=4", "-DKFW4_DMA_PHASE=0"],
+    "f2u5_e4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_DMA_EVERY=4", "-DKFW4_DMA_PHASE=0"],
+    "u5_rg4p0": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1", "-DKFW4_RG=4", "-DKFW4_DMA_PHASE=0"],
     "rg4": ["-DKFW4_RG=4"],
     "dma_cluster": ["-DKFW4_DMA_EVERY=2", "-DKFW4_DMA_PHASE=1"],
     "dma_spread6": ["-DKFW4_DMA_EVERY=6", "-DKFW4_DMA_PHASE=1"],
@@ -45,6 +51,9 @@ def build(names):
         p = subprocess.run(cmd, capture_output=True, text=True)
         if p.returncode:
             raise SystemExit(f"{name}: {p.stderr[-2000:]}")
+        nm = subprocess.run(["nm", "-D", "--undefined-only", str(so)], capture_output=True, text=True).stdout
+        if "device_stub" in nm:  # hipcc 7.2 dropped the launch stubs (gemm_w4.h notes)
+            raise SystemExit(f"{name}: launch stubs missing")
         return name
     with ThreadPoolExecutor(4) as ex:
         for n in ex.map(one, names):
