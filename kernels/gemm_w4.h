@@ -607,7 +607,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
                                    reinterpret_cast<uintptr_t>(HAS_RES ? R : nullptr)) & 7) &&
                       !(HAS_RES && ((ldr | sr) & 3));
   // VEC (compile time): bias / residual as 8-B vector loads (the fast path) or element loads
-  auto finish = [&](auto VEC, int i, int n, int m, uint2& pre_out) -> uint2 {
+  // UNIT (compile time): alpha == 1, the scale is skipped (128 v_pk_mul_f32 per wave)
+  auto finish = [&](auto VEC, auto UNIT, int i, int n, int m, uint2& pre_out) -> uint2 {
     constexpr bool vec = decltype(VEC)::value;
     const int col = n0 + wn * WT + n * 16 + elh * 4;
     float v[4];
@@ -636,7 +637,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= alpha;
+    for (int r = 0; r < 4; ++r)
+      if constexpr (!decltype(UNIT)::value) v[r] *= alpha;
     if (HAS_BIAS) {
       if constexpr (vec) {
         const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
@@ -716,7 +718,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
   };
   const int swap_col = 16 * (elh & 1) + 8 * (elh >> 1);
-  auto emit = [&](auto VEC, auto store) {
+  auto emit = [&](auto VEC, auto store, auto UNIT) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int m = m0 + wm * WT + i * 16 + elr;
@@ -727,7 +729,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #pragma unroll
       for (int n = 0; n < NR; n += 2) {
         uint2 pp{0, 0}, pq{0, 0};
-        uint2 p = finish(VEC, i, n, m, pp), q = finish(VEC, i, n + 1, m, pq);
+        uint2 p = finish(VEC, UNIT, i, n, m, pp), q = finish(VEC, UNIT, i, n + 1, m, pq);
         const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
         const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
         const int c0 = n0 + wn * WT + n * 16 + swap_col;
@@ -743,10 +745,14 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // uniform branches: interior tiles store unmasked straight-line 16-B stores, shifted edge tiles
   // mask per lane, an odd output takes the og path; only the path that runs is fetched
   if (og == 8 && vec_in) {
-    if (m0 == m_lo && n0 == n_lo) emit(T{}, store_all);
-    else emit(T{}, store16);
+    if (m0 == m_lo && n0 == n_lo) {
+      if (alpha == 1.f) emit(T{}, store_all, T{});
+      else emit(T{}, store_all, F{});
+    } else {
+      emit(T{}, store16, F{});
+    }
   } else {
-    emit(F{}, store_og);
+    emit(F{}, store_og, F{});
   }
   };  // epilogue
 

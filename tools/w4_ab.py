@@ -28,6 +28,7 @@ VARIANTS = {
     "unroll5": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1"],
     "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1"],
     "asmdma": ["-DKFW4_ASM_DMA=1"],
+    "prev": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1"],
     "f2u5_rg4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_RG=4", "-DKFW4_DMA_PHASE=0"],
     "f2u5_e4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_DMA_EVERY=4", "-DKFW4_DMA_PHASE=0"],
     "u5_rg4p0": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1", "-DKFW4_RG=4", "-DKFW4_DMA_PHASE=0"],
