@@ -228,7 +228,7 @@ def main() -> int:
             "parallelism": f"dp{world}",
         },
         "per_gpu_tflops": round(per_gpu_tflops, 2),
-        "kernel": "kfamd gemm_w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring, XCD remap, in-kernel edge tiles)",
+        "kernel": "kfamd gemm_w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring with the K loop unrolled over its 5-tile period, XCD remap, in-kernel edge tiles)",
         "check_rows": int(rows.numel()),
         "correct": bool(ok),
         "max_abs_err_vs_fp32": err,
