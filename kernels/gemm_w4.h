@@ -336,7 +336,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #define KFW4_UNROLL5 1  // K loop unrolled over the 5-slot ring's period: every slot index a constant
 #endif
 #ifndef KFW4_ASM_DMA
-#define KFW4_ASM_DMA 0
+#define KFW4_ASM_DMA 1
 #endif
   static_assert(!KFW4_ASM_DMA || (KFW4_FASTK == 2 && KFW4_DMA_PHASE >= 1), "asm DMA: voffset regs, M0 set one MFMA ahead");
   typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -501,6 +501,19 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     } else {
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     }
+    // KFW4_PREBAR: the first substep-1 MFMAs (registers only) issue between the wait and the barrier,
+    // so the matrix pipe has work while the waves meet; the reads of tile kt+1 start after it
+#ifndef KFW4_PREBAR
+#define KFW4_PREBAR 1
+#endif
+    constexpr int PB = KFW4_PREBAR;
+    static_assert(PB + RG * (2 * NR - 1) < MF && PB <= DMA_PHASE, "pre-barrier MFMAs");
+#pragma unroll
+    for (int m = 0; m < PB; ++m) {
+      KFW4_PIN();
+      mfma(acc[m / NR][m % NR], b1[m % NR], a1[m / NR]);
+      KFW4_PIN();
+    }
     KFW4_FENCE();
     __builtin_amdgcn_s_barrier();
     KFW4_FENCE();
@@ -508,8 +521,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     const unsigned long long t2 = stamp_k();
     // substep 1: MFMAs on F1(kt); read F0(kt+1); DMA B_{kt+2} -> A_kt's slot
 #pragma unroll
-    for (int m = 0; m < MF; ++m) {
-      if (!(DIAG && ABL == 2) && kNext && m % RG == 0 && m / RG < 2 * NR) read_frag0(sa1, sb1, a0, b0, m / RG);
+    for (int m = PB; m < MF; ++m) {
+      if (!(DIAG && ABL == 2) && kNext && (m - PB) % RG == 0 && (m - PB) / RG < 2 * NR)
+        read_frag0(sa1, sb1, a0, b0, (m - PB) / RG);
       if (KFW4_ASM_DMA && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
         m0_set(sa0, (m + 1) / DMA_EVERY);
       if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) stage_b(m / DMA_EVERY);

@@ -24,10 +24,13 @@ sys.path.insert(0, str(ROOT))
 OUT = ROOT / "kubeflow_rm_amd" / "lib" / "w4ab"
 
 VARIANTS = {
-    "base": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=0"],  # the round-3 K loop
+    "base": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=0", "-DKFW4_ASM_DMA=0", "-DKFW4_PREBAR=0"],  # the round-3 K loop
     "unroll5": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1"],
-    "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1"],
+    "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_ASM_DMA=0", "-DKFW4_PREBAR=0"],
     "asmdma": ["-DKFW4_ASM_DMA=1"],
+    "prebar1": ["-DKFW4_PREBAR=1"],
+    "prebar2": ["-DKFW4_PREBAR=2"],
+    "asm_prebar1": ["-DKFW4_ASM_DMA=1", "-DKFW4_PREBAR=1"],
     "prev": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1"],
     "f2u5_rg4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_RG=4", "-DKFW4_DMA_PHASE=0"],
     "f2u5_e4p0": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_DMA_EVERY=4", "-DKFW4_DMA_PHASE=0"],
