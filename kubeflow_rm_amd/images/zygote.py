@@ -33,6 +33,7 @@ exercises is notebook_controller.go Reconcile -> StatefulSet -> kubelet -> image
 from __future__ import annotations
 
 import argparse
+import gc
 import importlib
 import json
 import os
@@ -121,6 +122,7 @@ def _child(req: dict, closefds: list[int]) -> None:
     """Runs in the forked process: become the container, run its module, never return."""
     code = 1
     try:
+        gc.enable()
         for fd in closefds:
             try:
                 os.close(fd)
@@ -183,9 +185,15 @@ _PRELOADED: set[str] = set()
 
 def serve(sock_path: str, preload: list[str]) -> int:
     t0 = time.perf_counter()
+    # pre-fork server idiom (Python docs, gc.freeze): no collections while the preload allocates (no
+    # freed holes in shared pages), then every preloaded object moves to the permanent generation, so a
+    # container's collections never write the gc headers of the shared copies (copy-on-write faults on
+    # the cold-start path); each child re-enables gc first thing
+    gc.disable()
     for mod in preload:
         importlib.import_module(mod)
         _PRELOADED.add(mod)
+    gc.freeze()
     import_s = time.perf_counter() - t0
     if _gpu_driver_open():
         print(f"[zygote] refusing to serve: preloading {preload} opened the GPU driver", flush=True)
