@@ -339,6 +339,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #define KFW4_ASM_DMA 1
 #endif
   static_assert(!KFW4_ASM_DMA || (KFW4_FASTK == 2 && KFW4_DMA_PHASE >= 1), "asm DMA: voffset regs, M0 set one MFMA ahead");
+  // stream-K keeps the round-3 steady state: its persistent schedule's live state plus these
+  // registers (voffsets, descriptors, the unrolled loop's constants) spill
+  constexpr int kFastK = SK ? 0 : KFW4_FASTK;
+  constexpr bool kAsmDma = !SK && KFW4_ASM_DMA;
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   // raw buffer descriptors as SGPR quads for the asm pieces (gfx9: base, base_hi | stride 0, records, word 3)
   auto make_desc = [&](const void* p) __attribute__((always_inline)) -> i32x4 {
@@ -350,7 +354,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const unsigned lds_w = (unsigned)(uintptr_t)KFW4_LDS_PTR(smem) + (unsigned)(wid * PIECES * 1024);  // wave's pieces
   // KFW4_FASTK == 2: piece j's full voffset (chunk swizzle + j rows) in a register of its own
   unsigned vpa[PIECES], vpb[PIECES];
-  if (KFW4_FASTK == 2) {
+  if (kFastK == 2) {
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
       vpa[j] = sta.voff[Stage<LA, BM>::variant_of_piece(j)] + (unsigned)(j * rs_a);
@@ -458,9 +462,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(r), "s"(so) : "memory");
     };
     auto stage_a = [&](int j) __attribute__((always_inline)) {
-      if (KFW4_ASM_DMA) {
+      if (kAsmDma) {
         asm_dma(dra, vpa[j], (kt + 2) * kts_a);
-      } else if (KFW4_FASTK == 2) {  // per-piece voffset registers, one soffset per K-tile
+      } else if (kFastK == 2) {  // per-piece voffset registers, one soffset per K-tile
         // plain locals as the builtin's operands (see the soffset note above dma_a)
         const unsigned v = vpa[j];
         const int so = (kt + 2) * kts_a;
@@ -470,9 +474,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       else dma_a(kt + 2, sf, j, false);
     };
     auto stage_b = [&](int j) __attribute__((always_inline)) {
-      if (KFW4_ASM_DMA) {
+      if (kAsmDma) {
         asm_dma(drb, vpb[j], (kt + 2) * kts_b);
-      } else if (KFW4_FASTK == 2) {
+      } else if (kFastK == 2) {
         const unsigned v = vpb[j];
         const int so = (kt + 2) * kts_b;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, KFW4_LDS_PTR(smem + sa0 * TILE + (wid * PIECES + j) * 1024), 16,
@@ -485,7 +489,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #pragma unroll
     for (int m = 0; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && m % RG == 0 && m / RG < 2 * NR) read_frag1(sa0, sb0, a1, b1, m / RG);
-      if (KFW4_ASM_DMA && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
+      if (kAsmDma && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
         m0_set(sf, (m + 1) / DMA_EVERY);
       if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) stage_a(m / DMA_EVERY);
       if (KFW4_PIN_MFMA) KFW4_PIN();
@@ -524,7 +528,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     for (int m = PB; m < MF; ++m) {
       if (!(DIAG && ABL == 2) && kNext && (m - PB) % RG == 0 && (m - PB) / RG < 2 * NR)
         read_frag0(sa1, sb1, a0, b0, (m - PB) / RG);
-      if (KFW4_ASM_DMA && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
+      if (kAsmDma && kStage && (m + 1) % DMA_EVERY == DMA_PHASE && (m + 1) / DMA_EVERY < PIECES)
         m0_set(sa0, (m + 1) / DMA_EVERY);
       if (kStage && m % DMA_EVERY == DMA_PHASE && m / DMA_EVERY < PIECES) stage_b(m / DMA_EVERY);
       if (KFW4_PIN_MFMA) KFW4_PIN();
@@ -565,7 +569,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   };
   if (DIAG) t_loop0 = stamp();
   int kt = 0;
-  if (KFW4_UNROLL5) {
+  if (KFW4_UNROLL5 && !SK) {  // (stream-K: the unrolled loop spills beside the persistent schedule's state)
     // the ring's period is 5 tiles: (sa0, sb0, sa1, sb1, sf) = (0,1,2,3,4) -> (2,3,4,0,1) -> (4,0,1,2,3)
     // -> (1,2,3,4,0) -> (3,4,0,1,2) -> (0,1,2,3,4); state 0 again after each group of five
     using C0 = std::integral_constant<int, 0>;
@@ -789,7 +793,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       const __bf16* b = B_in + (LB == 0 ? (long long)n0 * ldb + kofs : (long long)n0 + kofs * ldb);
       ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, (short)0, nrec, kRsrcWord3);
       rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, nrec, kRsrcWord3);
-      if (KFW4_ASM_DMA) {
+      if (kAsmDma) {
         dra = make_desc(a);
         drb = make_desc(b);
       }
