@@ -2,7 +2,9 @@
 // (+ R), A [M][K], B [N][K], on the 4-wave template of gemm_w4.h (256x256 tile "w4" or 128x128
 // "w4s"), with in-kernel edge tiles (any M, N >= the tile, N % 8, K % 8) and an optional second
 // output Aux = the pre-activation (gelu/silu backward without recomputing the GEMM).
-// The backward layouts live in gemm_bf16_w4_t.hip.
+// The backward layouts live in gemm_bf16_w4_t.hip; the kernels of each activation in
+// tu/w4_nt_<act>.hip and stream-K in gemm_bf16_w4_sk.hip (separate translation units that the
+// library build compiles in parallel). This file: the dispatcher, split-K partials + reduce, diag.
 //
 // History kept out of this file: profiles/r1_gemm_w4 (register placement: asm MFMA with tied AGPR
 // accumulators, buffer_load..lds with SGPR row offsets), profiles/r1_gemm_w4c (5-slot ring),
@@ -11,133 +13,36 @@
 
 using namespace kfw4;
 
-namespace {
-
-template <int BM>
-int launch_nt(const void* A, const void* B, void* C, const void* bias, const void* R, void* Aux, int M, int N, int K,
-              int batch, long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
-              long long sc, long long sr, float alpha, int act, void* stream) {
-  const int rc = check_shape(0, 0, BM, A, B, C, bias, R, Aux, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr);
-  if (rc != KFAMD_OK) return rc;
-  if (Aux && (act == KFAMD_ACT_NONE || R)) return KFAMD_EINVAL;
-  if (R && act != KFAMD_ACT_NONE) return KFAMD_EINVAL;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid(((M + BM - 1) / BM) * ((N + BM - 1) / BM), batch), block(kThreads);
-  const __bf16* a = static_cast<const __bf16*>(A);
-  const __bf16* b = static_cast<const __bf16*>(B);
-  __bf16* c = static_cast<__bf16*>(C);
-  const __bf16* bs = static_cast<const __bf16*>(bias);
-  const __bf16* r = static_cast<const __bf16*>(R);
-  __bf16* x = static_cast<__bf16*>(Aux);
-  const bool hb = bias != nullptr, hr = R != nullptr, hx = Aux != nullptr;
-#define W4_LAUNCH(ACTV, HB, HR, HX)                                                                                \
-  hipLaunchKernelGGL((gemm_w4<ACTV, HB, HR, HX, 0, 0, BM>), grid, block, 0, s, a, b, c, bs, r, x, M, N, K, lda, ldb, \
-                     ldc, ldr, sa, sb, sc, sr, alpha, nullptr)
-#define W4_ACT(ACTV)                                       \
-  if (hx) {                                                \
-    if (hb) W4_LAUNCH(ACTV, true, false, true);            \
-    else W4_LAUNCH(ACTV, false, false, true);              \
-  } else {                                                 \
-    if (hb) W4_LAUNCH(ACTV, true, false, false);           \
-    else W4_LAUNCH(ACTV, false, false, false);             \
-  }
-  switch (act) {
-    case KFAMD_ACT_NONE:
-      if (hb && hr) W4_LAUNCH(KFAMD_ACT_NONE, true, true, false);
-      else if (hb) W4_LAUNCH(KFAMD_ACT_NONE, true, false, false);
-      else if (hr) W4_LAUNCH(KFAMD_ACT_NONE, false, true, false);
-      else W4_LAUNCH(KFAMD_ACT_NONE, false, false, false);
-      break;
-    case KFAMD_ACT_RELU:
-      if (hx) return KFAMD_EINVAL;  // relu's backward needs only the output's sign
-      if (hb) W4_LAUNCH(KFAMD_ACT_RELU, true, false, false);
-      else W4_LAUNCH(KFAMD_ACT_RELU, false, false, false);
-      break;
-    case KFAMD_ACT_GELU_TANH:
-      W4_ACT(KFAMD_ACT_GELU_TANH);
-      break;
-    case KFAMD_ACT_SILU:
-      W4_ACT(KFAMD_ACT_SILU);
-      break;
-    default:
-      return KFAMD_EINVAL;
-  }
-#undef W4_ACT
-#undef W4_LAUNCH
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+#ifndef KFAMD_DIAG  // (the diagnostic library holds only the stamped kernel below)
+extern "C" {
+int kfw4_nt_none(int, const void*, const void*, void*, const void*, const void*, void*, int, int, int, int, long long,
+                 long long, long long, long long, long long, long long, long long, long long, float, void*);
+int kfw4_nt_relu(int, const void*, const void*, void*, const void*, const void*, void*, int, int, int, int, long long,
+                 long long, long long, long long, long long, long long, long long, long long, float, void*);
+int kfw4_nt_gelu(int, const void*, const void*, void*, const void*, const void*, void*, int, int, int, int, long long,
+                 long long, long long, long long, long long, long long, long long, long long, float, void*);
+int kfw4_nt_silu(int, const void*, const void*, void*, const void*, const void*, void*, int, int, int, int, long long,
+                 long long, long long, long long, long long, long long, long long, long long, float, void*);
 }
 
-}  // namespace
-
 // NT layout on the w4 template; bm = 256 ("w4") or 128 ("w4s"). Shapes/alignment: check_shape.
+// One translation unit per activation (tu/w4_nt_<act>.hip, launcher gemm_w4_nt.h).
 extern "C" int kfamd_w4_launch_nt(int bm, const void* A, const void* B, void* C, const void* bias, const void* R,
                                   void* Aux, int M, int N, int K, int batch, long long lda, long long ldb, long long ldc,
                                   long long ldr, long long sa, long long sb, long long sc, long long sr, float alpha,
                                   int act, void* stream) {
-  if (bm == 256)
-    return launch_nt<256>(A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, act, stream);
-  if (bm == 128)
-    return launch_nt<128>(A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, act, stream);
-  return KFAMD_EINVAL;
-}
-
-// Stream-K on the 256x256 tile (NT layout, batch 1): a persistent grid of `grid` blocks (one per CU)
-// runs the whole waves of tiles, then the remaining rem = tiles % grid tiles in `splits` K-splits
-// each, round-robin over all blocks (gemm_w4.h SK). W: (splits - 1) * rem partial tiles of 256 x 256
-// fp32; flags: splits * rem words, never holding `epoch` from an earlier call (the caller keeps one
-// buffer per stream and a strictly increasing epoch). Negative `splits`: every owner recomputes its
-// producers' splits after the deadline (tests of that path).
-extern "C" int kfamd_w4_streamk_nt(const void* A, const void* B, void* C, const void* bias, const void* R, void* Aux,
-                                   int M, int N, int K, long long lda, long long ldb, long long ldc, long long ldr,
-                                   float alpha, int act, float* W, unsigned* flags, unsigned epoch, int grid,
-                                   int splits, void* stream) {
-  const int rc = check_shape(0, 0, 256, A, B, C, bias, R, Aux, M, N, K, lda, ldb, ldc, ldr, 0, 0, 0, 0);
-  if (rc != KFAMD_OK) return rc;
-  if (!W || !flags || epoch == 0 || grid < 8 || grid > 4096) return KFAMD_EINVAL;
-  // no pre-activation output: the second output's registers push the persistent loop's accumulators
-  // into scratch (the Aux forward runs on the plain kernel)
-  if (Aux) return KFAMD_EINVAL;
-  if (R && act != KFAMD_ACT_NONE) return KFAMD_EINVAL;
-  if ((reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(flags) & 3)) return KFAMD_EALIGN;
-  // an owner tracks its producers in a 64-bit mask; every split holds at least one K-tile
-  const int KT = (K + kBK - 1) / kBK;
-  // (splits < 0: the deadline path's test mode, see gemm_w4.h)
-  const int S = splits < 0 ? -splits : splits;
-  if (S < 1 || S > 64 || S > KT) return KFAMD_EINVAL;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 g(grid), block(kThreads);
-  const __bf16* a = static_cast<const __bf16*>(A);
-  const __bf16* b = static_cast<const __bf16*>(B);
-  __bf16* c = static_cast<__bf16*>(C);
-  const __bf16* bs = static_cast<const __bf16*>(bias);
-  const __bf16* r = static_cast<const __bf16*>(R);
-  const bool hb = bias != nullptr, hr = R != nullptr;
-#define SK_LAUNCH(ACTV, HB, HR, HX)                                                                                  \
-  hipLaunchKernelGGL((gemm_w4<ACTV, HB, HR, HX, 0, 0, 256, false, false, 0, true>), g, block, 0, s, a, b, c, bs, r, \
-                     nullptr, M, N, K, lda, ldb, ldc, ldr, 0LL, 0LL, 0LL, 0LL, alpha, nullptr, W, splits, flags, epoch)
   switch (act) {
     case KFAMD_ACT_NONE:
-      if (hb && hr) SK_LAUNCH(KFAMD_ACT_NONE, true, true, false);
-      else if (hb) SK_LAUNCH(KFAMD_ACT_NONE, true, false, false);
-      else if (hr) SK_LAUNCH(KFAMD_ACT_NONE, false, true, false);
-      else SK_LAUNCH(KFAMD_ACT_NONE, false, false, false);
-      break;
-#define SK_ACT(ACTV)                                   \
-  case ACTV:                                           \
-    if (hb) SK_LAUNCH(ACTV, true, false, false);       \
-    else SK_LAUNCH(ACTV, false, false, false);         \
-    break;
-    SK_ACT(KFAMD_ACT_RELU)
-    SK_ACT(KFAMD_ACT_GELU_TANH)
-    SK_ACT(KFAMD_ACT_SILU)
+      return kfw4_nt_none(bm, A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, stream);
+    case KFAMD_ACT_RELU:
+      return kfw4_nt_relu(bm, A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, stream);
+    case KFAMD_ACT_GELU_TANH:
+      return kfw4_nt_gelu(bm, A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, stream);
+    case KFAMD_ACT_SILU:
+      return kfw4_nt_silu(bm, A, B, C, bias, R, Aux, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, stream);
     default:
       return KFAMD_EINVAL;
   }
-#undef SK_ACT
-#undef SK_LAUNCH
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
 
 // Split-K partials on the 128x128 w4s tile (NT layout): W[splits][batch][M][N] fp32, K range
@@ -265,6 +170,8 @@ extern "C" int kfamd_splitk_reduce(const float* W, void* C, const void* bias, co
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
+
+#endif  // !KFAMD_DIAG
 
 #ifdef KFAMD_DIAG
 // Diagnostic build only (libkfamd_kernels_diag.so, kubeflow_rm_amd._build.build_diag_kernels; never

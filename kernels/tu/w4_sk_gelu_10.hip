@@ -1,0 +1,4 @@
+// tu/w4_sk_gelu_10.hip — stream-K kernel: gelu epilogue, bias true, residual false (gemm_w4_sk.h).
+#include "gemm_w4_sk.h"
+
+KFW4_SK_ENTRY(kfw4_sk_gelu_10, KFAMD_ACT_GELU_TANH, true, false)

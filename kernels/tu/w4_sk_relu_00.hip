@@ -1,0 +1,4 @@
+// tu/w4_sk_relu_00.hip — stream-K kernel: relu epilogue, bias false, residual false (gemm_w4_sk.h).
+#include "gemm_w4_sk.h"
+
+KFW4_SK_ENTRY(kfw4_sk_relu_00, KFAMD_ACT_RELU, false, false)

@@ -72,8 +72,9 @@ def build_diag_kernels() -> Path:
 
 
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
-    """Compile kernels/*.hip for gfx950 and link libkfamd_kernels.so (incremental)."""
-    srcs = sorted(KERNEL_DIR.glob("*.hip"))
+    """Compile kernels/*.hip and kernels/tu/*.hip (one template variant per translation unit, so the
+    slow ones build in parallel) for gfx950 and link libkfamd_kernels.so (incremental)."""
+    srcs = sorted(KERNEL_DIR.glob("*.hip")) + sorted((KERNEL_DIR / "tu").glob("*.hip"))
     headers = sorted(KERNEL_DIR.glob("*.h"))
     obj_dir = BUILD_DIR / "kernels"
     obj_dir.mkdir(parents=True, exist_ok=True)
@@ -123,8 +124,9 @@ def check_object_kernels(src: Path, obj: Path) -> None:
     hipcc 7.2 can drop a TU's launch stubs AND its whole device bundle with exit status 0 (seen with
     a struct member as a buffer builtin's soffset, kernels/gemm_w4.h): catch it per object."""
     import re
-    if not re.search(r"^\s*(template\s*<[^;{]*>\s*)?__global__", src.read_text(), re.M) and \
-            "gemm_w4<" not in src.read_text():
+    text = src.read_text()
+    if not re.search(r"^\s*(template\s*<[^;{]*>\s*)?__global__", text, re.M) and \
+            not any(k in text for k in ("gemm_w4<", "KFW4_NT_ENTRY(", "KFW4_SK_ENTRY(")):
         return
     if not kernel_descriptors(obj):
         raise RuntimeError(f"{obj}: compiled from {src.name} but holds no gfx950 kernel descriptors "
@@ -136,6 +138,12 @@ def check_kernel_library(lib: Path) -> None:
     missing = [k for k in REQUIRED_KERNELS if not any(k in n for n in names)]
     if missing:
         raise RuntimeError(f"{lib}: no gfx950 kernel descriptors for {missing} ({len(names)} kernels found)")
+    # the other face of the dropped-stub bug: a host pass that lost a kernel's launch stub leaves an
+    # undefined __device_stub__ reference, and the library fails to load (gemm_w4.h FASTK notes)
+    nm = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], capture_output=True, text=True)
+    stubs = [ln.split()[-1] for ln in nm.stdout.splitlines() if "__device_stub__" in ln]
+    if stubs:
+        raise RuntimeError(f"{lib}: undefined kernel launch stubs (host pass dropped them): {stubs[:3]}")
 
 
 SANITIZER_CXX = "/opt/rocm/lib/llvm/bin/clang++"
