@@ -27,6 +27,7 @@ VARIANTS = {
     "base": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=0", "-DKFW4_ASM_DMA=0", "-DKFW4_PREBAR=0"],  # the round-3 K loop
     "unroll5": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1"],
     "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_ASM_DMA=0", "-DKFW4_PREBAR=0"],
+    "r4": [],  # the production knobs
     "asmdma": ["-DKFW4_ASM_DMA=1"],
     "prebar1": ["-DKFW4_PREBAR=1"],
     "prebar2": ["-DKFW4_PREBAR=2"],
@@ -119,16 +120,19 @@ def main():
                           "median_tf": {k: round(statistics.median(v), 1) for k, v in tf.items()},
                           "best_tf": {k: round(max(v), 1) for k, v in tf.items()}}), flush=True)
         del A, B, C, ref
-    for s in [int(x) for x in a.diag.split(",") if x]:
-        A = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
-        B = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
-        C = torch.empty(s, s, device=dev, dtype=torch.bfloat16)
-        nblk = (s // 256) ** 2
+    for spec in [x for x in a.diag.split(",") if x]:
+        # s (s^3) or MxNxK: e.g. 1024x1024x8192 puts 16 blocks on 16 CUs (no chip-wide store burst)
+        M_, N_, K_ = (int(v) for v in spec.split("x")) if "x" in spec else (int(spec),) * 3
+        A = (torch.rand(M_, K_, device=dev) * 2 - 1).to(torch.bfloat16)
+        B = (torch.rand(N_, K_, device=dev) * 2 - 1).to(torch.bfloat16)
+        C = torch.empty(M_, N_, device=dev, dtype=torch.bfloat16)
+        nblk = (M_ // 256) * (N_ // 256)
         diag = torch.zeros(nblk * 4 * 16, dtype=torch.int64, device=dev)
-        nk = s // 64
+        nk = K_ // 64
+        s = spec
         for n, L in libs.items():
             for _ in range(3):
-                assert L.w4ab_diag(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, diag.data_ptr(), st) == 0
+                assert L.w4ab_diag(A.data_ptr(), B.data_ptr(), C.data_ptr(), M_, N_, K_, diag.data_ptr(), st) == 0
             torch.cuda.synchronize()
             d = diag.view(nblk, 4, 16).double()
             seg = (d[..., :4].sum(dim=(0, 1)) / (nblk * 4 * (nk - 1))).tolist()  # cycles per 64-k tile
