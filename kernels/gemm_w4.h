@@ -760,12 +760,63 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       }
     }
   };
+  // Interior tiles without the second output: every 16-B store covers 8 WHOLE 128-B lines (8 rows x
+  // 64 columns, consecutive lanes on consecutive 16-B chunks of a row) instead of 16 half lines: the
+  // CU's store path takes those in ~72 % of the time (epilogue 8.2 k -> 5.9 k cycles with the store
+  // layout alone, profiles/r4_gemm_isa). After the permlane16 swap lane (lh, lr) holds row lr, 16 B at
+  // column swap_col(lh) of its block pair's 32-column span; the pairs (n, n+1) and (n+2, n+3) of one
+  // fragment row make a 16 x 64 span, which each wave stages in its own 2 KiB of the idle LDS ring
+  // (no wave reads the ring after the last tile's mid barrier) and reads back row-major. Row r's 16-B
+  // slot c sits at r * 128 + 16 * (c ^ ((r >> 1) & 7)): the writes (16 rows, one slot each per 16
+  // lanes) and the reads (two rows of 8 slots per 16 lanes) both cover 16 distinct bank quads.
+  auto emit_fullline = [&](auto UNIT) {
+    static_assert(NR % 4 == 0, "full-line stores: two block pairs per span");
+    char* stage = smem + wid * 2048;
+    // write side: this lane's row lr, slots ch(lh) (pair n) and 4 + ch(lh) (pair n+2); ch = 2*(lh&1) + (lh>>1)
+    const int ch = 2 * (elh & 1) + (elh >> 1);
+    const int wsw = (elr >> 1) & 7;
+    const int w0 = elr * 128 + 16 * (ch ^ wsw), w1 = elr * 128 + 16 * ((4 + ch) ^ wsw);
+    // read side: rows t/8 (X) and 8 + t/8 (Y), slot t % 8
+    const int rr = elane >> 3, rc = elane & 7;
+    const int r0 = rr * 128 + 16 * (rc ^ ((rr >> 1) & 7)), r1 = (rr + 8) * 128 + 16 * (rc ^ (((rr + 8) >> 1) & 7));
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = m0 + wm * WT + i * 16 + elr;
+      __bf16* xrow = C + ((long long)(m0 + wm * WT + i * 16 + rr) * ldc + n0 + wn * WT + rc * 8);
+#pragma unroll
+      for (int n = 0; n < NR; n += 4) {
+        uint4 d[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint2 pp{0, 0}, pq{0, 0};
+          const uint2 p = finish(T{}, UNIT, i, n + 2 * h, m, pp), q = finish(T{}, UNIT, i, n + 2 * h + 1, m, pq);
+          const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
+          d[h] = uint4{sx[0], sy[0], sx[1], sy[1]};
+        }
+        *reinterpret_cast<uint4*>(stage + w0) = d[0];
+        *reinterpret_cast<uint4*>(stage + w1) = d[1];
+        const uint4 X = *reinterpret_cast<const uint4*>(stage + r0);
+        const uint4 Y = *reinterpret_cast<const uint4*>(stage + r1);
+        *reinterpret_cast<uint4*>(xrow + n * 16) = X;
+        *reinterpret_cast<uint4*>(xrow + 8 * ldc + n * 16) = Y;
+      }
+    }
+  };
+#ifndef KFW4_FULLLINE
+#define KFW4_FULLLINE 1
+#endif
   // uniform branches: interior tiles store unmasked straight-line 16-B stores, shifted edge tiles
   // mask per lane, an odd output takes the og path; only the path that runs is fetched
   if (og == 8 && vec_in) {
     if (m0 == m_lo && n0 == n_lo) {
-      if (alpha == 1.f) emit(T{}, store_all, T{});
-      else emit(T{}, store_all, F{});
+      if constexpr (KFW4_FULLLINE && !HAS_AUX) {
+        if (alpha == 1.f) emit_fullline(T{});
+        else emit_fullline(F{});
+      } else {
+        if (alpha == 1.f) emit(T{}, store_all, T{});
+        else emit(T{}, store_all, F{});
+      }
     } else {
       emit(T{}, store16, F{});
     }

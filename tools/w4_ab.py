@@ -28,6 +28,7 @@ VARIANTS = {
     "unroll5": ["-DKFW4_FASTK=0", "-DKFW4_UNROLL5=1"],
     "f2u5": ["-DKFW4_FASTK=2", "-DKFW4_UNROLL5=1", "-DKFW4_ASM_DMA=0", "-DKFW4_PREBAR=0"],
     "r4": [],  # the production knobs
+    "noful": ["-DKFW4_FULLLINE=0"],  # the half-line epilogue stores
     "asmdma": ["-DKFW4_ASM_DMA=1"],
     "prebar1": ["-DKFW4_PREBAR=1"],
     "prebar2": ["-DKFW4_PREBAR=2"],
