@@ -760,7 +760,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       }
     }
   };
-  // Interior tiles without the second output: every 16-B store covers 8 WHOLE 128-B lines (8 rows x
+  // Interior tiles (C and the pre-activation output alike): every 16-B store covers 8 WHOLE 128-B lines (8 rows x
   // 64 columns, consecutive lanes on consecutive 16-B chunks of a row) instead of 16 half lines: the
   // CU's store path takes those in ~72 % of the time (epilogue 8.2 k -> 5.9 k cycles with the store
   // layout alone, profiles/r4_gemm_isa). After the permlane16 swap lane (lh, lr) holds row lr, 16 B at
@@ -785,7 +785,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       __bf16* xrow = C + ((long long)(m0 + wm * WT + i * 16 + rr) * ldc + n0 + wn * WT + rc * 8);
 #pragma unroll
       for (int n = 0; n < NR; n += 4) {
-        uint4 d[2];
+        uint4 d[2], x[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           uint2 pp{0, 0}, pq{0, 0};
@@ -793,13 +793,29 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
           const auto sx = __builtin_amdgcn_permlane16_swap(p.x, q.x, false, false);
           const auto sy = __builtin_amdgcn_permlane16_swap(p.y, q.y, false, false);
           d[h] = uint4{sx[0], sy[0], sx[1], sy[1]};
+          if (HAS_AUX) {
+            const auto ax = __builtin_amdgcn_permlane16_swap(pp.x, pq.x, false, false);
+            const auto ay = __builtin_amdgcn_permlane16_swap(pp.y, pq.y, false, false);
+            x[h] = uint4{ax[0], ay[0], ax[1], ay[1]};
+          }
         }
         *reinterpret_cast<uint4*>(stage + w0) = d[0];
         *reinterpret_cast<uint4*>(stage + w1) = d[1];
+        if (HAS_AUX) {  // the pre-activation output, through its own 2 KiB
+          *reinterpret_cast<uint4*>(stage + 8192 + w0) = x[0];
+          *reinterpret_cast<uint4*>(stage + 8192 + w1) = x[1];
+        }
         const uint4 X = *reinterpret_cast<const uint4*>(stage + r0);
         const uint4 Y = *reinterpret_cast<const uint4*>(stage + r1);
         *reinterpret_cast<uint4*>(xrow + n * 16) = X;
         *reinterpret_cast<uint4*>(xrow + 8 * ldc + n * 16) = Y;
+        if (HAS_AUX) {
+          const long long ao = (long long)(xrow - C);
+          const uint4 XA = *reinterpret_cast<const uint4*>(stage + 8192 + r0);
+          const uint4 YA = *reinterpret_cast<const uint4*>(stage + 8192 + r1);
+          *reinterpret_cast<uint4*>(Aux + ao + n * 16) = XA;
+          *reinterpret_cast<uint4*>(Aux + ao + 8 * ldc + n * 16) = YA;
+        }
       }
     }
   };
@@ -810,7 +826,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // mask per lane, an odd output takes the og path; only the path that runs is fetched
   if (og == 8 && vec_in) {
     if (m0 == m_lo && n0 == n_lo) {
-      if constexpr (KFW4_FULLLINE && !HAS_AUX) {
+      if constexpr (KFW4_FULLLINE) {
         if (alpha == 1.f) emit_fullline(T{});
         else emit_fullline(F{});
       } else {
