@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <type_traits>
 #include "kfamd_kernels.h"
+#include <cstdlib>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -545,9 +546,19 @@ namespace {
 // w4 tile choice: the 128x128 tile (two blocks per CU) when the problem has at most half as many
 // 256x256 tiles as MI355X has CUs, or a dimension below 256 (profiles/r1_gemm_w4s: 1024^3 92 -> 206
 // TF, 2048^3 430 -> 848; at 3072^3, 144 tiles, the 256 tile still wins 980 : 904).
+// 256-tile count up to which the 128 tile runs instead (2 blocks per CU); KFAMD_W4_TILE128_MAX
+// overrides it for A/B runs (read once)
+long long w4_tile128_max() {
+  static const long long v = [] {
+    const char* e = std::getenv("KFAMD_W4_TILE128_MAX");
+    return e && *e ? std::atoll(e) : 128LL;
+  }();
+  return v;
+}
+
 int w4_tile(int M, int N, int batch) {
   const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256) * batch;
-  return (t256 <= 128 || M < 256 || N < 256) ? 128 : 256;
+  return (t256 <= w4_tile128_max() || M < 256 || N < 256) ? 128 : 256;
 }
 }  // namespace
 

@@ -698,6 +698,34 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   if constexpr (SPLIT) {
     // raw fp32 partials, 4 consecutive columns per lane per block: W[z][m][n], ld N
     float* Wz = W + ((long long)blockIdx.z * gridDim.y + blockIdx.y) * (long long)M * N;
+#ifndef KFW4_FULLLINE
+#define KFW4_FULLLINE 1
+#endif
+    if (KFW4_FULLLINE && m0 == m_lo && n0 == n_lo) {
+      // interior tile: whole 128-B lines per store, as the bf16 epilogue below. A block pair (n, n+1)
+      // is 16 rows x 32 fp32; lane (lh, lr) holds row lr, 16 B at slot (n & 1) * 4 + lh; staged in the
+      // wave's 2 KiB of the idle ring (slot c of row r at r * 128 + 16 * (c ^ ((r >> 1) & 7))) and read
+      // back by rows (8 lanes per row)
+      char* stage = smem + wid * 2048;
+      const int wsw = (elr >> 1) & 7;
+      const int w0 = elr * 128 + 16 * (elh ^ wsw), w1 = elr * 128 + 16 * ((4 + elh) ^ wsw);
+      const int rr = elane >> 3, rc = elane & 7;
+      const int r0 = rr * 128 + 16 * (rc ^ ((rr >> 1) & 7)), r1 = (rr + 8) * 128 + 16 * (rc ^ (((rr + 8) >> 1) & 7));
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        float* wrow = Wz + (long long)(m0 + wm * WT + i * 16 + rr) * N + n0 + wn * WT + rc * 4;
+#pragma unroll
+        for (int n = 0; n < NR; n += 2) {
+          *reinterpret_cast<f32x4*>(stage + w0) = acc[i][n];
+          *reinterpret_cast<f32x4*>(stage + w1) = acc[i][n + 1];
+          const f32x4 X = *reinterpret_cast<const f32x4*>(stage + r0);
+          const f32x4 Y = *reinterpret_cast<const f32x4*>(stage + r1);
+          *reinterpret_cast<f32x4*>(wrow + n * 16) = X;
+          *reinterpret_cast<f32x4*>(wrow + 8LL * N + n * 16) = Y;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int m = m0 + wm * WT + i * 16 + elr;
