@@ -79,3 +79,39 @@ extern "C" int kfamd_w4_launch_t(int la, int lb, int bm, const void* A, const vo
 #undef W4T
   return KFAMD_EINVAL;
 }
+
+// the split-K fixup kernels, one operand layout per translation unit (kernels/tu/w4_fix_*.hip)
+extern "C" {
+#define KFW4_FIX_DECL(NAME)                                                                                        \
+  int NAME(const void*, const void*, void*, const void*, int, int, int, int, long long, long long, long long,      \
+           long long, long long, long long, long long, long long, float, float*, unsigned*, int, int, void*);
+KFW4_FIX_DECL(kfw4_fix_00)
+KFW4_FIX_DECL(kfw4_fix_11)
+KFW4_FIX_DECL(kfw4_fix_01)
+#undef KFW4_FIX_DECL
+}
+
+// Split-K with the in-kernel fixup on the 256x256 tile (gemm_w4.h SPLIT == 2): `splits` blocks per
+// tile over K ranges of kper (kper % 64 == 0, every split non-empty); the last block of each tile to
+// arrive adds the others' fp32 partials and runs the epilogue (alpha, optional residual R, which may
+// alias C). W: splits * batch * tiles partial tiles of 256 x 256 fp32 (16-B aligned); cnt: batch *
+// tiles arrival counters, zero on entry and left zero on exit (one buffer per stream).
+extern "C" int kfamd_w4_splitk_fix(int la, int lb, const void* A, const void* B, void* C, const void* R, int M, int N,
+                                   int K, int batch, long long lda, long long ldb, long long ldc, long long ldr,
+                                   long long sa, long long sb, long long sc, long long sr, float alpha, float* W,
+                                   unsigned* cnt, int splits, int kper, void* stream) {
+  const int rc = check_shape(la, lb, 256, A, B, C, nullptr, R, nullptr, M, N, K, lda, ldb, ldc, ldr, sa, sb, sc, sr);
+  if (rc != KFAMD_OK) return rc;
+  if (!W || !cnt || splits < 2 || splits > 64 || kper < kBK || kper % kBK || (long long)kper * (splits - 1) >= K)
+    return KFAMD_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(cnt) & 3)) return KFAMD_EALIGN;
+#define FIX(LA_, LB_)                                                                                              \
+  if (la == LA_ && lb == LB_)                                                                                      \
+    return kfw4_fix_##LA_##LB_(A, B, C, R, M, N, K, batch, lda, ldb, ldc, ldr, sa, sb, sc, sr, alpha, W, cnt, splits, \
+                               kper, stream);
+  FIX(0, 0)
+  FIX(1, 1)
+  FIX(0, 1)
+#undef FIX
+  return KFAMD_EINVAL;
+}

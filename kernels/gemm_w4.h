@@ -206,6 +206,13 @@ struct Reader {
 // SPLIT (split-K, for problems with too few output tiles to fill 256 CUs): blockIdx.z takes the K
 // range [z*kper, (z+1)*kper) and the block stores its raw fp32 partial tile to W[z][M][N]; the
 // epilogue (alpha, bias, activation, Aux, residual) runs in splitk_reduce (gemm_bf16.hip).
+// SPLIT == 2 (split-K with the fixup in the kernel, 256 tile, for tile counts well under the CU
+// count): the same K ranges, but every split block stores its fp32 partial in accumulator-fragment
+// order - wave w's f32x4 (i, n) for its 64 lanes is 1 KiB contiguous, so each store and load covers 8
+// whole 128-B lines - written through to the agent's coherence point (sc1), then counts itself in on
+// the tile's arrival counter (sk_flags[tile]). The block that arrives last adds the other splits'
+// partials to its accumulators, rearms the counter (0) and runs the full epilogue. Nobody waits on
+// anybody, so the grid needs no co-residency.
 // SK (stream-K, for grids that leave part of the last wave of 256 CUs idle): a persistent grid of
 // G = gridDim.x blocks (one per CU) first runs the whole data-parallel waves (tiles [0, T - T % G)),
 // then the remaining tiles in kper K-splits each, spread round-robin over all G blocks. The block
@@ -213,7 +220,7 @@ struct Reader {
 // released with an agent-scope flag = epoch) and runs the epilogue; a partial that does not arrive
 // within the deadline is recomputed by the owner itself, so a non-co-resident grid is slow, never
 // hung or wrong.
-template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, bool SPLIT = false,
+template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, int SPLIT = 0,
           bool DIAG = false, int ABL = 0, bool SK = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
@@ -252,7 +259,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(RG * (2 * NR - 1) < MF, "every fragment read inside its substep");
   static_assert(BM == 256 || BM == 128, "tile");
   static_assert(!HAS_AUX || ACT != KFAMD_ACT_NONE, "aux = pre-activation");
-  static_assert(!SPLIT || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
+  static_assert(SPLIT != 1 || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
+  static_assert(SPLIT != 2 || BM == 256, "split-K fixup: 256 tile");
   static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
   __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
@@ -695,7 +703,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     const bf16x2 hi = __builtin_convertvector((f32x2{v[2], v[3]}), bf16x2);
     return uint2{__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
   };
-  if constexpr (SPLIT) {
+  if constexpr (SPLIT == 1) {
     // raw fp32 partials, 4 consecutive columns per lane per block: W[z][m][n], ld N
     float* Wz = W + ((long long)blockIdx.z * gridDim.y + blockIdx.y) * (long long)M * N;
 #ifndef KFW4_FULLLINE
@@ -1051,6 +1059,60 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     return;
   }
   run_k();
+  if constexpr (SPLIT == 2) {
+    // ---- split-K fixup: publish this split's partial, the last split to arrive finishes the tile ----
+    const int el = lane_id_fresh();
+    const long long tile_id = (long long)blockIdx.y * nwg + wg;
+    constexpr long long kPerTile = (long long)BM * BN;  // floats
+    const long long zstride = (long long)gridDim.y * nwg * kPerTile;
+    const unsigned lane_off = (unsigned)(wid * (NR * NR * 1024) + el * 16);
+    {
+      __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(W + (long long)blockIdx.z * zstride + tile_id * kPerTile), (short)0, kNumRecords, kRsrcWord3);
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int n = 0; n < NR; ++n) {
+          i32x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float a;
+            asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][n][r]));
+            v[r] = __builtin_bit_cast(int, a);
+          }
+          // sc1: written through to the agent's coherence point, visible to a reader on another XCD
+          __builtin_amdgcn_raw_buffer_store_b128(v, rw, lane_off, (i * NR + n) * 1024, 16);
+        }
+    }
+    // this block's partial is complete at agent scope before it counts itself in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int* bc =
+        reinterpret_cast<volatile __attribute__((address_space(3))) int*>(KFW4_LDS_PTR(smem + kSlots * TILE - 16));
+    if (tid == 0) *bc = (int)__hip_atomic_fetch_add(sk_flags + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int arrived = __builtin_amdgcn_readfirstlane(*bc);
+    if (arrived != (int)gridDim.z - 1) return;
+    // last split: every other partial is in; rearm the counter for the next launch on this stream
+    if (tid == 0) __hip_atomic_store(sk_flags + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int z = 0; z < (int)gridDim.z; ++z) {
+      if (z == (int)blockIdx.z) continue;
+      __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(W + (long long)z * zstride + tile_id * kPerTile), (short)0, kNumRecords, kRsrcWord3);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        i32x4 t[NR];
+#pragma unroll
+        for (int n = 0; n < NR; ++n) t[n] = __builtin_amdgcn_raw_buffer_load_b128(rz, lane_off, (i * NR + n) * 1024, 16);
+#pragma unroll
+        for (int n = 0; n < NR; ++n) acc[i][n] += __builtin_bit_cast(f32x4, t[n]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+      for (int n = 0; n < NR; ++n) asm volatile("" : "+a"(acc[i][n]));
+  }
   epilogue();
   if (DIAG) {
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();

@@ -126,7 +126,7 @@ def check_object_kernels(src: Path, obj: Path) -> None:
     import re
     text = src.read_text()
     if not re.search(r"^\s*(template\s*<[^;{]*>\s*)?__global__", text, re.M) and \
-            not any(k in text for k in ("gemm_w4<", "KFW4_NT_ENTRY(", "KFW4_SK_ENTRY(")):
+            not any(k in text for k in ("gemm_w4<", "KFW4_NT_ENTRY(", "KFW4_SK_ENTRY(", "KFW4_FIX_ENTRY(")):
         return
     if not kernel_descriptors(obj):
         raise RuntimeError(f"{obj}: compiled from {src.name} but holds no gfx950 kernel descriptors "

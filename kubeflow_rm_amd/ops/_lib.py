@@ -33,6 +33,8 @@ _SIGNATURES = {
                                    c_ll, c_ll, c_vp]),
     "kfamd_w4_splitk_t": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_ll,
                                   c_ll, c_ll, c_ll, c_vp]),
+    "kfamd_w4_splitk_fix": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll,
+                                    c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_vp, c_vp, c_int, c_int, c_vp]),
     "kfamd_w4_streamk_nt": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll,
                                     c_float, c_int, c_vp, c_vp, ctypes.c_uint, c_int, c_int, c_vp]),
     "kfamd_splitk_reduce": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll,

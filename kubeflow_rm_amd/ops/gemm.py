@@ -151,6 +151,10 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, *, bias: torch.Tensor | None = Non
         r3 = residual.view(batch, M, N) if batched else residual.reshape(M, N)
         r_ptr, ldr = r3.data_ptr(), r3.stride(-2)
         sr = r3.stride(0) if batched else M * ldr
+    fx = (fixk_plan(M, N, K, batch) if variant == "auto" and bias is None and act == "none" else None)
+    if fx is not None and _fixk(0, 0, a3, b, c3, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, fx, r_ptr=r_ptr, ldr=ldr,
+                                sr=sr, alpha=alpha) == 0:
+        return out
     plan = splitk_plan(M, N, K, batch) if variant == "auto" else None
     if plan is not None and _splitk(0, 0, a3, b, c3, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, bias=bias,
                                     r_ptr=r_ptr, ldr=ldr, sr=sr, aux=None, alpha=alpha, act=act) == 0:
@@ -234,6 +238,67 @@ def _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *,
                                  float(alpha), ACTS[act], st)
 
 
+# Split-K with the in-kernel fixup (kfamd_w4_splitk_fix, gemm_w4.h SPLIT == 2): a problem with far
+# fewer 256x256 tiles than CUs (a weight gradient of a square projection: 2048^2 x 8192 is 64 tiles)
+# runs S K-splits per tile on the 256 tile; every split stores its fp32 partial in fragment order
+# (whole 128-B lines per store), the last split of a tile to arrive adds the others and runs the
+# epilogue. No reduce launch, no waiting, no co-residency assumption. FIXK_SPLITS pins S for A/B runs.
+FIXK = True
+FIXK_SPLITS: int | None = None
+_FIXK_MIN_KT = 32            # K-tiles (x64) per split: shallower splits are prologue / partial bound
+_FIXK_KT_CYC = 2300.0        # cycles per 64-k tile of the 256 kernel (profiles/r4_gemm_isa)
+_FIXK_UNIT_CYC = 3000.0      # prologue + epilogue share of a block
+_FIXK_PART_CYC = 13000.0     # one fp32 partial tile out of a CU (256 KiB through the store path)
+_FIXK_READ_CYC = 9000.0      # one partial tile read back by the owner
+_fixk_ws: dict = {}          # (device, stream) -> [W fp32 partials, arrival counters]
+
+
+def fixk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
+    """(splits, kper) for a 256-tile split-K fixup run of a problem with too few tiles, else None."""
+    if not FIXK or M < 256 or N < 256 or not _w4_shape(M, N, K):
+        return None
+    tiles = -(-M // 256) * -(-N // 256) * batch
+    kt = -(-K // 64)
+    if FIXK_SPLITS is not None:
+        best = FIXK_SPLITS
+    else:
+        # (below 32 tiles the 128-tile split-K above wins: profiles/r4_fixk)
+        if tiles > _NUM_CUS // 2 or tiles < 32:
+            return None
+
+        def cost(s):
+            rounds = -(-tiles * s // _NUM_CUS)
+            per = -(-kt // s) * _FIXK_KT_CYC + _FIXK_UNIT_CYC + (_FIXK_PART_CYC if s > 1 else 0.0)
+            return rounds * per + (s - 1) * _FIXK_READ_CYC
+        cands = [s for s in range(2, 17) if kt // s >= _FIXK_MIN_KT]
+        if not cands:
+            return None
+        best = min(cands, key=lambda s: (cost(s), s))
+        if cost(best) >= 0.8 * cost(1):
+            return None
+    if best < 2:
+        return None
+    kper = _round_up(-(-K // best), 64)
+    splits = -(-K // kper)
+    return (splits, kper) if splits >= 2 else None
+
+
+def _fixk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *, r_ptr, ldr, sr, alpha) -> int:
+    splits, kper = plan
+    tiles = -(-M // 256) * -(-N // 256) * batch
+    key = (a.device, _stream_ptr(a))
+    ws = _fixk_ws.get(key)
+    need_w = splits * tiles * 256 * 256
+    if ws is None or ws[0].numel() < need_w or ws[1].numel() < tiles:
+        old = (ws[0].numel(), ws[1].numel()) if ws is not None else (0, 0)
+        ws = [torch.empty(max(need_w, old[0]), dtype=torch.float32, device=a.device),
+              torch.zeros(max(tiles, old[1], 1024), dtype=torch.int32, device=a.device)]
+        _fixk_ws[key] = ws
+    return _lib.lib().kfamd_w4_splitk_fix(la, lb, a.data_ptr(), b.data_ptr(), c.data_ptr(), r_ptr, M, N, K, batch,
+                                          lda, ldb, ldc, ldr, sa, sb, sc, sr, float(alpha), ws[0].data_ptr(),
+                                          ws[1].data_ptr(), splits, kper, _stream_ptr(a))
+
+
 # Stream-K (kfamd_w4_streamk_nt, gemm_w4.h SK): a 256x256-tile problem whose tile count leaves the
 # last wave of 256 CUs partly idle (e.g. 144 tiles of 3072^2: 56 % of one wave) runs as a persistent
 # grid of one block per CU: the whole waves as plain tiles, then the leftover tiles in S K-splits
@@ -301,6 +366,10 @@ def _ex(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, *, bias=None
     r_ptr, ldr, sr = None, 0, 0
     if residual is not None:
         r_ptr, ldr, sr = residual.data_ptr(), residual.stride(-2), (residual.stride(0) if residual.dim() == 3 else 0)
+    fx = fixk_plan(M, N, K, batch) if bias is None and aux is None and act == "none" and (la, lb) != (1, 0) else None
+    if fx is not None and _fixk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, fx, r_ptr=r_ptr, ldr=ldr,
+                                sr=sr, alpha=alpha) == 0:
+        return 0
     plan = splitk_plan(M, N, K, batch)
     if plan is not None:
         rc = _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, bias=bias, r_ptr=r_ptr,

@@ -1,0 +1,32 @@
+"""GEMM launch plans (CPU: pure shape arithmetic in kubeflow_rm_amd.ops.gemm)."""
+from kubeflow_rm_amd.ops import gemm
+
+
+def test_fixk_plan_takes_few_tile_problems():
+    # 2048^2 x 8192 (a square projection's weight gradient): 64 tiles of 256 -> split along K
+    splits, kper = gemm.fixk_plan(2048, 2048, 8192)
+    assert splits >= 2 and kper % 64 == 0 and (splits - 1) * kper < 8192 <= splits * kper
+    assert 64 * splits <= gemm._NUM_CUS
+    # enough tiles to fill the chip, or too few for the 256 tile: other paths
+    assert gemm.fixk_plan(8192, 8192, 8192) is None
+    assert gemm.fixk_plan(6144, 2048, 8192) is None
+    assert gemm.fixk_plan(768, 768, 32768) is None
+    # shallow K: nothing to split
+    assert gemm.fixk_plan(2048, 2048, 1024) is None
+    # off the 8-element grid / below the tile
+    assert gemm.fixk_plan(2048, 2046, 8192) is None
+    assert gemm.fixk_plan(200, 4096, 8192) is None
+
+
+def test_fixk_plan_switches():
+    old = gemm.FIXK
+    try:
+        gemm.FIXK = False
+        assert gemm.fixk_plan(2048, 2048, 8192) is None
+    finally:
+        gemm.FIXK = old
+    gemm.FIXK_SPLITS = 3
+    try:
+        assert gemm.fixk_plan(8192, 8192, 8192) == (3, 2752)
+    finally:
+        gemm.FIXK_SPLITS = None

@@ -374,6 +374,53 @@ def test_splitk_batched_matches_unsplit():
     _assert_close(whole, ref, 4096)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 2048, 8192), (2000, 1800, 8200), (3072, 768, 32768)])
+def test_fixk_plan_and_numerics(M, N, K):
+    """Split-K with the in-kernel fixup (256 tile, the last split of each tile adds the others' fp32
+    partials): the plan takes it, every layout it runs (NT, wgrad TN-T, dgrad) matches fp32 and the
+    unsplit kernel, in-place accumulation (residual = out) works, and the arrival counters are back
+    to zero after every call."""
+    from kubeflow_rm_amd.ops import gemm, gemm_nt, mm
+    splits, kper = gemm.fixk_plan(M, N, K)
+    assert splits >= 2 and kper % 64 == 0 and (splits - 1) * kper < K <= splits * kper
+    a, b = _rand(M, K, seed=91), _rand(N, K, seed=92)
+    ref = _ref_gemm(a, b)
+    _assert_close(gemm_nt(a, b), ref, K)
+    for ta, tb in ((True, True), (False, True)):
+        aa = a.t().contiguous() if ta else a
+        bb = b if tb else b.t().contiguous()
+        out = mm(aa, bb, trans_a=ta, trans_b=tb)
+        _assert_close(out, _ref_mm(aa, bb, ta, tb), K)
+        gemm.FIXK = False
+        try:
+            whole = mm(aa, bb, trans_a=ta, trans_b=tb)
+        finally:
+            gemm.FIXK = True
+        err = (out.float() - whole.float()).abs().max().item()
+        assert err <= 1e-2 * (whole.float().abs().max().item() + 1e-3), err
+        ref2 = _ref_mm(aa, bb, ta, tb, alpha=0.5, residual=out)
+        mm(aa, bb, trans_a=ta, trans_b=tb, out=out, residual=out, alpha=0.5)
+        _assert_close(out, ref2, K)
+    torch.cuda.synchronize()
+    for w, cnt in gemm._fixk_ws.values():
+        assert int(cnt.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("S", [2, 3, 5, 16])
+def test_fixk_forced_splits_batched(S):
+    """Any split count, batched operands, repeated launches over the same workspace."""
+    from kubeflow_rm_amd.ops import gemm, mm
+    a, b = _rand(2, 4096, 512, seed=93), _rand(2, 4096, 768, seed=94)
+    gemm.FIXK_SPLITS = S
+    try:
+        assert gemm.fixk_plan(512, 768, 4096, 2)[0] == S
+        for _ in range(3):
+            out = mm(a, b, trans_a=True)
+            _assert_close(out, _ref_mm(a, b, True, False), 4096)
+    finally:
+        gemm.FIXK_SPLITS = None
+
+
 @pytest.fixture
 def streamk_on():
     from kubeflow_rm_amd.ops import gemm
