@@ -855,6 +855,70 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       }
     }
   };
+  // Interior tiles with a residual: the residual is read as whole lines too. The scattered 8-B
+  // fragment-order loads finish() makes touch 16 half-filled lines per instruction, and the load
+  // path is charged per line like the store path (an out-projection forward, K = 2048, spent ~40 k
+  // cycles outside its K loop, profiles/r4_train_trace). Here each wave stages alpha / bias /
+  // activation results as fp32 (a 16 x 64 span is 4 KiB: row r's 16-B chunk c at r * 256 +
+  // 16 * (c ^ r), so writes and reads both spread over all banks), reads them back row-major (8
+  // columns per lane), adds the residual loaded row-major (8 lanes per 128-B line; the loads are
+  // issued before the LDS round trip) in fp32 as finish() does, and stores whole lines.
+  auto pre_res = [&](auto UNIT, int i, int n) __attribute__((always_inline)) -> f32x4 {
+    const int col = n0 + wn * WT + n * 16 + elh * 4;
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a;
+      asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[i][n][r]));
+      v[r] = a;
+    }
+    if constexpr (!decltype(UNIT)::value) v *= alpha;
+    if (HAS_BIAS) {
+      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
+    }
+    if (ACT != KFAMD_ACT_NONE) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
+    }
+    return v;
+  };
+  auto emit_fullline_res = [&](auto UNIT) {
+    static_assert(NR % 4 == 0, "full-line stores: four blocks per span");
+    char* stage = smem + wid * 4096;
+    const int rr = elane >> 3, rc = elane & 7;
+    const int ra0 = rr * 256 + 16 * ((2 * rc) ^ rr), ra1 = rr * 256 + 16 * ((2 * rc + 1) ^ rr);
+    const int rb0 = (rr + 8) * 256 + 16 * ((2 * rc) ^ (rr + 8)), rb1 = (rr + 8) * 256 + 16 * ((2 * rc + 1) ^ (rr + 8));
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const long long row = m0 + wm * WT + i * 16 + rr;
+      __bf16* xrow = C + (row * ldc + n0 + wn * WT + rc * 8);
+      const __bf16* rrow = R + (row * ldr + n0 + wn * WT + rc * 8);
+#pragma unroll
+      for (int n = 0; n < NR; n += 4) {
+        const bf16x8 RX = *reinterpret_cast<const bf16x8*>(rrow + n * 16);
+        const bf16x8 RY = *reinterpret_cast<const bf16x8*>(rrow + 8 * ldr + n * 16);
+#pragma unroll
+        for (int nn = 0; nn < 4; ++nn)
+          *reinterpret_cast<f32x4*>(stage + elr * 256 + 16 * ((4 * nn + elh) ^ elr)) = pre_res(UNIT, i, n + nn);
+        const f32x4 xa = *reinterpret_cast<const f32x4*>(stage + ra0), xb = *reinterpret_cast<const f32x4*>(stage + ra1);
+        const f32x4 ya = *reinterpret_cast<const f32x4*>(stage + rb0), yb = *reinterpret_cast<const f32x4*>(stage + rb1);
+        bf16x8 X, Y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          X[r] = (__bf16)(xa[r] + (float)RX[r]);
+          X[4 + r] = (__bf16)(xb[r] + (float)RX[4 + r]);
+          Y[r] = (__bf16)(ya[r] + (float)RY[r]);
+          Y[4 + r] = (__bf16)(yb[r] + (float)RY[4 + r]);
+        }
+        *reinterpret_cast<bf16x8*>(xrow + n * 16) = X;
+        *reinterpret_cast<bf16x8*>(xrow + 8 * ldc + n * 16) = Y;
+      }
+    }
+  };
+  // the residual as 16-B rows (its own alignment; vec_in only asks for 8 B)
+  const bool res16 = HAS_RES && !(reinterpret_cast<uintptr_t>(HAS_RES ? R : nullptr) & 15) && !((ldr | sr) & 7);
 #ifndef KFW4_FULLLINE
 #define KFW4_FULLLINE 1
 #endif
@@ -862,7 +926,14 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // mask per lane, an odd output takes the og path; only the path that runs is fetched
   if (og == 8 && vec_in) {
     if (m0 == m_lo && n0 == n_lo) {
-      if constexpr (KFW4_FULLLINE) {
+      if constexpr (KFW4_FULLLINE && HAS_RES && !HAS_AUX && !SK) {  // (the stream-K owner adds partials in finish())
+        if (res16) {
+          if (alpha == 1.f) emit_fullline_res(T{});
+          else emit_fullline_res(F{});
+        } else {
+          emit(T{}, store_all, F{});
+        }
+      } else if constexpr (KFW4_FULLLINE) {
         if (alpha == 1.f) emit_fullline(T{});
         else emit_fullline(F{});
       } else {
@@ -1061,6 +1132,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   run_k();
   if constexpr (SPLIT == 2) {
     // ---- split-K fixup: publish this split's partial, the last split to arrive finishes the tile ----
+#ifndef KFW4_FIX_AB
+#define KFW4_FIX_AB 0  // timing ablations (tools/fix_ab.py builds): 1 no partial stores, 2 no partial reads, 4 no sc1
+#endif
+    constexpr int kFixPol = (KFW4_FIX_AB & 4) ? 0 : 16;  // sc1
     const int el = lane_id_fresh();
     const long long tile_id = (long long)blockIdx.y * nwg + wg;
     constexpr long long kPerTile = (long long)BM * BN;  // floats
@@ -1081,7 +1156,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
             v[r] = __builtin_bit_cast(int, a);
           }
           // sc1: written through to the agent's coherence point, visible to a reader on another XCD
-          __builtin_amdgcn_raw_buffer_store_b128(v, rw, lane_off, (i * NR + n) * 1024, 16);
+          if (!(KFW4_FIX_AB & 1)) __builtin_amdgcn_raw_buffer_store_b128(v, rw, lane_off, (i * NR + n) * 1024, kFixPol);
         }
     }
     // this block's partial is complete at agent scope before it counts itself in
@@ -1095,17 +1170,27 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     if (arrived != (int)gridDim.z - 1) return;
     // last split: every other partial is in; rearm the counter for the next launch on this stream
     if (tid == 0) __hip_atomic_store(sk_flags + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int z = 0; z < (int)gridDim.z; ++z) {
+    // one split at a time, two fragment rows of loads in flight (row i + 1 is requested before row i
+    // is added); the scheduling barriers keep the compiler from hoisting every row's loads at once,
+    // which spilled them to scratch behind vmcnt(0) waits
+    for (int z = 0; z < ((KFW4_FIX_AB & 2) ? 0 : (int)gridDim.z); ++z) {
       if (z == (int)blockIdx.z) continue;
       __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
           (void*)(W + (long long)z * zstride + tile_id * kPerTile), (short)0, kNumRecords, kRsrcWord3);
+      i32x4 t[2][NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) t[0][n] = __builtin_amdgcn_raw_buffer_load_b128(rz, lane_off, n * 1024, kFixPol);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        i32x4 t[NR];
+        if (i + 1 < NR) {
 #pragma unroll
-        for (int n = 0; n < NR; ++n) t[n] = __builtin_amdgcn_raw_buffer_load_b128(rz, lane_off, (i * NR + n) * 1024, 16);
+          for (int n = 0; n < NR; ++n)
+            t[(i + 1) & 1][n] = __builtin_amdgcn_raw_buffer_load_b128(rz, lane_off, ((i + 1) * NR + n) * 1024, kFixPol);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int n = 0; n < NR; ++n) acc[i][n] += __builtin_bit_cast(f32x4, t[n]);
+        for (int n = 0; n < NR; ++n) acc[i][n] += __builtin_bit_cast(f32x4, t[i & 1][n]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
