@@ -632,6 +632,13 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const bool vec_in = og >= 4 && !((reinterpret_cast<uintptr_t>(HAS_BIAS ? bias : nullptr) |
                                    reinterpret_cast<uintptr_t>(HAS_RES ? R : nullptr)) & 7) &&
                       !(HAS_RES && ((ldr | sr) & 3));
+  // the bias fragments of this lane's columns (n0 + wn*WT + 16n + 4lh; the same for every fragment
+  // row i), loaded once up front: eight loads in flight instead of one load and wait per fragment
+  bf16x4 bpre[NR];
+  if (HAS_BIAS && vec_in) {
+#pragma unroll
+    for (int n = 0; n < NR; ++n) bpre[n] = *reinterpret_cast<const bf16x4*>(bias + n0 + wn * WT + n * 16 + elh * 4);
+  }
   // VEC (compile time): bias / residual as 8-B vector loads (the fast path) or element loads
   // UNIT (compile time): alpha == 1, the scale is skipped (128 v_pk_mul_f32 per wave)
   auto finish = [&](auto VEC, auto UNIT, int i, int n, int m, uint2& pre_out) -> uint2 {
@@ -667,7 +674,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       if constexpr (!decltype(UNIT)::value) v[r] *= alpha;
     if (HAS_BIAS) {
       if constexpr (vec) {
-        const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+        const bf16x4 bb = bpre[n];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
       } else {
@@ -864,7 +871,6 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // columns per lane), adds the residual loaded row-major (8 lanes per 128-B line; the loads are
   // issued before the LDS round trip) in fp32 as finish() does, and stores whole lines.
   auto pre_res = [&](auto UNIT, int i, int n) __attribute__((always_inline)) -> f32x4 {
-    const int col = n0 + wn * WT + n * 16 + elh * 4;
     f32x4 v;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -874,7 +880,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
     if constexpr (!decltype(UNIT)::value) v *= alpha;
     if (HAS_BIAS) {
-      const bf16x4 bb = *reinterpret_cast<const bf16x4*>(bias + col);
+      const bf16x4 bb = bpre[n];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
     }

@@ -245,16 +245,18 @@ def _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *,
 # epilogue. No reduce launch, no waiting, no co-residency assumption. FIXK_SPLITS pins S for A/B runs.
 FIXK = True
 FIXK_SPLITS: int | None = None
-_FIXK_MIN_KT = 32            # K-tiles (x64) per split: shallower splits are prologue / partial bound
-_FIXK_KT_CYC = 2300.0        # cycles per 64-k tile of the 256 kernel (profiles/r4_gemm_isa)
-_FIXK_UNIT_CYC = 3000.0      # prologue + epilogue share of a block
-_FIXK_PART_CYC = 13000.0     # one fp32 partial tile out of a CU (256 KiB through the store path)
-_FIXK_READ_CYC = 9000.0      # one partial tile read back by the owner
+_FIXK_MIN_KT = 64            # K-tiles (x64) per split: shallower splits pay more for the partial than they save
 _fixk_ws: dict = {}          # (device, stream) -> [W fp32 partials, arrival counters]
 
 
 def fixk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
-    """(splits, kper) for a 256-tile split-K fixup run of a problem with too few tiles, else None."""
+    """(splits, kper) for a 256-tile split-K fixup run of a problem with too few tiles, else None.
+
+    Measured (profiles/r4_fixk): each split publishes a 256 KiB fp32 partial through the CU's store
+    path and the owner reads the others back (~8-15 us per split round), which pays only when every
+    split keeps >= 64 K-tiles and the splits fill >= 3/4 of the CUs: 4096x2048x8192 at 2 splits
+    106 us vs 115 on the 128 tile; 3072x768x32768 at 6 164 us vs 177 (128-tile split-K). 2048^2 x
+    8192 (64 tiles) stays on the 128 tile (65 us vs 70 at 4 splits, 87 at 2)."""
     if not FIXK or M < 256 or N < 256 or not _w4_shape(M, N, K):
         return None
     tiles = -(-M // 256) * -(-N // 256) * batch
@@ -262,19 +264,10 @@ def fixk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
     if FIXK_SPLITS is not None:
         best = FIXK_SPLITS
     else:
-        # (below 32 tiles the 128-tile split-K above wins: profiles/r4_fixk)
-        if tiles > _NUM_CUS // 2 or tiles < 32:
+        if tiles < 32 or tiles > _NUM_CUS // 2:
             return None
-
-        def cost(s):
-            rounds = -(-tiles * s // _NUM_CUS)
-            per = -(-kt // s) * _FIXK_KT_CYC + _FIXK_UNIT_CYC + (_FIXK_PART_CYC if s > 1 else 0.0)
-            return rounds * per + (s - 1) * _FIXK_READ_CYC
-        cands = [s for s in range(2, 17) if kt // s >= _FIXK_MIN_KT]
-        if not cands:
-            return None
-        best = min(cands, key=lambda s: (cost(s), s))
-        if cost(best) >= 0.8 * cost(1):
+        best = min(_NUM_CUS // tiles, kt // _FIXK_MIN_KT)
+        if best < 2 or tiles * best < _NUM_CUS * 3 // 4:
             return None
     if best < 2:
         return None

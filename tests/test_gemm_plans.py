@@ -3,10 +3,14 @@ from kubeflow_rm_amd.ops import gemm
 
 
 def test_fixk_plan_takes_few_tile_problems():
-    # 2048^2 x 8192 (a square projection's weight gradient): 64 tiles of 256 -> split along K
-    splits, kper = gemm.fixk_plan(2048, 2048, 8192)
-    assert splits >= 2 and kper % 64 == 0 and (splits - 1) * kper < 8192 <= splits * kper
-    assert 64 * splits <= gemm._NUM_CUS
+    # 4096x2048x8192: 128 tiles of 256 -> two K-splits fill the 256 CUs, 64 K-tiles each
+    assert gemm.fixk_plan(4096, 2048, 8192) == (2, 4096)
+    # a deep-K gpt-small weight gradient: 36 tiles, 7 splits
+    splits, kper = gemm.fixk_plan(3072, 768, 32768)
+    assert splits == 7 and kper % 64 == 0 and (splits - 1) * kper < 32768 <= splits * kper
+    assert 36 * splits <= gemm._NUM_CUS
+    # 64 tiles with 128 K-tiles: two splits would fill half the chip; the 128 tile does better
+    assert gemm.fixk_plan(2048, 2048, 8192) is None
     # enough tiles to fill the chip, or too few for the 256 tile: other paths
     assert gemm.fixk_plan(8192, 8192, 8192) is None
     assert gemm.fixk_plan(6144, 2048, 8192) is None

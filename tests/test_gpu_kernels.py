@@ -374,7 +374,7 @@ def test_splitk_batched_matches_unsplit():
     _assert_close(whole, ref, 4096)
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 2048, 8192), (2000, 1800, 8200), (3072, 768, 32768)])
+@pytest.mark.parametrize("M,N,K", [(4096, 2048, 8192), (4000, 1800, 8200), (3072, 768, 32768)])
 def test_fixk_plan_and_numerics(M, N, K):
     """Split-K with the in-kernel fixup (256 tile, the last split of each tile adds the others' fp32
     partials): the plan takes it, every layout it runs (NT, wgrad TN-T, dgrad) matches fp32 and the
