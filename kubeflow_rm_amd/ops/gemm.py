@@ -245,18 +245,21 @@ def _splitk(la, lb, a, b, c, M, N, K, batch, lda, ldb, ldc, sa, sb, sc, plan, *,
 # epilogue. No reduce launch, no waiting, no co-residency assumption. FIXK_SPLITS pins S for A/B runs.
 FIXK = True
 FIXK_SPLITS: int | None = None
-_FIXK_MIN_KT = 64            # K-tiles (x64) per split: shallower splits pay more for the partial than they save
+_FIXK_MIN_KT = 32            # K-tiles (x64) per split: shallower splits pay more for the partial than they save
+_FIXK_MAX = 7
 _fixk_ws: dict = {}          # (device, stream) -> [W fp32 partials, arrival counters]
 
 
 def fixk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
     """(splits, kper) for a 256-tile split-K fixup run of a problem with too few tiles, else None.
 
-    Measured (profiles/r4_fixk): each split publishes a 256 KiB fp32 partial through the CU's store
-    path and the owner reads the others back (~8-15 us per split round), which pays only when every
-    split keeps >= 64 K-tiles and the splits fill >= 3/4 of the CUs: 4096x2048x8192 at 2 splits
-    106 us vs 115 on the 128 tile; 3072x768x32768 at 6 164 us vs 177 (128-tile split-K). 2048^2 x
-    8192 (64 tiles) stays on the 128 tile (65 us vs 70 at 4 splits, 87 at 2)."""
+    Measured against the previous plans (profiles/r4_fixk/fixk.jsonl; hot = operands cache-resident,
+    cold = after a 512 MiB eviction): each split publishes a 256 KiB fp32 partial through the CU's
+    store path and the owner reads the others back, which pays when every split keeps >= 32 K-tiles
+    and the splits fill >= 70 % of the CUs: 2048^2 x 8192 at 4 splits 69.0 / 86.4 us vs 69.5 / 106.0
+    on the 128 tile; 4096x2048x8192 at 2 104.8 / 115.5 vs 116.9 / 140.3; 3072x768x32768 at 7
+    152.6 / 164.2 vs 179.6 / 222.9 (128-tile split-K); 2304x768x32768 at 7 113.9 / 151.6 vs
+    127.6 / 170.4. More than 7 splits lose (the owner reads every partial)."""
     if not FIXK or M < 256 or N < 256 or not _w4_shape(M, N, K):
         return None
     tiles = -(-M // 256) * -(-N // 256) * batch
@@ -264,10 +267,10 @@ def fixk_plan(M: int, N: int, K: int, batch: int = 1) -> tuple[int, int] | None:
     if FIXK_SPLITS is not None:
         best = FIXK_SPLITS
     else:
-        if tiles < 32 or tiles > _NUM_CUS // 2:
+        if tiles < 24 or tiles > _NUM_CUS // 2:
             return None
-        best = min(_NUM_CUS // tiles, kt // _FIXK_MIN_KT)
-        if best < 2 or tiles * best < _NUM_CUS * 3 // 4:
+        best = min(_NUM_CUS // tiles, kt // _FIXK_MIN_KT, _FIXK_MAX)
+        if best < 2 or tiles * best < _NUM_CUS * 7 // 10:
             return None
     if best < 2:
         return None

@@ -9,12 +9,14 @@ def test_fixk_plan_takes_few_tile_problems():
     splits, kper = gemm.fixk_plan(3072, 768, 32768)
     assert splits == 7 and kper % 64 == 0 and (splits - 1) * kper < 32768 <= splits * kper
     assert 36 * splits <= gemm._NUM_CUS
-    # 64 tiles with 128 K-tiles: two splits would fill half the chip; the 128 tile does better
-    assert gemm.fixk_plan(2048, 2048, 8192) is None
+    # a square projection's weight gradient, 64 tiles: four splits of 32 K-tiles
+    assert gemm.fixk_plan(2048, 2048, 8192) == (4, 2048)
+    # 32 K-tiles in all: nothing to split
+    assert gemm.fixk_plan(2048, 2048, 2048) is None
     # enough tiles to fill the chip, or too few for the 256 tile: other paths
     assert gemm.fixk_plan(8192, 8192, 8192) is None
     assert gemm.fixk_plan(6144, 2048, 8192) is None
-    assert gemm.fixk_plan(768, 768, 32768) is None
+    assert gemm.fixk_plan(768, 768, 32768) is None  # 9 tiles: the 128-tile split-K
     # shallow K: nothing to split
     assert gemm.fixk_plan(2048, 2048, 1024) is None
     # off the 8-element grid / below the tile
