@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r4_proftrain
+OUT=$R/gpurun_out/${PROF_OUT:-r4_proftrain}
 mkdir -p $OUT
 for b in native torch; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$b -o run -- python3 $R/tools/prof_train.py $b gpt-1b 4 2048 > $OUT/$b.log 2>&1 || exit $?

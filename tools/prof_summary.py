@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarize tools/gpu_prof_gemm.sh output: per kernel, counter means, mean dispatch time, effective clock."""
+"""Summarize tools/runs/gpu_prof_gemm.sh output: per kernel, counter means, mean dispatch time, effective clock."""
 import collections
 import csv
 import sys
