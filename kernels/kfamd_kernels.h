@@ -102,6 +102,11 @@ int kfamd_pad_k_bf16(const void* src0, void* dst0, long long rows0, long long ld
 long long kfamd_act_grad_workspace(int rows, int cols);
 // y = act(z) elementwise (n % 8 == 0, 16-B aligned): the forward activation as its own pass
 int kfamd_act_fwd_bf16(const void* z, void* y, long long n, int act, void* stream);
+// attention backward: dq / dk / dv [B][H][T][D] (strided) packed into the fused QKV gradient
+// [B][T][3][H][D] in one pass (kernels/qkv_pack_bf16.hip)
+int kfamd_qkv_pack_bf16(const void* dq, const void* dk, const void* dv, void* out, int B, int T, int H, int D,
+                        long long qb, long long qh, long long qt, long long kb, long long kh, long long kt,
+                        long long vb, long long vh, long long vt, void* stream);
 int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows, int cols,
                         int act, void* stream);
 

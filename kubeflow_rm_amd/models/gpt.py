@@ -18,6 +18,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
+from kubeflow_rm_amd import ops
 from kubeflow_rm_amd.parallel import tp as tpl
 
 
@@ -109,7 +110,7 @@ class Block(torch.nn.Module):
         B, T, _ = x.shape
         h, hd = self.local_heads, self.cfg.head_dim
         qkv = self.qkv(x)  # [B, T, 3 * h * hd] — the column shard is [q_h | k_h | v_h] per rank
-        q, k, v = qkv.view(B, T, 3, h, hd).permute(2, 0, 3, 1, 4)
+        q, k, v = ops.split_heads(qkv, h, hd)  # backward: one pass into the QKV gradient layout
         y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return self.proj(y.transpose(1, 2).reshape(B, T, h * hd), residual=residual)
 

@@ -41,6 +41,8 @@ _SIGNATURES = {
                                     c_ll, c_float, c_int, c_vp]),
     "kfamd_pad_k_bf16": (c_int, [c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_vp]),
     "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
+    "kfamd_qkv_pack_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll,
+                                    c_ll, c_ll, c_ll, c_ll, c_vp]),
     "kfamd_act_fwd_bf16": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp]),
     "kfamd_xent_fwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp]),
     "kfamd_xent_bwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp]),

@@ -619,3 +619,31 @@ def test_cross_entropy_matches_fp32(rows, V):
     assert abs(loss.item() - ref.item()) <= 1e-3 * abs(ref.item()) + 1e-3, (loss.item(), ref.item())
     err = (x.grad.float() - xr.grad).abs().max().item()
     assert err <= 1e-2 * xr.grad.abs().max().item() + 1e-6, err
+
+
+@pytest.mark.parametrize("B,T,h,hd", [(2, 256, 4, 64), (1, 100, 3, 128)])
+def test_split_heads_backward_packs_qkv_grad(B, T, h, hd):
+    """ops.split_heads: the same q / k / v views as view + permute, and a backward (the HIP pack of
+    SDPA's dq / dk / dv into the fused QKV gradient) bitwise equal to autograd's own."""
+    from kubeflow_rm_amd import ops
+    qkv = _rand(B, T, 3 * h * hd, seed=95).requires_grad_(True)
+    ref = qkv.detach().clone().requires_grad_(True)
+    q, k, v = ops.split_heads(qkv, h, hd)
+    qr, kr, vr = ref.view(B, T, 3, h, hd).permute(2, 0, 3, 1, 4)
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        assert a.shape == b.shape and torch.equal(a, b)
+    F = torch.nn.functional
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    yr = F.scaled_dot_product_attention(qr, kr, vr, is_causal=True)
+    g = _rand(*y.shape, seed=96)
+    y.backward(g)
+    yr.backward(g)
+    assert torch.equal(qkv.grad, ref.grad)
+    # a gradient autograd does not produce (v unused) packs zeros
+    qkv.grad = None
+    q, k, v = ops.split_heads(qkv, h, hd)
+    (q.float().sum() + 2 * k.float().sum()).backward()
+    gq = qkv.grad.view(B, T, 3, h, hd)
+    assert torch.equal(gq[:, :, 0], torch.ones_like(gq[:, :, 0]))
+    assert torch.equal(gq[:, :, 1], torch.full_like(gq[:, :, 1], 2))
+    assert not gq[:, :, 2].any()
