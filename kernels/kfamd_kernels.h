@@ -102,6 +102,11 @@ int kfamd_pad_k_bf16(const void* src0, void* dst0, long long rows0, long long ld
 long long kfamd_act_grad_workspace(int rows, int cols);
 // y = act(z) elementwise (n % 8 == 0, 16-B aligned): the forward activation as its own pass
 int kfamd_act_fwd_bf16(const void* z, void* y, long long n, int act, void* stream);
+// multi-tensor AdamW over bf16 params / grads / moments, one launch per step (kernels/adamw_bf16.hip)
+int kfamd_adamw_tensor_bytes(void);
+int kfamd_adamw_chunk(void);
+int kfamd_adamw_bf16(const void* table, int ntensors, long long nchunks, float lr, float b1, float b2, float eps,
+                     float wd, float step_size, float inv_sqrt_bc2, void* stream);
 // attention backward: dq / dk / dv [B][H][T][D] (strided) packed into the fused QKV gradient
 // [B][T][3][H][D] in one pass (kernels/qkv_pack_bf16.hip)
 int kfamd_qkv_pack_bf16(const void* dq, const void* dk, const void* dv, void* out, int B, int T, int H, int D,

@@ -41,6 +41,10 @@ _SIGNATURES = {
                                     c_ll, c_float, c_int, c_vp]),
     "kfamd_pad_k_bf16": (c_int, [c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_ll, c_ll, c_int, c_int, c_vp]),
     "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
+    "kfamd_adamw_tensor_bytes": (c_int, []),
+    "kfamd_adamw_chunk": (c_int, []),
+    "kfamd_adamw_bf16": (c_int, [c_vp, c_int, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float,
+                                 c_vp]),
     "kfamd_qkv_pack_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll,
                                     c_ll, c_ll, c_ll, c_ll, c_vp]),
     "kfamd_act_fwd_bf16": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp]),

@@ -16,7 +16,11 @@ def main():
     B, T = (int(sys.argv[3]) if len(sys.argv) > 3 else 4), (int(sys.argv[4]) if len(sys.argv) > 4 else 2048)
     dev = torch.device("cuda", 0)
     m = gpt.build(name, device=dev)
-    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, fused=True)
+    if which == "torch":
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-4, fused=True)
+    else:
+        from kubeflow_rm_amd.optim import AdamW
+        opt = AdamW(m.parameters(), lr=1e-4)
     idx = torch.randint(0, m.cfg.vocab_size, (B, T), device=dev)
     ctx = ops.torch_reference() if which == "torch" else open("/dev/null")
     with ctx:

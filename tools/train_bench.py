@@ -2,7 +2,8 @@
 """GPT training step on one MI355X: the framework's kernels vs plain torch ops on the same model.
 
 One step = forward + backward + AdamW update of kubeflow_rm_amd.models.gpt (bf16 weights and
-activations, fused AdamW), on synthetic tokens. ``--backend native`` runs the projections on the
+activations), on synthetic tokens; native steps with kubeflow_rm_amd.optim.AdamW (one HIP launch),
+torch with torch's fused AdamW. ``--backend native`` runs the projections on the
 w4 MFMA GEMM (bias / GELU / residual epilogues, pre-activation output, fused act-grad, transposed
 backward layouts) and LayerNorm on the wave-per-row kernel; ``--backend torch`` runs the same model
 inside ``ops.torch_reference()`` (F.linear / F.layer_norm: hipBLASLt + torch's LayerNorm). Both use
@@ -37,7 +38,10 @@ def main():
 
     dev = torch.device("cuda", 0)
     model = gpt.build(args.model, device=dev)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)
+    # native: the framework's multi-tensor AdamW kernel; torch: torch's fused AdamW (separate moments)
+    from kubeflow_rm_amd.optim import AdamW
+    opts = {"native": AdamW(model.parameters(), lr=1e-4),
+            "torch": torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)}
     g = torch.Generator(device=dev).manual_seed(0)
     V = model.cfg.vocab_size
     idx = torch.randint(0, V, (args.batch, args.seq), generator=g, device=dev)
@@ -45,7 +49,7 @@ def main():
     tokens = args.batch * args.seq
     fpt = model.flops_per_token(args.seq)
 
-    def step():
+    def step(opt):
         opt.zero_grad(set_to_none=True)
         _, loss = model(idx, tgt)
         loss.backward()
@@ -56,11 +60,11 @@ def main():
         ctx = ops.torch_reference() if backend == "torch" else _null()
         with ctx:
             for _ in range(args.warmup):
-                step()
+                step(opts[backend])
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             for _ in range(n):
-                loss = step()
+                loss = step(opts[backend])
             torch.cuda.synchronize(dev)
             return (time.perf_counter() - t0) / n, float(loss.item())
 
