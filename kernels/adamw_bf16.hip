@@ -26,17 +26,11 @@ struct AdamWTensor {  // 48 bytes, host-written (kfamd_adamw_tensor_bytes)
 
 constexpr int kChunk = 8 * 256 * 8;  // elements per block: 8 steps of 8 elements per thread
 
-__global__ __launch_bounds__(256) void adamw(const AdamWTensor* __restrict__ tab, int ntensors, float lr, float b1,
-                                             float b2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
-  // tensor of this block: the last t with chunk0 <= blockIdx.x
-  int lo = 0, hi = ntensors - 1;
+__global__ __launch_bounds__(256) void adamw(const AdamWTensor* __restrict__ tab, const int* __restrict__ owner,
+                                             float lr, float b1, float b2, float eps, float wd, float step_size,
+                                             float inv_sqrt_bc2) {
   const long long cb = blockIdx.x;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab[mid].chunk0 <= cb) lo = mid;
-    else hi = mid - 1;
-  }
-  const AdamWTensor t = tab[lo];
+  const AdamWTensor t = tab[owner[cb]];  // the tensor this chunk belongs to (host-built map)
   const long long base = (cb - t.chunk0) * kChunk;
   const long long end = min(t.n, base + kChunk);
   const float decay = 1.f - lr * wd;
@@ -91,14 +85,16 @@ __global__ __launch_bounds__(256) void adamw(const AdamWTensor* __restrict__ tab
 extern "C" int kfamd_adamw_tensor_bytes() { return (int)sizeof(AdamWTensor); }
 extern "C" int kfamd_adamw_chunk() { return kChunk; }
 
-// one AdamW step over every tensor of a device-resident table; nchunks = the table's total chunks.
+// one AdamW step over every tensor of a device-resident table; nchunks = the table's total chunks,
 // step_size = lr / (1 - b1^t), inv_sqrt_bc2 = 1 / sqrt(1 - b2^t).
-extern "C" int kfamd_adamw_bf16(const void* table, int ntensors, long long nchunks, float lr, float b1, float b2,
+// owner: nchunks int32, the table row of each chunk.
+extern "C" int kfamd_adamw_bf16(const void* table, const void* owner, long long nchunks, float lr, float b1, float b2,
                                 float eps, float wd, float step_size, float inv_sqrt_bc2, void* stream) {
-  if (!table || ntensors <= 0 || nchunks <= 0 || nchunks > 0x7fffffffLL) return KFAMD_EINVAL;
-  if (reinterpret_cast<uintptr_t>(table) & 15) return KFAMD_EALIGN;
+  if (!table || !owner || nchunks <= 0 || nchunks > 0x7fffffffLL) return KFAMD_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(table) & 15) || (reinterpret_cast<uintptr_t>(owner) & 3)) return KFAMD_EALIGN;
   hipLaunchKernelGGL(adamw, dim3((unsigned)nchunks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const AdamWTensor*>(table), ntensors, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+                     static_cast<const AdamWTensor*>(table), static_cast<const int*>(owner), lr, b1, b2, eps, wd,
+                     step_size, inv_sqrt_bc2);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }

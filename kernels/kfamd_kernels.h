@@ -105,7 +105,7 @@ int kfamd_act_fwd_bf16(const void* z, void* y, long long n, int act, void* strea
 // multi-tensor AdamW over bf16 params / grads / moments, one launch per step (kernels/adamw_bf16.hip)
 int kfamd_adamw_tensor_bytes(void);
 int kfamd_adamw_chunk(void);
-int kfamd_adamw_bf16(const void* table, int ntensors, long long nchunks, float lr, float b1, float b2, float eps,
+int kfamd_adamw_bf16(const void* table, const void* owner, long long nchunks, float lr, float b1, float b2, float eps,
                      float wd, float step_size, float inv_sqrt_bc2, void* stream);
 // attention backward: dq / dk / dv [B][H][T][D] (strided) packed into the fused QKV gradient
 // [B][T][3][H][D] in one pass (kernels/qkv_pack_bf16.hip)

@@ -43,7 +43,7 @@ _SIGNATURES = {
     "kfamd_act_grad_workspace": (c_ll, [c_int, c_int]),
     "kfamd_adamw_tensor_bytes": (c_int, []),
     "kfamd_adamw_chunk": (c_int, []),
-    "kfamd_adamw_bf16": (c_int, [c_vp, c_int, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float,
+    "kfamd_adamw_bf16": (c_int, [c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float,
                                  c_vp]),
     "kfamd_qkv_pack_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll,
                                     c_ll, c_ll, c_ll, c_ll, c_vp]),

@@ -73,20 +73,21 @@ class AdamW(torch.optim.Optimizer):
         key = tuple(ptrs)
         cached = self._tables.get((dev, gi))
         if cached is None or cached[0] != key:
-            rows, c0 = [], 0
-            for pp, gp, mp, vp, n in ptrs:
+            rows, owner, c0 = [], [], 0
+            for i, (pp, gp, mp, vp, n) in enumerate(ptrs):
                 rows.append([pp, gp, mp, vp, n, c0])
-                c0 += -(-n // chunk)
+                nc = -(-n // chunk)
+                owner.append(torch.full((nc,), i, dtype=torch.int32))
+                c0 += nc
             assert L.kfamd_adamw_tensor_bytes() == 48
-            host = torch.tensor(rows, dtype=torch.int64).pin_memory() if torch.cuda.is_available() else \
-                torch.tensor(rows, dtype=torch.int64)
-            table = host.to(dev, non_blocking=True)
-            cached = (key, table, len(rows), c0, host)
+            host = (torch.tensor(rows, dtype=torch.int64).pin_memory(), torch.cat(owner).pin_memory())
+            table, own = host[0].to(dev, non_blocking=True), host[1].to(dev, non_blocking=True)
+            cached = (key, (table, own), len(rows), c0, host)
             self._tables[(dev, gi)] = cached
-        _, table, ntens, nchunks, _ = cached
+        _, (table, own), _, nchunks, _ = cached
         step_size = lr / (1.0 - b1 ** t)
         inv_sqrt_bc2 = 1.0 / math.sqrt(1.0 - b2 ** t)
-        rc = L.kfamd_adamw_bf16(table.data_ptr(), ntens, nchunks, float(lr), float(b1), float(b2), float(eps),
+        rc = L.kfamd_adamw_bf16(table.data_ptr(), own.data_ptr(), nchunks, float(lr), float(b1), float(b2), float(eps),
                                 float(wd), float(step_size), float(inv_sqrt_bc2),
                                 torch.cuda.current_stream(dev).cuda_stream)
         _lib.check(rc, "adamw")
