@@ -34,15 +34,17 @@ def test_rejects_bad_hyperparameters():
 @pytest.mark.gpu
 def test_bf16_cuda_kernel_matches_reference():
     """Odd sizes (tails past the 8-element vectors, several chunks), a parameter without a gradient,
-    re-allocated gradients: every step within one bf16 ulp of the same update emulated in fp32 with
-    the kernel's rounding points (m, v, p rounded to bf16 once per step)."""
+    re-allocated gradients: every step within two bf16 ulps of the same update emulated in fp32 with
+    the kernel's rounding points (m, v, p rounded to bf16 once per step; fp32 operation order can flip
+    a rounding, and a flipped p or moment carries into the next step). lr = 5e-2 makes a wrong update
+    (no bias correction, wrong decay) several times that tolerance."""
     from kubeflow_rm_amd import ops
     assert ops.available()
     g0 = torch.Generator(device="cuda").manual_seed(0)
     shapes = [(1000, 37), (3,), (65536 * 2 + 5,), (256, 256)]
     ps = [torch.nn.Parameter((torch.rand(s, generator=g0, device="cuda") * 2 - 1).to(torch.bfloat16)) for s in shapes]
     idle = torch.nn.Parameter(torch.ones(8, device="cuda", dtype=torch.bfloat16))
-    lr, b1, b2, eps, wd = 1e-2, 0.9, 0.95, 1e-8, 0.1
+    lr, b1, b2, eps, wd = 5e-2, 0.9, 0.95, 1e-8, 0.1
     opt = AdamW(ps + [idle], lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
     ref = [p.detach().clone() for p in ps]
     mr = [torch.zeros_like(p) for p in ps]
@@ -62,8 +64,8 @@ def test_bf16_cuda_kernel_matches_reference():
         torch.cuda.synchronize()
         for i, p in enumerate(ps):
             d = (p.detach().float() - ref[i].float()).abs()
-            ulp = ref[i].float().abs().clamp(min=1e-6) * 2 ** -7
+            ulp = ref[i].float().abs().clamp(min=1e-6) * 2 ** -6  # two ulps
             assert bool((d <= ulp + 1e-6).all()), (t, i, d.max().item())
             assert torch.equal(opt.state[p]["exp_avg"].float().sub(mr[i].float()).abs().le(
-                mr[i].float().abs() * 2 ** -7 + 1e-7).all(), torch.tensor(True, device="cuda"))
+                mr[i].float().abs() * 2 ** -6 + 1e-7).all(), torch.tensor(True, device="cuda"))
     assert torch.equal(idle.detach(), torch.ones_like(idle))
