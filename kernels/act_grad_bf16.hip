@@ -88,7 +88,9 @@ __global__ __launch_bounds__(kThreads) void act_grad(const __bf16* __restrict__ 
 }
 
 // db[c] = sum over row blocks of ws[b][c]: 64 columns x 4 row-slices per 256-thread block
-__global__ __launch_bounds__(256) void colsum_finalize(const float* __restrict__ ws, float* __restrict__ db, int nblk,
+// OB: write the sums as bf16 (the bias dtype: saves autograd a separate cast launch per bias)
+template <bool OB>
+__global__ __launch_bounds__(256) void colsum_finalize(const float* __restrict__ ws, void* __restrict__ db, int nblk,
                                                        int cols) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
@@ -100,7 +102,11 @@ __global__ __launch_bounds__(256) void colsum_finalize(const float* __restrict__
   }
   red[sl][cl] = s;
   __syncthreads();
-  if (sl == 0 && c < cols) db[c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (sl == 0 && c < cols) {
+    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (OB) static_cast<__bf16*>(db)[c] = (__bf16)v;
+    else static_cast<float*>(db)[c] = v;
+  }
 }
 
 // Forward activation as its own HBM pass: y = act(z), n elements (n % 8 == 0, 16-B aligned). For
@@ -145,9 +151,10 @@ extern "C" long long kfamd_act_grad_workspace(int rows, int cols) {
 }
 
 // g = dy * act'(z) (g may be null when act == NONE: only the column sums are produced);
-// db (fp32 [cols], optional) = column sums of g; workspace: kfamd_act_grad_workspace bytes (when db).
-extern "C" int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows,
-                                   int cols, int act, void* stream) {
+// db ([cols], optional; fp32, or bf16 when db_bf16) = column sums of g (accumulated in fp32);
+// workspace: kfamd_act_grad_workspace bytes (when db).
+extern "C" int kfamd_act_grad_bf16_v2(const void* dy, const void* z, void* g, void* db, int db_bf16, float* workspace,
+                                      int rows, int cols, int act, void* stream) {
   if (!dy || rows <= 0 || cols <= 0 || cols % 8) return KFAMD_EINVAL;
   if (act < KFAMD_ACT_NONE || act > KFAMD_ACT_SILU) return KFAMD_EINVAL;
   if (act != KFAMD_ACT_NONE && (!z || !g)) return KFAMD_EINVAL;
@@ -174,7 +181,15 @@ extern "C" int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float
     case KFAMD_ACT_SILU: AG(KFAMD_ACT_SILU); break;
   }
 #undef AG
-  if (sum) hipLaunchKernelGGL(colsum_finalize, dim3((cols + 63) / 64), dim3(256), 0, s, workspace, db, nblk, cols);
+  if (sum) {
+    if (db_bf16) hipLaunchKernelGGL(colsum_finalize<true>, dim3((cols + 63) / 64), dim3(256), 0, s, workspace, db, nblk, cols);
+    else hipLaunchKernelGGL(colsum_finalize<false>, dim3((cols + 63) / 64), dim3(256), 0, s, workspace, db, nblk, cols);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows,
+                                   int cols, int act, void* stream) {
+  return kfamd_act_grad_bf16_v2(dy, z, g, db, 0, workspace, rows, cols, act, stream);
 }

@@ -114,6 +114,9 @@ int kfamd_qkv_pack_bf16(const void* dq, const void* dk, const void* dv, void* ou
                         long long vb, long long vh, long long vt, void* stream);
 int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows, int cols,
                         int act, void* stream);
+// the same with db written as bf16 when db_bf16 (fp32 accumulation)
+int kfamd_act_grad_bf16_v2(const void* dy, const void* z, void* g, void* db, int db_bf16, float* workspace, int rows,
+                           int cols, int act, void* stream);
 
 // LayerNorm forward over the last dim (hidden). x,y: [rows][hidden] bf16 (row stride = hidden).
 // gamma/beta: [hidden] bf16 (beta may be null). mean/rstd: optional fp32 [rows] (saved for bwd).
@@ -130,6 +133,10 @@ long long kfamd_layernorm_bwd_workspace(int rows, int hidden);
 int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, const float* mean,
                              const float* rstd, void* dx, float* dgamma, float* dbeta,
                              float* workspace, int rows, int hidden, void* stream);
+// the same with dgamma / dbeta written as bf16 when dgb_bf16 (fp32 accumulation)
+int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const void* gamma, const float* mean,
+                                const float* rstd, void* dx, void* dgamma, void* dbeta, int dgb_bf16,
+                                float* workspace, int rows, int hidden, void* stream);
 
 // ---- K3: one-shot all-reduce over peer-visible buffers ------------------------------------------
 enum kfamd_dtype { KFAMD_DTYPE_F32 = 0, KFAMD_DTYPE_BF16 = 1 };

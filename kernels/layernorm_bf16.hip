@@ -290,8 +290,10 @@ __global__ __launch_bounds__(256) void ln_bwd_dgb_partial(const __bf16* __restri
 // Sum of the chunk partials: 64 columns x 4 chunk lanes per block, each lane's loads independent (8 in
 // flight), then a 4-way LDS reduce. (One thread per column summing all chunks in order was latency
 // bound: 37.6 us for 128 chunks x 2048 columns on 8 blocks, profiles/r4_train_trace.)
-__global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restrict__ ws, float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta, int nchunks, int hidden) {
+// OB: write bf16 (the parameter dtype), else fp32
+template <bool OB>
+__global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restrict__ ws, void* __restrict__ dgamma,
+                                                          void* __restrict__ dbeta, int nchunks, int hidden) {
   __shared__ float sg[kRowLanes][kColsPerBlock], sb[kRowLanes][kColsPerBlock];
   const int cl = threadIdx.x & (kColsPerBlock - 1), kl = threadIdx.x / kColsPerBlock;
   const int c = blockIdx.x * kColsPerBlock + cl;
@@ -309,8 +311,13 @@ __global__ __launch_bounds__(256) void ln_bwd_dgb_finalize(const float* __restri
   if (kl == 0 && c < hidden) {
     tg = sg[0][cl] + sg[1][cl] + sg[2][cl] + sg[3][cl];
     tb = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
-    if (dgamma) dgamma[c] = tg;
-    if (dbeta) dbeta[c] = tb;
+    if (OB) {
+      if (dgamma) static_cast<__bf16*>(dgamma)[c] = (__bf16)tg;
+      if (dbeta) static_cast<__bf16*>(dbeta)[c] = (__bf16)tb;
+    } else {
+      if (dgamma) static_cast<float*>(dgamma)[c] = tg;
+      if (dbeta) static_cast<float*>(dbeta)[c] = tb;
+    }
   }
 }
 
@@ -387,10 +394,10 @@ extern "C" long long kfamd_layernorm_bwd_workspace(int rows, int hidden) {
   return 2LL * nch * hidden * (long long)sizeof(float);
 }
 
-extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma,
-                                        const float* mean, const float* rstd, void* dx,
-                                        float* dgamma, float* dbeta, float* workspace, int rows,
-                                        int hidden, void* stream) {
+// dgamma / dbeta: fp32, or bf16 (the parameter dtype) when dgb_bf16; sums accumulate in fp32 either way
+extern "C" int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const void* gamma, const float* mean,
+                                           const float* rstd, void* dx, void* dgamma, void* dbeta, int dgb_bf16,
+                                           float* workspace, int rows, int hidden, void* stream) {
   if (!dy || !x || !gamma || !mean || !rstd || !dx || rows <= 0 || hidden <= 0) return KFAMD_EINVAL;
   if ((dgamma || dbeta) && !workspace) return KFAMD_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -422,9 +429,16 @@ extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const voi
     const int nch = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
     dim3 grid((hidden + kColsPerBlock - 1) / kColsPerBlock, nch);
     hipLaunchKernelGGL(ln_bwd_dgb_partial, grid, dim3(256), 0, s, dyp, xp, mean, rstd, workspace, rows, hidden);
-    hipLaunchKernelGGL(ln_bwd_dgb_finalize, dim3((hidden + kColsPerBlock - 1) / kColsPerBlock), dim3(256), 0, s, workspace,
-                       dgamma, dbeta, nch, hidden);
+    const dim3 fg((hidden + kColsPerBlock - 1) / kColsPerBlock);
+    if (dgb_bf16) hipLaunchKernelGGL(ln_bwd_dgb_finalize<true>, fg, dim3(256), 0, s, workspace, dgamma, dbeta, nch, hidden);
+    else hipLaunchKernelGGL(ln_bwd_dgb_finalize<false>, fg, dim3(256), 0, s, workspace, dgamma, dbeta, nch, hidden);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, const float* mean,
+                                        const float* rstd, void* dx, float* dgamma, float* dbeta, float* workspace,
+                                        int rows, int hidden, void* stream) {
+  return kfamd_layernorm_bwd_bf16_v2(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, 0, workspace, rows, hidden, stream);
 }

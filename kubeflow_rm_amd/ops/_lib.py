@@ -51,11 +51,14 @@ _SIGNATURES = {
     "kfamd_xent_fwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_ll, c_vp]),
     "kfamd_xent_bwd_bf16": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_vp]),
     "kfamd_act_grad_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "kfamd_act_grad_bf16_v2": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp]),
     "kfamd_layernorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),
     "kfamd_rmsnorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),
     "kfamd_layernorm_bwd_workspace": (c_ll, [c_int, c_int]),
     "kfamd_layernorm_bwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_int, c_int, c_vp]),
+    "kfamd_layernorm_bwd_bf16_v2": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
+                                            c_int, c_vp]),
     "kfamd_allreduce_oneshot_flag_bytes": (c_ll, [c_int, c_int]),
     "kfamd_allreduce_oneshot_blocks": (c_int, [c_ll, c_int]),
     "kfamd_allreduce_oneshot_set_timeout_ms": (None, [c_int]),

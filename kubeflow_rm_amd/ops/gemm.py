@@ -482,9 +482,11 @@ def gemm_nt_preact(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | 
     return yf.to(torch.bfloat16), z
 
 
-def act_grad(gy: torch.Tensor, z: torch.Tensor | None, act: str, need_bias_grad: bool):
+def act_grad(gy: torch.Tensor, z: torch.Tensor | None, act: str, need_bias_grad: bool,
+             db_dtype: torch.dtype = torch.float32):
     """(g, db): g = gy * act'(z) (z = pre-activation; the output y for relu), db = column sums of g
-    (fp32) — one fused HIP pass (kernels/act_grad_bf16.hip). act == 'none': g = gy."""
+    (accumulated in fp32, returned as ``db_dtype``: fp32 or bf16) — one fused HIP pass
+    (kernels/act_grad_bf16.hip). act == 'none': g = gy."""
     rows, cols = gy.shape
     L = _lib.lib()
     if act == "none" and not need_bias_grad:
@@ -501,15 +503,17 @@ def act_grad(gy: torch.Tensor, z: torch.Tensor | None, act: str, need_bias_grad:
                 f = F.gelu(p, approximate="tanh") if act in ("gelu", "gelu_tanh") else F.silu(p)
                 (gf,) = torch.autograd.grad(f, p, gy.float())
             g = gf.to(torch.bfloat16)
-        return g, (g.float().sum(0) if need_bias_grad else None)
+        return g, (g.float().sum(0).to(db_dtype) if need_bias_grad else None)
     g = gy if act == "none" else torch.empty_like(gy)
     db = ws = None
+    db_bf16 = db_dtype == torch.bfloat16
     if need_bias_grad:
-        db = torch.empty(cols, dtype=torch.float32, device=gy.device)
+        db = torch.empty(cols, dtype=torch.bfloat16 if db_bf16 else torch.float32, device=gy.device)
         ws = torch.empty(L.kfamd_act_grad_workspace(rows, cols) // 4, dtype=torch.float32, device=gy.device)
-    rc = L.kfamd_act_grad_bf16(gy.data_ptr(), z.data_ptr() if z is not None else None,
-                               g.data_ptr() if act != "none" else None, db.data_ptr() if db is not None else None,
-                               ws.data_ptr() if ws is not None else None, rows, cols, ACTS[act], _stream_ptr(gy))
+    rc = L.kfamd_act_grad_bf16_v2(gy.data_ptr(), z.data_ptr() if z is not None else None,
+                                  g.data_ptr() if act != "none" else None, db.data_ptr() if db is not None else None,
+                                  int(db_bf16), ws.data_ptr() if ws is not None else None, rows, cols, ACTS[act],
+                                  _stream_ptr(gy))
     _lib.check(rc, f"act_grad[{rows}x{cols}]")
     return g, db
 
@@ -554,7 +558,8 @@ class _Linear(torch.autograd.Function):
             gy2 = gy2.contiguous()
         need_db = bias is not None and ctx.needs_input_grad[2]
         zz = zy.reshape(-1, N) if zy is not None else None
-        g, db = act_grad(gy2, zz, ctx.act, need_db)
+        g, db = act_grad(gy2, zz, ctx.act, need_db,
+                         db_dtype=torch.bfloat16 if need_db and bias.dtype == torch.bfloat16 else torch.float32)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = mm(g, weight).reshape(ctx.xshape)

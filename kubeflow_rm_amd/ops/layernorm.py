@@ -86,13 +86,16 @@ class _LayerNorm(torch.autograd.Function):
         gy2 = gy.reshape(-1, H).contiguous().to(torch.bfloat16)
         rows = x2.shape[0]
         dx = torch.empty_like(x2)
-        dgamma = torch.empty(H, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(H, dtype=torch.float32, device=x.device)
+        # the parameter grads in the parameter dtype straight from the kernel (fp32 sums either way)
+        pbf16 = weight.dtype == torch.bfloat16
+        gdt = torch.bfloat16 if pbf16 else torch.float32
+        dgamma = torch.empty(H, dtype=gdt, device=x.device)
+        dbeta = torch.empty(H, dtype=gdt, device=x.device)
         ws_bytes = _lib.lib().kfamd_layernorm_bwd_workspace(rows, H)
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device)
-        rc = _lib.lib().kfamd_layernorm_bwd_bf16(
+        rc = _lib.lib().kfamd_layernorm_bwd_bf16_v2(
             gy2.data_ptr(), x2.data_ptr(), weight.contiguous().data_ptr(), mean.data_ptr(),
-            rstd.data_ptr(), dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), ws.data_ptr(),
+            rstd.data_ptr(), dx.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), int(pbf16), ws.data_ptr(),
             rows, H, _stream_ptr(x))
         _lib.check(rc, f"layernorm_bwd[{rows}x{H}]")
         return (dx.view(x.shape), dgamma.to(weight.dtype),

@@ -294,6 +294,10 @@ def test_act_grad_fused(act, rows, cols):
     assert (g.float() - gr).abs().max().item() <= 1e-2 * (gr.abs().max().item() + 1e-3) + 1e-2
     dbr = g.float().sum(0)
     assert (db - dbr).abs().max().item() <= 1e-3 * (dbr.abs().max().item() + 1.0)
+    # the bias grad written as bf16 by the kernel (the linear backward's form): fp32 sums, one rounding
+    _, db16 = act_grad(gy, z, act, True, db_dtype=torch.bfloat16)
+    assert db16.dtype == torch.bfloat16
+    assert (db16.float() - dbr).abs().max().item() <= 2 ** -8 * dbr.abs().max().item() + 1e-3 * (dbr.abs().max().item() + 1.0)
 
 
 @pytest.mark.parametrize("act", ["none", "relu", "gelu_tanh", "silu"])
