@@ -42,6 +42,10 @@ VARIANTS = {
     "dma_spread6": ["-DKFW4_DMA_EVERY=6", "-DKFW4_DMA_PHASE=1"],
     "nopin": ["-DKFW4_PIN_MFMA=0"],
     "noprio": ["-DKFW4_PRIO=0"],
+    "gm2": ["-DKFW4_GROUP_M=2"],
+    "gm8": ["-DKFW4_GROUP_M=8"],
+    "gm16": ["-DKFW4_GROUP_M=16"],
+    "phase3": ["-DKFW4_DMA_PHASE=3"],
 }
 
 
