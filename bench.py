@@ -58,6 +58,14 @@ def parse_args():
                         "(rank 0; reported as torch_matmul_tflops_per_gpu, never as the value)")
     p.add_argument("--no-allreduce-sweep", action="store_true",
                    help="skip the RCCL all-reduce busbw sweep run after the timed region when N > 1")
+    p.add_argument("--force-dist", action=argparse.BooleanOptionalAction,
+                   default=os.environ.get("KFAMD_FORCE_DIST", "") not in ("", "0"),
+                   help="run the multi-GPU code path at WORLD_SIZE=1 too: RCCL process group, gloo CPU group, "
+                        "barriers, the RCCL / peer all-reduce sweeps and the cold-start parking "
+                        "(e.g. torchrun --nproc-per-node 1 bench.py --force-dist on a one-GPU box)")
+    p.add_argument("--ab-blocks", type=int, default=5,
+                   help="interleaved blocks of STEPS GEMMs, ours then torch.matmul (hipBLASLt), after the timed "
+                        "region: both medians and their ratio are reported (0 disables)")
     p.add_argument("--budget-s", type=float, default=float(os.environ.get("KFAMD_BENCH_BUDGET_S", "450")),
                    help="wall-clock budget from process start for everything after the timed region: extras "
                         "that do not fit are reported as skipped, one that hangs as timeout (bench_extras.py)")
@@ -149,10 +157,19 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world} (n_gpus reports WORLD_SIZE)", file=sys.stderr)
+    # the multi-GPU code path: world > 1, or forced at world 1 so one GPU executes it end to end
+    distributed = world > 1 or args.force_dist
+    if args.force_dist:
+        os.environ["KFAMD_FORCE_DIST"] = "1"  # parallel.tp / parallel.dp follow the same switch
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and not os.environ.get("MASTER_PORT"):
+            from kubeflow_rm_amd.parallel.dist import _free_port
+            os.environ["MASTER_PORT"] = str(_free_port())
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("nccl", device_id=dev)
 
     from kubeflow_rm_amd import ops
@@ -186,7 +203,7 @@ def main() -> int:
         step()
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier(device_ids=[local_rank])
 
     barrier()
@@ -199,7 +216,7 @@ def main() -> int:
     dt = time.perf_counter() - t0
 
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt_max = t.item()
     ms_per_step = dt_max / args.steps * 1e3
@@ -227,6 +244,7 @@ def main() -> int:
             "seq_len": None,
             "parallelism": f"dp{world}",
         },
+        "dist_path": "rccl" if distributed else "none",
         "per_gpu_tflops": round(per_gpu_tflops, 2),
         "kernel": "kfamd gemm_w4 (4 waves x 128x128, one wave/SIMD, asm MFMA 16x16x32 bf16 with AGPR accumulators, buffer_load..lds into a 5-slot LDS ring with the K loop unrolled over its 5-tile period, XCD remap, in-kernel edge tiles)",
         "check_rows": int(rows.numel()),
@@ -237,19 +255,53 @@ def main() -> int:
     # everything after the timed region is an extra: own try, own deadline, overall budget, and a
     # watchdog that prints the line with what was measured if one of them hangs (bench_extras.py)
     from kubeflow_rm_amd.bench_extras import Extras, print_line
-    cpu_group = dist.new_group(backend="gloo") if world > 1 else None
+    import datetime
+    # the CPU group's own timeout bounds every wait on it (ranks != 0 park on it during rank 0's
+    # cold starts): past the budget a barrier raises instead of waiting for the 30-minute default
+    cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=args.budget_s + 60)) \
+        if distributed else None
 
     def agree(flag: bool) -> bool:
-        if world == 1:
+        if not distributed:
             return flag
         f = torch.tensor([1 if flag else 0], dtype=torch.int32)
         dist.all_reduce(f, op=dist.ReduceOp.MIN, group=cpu_group)
         return bool(f.item())
 
-    ex = Extras(args.budget_s, t_start=T_START, rank=rank, agree=agree, exit_code=0 if ok else 1,
+    ex = Extras(args.budget_s, t_start=T_START, rank=rank, agree=agree,
                 emit=lambda rep: print_line({**line, **rep}))
 
-    if world > 1 and not args.no_allreduce_sweep:
+    if args.compare_torch and args.ab_blocks > 0 and rank == 0:
+        # fair comparison with hipBLASLt: interleaved ABAB blocks of STEPS GEMMs
+        # on the same operands and the same warm part, not one torch block after ours
+        def ab(_ex):
+            import statistics
+            ours, theirs = [], []
+
+            def block(fn):
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    fn()
+                torch.cuda.synchronize(dev)
+                return flops * args.steps / (time.perf_counter() - t1) / 1e12
+
+            def torch_mm():
+                torch.matmul(a, b.t(), out=c)
+
+            for _ in range(3):
+                torch_mm()
+            for _ in range(args.ab_blocks):
+                ours.append(block(step))
+                theirs.append(block(torch_mm))
+            mo, mt = statistics.median(ours), statistics.median(theirs)
+            return {"ab_ours_tflops_median": round(mo, 1), "ab_hipblaslt_tflops_median": round(mt, 1),
+                    "ab_ratio_ours_over_hipblaslt": round(mo / mt, 4), "ab_blocks": args.ab_blocks,
+                    "ab_ours_tflops": [round(x, 1) for x in ours], "ab_hipblaslt_tflops": [round(x, 1) for x in theirs],
+                    "torch_matmul_tflops_per_gpu": round(mt, 1)}
+        ex.run("gemm_ab_vs_hipblaslt", ab, est_s=3, timeout_s=60)
+
+    if distributed and not args.no_allreduce_sweep:
         # BASELINE §3 "RCCL all-reduce busbw over xGMI" on the same N GPUs, outside the timed GEMM
         # region (every rank participates; rank 0 reports)
         # 8 B .. 1 GiB, fp32 and bf16, algbw and busbw = algbw * 2(n-1)/n
@@ -281,38 +333,37 @@ def main() -> int:
             return {"xgmi_peer": xg, "xgmi_peer_GBps": xg["pair_GBps_median"]}
         ex.run("xgmi_probe", xgmi, est_s=10, timeout_s=60, collective=True)
 
-    if args.compare_torch and rank == 0:
-        def hipblaslt(_ex):
-            for _ in range(5):
-                torch.matmul(a, b.t())
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                torch.matmul(a, b.t())
-            torch.cuda.synchronize(dev)
-            return {"torch_matmul_tflops_per_gpu": round(flops * args.steps / (time.perf_counter() - t1) / 1e12, 1)}
-        ex.run("torch_matmul", hipblaslt, est_s=2, timeout_s=30)
-
     if args.coldstart_runs > 0:
         # the N-GPU notebook needs every GPU: free this rank's memory, park ranks != 0 on a CPU
         # (gloo) barrier — an RCCL barrier would keep a spinning kernel on their GPUs
         del a, b, c
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
-        if world > 1:
+        if distributed:
             dist.barrier(group=cpu_group)
         if rank == 0:
             run_cold_starts(ex, args, world)
-        if world > 1:
-            # ranks != 0 wait here for rank 0's cold starts; the watchdog bounds the wait
-            dist.barrier(group=cpu_group)
+        if distributed:
+            # ranks != 0 wait here for rank 0's cold starts: the CPU group's timeout (budget + 60 s)
+            # bounds the wait, and a rank that times out fails the run
+            try:
+                dist.barrier(group=cpu_group)
+            except Exception as e:  # noqa: BLE001
+                print(f"rank {rank}: cold-start barrier failed: {type(e).__name__}: {e}", file=sys.stderr)
+                ex.finish()
+                if rank == 0:
+                    ex.emit_once({"rank_barrier_error": f"{type(e).__name__}: {e}"[:500]})
+                sys.stdout.flush()
+                os._exit(124)
 
     line.update(ex.finish())
     if rank == 0:
         ex.emit_once()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
-    return 0 if ok else 1
+    if not ok:
+        return 1
+    return 124 if ex.timed_out else 0
 
 
 if __name__ == "__main__":

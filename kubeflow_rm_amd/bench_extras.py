@@ -12,8 +12,10 @@ notebook pod that never becomes Ready). None of them may cost the headline JSON 
   estimate does not fit in what is left is recorded as ``skipped`` and not started;
 * a watchdog thread enforces the hard limit: if an extra is still running ``grace_s`` after its own
   deadline (or the overall budget is spent) it is recorded as ``timeout``, rank 0 prints the JSON line
-  with everything measured so far, and the process leaves with ``os._exit`` (a hung collective cannot
-  be interrupted from Python). Ranks other than 0 leave a few seconds later and print nothing.
+  with everything measured so far, and the process leaves with ``os._exit(124)`` (a hung collective
+  cannot be interrupted from Python). Ranks other than 0 leave a few seconds later and print nothing.
+  The exit status is 124 whatever the headline verdict: a hang is a failure the driver must see, not
+  a footnote in ``extras_status``.
 
 Collective extras (every rank participates) agree on run / skip through ``agree`` (a MIN all-reduce
 over the CPU group supplied by bench.py), so no rank enters a collective the others skipped.
@@ -31,17 +33,20 @@ import time
 from typing import Callable
 
 
+TIMEOUT_EXIT = 124  # the exit status of a run whose extra hung (as timeout(1))
+
+
 class Extras:
     def __init__(self, budget_s: float, t_start: float | None = None, rank: int = 0,
                  emit: Callable[[dict], None] | None = None, agree: Callable[[bool], bool] | None = None,
-                 grace_s: float = 10.0, nonzero_rank_delay_s: float = 5.0, exit_code: int = 0):
+                 grace_s: float = 10.0, nonzero_rank_delay_s: float = 5.0):
         self.t_start = time.time() if t_start is None else t_start
         self.budget_deadline = self.t_start + budget_s
         self.rank = rank
         self.emit = emit
         self.agree = agree
         self.grace_s = grace_s
-        self.exit_code = exit_code
+        self.timed_out = False
         self.data: dict = {}
         self.status: dict[str, dict] = {}
         self._lock = threading.Lock()
@@ -122,6 +127,7 @@ class Extras:
                 cur, cur_dl = self._current, self._current_deadline
             hard = min(cur_dl + self.grace_s, self.budget_deadline + self.grace_s) + self._hard_delay
             if cur is not None and time.time() > hard:
+                self.timed_out = True
                 self.status[cur] = {"status": "timeout", "s": round(time.time() - self.t_start, 1),
                                     "error": "still running past its deadline; the process exits with what it has"}
                 try:
@@ -131,7 +137,7 @@ class Extras:
                         sys.stdout.flush()
                         sys.stderr.flush()
                     finally:
-                        os._exit(self.exit_code)
+                        os._exit(TIMEOUT_EXIT)
 
 
 def print_line(line: dict) -> None:

@@ -19,7 +19,9 @@ def _sync(dev):
 
 def allreduce_sweep(max_bytes: int = 256 << 20, min_bytes: int = 8, step: int = 8, iters_small: int = 50,
                     iters_large: int = 10, dtype=torch.float32, device=None, group=None) -> list[dict]:
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if not dist.is_initialized():
+        raise RuntimeError("allreduce_sweep needs an initialised process group (world size 1 included)")
+    world = dist.get_world_size(group)
     dev = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
     esz = torch.tensor([], dtype=dtype).element_size()
     buf = torch.ones(max(max_bytes // esz, 1), dtype=dtype, device=dev)
@@ -29,16 +31,15 @@ def allreduce_sweep(max_bytes: int = 256 << 20, min_bytes: int = 8, step: int = 
         n = max(nbytes // esz, 1)
         x = buf[:n]
         iters = iters_small if nbytes < (1 << 20) else iters_large
+        # every size runs the collective, world size 1 included: there RCCL still builds its
+        # communicator and launches its kernel (a copy), so a one-GPU box exercises this exact path
         for _ in range(3):
-            if world > 1:
-                dist.all_reduce(x, group=group)
+            dist.all_reduce(x, group=group)
         _sync(dev)
-        if world > 1:
-            dist.barrier(group=group)
+        dist.barrier(group=group)
         t0 = time.perf_counter()
         for _ in range(iters):
-            if world > 1:
-                dist.all_reduce(x, group=group)
+            dist.all_reduce(x, group=group)
         _sync(dev)
         dt = (time.perf_counter() - t0) / iters
         algbw = n * esz / dt / 1e9 if dt > 0 else 0.0

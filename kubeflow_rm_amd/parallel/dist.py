@@ -53,9 +53,24 @@ def device_for_local_rank(local_rank: int) -> int:
     return local_rank
 
 
-def init(backend: str | None = None, timeout_s: float = 600.0) -> DistEnv:
+def force_pg_requested() -> bool:
+    """``KFAMD_FORCE_DIST=1``: bring up the process group even at WORLD_SIZE=1, so a one-GPU run
+    executes the same RCCL code (communicator init, barriers, bucketed all-reduces) as an N-GPU job."""
+    return os.environ.get("KFAMD_FORCE_DIST", "") not in ("", "0")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init(backend: str | None = None, timeout_s: float = 600.0, force_pg: bool | None = None) -> DistEnv:
     """Initialise torch.distributed from the env (idempotent). backend: nccl (=RCCL on ROCm) when
-    GPUs are visible, else gloo."""
+    GPUs are visible, else gloo. ``force_pg`` (default: ``KFAMD_FORCE_DIST``) creates the process
+    group at world size 1 too (a private 127.0.0.1 port is picked when MASTER_PORT is unset: no other
+    rank can meet it there)."""
     global _ENV
     if _ENV is not None:
         return _ENV
@@ -70,8 +85,12 @@ def init(backend: str | None = None, timeout_s: float = 600.0) -> DistEnv:
         dev = device_for_local_rank(local_rank) % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(dev)
         device = torch.device("cuda", dev)
-    if world > 1 and not dist.is_initialized():
+    if force_pg is None:
+        force_pg = force_pg_requested()
+    if (world > 1 or force_pg) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and not os.environ.get("MASTER_PORT"):
+            os.environ["MASTER_PORT"] = str(_free_port())
         if not os.environ.get("MASTER_PORT"):
             # no silent shared default: two jobs on one host would meet in the same TCPStore
             raise RuntimeError("WORLD_SIZE > 1 but MASTER_PORT is unset: run under torchrun, "

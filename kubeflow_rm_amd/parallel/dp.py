@@ -50,6 +50,10 @@ class GradBucketer:
                  group=None, average: bool = True):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # with a process group the buckets are reduced at every world size, 1 included (a one-GPU
+        # run then executes the same RCCL calls and bucket copies as an N-GPU job); without one
+        # there is nothing to reduce
+        self.active = dist.is_initialized()
         self.average = average
         self.reduce_dtype = reduce_dtype
         params = [p for p in params if p.requires_grad]
@@ -88,7 +92,7 @@ class GradBucketer:
         self.buckets.append(_Bucket(params=params, numel=numel, dtype=dtype, offsets=offs, pending=len(params)))
 
     def _on_grad(self, p: torch.Tensor) -> None:
-        if self.world == 1:
+        if not self.active:
             return
         if not self._callback_queued:
             torch.autograd.Variable._execution_engine.queue_callback(self.finish)
@@ -115,7 +119,7 @@ class GradBucketer:
                 used[i].zero_()
             else:
                 b.buffer[off:off + p.numel()].copy_(p.grad.reshape(-1))
-        if self.average:
+        if self.average and self.world > 1:
             b.buffer.div_(self.world)
         b.work = dist.all_reduce(b.buffer, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.comm_bytes += b.numel * b.buffer.element_size()
@@ -126,7 +130,7 @@ class GradBucketer:
         reduced gradients back (end of backward). Call it directly after a backward in which this
         rank produced no gradient at all (no hook fired, so nothing queued it)."""
         self._callback_queued = False
-        if self.world > 1:
+        if self.active:
             while self._next < len(self.buckets):
                 self._launch(self._next)
                 self._next += 1

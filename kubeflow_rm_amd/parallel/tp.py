@@ -64,6 +64,17 @@ def _world(group):
     return dist.get_world_size(group) if dist.is_initialized() else 1
 
 
+# KFAMD_FORCE_DIST=1 (parallel.dist.force_pg_requested): a TP group of size 1 still issues its
+# all-reduces / all-gathers, so a one-GPU box runs the same RCCL calls as a TP job
+def _collective(group) -> bool:
+    if not dist.is_initialized():
+        return False
+    if dist.get_world_size(group) > 1:
+        return True
+    from kubeflow_rm_amd.parallel.dist import force_pg_requested
+    return force_pg_requested()
+
+
 def _rank(group):
     return dist.get_rank(group) if dist.is_initialized() else 0
 
@@ -76,7 +87,7 @@ class _CopyToTP(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if _world(ctx.group) > 1:
+        if _collective(ctx.group):
             g = _all_reduce(g.contiguous(), ctx.group)
         return g, None
 
@@ -84,7 +95,7 @@ class _CopyToTP(torch.autograd.Function):
 class _ReduceFromTP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
-        if _world(group) > 1:
+        if _collective(group):
             x = _all_reduce(x.contiguous(), group)
         return x
 
@@ -98,7 +109,7 @@ class _GatherFromTP(torch.autograd.Function):
     def forward(ctx, x, group):
         ctx.group = group
         n = _world(group)
-        if n == 1:
+        if not _collective(group):
             return x
         parts = [torch.empty_like(x) for _ in range(n)]
         dist.all_gather(parts, x.contiguous(), group=group)
@@ -122,7 +133,7 @@ class _ScatterToTP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         n = _world(ctx.group)
-        if n == 1:
+        if not _collective(ctx.group):
             return g, None
         parts = [torch.empty_like(g) for _ in range(n)]
         dist.all_gather(parts, g.contiguous(), group=ctx.group)
@@ -192,7 +203,7 @@ class RowParallelLinear(torch.nn.Module):
     def forward(self, x, residual=None):
         if not self.input_is_parallel:
             x = scatter_to_tp(x, self.group)
-        if _world(self.group) == 1:
+        if not _collective(self.group):
             return _linear(x, self.weight, self.bias, residual=residual)
         y = reduce_from_tp(_linear(x, self.weight), self.group)
         if self.bias is not None:

@@ -90,7 +90,8 @@ ex.emit_once()
 
 def test_bench_extra_that_hangs_still_yields_the_line(tmp_path):
     """one extra hangs on every rank; the self-launched job still ends well inside
-    the budget with exactly one JSON line, the hung extra marked ``timeout``, the finished ones kept."""
+    the budget with exactly one JSON line, the hung extra marked ``timeout``, the finished ones kept,
+    and the exit status is 124 (not the headline's 0)."""
     import time
     stub = tmp_path / "hang.py"
     stub.write_text(_HANG_STUB)
@@ -100,7 +101,7 @@ def test_bench_extra_that_hangs_still_yields_the_line(tmp_path):
     p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     took = time.time() - t0
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == 124, (p.returncode, p.stderr)  # a hang fails the run
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
