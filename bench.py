@@ -46,9 +46,11 @@ def parse_args():
     p.add_argument("--prewarm-s", type=float, default=float(os.environ.get("KFAMD_BENCH_PREWARM_S", "1.0")),
                    help="untimed GEMM time before the W warmup steps, so the timed steps run at the "
                         "sustained clock rather than on the DVFS ramp from idle (0 disables)")
-    p.add_argument("--m", type=int, default=8192)
-    p.add_argument("--n", type=int, default=8192)
-    p.add_argument("--k", type=int, default=8192)
+    # --gemm-m/-n/-k: the spellings to use behind torch.distributed.run, whose parser rejects "--m"
+    # as an ambiguous prefix of its own options even after the script name
+    p.add_argument("--m", "--gemm-m", dest="m", type=int, default=8192)
+    p.add_argument("--n", "--gemm-n", dest="n", type=int, default=8192)
+    p.add_argument("--k", "--gemm-k", dest="k", type=int, default=8192)
     p.add_argument("--coldstart-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_RUNS", "10")),
                    help="cold-start runs of one N-GPU notebook through the native control plane (rank 0)")
     p.add_argument("--coldstart-torch-runs", type=int, default=int(os.environ.get("KFAMD_COLDSTART_TORCH_RUNS", "5")),

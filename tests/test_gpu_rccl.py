@@ -99,7 +99,7 @@ def test_allreduce_sweep_calls_rccl_at_world_one(nccl_env):
     from kubeflow_rm_amd.parallel.collectives import allreduce_sweep
     sw = allreduce_sweep(max_bytes=64 << 20, min_bytes=8, step=8, iters_small=5, iters_large=3,
                          dtype=torch.bfloat16, device=nccl_env.device)
-    assert [r["bytes"] for r in sw] == [8 << (3 * i) for i in range(len(sw))] and sw[-1]["bytes"] == 32 << 20
+    assert [r["bytes"] for r in sw] == [8 << (3 * i) for i in range(len(sw))] and sw[-1]["bytes"] == 16 << 20
     # every size launched RCCL work: a measurable time and a finite algbw (busbw is 0 at n = 1)
     assert all(r["us"] > 0 and r["algbw_GBps"] > 0 and r["busbw_GBps"] == 0 for r in sw), sw
 
@@ -177,8 +177,8 @@ def test_bench_force_dist_runs_the_multi_gpu_path_under_torchrun(tmp_path):
                                                              "KFAMD_FORCE_DIST")}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
-           "--gpus", "1", "--steps", "5", "--warmup", "2", "--prewarm-s", "0.2", "--m", "2048", "--n", "2048",
-           "--k", "2048", "--force-dist", "--coldstart-runs", "1", "--coldstart-torch-runs", "0", "--ab-blocks", "2",
+           "--gpus", "1", "--steps", "5", "--warmup", "2", "--prewarm-s", "0.2", "--gemm-m", "2048", "--gemm-n",
+           "2048", "--gemm-k", "2048", "--force-dist", "--coldstart-runs", "1", "--coldstart-torch-runs", "0", "--ab-blocks", "2",
            "--budget-s", "240"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     (tmp_path / "bench.log").write_text(p.stdout + "\n" + p.stderr)
