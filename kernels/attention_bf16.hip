@@ -1,0 +1,670 @@
+// attention_bf16.hip — flash attention forward + backward for gfx950 (bf16 I/O, fp32 softmax).
+//
+// The in-notebook model's attention (models/gpt.py) without the N x N score matrix and without
+// torch's aotriton (Triton-generated) kernels: every product runs on v_mfma_f32_32x32x16_bf16,
+// the online softmax in fp32 registers, K/V tiles staged through a swizzled LDS image.
+//
+// Layout and lane maps (cdna_hip_programming.md §3, "An accumulator tile as the next MFMA's
+// operand"): a 32x32 accumulator has its column on the lane (lane & 31) and its rows in the 16
+// registers, row(reg, half) = (reg & 3) + 8 * (reg >> 2) + 4 * half. Every product is oriented
+// so that the NEXT product sums over the accumulator's row index, which lets the accumulator
+// (converted to bf16 pairwise) be that product's operand with no lane movement:
+//
+//   forward, per wave = 32 query rows, per 64-key tile:
+//     S^T[key][q]  = K . Q^T          A = K rows (LDS, ds_read_b128), B = Q (registers)
+//     O^T[d][q]   += V^T . P^T        A = V columns (LDS, ds_read_b64_tr_b16), B = P^T = the S^T
+//                                     accumulator in bf16 (query on the lane: the online-softmax
+//                                     max / sum / rescale of a row stay in its lane pair)
+//   backward, per wave = 32 keys, per 32-query tile (keys on the lane):
+//     S[q][key]   = Q . K^T - lse/scale    (the row constant preloaded into the accumulator)
+//     dP[q][key]  = dO . V^T - delta       (delta = rowsum(dO * O), preloaded the same way)
+//     dV^T[d][key] += dO^T . P             A = dO columns (tr reads), B = P accumulator
+//     dK^T[d][key] += Q^T . dS             A = Q columns (tr reads),  B = dS accumulator
+//     dQ[q][d]    += dS . K                dS crosses LDS once as a [key][q] image (tr reads for
+//                                          the A operand), K columns by tr reads; one wave per
+//                                          32-column d slice, f32 atomics into a workspace
+//
+// LDS images: one swizzle per head dim serves both the row reads (ds_read_b128 of a 16-B chunk
+// by 32 different rows) and the transposed reads (ds_read_b64_tr_b16 of 4 consecutive rows by 32
+// columns) without bank conflicts (T2 / T10): 16-B chunk ch of row r sits at chunk
+//   D = 128 (256-B rows): ch ^ (((r & 3) << 2) | ((r >> 2) & 3))
+//   D =  64 (128-B rows): ch ^ g((r >> 1) & 7),  g(x) = ((x & 1) << 2) | (x >> 1)
+//
+// Tensors are [B][H][T][D] views with element strides (b, h, t) and a contiguous head dim, so the
+// fused QKV projection output [B][T][3][H][D] is read in place and the output / gradients are
+// written straight into [B][T][H][D] / [B][T][3][H][D] (no transposes around the kernel).
+// Causal masking is key <= query. The forward's workgroups run heaviest query block first; the
+// backward's key blocks are heaviest first already (block 0 sees every query).
+//
+// Counterpart in the reference: none (its notebook images ship the framework's own attention);
+// SURVEY §7.1C rules out Triton on the hot path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kfamd_kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+struct AttnShape {
+  int B, H, T;
+  float scale;
+  // element strides (b, h, t) of q, k, v, o, do, dq, dk, dv
+  long long s[8][3];
+};
+
+enum { TQ = 0, TK = 1, TV = 2, TO = 3, TDO = 4, TDQ = 5, TDK = 6, TDV = 7 };
+
+__device__ __forceinline__ long long base_off(const AttnShape& a, int t, int b, int h) {
+  return b * a.s[t][0] + h * a.s[t][1];
+}
+
+// bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"): the
+// blocks dealt to one XCD (bid % 8 equal) get consecutive logical ids, so a head's blocks share L2
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int D>
+__device__ __forceinline__ int swz(int row, int ch) {
+  if constexpr (D == 128) {
+    return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  } else {
+    const int x = (row >> 1) & 7;
+    return ch ^ (((x & 1) << 2) | (x >> 1));
+  }
+}
+
+// byte offset of 16-B chunk ch of row `row` in an image of D-element bf16 rows
+template <int D>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return row * (D * 2) + (swz<D>(row, ch) << 4);
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack2(float x, float y) {
+  const bf16x2 v = __builtin_convertvector((f32x2){x, y}, bf16x2);
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16 at an LDS byte offset: 4 consecutive rows x 16 columns per 16-lane group,
+// lane i of the group receives column i (row q in element q)
+__device__ __forceinline__ s16x4 tr_read(const char* smem, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + byte_off));
+}
+
+__device__ __forceinline__ bf16x8 join(s16x4 lo, s16x4 hi) {
+  const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 lds_row(const char* smem, int byte_off) {
+  return *reinterpret_cast<const bf16x8*>(smem + byte_off);
+}
+
+__device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_cast<const u32x4*>(p); }
+
+// The A operand of a product whose k index is an accumulator's row (the permuted order of
+// §3): element j of lane half hh is row kbase + 8 * (j >> 2) + 4 * hh + (j & 3) of the operand's
+// k dimension, column `col` (this lane's row of the A operand). Read as two tr reads of 4 rows.
+// Address of lane (group g, index i = 4 qq + p): row kbase + 4 hh + qq (+ 8), columns
+// col0 + 4 p .. +3 with col0 = the 16-column half of the 32-column tile this group covers.
+template <int D>
+__device__ __forceinline__ bf16x8 tr_operand(const char* smem, int kbase, int colbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3, hh = lane >> 5;
+  const int col = colbase + 16 * (g & 1) + 4 * p;
+  const int r0 = kbase + 4 * hh + qq;
+  const int off0 = img_off<D>(r0, col >> 3) + 8 * (p & 1);
+  const int off1 = img_off<D>(r0 + 8, col >> 3) + 8 * (p & 1);
+  return join(tr_read(smem, off0), tr_read(smem, off1));
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward: one workgroup = 4 waves = 128 query rows of one (b, h); 64-key K/V tiles through a
+// double-buffered LDS image, register-staged (issued before the tile's products, written after)
+// ------------------------------------------------------------------------------------------------
+constexpr int FQ = 128, FK = 64;
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                   const __bf16* __restrict__ v, __bf16* __restrict__ o,
+                                                   float* __restrict__ lse, AttnShape a) {
+  constexpr int KS = D / 16;           // k-steps of the QK^T product
+  constexpr int ND = D / 32;           // 32-wide d tiles of O
+  constexpr int CH = D / 8;            // 16-B chunks per row
+  constexpr int NCH = FK * CH / 256;   // chunks per thread per K (and per V) tile
+  constexpr int TILE = FK * D * 2;     // bytes of one K (or V) tile image
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K, V]
+
+  const int nq = (a.T + FQ - 1) / FQ;
+  const int nwg = nq * a.H * a.B;
+  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  const int qblk = nq - 1 - (lid % nq);  // heaviest (most keys) first within each head
+  const int bh = lid / nq, h = bh % a.H, b = bh / a.H;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
+  const int T = a.T;
+
+  const __bf16* qb = q + base_off(a, TQ, b, h);
+  const __bf16* kb = k + base_off(a, TK, b, h);
+  const __bf16* vb = v + base_off(a, TV, b, h);
+  const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2];
+
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    u32x4 x = {0u, 0u, 0u, 0u};
+    if (qrow < T) x = gload16(qb + qrow * qt + kk * 16 + 8 * hh);
+    qf[kk] = __builtin_bit_cast(bf16x8, x);
+  }
+
+  const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
+
+  u32x4 kreg[NCH], vreg[NCH];
+  auto stage_load = [&](int tile) {
+    const int k0 = tile * FK;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int key = k0 + row;
+      u32x4 xk = {0u, 0u, 0u, 0u}, xv = {0u, 0u, 0u, 0u};
+      if (key < T) {
+        xk = gload16(kb + key * kt + ch * 8);
+        xv = gload16(vb + key * vt + ch * 8);
+      }
+      kreg[i] = xk;
+      vreg[i] = xv;
+    }
+  };
+  auto stage_write = [&](int buf) {
+    char* kimg = smem + buf * 2 * TILE;
+    char* vimg = kimg + TILE;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int off = img_off<D>(row, ch);
+      *reinterpret_cast<u32x4*>(kimg + off) = kreg[i];
+      *reinterpret_cast<u32x4*>(vimg + off) = vreg[i];
+    }
+  };
+
+  const float c = a.scale * kLog2e;
+  float m = -INFINITY, l = 0.f;
+  f32x16 oacc[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) oacc[n] = (f32x16){};
+
+  stage_load(0);
+  stage_write(0);
+  __syncthreads();
+
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * FK;
+    const bool more = j + 1 < ntiles;
+    if (more) stage_load(j + 1);
+    const char* kimg = smem + (j & 1) * 2 * TILE;
+    const char* vimg = kimg + TILE;
+    // a wave whose 32 rows all precede the tile's first key has nothing to do (causal)
+    if (!(CAUSAL && k0 > qw + 31)) {
+      f32x16 sacc[2] = {(f32x16){}, (f32x16){}};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 kf = lds_row(kimg, img_off<D>(32 * t + r, 2 * kk + hh));
+          sacc[t] = mfma32(kf, qf[kk], sacc[t]);
+        }
+      }
+      // masks: causal (key > query) on tiles that reach the wave's diagonal, key >= T on the tail
+      const bool causal_mask = CAUSAL && k0 + FK - 1 > qw;
+      if (causal_mask || k0 + FK > T) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int key = k0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if ((CAUSAL && key > qrow) || key >= T) sacc[t][e] = -INFINITY;
+          }
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mn = fmaxf(m, mx);  // finite: the first tile holds key 0 <= every query
+      const float alpha = exp2f((m - mn) * c);
+      m = mn;
+      const float mc = mn * c;
+      float rs = 0.f;
+      uint32_t pf[2][2][4];  // [t][s][pair]: P^T as the B operand of PV
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) {
+          const float p0 = exp2f(fmaf(sacc[t][e], c, -mc));
+          const float p1 = exp2f(fmaf(sacc[t][e + 1], c, -mc));
+          rs += p0 + p1;
+          pf[t][e >> 3][(e & 7) >> 1] = pack2(p0, p1);
+        }
+      }
+      l = l * alpha + rs;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) oacc[n] *= alpha;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 vf = tr_operand<D>(vimg, 32 * t + 16 * s, 32 * n, lane);
+            const u32x4 pw = {pf[t][s][0], pf[t][s][1], pf[t][s][2], pf[t][s][3]};
+            oacc[n] = mfma32(vf, __builtin_bit_cast(bf16x8, pw), oacc[n]);
+          }
+        }
+      }
+    }
+    if (more) stage_write((j + 1) & 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
+  const float lt = l + __shfl_xor(l, 32);
+  const float inv = 1.f / lt;
+  if (qrow < T) {
+    __bf16* ob = o + base_off(a, TO, b, h) + qrow * a.s[TO][2];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x2 v2 = {pack2(oacc[n][4 * g] * inv, oacc[n][4 * g + 1] * inv),
+                          pack2(oacc[n][4 * g + 2] * inv, oacc[n][4 * g + 3] * inv)};
+        *reinterpret_cast<u32x2*>(ob + 32 * n + 8 * g + 4 * hh) = v2;
+      }
+    }
+    if (hh == 0) lse[((long long)b * a.H + h) * T + qrow] = m * a.scale + logf(lt);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward prologue: delta[b][h][t] = sum_d dO * O (fp32)
+// ------------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__ o, const __bf16* __restrict__ dout,
+                                                      float* __restrict__ delta, AttnShape a) {
+  constexpr int LPR = D / 8;        // lanes per row (16 B each)
+  constexpr int RPB = 256 / LPR;    // rows per block
+  const long long nrows = (long long)a.B * a.H * a.T;
+  const long long row = (long long)blockIdx.x * RPB + threadIdx.x / LPR;
+  const int part = threadIdx.x % LPR;
+  float s = 0.f;
+  if (row < nrows) {
+    const int t = (int)(row % a.T);
+    const int h = (int)((row / a.T) % a.H);
+    const int b = (int)(row / ((long long)a.T * a.H));
+    const u32x4 x = gload16(o + base_off(a, TO, b, h) + t * a.s[TO][2] + part * 8);
+    const u32x4 y = gload16(dout + base_off(a, TDO, b, h) + t * a.s[TDO][2] + part * 8);
+    const bf16x8 xb = __builtin_bit_cast(bf16x8, x), yb = __builtin_bit_cast(bf16x8, y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = fmaf((float)xb[e], (float)yb[e], s);
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (row < nrows && part == 0) delta[row] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward: one workgroup = 4 waves = 128 keys of one (b, h); 32-row query tiles (Q, dO, lse,
+// delta) double-buffered through LDS; dK / dV in registers for the whole sweep
+// ------------------------------------------------------------------------------------------------
+constexpr int BK = 128, BQ = 32;
+
+// D = 128 holds dK^T, dV^T (128 registers) and V (32) for the whole sweep: one wave per SIMD
+// (512-register budget, no spills); D = 64 fits two
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                   const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                   const float* __restrict__ lse, const float* __restrict__ delta,
+                                                   float* __restrict__ dq_acc, __bf16* __restrict__ dk,
+                                                   __bf16* __restrict__ dv, AttnShape a, long long dq_st,
+                                                   long long dq_sh, long long dq_sb) {
+  constexpr int KS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int CH = D / 8;
+  constexpr int KIMG = BK * D * 2;          // K image: [128 keys][D]
+  constexpr int QT = BQ * D * 2;            // one Q (or dO) tile image: [32][D]
+  constexpr int DST = BK * BQ * 2;          // dS^T image: [128 keys][32 q], 64-B rows
+  constexpr int NQC = BQ * CH / 256;        // chunks per thread per Q (and per dO) tile
+  constexpr int KSPLIT = 4 / ND;            // waves sharing one dQ d-tile (key range split)
+  static_assert(NQC >= 1 && KSPLIT >= 1, "head dim");
+  __shared__ __attribute__((aligned(16))) char smem[KIMG + 4 * QT + DST + 4 * BQ * 4];
+  char* const kimg = smem;
+  char* const qtiles = smem + KIMG;         // [buf][Q, dO]
+  char* const dst = qtiles + 4 * QT;
+  float* const rowc = reinterpret_cast<float*>(dst + DST);  // [buf][lse(32), delta(32)]
+
+  const int T = a.T;
+  const int nk = (T + BK - 1) / BK;
+  const int nwg = nk * a.H * a.B;
+  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  const int kblk = lid % nk;               // block 0 (all queries) first within each head
+  const int bh = lid / nk, h = bh % a.H, b = bh / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int k0 = kblk * BK, kw = k0 + 32 * w, key = kw + r;
+
+  const __bf16* qb = q + base_off(a, TQ, b, h);
+  const __bf16* kb = k + base_off(a, TK, b, h);
+  const __bf16* vb = v + base_off(a, TV, b, h);
+  const __bf16* dob = dout + base_off(a, TDO, b, h);
+  const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2], dot = a.s[TDO][2];
+  const float* lseb = lse + ((long long)b * a.H + h) * T;
+  const float* deltab = delta + ((long long)b * a.H + h) * T;
+
+  // K image for the dQ product (tr reads) and the S product (row reads); V rows in registers
+#pragma unroll
+  for (int i = 0; i < BK * CH / 256; ++i) {
+    const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+    u32x4 x = {0u, 0u, 0u, 0u};
+    if (k0 + row < T) x = gload16(kb + (k0 + row) * kt + ch * 8);
+    *reinterpret_cast<u32x4*>(kimg + img_off<D>(row, ch)) = x;
+  }
+  bf16x8 vf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    u32x4 x = {0u, 0u, 0u, 0u};
+    if (key < T) x = gload16(vb + key * vt + kk * 16 + 8 * hh);
+    vf[kk] = __builtin_bit_cast(bf16x8, x);
+  }
+
+  const int qstart = CAUSAL ? k0 : 0;
+  const int ntiles = (T - qstart + BQ - 1) / BQ;
+
+  u32x4 qreg[NQC], oreg[NQC];
+  float rreg = 0.f;
+  auto stage_load = [&](int tile) {
+    const int q0 = qstart + tile * BQ;
+#pragma unroll
+    for (int i = 0; i < NQC; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      u32x4 xq = {0u, 0u, 0u, 0u}, xo = {0u, 0u, 0u, 0u};
+      if (q0 + row < T) {
+        xq = gload16(qb + (q0 + row) * qt + ch * 8);
+        xo = gload16(dob + (q0 + row) * dot + ch * 8);
+      }
+      qreg[i] = xq;
+      oreg[i] = xo;
+    }
+    if (tid < 2 * BQ) {
+      const int row = tid & (BQ - 1);
+      rreg = 0.f;
+      if (q0 + row < T) rreg = tid < BQ ? lseb[q0 + row] : deltab[q0 + row];
+    }
+  };
+  auto stage_write = [&](int buf) {
+    char* qi = qtiles + buf * 2 * QT;
+    char* oi = qi + QT;
+#pragma unroll
+    for (int i = 0; i < NQC; ++i) {
+      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int off = img_off<D>(row, ch);
+      *reinterpret_cast<u32x4*>(qi + off) = qreg[i];
+      *reinterpret_cast<u32x4*>(oi + off) = oreg[i];
+    }
+    if (tid < 2 * BQ) rowc[buf * 2 * BQ + tid] = rreg;
+  };
+
+  const float c = a.scale * kLog2e;
+  const float inv_scale = 1.f / a.scale;
+  f32x16 dkacc[ND], dvacc[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) {
+    dkacc[n] = (f32x16){};
+    dvacc[n] = (f32x16){};
+  }
+  // dQ work split: d tile nq_ of the query tile, over keys [kq0, kq0 + 128 / KSPLIT)
+  const int dqn = w % ND, kq0 = (w / ND) * (BK / KSPLIT);
+
+  if (ntiles > 0) {
+    stage_load(0);
+    stage_write(0);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int q0 = qstart + it * BQ;
+    const bool more = it + 1 < ntiles;
+    if (more) stage_load(it + 1);
+    const char* qi = qtiles + (it & 1) * 2 * QT;
+    const char* oi = qi + QT;
+    const float* lse_s = rowc + (it & 1) * 2 * BQ;
+    const float* del_s = lse_s + BQ;
+
+    // causal: every query of the tile precedes every key of the wave -> P = dS = 0
+    const bool idle = CAUSAL && q0 + BQ - 1 < kw;
+    if (!idle) {
+      f32x16 sacc, dpacc;
+      // row constants: -lse / scale and -delta for the query rows of this lane's registers
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_s + 8 * g + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(del_s + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sacc[4 * g + e] = -l4[e] * inv_scale;
+          dpacc[4 * g + e] = -d4[e];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const bf16x8 qa = lds_row(qi, img_off<D>(r, 2 * kk + hh));
+        const bf16x8 kbf = lds_row(kimg, img_off<D>(32 * w + r, 2 * kk + hh));
+        sacc = mfma32(qa, kbf, sacc);
+        const bf16x8 oa = lds_row(oi, img_off<D>(r, 2 * kk + hh));
+        dpacc = mfma32(oa, vf[kk], dpacc);
+      }
+      // P and dS; rows q = q0 + (e & 3) + 8 (e >> 2) + 4 hh, column = this lane's key
+      const bool need_mask = (CAUSAL && q0 < kw + 31) || q0 + BQ > T || key >= T;
+      uint32_t pf[2][4], sf[2][4];
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        float p0 = exp2f(sacc[e] * c), p1 = exp2f(sacc[e + 1] * c);
+        if (need_mask) {
+          const int qa0 = q0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if ((CAUSAL && qa0 < key) || qa0 >= T || key >= T) p0 = 0.f;
+          if ((CAUSAL && qa0 + 1 < key) || qa0 + 1 >= T || key >= T) p1 = 0.f;
+        }
+        pf[e >> 3][(e & 7) >> 1] = pack2(p0, p1);
+        sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
+      }
+      // dV^T += dO^T . P and dK^T += Q^T . dS (k = the query rows, permuted order)
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u32x4 pw = {pf[s][0], pf[s][1], pf[s][2], pf[s][3]};
+          const u32x4 sw = {sf[s][0], sf[s][1], sf[s][2], sf[s][3]};
+          const bf16x8 doa = tr_operand<D>(oi, 16 * s, 32 * n, lane);
+          dvacc[n] = mfma32(doa, __builtin_bit_cast(bf16x8, pw), dvacc[n]);
+          const bf16x8 qa = tr_operand<D>(qi, 16 * s, 32 * n, lane);
+          dkacc[n] = mfma32(qa, __builtin_bit_cast(bf16x8, sw), dkacc[n]);
+        }
+      }
+      // dS^T image [key][q]: registers 4g..4g+3 are queries 8g + 4hh .. +3 of this lane's key
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x2 v2 = {sf[g >> 1][2 * (g & 1)], sf[g >> 1][2 * (g & 1) + 1]};
+        *reinterpret_cast<u32x2*>(dst + (32 * w + r) * 64 + (8 * g + 4 * hh) * 2) = v2;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<u32x2*>(dst + (32 * w + r) * 64 + (8 * g + 4 * hh) * 2) = (u32x2){0u, 0u};
+    }
+    __syncthreads();
+
+    // dQ[q][d] (this wave: d tile dqn over keys kq0 .. kq0 + 128/KSPLIT): A = dS rows from the
+    // [key][q] image by tr reads, B = K columns from the K image by tr reads
+    {
+      f32x16 dqacc = (f32x16){};
+      const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
+#pragma unroll
+      for (int kk = 0; kk < BK / KSPLIT / 16; ++kk) {
+        const int kr = kq0 + 16 * kk + 8 * hh + qq;   // key row of this lane's tr-read address
+        const int qc = 16 * (g & 1) + 4 * p;          // query column
+        const bf16x8 da = join(tr_read(dst, kr * 64 + qc * 2), tr_read(dst, (kr + 4) * 64 + qc * 2));
+        const int dc = 32 * dqn + 16 * (g & 1) + 4 * p;
+        const bf16x8 kbf = join(tr_read(kimg, img_off<D>(kr, dc >> 3) + 8 * (p & 1)),
+                                tr_read(kimg, img_off<D>(kr + 4, dc >> 3) + 8 * (p & 1)));
+        dqacc = mfma32(da, kbf, dqacc);
+      }
+      // rows q0 + (e & 3) + 8 (e >> 2) + 4 hh, column d = 32 dqn + r: f32 atomics, each wave
+      // instruction two 128-B row segments
+      float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qr = q0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (qr < T) __hip_atomic_fetch_add(dqb + qr * dq_st, dqacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (more) stage_write((it + 1) & 1);
+    __syncthreads();
+  }
+
+  // epilogue: dK = scale * (dK^T)^T, dV; lane = key, rows d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
+  if (key < T) {
+    __bf16* dkr = dk + base_off(a, TDK, b, h) + key * a.s[TDK][2];
+    __bf16* dvr = dv + base_off(a, TDV, b, h) + key * a.s[TDV][2];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * n + 8 * g + 4 * hh;
+        const float s = a.scale;
+        *reinterpret_cast<u32x2*>(dkr + d) =
+            (u32x2){pack2(dkacc[n][4 * g] * s, dkacc[n][4 * g + 1] * s), pack2(dkacc[n][4 * g + 2] * s, dkacc[n][4 * g + 3] * s)};
+        *reinterpret_cast<u32x2*>(dvr + d) =
+            (u32x2){pack2(dvacc[n][4 * g], dvacc[n][4 * g + 1]), pack2(dvacc[n][4 * g + 2], dvacc[n][4 * g + 3])};
+      }
+    }
+  }
+}
+
+// dq (bf16, strided) = scale * dq_acc (f32 [B][T][H][D] with strides st / sh / sb)
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dq(const float* __restrict__ dq_acc, __bf16* __restrict__ dq,
+                                                   AttnShape a, long long st, long long sh, long long sb) {
+  constexpr int LPR = D / 8;
+  constexpr int RPB = 256 / LPR;
+  const long long nrows = (long long)a.B * a.H * a.T;
+  const long long row = (long long)blockIdx.x * RPB + threadIdx.x / LPR;
+  const int part = threadIdx.x % LPR;
+  if (row >= nrows) return;
+  const int t = (int)(row % a.T);
+  const int h = (int)((row / a.T) % a.H);
+  const int b = (int)(row / ((long long)a.T * a.H));
+  const float* src = dq_acc + b * sb + h * sh + t * st + part * 8;
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(src), x1 = *reinterpret_cast<const f32x4*>(src + 4);
+  const float s = a.scale;
+  const u32x4 y = {pack2(x0[0] * s, x0[1] * s), pack2(x0[2] * s, x0[3] * s), pack2(x1[0] * s, x1[1] * s),
+                   pack2(x1[2] * s, x1[3] * s)};
+  *reinterpret_cast<u32x4*>(dq + base_off(a, TDQ, b, h) + t * a.s[TDQ][2] + part * 8) = y;
+}
+
+bool fill_shape(AttnShape& s, int B, int H, int T, int D, float scale, const long long* strides, int ntensors) {
+  if (B <= 0 || H <= 0 || T <= 0 || (D != 64 && D != 128) || !strides) return false;
+  s.B = B;
+  s.H = H;
+  s.T = T;
+  s.scale = scale;
+  for (int t = 0; t < 8; ++t)
+    for (int j = 0; j < 3; ++j) s.s[t][j] = t < ntensors ? strides[3 * t + j] : 0;
+  for (int t = 0; t < ntensors; ++t)
+    for (int j = 0; j < 3; ++j)
+      if (strides[3 * t + j] & 7) return false;  // 16-B aligned rows
+  return true;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H, int T,
+                                   int D, float scale, int causal, const long long* strides, void* stream) {
+  AttnShape s;
+  if (!q || !k || !v || !o || !lse) return KFAMD_EINVAL;
+  if (!fill_shape(s, B, H, T, D, scale, strides, 4)) return KFAMD_EINVAL;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return KFAMD_EALIGN;
+  const long long nwg = (long long)((T + FQ - 1) / FQ) * H * B;
+  if (nwg >= (1ll << 31)) return KFAMD_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                       static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),
+                       static_cast<float*>(lse), s);
+  };
+  if (D == 128) causal ? go(attn_fwd<128, true>) : go(attn_fwd<128, false>);
+  else causal ? go(attn_fwd<64, true>) : go(attn_fwd<64, false>);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" long long kfamd_attn_bwd_workspace(int B, int H, int T, int D) {
+  // dq_acc f32 [B][T][H][D] + delta f32 [B][H][T]
+  return (long long)B * T * H * D * 4 + (long long)B * H * T * 4;
+}
+
+// strides: 8 tensors x (b, h, t): q, k, v, o, do, dq, dk, dv. workspace: kfamd_attn_bwd_workspace bytes
+// (16-B aligned); it is zeroed here on the stream (memset node) before the dQ atomics.
+extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                   const void* lse, void* dq, void* dk, void* dv, void* workspace, int B, int H, int T,
+                                   int D, float scale, int causal, const long long* strides, void* stream) {
+  AttnShape s;
+  if (!q || !k || !v || !o || !dout || !lse || !dq || !dk || !dv || !workspace) return KFAMD_EINVAL;
+  if (!fill_shape(s, B, H, T, D, scale, strides, 8)) return KFAMD_EINVAL;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o) || !al16(dout) || !al16(dq) || !al16(dk) || !al16(dv) ||
+      !al16(workspace))
+    return KFAMD_EALIGN;
+  const long long nk = (long long)((T + BK - 1) / BK) * H * B;
+  if (nk >= (1ll << 31)) return KFAMD_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* dq_acc = static_cast<float*>(workspace);
+  float* delta = dq_acc + (long long)B * T * H * D;
+  const long long dq_st = (long long)H * D, dq_sh = D, dq_sb = (long long)T * H * D;
+  hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * T * H * D * 4, st);
+  if (e != hipSuccess) return static_cast<int>(e);
+  const long long rows = (long long)B * H * T;
+  const unsigned rblocks = (unsigned)((rows + 256 / (D / 8) - 1) / (256 / (D / 8)));
+  auto run = [&](auto delta_k, auto main_k, auto dq_k) {
+    hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
+                       static_cast<const __bf16*>(dout), delta, s);
+    hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                       static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
+                       static_cast<const float*>(lse), static_cast<const float*>(delta), dq_acc,
+                       static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s, dq_st, dq_sh, dq_sb);
+    hipLaunchKernelGGL(dq_k, dim3(rblocks), dim3(256), 0, st, static_cast<const float*>(dq_acc),
+                       static_cast<__bf16*>(dq), s, dq_st, dq_sh, dq_sb);
+  };
+  if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true>, attn_bwd_dq<128>)
+                       : run(attn_bwd_delta<128>, attn_bwd<128, false>, attn_bwd_dq<128>);
+  else causal ? run(attn_bwd_delta<64>, attn_bwd<64, true>, attn_bwd_dq<64>)
+              : run(attn_bwd_delta<64>, attn_bwd<64, false>, attn_bwd_dq<64>);
+  e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}

@@ -172,6 +172,18 @@ int kfamd_copy_async(void* dst, const void* src, long long bytes, void* stream);
 // Library identity (for the loud "native code loaded" check).
 const char* kfamd_build_info(void);
 
+// Flash attention (attention_bf16.hip), bf16 I/O, fp32 softmax, head dim D = 64 or 128.
+// Tensors are [B][H][T][D] views with element strides (b, h, t) (multiples of 8) and D contiguous;
+// strides[3 * i + {0, 1, 2}] for tensor i in the order q, k, v, o (forward) or q, k, v, o, do, dq,
+// dk, dv (backward). lse: f32 [B][H][T] (written by the forward, read by the backward).
+// causal: key <= query. The backward zeroes and uses `workspace` (kfamd_attn_bwd_workspace bytes).
+int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H, int T,
+                        int D, float scale, int causal, const long long* strides, void* stream);
+long long kfamd_attn_bwd_workspace(int B, int H, int T, int D);
+int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                        const void* lse, void* dq, void* dk, void* dv, void* workspace, int B, int H, int T,
+                        int D, float scale, int causal, const long long* strides, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,8 +3,10 @@
 Used by the multi-GPU notebook smoke (BASELINE config 4: DP/TP over RCCL inside a pod), the
 examples and ``smoke()``. Every projection runs on the hand-written MFMA GEMM with its fused
 epilogue (bias + GELU for the MLP up-projection; residual for the down-projection), LayerNorm
-on the wave-per-row kernel, the LM-head loss on the bf16 cross-entropy kernel, attention on
-``scaled_dot_product_attention`` (ROCm flash path).
+on the wave-per-row kernel, the LM-head loss on the bf16 cross-entropy kernel, causal attention on
+the hand-written flash kernels (``ops.attention_qkv``: reads the fused QKV output in place, writes
+the output projection's input layout; head dims 64 / 128). Other head dims and the torch reference
+mode use ``scaled_dot_product_attention``.
 With a tensor-parallel group the attention heads and the MLP are split Megatron-style
 (QKV / fc1 column-parallel, out-proj / fc2 row-parallel: one all-reduce per sub-block).
 
@@ -110,6 +112,9 @@ class Block(torch.nn.Module):
         B, T, _ = x.shape
         h, hd = self.local_heads, self.cfg.head_dim
         qkv = self.qkv(x)  # [B, T, 3 * h * hd] — the column shard is [q_h | k_h | v_h] per rank
+        if ops.native_enabled() and ops.attention_supported(qkv, hd):
+            y = ops.attention_qkv(qkv.contiguous(), h, hd, causal=True)  # [B, T, h * hd]
+            return self.proj(y, residual=residual)
         q, k, v = ops.split_heads(qkv, h, hd)  # backward: one pass into the QKV gradient layout
         y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return self.proj(y.transpose(1, 2).reshape(B, T, h * hd), residual=residual)

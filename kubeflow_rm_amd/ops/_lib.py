@@ -72,6 +72,11 @@ _SIGNATURES = {
     "kfamd_ipc_close": (c_int, [c_vp]),
     "kfamd_ipc_free": (c_int, [c_vp]),
     "kfamd_copy_async": (c_int, [c_vp, c_vp, c_ll, c_vp]),
+    "kfamd_attn_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_float, c_int,
+                                    ctypes.POINTER(c_ll), c_vp]),
+    "kfamd_attn_bwd_workspace": (c_ll, [c_int, c_int, c_int, c_int]),
+    "kfamd_attn_bwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                                    c_int, c_float, c_int, ctypes.POINTER(c_ll), c_vp]),
     "kfamd_build_info": (ctypes.c_char_p, []),
 }
 
