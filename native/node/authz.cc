@@ -4,7 +4,9 @@
 #include <arpa/inet.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdlib>
+#include <cstring>
 
 #include "core/util.h"
 
@@ -26,6 +28,52 @@ bool ipv4_in_cidr(const std::string& ip, const std::string& cidr) {
   if (bits <= 0) return true;
   const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ~((1u << (32 - bits)) - 1);
   return (ntohl(a.s_addr) & mask) == (ntohl(n.s_addr) & mask);
+}
+
+std::string normalize_authz_path(const std::string& decoded_path) {
+  std::string p = decoded_path;
+  std::replace(p.begin(), p.end(), '\\', '/');
+  if (p.empty() || p[0] != '/') p.insert(p.begin(), '/');
+  std::vector<std::string> out;
+  size_t i = 1;
+  bool trailing = false;  // the path ends in '/' (or in a dot segment, which names a directory)
+  while (i <= p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    const std::string seg = p.substr(i, j - i);
+    const bool last = j == p.size();
+    if (seg == "..") {
+      if (!out.empty()) out.pop_back();
+      trailing = last;
+    } else if (seg == ".") {
+      trailing = last;
+    } else {
+      out.push_back(seg);
+      trailing = false;
+    }
+    i = j + 1;
+  }
+  std::string r;
+  for (const auto& seg : out) r += "/" + seg;
+  if (r.empty() || trailing) r += "/";
+  return r;
+}
+
+std::string encode_request_path(const std::string& path) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string r;
+  r.reserve(path.size());
+  for (unsigned char ch : path) {
+    const bool keep = std::isalnum(ch) || std::strchr("-._~!$&'()*+,;=:@/", ch) != nullptr;
+    if (keep && ch != 0) {
+      r.push_back(static_cast<char>(ch));
+    } else {
+      r.push_back('%');
+      r.push_back(hex[ch >> 4]);
+      r.push_back(hex[ch & 15]);
+    }
+  }
+  return r;
 }
 
 namespace {
@@ -67,8 +115,8 @@ bool operation_matches(const Json& op, const AuthzRequest& r) {
   if (!field_ok(op, "hosts", "notHosts", host, true)) return false;
   if (!field_ok(op, "ports", "notPorts", std::to_string(r.port))) return false;
   if (!field_ok(op, "methods", "notMethods", r.method)) return false;
-  const std::string path = r.path.substr(0, r.path.find('?'));
-  if (!field_ok(op, "paths", "notPaths", path)) return false;
+  // r.path is the normalized path alone (the query was split off before decoding)
+  if (!field_ok(op, "paths", "notPaths", r.path)) return false;
   return true;
 }
 

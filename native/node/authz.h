@@ -46,6 +46,16 @@ struct AuthzDecision {
 };
 
 bool istio_string_match(const std::string& pattern, const std::string& value);
+
+// Istio's default pathNormalization (BASE) of an already percent-decoded request path: backslashes
+// become slashes and RFC 3986 §5.2.4 remove_dot_segments collapses "." / ".." segments (never above
+// the root). A decoded '?' or '#' stays part of the path: policies are matched on, and the request
+// is forwarded with, exactly this string (/x/../admin, /./, %3F no longer slip past a
+// DENY paths rule).
+std::string normalize_authz_path(const std::string& decoded_path);
+// The path as an upstream request-line token: every byte outside RFC 3986 pchar ('/' included)
+// percent-encoded, so a decoded '?', '#', '%' or space reaches the backend as data, not syntax.
+std::string encode_request_path(const std::string& path);
 bool ipv4_in_cidr(const std::string& ip, const std::string& cidr);
 
 // policies: AuthorizationPolicy objects (any namespaces; filtered here); workload_ns / labels: the

@@ -98,8 +98,17 @@ Gateway::Identity Gateway::review_token(const std::string& token) {
 bool Gateway::authorize(const std::string& dest_host, int dest_port, const HttpRequest& req, const std::string& path,
                         const Headers& fwd, const std::string& principal, const std::string& source_ns, std::string* why) {
   if (!o_.enforce || !policies_) return true;
+  // fail closed: until both informers have listed, "no ALLOW policy applies" would
+  // admit everything; a destination that is not a Service has no workload to evaluate against
+  if (!policies_->synced() || (services_ && !services_->synced())) {
+    if (why) *why = "authorization policies not synced yet";
+    return false;
+  }
   std::string svc, ns;
-  if (!split_service_host(dest_host, svc, ns)) return true;  // not a Service destination
+  if (!split_service_host(dest_host, svc, ns)) {
+    if (why) *why = "destination " + dest_host + " is not a Service";
+    return false;
+  }
   std::map<std::string, std::string> labels;  // the workload's labels: the Service's selector
   Json s;
   if (services_ && services_->get(ns, svc, s))
@@ -176,12 +185,14 @@ bool Gateway::match(const std::vector<Json>& vss, const std::string& gateway, co
 
 void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   const std::string host = req.header("Host");
+  // routing, authorization and the upstream request all see one normalized path (Istio BASE)
+  const std::string path = normalize_authz_path(req.path);
   Route rt;
-  bool ok = vs_ && match(vs_->list(), o_.gateway_name, host, req.path, rt);
+  bool ok = vs_ && match(vs_->list(), o_.gateway_name, host, path, rt);
   bool routed_by_route = false;  // OpenShift Routes bypass the mesh (the ODH OAuth proxy guards them)
   std::string target_path;
   if (ok) {
-    std::string rest = req.path.size() >= rt.prefix.size() ? req.path.substr(rt.prefix.size()) : "";
+    std::string rest = path.size() >= rt.prefix.size() ? path.substr(rt.prefix.size()) : "";
     target_path = rt.rewrite + rest;
     if (target_path.empty()) target_path = "/";
   } else if (routes_) {
@@ -200,16 +211,16 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
           for (const auto& p : s.at_path({"spec", "ports"}).as_array())
             if (p["name"].as_string() == tp.as_string() || p["targetPort"] == tp) rt.dest_port = static_cast<int>(p["port"].as_int());
       }
-      target_path = req.path;
+      target_path = path;
       ok = routed_by_route = true;
       break;
     }
   }
   if (!ok) {
-    resp.text(404, "no route for " + host + req.path + "\n");
+    resp.text(404, "no route for " + host + path + "\n");
     return;
   }
-  std::string url = "http://" + rt.dest_host + ":" + std::to_string(rt.dest_port) + target_path +
+  std::string url = "http://" + rt.dest_host + ":" + std::to_string(rt.dest_port) + encode_request_path(target_path) +
                     (req.raw_query.empty() ? "" : "?" + req.raw_query);
   // authentication: a trusted authn proxy's assertion, else a bearer token / session cookie
   // (TokenReview); client-supplied identity headers never pass otherwise
@@ -233,7 +244,7 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   if (who.authenticated && !who.service_account()) h[o_.userid_header] = o_.userid_prefix + who.username;
   for (const auto& m : rt.headers.as_object()) h[m.first] = m.second.as_string();
   h["X-Forwarded-Prefix"] = rt.prefix;
-  h["X-Envoy-Original-Path"] = req.path;
+  h["X-Envoy-Original-Path"] = path;
   // authorization at the destination workload (what its Istio sidecar does in the reference): the
   // request arrives from the ingress gateway's principal, with the path after the rewrite
   std::string why;
@@ -276,14 +287,16 @@ void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
   const size_t colon = host.find(':');
   const int port = colon == std::string::npos ? 80 : std::atoi(host.c_str() + colon + 1);
   std::string why;
-  if (!authorize(host.substr(0, colon), port, req, req.path, h, principal, source_ns, &why)) {
+  const std::string path = normalize_authz_path(req.path);
+  if (!authorize(host.substr(0, colon), port, req, path, h, principal, source_ns, &why)) {
     decisions_->inc({"mesh", "deny"});
     resp.headers["X-Kfamd-Authz"] = why;
     resp.text(403, "RBAC: access denied");
     return;
   }
   if (o_.enforce) decisions_->inc({"mesh", "allow"});
-  const std::string url = "http://" + svc + "." + ns + ".svc." + o_.cluster_domain + ":" + std::to_string(port) + req.path +
+  const std::string url = "http://" + svc + "." + ns + ".svc." + o_.cluster_domain + ":" + std::to_string(port) +
+                          encode_request_path(path) +
                           (req.raw_query.empty() ? "" : "?" + req.raw_query);
   forward(req, resp, url, std::move(h), 300000);
 }

@@ -5,9 +5,10 @@ One step = forward + backward + AdamW update of kubeflow_rm_amd.models.gpt (bf16
 activations), on synthetic tokens; native steps with kubeflow_rm_amd.optim.AdamW (one HIP launch),
 torch with torch's fused AdamW. ``--backend native`` runs the projections on the
 w4 MFMA GEMM (bias / GELU / residual epilogues, pre-activation output, fused act-grad, transposed
-backward layouts) and LayerNorm on the wave-per-row kernel; ``--backend torch`` runs the same model
-inside ``ops.torch_reference()`` (F.linear / F.layer_norm: hipBLASLt + torch's LayerNorm). Both use
-torch's scaled_dot_product_attention, embedding and cross-entropy. Rounds alternate between the two
+backward layouts), LayerNorm on the wave-per-row kernel and attention on the flash kernels
+(kernels/attention_bf16.hip); ``--backend torch`` runs the same model inside
+``ops.torch_reference()`` (F.linear / F.layer_norm / scaled_dot_product_attention: hipBLASLt,
+torch's LayerNorm, aotriton). Both use torch's embedding. Rounds alternate between the two
 backends so clock drift hits both.
 
 python tools/train_bench.py --model gpt-small --batch 8 --seq 1024 --steps 10 --rounds 3

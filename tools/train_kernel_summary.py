@@ -32,8 +32,10 @@ def group(name: str) -> str:
     if "Cijk" in n:
         tag = re.search(r"Cijk_(A\w{3})_(B\w{3})", n)
         return "hipBLASLt " + (f"{tag.group(1)}_{tag.group(2)}" if tag else "")
+    if ("GLOBAL__N" in n or "anonymous namespace" in n) and ("attn_fwd" in n or "attn_bwd" in n):
+        return "ours: attention (flash)"  # kernels/attention_bf16.hip (aotriton's is a bare "attn_fwd")
     if "attn" in n or "flash" in n.lower() or "bwd_kernel" in n:
-        return "attention (torch SDPA)"
+        return "attention (torch SDPA / aotriton)"
     if "norm" in n.lower():
         return "layernorm"
     if "xent" in n or "cross_entropy" in n.lower() or "nll" in n.lower() or "softmax" in n.lower():
