@@ -20,7 +20,8 @@ class AdamW(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or not 0 <= betas[0] < 1 or not 0 <= betas[1] < 1 or weight_decay < 0:
             raise ValueError("invalid AdamW hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
-        self._tables: dict = {}  # (device, group index) -> (pointers, table, ntensors, nchunks, pinned host copy)
+        # (device, (group index, step-count rank)) -> (pointers, table, ntensors, nchunks, pinned host copy)
+        self._tables: dict = {}
 
     def _native_ok(self, p: torch.Tensor) -> bool:
         from kubeflow_rm_amd import ops
@@ -44,13 +45,20 @@ class AdamW(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                elif torch.is_tensor(st["step"]):  # a state loaded from torch.optim.AdamW keeps a tensor
+                    st["step"] = int(st["step"].item())
                 st["step"] += 1
                 (native if self._native_ok(p) else other).append(p)
+            # one launch per (device, step count); normally one. The pointer table of each is cached
+            # under its rank among this step's step counts on that device, which stays the same
+            # from step to step (keying it by the step count would rebuild it every step)
             by_step: dict = {}
             for p in native:
                 by_step.setdefault((p.device, self.state[p]["step"]), []).append(p)
-            for (dev, t), ps in by_step.items():
-                self._launch(gi, dev, ps, t, lr, b1, b2, eps, wd)
+            rank: dict = {}
+            for (dev, t), ps in sorted(by_step.items(), key=lambda kv: (str(kv[0][0]), kv[0][1])):
+                k = rank[dev] = rank.get(dev, -1) + 1
+                self._launch((gi, k), dev, ps, t, lr, b1, b2, eps, wd)
             if other:
                 torch.optim._functional.adamw(
                     [p for p in other], [p.grad for p in other], [self.state[p]["exp_avg"] for p in other],

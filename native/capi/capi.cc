@@ -30,6 +30,7 @@
 #include "core/util.h"
 #include "gpu/smi.h"
 #include "gpu/topology.h"
+#include "node/authz.h"
 
 namespace kf {
 namespace {
@@ -79,6 +80,27 @@ void register_core(CapiRegistry& R) {
     return sel.matches(a["object"]);
   });
   R.add("merge_patch", [](const Json& a) -> Json { return merge_patch(a["target"], a["patch"]); });
+  // the gateway's policy enforcement point (node/authz.cc): path normalization, request-line
+  // encoding and AuthorizationPolicy evaluation
+  R.add("authz_normalize_path", [](const Json& a) -> Json { return normalize_authz_path(a["path"].as_string()); });
+  R.add("authz_encode_path", [](const Json& a) -> Json { return encode_request_path(a["path"].as_string()); });
+  R.add("authz_evaluate", [](const Json& a) -> Json {
+    AuthzRequest r;
+    const Json& q = a["request"];
+    r.principal = q["principal"].as_string();
+    r.source_namespace = q["source_namespace"].as_string();
+    r.source_ip = r.remote_ip = q["ip"].as_string();
+    r.method = q["method"].as_string_or("GET");
+    r.path = q["path"].as_string();
+    r.host = q["host"].as_string();
+    r.port = static_cast<int>(q["port"].as_int(80));
+    for (const auto& kv : q["headers"].as_object()) r.headers[to_lower(kv.first)] = kv.second.as_string();
+    std::map<std::string, std::string> labels;
+    for (const auto& kv : a["labels"].as_object()) labels[kv.first] = kv.second.as_string();
+    const AuthzDecision d = evaluate_authz(vec(a["policies"]), r, a["namespace"].as_string(), labels,
+                                           a["root_namespace"].as_string_or("istio-system"));
+    return Json{{"allowed", d.allowed}, {"policy", d.policy}, {"reason", d.reason}};
+  });
   R.add("diff_merge_patch", [](const Json& a) -> Json { return diff_merge_patch(a["from"], a["to"]); });
   R.add("apply_json_patch", [](const Json& a) -> Json { return apply_json_patch(a["target"], a["ops"]); });
   R.add("diff_json_patch", [](const Json& a) -> Json { return diff_json_patch(a["from"], a["to"]); });

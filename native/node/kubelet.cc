@@ -534,24 +534,34 @@ int wait_probe_process(pid_t pid, int timeout_ms) {
 #else
   const int pfd = -1;
 #endif
-  bool timed_out = false;
+  bool timed_out = false, waited = false;
   if (pfd >= 0) {
     pollfd p{pfd, POLLIN, 0};
     int rc;
     do rc = ::poll(&p, 1, timeout_ms);
     while (rc < 0 && errno == EINTR);
-    timed_out = rc == 0;
     ::close(pfd);
-  } else {
+    // a poll that fails for any other reason falls back to the deadline loop below: never a
+    // blocking waitpid on a probe that may not exit
+    if (rc >= 0) {
+      timed_out = rc == 0;
+      waited = true;
+    }
+  }
+  if (!waited) {
     const double deadline = now_seconds() + timeout_ms / 1000.0;
-    while (::waitpid(pid, &st, WNOHANG) == 0) {
+    pid_t r;
+    while ((r = ::waitpid(pid, &st, WNOHANG)) == 0 || (r < 0 && errno == EINTR)) {
       if (now_seconds() > deadline) {
         timed_out = true;
         break;
       }
       ::usleep(5000);
     }
-    if (!timed_out) return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+    if (!timed_out) {
+      if (r < 0) return 128;  // not our child any more (reaped elsewhere)
+      return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+    }
   }
   if (timed_out) ::kill(-pid, SIGKILL);
   while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {

@@ -187,3 +187,77 @@ def test_culling_still_reads_kernels_through_the_mesh(cl):
         text = r.read().decode()
     allow = [ln for ln in text.splitlines() if ln.startswith('gateway_authz_decisions_total{listener="mesh",result="allow"}')]
     assert allow and float(allow[0].split()[-1]) > 0, allow
+
+
+def test_policy_paths_are_normalized_like_istio_base():
+    """policies are matched on the RFC 3986-normalized path (Istio's default BASE
+    normalization), the decoded '?' stays part of the path, and the same string is forwarded."""
+    from kubeflow_rm_amd import native
+    norm = lambda p: native.call("authz_normalize_path", path=p)  # noqa: E731
+    assert norm("/x/../admin") == "/admin"
+    assert norm("/a/./b/") == "/a/b/"
+    assert norm("/../../etc") == "/etc"
+    assert norm("/a/b/..") == "/a/"
+    assert norm("\\a\\..\\b") == "/b"
+    assert norm("/api/status?x") == "/api/status?x"      # a decoded %3F is data, not a query
+    assert native.call("authz_encode_path", path="/a b/c?d#e%f") == "/a%20b/c%3Fd%23e%25f"
+    deny = {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy",
+            "metadata": {"name": "no-admin", "namespace": "ns"},
+            "spec": {"action": "DENY", "rules": [{"to": [{"operation": {"paths": ["/admin*"]}}]}]}}
+
+    def allowed(path):
+        return native.call("authz_evaluate", policies=[deny], namespace="ns", labels={},
+                           request={"path": norm(path), "method": "GET"})["allowed"]
+    assert not allowed("/admin/x") and not allowed("/x/../admin") and not allowed("/./admin")
+    assert allowed("/public/admin")
+
+
+def test_dot_segments_and_encoded_query_cannot_dodge_a_deny_rule(cl):
+    c = cl.client
+    pol = {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy",
+           "metadata": {"name": "deny-terminals", "namespace": "alice"},
+           "spec": {"action": "DENY", "rules": [{"to": [{"operation": {
+               "paths": ["/notebook/alice/nb/api/terminals", "/notebook/alice/nb/admin*"]}}]}]}}
+    c.create(pol)
+    try:
+        base = cl.gateway + "/notebook/alice/nb/"
+        get = lambda p: _http(base + p, headers=cl.user_headers(ALICE))  # noqa: E731
+        assert _eventually(lambda: get("api/terminals")[0], 403) == 403
+        for p in ("api/x/../terminals", "api/./terminals", "api/%2E%2E/api/terminals", "x/../admin/panel",
+                  "api/../api/terminals"):
+            code, _ = get(p)
+            assert code == 403, p
+        # a decoded '?' is part of the evaluated path (no exact match here) and reaches the backend
+        # encoded: the backend sees the very path the policy saw, not ".../api/terminals"
+        code, body = get("api/terminals%3Fx")
+        assert code == 404 and "%3F" in body, (code, body)
+        assert get("api/status")[0] == 200
+    finally:
+        c.delete("security.istio.io/v1beta1", "AuthorizationPolicy", "deny-terminals", "alice")
+
+
+def test_non_service_destination_is_denied_when_enforcing(cl):
+    """a VirtualService destination that names no Service has no workload policy set to
+    evaluate; the enforcing gateway refuses it instead of forwarding unchecked."""
+    c = cl.client
+    c.create({"apiVersion": "networking.istio.io/v1alpha3", "kind": "VirtualService",
+              "metadata": {"name": "external", "namespace": "alice"},
+              "spec": {"gateways": ["kubeflow/kubeflow-gateway"], "hosts": ["*"],
+                       "http": [{"match": [{"uri": {"prefix": "/external/"}}],
+                                 "route": [{"destination": {"host": "httpbin.example.com", "port": {"number": 80}}}]}]}})
+    try:
+        def probe():
+            req = urllib.request.Request(cl.gateway + "/external/x", headers=cl.user_headers(ALICE))
+            try:
+                with urllib.request.urlopen(req, timeout=10) as r:
+                    return r.status, r.headers.get("X-Kfamd-Authz", "")
+            except urllib.error.HTTPError as e:
+                return e.code, e.headers.get("X-Kfamd-Authz", "")
+        deadline = time.time() + 20
+        got = probe()
+        while got[0] == 404 and time.time() < deadline:
+            time.sleep(0.1)
+            got = probe()
+        assert got[0] == 403 and "not a Service" in got[1], got
+    finally:
+        c.delete("networking.istio.io/v1alpha3", "VirtualService", "external", "alice")

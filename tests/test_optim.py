@@ -68,8 +68,61 @@ def test_bf16_cuda_kernel_matches_reference():
             assert bool((d <= ulp + 1e-6).all()), (t, i, d.max().item())
             assert torch.equal(opt.state[p]["exp_avg"].float().sub(mr[i].float()).abs().le(
                 mr[i].float().abs() * 2 ** -6 + 1e-7).all(), torch.tensor(True, device="cuda"))
+            dv = (opt.state[p]["exp_avg_sq"].float() - vr[i].float()).abs()
+            assert bool((dv <= vr[i].float().abs() * 2 ** -6 + 1e-9).all()), (t, i, dv.max().item())
             # re-sync the emulation to the kernel's state: each step is checked on its own rounding
             ref[i] = p.detach().clone()
             mr[i] = opt.state[p]["exp_avg"].clone()
             vr[i] = opt.state[p]["exp_avg_sq"].clone()
     assert torch.equal(idle.detach(), torch.ones_like(idle))
+
+
+def test_tensor_step_from_a_torch_state_becomes_an_int():
+    """a state loaded from torch.optim.AdamW carries ``step`` as a tensor; it is normalised
+    to an int, so launches group (and pointer tables cache) by value, not by tensor identity."""
+    torch.manual_seed(0)
+    m = torch.nn.Linear(4, 2)
+    src = torch.optim.AdamW(m.parameters(), lr=1e-2)
+    m(torch.randn(3, 4)).sum().backward()
+    src.step()
+    opt = AdamW(m.parameters(), lr=1e-2)
+    opt.load_state_dict(src.state_dict())
+    assert all(torch.is_tensor(opt.state[p]["step"]) for p in m.parameters())
+    m(torch.randn(3, 4)).sum().backward()
+    opt.step()
+    assert all(opt.state[p]["step"] == 2 and isinstance(opt.state[p]["step"], int) for p in m.parameters())
+
+
+@pytest.mark.gpu
+def test_bf16_moments_track_an_unsynced_emulation_over_20_steps():
+    """without re-syncing, the kernel's p / exp_avg / exp_avg_sq after 20 steps stay
+    within bf16 rounding noise of the fp32 emulation (slow drift in v would show here), and one
+    state-loaded parameter group keeps ONE cached pointer table."""
+    g0 = torch.Generator(device="cuda").manual_seed(1)
+    shapes = [(513, 129), (70_001,)]
+    ps = [torch.nn.Parameter((torch.rand(s, generator=g0, device="cuda") * 2 - 1).to(torch.bfloat16)) for s in shapes]
+    lr, b1, b2, eps, wd = 1e-2, 0.9, 0.95, 1e-8, 0.1
+    opt = AdamW(ps, lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    ref = [p.detach().float().clone() for p in ps]
+    mr = [torch.zeros_like(r) for r in ref]
+    vr = [torch.zeros_like(r) for r in ref]
+    for t in range(1, 21):
+        grads = [(torch.randn(p.shape, generator=g0, device="cuda") * 0.1).to(torch.bfloat16) for p in ps]
+        for p, g in zip(ps, grads):
+            p.grad = g.clone()
+        opt.step()
+        ss, ib = lr / (1 - b1 ** t), 1 / math.sqrt(1 - b2 ** t)
+        for i, g in enumerate(grads):
+            gf = g.float()
+            mr[i] = b1 * mr[i] + (1 - b1) * gf
+            vr[i] = b2 * vr[i] + (1 - b2) * gf * gf
+            ref[i] = ref[i] * (1 - lr * wd) - ss * mr[i] / (vr[i].sqrt() * ib + eps)
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        return ((a.float() - b).norm() / b.norm()).item()
+    for i, p in enumerate(ps):
+        assert rel(opt.state[p]["exp_avg"], mr[i]) < 1e-2, i
+        assert rel(opt.state[p]["exp_avg_sq"], vr[i]) < 1e-2, i
+        assert rel(p.detach(), ref[i]) < 1e-2, i
+    assert len(opt._tables) == 1
