@@ -191,15 +191,11 @@ class KubeClient:
             params["dryRun"] = "All"
         return self._req("DELETE", self.path(api_version, kind, namespace, name), params=params)
 
-    def apply(self, obj: dict) -> dict:
-        """Create or (merge-)update — kubectl apply semantics without the last-applied annotation."""
-        md = obj.get("metadata", {})
-        try:
-            return self.create(obj)
-        except ApiException as e:
-            if e.status != 409:
-                raise
-        return self.patch(obj["apiVersion"], obj["kind"], md["name"], obj, md.get("namespace"), "merge")
+    def apply(self, obj: dict, dry_run: bool = False) -> dict:
+        """``kubectl apply`` (client-side): create, or three-way strategic merge patch against the
+        last-applied-configuration annotation (kubeflow_rm_amd.apply). Returns the object."""
+        from .apply import apply_object
+        return apply_object(self, obj, dry_run=dry_run)[1]
 
     def exists(self, api_version: str, kind: str, name: str, namespace: str | None = None) -> bool:
         try:

@@ -39,24 +39,21 @@ def apply_order(objs: list[dict]) -> list[dict]:
 
 
 def apply(client: KubeClient, objs: list[dict], dry_run: bool = False, log=print) -> list[str]:
-    """Create-or-merge every object in dependency order; returns "kind/name" lines."""
+    """``kubectl apply`` every object in dependency order (kubeflow_rm_amd.apply: last-applied
+    annotation + three-way strategic merge patch). ``dry_run``: the same requests with dryRun=All
+    (server-side: validation, admission, defaulting, nothing stored), so a changed object reports
+    "configured" from a real diff. Returns "kind/name verb" lines (created / configured / unchanged)."""
+    from .apply import apply_object
     done = []
     for o in apply_order(objs):
         md = o["metadata"]
-        ref = f"{o['kind']}/{md['name']}" + (f" -n {md['namespace']}" if md.get("namespace") else "")
+        verb, live = apply_object(client, o, dry_run=dry_run)
+        ns = md.get("namespace") or ((live or {}).get("metadata") or {}).get("namespace")
+        ref = f"{o['kind']}/{md['name']}" + (f" -n {ns}" if ns else "")
         if dry_run:
-            try:
-                client.create(o, namespace=md.get("namespace"), dry_run=True)
-                verb = "created (dry run)"
-            except ApiException as e:
-                if e.status != 409:
-                    raise
-                verb = "unchanged (exists)"
-        else:
-            client.apply(o)
-            verb = "applied"
-            if o["kind"] == "CustomResourceDefinition":
-                _wait_crd(client, o)
+            verb += " (server dry run)"
+        elif o["kind"] == "CustomResourceDefinition" and verb != "unchanged":
+            _wait_crd(client, o)
         done.append(f"{ref} {verb}")
         if log:
             log(f"{ref} {verb}")

@@ -746,16 +746,19 @@ Json strategic_merge_patch(const Json& target, const Json& patch, const std::str
     }
     Json out = target;
     for (const auto& item : patch.as_array()) {
-      if (!item.is_object() || !item.has(key)) {
+      // Service ports merge by "port" (container ports by "containerPort", the table's key)
+      const char* k = key;
+      if (field == "ports" && item.is_object() && !item.has(k) && item.has("port")) k = "port";
+      if (!item.is_object() || !item.has(k)) {
         out.push_back(item);
         continue;
       }
-      const Json& kv = item[key];
+      const Json& kv = item[k];
       bool del = item["$patch"].as_string() == "delete";
       auto& arr = out.mut_array();
       bool merged = false;
       for (size_t i = 0; i < arr.size(); ++i) {
-        if (arr[i][key] == kv) {
+        if (arr[i][k] == kv) {
           if (del) {
             arr.erase(arr.begin() + static_cast<long>(i));
           } else {
