@@ -134,6 +134,11 @@ int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, c
                              const float* rstd, void* dx, float* dgamma, float* dbeta,
                              float* workspace, int rows, int hidden, void* stream);
 // the same with dgamma / dbeta written as bf16 when dgb_bf16 (fp32 accumulation)
+// v3: dres (optional, [rows][hidden] bf16, not aliasing dx): dx = dres + the LayerNorm input
+// gradient (a pre-norm residual stream's two gradient contributions in one store)
+int kfamd_layernorm_bwd_bf16_v3(const void* dy, const void* dres, const void* x, const void* gamma,
+                                const float* mean, const float* rstd, void* dx, void* dgamma, void* dbeta,
+                                int dgb_bf16, float* workspace, int rows, int hidden, void* stream);
 int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const void* gamma, const float* mean,
                                 const float* rstd, void* dx, void* dgamma, void* dbeta, int dgb_bf16,
                                 float* workspace, int rows, int hidden, void* stream);

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
                                                      const __bf16* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
+                                                     const __bf16* __restrict__ dres,
                                                      __bf16* __restrict__ dx, int rows) {
   using vec_t = __bf16 __attribute__((ext_vector_type(W)));
   constexpr int H = VPL * 64 * W;
@@ -157,6 +158,8 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
   const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
   const float mu = mean[row], rs = rstd[row];
   vec_t* dxr = reinterpret_cast<vec_t*>(dx + (long long)row * H);
+  // dres: the residual stream's own gradient, added in the store (one pass instead of an add kernel)
+  const vec_t* rr = dres ? reinterpret_cast<const vec_t*>(dres + (long long)row * H) : nullptr;
   if constexpr (VPL < 16) {
     // the widened row (xhat, gamma * dy) stays in registers between the passes
     float xh[VPL][W], gd[VPL][W];
@@ -176,8 +179,14 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
       vec_t o;
+      if (rr) {
+        const vec_t rv = rr[j * 64 + lane];
 #pragma unroll
-      for (int e = 0; e < W; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
+        for (int e = 0; e < W; ++e) o[e] = (__bf16)(fmaf(rs, gd[j][e] - xh[j][e] * c1 - c2, (float)rv[e]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < W; ++e) o[e] = (__bf16)(rs * (gd[j][e] - xh[j][e] * c1 - c2));
+      }
       dxr[j * 64 + lane] = o;
     }
   } else {
@@ -210,11 +219,13 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_wave(const __bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
       const vec_t gv = g8[j * 64 + lane];
+      vec_t rv = {};
+      if (rr) rv = rr[j * 64 + lane];
       vec_t o;
 #pragma unroll
       for (int e = 0; e < W; ++e) {
         const float xh = ((float)xv[j][e] - mu) * rs, gd = (float)dv[j][e] * (float)gv[e];
-        o[e] = (__bf16)(rs * (gd - xh * c1 - c2));
+        o[e] = (__bf16)(fmaf(rs, gd - xh * c1 - c2, (float)rv[e]));
       }
       dxr[j * 64 + lane] = o;
     }
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_block(const __bf16* __restrict_
                                                       const __bf16* __restrict__ gamma,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ rstd,
+                                                      const __bf16* __restrict__ dres,
                                                       __bf16* __restrict__ dx, int hidden) {
   __shared__ float red[4];
   const long long row = blockIdx.x;
@@ -243,7 +255,7 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_block(const __bf16* __restrict_
   __bf16* dxr = dx + row * hidden;
   for (int i = threadIdx.x; i < hidden; i += 256) {
     const float xh = ((float)xr[i] - mu) * rs, g = (float)dyr[i] * (float)gamma[i];
-    dxr[i] = (__bf16)(rs * (g - xh * c1 - c2));
+    dxr[i] = (__bf16)(fmaf(rs, g - xh * c1 - c2, dres ? (float)dres[row * hidden + i] : 0.f));
   }
 }
 
@@ -394,36 +406,40 @@ extern "C" long long kfamd_layernorm_bwd_workspace(int rows, int hidden) {
   return 2LL * nch * hidden * (long long)sizeof(float);
 }
 
-// dgamma / dbeta: fp32, or bf16 (the parameter dtype) when dgb_bf16; sums accumulate in fp32 either way
-extern "C" int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const void* gamma, const float* mean,
-                                           const float* rstd, void* dx, void* dgamma, void* dbeta, int dgb_bf16,
-                                           float* workspace, int rows, int hidden, void* stream) {
+// dgamma / dbeta: fp32, or bf16 (the parameter dtype) when dgb_bf16; sums accumulate in fp32 either way.
+// dres (optional, same layout as dx): dx = dres + the LayerNorm input gradient — the pre-norm
+// residual stream's two gradient contributions summed in the dx store.
+extern "C" int kfamd_layernorm_bwd_bf16_v3(const void* dy, const void* dres, const void* x, const void* gamma,
+                                           const float* mean, const float* rstd, void* dx, void* dgamma, void* dbeta,
+                                           int dgb_bf16, float* workspace, int rows, int hidden, void* stream) {
   if (!dy || !x || !gamma || !mean || !rstd || !dx || rows <= 0 || hidden <= 0) return KFAMD_EINVAL;
+  if (dres == dx) return KFAMD_EINVAL;
   if ((dgamma || dbeta) && !workspace) return KFAMD_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const __bf16* dyp = static_cast<const __bf16*>(dy);
   const __bf16* xp = static_cast<const __bf16*>(x);
   const __bf16* gp = static_cast<const __bf16*>(gamma);
   __bf16* dxp = static_cast<__bf16*>(dx);
+  const __bf16* rp = static_cast<const __bf16*>(dres);
   const int vpl = vpl_for(hidden);
-  const bool vec = vpl && a16(dy) && a16(x) && a16(gamma) && a16(dx);
+  const bool vec = vpl && a16(dy) && a16(x) && a16(gamma) && a16(dx) && (!dres || a16(dres));
   if (vec) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (vpl) {
 #define KFAMD_LN_BWD_CASE(V) \
-  case V: hipLaunchKernelGGL((ln_bwd_dx_wave<V>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+  case V: hipLaunchKernelGGL((ln_bwd_dx_wave<V>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, rows); break;
       KFAMD_FOR_EACH_VPL(KFAMD_LN_BWD_CASE)
 #undef KFAMD_LN_BWD_CASE
     }
-  } else if (const int v4 = vpl4_for(hidden); v4 && a8(dy) && a8(x) && a8(gamma) && a8(dx)) {
+  } else if (const int v4 = vpl4_for(hidden); v4 && a8(dy) && a8(x) && a8(gamma) && a8(dx) && (!dres || a8(dres))) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (v4) {
-      case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 3: hipLaunchKernelGGL((ln_bwd_dx_wave<3, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
-      case 5: hipLaunchKernelGGL((ln_bwd_dx_wave<5, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, dxp, rows); break;
+      case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, rows); break;
+      case 3: hipLaunchKernelGGL((ln_bwd_dx_wave<3, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, rows); break;
+      case 5: hipLaunchKernelGGL((ln_bwd_dx_wave<5, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, rows); break;
     }
   } else {
-    hipLaunchKernelGGL(ln_bwd_dx_block, dim3(rows), dim3(256), 0, s, dyp, xp, gp, mean, rstd, dxp, hidden);
+    hipLaunchKernelGGL(ln_bwd_dx_block, dim3(rows), dim3(256), 0, s, dyp, xp, gp, mean, rstd, rp, dxp, hidden);
   }
   if (dgamma || dbeta) {
     const int nch = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
@@ -435,6 +451,13 @@ extern "C" int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const 
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
+extern "C" int kfamd_layernorm_bwd_bf16_v2(const void* dy, const void* x, const void* gamma, const float* mean,
+                                           const float* rstd, void* dx, void* dgamma, void* dbeta, int dgb_bf16,
+                                           float* workspace, int rows, int hidden, void* stream) {
+  return kfamd_layernorm_bwd_bf16_v3(dy, nullptr, x, gamma, mean, rstd, dx, dgamma, dbeta, dgb_bf16, workspace, rows,
+                                     hidden, stream);
 }
 
 extern "C" int kfamd_layernorm_bwd_bf16(const void* dy, const void* x, const void* gamma, const float* mean,

@@ -21,7 +21,9 @@ from pathlib import Path
 from .client import KubeClient
 
 ROOT = Path(__file__).resolve().parent.parent
-BIN = Path(__file__).resolve().parent / "bin"
+# KFAMD_BIN_DIR: another build of the native binaries (tools/sanitize.sh points it at the TSAN /
+# ASan builds, so the split components run instrumented too)
+BIN = Path(os.environ.get("KFAMD_BIN_DIR") or Path(__file__).resolve().parent / "bin")
 
 
 def kflite_binary() -> Path:

@@ -73,6 +73,15 @@ class LayerNorm(torch.nn.Module):
     def forward(self, x):
         return _layer_norm(x, self.weight, self.bias)
 
+    def with_residual(self, x):
+        """(LayerNorm(x), r) with r = x for the block's residual add: on the HIP path the two gradient
+        contributions to x are summed inside the LayerNorm backward kernel (no separate add)."""
+        if x.is_cuda:
+            from kubeflow_rm_amd import ops
+            if ops.native_enabled():
+                return ops.layer_norm_residual(x, self.weight, self.bias)
+        return self(x), x
+
 
 def _qkv_shard(cfg: GPTConfig, tp: int, rank: int, seed: int, device) -> torch.Tensor:
     full = tpl.full_weight((3 * cfg.d_model, cfg.d_model), seed)
@@ -120,9 +129,12 @@ class Block(torch.nn.Module):
         return self.proj(y.transpose(1, 2).reshape(B, T, h * hd), residual=residual)
 
     def forward(self, x):
-        # both residual adds ride in the output projections' GEMM epilogues (without TP)
-        x = self.attention(self.ln1(x), residual=x)
-        return self.fc2(self.fc1(self.ln2(x)), residual=x)
+        # both residual adds ride in the output projections' GEMM epilogues (without TP); the
+        # residual gradient joins the LayerNorm backward's dx store (LayerNorm.with_residual)
+        h, r = self.ln1.with_residual(x)
+        x = self.attention(h, residual=r)
+        h, r = self.ln2.with_residual(x)
+        return self.fc2(self.fc1(h), residual=r)
 
 
 class GPT(torch.nn.Module):

@@ -59,6 +59,8 @@ _SIGNATURES = {
                                          c_int, c_int, c_vp]),
     "kfamd_layernorm_bwd_bf16_v2": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
                                             c_int, c_vp]),
+    "kfamd_layernorm_bwd_bf16_v3": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                                            c_int, c_int, c_vp]),
     "kfamd_allreduce_oneshot_flag_bytes": (c_ll, [c_int, c_int]),
     "kfamd_allreduce_oneshot_blocks": (c_int, [c_ll, c_int]),
     "kfamd_allreduce_oneshot_set_timeout_ms": (None, [c_int]),

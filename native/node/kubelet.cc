@@ -20,6 +20,8 @@
 #include <cerrno>
 #include <cstring>
 #include <fstream>
+#include <functional>
+#include <optional>
 #include <regex>
 #include <set>
 
@@ -915,569 +917,612 @@ bool Kubelet::read_logs(const std::string& ns, const std::string& pod, const std
 }
 
 // ---- reconcile ---------------------------------------------------------------------------------
-Result Kubelet::reconcile(const Request& r, std::string* err) {
-  if (stopping_) return {};
+// ---- one reconcile pass, in units ------------------------------------------
+// reconcile() = look up the runtime -> termination | admission (sandbox, GPUs, volumes, containers)
+// -> init containers -> long-running containers (start, exit/restart, probes) -> readiness report
+// -> status. Everything one pass shares is in PodSync.
+
+namespace {
+// Until a pod is Ready the kubelet re-syncs it every 5 ms (cold start is on the notebook's critical
+// path; a sync of an unchanged pod costs no API call), afterwards at the 1 s relist.
+constexpr double kStartupPoll = 0.005;
+
+Json terminated_state(const ContainerRt& cr) {
+  return Json{{"terminated", Json{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at},
+                                  {"finishedAt", cr.finished_at}, {"message", cr.message}}}};
+}
+
+// a running container whose process ended: record its termination (false when it still runs)
+bool handle_exit(ContainerRt& cr) {
+  int code = 0;
+  std::string reason;
+  if (cr.pid <= 0 || cr.state != "running" || !reap_container(cr.pid, cr.zfd, cr.zorphan, code, reason)) return false;
+  cr.pid = -1;
+  cr.state = "terminated";
+  cr.exit_code = code;
+  cr.reason = reason;
+  cr.finished_at = ms_now();
+  cr.ready = false;
+  std::string msg;
+  if (read_file(cr.term_path, msg)) cr.message = msg.substr(0, 4096);
+  else cr.message.clear();
+  return true;
+}
+
+Json container_status(const ContainerRt& cr, const Json& c) {
+  Json state;
+  if (cr.state == "running") {
+    state = Json{{"running", Json{{"startedAt", cr.started_at}}}};
+  } else if (cr.state == "terminated") {
+    Json t{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at}, {"finishedAt", cr.finished_at},
+           {"containerID", "kflite://" + cr.name}};
+    if (!cr.message.empty()) t["message"] = cr.message;
+    state = Json{{"terminated", t}};
+  } else {
+    Json w{{"reason", cr.reason.empty() ? "ContainerCreating" : cr.reason}};
+    if (!cr.message.empty()) w["message"] = cr.message;
+    state = Json{{"waiting", w}};
+  }
+  Json s{{"name", cr.name}, {"state", state}, {"lastState", cr.last_state}, {"ready", cr.ready},
+         {"restartCount", cr.restarts}, {"image", c["image"]}, {"imageID", "kflite-recipe://" + c["image"].as_string()},
+         {"started", cr.state == "running"}};
+  if (cr.pid > 0) s["containerID"] = "kflite://" + std::to_string(cr.pid);
+  return s;
+}
+
+bool wants_pod_gpus(const Json& c) {
+  return resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 || shares_pod_gpus(c);
+}
+}  // namespace
+
+struct Kubelet::PodSync {
+  const Request& r;
   Json pod;
-  ApiError e = c_->get("v1", "Pod", r.ns, r.name, pod);
   std::shared_ptr<PodRuntime> rt;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    auto k = key_to_uid_.find(r.ns + "/" + r.name);
-    if (k != key_to_uid_.end()) {
-      auto it = pods_.find(k->second);
-      if (it != pods_.end()) rt = it->second;
-      if (e.code == 404 || (!e && pod.str_at({"metadata", "uid"}) != k->second)) {
-        // pod object is gone (or replaced by a new incarnation): tear the old sandbox down
-        if (rt) {
-          std::lock_guard<std::mutex> pl(rt->op_mu);
-          terminate_pod(*rt, 0);
-          alloc_->release(rt->uid);
-          rdzv_ports_.erase(rt->rdzv_port);
-          prober_->forget_pod(rt->uid);
-          pods_.erase(rt->uid);
-        }
-        key_to_uid_.erase(k);
-        rt.reset();
-        if (e.code == 404) return {};
-      }
-    }
-  }
-  if (e.code == 404) return {};
-  if (e) {
-    *err = e.message;
-    return {};
-  }
-  if (pod.at_path({"spec", "nodeName"}).as_string() != cfg_.node_name) return {};
-  std::unique_lock<std::mutex> pod_lock;
-  if (rt) {
-    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
-    if (stopping_) return {};
-  }
-  const std::string uid = pod.str_at({"metadata", "uid"});
-  const std::string restart_policy = pod.at_path({"spec", "restartPolicy"}).as_string_or("Always");
-
-  // ---- termination ------------------------------------------------------------------------------
-  if (pod.at_path({"metadata", "deletionTimestamp"}).is_string()) {
-    if (rt) {
-      if (!rt->announced_kill) {
-        rt->announced_kill = true;
-        for (auto& c : rt->main)
-          if (c.state == "running") rec_->event(pod, "Normal", "Killing", "Stopping container " + c.name);
-      }
-      terminate_pod(*rt, pod.at_path({"metadata", "deletionGracePeriodSeconds"}).as_int(30));
-      alloc_->release(uid);
-      std::lock_guard<std::mutex> g(mu_);
-      rdzv_ports_.erase(rt->rdzv_port);
-      prober_->forget_pod(uid);
-      pods_.erase(uid);
-      key_to_uid_.erase(r.ns + "/" + r.name);
-    }
-    ApiError de = c_->remove("v1", "Pod", r.ns, r.name, "", 0);
-    if (de && de.code != 404) *err = de.message;
-    return {};
-  }
-  const std::string phase = pod.at_path({"status", "phase"}).as_string();
-  if (!rt && (phase == "Succeeded" || phase == "Failed")) return {};
-
-  // ---- admission: sandbox, IP, GPUs, volumes ------------------------------------------------------
-  if (!rt) {
-    rt = std::make_shared<PodRuntime>();
-    rt->uid = uid;
-    rt->ns = r.ns;
-    rt->name = r.name;
-    rt->dir = cfg_.root_dir + "/pods/" + r.ns + "_" + r.name + "_" + uid.substr(0, 8);
-    make_dirs(rt->dir + "/rootfs");
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      uint32_t n = next_ip_++;
-      rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
-    }
-    rt->start_time = ms_now();
-    // device plugin Allocate: topology-aware GPU placement
-    int want_gpus = 0;
-    for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
-      want_gpus += static_cast<int>(resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})));
-    if (want_gpus > 0) {
-      if (!alloc_->allocate(uid, want_gpus, rt->gpus)) {
-        rt->gpu_ok = false;
-      } else {
-        std::vector<std::string> ids, ring;
-        for (int d : rt->gpus.devices) ids.push_back(std::to_string(d));
-        for (int d : rt->gpus.ring) ring.push_back(std::to_string(d));
-        if (rt->gpus.devices.size() > 1) rt->rdzv_port = alloc_rdzv_port();
-        c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
-          o["metadata"]["annotations"][ANNOTATION_GPU_IDS] = join(ids, ",");
-          o["metadata"]["annotations"][ANNOTATION_XGMI_RING] = join(ring, ",");
-          o["metadata"]["annotations"]["amd.com/gpu-placement"] = rt->gpus.reason;
-          if (rt->rdzv_port) o["metadata"]["annotations"]["kfamd.io/rendezvous"] = rt->ip + ":" + std::to_string(rt->rdzv_port);
-          return true;
-        });
-      }
-    }
-    // volumes
-    std::map<std::string, std::string> vol_dirs;
-    for (const auto& v : pod.at_path({"spec", "volumes"}).as_array()) {
-      const std::string vname = v["name"].as_string();
-      std::string dir;
-      if (v["persistentVolumeClaim"].is_object()) {
-        dir = cfg_.root_dir + "/pv/" + r.ns + "/" + v.at_path({"persistentVolumeClaim", "claimName"}).as_string();
-      } else if (v["hostPath"].is_object()) {
-        dir = v.at_path({"hostPath", "path"}).as_string();
-      } else {
-        dir = rt->dir + "/volumes/" + vname;
-      }
-      make_dirs(dir);
-      if (v["configMap"].is_object() || v["secret"].is_object()) {
-        const bool secret = v["secret"].is_object();
-        Json src;
-        const std::string sname = secret ? v.at_path({"secret", "secretName"}).as_string() : v.at_path({"configMap", "name"}).as_string();
-        if (!c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, sname, src)) {
-          for (const auto& m : src["data"].as_object())
-            write_file(dir + "/" + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
-          if (secret)
-            for (const auto& m : src["stringData"].as_object()) write_file(dir + "/" + m.first, m.second.as_string());
-        }
-      }
-      vol_dirs[vname] = dir;
-    }
-    auto build = [&](const Json& list, bool init, std::vector<ContainerRt>& out) {
-      for (const auto& c : list.as_array()) {
-        ContainerRt cr;
-        cr.name = c["name"].as_string();
-        cr.init = init;
-        cr.sidecar = init && c["restartPolicy"].as_string() == "Always";
-        cr.log_path = rt->dir + "/" + cr.name + ".log";
-        cr.term_path = rt->dir + "/" + cr.name + ".termination-log";
-        for (const auto& vm : c["volumeMounts"].as_array()) {
-          auto it = vol_dirs.find(vm["name"].as_string());
-          if (it == vol_dirs.end()) continue;
-          std::string host = it->second;
-          if (!vm["subPath"].as_string().empty()) {
-            host += "/" + vm["subPath"].as_string();
-            if (!file_exists(host)) make_dirs(host);
-          }
-          rt->mounts[vm["mountPath"].as_string()] = host;
-        }
-        out.push_back(cr);
-      }
-    };
-    build(pod.at_path({"spec", "initContainers"}), true, rt->init);
-    build(pod.at_path({"spec", "containers"}), false, rt->main);
-    // materialise mount points inside the pod rootfs as symlinks
-    for (const auto& m : rt->mounts) {
-      std::string link = rt->dir + "/rootfs" + m.first;
-      size_t slash = link.rfind('/');
-      make_dirs(link.substr(0, slash));
-      ::unlink(link.c_str());
-      if (::symlink(m.second.c_str(), link.c_str()) != 0) make_dirs(link);
-    }
-    std::lock_guard<std::mutex> g(mu_);
-    pods_[uid] = rt;
-    key_to_uid_[r.ns + "/" + r.name] = uid;
-  }
-  if (!pod_lock.owns_lock()) {
-    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
-    if (stopping_) return {};
-  }
-
-  if (!rt->gpu_ok) {
-    // UnexpectedAdmissionError: the device plugin could not satisfy the request
-    c_->update_with_retry(
-        "v1", "Pod", r.ns, r.name,
-        [&](Json& o) {
-          if (o.at_path({"status", "phase"}).as_string() == "Failed") return false;
-          o["status"]["phase"] = "Failed";
-          o["status"]["reason"] = "UnexpectedAdmissionError";
-          o["status"]["message"] = "Allocate failed due to requested number of devices unavailable for amd.com/gpu";
-          return true;
-        },
-        true);
-    return {};
-  }
-
-  // ---- run containers -------------------------------------------------------------------------------
-  const Json& spec = pod["spec"];
-  auto container_spec = [&](const ContainerRt& cr) -> const Json& {
-    for (const auto& c : spec[cr.init ? "initContainers" : "containers"].as_array())
+  std::string uid, restart_policy;
+  double next_wake = 1.0;
+  const Json& container_spec(const ContainerRt& cr) const {
+    for (const auto& c : pod["spec"][cr.init ? "initContainers" : "containers"].as_array())
       if (c["name"].as_string() == cr.name) return c;
     static const Json empty;
     return empty;
-  };
-  auto env_for = [&](const Json& c, std::vector<std::string>& envv, std::map<std::string, std::string>& envm) {
-    auto set = [&](const std::string& k, const std::string& v) { envm[k] = v; };
-    for (char** e = environ; *e; ++e) {
-      std::string kv = *e;
-      size_t eq = kv.find('=');
-      if (eq == std::string::npos) continue;
-      std::string k = kv.substr(0, eq);
-      // pass through the host runtime basics only (containers do not inherit the kubelet env)
-      if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || starts_with(k, "HSA_") ||
-          starts_with(k, "KFAMD_") || starts_with(k, "ROCM") || k == "OMP_NUM_THREADS" || k == "PYTHONUNBUFFERED")
-        set(k, kv.substr(eq + 1));
+  }
+};
+
+// the runtime of r's pod; tears down a runtime whose pod is gone or was replaced (new uid)
+std::shared_ptr<Kubelet::PodRuntime> Kubelet::lookup_runtime(const Request& r, const ApiError& e, const Json& pod) {
+  std::shared_ptr<PodRuntime> rt;
+  std::lock_guard<std::mutex> g(mu_);
+  auto k = key_to_uid_.find(r.ns + "/" + r.name);
+  if (k == key_to_uid_.end()) return rt;
+  auto it = pods_.find(k->second);
+  if (it != pods_.end()) rt = it->second;
+  if (e.code == 404 || (!e && pod.str_at({"metadata", "uid"}) != k->second)) {
+    if (rt) {
+      std::lock_guard<std::mutex> pl(rt->op_mu);
+      terminate_pod(*rt, 0);
+      alloc_->release(rt->uid);
+      rdzv_ports_.erase(rt->rdzv_port);
+      prober_->forget_pod(rt->uid);
+      pods_.erase(rt->uid);
     }
-    const std::string rootfs = rt->dir + "/rootfs";
-    std::string home = rootfs + "/home/jovyan";
-    auto hm = rt->mounts.find("/home/jovyan");
-    if (hm != rt->mounts.end()) home = hm->second;
-    make_dirs(home);
-    set("HOME", home);
-    set("HOSTNAME", r.name);
-    set("POD_NAME", r.name);
-    set("POD_NAMESPACE", r.ns);
-    set("POD_IP", rt->ip);
-    set("KFAMD_POD_DIR", rt->dir);
-    set("KFAMD_ROOTFS", rootfs);
-    set("KFAMD_TERMINATION_LOG", rt->dir + "/" + c["name"].as_string() + ".termination-log");
-    Json mounts = Json::object();
-    for (const auto& m : rt->mounts) mounts[m.first] = m.second;
-    set("KFAMD_VOLUME_MOUNTS", mounts.dump());
-    set("PYTHONPATH", cfg_.repo_root);
-    set("PYTHONUNBUFFERED", "1");
-    {
-      std::vector<std::string> ports;
-      for (const auto& p : c["ports"].as_array()) ports.push_back(std::to_string(p["containerPort"].as_int()));
-      set("KFAMD_CONTAINER_PORTS", join(ports, ","));
-      set("KFAMD_CONTAINER_NAME", c["name"].as_string());
+    key_to_uid_.erase(k);
+    rt.reset();
+  }
+  return rt;
+}
+
+// deletionTimestamp set: stop the containers (grace period), release the node's resources and
+// remove the object
+void Kubelet::finish_deletion(const Request& r, const Json& pod, const std::shared_ptr<PodRuntime>& rt,
+                              std::string* err) {
+  if (rt) {
+    if (!rt->announced_kill) {
+      rt->announced_kill = true;
+      for (auto& c : rt->main)
+        if (c.state == "running") rec_->event(pod, "Normal", "Killing", "Stopping container " + c.name);
     }
-    Url u;
-    if (Url::parse(cfg_.api_url, u)) {
-      set("KUBERNETES_SERVICE_HOST", u.host);
-      set("KUBERNETES_SERVICE_PORT", std::to_string(u.port));
-      set("KFAMD_API_URL", cfg_.api_url);
+    terminate_pod(*rt, pod.at_path({"metadata", "deletionGracePeriodSeconds"}).as_int(30));
+    alloc_->release(rt->uid);
+    std::lock_guard<std::mutex> g(mu_);
+    rdzv_ports_.erase(rt->rdzv_port);
+    prober_->forget_pod(rt->uid);
+    pods_.erase(rt->uid);
+    key_to_uid_.erase(r.ns + "/" + r.name);
+  }
+  ApiError de = c_->remove("v1", "Pod", r.ns, r.name, "", 0);
+  if (de && de.code != 404) *err = de.message;
+}
+
+// device plugin Allocate: topology-aware GPU placement, recorded on the pod
+void Kubelet::allocate_gpus(PodRuntime& rt, const Json& pod) {
+  int want = 0;
+  for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
+    want += static_cast<int>(resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})));
+  if (want <= 0) return;
+  if (!alloc_->allocate(rt.uid, want, rt.gpus)) {
+    rt.gpu_ok = false;
+    return;
+  }
+  std::vector<std::string> ids, ring;
+  for (int d : rt.gpus.devices) ids.push_back(std::to_string(d));
+  for (int d : rt.gpus.ring) ring.push_back(std::to_string(d));
+  if (rt.gpus.devices.size() > 1) rt.rdzv_port = alloc_rdzv_port();
+  c_->update_with_retry("v1", "Pod", rt.ns, rt.name, [&](Json& o) {
+    o["metadata"]["annotations"][ANNOTATION_GPU_IDS] = join(ids, ",");
+    o["metadata"]["annotations"][ANNOTATION_XGMI_RING] = join(ring, ",");
+    o["metadata"]["annotations"]["amd.com/gpu-placement"] = rt.gpus.reason;
+    if (rt.rdzv_port) o["metadata"]["annotations"]["kfamd.io/rendezvous"] = rt.ip + ":" + std::to_string(rt.rdzv_port);
+    return true;
+  });
+}
+
+// volumes (emptyDir / PVC / hostPath / configMap / secret) under the sandbox: volume name -> host dir
+std::map<std::string, std::string> Kubelet::prepare_volumes(PodRuntime& rt, const Json& pod) {
+  std::map<std::string, std::string> vol_dirs;
+  for (const auto& v : pod.at_path({"spec", "volumes"}).as_array()) {
+    const std::string vname = v["name"].as_string();
+    std::string dir;
+    if (v["persistentVolumeClaim"].is_object()) {
+      dir = cfg_.root_dir + "/pv/" + rt.ns + "/" + v.at_path({"persistentVolumeClaim", "claimName"}).as_string();
+    } else if (v["hostPath"].is_object()) {
+      dir = v.at_path({"hostPath", "path"}).as_string();
+    } else {
+      dir = rt.dir + "/volumes/" + vname;
     }
-    // GPU wiring from the device plugin allocation (and for a container that shares the pod's
-    // GPUs without a second allocation: the gpu-readiness sidecar)
-    const bool wants_gpu = resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 ||
-                           shares_pod_gpus(c);
-    if (wants_gpu && !rt->gpus.devices.empty()) {
-      const Json genv = gpu_env_for(rt->gpus, alloc_->topology(), rt->gpus.devices.size() > 1, rt->ip, rt->rdzv_port);
-      for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
-      const auto local = alloc_->topology().local_cpus(rt->gpus.devices);
-      if (cfg_.numa_pinning && !local.empty()) set("KFAMD_CPU_AFFINITY", format_cpulist(local));
-      // Node-level code-object cache shared by every GPU container (the device plugin's Allocate
-      // response carries this env + mount). comgr caches the runtime's device-code builds under
-      // $HOME/.cache/comgr by default, and every pod starts with an empty HOME: that miss cost
-      // ~140 ms of each cold start on MI355X (profiles/r1_coldstart2/README.md).
-      // Keyed per namespace: profiles are tenants, and a cache one tenant can write must never
-      // feed code objects to another tenant's pods (a namespace's own pods share its warm cache).
-      const std::string cache = cfg_.root_dir + "/gpu-cache/comgr/" + r.ns;
-      make_dirs(cache);
-      set("AMD_COMGR_CACHE_DIR", cache);
-    }
-    for (const auto& ef : c["envFrom"].as_array()) {
-      const bool secret = ef["secretRef"].is_object();
-      const std::string name = secret ? ef.at_path({"secretRef", "name"}).as_string() : ef.at_path({"configMapRef", "name"}).as_string();
+    make_dirs(dir);
+    if (v["configMap"].is_object() || v["secret"].is_object()) {
+      const bool secret = v["secret"].is_object();
       Json src;
-      if (c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, name, src)) continue;
-      for (const auto& m : src["data"].as_object())
-        set(ef["prefix"].as_string() + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
-    }
-    for (const auto& ev : c["env"].as_array()) {
-      const std::string name = ev["name"].as_string();
-      if (ev.has("value")) {
-        set(name, expand_vars(ev["value"].as_string(), envm));
-        continue;
+      const std::string sname = secret ? v.at_path({"secret", "secretName"}).as_string() : v.at_path({"configMap", "name"}).as_string();
+      if (!c_->get("v1", secret ? "Secret" : "ConfigMap", rt.ns, sname, src)) {
+        for (const auto& m : src["data"].as_object())
+          write_file(dir + "/" + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
+        if (secret)
+          for (const auto& m : src["stringData"].as_object()) write_file(dir + "/" + m.first, m.second.as_string());
       }
-      const Json& vf = ev["valueFrom"];
-      if (vf["fieldRef"].is_object()) {
-        const std::string path = vf.at_path({"fieldRef", "fieldPath"}).as_string();
-        if (path == "metadata.name") set(name, r.name);
-        else if (path == "metadata.namespace") set(name, r.ns);
-        else if (path == "status.podIP") set(name, rt->ip);
-        else if (path == "spec.nodeName") set(name, cfg_.node_name);
-        else if (path == "metadata.uid") set(name, uid);
-        else if (starts_with(path, "metadata.annotations['")) set(name, annotation(pod, path.substr(22, path.size() - 24)));
-        else if (starts_with(path, "metadata.labels['")) set(name, label(pod, path.substr(17, path.size() - 19)));
-      } else if (vf["configMapKeyRef"].is_object() || vf["secretKeyRef"].is_object()) {
-        const bool secret = vf["secretKeyRef"].is_object();
-        const Json& ref = secret ? vf["secretKeyRef"] : vf["configMapKeyRef"];
-        Json src;
-        if (!c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, ref["name"].as_string(), src)) {
-          const Json& v = src["data"][ref["key"].as_string()];
-          if (v.is_string()) set(name, secret ? base64_decode(v.as_string()) : v.as_string());
+    }
+    vol_dirs[vname] = dir;
+  }
+  return vol_dirs;
+}
+
+// container runtimes in spec order, with their volume mounts; mount points materialised in the
+// pod rootfs as symlinks
+void Kubelet::build_containers(PodRuntime& rt, const Json& pod, const std::map<std::string, std::string>& vol_dirs) {
+  auto build = [&](const Json& list, bool init, std::vector<ContainerRt>& out) {
+    for (const auto& c : list.as_array()) {
+      ContainerRt cr;
+      cr.name = c["name"].as_string();
+      cr.init = init;
+      cr.sidecar = init && c["restartPolicy"].as_string() == "Always";
+      cr.log_path = rt.dir + "/" + cr.name + ".log";
+      cr.term_path = rt.dir + "/" + cr.name + ".termination-log";
+      for (const auto& vm : c["volumeMounts"].as_array()) {
+        auto it = vol_dirs.find(vm["name"].as_string());
+        if (it == vol_dirs.end()) continue;
+        std::string host = it->second;
+        if (!vm["subPath"].as_string().empty()) {
+          host += "/" + vm["subPath"].as_string();
+          if (!file_exists(host)) make_dirs(host);
         }
-      } else if (vf["resourceFieldRef"].is_object()) {
-        const std::string res = vf.at_path({"resourceFieldRef", "resource"}).as_string();
-        auto parts = split(res, '.');
-        if (parts.size() == 2) set(name, c.at_path({"resources", parts[0].c_str(), parts[1].c_str()}).as_string());
+        rt.mounts[vm["mountPath"].as_string()] = host;
       }
+      out.push_back(cr);
     }
-    envv.clear();
-    for (auto& kv : envm) envv.push_back(kv.first + "=" + kv.second);
   };
-  auto start_container = [&](ContainerRt& cr) {
-    const Json& c = container_spec(cr);
+  build(pod.at_path({"spec", "initContainers"}), true, rt.init);
+  build(pod.at_path({"spec", "containers"}), false, rt.main);
+  for (const auto& m : rt.mounts) {
+    std::string link = rt.dir + "/rootfs" + m.first;
+    size_t slash = link.rfind('/');
+    make_dirs(link.substr(0, slash));
+    ::unlink(link.c_str());
+    if (::symlink(m.second.c_str(), link.c_str()) != 0) make_dirs(link);
+  }
+}
+
+// admission of a new pod: sandbox dir, pod IP, GPUs, volumes, containers; registered on the node
+std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json& pod) {
+  auto rt = std::make_shared<PodRuntime>();
+  rt->uid = pod.str_at({"metadata", "uid"});
+  rt->ns = r.ns;
+  rt->name = r.name;
+  rt->dir = cfg_.root_dir + "/pods/" + r.ns + "_" + r.name + "_" + rt->uid.substr(0, 8);
+  make_dirs(rt->dir + "/rootfs");
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    uint32_t n = next_ip_++;
+    rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
+  }
+  rt->start_time = ms_now();
+  allocate_gpus(*rt, pod);
+  build_containers(*rt, pod, prepare_volumes(*rt, pod));
+  std::lock_guard<std::mutex> g(mu_);
+  pods_[rt->uid] = rt;
+  key_to_uid_[r.ns + "/" + r.name] = rt->uid;
+  return rt;
+}
+
+// UnexpectedAdmissionError: the device plugin could not satisfy the request
+void Kubelet::fail_admission(const Request& r) {
+  c_->update_with_retry(
+      "v1", "Pod", r.ns, r.name,
+      [&](Json& o) {
+        if (o.at_path({"status", "phase"}).as_string() == "Failed") return false;
+        o["status"]["phase"] = "Failed";
+        o["status"]["reason"] = "UnexpectedAdmissionError";
+        o["status"]["message"] = "Allocate failed due to requested number of devices unavailable for amd.com/gpu";
+        return true;
+      },
+      true);
+}
+
+// the environment of container c (host basics, downward API, GPU wiring, envFrom, env)
+void Kubelet::container_env(const PodSync& s, const Json& c, std::vector<std::string>& envv,
+                            std::map<std::string, std::string>& envm) {
+  const PodRuntime& rt = *s.rt;
+  const Request& r = s.r;
+  auto set = [&](const std::string& k, const std::string& v) { envm[k] = v; };
+  for (char** e = environ; *e; ++e) {
+    std::string kv = *e;
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos) continue;
+    std::string k = kv.substr(0, eq);
+    // pass through the host runtime basics only (containers do not inherit the kubelet env)
+    if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || starts_with(k, "HSA_") ||
+        starts_with(k, "KFAMD_") || starts_with(k, "ROCM") || k == "OMP_NUM_THREADS" || k == "PYTHONUNBUFFERED")
+      set(k, kv.substr(eq + 1));
+  }
+  const std::string rootfs = rt.dir + "/rootfs";
+  std::string home = rootfs + "/home/jovyan";
+  auto hm = rt.mounts.find("/home/jovyan");
+  if (hm != rt.mounts.end()) home = hm->second;
+  make_dirs(home);
+  set("HOME", home);
+  set("HOSTNAME", r.name);
+  set("POD_NAME", r.name);
+  set("POD_NAMESPACE", r.ns);
+  set("POD_IP", rt.ip);
+  set("KFAMD_POD_DIR", rt.dir);
+  set("KFAMD_ROOTFS", rootfs);
+  set("KFAMD_TERMINATION_LOG", rt.dir + "/" + c["name"].as_string() + ".termination-log");
+  Json mounts = Json::object();
+  for (const auto& m : rt.mounts) mounts[m.first] = m.second;
+  set("KFAMD_VOLUME_MOUNTS", mounts.dump());
+  set("PYTHONPATH", cfg_.repo_root);
+  set("PYTHONUNBUFFERED", "1");
+  {
+    std::vector<std::string> ports;
+    for (const auto& p : c["ports"].as_array()) ports.push_back(std::to_string(p["containerPort"].as_int()));
+    set("KFAMD_CONTAINER_PORTS", join(ports, ","));
+    set("KFAMD_CONTAINER_NAME", c["name"].as_string());
+  }
+  Url u;
+  if (Url::parse(cfg_.api_url, u)) {
+    set("KUBERNETES_SERVICE_HOST", u.host);
+    set("KUBERNETES_SERVICE_PORT", std::to_string(u.port));
+    set("KFAMD_API_URL", cfg_.api_url);
+  }
+  // GPU wiring from the device plugin allocation (and for a container that shares the pod's GPUs
+  // without a second allocation: the gpu-readiness sidecar)
+  if (wants_pod_gpus(c) && !rt.gpus.devices.empty()) {
+    const Json genv = gpu_env_for(rt.gpus, alloc_->topology(), rt.gpus.devices.size() > 1, rt.ip, rt.rdzv_port);
+    for (const auto& ev : genv.as_array()) set(ev["name"].as_string(), ev["value"].as_string());
+    const auto local = alloc_->topology().local_cpus(rt.gpus.devices);
+    if (cfg_.numa_pinning && !local.empty()) set("KFAMD_CPU_AFFINITY", format_cpulist(local));
+    // Node-level code-object cache shared by every GPU container (the device plugin's Allocate
+    // response carries this env + mount). comgr caches the runtime's device-code builds under
+    // $HOME/.cache/comgr by default, and every pod starts with an empty HOME: that miss cost
+    // ~140 ms of each cold start on MI355X (profiles/r1_coldstart2/README.md).
+    // Keyed per namespace: profiles are tenants, and a cache one tenant can write must never
+    // feed code objects to another tenant's pods (a namespace's own pods share its warm cache).
+    const std::string cache = cfg_.root_dir + "/gpu-cache/comgr/" + r.ns;
+    make_dirs(cache);
+    set("AMD_COMGR_CACHE_DIR", cache);
+  }
+  for (const auto& ef : c["envFrom"].as_array()) {
+    const bool secret = ef["secretRef"].is_object();
+    const std::string name = secret ? ef.at_path({"secretRef", "name"}).as_string() : ef.at_path({"configMapRef", "name"}).as_string();
+    Json src;
+    if (c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, name, src)) continue;
+    for (const auto& m : src["data"].as_object())
+      set(ef["prefix"].as_string() + m.first, secret ? base64_decode(m.second.as_string()) : m.second.as_string());
+  }
+  for (const auto& ev : c["env"].as_array()) {
+    const std::string name = ev["name"].as_string();
+    if (ev.has("value")) {
+      set(name, expand_vars(ev["value"].as_string(), envm));
+      continue;
+    }
+    const Json& vf = ev["valueFrom"];
+    if (vf["fieldRef"].is_object()) {
+      const std::string path = vf.at_path({"fieldRef", "fieldPath"}).as_string();
+      if (path == "metadata.name") set(name, r.name);
+      else if (path == "metadata.namespace") set(name, r.ns);
+      else if (path == "status.podIP") set(name, rt.ip);
+      else if (path == "spec.nodeName") set(name, cfg_.node_name);
+      else if (path == "metadata.uid") set(name, s.uid);
+      else if (starts_with(path, "metadata.annotations['")) set(name, annotation(s.pod, path.substr(22, path.size() - 24)));
+      else if (starts_with(path, "metadata.labels['")) set(name, label(s.pod, path.substr(17, path.size() - 19)));
+    } else if (vf["configMapKeyRef"].is_object() || vf["secretKeyRef"].is_object()) {
+      const bool secret = vf["secretKeyRef"].is_object();
+      const Json& ref = secret ? vf["secretKeyRef"] : vf["configMapKeyRef"];
+      Json src;
+      if (!c_->get("v1", secret ? "Secret" : "ConfigMap", r.ns, ref["name"].as_string(), src)) {
+        const Json& v = src["data"][ref["key"].as_string()];
+        if (v.is_string()) set(name, secret ? base64_decode(v.as_string()) : v.as_string());
+      }
+    } else if (vf["resourceFieldRef"].is_object()) {
+      const std::string res = vf.at_path({"resourceFieldRef", "resource"}).as_string();
+      auto parts = split(res, '.');
+      if (parts.size() == 2) set(name, c.at_path({"resources", parts[0].c_str(), parts[1].c_str()}).as_string());
+    }
+  }
+  envv.clear();
+  for (auto& kv : envm) envv.push_back(kv.first + "=" + kv.second);
+}
+
+// a container's process: forked from the recipe's zygote when one serves it, else a fresh exec
+void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
+  PodRuntime& rt = *s.rt;
+  const Json& c = s.container_spec(cr);
+  std::vector<std::string> envv;
+  std::map<std::string, std::string> envm;
+  container_env(s, c, envv, envm);
+  std::string why, zygote;
+  std::vector<std::string> argv = resolve_argv(c, &why, &zygote);
+  for (auto& a : argv) a = expand_vars(a, envm);
+  std::string wd = c["workingDir"].as_string();
+  std::string cwd = rt.dir + "/rootfs";
+  if (!wd.empty()) {
+    auto m = rt.mounts.find(wd);
+    cwd = m != rt.mounts.end() ? m->second : rt.dir + "/rootfs" + wd;
+    make_dirs(cwd);
+    // follow a symlinked mount point
+    char buf[4096];
+    if (!realpath(cwd.c_str(), buf)) make_dirs(cwd);
+  }
+  ::unlink(cr.term_path.c_str());
+  std::string serr;
+  {
+    std::ofstream lf(cr.log_path, std::ios::app);
+    lf << "# kflite: starting " << cr.name << " (" << why << "): " << join(argv, " ") << "\n";
+  }
+  // topology-manager "single-numa-node"-style placement for GPU containers: the process tree runs
+  // on the CPUs local to its GPUs (host<->HBM copies, RCCL proxy threads, data loaders)
+  std::vector<int> cpus;
+  if (cfg_.numa_pinning && !rt.gpus.devices.empty() && wants_pod_gpus(c)) cpus = alloc_->topology().local_cpus(rt.gpus.devices);
+  pid_t pid = -1;
+  cr.zfd = -1;
+  cr.zorphan = false;
+  // a recipe with a zygote forks from the pre-imported interpreter when one serves it ('python -m'
+  // containers only); otherwise, or when it does not answer, a fresh interpreter as always
+  Zygote zy;
+  if (!zygote.empty()) {
+    std::lock_guard<std::mutex> g(zy_mu_);
+    auto it = zygotes_.find(zygote);
+    if (it != zygotes_.end()) zy = it->second;
+  }
+  if (zy.pid > 0 && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
+    std::string zerr;
+    pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
+    if (pid > 0) {
+      std::ofstream lf(cr.log_path, std::ios::app);
+      lf << "# kflite: forked from zygote " << zy.pid << " (preloaded " << zygote << ")\n";
+    } else if (!zerr.empty()) {
+      std::ofstream lf(cr.log_path, std::ios::app);
+      lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";
+    }
+  }
+  static const auto starts = Registry::global().counter(
+      "kubelet_container_starts_total", "container processes started, by how: zygote fork or fresh exec", {"mode"});
+  if (pid > 0) starts->inc({"zygote"});
+  if (pid < 0) {
+    pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
+    if (pid > 0) starts->inc({"fresh"});
+  }
+  if (pid < 0) {
+    cr.state = "waiting";
+    cr.reason = "CreateContainerError";
+    cr.message = serr;
+    rec_->event(s.pod, "Warning", "Failed", "Error: " + serr);
+    cr.backoff_until = now_seconds() + cfg_.restart_backoff;
+    return;
+  }
+  cr.pid = pid;
+  cr.state = "running";
+  cr.reason = "";
+  cr.envv = envv;
+  cr.cwd = cwd;
+  cr.cpus = cpus;
+  cr.started_at = ms_now();
+  if (cr.zfd >= 0) {
+    const int dfd = ::fcntl(cr.zfd, F_DUPFD_CLOEXEC, 0);  // the watch closes its own copy
+    if (dfd >= 0) watch_fd(dfd, s.r.ns, s.r.name);
+  } else {
+    watch_exit(pid, s.r.ns, s.r.name);
+  }
+  cr.run_started = now_seconds();
+  cr.probe_gen = Prober::next_generation();
+  cr.ready = false;
+  cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
+  const Json& sp = c["startupProbe"];
+  cr.started_probe_ok = !sp.is_object();
+  cr.next_startup_probe = now_seconds() + static_cast<double>(probe_i(sp, "initialDelaySeconds", 0));
+  cr.next_ready_probe = now_seconds() + static_cast<double>(probe_i(c["readinessProbe"], "initialDelaySeconds", 0));
+  cr.next_live_probe = now_seconds() + static_cast<double>(probe_i(c["livenessProbe"], "initialDelaySeconds", 0));
+  rec_->event(s.pod, "Normal", "Started", "Started container " + cr.name);
+}
+
+// The probe as a self-contained closure (copies of the spec, the pod IP and the container env): it
+// runs on a Prober thread, never on a reconcile worker.
+std::function<bool()> Kubelet::make_probe(const PodSync& s, const Json& probe, const Json& c) {
+  const PodRuntime& rt = *s.rt;
+  const int timeout = static_cast<int>(probe_i(probe, "timeoutSeconds", 1)) * 1000;
+  auto port_of = [&](const Json& p) -> int {
+    if (p.is_number()) return static_cast<int>(p.as_int());
+    for (const auto& cp : c["ports"].as_array())
+      if (cp["name"].as_string() == p.as_string()) return static_cast<int>(cp["containerPort"].as_int());
+    return std::atoi(p.as_string().c_str());
+  };
+  if (probe["httpGet"].is_object()) {
+    const Json& hg = probe["httpGet"];
+    const std::string host = hg["host"].as_string_or(rt.ip);
+    std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
+    Headers h;
+    for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
+    return [url, h, timeout] {
+      HttpResult res = http_request("GET", url, "", h, timeout);
+      return res.status >= 200 && res.status < 400;
+    };
+  }
+  if (probe["tcpSocket"].is_object()) {
+    const std::string ip = rt.ip;
+    const int port = port_of(probe.at_path({"tcpSocket", "port"}));
+    return [ip, port, timeout] { return tcp_connect(ip, port, timeout); };
+  }
+  if (probe["exec"].is_object()) {
+    std::vector<std::string> argv;
+    for (const auto& a : probe.at_path({"exec", "command"}).as_array()) argv.push_back(a.as_string());
+    if (argv.empty()) return [] { return false; };
     std::vector<std::string> envv;
     std::map<std::string, std::string> envm;
-    env_for(c, envv, envm);
-    std::string why, zygote;
-    std::vector<std::string> argv = resolve_argv(c, &why, &zygote);
-    for (auto& a : argv) a = expand_vars(a, envm);
-    std::string wd = c["workingDir"].as_string();
-    std::string cwd = rt->dir + "/rootfs";
-    if (!wd.empty()) {
-      auto m = rt->mounts.find(wd);
-      cwd = m != rt->mounts.end() ? m->second : rt->dir + "/rootfs" + wd;
-      make_dirs(cwd);
-      // follow a symlinked mount point
-      char buf[4096];
-      if (!realpath(cwd.c_str(), buf)) make_dirs(cwd);
-    }
-    ::unlink(cr.term_path.c_str());
-    std::string serr;
-    {
-      std::ofstream lf(cr.log_path, std::ios::app);
-      lf << "# kflite: starting " << cr.name << " (" << why << "): " << join(argv, " ") << "\n";
-    }
-    // topology-manager "single-numa-node"-style placement for GPU containers: the process tree
-    // runs on the CPUs local to its GPUs (host<->HBM copies, RCCL proxy threads, data loaders)
-    std::vector<int> cpus;
-    if (cfg_.numa_pinning && !rt->gpus.devices.empty() &&
-        (resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 || shares_pod_gpus(c)))
-      cpus = alloc_->topology().local_cpus(rt->gpus.devices);
-    pid_t pid = -1;
-    cr.zfd = -1;
-    cr.zorphan = false;
-    // a recipe with a zygote forks from the pre-imported interpreter when one serves it ('python -m'
-    // containers only); otherwise, or when it does not answer, a fresh interpreter as always
-    Zygote zy;
-    if (!zygote.empty()) {
-      std::lock_guard<std::mutex> g(zy_mu_);
-      auto it = zygotes_.find(zygote);
-      if (it != zygotes_.end()) zy = it->second;
-    }
-    if (zy.pid > 0 && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
-      std::string zerr;
-      pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
-      if (pid > 0) {
-        std::ofstream lf(cr.log_path, std::ios::app);
-        lf << "# kflite: forked from zygote " << zy.pid << " (preloaded " << zygote << ")\n";
-      } else if (!zerr.empty()) {
-        std::ofstream lf(cr.log_path, std::ios::app);
-        lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";
-      }
-    }
-    static const auto starts = Registry::global().counter(
-        "kubelet_container_starts_total", "container processes started, by how: zygote fork or fresh exec", {"mode"});
-    if (pid > 0) starts->inc({"zygote"});
-    if (pid < 0) {
-      pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
-      if (pid > 0) starts->inc({"fresh"});
-    }
-    if (pid < 0) {
-      cr.state = "waiting";
-      cr.reason = "CreateContainerError";
-      cr.message = serr;
-      rec_->event(pod, "Warning", "Failed", "Error: " + serr);
-      cr.backoff_until = now_seconds() + cfg_.restart_backoff;
-      return;
-    }
-    cr.pid = pid;
-    cr.state = "running";
-    cr.reason = "";
-    cr.envv = envv;
-    cr.cwd = cwd;
-    cr.cpus = cpus;
-    cr.started_at = ms_now();
-    if (cr.zfd >= 0) {
-      const int dfd = ::fcntl(cr.zfd, F_DUPFD_CLOEXEC, 0);  // the watch closes its own copy
-      if (dfd >= 0) watch_fd(dfd, r.ns, r.name);
-    } else {
-      watch_exit(pid, r.ns, r.name);
-    }
-    cr.run_started = now_seconds();
-    cr.probe_gen = Prober::next_generation();
-    cr.ready = false;
-    cr.ready_ok = cr.ready_fail = cr.live_fail = cr.startup_ok = cr.startup_fail = 0;
-    const Json& sp = c["startupProbe"];
-    cr.started_probe_ok = !sp.is_object();
-    cr.next_startup_probe = now_seconds() + static_cast<double>(probe_i(sp, "initialDelaySeconds", 0));
-    cr.next_ready_probe = now_seconds() + static_cast<double>(probe_i(c["readinessProbe"], "initialDelaySeconds", 0));
-    cr.next_live_probe = now_seconds() + static_cast<double>(probe_i(c["livenessProbe"], "initialDelaySeconds", 0));
-    rec_->event(pod, "Normal", "Started", "Started container " + cr.name);
-  };
-  // The probe as a self-contained closure (copies of the spec, the pod IP and the container env):
-  // it runs on a Prober thread, never on this reconcile worker.
-  auto make_probe = [&](const Json& probe, const Json& c) -> std::function<bool()> {
-    const int timeout = static_cast<int>(probe_i(probe, "timeoutSeconds", 1)) * 1000;
-    auto port_of = [&](const Json& p) -> int {
-      if (p.is_number()) return static_cast<int>(p.as_int());
-      for (const auto& cp : c["ports"].as_array())
-        if (cp["name"].as_string() == p.as_string()) return static_cast<int>(cp["containerPort"].as_int());
-      return std::atoi(p.as_string().c_str());
+    container_env(s, c, envv, envm);
+    const std::string cwd = rt.dir + "/rootfs", log = rt.dir + "/probe.log";
+    return [argv, envv, cwd, log, timeout] {
+      pid_t pid = spawn(argv, envv, cwd, log, nullptr);
+      if (pid < 0) return false;
+      return wait_probe_process(pid, timeout) == 0;
     };
-    if (probe["httpGet"].is_object()) {
-      const Json& hg = probe["httpGet"];
-      const std::string host = hg["host"].as_string_or(rt->ip);
-      std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
-      Headers h;
-      for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
-      return [url, h, timeout] {
-        HttpResult res = http_request("GET", url, "", h, timeout);
-        return res.status >= 200 && res.status < 400;
-      };
+  }
+  return [] { return true; };
+}
+
+// The verdict of this container's last `kind` probe, if one finished; starts one when `due`.
+std::optional<bool> Kubelet::probe_verdict(PodSync& s, ContainerRt& cr, const char* kind, const Json& probe,
+                                           const Json& c, bool due) {
+  const std::string key = s.rt->uid + "/" + (cr.init ? "init:" : "") + cr.name + "/" + kind;
+  const bool start = due && !prober_->in_flight(key);
+  return prober_->poll(key, cr.probe_gen, start, s.r.ns, s.r.name, start ? make_probe(s, probe, c) : nullptr);
+}
+
+// Probes of one running container (startup gates readiness/liveness); lowers s.next_wake.
+void Kubelet::tick_probes(PodSync& s, ContainerRt& cr, const Json& c) {
+  const double now = now_seconds();
+  const Json& sp = c["startupProbe"];
+  if (!cr.started_probe_ok) {
+    if (auto v = probe_verdict(s, cr, "startup", sp, c, now >= cr.next_startup_probe)) {
+      if (*v) {
+        if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
+      } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
+        rec_->event(s.pod, "Warning", "Unhealthy", "Startup probe failed");
+        ::kill(-cr.pid, SIGKILL);
+      }
+      cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
     }
-    if (probe["tcpSocket"].is_object()) {
-      const std::string ip = rt->ip;
-      const int port = port_of(probe.at_path({"tcpSocket", "port"}));
-      return [ip, port, timeout] { return tcp_connect(ip, port, timeout); };
-    }
-    if (probe["exec"].is_object()) {
-      std::vector<std::string> argv;
-      for (const auto& a : probe.at_path({"exec", "command"}).as_array()) argv.push_back(a.as_string());
-      if (argv.empty()) return [] { return false; };
-      std::vector<std::string> envv;
-      std::map<std::string, std::string> envm;
-      env_for(c, envv, envm);
-      const std::string cwd = rt->dir + "/rootfs", log = rt->dir + "/probe.log";
-      return [argv, envv, cwd, log, timeout] {
-        pid_t pid = spawn(argv, envv, cwd, log, nullptr);
-        if (pid < 0) return false;
-        return wait_probe_process(pid, timeout) == 0;
-      };
-    }
-    return [] { return true; };
-  };
-  // The verdict of this container's last `kind` probe, if one finished; starts one when `due`.
-  auto probe_verdict = [&](ContainerRt& cr, const char* kind, const Json& probe, const Json& c,
-                           bool due) -> std::optional<bool> {
-    const std::string key = rt->uid + "/" + (cr.init ? "init:" : "") + cr.name + "/" + kind;
-    const bool start = due && !prober_->in_flight(key);
-    return prober_->poll(key, cr.probe_gen, start, r.ns, r.name, start ? make_probe(probe, c) : nullptr);
-  };
-  auto handle_exit = [&](ContainerRt& cr) {
-    int code = 0;
-    std::string reason;
-    if (cr.pid <= 0 || cr.state != "running" || !reap_container(cr.pid, cr.zfd, cr.zorphan, code, reason)) return false;
-    cr.pid = -1;
-    cr.state = "terminated";
-    cr.exit_code = code;
-    cr.reason = reason;
-    cr.finished_at = ms_now();
-    cr.ready = false;
-    std::string msg;
-    if (read_file(cr.term_path, msg)) cr.message = msg.substr(0, 4096);
-    else cr.message.clear();
-    return true;
-  };
-  double next_wake = 1.0;
-  // Until a pod is Ready the kubelet re-syncs it every 5 ms (cold start is on the notebook's
-  // critical path; a sync of an unchanged pod costs no API call), afterwards at the 1 s relist.
-  constexpr double kStartupPoll = 0.005;
-  // Probes of one running container (startup gates readiness/liveness); keeps next_wake.
-  auto tick_probes = [&](ContainerRt& cr, const Json& c) {
-    const double now = now_seconds();
-    const Json& sp = c["startupProbe"];
-    if (!cr.started_probe_ok) {
-      if (auto v = probe_verdict(cr, "startup", sp, c, now >= cr.next_startup_probe)) {
-        if (*v) {
-          if (++cr.startup_ok >= probe_i(sp, "successThreshold", 1)) cr.started_probe_ok = true;
-        } else if (++cr.startup_fail >= probe_i(sp, "failureThreshold", 3)) {
-          rec_->event(pod, "Warning", "Unhealthy", "Startup probe failed");
-          ::kill(-cr.pid, SIGKILL);
-        }
-        cr.next_startup_probe = now + static_cast<double>(probe_i(sp, "periodSeconds", 10));
+  }
+  if (!cr.started_probe_ok) {
+    s.next_wake = std::min(s.next_wake, 0.1);
+    return;
+  }
+  const Json& rp = c["readinessProbe"];
+  if (!rp.is_object()) {
+    cr.ready = true;
+  } else if (auto v = probe_verdict(s, cr, "readiness", rp, c, now >= cr.next_ready_probe)) {
+    if (*v) {
+      cr.ready_fail = 0;
+      if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
+    } else {
+      cr.ready_ok = 0;
+      if (++cr.ready_fail >= probe_i(rp, "failureThreshold", 3)) {
+        if (cr.ready) rec_->event(s.pod, "Warning", "Unhealthy", "Readiness probe failed");
+        cr.ready = false;
       }
     }
-    if (!cr.started_probe_ok) {
-      next_wake = std::min(next_wake, 0.1);
+    // probe fast until the first success (cold-start latency: the readiness sidecar's verdict or the
+    // server's first answer is seen within ~5 ms), then at periodSeconds
+    cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : kStartupPoll);
+  }
+  const Json& lp = c["livenessProbe"];
+  if (lp.is_object()) {
+    if (auto v = probe_verdict(s, cr, "liveness", lp, c, now >= cr.next_live_probe)) {
+      if (*v) {
+        cr.live_fail = 0;
+      } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
+        rec_->event(s.pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
+        ::kill(-cr.pid, SIGKILL);
+      }
+      cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
+    }
+  }
+  if (!cr.ready) {
+    s.next_wake = std::min(s.next_wake, kStartupPoll);
+  } else {
+    // wake for the next due probe; a container without probes only needs the 1 s exit-detection
+    // relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
+    double due = 1e30;
+    if (rp.is_object()) due = std::min(due, cr.next_ready_probe);
+    if (lp.is_object()) due = std::min(due, cr.next_live_probe);
+    if (due < 1e30) s.next_wake = std::min(s.next_wake, std::max(0.2, due - now));
+  }
+}
+
+// a long-running container (main, or started sidecar): exit -> restart per policy with back-off, probes
+void Kubelet::tick_long_running(PodSync& s, ContainerRt& cr, bool always_restart) {
+  const Json& c = s.container_spec(cr);
+  if (cr.state == "running") {
+    if (!handle_exit(cr)) {
+      tick_probes(s, cr, c);
       return;
     }
-    const Json& rp = c["readinessProbe"];
-    if (!rp.is_object()) {
-      cr.ready = true;
-    } else if (auto v = probe_verdict(cr, "readiness", rp, c, now >= cr.next_ready_probe)) {
-      const bool ok = *v;
-      if (ok) {
-        cr.ready_fail = 0;
-        if (++cr.ready_ok >= probe_i(rp, "successThreshold", 1)) cr.ready = true;
-      } else {
-        cr.ready_ok = 0;
-        if (++cr.ready_fail >= probe_i(rp, "failureThreshold", 3)) {
-          if (cr.ready) rec_->event(pod, "Warning", "Unhealthy", "Readiness probe failed");
-          cr.ready = false;
-        }
+  }
+  if (cr.state == "terminated") {
+    const bool restart = always_restart || s.restart_policy == "Always" ||
+                         (s.restart_policy == "OnFailure" && cr.exit_code != 0);
+    if (!restart) return;
+    cr.last_state = terminated_state(cr);
+    cr.restarts++;
+    cr.state = "waiting";
+    cr.reason = "CrashLoopBackOff";
+    double ran = now_seconds() - cr.run_started;
+    double backoff = ran > 600 ? cfg_.restart_backoff : std::min(300.0, cfg_.restart_backoff * (1 << std::min(cr.restarts - 1, 5)));
+    cr.backoff_until = now_seconds() + backoff;
+    rec_->event(s.pod, "Warning", "BackOff", "Back-off restarting failed container " + cr.name);
+  }
+  if (cr.state == "waiting") {
+    if (now_seconds() >= cr.backoff_until) {
+      start_container(s, cr);
+      // no startup / readiness probe: Ready as soon as it runs (Kubernetes' default Success), in
+      // this pass rather than the next re-sync
+      if (cr.state == "running" && !c["startupProbe"].is_object() && !c["readinessProbe"].is_object()) {
+        cr.started_probe_ok = true;
+        cr.ready = true;
       }
-      // probe fast until the first success (cold-start latency: the readiness sidecar's verdict or
-      // the server's first answer is seen within ~5 ms), then at periodSeconds
-      cr.next_ready_probe = now + (cr.ready ? static_cast<double>(probe_i(rp, "periodSeconds", 10)) : kStartupPoll);
-    }
-    const Json& lp = c["livenessProbe"];
-    if (lp.is_object()) {
-      if (auto v = probe_verdict(cr, "liveness", lp, c, now >= cr.next_live_probe)) {
-        if (*v) {
-          cr.live_fail = 0;
-        } else if (++cr.live_fail >= probe_i(lp, "failureThreshold", 3)) {
-          rec_->event(pod, "Warning", "Unhealthy", "Liveness probe failed; container will be restarted");
-          ::kill(-cr.pid, SIGKILL);
-        }
-        cr.next_live_probe = now + static_cast<double>(probe_i(lp, "periodSeconds", 10));
-      }
-    }
-    if (!cr.ready) {
-      next_wake = std::min(next_wake, kStartupPoll);
+      s.next_wake = std::min(s.next_wake, kStartupPoll);
     } else {
-      // wake for the next due probe; a container without probes only needs the 1 s
-      // exit-detection relist (PLEG-like), not a 0.2 s spin on "probe due at t=0"
-      double due = 1e30;
-      if (rp.is_object()) due = std::min(due, cr.next_ready_probe);
-      if (lp.is_object()) due = std::min(due, cr.next_live_probe);
-      if (due < 1e30) next_wake = std::min(next_wake, std::max(0.2, due - now));
+      s.next_wake = std::min(s.next_wake, cr.backoff_until - now_seconds());
     }
-  };
-  // a long-running container (main, or sidecar): exit -> restart per policy with back-off, probes
-  auto tick_long_running = [&](ContainerRt& cr, bool always_restart) {
-    const Json& c = container_spec(cr);
-    if (cr.state == "running") {
-      if (!handle_exit(cr)) {
-        tick_probes(cr, c);
-        return;
-      }
-    }
-    if (cr.state == "terminated") {
-      const bool restart = always_restart || restart_policy == "Always" ||
-                           (restart_policy == "OnFailure" && cr.exit_code != 0);
-      if (!restart) return;
-      cr.last_state = Json{{"terminated", Json{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at},
-                                               {"finishedAt", cr.finished_at}, {"message", cr.message}}}};
-      cr.restarts++;
-      cr.state = "waiting";
-      cr.reason = "CrashLoopBackOff";
-      double ran = now_seconds() - cr.run_started;
-      double backoff = ran > 600 ? cfg_.restart_backoff : std::min(300.0, cfg_.restart_backoff * (1 << std::min(cr.restarts - 1, 5)));
-      cr.backoff_until = now_seconds() + backoff;
-      rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + cr.name);
-    }
-    if (cr.state == "waiting") {
-      if (now_seconds() >= cr.backoff_until) {
-        start_container(cr);
-        // no startup / readiness probe: Ready as soon as it runs (Kubernetes' default Success),
-        // in this pass rather than the next re-sync
-        if (cr.state == "running" && !c["startupProbe"].is_object() && !c["readinessProbe"].is_object()) {
-          cr.started_probe_ok = true;
-          cr.ready = true;
-        }
-        next_wake = std::min(next_wake, kStartupPoll);
-      } else {
-        next_wake = std::min(next_wake, cr.backoff_until - now_seconds());
-      }
-    }
-  };
-  // init containers, sequentially. A native sidecar (restartPolicy: Always) counts as done once it
-  // is STARTED (running, startup probe passed): the next init container / the main containers
-  // start while it keeps running, and it is restarted whenever it exits (KEP-753 semantics).
-  while (rt->init_done < rt->init.size() && !rt->init_failed) {
-    ContainerRt& ic = rt->init[rt->init_done];
+  }
+}
+
+// init containers, sequentially. A native sidecar (restartPolicy: Always) counts as done once it is
+// STARTED (running, startup probe passed): the next init container / the main containers start
+// while it keeps running, and it is restarted whenever it exits (KEP-753 semantics).
+void Kubelet::run_init_containers(PodSync& s) {
+  PodRuntime& rt = *s.rt;
+  while (rt.init_done < rt.init.size() && !rt.init_failed) {
+    ContainerRt& ic = rt.init[rt.init_done];
     if (ic.state == "waiting") {
       if (now_seconds() < ic.backoff_until) {
-        next_wake = std::min(next_wake, ic.backoff_until - now_seconds());
+        s.next_wake = std::min(s.next_wake, ic.backoff_until - now_seconds());
         break;
       }
-      start_container(ic);
-      next_wake = kStartupPoll;
-      if (ic.sidecar && ic.state == "running" && !container_spec(ic)["startupProbe"].is_object()) {
+      start_container(s, ic);
+      s.next_wake = kStartupPoll;
+      if (ic.sidecar && ic.state == "running" && !s.container_spec(ic)["startupProbe"].is_object()) {
         ic.started_probe_ok = true;
-        rt->init_done++;
+        rt.init_done++;
         continue;
       }
       break;
@@ -1485,111 +1530,89 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     if (ic.state == "running") {
       if (handle_exit(ic)) continue;
       if (ic.sidecar) {
-        tick_probes(ic, container_spec(ic));
+        tick_probes(s, ic, s.container_spec(ic));
         if (ic.started_probe_ok) {
-          rt->init_done++;
+          rt.init_done++;
           continue;
         }
       }
-      next_wake = kStartupPoll;  // init containers gate the pod: notice their exit within ~10 ms
+      s.next_wake = kStartupPoll;  // init containers gate the pod: notice their exit within ~10 ms
       break;
     }
     // terminated
     if (ic.exit_code == 0 && !ic.sidecar) {
-      rt->init_done++;
+      rt.init_done++;
       continue;
     }
-    if (restart_policy == "Never" && !ic.sidecar) {
-      rt->init_failed = true;
+    if (s.restart_policy == "Never" && !ic.sidecar) {
+      rt.init_failed = true;
       break;
     }
-    ic.last_state = Json{{"terminated", Json{{"exitCode", ic.exit_code}, {"reason", ic.reason}, {"startedAt", ic.started_at},
-                                             {"finishedAt", ic.finished_at}, {"message", ic.message}}}};
+    ic.last_state = terminated_state(ic);
     ic.restarts++;
     ic.state = "waiting";
     ic.reason = "CrashLoopBackOff";
     ic.backoff_until = now_seconds() + std::min(300.0, cfg_.restart_backoff * (1 << std::min(ic.restarts - 1, 5)));
-    rec_->event(pod, "Warning", "BackOff", "Back-off restarting failed container " + ic.name);
+    rec_->event(s.pod, "Warning", "BackOff", "Back-off restarting failed container " + ic.name);
     break;
   }
-  const bool initialized = rt->init_done == rt->init.size();
-  // started sidecars run alongside everything after them
-  for (size_t i = 0; i < rt->init_done && i < rt->init.size(); ++i)
-    if (rt->init[i].sidecar) tick_long_running(rt->init[i], true);
-  if (initialized)
-    for (auto& cr : rt->main) tick_long_running(cr, false);
-  // the gpu-readiness sidecar's report (its termination-log file, written before it turns Ready)
-  // goes onto the pod as notebooks.kubeflow.org/gpu-readiness, where the notebook controller
-  // surfaces it as status.gpuReadiness; written before the status update that makes the pod Ready
-  for (const auto& cr : rt->init) {
-    if (!cr.sidecar || cr.name != "gpu-readiness" || !cr.ready || rt->readiness_published) continue;
+}
+
+// the gpu-readiness sidecar's report (its termination-log file, written before it turns Ready) goes
+// onto the pod as notebooks.kubeflow.org/gpu-readiness, where the notebook controller surfaces it as
+// status.gpuReadiness; written before the status update that makes the pod Ready
+void Kubelet::publish_readiness(PodSync& s) {
+  PodRuntime& rt = *s.rt;
+  for (const auto& cr : rt.init) {
+    if (!cr.sidecar || cr.name != "gpu-readiness" || !cr.ready || rt.readiness_published) continue;
     std::string rep;
     if (!read_file(cr.term_path, rep) || rep.empty()) continue;
-    rt->readiness_published = true;
-    c_->update_with_retry("v1", "Pod", r.ns, r.name, [&](Json& o) {
-      if (o.str_at({"metadata", "uid"}) != uid) return false;
+    rt.readiness_published = true;
+    c_->update_with_retry("v1", "Pod", s.r.ns, s.r.name, [&](Json& o) {
+      if (o.str_at({"metadata", "uid"}) != s.uid) return false;
       o["metadata"]["annotations"][ANNOTATION_GPU_READINESS] = rep.substr(0, 4096);
       o["metadata"]["annotations"]["notebooks.kubeflow.org/gpu-readiness-at"] = ms_now();
       return true;
     });
   }
+}
 
-  // ---- status --------------------------------------------------------------------------------------
-  auto cstatus = [&](const ContainerRt& cr) {
-    const Json& c = container_spec(cr);
-    Json state;
-    if (cr.state == "running") {
-      state = Json{{"running", Json{{"startedAt", cr.started_at}}}};
-    } else if (cr.state == "terminated") {
-      Json t{{"exitCode", cr.exit_code}, {"reason", cr.reason}, {"startedAt", cr.started_at}, {"finishedAt", cr.finished_at},
-             {"containerID", "kflite://" + cr.name}};
-      if (!cr.message.empty()) t["message"] = cr.message;
-      state = Json{{"terminated", t}};
-    } else {
-      Json w{{"reason", cr.reason.empty() ? "ContainerCreating" : cr.reason}};
-      if (!cr.message.empty()) w["message"] = cr.message;
-      state = Json{{"waiting", w}};
-    }
-    Json s{{"name", cr.name}, {"state", state}, {"lastState", cr.last_state}, {"ready", cr.ready},
-           {"restartCount", cr.restarts}, {"image", c["image"]}, {"imageID", "kflite-recipe://" + c["image"].as_string()},
-           {"started", cr.state == "running"}};
-    if (cr.pid > 0) s["containerID"] = "kflite://" + std::to_string(cr.pid);
-    return s;
-  };
+// phase, conditions and container statuses; written only when they changed
+ApiError Kubelet::write_status(PodSync& s) {
+  const PodRuntime& rt = *s.rt;
+  const bool initialized = rt.init_done == rt.init.size();
   Json init_st = Json::array(), main_st = Json::array();
-  for (const auto& cr : rt->init) init_st.push_back(cstatus(cr));
-  for (const auto& cr : rt->main) main_st.push_back(cstatus(cr));
-  bool all_ready = initialized && !rt->main.empty(), all_running = initialized, any_running = false, all_done = initialized,
-       any_failed = rt->init_failed;
-  for (const auto& cr : rt->init)
+  for (const auto& cr : rt.init) init_st.push_back(container_status(cr, s.container_spec(cr)));
+  for (const auto& cr : rt.main) main_st.push_back(container_status(cr, s.container_spec(cr)));
+  bool all_ready = initialized && !rt.main.empty(), any_running = false, all_done = initialized, any_failed = rt.init_failed;
+  for (const auto& cr : rt.init)
     if (cr.sidecar) all_ready = all_ready && cr.ready;  // sidecar readiness gates the pod's
-  for (const auto& cr : rt->main) {
+  for (const auto& cr : rt.main) {
     all_ready = all_ready && cr.ready;
-    all_running = all_running && cr.state == "running";
     any_running = any_running || cr.state == "running";
     all_done = all_done && cr.state == "terminated";
     any_failed = any_failed || (cr.state == "terminated" && cr.exit_code != 0);
   }
   std::string new_phase = "Pending";
-  if (rt->init_failed) new_phase = "Failed";
-  else if (initialized && all_done && restart_policy != "Always") new_phase = any_failed ? "Failed" : "Succeeded";
+  if (rt.init_failed) new_phase = "Failed";
+  else if (initialized && all_done && s.restart_policy != "Always") new_phase = any_failed ? "Failed" : "Succeeded";
   else if (initialized && (any_running || all_done)) new_phase = "Running";
 
-  if (!pod.has("apiVersion")) pod["apiVersion"] = "v1";
-  if (!pod.has("kind")) pod["kind"] = "Pod";
-  ApiError ue = c_->update_with_retry_from(
-      std::move(pod),
+  if (!s.pod.has("apiVersion")) s.pod["apiVersion"] = "v1";
+  if (!s.pod.has("kind")) s.pod["kind"] = "Pod";
+  return c_->update_with_retry_from(
+      std::move(s.pod),
       [&](Json& o) {
-        if (o.str_at({"metadata", "uid"}) != uid) return false;
+        if (o.str_at({"metadata", "uid"}) != s.uid) return false;
         Json st = o["status"];
         const Json old_st = st;
         st["phase"] = new_phase;
         st["hostIP"] = "127.0.0.1";
-        st["podIP"] = rt->ip;
-        st["podIPs"] = Json::array({Json{{"ip", rt->ip}}});
-        st["startTime"] = rt->start_time;
+        st["podIP"] = rt.ip;
+        st["podIPs"] = Json::array({Json{{"ip", rt.ip}}});
+        st["startTime"] = rt.start_time;
         st["containerStatuses"] = main_st;
-        if (!rt->init.empty()) st["initContainerStatuses"] = init_st;
+        if (!rt.init.empty()) st["initContainerStatuses"] = init_st;
         auto cond = [&](const char* type, bool ok, const std::string& reason) {
           Json conds = Json::array();
           std::string ts = ms_now();
@@ -1608,14 +1631,56 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
         cond("Initialized", initialized, "ContainersNotInitialized");
         cond("ContainersReady", all_ready, "ContainersNotReady");
         cond("Ready", all_ready, "ContainersNotReady");
-        (void)all_running;
         if (st == old_st) return false;
         o["status"] = st;
         return true;
       },
       true);
+}
+
+Result Kubelet::reconcile(const Request& r, std::string* err) {
+  if (stopping_) return {};
+  Json pod;
+  ApiError e = c_->get("v1", "Pod", r.ns, r.name, pod);
+  std::shared_ptr<PodRuntime> rt = lookup_runtime(r, e, pod);
+  if (e.code == 404) return {};
+  if (e) {
+    *err = e.message;
+    return {};
+  }
+  if (pod.at_path({"spec", "nodeName"}).as_string() != cfg_.node_name) return {};
+  std::unique_lock<std::mutex> pod_lock;
+  if (rt) {
+    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
+    if (stopping_) return {};
+  }
+  if (pod.at_path({"metadata", "deletionTimestamp"}).is_string()) {
+    finish_deletion(r, pod, rt, err);
+    return {};
+  }
+  const std::string phase = pod.at_path({"status", "phase"}).as_string();
+  if (!rt && (phase == "Succeeded" || phase == "Failed")) return {};
+  if (!rt) rt = admit(r, pod);
+  if (!pod_lock.owns_lock()) {
+    pod_lock = std::unique_lock<std::mutex>(rt->op_mu);
+    if (stopping_) return {};
+  }
+  if (!rt->gpu_ok) {
+    fail_admission(r);
+    return {};
+  }
+  PodSync s{r, std::move(pod), rt, rt->uid, ""};
+  s.restart_policy = s.pod.at_path({"spec", "restartPolicy"}).as_string_or("Always");
+  run_init_containers(s);
+  // started sidecars run alongside everything after them
+  for (size_t i = 0; i < rt->init_done && i < rt->init.size(); ++i)
+    if (rt->init[i].sidecar) tick_long_running(s, rt->init[i], true);
+  if (rt->init_done == rt->init.size())
+    for (auto& cr : rt->main) tick_long_running(s, cr, false);
+  publish_readiness(s);
+  ApiError ue = write_status(s);
   if (ue && ue.code != 404) *err = ue.message;
-  return Result::after(std::max(kStartupPoll, next_wake));
+  return Result::after(std::max(kStartupPoll, s.next_wake));
 }
 
 // GPU metrics (SURVEY §5.5 build additions), scraped from the kubelet's registry: which pod holds

@@ -26,6 +26,8 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
+#include <optional>
 #include <map>
 #include <set>
 #include <memory>
@@ -94,6 +96,8 @@ struct KubeletConfig {
   bool pod_zygote = false;
 };
 
+struct ContainerRt;  // one container's process state (kubelet.cc)
+
 class Kubelet {
  public:
   Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg);
@@ -124,6 +128,26 @@ class Kubelet {
   void register_telemetry_metrics();
   bool metrics_registered_ = false;
   void terminate_pod(PodRuntime& rt, int64_t grace_s);
+  // one reconcile pass, in units (kubelet.cc): lookup / deletion / admission, then the containers
+  struct PodSync;
+  std::shared_ptr<PodRuntime> lookup_runtime(const Request& r, const ApiError& e, const Json& pod);
+  void finish_deletion(const Request& r, const Json& pod, const std::shared_ptr<PodRuntime>& rt, std::string* err);
+  std::shared_ptr<PodRuntime> admit(const Request& r, const Json& pod);
+  void allocate_gpus(PodRuntime& rt, const Json& pod);
+  std::map<std::string, std::string> prepare_volumes(PodRuntime& rt, const Json& pod);
+  void build_containers(PodRuntime& rt, const Json& pod, const std::map<std::string, std::string>& vol_dirs);
+  void fail_admission(const Request& r);
+  void container_env(const PodSync& s, const Json& c, std::vector<std::string>& envv,
+                     std::map<std::string, std::string>& envm);
+  void start_container(PodSync& s, ContainerRt& cr);
+  std::function<bool()> make_probe(const PodSync& s, const Json& probe, const Json& c);
+  std::optional<bool> probe_verdict(PodSync& s, ContainerRt& cr, const char* kind, const Json& probe, const Json& c,
+                                    bool due);
+  void tick_probes(PodSync& s, ContainerRt& cr, const Json& c);
+  void tick_long_running(PodSync& s, ContainerRt& cr, bool always_restart);
+  void run_init_containers(PodSync& s);
+  void publish_readiness(PodSync& s);
+  ApiError write_status(PodSync& s);
   std::shared_ptr<Client> c_;
   KubeletConfig cfg_;
   std::unique_ptr<GpuAllocator> alloc_;

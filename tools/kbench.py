@@ -214,10 +214,54 @@ def main():
             ts.append(timeit(lambda: ops.layer_norm_fwd(x, w, bb), 50, dev))
             tt.append(timeit(lambda: torch.nn.functional.layer_norm(x, (H,), w, bb), 50, dev))
         bytes_moved = 2 * rows * H * 2
+        # the copy roof on this device and shape: a D2D copy of the same bytes (read + write)
+        dst = torch.empty_like(x)
+        tc = min(timeit(lambda: dst.copy_(x), 50, dev) for _ in range(args.rounds))
         emit({"kind": "layernorm_fwd_bf16", "rows": rows, "hidden": H,
               "ours_GBps": round(bytes_moved / min(ts) / 1e9, 1),
               "torch_GBps": round(bytes_moved / min(tt) / 1e9, 1),
+              "copy_GBps": round(bytes_moved / tc / 1e9, 1),
+              "ours_of_copy_roof": round(tc / min(ts), 3),
               "ours_us": round(min(ts) * 1e6, 1), "torch_us": round(min(tt) * 1e6, 1)})
+        # backward: the dx pass alone (reads dy, x; writes dx), with the residual gradient folded in
+        # (+ one read), the whole backward with dgamma / dbeta, and torch's autograd LayerNorm backward
+        from kubeflow_rm_amd.ops import _lib as L
+        _, mean, rstd = ops.layer_norm_fwd(x, w, bb, save_stats=True)
+        gy = torch.randn(rows, H, device=dev).to(torch.bfloat16)
+        gr = torch.randn(rows, H, device=dev).to(torch.bfloat16)
+        dx = torch.empty_like(x)
+        dg = torch.empty(H, device=dev, dtype=torch.bfloat16)
+        db = torch.empty(H, device=dev, dtype=torch.bfloat16)
+        ws = torch.empty(L.lib().kfamd_layernorm_bwd_workspace(rows, H) // 4, device=dev, dtype=torch.float32)
+        st = torch.cuda.current_stream(dev).cuda_stream
+
+        def bwd(res, full):
+            L.lib().kfamd_layernorm_bwd_bf16_v3(gy.data_ptr(), gr.data_ptr() if res else None, x.data_ptr(),
+                                                w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                                dg.data_ptr() if full else None, db.data_ptr() if full else None, 1,
+                                                ws.data_ptr(), rows, H, st)
+        xr = x.clone().requires_grad_(True)
+        wr, br = w.clone().requires_grad_(True), bb.clone().requires_grad_(True)
+        yr = torch.nn.functional.layer_norm(xr, (H,), wr, br)
+
+        def torch_bwd():
+            torch.autograd.grad(yr, (xr, wr, br), gy, retain_graph=True)
+        res = {"dx": [], "dx_res": [], "full": [], "full_res": [], "torch": []}
+        for _ in range(args.rounds):
+            res["dx"].append(timeit(lambda: bwd(False, False), 50, dev))
+            res["dx_res"].append(timeit(lambda: bwd(True, False), 50, dev))
+            res["full"].append(timeit(lambda: bwd(False, True), 50, dev))
+            res["full_res"].append(timeit(lambda: bwd(True, True), 50, dev))
+            res["torch"].append(timeit(torch_bwd, 20, dev))
+        b3, b4 = 3 * rows * H * 2, 4 * rows * H * 2
+        emit({"kind": "layernorm_bwd_bf16", "rows": rows, "hidden": H,
+              "dx_us": round(min(res["dx"]) * 1e6, 1), "dx_GBps": round(b3 / min(res["dx"]) / 1e9, 1),
+              "dx_res_us": round(min(res["dx_res"]) * 1e6, 1), "dx_res_GBps": round(b4 / min(res["dx_res"]) / 1e9, 1),
+              "full_us": round(min(res["full"]) * 1e6, 1), "full_res_us": round(min(res["full_res"]) * 1e6, 1),
+              "torch_full_us": round(min(res["torch"]) * 1e6, 1),
+              "copy_GBps": round(bytes_moved / tc / 1e9, 1)})
+        del x, w, bb, gy, gr, dx, dst, ws, xr, yr
+        torch.cuda.empty_cache()
     if args.out:
         Path(args.out).parent.mkdir(parents=True, exist_ok=True)
         Path(args.out).write_text("\n".join(json.dumps(d) for d in out) + "\n")

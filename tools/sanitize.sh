@@ -9,13 +9,16 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-profiles/r1_sanitizers}
 mkdir -p "$OUT"
-SUITES="tests/test_zygote.py tests/test_kubectl_cli.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py"
+# every suite that drives the native control plane concurrently (the prober pool,
+# the TokenReview cache, the mesh listener, kubectl create/patch/apply and the split binaries too)
+SUITES="tests/test_zygote.py tests/test_kubectl_cli.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py tests/test_kubelet_probes.py tests/test_gateway_authz.py tests/test_kubectl_mutate.py tests/test_kubectl_apply.py tests/test_split_binaries.py tests/test_tls.py"
 rc=0
 for san in thread address; do
   python -c "from kubeflow_rm_amd import _build; _build.build_native(sanitize='$san', build_type='RelWithDebInfo')" \
     > "$OUT/build_$san.log" 2>&1 || { echo "build $san failed"; exit 1; }
   logdir=$(mktemp -d /tmp/kfamd-san-XXXX)
-  export KFAMD_KFLITE=$PWD/build/native-$san/bin/kflite KFAMD_TIMEOUT_SCALE=6
+  # kflite and every split binary (KFAMD_BIN_DIR) from the instrumented build
+  export KFAMD_KFLITE=$PWD/build/native-$san/bin/kflite KFAMD_BIN_DIR=$PWD/build/native-$san/bin KFAMD_TIMEOUT_SCALE=6
   export TSAN_OPTIONS="halt_on_error=0 exitcode=0 log_path=$logdir/report"
   export ASAN_OPTIONS="halt_on_error=0 detect_leaks=1 log_path=$logdir/report"
   export UBSAN_OPTIONS="print_stacktrace=1 log_path=$logdir/report"
@@ -26,6 +29,6 @@ for san in thread address; do
   echo "$san: $n sanitizer reports"
   grep -E '^SUMMARY' "$OUT/reports_$san.txt" | sort | uniq -c | sort -rn | head -20
   rm -rf "$logdir"
-  unset KFAMD_KFLITE KFAMD_TIMEOUT_SCALE TSAN_OPTIONS ASAN_OPTIONS UBSAN_OPTIONS
+  unset KFAMD_KFLITE KFAMD_BIN_DIR KFAMD_TIMEOUT_SCALE TSAN_OPTIONS ASAN_OPTIONS UBSAN_OPTIONS
 done
 exit $rc
