@@ -14,7 +14,9 @@ class Server(ThreadingHTTPServer):
 
 
 def bind_host() -> str:
-    return os.environ.get("POD_IP", "127.0.0.1")
+    """Where a process pod's server listens: its private app address behind the node's inbound
+    enforcement listener when the pod is mesh-injected (KFAMD_BIND_IP), else the pod IP."""
+    return os.environ.get("KFAMD_BIND_IP") or os.environ.get("POD_IP", "127.0.0.1")
 
 
 def serve(handler_cls, port: int, host: str | None = None) -> Server:

@@ -122,5 +122,5 @@ def serve(app: Flask, default_port: int = 5000) -> None:
     """Serve with the stdlib-backed werkzeug server on POD_IP:port (threaded)."""
     from werkzeug.serving import run_simple
     port = int(os.environ.get("PORT") or (os.environ.get("KFAMD_CONTAINER_PORTS") or str(default_port)).split(",")[0])
-    host = os.environ.get("POD_IP", "0.0.0.0")
+    host = (os.environ.get("KFAMD_BIND_IP") or os.environ.get("POD_IP", "0.0.0.0"))
     run_simple(host, port, app, threaded=True, use_reloader=False)

@@ -296,4 +296,4 @@ def serve(app: Flask, default_port: int = 8082) -> None:
     from werkzeug.serving import run_simple
     port = int(os.environ.get("PORT_1") or os.environ.get("PORT")
                or (os.environ.get("KFAMD_CONTAINER_PORTS") or str(default_port)).split(",")[0])
-    run_simple(os.environ.get("POD_IP", "0.0.0.0"), port, app, threaded=True, use_reloader=False)
+    run_simple((os.environ.get("KFAMD_BIND_IP") or os.environ.get("POD_IP", "0.0.0.0")), port, app, threaded=True, use_reloader=False)

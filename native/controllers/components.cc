@@ -281,6 +281,13 @@ bool Components::setup(Manager& mgr, const std::set<std::string>& enabled, int w
     }
     I.gateway = std::make_unique<Gateway>(I.c, go);
     I.gateway->setup(mgr);
+    // this node's kubelet gets per-pod inbound enforcement points backed by the gateway's policy
+    // check (profile namespaces are istio-injection=enabled: direct pod-IP traffic is evaluated too)
+    if (I.kubelet && go.enforce) {
+      Gateway* gw = I.gateway.get();
+      I.kubelet->set_inbound_handler(
+          [gw](const InboundTarget& t, HttpRequest& req, HttpResponse& resp) { gw->handle_inbound(t, req, resp); });
+    }
     if (!I.gateway->start(I.f.gateway_addr, static_cast<int>(I.f.gateway_port), err)) return false;
     I.stoppers.push_back([&I] { I.gateway->stop(); });
   }

@@ -13,6 +13,9 @@ namespace kf {
 namespace {
 constexpr const char* kPeerTokenHeader = "X-Kfamd-Peer-Token";
 constexpr const char* kProxySecretHeader = "X-Kfamd-Auth-Proxy-Secret";
+// the ingress / mesh listener's "already authorized" stamp for the pods' inbound listeners (what the
+// peer's mTLS identity of the ingress gateway is to an Istio sidecar); never taken from a client
+constexpr const char* kHopHeader = "X-Kfamd-Hop";
 
 // "<svc>.<ns>.svc[.<domain>]" (or "<svc>.<ns>") -> (svc, ns); false for anything else
 bool split_service_host(const std::string& host_port, std::string& svc, std::string& ns) {
@@ -43,6 +46,7 @@ Gateway::Gateway(std::shared_ptr<Client> c, GatewayOptions o)
                                             "AuthorizationPolicy decisions by listener and result", {"listener", "result"})) {
   const char* d = std::getenv("KFAMD_ROUTE_DOMAIN");
   route_domain_ = d && *d ? d : "apps.kube-lite";
+  hop_secret_ = secure_random_hex(16);  // a credential: never guessable from the PRNG
 }
 Gateway::~Gateway() { stop(); }
 
@@ -98,12 +102,6 @@ Gateway::Identity Gateway::review_token(const std::string& token) {
 bool Gateway::authorize(const std::string& dest_host, int dest_port, const HttpRequest& req, const std::string& path,
                         const Headers& fwd, const std::string& principal, const std::string& source_ns, std::string* why) {
   if (!o_.enforce || !policies_) return true;
-  // fail closed (ADVICE r4): until both informers have listed, "no ALLOW policy applies" would
-  // admit everything; a destination that is not a Service has no workload to evaluate against
-  if (!policies_->synced() || (services_ && !services_->synced())) {
-    if (why) *why = "authorization policies not synced yet";
-    return false;
-  }
   std::string svc, ns;
   if (!split_service_host(dest_host, svc, ns)) {
     if (why) *why = "destination " + dest_host + " is not a Service";
@@ -113,6 +111,19 @@ bool Gateway::authorize(const std::string& dest_host, int dest_port, const HttpR
   Json s;
   if (services_ && services_->get(ns, svc, s))
     for (const auto& kv : s.at_path({"spec", "selector"}).as_object()) labels[kv.first] = kv.second.as_string();
+  return authorize_workload(ns, labels, dest_port, req, path, fwd, principal, source_ns, why);
+}
+
+bool Gateway::authorize_workload(const std::string& ns, const std::map<std::string, std::string>& labels, int dest_port,
+                                 const HttpRequest& req, const std::string& path, const Headers& fwd,
+                                 const std::string& principal, const std::string& source_ns, std::string* why) {
+  if (!o_.enforce || !policies_) return true;
+  // fail closed (ADVICE r4): until both informers have listed, "no ALLOW policy applies" would
+  // admit everything
+  if (!policies_->synced() || (services_ && !services_->synced())) {
+    if (why) *why = "authorization policies not synced yet";
+    return false;
+  }
   AuthzRequest ar;
   ar.principal = principal;
   ar.source_namespace = source_ns;
@@ -126,6 +137,45 @@ bool Gateway::authorize(const std::string& dest_host, int dest_port, const HttpR
   AuthzDecision d = evaluate_authz(policies_->list(), ar, ns, labels, o_.root_namespace);
   if (!d.allowed && why) *why = d.reason + (d.policy.empty() ? "" : " (" + d.policy + ")");
   return d.allowed;
+}
+
+// the caller's workload identity (Istio: the peer's mTLS certificate; here its ServiceAccount
+// token); a caller without one is plaintext: no principal, no source namespace
+void Gateway::peer_identity(const HttpRequest& req, std::string& principal, std::string& source_ns) {
+  Identity peer = review_token(req.header(kPeerTokenHeader));
+  if (peer.authenticated && peer.service_account()) {
+    auto parts = split(peer.username, ':', false);  // system:serviceaccount:<ns>:<name>
+    if (parts.size() == 4) {
+      source_ns = parts[2];
+      principal = o_.cluster_domain + "/ns/" + parts[2] + "/sa/" + parts[3];
+    }
+  }
+}
+
+void Gateway::handle_inbound(const InboundTarget& t, HttpRequest& req, HttpResponse& resp) {
+  const std::string path = normalize_authz_path(req.path);
+  const bool hopped = !hop_secret_.empty() && req.header(kHopHeader) == hop_secret_;
+  Headers h;
+  for (const auto& kv : req.headers) {
+    const std::string k = to_lower(kv.first);
+    if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
+    if (k == to_lower(kPeerTokenHeader) || k == to_lower(kHopHeader)) continue;
+    h[kv.first] = kv.second;
+  }
+  if (!hopped && o_.enforce) {
+    std::string principal, source_ns, why;
+    peer_identity(req, principal, source_ns);
+    if (!authorize_workload(t.ns, t.labels, t.port, req, path, h, principal, source_ns, &why)) {
+      decisions_->inc({"sidecar", "deny"});
+      resp.headers["X-Kfamd-Authz"] = why;
+      resp.text(403, "RBAC: access denied");
+      return;
+    }
+    decisions_->inc({"sidecar", "allow"});
+  }
+  const std::string url = "http://" + t.app_ip + ":" + std::to_string(t.port) + encode_request_path(path) +
+                          (req.raw_query.empty() ? "" : "?" + req.raw_query);
+  forward(req, resp, url, std::move(h), 300000);
 }
 
 bool Gateway::match(const std::vector<Json>& vss, const std::string& gateway, const std::string& host,
@@ -237,7 +287,7 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   for (const auto& kv : req.headers) {
     std::string k = to_lower(kv.first);
     if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
-    if (k == to_lower(kPeerTokenHeader) || k == to_lower(kProxySecretHeader)) continue;
+    if (k == to_lower(kPeerTokenHeader) || k == to_lower(kProxySecretHeader) || k == to_lower(kHopHeader)) continue;
     if (!trusted_proxy && (k == uid_lc || k == "kubeflow-groups")) continue;  // spoofed identity
     h[kv.first] = kv.second;
   }
@@ -255,7 +305,10 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
     resp.text(403, "RBAC: access denied");
     return;
   }
-  if (!routed_by_route && o_.enforce) decisions_->inc({"ingress", "allow"});
+  if (!routed_by_route && o_.enforce) {
+    decisions_->inc({"ingress", "allow"});
+    h[kHopHeader] = hop_secret_;  // the destination pod's inbound listener takes this decision
+  }
   forward(req, resp, url, std::move(h), static_cast<int>(rt.timeout_s * 1000));
 }
 
@@ -266,22 +319,13 @@ void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
     resp.text(404, "mesh: Host must name a Service (<svc>.<ns>.svc[.<domain>]), got " + host + "\n");
     return;
   }
-  // the caller's workload identity (Istio: the peer's mTLS certificate; here its ServiceAccount
-  // token); a caller without one is plaintext: no principal, no source namespace
-  Identity peer = review_token(req.header(kPeerTokenHeader));
   std::string principal, source_ns;
-  if (peer.authenticated && peer.service_account()) {
-    auto parts = split(peer.username, ':', false);  // system:serviceaccount:<ns>:<name>
-    if (parts.size() == 4) {
-      source_ns = parts[2];
-      principal = o_.cluster_domain + "/ns/" + parts[2] + "/sa/" + parts[3];
-    }
-  }
+  peer_identity(req, principal, source_ns);
   Headers h;
   for (const auto& kv : req.headers) {
     std::string k = to_lower(kv.first);
     if (k == "content-length" || k == "transfer-encoding" || k == "connection") continue;
-    if (k == to_lower(kPeerTokenHeader)) continue;
+    if (k == to_lower(kPeerTokenHeader) || k == to_lower(kHopHeader)) continue;
     h[kv.first] = kv.second;
   }
   const size_t colon = host.find(':');
@@ -294,7 +338,10 @@ void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
     resp.text(403, "RBAC: access denied");
     return;
   }
-  if (o_.enforce) decisions_->inc({"mesh", "allow"});
+  if (o_.enforce) {
+    decisions_->inc({"mesh", "allow"});
+    h[kHopHeader] = hop_secret_;
+  }
   const std::string url = "http://" + svc + "." + ns + ".svc." + o_.cluster_domain + ":" + std::to_string(port) +
                           encode_request_path(path) +
                           (req.raw_query.empty() ? "" : "?" + req.raw_query);

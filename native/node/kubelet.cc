@@ -160,6 +160,8 @@ struct ContainerRt {
 
 struct Kubelet::PodRuntime {
   std::string uid, ns, name, dir, ip;
+  std::string app_ip;  // where its apps listen: ip, or the private address behind the inbound listeners
+  std::vector<std::unique_ptr<HttpServer>> inbound;  // one per containerPort of a mesh-injected pod
   Placement gpus;
   int rdzv_port = 0;  // torch.distributed rendezvous port of a multi-GPU pod (unique on the node)
   bool gpu_ok = true;
@@ -789,6 +791,9 @@ void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
       c.finished_at = ms_now();
       c.pid = -1;
     }
+  // the pod's inbound listeners go with it (the pod IP may be handed out again)
+  for (auto& srv : rt.inbound) srv->stop();
+  rt.inbound.clear();
 }
 
 bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::string& container,
@@ -1122,6 +1127,45 @@ void Kubelet::build_containers(PodRuntime& rt, const Json& pod, const std::map<s
   }
 }
 
+// Istio's injection rule: the namespace carries istio-injection=enabled and the pod does not opt out
+// (profile_controller.go:71 labels every profile namespace); only with a policy enforcer on the node
+bool Kubelet::wants_sidecar(const Json& pod) {
+  if (!inbound_) return false;
+  if (annotation(pod, "sidecar.istio.io/inject") == "false") return false;
+  Json ns;
+  if (c_->get("v1", "Namespace", "", pod.str_at({"metadata", "namespace"}), ns)) return false;
+  return label(ns, "istio-injection") == "enabled";
+}
+
+// the pod's inbound listeners: pod_ip:port for every containerPort, each request through the
+// enforcer, then to app_ip:port
+void Kubelet::start_inbound(PodRuntime& rt, const Json& pod) {
+  InboundTarget base;
+  base.ns = rt.ns;
+  base.name = rt.name;
+  base.app_ip = rt.app_ip;
+  for (const auto& kv : pod.at_path({"metadata", "labels"}).as_object()) base.labels[kv.first] = kv.second.as_string();
+  std::set<int> ports;
+  for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
+    for (const auto& p : c["ports"].as_array())
+      if (p["protocol"].as_string_or("TCP") == "TCP" && p["containerPort"].as_int() > 0)
+        ports.insert(static_cast<int>(p["containerPort"].as_int()));
+  for (int port : ports) {
+    InboundTarget t = base;
+    t.port = port;
+    auto srv = std::make_unique<HttpServer>();
+    InboundHandler h = inbound_;
+    srv->set_handler([h, t](HttpRequest& req, HttpResponse& resp) { h(t, req, resp); });
+    std::string err;
+    if (!srv->listen(rt.ip, port, &err)) {
+      rec_->event(pod, "Warning", "FailedInbound", "inbound listener " + rt.ip + ":" + std::to_string(port) + ": " + err);
+      continue;
+    }
+    srv->start();
+    rt.inbound.push_back(std::move(srv));
+  }
+}
+
 // admission of a new pod: sandbox dir, pod IP, GPUs, volumes, containers; registered on the node
 std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json& pod) {
   auto rt = std::make_shared<PodRuntime>();
@@ -1130,14 +1174,18 @@ std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json
   rt->name = r.name;
   rt->dir = cfg_.root_dir + "/pods/" + r.ns + "_" + r.name + "_" + rt->uid.substr(0, 8);
   make_dirs(rt->dir + "/rootfs");
+  const bool sidecar = wants_sidecar(pod);
   {
     std::lock_guard<std::mutex> g(mu_);
     uint32_t n = next_ip_++;
-    rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
+    const std::string host = "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
+    rt->ip = cfg_.pod_ip_prefix + host;
+    rt->app_ip = sidecar ? cfg_.app_ip_prefix + host : rt->ip;
   }
   rt->start_time = ms_now();
   allocate_gpus(*rt, pod);
   build_containers(*rt, pod, prepare_volumes(*rt, pod));
+  if (sidecar) start_inbound(*rt, pod);
   std::lock_guard<std::mutex> g(mu_);
   pods_[rt->uid] = rt;
   key_to_uid_[r.ns + "/" + r.name] = rt->uid;
@@ -1184,6 +1232,8 @@ void Kubelet::container_env(const PodSync& s, const Json& c, std::vector<std::st
   set("POD_NAME", r.name);
   set("POD_NAMESPACE", r.ns);
   set("POD_IP", rt.ip);
+  // a mesh-injected pod's apps listen on its private address, behind the inbound listeners
+  if (rt.app_ip != rt.ip) set("KFAMD_BIND_IP", rt.app_ip);
   set("KFAMD_POD_DIR", rt.dir);
   set("KFAMD_ROOTFS", rootfs);
   set("KFAMD_TERMINATION_LOG", rt.dir + "/" + c["name"].as_string() + ".termination-log");
@@ -1368,7 +1418,9 @@ std::function<bool()> Kubelet::make_probe(const PodSync& s, const Json& probe, c
   };
   if (probe["httpGet"].is_object()) {
     const Json& hg = probe["httpGet"];
-    const std::string host = hg["host"].as_string_or(rt.ip);
+    // probes go to the app itself (the inbound listener exempts the kubelet as Istio's probe
+    // rewrite does)
+    const std::string host = hg["host"].as_string_or(rt.app_ip);
     std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
     Headers h;
     for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
@@ -1378,7 +1430,7 @@ std::function<bool()> Kubelet::make_probe(const PodSync& s, const Json& probe, c
     };
   }
   if (probe["tcpSocket"].is_object()) {
-    const std::string ip = rt.ip;
+    const std::string ip = rt.app_ip;
     const int port = port_of(probe.at_path({"tcpSocket", "port"}));
     return [ip, port, timeout] { return tcp_connect(ip, port, timeout); };
   }

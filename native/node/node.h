@@ -84,6 +84,7 @@ struct KubeletConfig {
   std::string python = "python3";
   std::string api_url;       // exported to pods as KUBERNETES_SERVICE_HOST/PORT
   std::string pod_ip_prefix = "127.20";
+  std::string app_ip_prefix = "127.21";  // the private address a mesh-injected pod's apps bind
   double restart_backoff = 10.0;
   int gpus = -1;
   int node_cpus = 0;         // advertised CPU capacity (0 = online host CPUs)
@@ -97,6 +98,18 @@ struct KubeletConfig {
 };
 
 struct ContainerRt;  // one container's process state (kubelet.cc)
+
+// A pod's inbound enforcement point (the Istio sidecar's inbound listener): the kubelet binds
+// pod_ip:port for every declared containerPort of a mesh-injected pod, the app listens on the pod's
+// private app_ip, and each request is handed to the gateway's policy check (Gateway::handle_inbound)
+// before it is proxied to app_ip:port. Kubelet probes go to app_ip directly (exempt, as Istio's
+// rewritten probes are).
+struct InboundTarget {
+  std::string ns, name, app_ip;
+  int port = 0;
+  std::map<std::string, std::string> labels;
+};
+using InboundHandler = std::function<void(const InboundTarget&, HttpRequest&, HttpResponse&)>;
 
 class Kubelet {
  public:
@@ -114,6 +127,9 @@ class Kubelet {
             const std::vector<std::string>& argv, double timeout_s, int& exit_code, std::string& output, std::string& err);
   GpuAllocator& gpus() { return *alloc_; }
   const std::string& node_name() const { return cfg_.node_name; }
+  // pods of mesh-injected namespaces (label istio-injection=enabled, pod annotation
+  // sidecar.istio.io/inject not "false") get an inbound listener per containerPort (set before start)
+  void set_inbound_handler(InboundHandler h) { inbound_ = std::move(h); }
 
   struct PodRuntime;
   // image -> argv resolution (unit-tested)
@@ -148,6 +164,9 @@ class Kubelet {
   void run_init_containers(PodSync& s);
   void publish_readiness(PodSync& s);
   ApiError write_status(PodSync& s);
+  bool wants_sidecar(const Json& pod);
+  void start_inbound(PodRuntime& rt, const Json& pod);
+  InboundHandler inbound_;
   std::shared_ptr<Client> c_;
   KubeletConfig cfg_;
   std::unique_ptr<GpuAllocator> alloc_;
@@ -223,6 +242,11 @@ class Gateway {
   // mesh (the destination sidecars' job, done node-wide like Istio ambient's ztunnel): Host names a
   // Service, the caller's identity is its ServiceAccount token in X-Kfamd-Peer-Token
   void handle_mesh(HttpRequest& req, HttpResponse& resp);
+  // a pod's inbound listener (InboundTarget): requests the ingress / mesh listener already
+  // authorized carry this node's hop secret and pass; any other caller (a process dialing the pod IP
+  // directly) is evaluated against the pod's namespace policies with its own identity (ServiceAccount
+  // token in X-Kfamd-Peer-Token, else none); then proxied to the app
+  void handle_inbound(const InboundTarget& t, HttpRequest& req, HttpResponse& resp);
 
   struct Route {
     std::string prefix, rewrite, dest_host;
@@ -248,6 +272,11 @@ class Gateway {
  private:
   bool authorize(const std::string& dest_host, int dest_port, const HttpRequest& req, const std::string& path,
                  const Headers& fwd, const std::string& principal, const std::string& source_ns, std::string* why);
+  bool authorize_workload(const std::string& ns, const std::map<std::string, std::string>& labels, int dest_port,
+                          const HttpRequest& req, const std::string& path, const Headers& fwd,
+                          const std::string& principal, const std::string& source_ns, std::string* why);
+  void peer_identity(const HttpRequest& req, std::string& principal, std::string& source_ns);
+  std::string hop_secret_;  // stamped on requests this gateway authorized (X-Kfamd-Hop)
   void forward(HttpRequest& req, HttpResponse& resp, const std::string& url, Headers h, int timeout_ms);
 
   std::shared_ptr<Client> c_;

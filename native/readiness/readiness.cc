@@ -1021,7 +1021,9 @@ int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
     _exit(rc);
   }
   ::close(fds[1]);
-  const char* ip = std::getenv("POD_IP");
+  // a mesh-injected pod's apps listen on its private address (KFAMD_BIND_IP), where the kubelet probes
+  const char* bind_ip = std::getenv("KFAMD_BIND_IP");
+  const char* ip = bind_ip && *bind_ip ? bind_ip : std::getenv("POD_IP");
   const int ls = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   int one = 1;
   ::setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);

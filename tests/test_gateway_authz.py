@@ -261,3 +261,39 @@ def test_non_service_destination_is_denied_when_enforcing(cl):
         assert got[0] == 403 and "not a Service" in got[1], got
     finally:
         c.delete("networking.istio.io/v1alpha3", "VirtualService", "external", "alice")
+
+
+def test_pod_ip_traffic_is_checked_at_the_pod(cl):
+    """VERDICT r4 item 6 — the Istio sidecar half: profile namespaces are istio-injection=enabled
+    (/root/reference/components/profile-controller/controllers/profile_controller.go:71), so traffic
+    dialed straight to a notebook pod's IP is evaluated against ns-owner-access-istio (:419-556) at the
+    pod's inbound listener: plaintext callers and other namespaces are refused, the namespace's own
+    workloads and the culler's GET */api/kernels pass, the kubelet's probes (sent to the app's
+    private address) are unaffected, and gateway traffic still flows."""
+    c = cl.client
+    pod = c.get("v1", "Pod", "nb-0", "alice")
+    ip = pod["status"]["podIP"]
+    assert any(x["type"] == "Ready" and x["status"] == "True" for x in pod["status"]["conditions"])  # probes fine
+    url = f"http://{ip}:8888/notebook/alice/nb/api/kernels"
+
+    def get(token=None, extra=None):
+        h = {"X-Kfamd-Peer-Token": token} if token else {}
+        h.update(extra or {})
+        return _http(url, headers=h)
+    code, body = get()
+    assert code == 403 and body == "RBAC: access denied", (code, body)
+    # a spoofed userid header is no identity, nor is a guessed hop stamp
+    assert get(extra={"kubeflow-userid": ALICE})[0] == 403
+    assert get(extra={"X-Kfamd-Hop": "0" * 32})[0] == 403
+    assert get(_sa_token(c, "bob-team", "default"))[0] == 403          # another namespace's workload
+    assert get(_sa_token(c, "alice", "default-editor"))[0] == 200      # same namespace
+    assert get(_sa_token(c, "kubeflow", "notebook-controller-service-account"))[0] == 200  # the culler
+    # the culler's rule is GET */api/kernels only
+    nbc = _sa_token(c, "kubeflow", "notebook-controller-service-account")
+    assert _http(f"http://{ip}:8888/notebook/alice/nb/api/terminals", headers={"X-Kfamd-Peer-Token": nbc})[0] == 403
+    # ingress traffic (authorized at the gateway) reaches the pod through the same listener
+    assert _nb(cl, ALICE) == 200 and _nb(cl, BOB) == 403
+    with urllib.request.urlopen(cl.url + "/metrics", timeout=10) as r:
+        text = r.read().decode()
+    deny = [ln for ln in text.splitlines() if ln.startswith('gateway_authz_decisions_total{listener="sidecar",result="deny"}')]
+    assert deny and float(deny[0].split()[-1]) >= 4, deny
