@@ -95,6 +95,10 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// v_exp_f32 as is: the libm exp2f wraps it in a denormal range reduction (v_cmp, v_cndmask, v_ldexp
+// per call) that softmax does not need — a result below 2^-126 is 0 for a probability
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ uint32_t pack2(float x, float y) {
   const bf16x2 v = __builtin_convertvector((f32x2){x, y}, bf16x2);
   return __builtin_bit_cast(uint32_t, v);
@@ -250,7 +254,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
         for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float mn = fmaxf(m, mx);  // finite: the first tile holds key 0 <= every query
-      const float alpha = exp2f((m - mn) * c);
+      // O and l are rescaled only when some row's max grew (exact: alpha == 1 otherwise); late in a
+      // row's sweep that is the rare case, and the 64-register multiply is skipped
+      const bool grew = __builtin_amdgcn_ballot_w64(mx > m) != 0;
+      const float alpha = grew ? fast_exp2((m - mn) * c) : 1.f;
       m = mn;
       const float mc = mn * c;
       float rs = 0.f;
@@ -259,15 +266,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int e = 0; e < 16; e += 2) {
-          const float p0 = exp2f(fmaf(sacc[t][e], c, -mc));
-          const float p1 = exp2f(fmaf(sacc[t][e + 1], c, -mc));
+          const float p0 = fast_exp2(fmaf(sacc[t][e], c, -mc));
+          const float p1 = fast_exp2(fmaf(sacc[t][e + 1], c, -mc));
           rs += p0 + p1;
           pf[t][e >> 3][(e & 7) >> 1] = pack2(p0, p1);
         }
       }
-      l = l * alpha + rs;
+      if (grew) {
+        l = l * alpha + rs;
 #pragma unroll
-      for (int n = 0; n < ND; ++n) oacc[n] *= alpha;
+        for (int n = 0; n < ND; ++n) oacc[n] *= alpha;
+      } else {
+        l += rs;
+      }
 #pragma unroll
       for (int n = 0; n < ND; ++n) {
 #pragma unroll
@@ -330,11 +341,22 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
   if (row < nrows && part == 0) delta[row] = s;
 }
 
+// dS^T image [128 keys][64 queries]: 128-B rows of sixteen 8-B slots (4 queries each), slot ^ f(row),
+// f(row) = (row & 15) ^ (((row >> 1) & 1) << 3). The accumulator's stores (16 lanes = 16 consecutive
+// keys, one slot each) cover all 32 write banks (unswizzled: one slot column, 16-way); the dQ
+// product's transposed reads (4 consecutive keys x 32 queries per 32-lane half) put rows r and r+2,
+// which share a 256-B bank window, on opposite 8-slot halves. (The round-5 first cut's 32-query image
+// without a swizzle cost SQ_LDS_BANK_CONFLICT 4.7e7 cycles per 3 gpt-1b backward passes.)
+__device__ __forceinline__ int dst_off(int row, int slot8) {
+  return row * 128 + ((slot8 ^ ((row & 15) ^ (((row >> 1) & 1) << 3))) << 3);
+}
+
 // ------------------------------------------------------------------------------------------------
-// backward: one workgroup = 4 waves = 128 keys of one (b, h); 32-row query tiles (Q, dO, lse,
-// delta) double-buffered through LDS; dK / dV in registers for the whole sweep
+// backward: one workgroup = 4 waves = 128 keys of one (b, h); 64-row query tiles (Q, dO, lse,
+// delta) double-buffered through LDS, two 32-row S / dP sub-tiles per wave; dK / dV in registers
+// for the whole sweep
 // ------------------------------------------------------------------------------------------------
-constexpr int BK = 128, BQ = 32;
+constexpr int BK = 128, BQ = 64, QS = BQ / 32;
 
 // D = 128 holds dK^T, dV^T (128 registers) and V (32) for the whole sweep: one wave per SIMD
 // (512-register budget, no spills); D = 64 fits two
@@ -349,16 +371,16 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   constexpr int ND = D / 32;
   constexpr int CH = D / 8;
   constexpr int KIMG = BK * D * 2;          // K image: [128 keys][D]
-  constexpr int QT = BQ * D * 2;            // one Q (or dO) tile image: [32][D]
-  constexpr int DST = BK * BQ * 2;          // dS^T image: [128 keys][32 q], 64-B rows
+  constexpr int QT = BQ * D * 2;            // one Q (or dO) tile image: [64][D]
+  constexpr int DST = BK * BQ * 2;          // dS^T image: [128 keys][64 q]
   constexpr int NQC = BQ * CH / 256;        // chunks per thread per Q (and per dO) tile
-  constexpr int KSPLIT = 4 / ND;            // waves sharing one dQ d-tile (key range split)
-  static_assert(NQC >= 1 && KSPLIT >= 1, "head dim");
+  constexpr int DQT = QS * ND / 4;          // 32x32 dQ tiles per wave per query tile
+  static_assert(NQC >= 1 && DQT >= 1, "head dim");
   __shared__ __attribute__((aligned(16))) char smem[KIMG + 4 * QT + DST + 4 * BQ * 4];
   char* const kimg = smem;
   char* const qtiles = smem + KIMG;         // [buf][Q, dO]
   char* const dst = qtiles + 4 * QT;
-  float* const rowc = reinterpret_cast<float*>(dst + DST);  // [buf][lse(32), delta(32)]
+  float* const rowc = reinterpret_cast<float*>(dst + DST);  // [buf][lse(64), delta(64)]
 
   const int T = a.T;
   const int nk = (T + BK - 1) / BK;
@@ -438,8 +460,6 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
     dkacc[n] = (f32x16){};
     dvacc[n] = (f32x16){};
   }
-  // dQ work split: d tile nq_ of the query tile, over keys [kq0, kq0 + 128 / KSPLIT)
-  const int dqn = w % ND, kq0 = (w / ND) * (BK / KSPLIT);
 
   if (ntiles > 0) {
     stage_load(0);
@@ -459,88 +479,97 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
     // causal: every query of the tile precedes every key of the wave -> P = dS = 0
     const bool idle = CAUSAL && q0 + BQ - 1 < kw;
     if (!idle) {
-      f32x16 sacc, dpacc;
-      // row constants: -lse / scale and -delta for the query rows of this lane's registers
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_s + 8 * g + 4 * hh);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(del_s + 8 * g + 4 * hh);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          sacc[4 * g + e] = -l4[e] * inv_scale;
-          dpacc[4 * g + e] = -d4[e];
-        }
-      }
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const bf16x8 qa = lds_row(qi, img_off<D>(r, 2 * kk + hh));
-        const bf16x8 kbf = lds_row(kimg, img_off<D>(32 * w + r, 2 * kk + hh));
-        sacc = mfma32(qa, kbf, sacc);
-        const bf16x8 oa = lds_row(oi, img_off<D>(r, 2 * kk + hh));
-        dpacc = mfma32(oa, vf[kk], dpacc);
-      }
-      // P and dS; rows q = q0 + (e & 3) + 8 (e >> 2) + 4 hh, column = this lane's key
       const bool need_mask = (CAUSAL && q0 < kw + 31) || q0 + BQ > T || key >= T;
-      uint32_t pf[2][4], sf[2][4];
 #pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        float p0 = exp2f(sacc[e] * c), p1 = exp2f(sacc[e + 1] * c);
-        if (need_mask) {
-          const int qa0 = q0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if ((CAUSAL && qa0 < key) || qa0 >= T || key >= T) p0 = 0.f;
-          if ((CAUSAL && qa0 + 1 < key) || qa0 + 1 >= T || key >= T) p1 = 0.f;
+      for (int j = 0; j < QS; ++j) {
+        // one 32-row sub-tile at a time: its P / dS fragments are consumed before the next one's exist
+        uint32_t pf[2][4], sf[2][4];
+        f32x16 sacc, dpacc;
+        // row constants: -lse / scale and -delta for the query rows of this lane's registers
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_s + 32 * j + 8 * g + 4 * hh);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(del_s + 32 * j + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sacc[4 * g + e] = -l4[e] * inv_scale;
+            dpacc[4 * g + e] = -d4[e];
+          }
         }
-        pf[e >> 3][(e & 7) >> 1] = pack2(p0, p1);
-        sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
-      }
-      // dV^T += dO^T . P and dK^T += Q^T . dS (k = the query rows, permuted order)
 #pragma unroll
-      for (int n = 0; n < ND; ++n) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const u32x4 pw = {pf[s][0], pf[s][1], pf[s][2], pf[s][3]};
-          const u32x4 sw = {sf[s][0], sf[s][1], sf[s][2], sf[s][3]};
-          const bf16x8 doa = tr_operand<D>(oi, 16 * s, 32 * n, lane);
-          dvacc[n] = mfma32(doa, __builtin_bit_cast(bf16x8, pw), dvacc[n]);
-          const bf16x8 qa = tr_operand<D>(qi, 16 * s, 32 * n, lane);
-          dkacc[n] = mfma32(qa, __builtin_bit_cast(bf16x8, sw), dkacc[n]);
+        for (int kk = 0; kk < KS; ++kk) {
+          const bf16x8 qa = lds_row(qi, img_off<D>(32 * j + r, 2 * kk + hh));
+          const bf16x8 kbf = lds_row(kimg, img_off<D>(32 * w + r, 2 * kk + hh));
+          sacc = mfma32(qa, kbf, sacc);
+          const bf16x8 oa = lds_row(oi, img_off<D>(32 * j + r, 2 * kk + hh));
+          dpacc = mfma32(oa, vf[kk], dpacc);
         }
-      }
-      // dS^T image [key][q]: registers 4g..4g+3 are queries 8g + 4hh .. +3 of this lane's key
+        // P and dS; rows q = q0 + 32 j + (e & 3) + 8 (e >> 2) + 4 hh, column = this lane's key
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const u32x2 v2 = {sf[g >> 1][2 * (g & 1)], sf[g >> 1][2 * (g & 1) + 1]};
-        *reinterpret_cast<u32x2*>(dst + (32 * w + r) * 64 + (8 * g + 4 * hh) * 2) = v2;
+        for (int e = 0; e < 16; e += 2) {
+          float p0 = fast_exp2(sacc[e] * c), p1 = fast_exp2(sacc[e + 1] * c);
+          if (need_mask) {
+            const int qa0 = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if ((CAUSAL && qa0 < key) || qa0 >= T || key >= T) p0 = 0.f;
+            if ((CAUSAL && qa0 + 1 < key) || qa0 + 1 >= T || key >= T) p1 = 0.f;
+          }
+          pf[e >> 3][(e & 7) >> 1] = pack2(p0, p1);
+          sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
+        }
+        // dS^T image [key][q]: registers 4g..4g+3 are queries 32 j + 8 g + 4 hh .. +3 of this lane's key
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const u32x2 v2 = {sf[g >> 1][2 * (g & 1)], sf[g >> 1][2 * (g & 1) + 1]};
+          *reinterpret_cast<u32x2*>(dst + dst_off(32 * w + r, 8 * j + 2 * g + hh)) = v2;
+        }
+        // dV^T += dO^T . P and dK^T += Q^T . dS over this sub-tile's rows (permuted k order)
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+#pragma unroll
+          for (int sx = 0; sx < 2; ++sx) {
+            const u32x4 pw = {pf[sx][0], pf[sx][1], pf[sx][2], pf[sx][3]};
+            const u32x4 sw = {sf[sx][0], sf[sx][1], sf[sx][2], sf[sx][3]};
+            const bf16x8 doa = tr_operand<D>(oi, 32 * j + 16 * sx, 32 * n, lane);
+            dvacc[n] = mfma32(doa, __builtin_bit_cast(bf16x8, pw), dvacc[n]);
+            const bf16x8 qa = tr_operand<D>(qi, 32 * j + 16 * sx, 32 * n, lane);
+            dkacc[n] = mfma32(qa, __builtin_bit_cast(bf16x8, sw), dkacc[n]);
+          }
+        }
       }
     } else {
+      // this wave's 32 rows of the dS^T image are zero (lane half hh clears slots 8 hh .. 8 hh + 7)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<u32x2*>(dst + (32 * w + r) * 64 + (8 * g + 4 * hh) * 2) = (u32x2){0u, 0u};
+      for (int sl = 0; sl < 8; ++sl)
+        *reinterpret_cast<u32x2*>(dst + dst_off(32 * w + r, 8 * hh + sl)) = (u32x2){0u, 0u};
     }
     __syncthreads();
 
-    // dQ[q][d] (this wave: d tile dqn over keys kq0 .. kq0 + 128/KSPLIT): A = dS rows from the
-    // [key][q] image by tr reads, B = K columns from the K image by tr reads
+    // dQ[q][d]: this wave's 32x32 output tiles (query sub-tile j, d tile n), all 128 keys: A = dS rows
+    // from the [key][q] image by tr reads, B = K columns from the K image by tr reads
     {
-      f32x16 dqacc = (f32x16){};
       const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
 #pragma unroll
-      for (int kk = 0; kk < BK / KSPLIT / 16; ++kk) {
-        const int kr = kq0 + 16 * kk + 8 * hh + qq;   // key row of this lane's tr-read address
-        const int qc = 16 * (g & 1) + 4 * p;          // query column
-        const bf16x8 da = join(tr_read(dst, kr * 64 + qc * 2), tr_read(dst, (kr + 4) * 64 + qc * 2));
-        const int dc = 32 * dqn + 16 * (g & 1) + 4 * p;
-        const bf16x8 kbf = join(tr_read(kimg, img_off<D>(kr, dc >> 3) + 8 * (p & 1)),
-                                tr_read(kimg, img_off<D>(kr + 4, dc >> 3) + 8 * (p & 1)));
-        dqacc = mfma32(da, kbf, dqacc);
-      }
-      // rows q0 + (e & 3) + 8 (e >> 2) + 4 hh, column d = 32 dqn + r: f32 atomics, each wave
-      // instruction two 128-B row segments
-      float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
+      for (int tt = 0; tt < DQT; ++tt) {
+        const int t = w + 4 * tt, j = t / ND, dqn = t % ND;
+        f32x16 dqacc = (f32x16){};
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int qr = q0 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-        if (qr < T) __hip_atomic_fetch_add(dqb + qr * dq_st, dqacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int kk = 0; kk < BK / 16; ++kk) {
+          const int kr = 16 * kk + 8 * hh + qq;          // key row of this lane's tr-read address
+          const int qs = 8 * j + 4 * (g & 1) + p;        // 8-B slot of queries 32 j + 16 (g & 1) + 4 p .. +3
+          const bf16x8 da = join(tr_read(dst, dst_off(kr, qs)), tr_read(dst, dst_off(kr + 4, qs)));
+          const int dc = 32 * dqn + 16 * (g & 1) + 4 * p;
+          const bf16x8 kbf = join(tr_read(kimg, img_off<D>(kr, dc >> 3) + 8 * (p & 1)),
+                                  tr_read(kimg, img_off<D>(kr + 4, dc >> 3) + 8 * (p & 1)));
+          dqacc = mfma32(da, kbf, dqacc);
+        }
+        // rows q0 + 32 j + (e & 3) + 8 (e >> 2) + 4 hh, column d = 32 dqn + r: f32 atomics, each wave
+        // instruction two 128-B row segments
+        float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int qr = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (qr < T) __hip_atomic_fetch_add(dqb + qr * dq_st, dqacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
     if (more) stage_write((it + 1) & 1);
