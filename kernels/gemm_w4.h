@@ -221,7 +221,7 @@ struct Reader {
 // within the deadline is recomputed by the owner itself, so a non-co-resident grid is slow, never
 // hung or wrong.
 template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, int SPLIT = 0,
-          bool DIAG = false, int ABL = 0, bool SK = false>
+          bool DIAG = false, int ABL = 0, bool SK = false, bool PO = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
@@ -262,6 +262,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(SPLIT != 1 || (ACT == KFAMD_ACT_NONE && !HAS_BIAS && !HAS_RES && !HAS_AUX), "split-K: epilogue in the reduce");
   static_assert(SPLIT != 2 || BM == 256, "split-K fixup: 256 tile");
   static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
+  static_assert(!PO || (BM == 256 && !SPLIT && !SK && !DIAG), "persistent overlapped: 256 tile, whole K");
+  // PO: the epilogue's LDS staging lives in the ring's fifth slot, which the next tile's prologue
+  // (tiles 0 and 1 into slots 0-3) leaves alone, so that prologue can be issued before the epilogue
+  constexpr int kEpiBase = PO ? (kSlots - 1) * TILE : 0;
   __shared__ __attribute__((aligned(16))) char smem[kSlots * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -426,20 +430,28 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   unsigned long long sk_mask = 0;  // stream-K owner: which producer splits' partials the epilogue adds
   int sk_base = 0, sk_stride = 0;  // ... split j's partial is slot sk_base + j * sk_stride
   // prologue + K loop over the current (ra, rb, nk, koff): adds into acc
-  auto run_k = [&]() __attribute__((always_inline)) {
-  // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
-  int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
-#pragma unroll
-  for (int j = 0; j < PIECES; ++j) {
-    dma_a(0, sa0, j, true);
-    dma_b(0, sb0, j, true);
-  }
-  if (nk > 1) {
+  // the first two K tiles into slots 0-3 (PO issues them for the next tile before this one's epilogue)
+  auto issue_prologue = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
-      dma_a(1, sa1, j, false);
-      dma_b(1, sb1, j, false);
+      dma_a(0, 0, j, true);
+      dma_b(0, 1, j, true);
     }
+    if (nk > 1) {
+#pragma unroll
+      for (int j = 0; j < PIECES; ++j) {
+        dma_a(1, 2, j, false);
+        dma_b(1, 3, j, false);
+      }
+    }
+  };
+  auto run_k = [&](auto pro_issued) __attribute__((always_inline)) {
+  // slot state (wave-uniform): tile t in (sa0, sb0), tile t+1 in (sa1, sb1), free slot sf
+  int sa0 = 0, sb0 = 1, sa1 = 2, sb1 = 3, sf = 4;
+  if constexpr (!decltype(pro_issued)::value) issue_prologue();
+  if (nk > 1) {
+    // (PO: the epilogue's stores were issued after these DMAs; counting them in too only waits
+    // longer, and the epilogue has covered the DMAs' latency)
     if constexpr (BM == 256) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   } else {
@@ -464,7 +476,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     const unsigned lw = lds_w;  // (named here: a nested generic lambda does not capture it otherwise)
     auto m0_set = [&](int slot, int j) __attribute__((always_inline)) {
       const unsigned m0v = lw + (unsigned)(slot * TILE + j * 1024);
-      asm volatile("s_mov_b32 m0, %0" ::"s"(m0v) : "memory");
+      asm volatile("s_mov_b32 m0, %0" ::"s"(m0v) : "memory", "m0");
     };
     auto asm_dma = [&](const i32x4& r, unsigned v, int so) __attribute__((always_inline)) {
       asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(v), "s"(r), "s"(so) : "memory");
@@ -721,7 +733,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       // is 16 rows x 32 fp32; lane (lh, lr) holds row lr, 16 B at slot (n & 1) * 4 + lh; staged in the
       // wave's 2 KiB of the idle ring (slot c of row r at r * 128 + 16 * (c ^ ((r >> 1) & 7))) and read
       // back by rows (8 lanes per row)
-      char* stage = smem + wid * 2048;
+      char* stage = smem + kEpiBase + wid * 2048;
       const int wsw = (elr >> 1) & 7;
       const int w0 = elr * 128 + 16 * (elh ^ wsw), w1 = elr * 128 + 16 * ((4 + elh) ^ wsw);
       const int rr = elane >> 3, rc = elane & 7;
@@ -814,7 +826,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   // lanes) and the reads (two rows of 8 slots per 16 lanes) both cover 16 distinct bank quads.
   auto emit_fullline = [&](auto UNIT) {
     static_assert(NR % 4 == 0, "full-line stores: two block pairs per span");
-    char* stage = smem + wid * 2048;
+    char* stage = smem + kEpiBase + wid * 2048;
     // write side: this lane's row lr, slots ch(lh) (pair n) and 4 + ch(lh) (pair n+2); ch = 2*(lh&1) + (lh>>1)
     const int ch = 2 * (elh & 1) + (elh >> 1);
     const int wsw = (elr >> 1) & 7;
@@ -892,7 +904,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   };
   auto emit_fullline_res = [&](auto UNIT) {
     static_assert(NR % 4 == 0, "full-line stores: four blocks per span");
-    char* stage = smem + wid * 4096;
+    char* stage = smem + kEpiBase + wid * 4096;
     const int rr = elane >> 3, rc = elane & 7;
     const int ra0 = rr * 256 + 16 * ((2 * rc) ^ rr), ra1 = rr * 256 + 16 * ((2 * rc + 1) ^ rr);
     const int rb0 = (rr + 8) * 256 + 16 * ((2 * rc) ^ (rr + 8)), rb1 = (rr + 8) * 256 + 16 * ((2 * rc + 1) ^ (rr + 8));
@@ -1073,7 +1085,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       }
       zero_acc_if(zero);
       __syncthreads();  // the previous item's fragment reads are done before the ring refills
-      run_k();
+      run_k(std::false_type{});
       if (role == 1) {
 #pragma unroll
         for (int i = 0; i < NR; ++i)
@@ -1135,7 +1147,73 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     }
     return;
   }
-  run_k();
+  if constexpr (PO) {
+    // ---- persistent, overlapped (batch 1, whole K): block b runs tiles b, b + G, b + 2G, ... of the
+    // XCD-remapped order (G % 8 == 0 keeps every tile of a block on its XCD's contiguous chunk). The
+    // next tile's first two K tiles are DMA'd before this tile's epilogue, so their latency and the
+    // ring refill hide under its stores; no block boundary between tiles.
+    const int G = gridDim.x;
+    auto set_tile = [&](int w) __attribute__((always_inline)) {
+      const int gg = w / per_group, fm = gg * kGroupM;
+      const int gmm = min(tiles_m - fm, kGroupM);
+      const int tm_ = fm + (w % per_group) % gmm, tn_ = (w % per_group) / gmm;
+      m_lo = tm_ * BM;
+      n_lo = tn_ * BN;
+      m0 = min(m_lo, M - BM);
+      n0 = min(n_lo, N - BN);
+    };
+    auto set_operands = [&]() __attribute__((always_inline)) {
+      const __bf16* a = A_in + (LA == 0 ? (long long)m0 * lda + ka : (long long)m0 + ka * lda);
+      const __bf16* b = B_in + (LB == 0 ? (long long)n0 * ldb + ka : (long long)n0 + ka * ldb);
+      ra = __builtin_amdgcn_make_buffer_rsrc((void*)a, (short)0, nrec, kRsrcWord3);
+      rb = __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, nrec, kRsrcWord3);
+      if (kAsmDma) {
+        dra = make_desc(a);
+        drb = make_desc(b);
+      }
+    };
+    static_assert(NR % 4 == 0, "zero_acc: 4 accumulators per asm");
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+      // an MFMA of zero fragments with C = 0 writes each AGPR (one unconditional def per tile, so the
+      // loop-carried accumulators stay in AGPRs); the asm pads the VALU -> MFMA operand hazard of the
+      // zero fragment's v_mov (invisible to the hazard recognizer) and its own write latency
+      const bf16x8 z = {};
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int n = 0; n < NR; n += 4)
+          asm volatile(
+              "s_nop 4\n\tv_mfma_f32_16x16x32_bf16 %0, %4, %4, 0\n\tv_mfma_f32_16x16x32_bf16 %1, %4, %4, 0\n\t"
+              "v_mfma_f32_16x16x32_bf16 %2, %4, %4, 0\n\tv_mfma_f32_16x16x32_bf16 %3, %4, %4, 0\n\t"
+              "s_nop 7\n\ts_nop 7\n\ts_nop 7"
+              : "=a"(acc[i][n]), "=a"(acc[i][n + 1]), "=a"(acc[i][n + 2]), "=a"(acc[i][n + 3])
+              : "v"(z));
+    };
+    int j = blockIdx.x;  // the kernel prologue set this block's first tile (wg = xcd_remap(j, nwg))
+    issue_prologue();
+    while (true) {
+      run_k(std::true_type{});
+      const int jn = j + G;
+      const bool more = jn < nwg;
+      const int cm0 = m0, cn0 = n0, cmlo = m_lo, cnlo = n_lo;
+      int nm0 = 0, nn0 = 0, nmlo = 0, nnlo = 0;
+      if (more) {
+        set_tile(xcd_remap(jn, nwg));
+        set_operands();
+        nm0 = m0, nn0 = n0, nmlo = m_lo, nnlo = n_lo;
+        m0 = cm0, n0 = cn0, m_lo = cmlo, n_lo = cnlo;
+        __syncthreads();  // every wave's last fragment reads of this tile are done before the ring refills
+        issue_prologue();
+      }
+      epilogue();
+      if (!more) break;
+      m0 = nm0, n0 = nn0, m_lo = nmlo, n_lo = nnlo;
+      j = jn;
+      zero_acc();
+    }
+    return;
+  }
+  run_k(std::false_type{});
   if constexpr (SPLIT == 2) {
     // ---- split-K fixup: publish this split's partial, the last split to arrive finishes the tile ----
 #ifndef KFW4_FIX_AB

@@ -30,3 +30,19 @@ extern "C" int w4ab_diag(const void* A, const void* B, void* C, int M, int N, in
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
+
+// persistent, overlapped schedule (gemm_w4.h PO): `grid` blocks (a multiple of 8, e.g. the CU count)
+// each run tiles b, b + grid, ... of the XCD-remapped order
+extern "C" int w4ab_po(const void* A, const void* B, void* C, int M, int N, int K, int grid_blocks, void* stream) {
+  const int rc = check_shape(0, 0, 256, A, B, C, nullptr, nullptr, nullptr, M, N, K, K, K, N, 0, 0, 0, 0, 0);
+  if (rc != KFAMD_OK) return rc;
+  const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
+  if (grid_blocks <= 0 || grid_blocks % 8) return KFAMD_EINVAL;
+  dim3 grid(grid_blocks < nwg ? grid_blocks : nwg, 1), block(kThreads);
+  hipLaunchKernelGGL((gemm_w4<KFAMD_ACT_NONE, false, false, false, 0, 0, 256, 0, false, 0, false, true>), grid,
+                     block, 0, reinterpret_cast<hipStream_t>(stream), static_cast<const __bf16*>(A),
+                     static_cast<const __bf16*>(B), static_cast<__bf16*>(C), nullptr, nullptr, nullptr, M, N, K,
+                     (long long)K, (long long)K, (long long)N, 0LL, 0LL, 0LL, 0LL, 0LL, 1.0f, nullptr);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}

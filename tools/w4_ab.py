@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--sizes", default="4096,8192,16384")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--diag", default="8192")
+    ap.add_argument("--po-grid", type=int, default=256, help="blocks of the persistent-overlapped (PO) launch")
     a = ap.parse_args()
     names = [v for v in a.variants.split(",") if v]
     if a.build:
@@ -92,6 +93,8 @@ def main():
         L.w4ab_nt.argtypes = [vp, vp, vp, i, i, i, vp]
         L.w4ab_diag.restype = i
         L.w4ab_diag.argtypes = [vp, vp, vp, i, i, i, vp, vp]
+        L.w4ab_po.restype = i
+        L.w4ab_po.argtypes = [vp, vp, vp, i, i, i, i, vp]
         libs[n] = L
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev).cuda_stream
@@ -105,10 +108,15 @@ def main():
             assert L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st) == 0
             torch.cuda.synchronize()
             same[n] = bool(torch.equal(C, ref))
+            C.zero_()
+            assert L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, a.po_grid, st) == 0
+            torch.cuda.synchronize()
+            same[n + "_po"] = bool(torch.equal(C, ref))
         iters = max(5, int(3e13 / (2 * s ** 3)))
         fns = {"prod": lambda: ops.gemm_nt(A, B, out=C), "torch": lambda: torch.matmul(A, B.t())}
         for n, L in libs.items():
             fns[n] = (lambda L=L: L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st))
+            fns[n + "_po"] = (lambda L=L: L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, a.po_grid, st))
         t_end = time.perf_counter() + 1.0
         while time.perf_counter() < t_end:
             fns["prod"]()
