@@ -1798,75 +1798,22 @@ void Kubelet::register_gpu_metrics() {
   metrics_registered_ = true;
 }
 
-// Live SMU telemetry per MI355X (AMD SMI gpu_metrics, gpu/smi.h), labelled with the pod that holds
-// the device: what a notebook's GPUs are doing (GFX / HBM-controller activity), the clock they
-// hold under load (MFMA-dense kernels are clock-limited on this part), power, temperatures,
-// energy, xGMI traffic per link (RCCL rings over xGMI) and power/thermal throttle residency. One
-// AMD SMI sample serves every family of a scrape (cached 1 s).
-void Kubelet::register_telemetry_metrics() {
+namespace {
+
+// one discovered GPU's latest sample: device index, telemetry, the sample before (throttle residency
+// is a delta), and the pod holding it
+struct TelemetryRow {
+  int gpu;
+  GpuTelemetry t;
+  bool has_prev;
+  GpuTelemetry prev;
+  std::string ns, pod;
+};
+using TelemetryRows = std::function<std::vector<TelemetryRow>()>;
+
+// the metric families over one (cached) telemetry source
+void add_telemetry_families(const TelemetryRows& rows) {
   auto& reg = Registry::global();
-  struct Cache {
-    std::mutex mu;
-    double at = -1e9;
-    std::vector<GpuTelemetry> last, prev;  // prev: the sample before, for throttle-residency deltas
-  };
-  auto cache = std::make_shared<Cache>();
-  // (device index, telemetry, previous telemetry or null, namespace, pod) for every discovered GPU
-  struct Row {
-    int gpu;
-    GpuTelemetry t;
-    bool has_prev;
-    GpuTelemetry prev;
-    std::string ns, pod;
-  };
-  auto rows = [this, cache]() {
-    std::vector<Row> out;
-    std::vector<GpuTelemetry> cur, prev;
-    {
-      std::lock_guard<std::mutex> g(cache->mu);
-      const double t = now_seconds();
-      if (t - cache->at > 1.0) {
-        auto s = AmdSmi::instance().sample();
-        if (!s.empty()) {
-          cache->prev = std::move(cache->last);
-          cache->last = std::move(s);
-        }
-        cache->at = t;
-      }
-      cur = cache->last;
-      prev = cache->prev;
-    }
-    if (cur.empty()) return out;
-    std::map<int, std::pair<std::string, std::string>> owner;
-    const auto allocs = alloc_->allocations();
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      for (const auto& a : allocs) {
-        auto it = pods_.find(a.first);
-        for (int d : a.second)
-          owner[d] = it != pods_.end() ? std::make_pair(it->second->ns, it->second->name) : std::make_pair(std::string(), a.first);
-      }
-    }
-    for (const auto& gdev : alloc_->topology().gpus) {
-      for (const auto& t : cur) {
-        if (t.bdf != gdev.pci_bus) continue;
-        Row r{gdev.index, t, false, {}, "", ""};
-        for (const auto& p : prev)
-          if (p.bdf == t.bdf) {
-            r.has_prev = true;
-            r.prev = p;
-          }
-        auto o = owner.find(gdev.index);
-        if (o != owner.end()) {
-          r.ns = o->second.first;
-          r.pod = o->second.second;
-        }
-        out.push_back(r);
-        break;
-      }
-    }
-    return out;
-  };
   using Field = double (*)(const GpuTelemetry&);
   struct PerPod {
     const char* name;
@@ -1958,6 +1905,71 @@ void Kubelet::register_telemetry_metrics() {
         }
         return out;
       }));
+}
+
+}  // namespace
+
+// Live SMU telemetry per MI355X (AMD SMI gpu_metrics, gpu/smi.h), labelled with the pod that holds
+// the device: what a notebook's GPUs are doing (GFX / HBM-controller activity), the clock they
+// hold under load (MFMA-dense kernels are clock-limited on this part), power, temperatures,
+// energy, xGMI traffic per link (RCCL rings over xGMI) and power/thermal throttle residency. One
+// AMD SMI sample serves every family of a scrape (cached 1 s).
+void Kubelet::register_telemetry_metrics() {
+  struct Cache {
+    std::mutex mu;
+    double at = -1e9;
+    std::vector<GpuTelemetry> last, prev;  // prev: the sample before, for throttle-residency deltas
+  };
+  auto cache = std::make_shared<Cache>();
+  auto rows = [this, cache]() {
+    std::vector<TelemetryRow> out;
+    std::vector<GpuTelemetry> cur, prev;
+    {
+      std::lock_guard<std::mutex> g(cache->mu);
+      const double t = now_seconds();
+      if (t - cache->at > 1.0) {
+        auto s = AmdSmi::instance().sample();
+        if (!s.empty()) {
+          cache->prev = std::move(cache->last);
+          cache->last = std::move(s);
+        }
+        cache->at = t;
+      }
+      cur = cache->last;
+      prev = cache->prev;
+    }
+    if (cur.empty()) return out;
+    std::map<int, std::pair<std::string, std::string>> owner;
+    const auto allocs = alloc_->allocations();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& a : allocs) {
+        auto it = pods_.find(a.first);
+        for (int d : a.second)
+          owner[d] = it != pods_.end() ? std::make_pair(it->second->ns, it->second->name) : std::make_pair(std::string(), a.first);
+      }
+    }
+    for (const auto& gdev : alloc_->topology().gpus) {
+      for (const auto& t : cur) {
+        if (t.bdf != gdev.pci_bus) continue;
+        TelemetryRow r{gdev.index, t, false, {}, "", ""};
+        for (const auto& p : prev)
+          if (p.bdf == t.bdf) {
+            r.has_prev = true;
+            r.prev = p;
+          }
+        auto o = owner.find(gdev.index);
+        if (o != owner.end()) {
+          r.ns = o->second.first;
+          r.pod = o->second.second;
+        }
+        out.push_back(r);
+        break;
+      }
+    }
+    return out;
+  };
+  add_telemetry_families(rows);
 }
 
 void Kubelet::setup(Manager& mgr) {
