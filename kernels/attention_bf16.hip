@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "kfamd_kernels.h"
+#include "wave_ops.h"
 
 namespace {
 
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[t][e]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = kfw::max_halves(mx);  // the row's other 32 keys (v_permlane32_swap; no LDS round trip)
       const float mn = fmaxf(m, mx);  // finite: the first tile holds key 0 <= every query
       // O and l are rescaled only when some row's max grew (exact: alpha == 1 otherwise); late in a
       // row's sweep that is the rare case, and the 64-register multiply is skipped
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   }
 
   // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
-  const float lt = l + __shfl_xor(l, 32);
+  const float lt = kfw::sum_halves(l);
   const float inv = 1.f / lt;
   if (qrow < T) {
     __bf16* ob = o + base_off(a, TO, b, h) + qrow * a.s[TO][2];
@@ -336,8 +337,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) s = fmaf((float)xb[e], (float)yb[e], s);
   }
-#pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  s = kfw::group_sum<LPR>(s);
   if (row < nrows && part == 0) delta[row] = s;
 }
 

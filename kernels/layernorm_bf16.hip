@@ -10,17 +10,15 @@
 //    partial-sum kernel + a finalize kernel (deterministic, no float atomics).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "kfamd_kernels.h"
+#include "wave_ops.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+using kfw::wave_sum;  // DPP + permlane swaps, no LDS round trips (wave_ops.h)
 
 // Block reduction for the generic (one workgroup per row) kernels. 256 threads = 4 waves.
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -37,7 +35,11 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // W bf16 per lane per unit: 8 (16-byte loads, hidden = 512 * VPL) or 4 (8-byte loads, hidden =
 // 256 * VPL for the widths 256 / 768 / 1280 that are not multiples of 512)
-template <int VPL, bool RMS, int W = 8>
+// PF: gamma / beta are loaded with the row, before the reductions (their L2 latency overlaps the
+// statistics instead of following them), at the cost of their registers: used at VPL 16 (hidden
+// 8192), +3.5 % at 8192 x 8192 and +4.6 % at 32768 x 8192; at VPL <= 8 it measured 1-5 % slower
+// (profiles/r5j_ln_ab)
+template <int VPL, bool RMS, int W = 8, bool PF = false>
 __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ x,
                                                     const __bf16* __restrict__ gamma,
                                                     const __bf16* __restrict__ beta,
@@ -57,6 +59,16 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   vec_t v[VPL];
 #pragma unroll
   for (int j = 0; j < VPL; ++j) v[j] = __builtin_nontemporal_load(&xr[j * 64 + lane]);  // streamed once
+  const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
+  const vec_t* b8 = reinterpret_cast<const vec_t*>(beta);
+  vec_t gpre[PF ? VPL : 1], bpre[PF ? VPL : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      gpre[j] = g8[j * 64 + lane];
+      if (!RMS && beta) bpre[j] = b8[j * 64 + lane];
+    }
+  }
   float mean = 0.f;
   if (!RMS) {
     float s = 0.f;
@@ -87,14 +99,12 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   if constexpr (kRepack)
 #pragma unroll
     for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
-  const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
-  const vec_t* b8 = reinterpret_cast<const vec_t*>(beta);
   vec_t* yr = reinterpret_cast<vec_t*>(y + (long long)row * H);
 #pragma unroll
   for (int j = 0; j < VPL; ++j) {
-    const vec_t g = g8[j * 64 + lane];
+    const vec_t g = PF ? gpre[PF ? j : 0] : g8[j * 64 + lane];
     vec_t b;
-    if (!RMS && beta) b = b8[j * 64 + lane];
+    if (!RMS && beta) b = PF ? bpre[PF ? j : 0] : b8[j * 64 + lane];
     vec_t o;
 #pragma unroll
     for (int e = 0; e < W; ++e) {
@@ -103,6 +113,96 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
       o[e] = (__bf16)r;
     }
     __builtin_nontemporal_store(o, &yr[j * 64 + lane]);
+  }
+}
+
+// Streaming forward (hidden = 512 * VPL, VPL <= 8): a grid of resident waves, each sweeping rows
+// wave, wave + nw, ... with the NEXT row's loads issued before this row's statistics, so every wave
+// always has a row in flight (no generation-by-generation load / compute / store phases, no tail of
+// late rows). gamma / beta sit in LDS (one copy per workgroup): their reads wait on lgkmcnt, so no
+// vmcnt wait for them also waits for the prefetched row.
+template <int VPL, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_stream(const __bf16* __restrict__ x,
+                                                      const __bf16* __restrict__ gamma,
+                                                      const __bf16* __restrict__ beta,
+                                                      __bf16* __restrict__ y, float* __restrict__ mean_out,
+                                                      float* __restrict__ rstd_out, int rows, float eps) {
+  constexpr int H = VPL * 512;
+  __shared__ bf16x8 sg[H / 8], sb[RMS ? 1 : H / 8];
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < H / 8; i += 256) {
+    sg[i] = reinterpret_cast<const bf16x8*>(gamma)[i];
+    if (!RMS) sb[i] = beta ? reinterpret_cast<const bf16x8*>(beta)[i] : bf16x8{};
+  }
+  __syncthreads();
+  const int nw = gridDim.x * 4;
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;  // wave-uniform; no barriers below
+  auto load = [&](bf16x8 (&v)[VPL], int r) __attribute__((always_inline)) {
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (long long)r * H);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) v[j] = __builtin_nontemporal_load(&xr[j * 64 + lane]);
+  };
+  // the empty asms "redefine" the packed row before each pass, so the compiler widens it per pass
+  // instead of keeping fp32 copies of both buffers live
+  auto opaque = [&](bf16x8 (&v)[VPL]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
+  };
+  auto finish = [&](bf16x8 (&v)[VPL], int r) __attribute__((always_inline)) {
+    opaque(v);
+    float mean = 0.f;
+    if (!RMS) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)v[j][e];
+      mean = wave_sum(s) * (1.f / H);
+    }
+    opaque(v);
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)v[j][e] - mean;
+        ss += d * d;
+      }
+    const float rstd = rsqrtf(wave_sum(ss) * (1.f / H) + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[r] = mean;
+      if (rstd_out) rstd_out[r] = rstd;
+    }
+    opaque(v);
+    bf16x8* yr = reinterpret_cast<bf16x8*>(y + (long long)r * H);
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const bf16x8 g = sg[j * 64 + lane];
+      bf16x8 b{};
+      if (!RMS) b = sb[j * 64 + lane];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float t = ((float)v[j][e] - mean) * rstd * (float)g[e];
+        if (!RMS) t += (float)b[e];
+        o[e] = (__bf16)t;
+      }
+      __builtin_nontemporal_store(o, &yr[j * 64 + lane]);
+    }
+  };
+  bf16x8 va[VPL], vb[VPL];
+  load(va, row);
+  while (true) {
+    const int r1 = row + nw;
+    if (r1 < rows) load(vb, r1);
+    finish(va, row);
+    if (r1 >= rows) break;
+    const int r2 = r1 + nw;
+    if (r2 < rows) load(va, r2);
+    finish(vb, r1);
+    if (r2 >= rows) break;
+    row = r2;
   }
 }
 
@@ -355,6 +455,25 @@ inline int vpl4_for(int hidden) {
   return (v == 1 || v == 3 || v == 5) ? v : 0;
 }
 
+// rows the device holds at once for a one-wave-per-row kernel of 256-thread blocks (occupancy x CUs
+// x 4 waves), per kernel, queried once
+template <auto kernel>
+long long resident_rows() {
+  static const long long n = [] {
+    int occ = 0, cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, 0) != hipSuccess) occ = 1;
+    return 4LL * (occ > 0 ? occ : 1) * (cus > 0 ? cus : 256);
+  }();
+  return n;
+}
+
+// Forward launch policy (profiles/r5j_ln_ab, one box, kbench): the one-shot wave-per-row kernel,
+// except when its grid would take between one and two generations of resident waves: there the
+// second generation's load / compute / store phases do not overlap the first's, and the streaming
+// kernel (resident waves, next row prefetched) is faster: 8192 x 4096 24.1 -> 22.1 us (6.06 TB/s).
+// At one generation or at four (16384 x 4096: 46.3 vs 47.4 us) the one-shot kernel wins.
 template <bool RMS>
 int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
              int rows, int hidden, float eps, void* stream) {
@@ -369,8 +488,18 @@ int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float*
   if (vec) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (vpl) {
-#define KFAMD_NORM_FWD_CASE(V) \
-  case V: hipLaunchKernelGGL((norm_fwd_wave<V, RMS>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); break;
+#define KFAMD_NORM_FWD_CASE(V)                                                                                   \
+  case V:                                                                                                      \
+    if (V <= 8 && rows > resident_rows<norm_fwd_wave<V, RMS, 8, V == 16>>() &&                              \
+        rows <= 2 * resident_rows<norm_fwd_wave<V, RMS, 8, V == 16>>()) {                                       \
+      const long long waves = resident_rows<norm_fwd_stream<V <= 8 ? V : 8, RMS>>();                             \
+      const long long rpw = (rows + waves - 1) / waves; /* rows per wave, the same for every wave */          \
+      hipLaunchKernelGGL((norm_fwd_stream<V <= 8 ? V : 8, RMS>), dim3((int)((rows + 4 * rpw - 1) / (4 * rpw))), \
+                         block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps);                                  \
+    } else {                                                                                                   \
+      hipLaunchKernelGGL((norm_fwd_wave<V, RMS, 8, V == 16>), grid, block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps); \
+    }                                                                                                          \
+    break;
       KFAMD_FOR_EACH_VPL(KFAMD_NORM_FWD_CASE)
 #undef KFAMD_NORM_FWD_CASE
     }

@@ -12,22 +12,15 @@
 #include <math.h>
 
 #include "kfamd_kernels.h"
+#include "wave_ops.h"
 
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kThreads = 256, kWaves = kThreads / 64;
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+using kfw::wave_max;  // DPP + permlane swaps (wave_ops.h)
+using kfw::wave_sum;
 
 // row max and sum of exp(x - max) over [0, V), online (one pass); result in every thread
 __device__ __forceinline__ void row_stats(const __bf16* __restrict__ x, int V, bool vec, float& mx, float& sm) {

@@ -146,6 +146,29 @@ def test_layernorm_fwd_bwd(rows, H):
     assert (b.grad.float() - br.grad).abs().max().item() < 2e-2 * (br.grad.abs().max().item() + 1)
 
 
+@pytest.mark.parametrize("rows,H,rms", [(6001, 4096, False), (8192, 4096, False), (12289, 1024, False),
+                                        (6001, 4096, True), (8192, 8192, False), (32768, 512, False)])
+def test_norm_forward_launch_paths(rows, H, rms):
+    """The forward's launch policy (layernorm_bf16.hip norm_fwd): 1-2 generations of resident waves
+    take the streaming kernel (resident waves, next row prefetched, gamma/beta in LDS) — 6001 / 8192
+    rows at hidden 4096, 12289 at 1024, odd counts leave waves with one row fewer; hidden 8192 takes
+    the gamma/beta-prefetch kernel; 32768 x 512 the one-shot kernel. Output and saved statistics vs fp32."""
+    from kubeflow_rm_amd import ops
+    x = (_rand(rows, H, seed=41, scale=2.0).float() + 0.5).to(torch.bfloat16)
+    w, b = _rand(H, seed=42), _rand(H, seed=43)
+    xf = x.float()
+    if rms:
+        y = ops.rms_norm(x, w, 1e-6)
+        ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * w.float()
+        assert (y.float() - ref).abs().max().item() < 3e-2
+        return
+    y, mean, rstd = ops.layer_norm_fwd(x, w, b, save_stats=True)
+    ref = torch.nn.functional.layer_norm(xf, (H,), w.float(), b.float(), 1e-5)
+    assert (y.float() - ref).abs().max().item() < 5e-2
+    assert torch.allclose(mean.float().view(-1), xf.mean(-1), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(rstd.float().view(-1), torch.rsqrt(xf.var(-1, unbiased=False) + 1e-5), atol=1e-3, rtol=1e-3)
+
+
 @pytest.mark.parametrize("rows,H", [(64, 4096), (5, 777), (41, 3072), (9, 6144), (26, 768)])
 def test_rmsnorm(rows, H):
     from kubeflow_rm_amd.ops import rms_norm

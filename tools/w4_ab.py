@@ -98,25 +98,29 @@ def main():
         libs[n] = L
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev).cuda_stream
-    for s in [int(x) for x in a.sizes.split(",") if x]:
-        A = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
-        B = (torch.rand(s, s, device=dev) * 2 - 1).to(torch.bfloat16)
+    for spec in [x for x in a.sizes.split(",") if x]:
+        # s (s^3) or MxNxK
+        M, N, K = (int(v) for v in spec.split("x")) if "x" in spec else (int(spec),) * 3
+        s = spec
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        B = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
         ref = ops.gemm_nt(A, B)
         C = torch.empty_like(ref)
         same = {}
         for n, L in libs.items():
-            assert L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st) == 0
+            assert L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, st) == 0
             torch.cuda.synchronize()
             same[n] = bool(torch.equal(C, ref))
             C.zero_()
-            assert L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, a.po_grid, st) == 0
+            assert L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, a.po_grid, st) == 0
             torch.cuda.synchronize()
             same[n + "_po"] = bool(torch.equal(C, ref))
-        iters = max(5, int(3e13 / (2 * s ** 3)))
+        flop = 2.0 * M * N * K
+        iters = max(5, int(3e13 / flop))
         fns = {"prod": lambda: ops.gemm_nt(A, B, out=C), "torch": lambda: torch.matmul(A, B.t())}
         for n, L in libs.items():
-            fns[n] = (lambda L=L: L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, st))
-            fns[n + "_po"] = (lambda L=L: L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), s, s, s, a.po_grid, st))
+            fns[n] = (lambda L=L: L.w4ab_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, st))
+            fns[n + "_po"] = (lambda L=L: L.w4ab_po(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, a.po_grid, st))
         t_end = time.perf_counter() + 1.0
         while time.perf_counter() < t_end:
             fns["prod"]()
@@ -128,7 +132,7 @@ def main():
                 for _ in range(iters):
                     fn()
                 torch.cuda.synchronize()
-                tf[k].append(2 * s ** 3 * iters / (time.perf_counter() - t0) / 1e12)
+                tf[k].append(flop * iters / (time.perf_counter() - t0) / 1e12)
         print(json.dumps({"size": s, "bitwise_equal_to_prod": same,
                           "median_tf": {k: round(statistics.median(v), 1) for k, v in tf.items()},
                           "best_tf": {k: round(max(v), 1) for k, v in tf.items()}}), flush=True)
