@@ -10,7 +10,6 @@
 //    partial-sum kernel + a finalize kernel (deterministic, no float atomics).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include "kfamd_kernels.h"
 #include "wave_ops.h"
 
@@ -116,12 +115,14 @@ __global__ __launch_bounds__(256) void norm_fwd_wave(const __bf16* __restrict__ 
   }
 }
 
-// Streaming forward (hidden = 512 * VPL, VPL <= 8): a grid of resident waves, each sweeping rows
-// wave, wave + nw, ... with the NEXT row's loads issued before this row's statistics, so every wave
-// always has a row in flight (no generation-by-generation load / compute / store phases, no tail of
-// late rows). gamma / beta sit in LDS (one copy per workgroup): their reads wait on lgkmcnt, so no
-// vmcnt wait for them also waits for the prefetched row.
-template <int VPL, bool RMS>
+// Streaming forward (hidden = 512 * VPL): a grid of resident waves, each sweeping rows wave,
+// wave + nw, ... with the NEXT row in flight while this one is reduced and stored (no
+// generation-by-generation load / compute / store phases, no tail of late rows). VPL <= 8 double-
+// buffers the row (the next row's loads go out before this row's statistics); ROLL (VPL 16, where a
+// second buffer does not fit) reloads each 16-B piece for the next row right after its output is
+// stored. gamma / beta sit in LDS (one copy per workgroup): their reads wait on lgkmcnt, so no vmcnt
+// wait for them also waits for the prefetched row.
+template <int VPL, bool RMS, bool ROLL = false>
 __global__ __launch_bounds__(256) void norm_fwd_stream(const __bf16* __restrict__ x,
                                                       const __bf16* __restrict__ gamma,
                                                       const __bf16* __restrict__ beta,
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(256) void norm_fwd_stream(const __bf16* __restrict_
 #pragma unroll
     for (int j = 0; j < VPL; ++j) asm volatile("" : "+v"(v[j]));
   };
-  auto finish = [&](bf16x8 (&v)[VPL], int r) __attribute__((always_inline)) {
+  auto finish = [&](bf16x8 (&v)[VPL], int r, int rnext) __attribute__((always_inline)) {
     opaque(v);
     float mean = 0.f;
     if (!RMS) {
@@ -189,20 +190,33 @@ __global__ __launch_bounds__(256) void norm_fwd_stream(const __bf16* __restrict_
         o[e] = (__bf16)t;
       }
       __builtin_nontemporal_store(o, &yr[j * 64 + lane]);
+      if (ROLL && rnext >= 0)
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(x + (long long)rnext * H) + j * 64 + lane);
     }
   };
-  bf16x8 va[VPL], vb[VPL];
-  load(va, row);
-  while (true) {
-    const int r1 = row + nw;
-    if (r1 < rows) load(vb, r1);
-    finish(va, row);
-    if (r1 >= rows) break;
-    const int r2 = r1 + nw;
-    if (r2 < rows) load(va, r2);
-    finish(vb, r1);
-    if (r2 >= rows) break;
-    row = r2;
+  if constexpr (ROLL) {
+    bf16x8 va[VPL];
+    load(va, row);
+    while (true) {
+      const int rn = row + nw;
+      finish(va, row, rn < rows ? rn : -1);
+      if (rn >= rows) break;
+      row = rn;
+    }
+  } else {
+    bf16x8 va[VPL], vb[VPL];
+    load(va, row);
+    while (true) {
+      const int r1 = row + nw;
+      if (r1 < rows) load(vb, r1);
+      finish(va, row, -1);
+      if (r1 >= rows) break;
+      const int r2 = r1 + nw;
+      if (r2 < rows) load(va, r2);
+      finish(vb, r1, -1);
+      if (r2 >= rows) break;
+      row = r2;
+    }
   }
 }
 
@@ -469,11 +483,15 @@ long long resident_rows() {
   return n;
 }
 
-// Forward launch policy (profiles/r5j_ln_ab, one box, kbench): the one-shot wave-per-row kernel,
-// except when its grid would take between one and two generations of resident waves: there the
-// second generation's load / compute / store phases do not overlap the first's, and the streaming
-// kernel (resident waves, next row prefetched) is faster: 8192 x 4096 24.1 -> 22.1 us (6.06 TB/s).
-// At one generation or at four (16384 x 4096: 46.3 vs 47.4 us) the one-shot kernel wins.
+// Forward launch policy (profiles/r5_ln, kbench A/B runs on one box): the one-shot wave-per-row
+// kernel, except when its grid would take between one and two generations of resident waves (of the
+// plain kernel: the gamma / beta prefetch variant holds half as many): there
+// the second generation's load / compute / store phases do not overlap the first's, and the
+// streaming kernel (resident waves, next row in flight) is faster: 8192 x 4096 24.1 -> 22.1 us
+// (6.06 TB/s). At one generation (8192 x 2048: equal) or four (16384 x 4096: 46.3 vs 47.4 us) the
+// one-shot kernel stays. Hidden 8192 streams with the rolling reload up to two generations
+// (4096 x 8192 26.6 -> 24.7 us, 8192 x 8192 48.3-49.3 -> 47.7 us) and is 2.5-6 % slower beyond, where
+// the one-shot kernel with gamma / beta prefetched runs (32768 x 8192: 178.8 us, 6.0 TB/s).
 template <bool RMS>
 int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float* mean, float* rstd,
              int rows, int hidden, float eps, void* stream) {
@@ -490,8 +508,13 @@ int norm_fwd(const void* x, const void* gamma, const void* beta, void* y, float*
     switch (vpl) {
 #define KFAMD_NORM_FWD_CASE(V)                                                                                   \
   case V:                                                                                                      \
-    if (V <= 8 && rows > resident_rows<norm_fwd_wave<V, RMS, 8, V == 16>>() &&                              \
-        rows <= 2 * resident_rows<norm_fwd_wave<V, RMS, 8, V == 16>>()) {                                       \
+    if (V == 16 && rows <= 2 * resident_rows<norm_fwd_wave<V, RMS>>()) {                        \
+      const long long waves = resident_rows<norm_fwd_stream<16, RMS, true>>();                                  \
+      const long long rpw = (rows + waves - 1) / waves;                                                        \
+      hipLaunchKernelGGL((norm_fwd_stream<16, RMS, true>), dim3((int)((rows + 4 * rpw - 1) / (4 * rpw))),     \
+                         block, 0, s, xp, gp, bp, yp, mean, rstd, rows, eps);                                  \
+    } else if (V <= 8 && rows > resident_rows<norm_fwd_wave<V, RMS>>() &&                       \
+        rows <= 2 * resident_rows<norm_fwd_wave<V, RMS>>()) {                                       \
       const long long waves = resident_rows<norm_fwd_stream<V <= 8 ? V : 8, RMS>>();                             \
       const long long rpw = (rows + waves - 1) / waves; /* rows per wave, the same for every wave */          \
       hipLaunchKernelGGL((norm_fwd_stream<V <= 8 ? V : 8, RMS>), dim3((int)((rows + 4 * rpw - 1) / (4 * rpw))), \

@@ -147,12 +147,14 @@ def test_layernorm_fwd_bwd(rows, H):
 
 
 @pytest.mark.parametrize("rows,H,rms", [(6001, 4096, False), (8192, 4096, False), (12289, 1024, False),
-                                        (6001, 4096, True), (8192, 8192, False), (32768, 512, False)])
+                                        (6001, 4096, True), (8192, 8192, False), (37, 8192, False),
+                                        (4099, 8192, True), (20000, 8192, False), (32768, 512, False)])
 def test_norm_forward_launch_paths(rows, H, rms):
     """The forward's launch policy (layernorm_bf16.hip norm_fwd): 1-2 generations of resident waves
     take the streaming kernel (resident waves, next row prefetched, gamma/beta in LDS) — 6001 / 8192
-    rows at hidden 4096, 12289 at 1024, odd counts leave waves with one row fewer; hidden 8192 takes
-    the gamma/beta-prefetch kernel; 32768 x 512 the one-shot kernel. Output and saved statistics vs fp32."""
+    rows at hidden 4096, 12289 at 1024, odd counts leave waves with one row fewer; hidden 8192 up to
+    two generations the rolling-reload stream (37, 4099, 8192 rows), beyond it the gamma/beta-prefetch
+    kernel (20000); 32768 x 512 the one-shot kernel. Output and saved statistics vs fp32."""
     from kubeflow_rm_amd import ops
     x = (_rand(rows, H, seed=41, scale=2.0).float() + 0.5).to(torch.bfloat16)
     w, b = _rand(H, seed=42), _rand(H, seed=43)

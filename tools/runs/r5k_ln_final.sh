@@ -14,3 +14,5 @@ cut -c1-260 $OUT/kbench_ln.jsonl
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o ln -- python3 $R/tools/kbench.py --sizes "" --ln 8192x4096,8192x8192,32768x8192 --rounds 2 > $OUT/prof.log 2>&1 || exit $?
 grep -i "norm_fwd\|layer_norm_kernel\|ln_bwd" $OUT/prof/ln_kernel_stats.csv | cut -c1-200
+cd $R && timeout -k 10 300 python -u tools/train_bench.py --model gpt-1b --batch 4 --seq 2048 --steps 10 --rounds 3 --out $OUT/train.jsonl > $OUT/train.log 2>&1 || exit $?
+cat $OUT/train.jsonl
