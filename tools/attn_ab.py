@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Flash-attention build A/B: the kernel library re-linked with kernels/attention_bf16.hip compiled
+under other flags / -D knobs, one library per variant (kubeflow_rm_amd/lib/attnab/).
+
+  python tools/attn_ab.py --build [--variants a,b]   # host: compile + link every variant
+  KFAMD_KERNEL_LIB=kubeflow_rm_amd/lib/attnab/libkfamd_kernels_<v>.so python tools/attn_bench.py ...
+
+The GPU side is the ordinary tooling with ``KFAMD_KERNEL_LIB`` pointing at a variant (ops/_lib.py), so
+a variant runs the same numerics tests and the same interleaved bench as production
+(tools/runs/r5n_attn_ab.sh).
+"""
+from __future__ import annotations
+
+import argparse
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+OUT = ROOT / "kubeflow_rm_amd" / "lib" / "attnab"
+
+VARIANTS = {
+    "base": [],
+    # MFMA results in VGPRs unless the register budget forces AGPRs (the default picks the AGPR form
+    # and shuttles S / dP through v_accvgpr_read / write: 972 moves per backward iteration at D = 128)
+    "vgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
+def build(names):
+    from kubeflow_rm_amd import _build as B
+    B.build_kernels()
+    # the objects of the current sources (build/kernels also keeps objects of retired ones)
+    srcs = sorted(B.KERNEL_DIR.glob("*.hip")) + sorted((B.KERNEL_DIR / "tu").glob("*.hip"))
+    others = [B.BUILD_DIR / "kernels" / (s.stem + ".o") for s in srcs if s.stem != "attention_bf16"]
+    OUT.mkdir(parents=True, exist_ok=True)
+    for n in names:
+        obj = OUT / f"attention_bf16_{n}.o"
+        subprocess.run([B.HIPCC, *B.HIP_FLAGS, *VARIANTS[n], "-I", str(B.KERNEL_DIR), "-c",
+                        str(B.KERNEL_DIR / "attention_bf16.hip"), "-o", str(obj)], check=True)
+        lib = OUT / f"libkfamd_kernels_{n}.so"
+        subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(lib), str(obj),
+                        *map(str, others)], check=True)
+        B.check_kernel_library(lib)
+        print("built", lib.relative_to(ROOT), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    a = ap.parse_args()
+    names = [v for v in a.variants.split(",") if v]
+    if a.build:
+        build(names)
+
+
+if __name__ == "__main__":
+    main()
