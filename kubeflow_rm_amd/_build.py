@@ -71,6 +71,13 @@ def build_diag_kernels() -> Path:
     return DIAG_LIB
 
 
+# per-translation-unit compiler flags. attention_bf16.hip: MFMA results in VGPRs unless the budget
+# forces AGPRs — the default AGPR form shuttled S / dP through 972 v_accvgpr moves per backward
+# iteration at D = 128 (329 with this); gpt-1b backward 665 -> 636 us, the forward ~1 % faster, the
+# D = 64 backward level (profiles/r5n_attn_ab, tools/attn_ab.py)
+TU_FLAGS = {"attention_bf16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     """Compile kernels/*.hip and kernels/tu/*.hip (one template variant per translation unit, so the
     slow ones build in parallel) for gfx950 and link libkfamd_kernels.so (incremental)."""
@@ -89,8 +96,10 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     def compile_one(src: Path) -> Path:
         obj = obj_dir / (src.stem + ".o")
         info = src.name == "kfamd_info.hip"
-        if force or not _newer(obj, [src, *headers]) or (info and hash_changed):
+        deps = [src, *headers, *([Path(__file__)] if src.name in TU_FLAGS else [])]
+        if force or not _newer(obj, deps) or (info and hash_changed):
             extra = [f'-DKFAMD_SRC_HASH="{src_hash}"'] if info else []
+            extra += TU_FLAGS.get(src.name, [])
             _run([HIPCC, *HIP_FLAGS, *extra, "-I", str(KERNEL_DIR), "-c", str(src), "-o", str(obj)])
             check_object_kernels(src, obj)
         return obj

@@ -20,12 +20,18 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 OUT = ROOT / "kubeflow_rm_amd" / "lib" / "attnab"
 
-VARIANTS = {
-    "base": [],
-    # MFMA results in VGPRs unless the register budget forces AGPRs (the default picks the AGPR form
-    # and shuttles S / dP through v_accvgpr_read / write: 972 moves per backward iteration at D = 128)
-    "vgprform": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-}
+
+def _variants():
+    from kubeflow_rm_amd import _build as B
+    prod = B.TU_FLAGS.get("attention_bf16.hip", [])
+    return {
+        "prod": prod,  # the production flags (VGPR-form MFMA results)
+        # the compiler's default AGPR form: S / dP shuttled through v_accvgpr moves
+        "agprform": [],
+    }
+
+
+VARIANTS = _variants()
 
 
 def build(names):
