@@ -124,6 +124,21 @@ __device__ __forceinline__ bf16x8 lds_row(const char* smem, int byte_off) {
 
 __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_cast<const u32x4*>(p); }
 
+// KFATT_BUF: row-guarded loads and the dQ atomics as raw buffer operations over one (b, h) slice
+// whose range ends at row T: a row past T reads as zero / is dropped by the address unit, so the
+// inner loops carry no per-row branches (a divergent `if (row < T)` around each load / atomic split
+// the loops into ~30 basic blocks and cost the scheduler and the register allocator). The host
+// requires every slice's extent below 2^31 bytes (32-bit buffer offsets).
+#ifndef KFATT_BUF
+#define KFATT_BUF 1
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 // The A operand of a product whose k index is an accumulator's row (the permuted order of
 // §3): element j of lane half hh is row kbase + 8 * (j >> 2) + 4 * hh + (j & 3) of the operand's
 // k dimension, column `col` (this lane's row of the A operand). Read as two tr reads of 4 rows.
@@ -182,19 +197,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
 
   u32x4 kreg[NCH], vreg[NCH];
+  const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
   auto stage_load = [&](int tile) {
     const int k0 = tile * FK;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
       const int key = k0 + row;
-      u32x4 xk = {0u, 0u, 0u, 0u}, xv = {0u, 0u, 0u, 0u};
-      if (key < T) {
-        xk = gload16(kb + key * kt + ch * 8);
-        xv = gload16(vb + key * vt + ch * 8);
+      if constexpr (KFATT_BUF) {
+        kreg[i] = bload16(rk, 2 * (key * (int)kt + ch * 8));
+        vreg[i] = bload16(rv, 2 * (key * (int)vt + ch * 8));
+      } else {
+        u32x4 xk = {0u, 0u, 0u, 0u}, xv = {0u, 0u, 0u, 0u};
+        if (key < T) {
+          xk = gload16(kb + key * kt + ch * 8);
+          xv = gload16(vb + key * vt + ch * 8);
+        }
+        kreg[i] = xk;
+        vreg[i] = xv;
       }
-      kreg[i] = xk;
-      vreg[i] = xv;
     }
   };
   auto stage_write = [&](int buf) {
@@ -398,6 +419,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2], dot = a.s[TDO][2];
   const float* lseb = lse + ((long long)b * a.H + h) * T;
   const float* deltab = delta + ((long long)b * a.H + h) * T;
+  const auto rdq = slice_rsrc(dq_acc + b * dq_sb + h * dq_sh, 4LL * T * dq_st);
 
   // K image for the dQ product (tr reads) and the S product (row reads); V rows in registers
 #pragma unroll
@@ -420,18 +442,24 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
 
   u32x4 qreg[NQC], oreg[NQC];
   float rreg = 0.f;
+  const auto rq = slice_rsrc(qb, 2LL * T * qt), rdo = slice_rsrc(dob, 2LL * T * dot);
   auto stage_load = [&](int tile) {
     const int q0 = qstart + tile * BQ;
 #pragma unroll
     for (int i = 0; i < NQC; ++i) {
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
-      u32x4 xq = {0u, 0u, 0u, 0u}, xo = {0u, 0u, 0u, 0u};
-      if (q0 + row < T) {
-        xq = gload16(qb + (q0 + row) * qt + ch * 8);
-        xo = gload16(dob + (q0 + row) * dot + ch * 8);
+      if constexpr (KFATT_BUF) {
+        qreg[i] = bload16(rq, 2 * ((q0 + row) * (int)qt + ch * 8));
+        oreg[i] = bload16(rdo, 2 * ((q0 + row) * (int)dot + ch * 8));
+      } else {
+        u32x4 xq = {0u, 0u, 0u, 0u}, xo = {0u, 0u, 0u, 0u};
+        if (q0 + row < T) {
+          xq = gload16(qb + (q0 + row) * qt + ch * 8);
+          xo = gload16(dob + (q0 + row) * dot + ch * 8);
+        }
+        qreg[i] = xq;
+        oreg[i] = xo;
       }
-      qreg[i] = xq;
-      oreg[i] = xo;
     }
     if (tid < 2 * BQ) {
       const int row = tid & (BQ - 1);
@@ -564,11 +592,19 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
         }
         // rows q0 + 32 j + (e & 3) + 8 (e >> 2) + 4 hh, column d = 32 dqn + r: f32 atomics, each wave
         // instruction two 128-B row segments
-        float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
+        if constexpr (KFATT_BUF) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int qr = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (qr < T) __hip_atomic_fetch_add(dqb + qr * dq_st, dqacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int e = 0; e < 16; ++e) {
+            const int qr = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dqacc[e], rdq, 4 * (qr * (int)dq_st + 32 * dqn + r), 0, 0);
+          }
+        } else {
+          float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int qr = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if (qr < T) __hip_atomic_fetch_add(dqb + qr * dq_st, dqacc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
     }
@@ -632,6 +668,11 @@ bool fill_shape(AttnShape& s, int B, int H, int T, int D, float scale, const lon
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// a (b, h) slice of T rows read through a buffer descriptor (KFATT_BUF): 32-bit byte offsets
+bool slice_ok(int T, long long row_stride, int elem_bytes) {
+  return row_stride > 0 && (long long)T * row_stride * elem_bytes < (1ll << 31);
+}
+
 }  // namespace
 
 extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, void* o, void* lse, int B, int H, int T,
@@ -642,6 +683,7 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
   if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return KFAMD_EALIGN;
   const long long nwg = (long long)((T + FQ - 1) / FQ) * H * B;
   if (nwg >= (1ll << 31)) return KFAMD_EINVAL;
+  if (!slice_ok(T, s.s[TK][2], 2) || !slice_ok(T, s.s[TV][2], 2)) return KFAMD_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(256), 0, st, static_cast<const __bf16*>(q),
@@ -676,6 +718,7 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
   float* dq_acc = static_cast<float*>(workspace);
   float* delta = dq_acc + (long long)B * T * H * D;
   const long long dq_st = (long long)H * D, dq_sh = D, dq_sb = (long long)T * H * D;
+  if (!slice_ok(T, s.s[TQ][2], 2) || !slice_ok(T, s.s[TDO][2], 2) || !slice_ok(T, dq_st, 4)) return KFAMD_EINVAL;
   hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * T * H * D * 4, st);
   if (e != hipSuccess) return static_cast<int>(e);
   const long long rows = (long long)B * H * T;

@@ -28,6 +28,7 @@ def _variants():
         "prod": prod,  # the production flags (VGPR-form MFMA results)
         # the compiler's default AGPR form: S / dP shuttled through v_accvgpr moves
         "agprform": [],
+        "guarded": [*prod, "-DKFATT_BUF=0"],  # per-row `if (row < T)` loads and atomics
     }
 
 
