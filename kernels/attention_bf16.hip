@@ -132,11 +132,53 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_BUF
 #define KFATT_BUF 1
 #endif
+#ifndef KFATT_ABL
+#define KFATT_ABL 0  // timing ablations (tools/attn_ab.py builds): 1 = dQ atomics dropped
+#endif
+// Backward schedule (profiles/r5q_attn_split, tools/attn_ab.py variants, one box, 2 rounds each):
+//   gpt-1b 4x16x2048x128 bwd: register-staged + dQ atomics 570 us; + LDS-DMA staging 557-568; the
+//   atomics dropped (timing only) 525-545; the atomic-free dQ kernel 482 (-15 %); D = 64
+//   (16x12x2048): 827-832 -> 557-559 (-33 %: at D = 64 the fp32 atomics are a third of the pass);
+//   1x16x4096x128: 489-495 -> 417-419. The forward with LDS-DMA K / V was 2-7 % slower: kept off.
+#ifndef KFATT_DQ_SPLIT
+#define KFATT_DQ_SPLIT 1  // dQ by the atomic-free attn_bwd_dq_split kernel (recomputes S and dP)
+#endif
+#ifndef KFATT_DMA
+#define KFATT_DMA 1  // backward Q / dO tiles by LDS-DMA (attn_bwd stage_dma)
+#endif
+#ifndef KFATT_FWD_DMA
+#define KFATT_FWD_DMA 0  // forward K / V tiles by LDS-DMA (attn_fwd stage_dma)
+#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+// LDS-DMA as inline asm (KFATT_DMA): the compiler, seeing a buffer_load ... lds builtin, waits
+// vmcnt(0) before later LDS reads it cannot prove disjoint (it did, mid-tile, before the dV / dK tr
+// reads: the next tile's DMA latency exposed). The kernel's own waits cover the pieces instead.
+// The descriptor is an SGPR quad (base, base_hi | stride 0, records, gfx9 raw-buffer word 3); M0 holds
+// the wave's 1 KiB LDS destination (lane L writes +16 L); s_nop 1 covers the M0 -> LDS-DMA hazard.
+// (No compiler-generated code in this file uses M0: LDS instructions do not on gfx9+, and every
+// LDS-DMA here is this asm, so M0 is not listed as clobbered — hipcc treats it as reserved.)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 slice_desc(const void* base, long long bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  return i32x4{__builtin_amdgcn_readfirstlane((int)(unsigned)a), __builtin_amdgcn_readfirstlane((int)((a >> 32) & 0xffff)),
+               (int)bytes, 0x00020000};
+}
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void dma16(const i32x4& desc, unsigned lds, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc) : "memory");
+}
+__device__ __forceinline__ void dma4(const i32x4& desc, unsigned lds, int voff) {  // lane L -> +4 L
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dword %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc) : "memory");
 }
 
 // The A operand of a product whose k index is an accumulator's row (the permuted order of
@@ -196,12 +238,30 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
 
   const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
 
-  u32x4 kreg[NCH], vreg[NCH];
+  constexpr bool kDma = KFATT_FWD_DMA && KFATT_BUF;
+  u32x4 kreg[kDma ? 1 : NCH], vreg[kDma ? 1 : NCH];
   const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
+  const i32x4 dk_desc = slice_desc(kb, 2LL * T * kt), dv_desc = slice_desc(vb, 2LL * T * vt);
+  // KFATT_DMA: K / V tiles by LDS-DMA (as the backward's stage_dma): no staging registers
+  auto stage_dma = [&](int tile, int buf) {
+    constexpr int NPC = TILE / 1024 / 4;
+    const int k0 = tile * FK;
+    char* kimg = smem + buf * 2 * TILE;
+    char* vimg = kimg + TILE;
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int pc = w * NPC + i;
+      const int byte = pc * 1024 + lane * 16;
+      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
+      const int ch = sc ^ swz<D>(row, 0);
+      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * ((k0 + row) * (int)kt + ch * 8));
+      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * ((k0 + row) * (int)vt + ch * 8));
+    }
+  };
   auto stage_load = [&](int tile) {
     const int k0 = tile * FK;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
+    for (int i = 0; i < (kDma ? 0 : NCH); ++i) {
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
       const int key = k0 + row;
       if constexpr (KFATT_BUF) {
@@ -222,7 +282,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
     char* kimg = smem + buf * 2 * TILE;
     char* vimg = kimg + TILE;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
+    for (int i = 0; i < (kDma ? 0 : NCH); ++i) {
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
       const int off = img_off<D>(row, ch);
       *reinterpret_cast<u32x4*>(kimg + off) = kreg[i];
@@ -236,6 +296,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
 #pragma unroll
   for (int n = 0; n < ND; ++n) oacc[n] = (f32x16){};
 
+  if constexpr (kDma) {
+    stage_dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   stage_load(0);
   stage_write(0);
   __syncthreads();
@@ -243,7 +307,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   for (int j = 0; j < ntiles; ++j) {
     const int k0 = j * FK;
     const bool more = j + 1 < ntiles;
-    if (more) stage_load(j + 1);
+    if (more) {
+      if constexpr (kDma) stage_dma(j + 1, (j + 1) & 1);
+      stage_load(j + 1);
+    }
     const char* kimg = smem + (j & 1) * 2 * TILE;
     const char* vimg = kimg + TILE;
     // a wave whose 32 rows all precede the tile's first key has nothing to do (causal)
@@ -314,7 +381,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
         }
       }
     }
-    if (more) stage_write((j + 1) & 1);
+    if (more) {
+      if constexpr (kDma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces
+      stage_write((j + 1) & 1);
+    }
     __syncthreads();
   }
 
@@ -362,6 +432,145 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
   if (row < nrows && part == 0) delta[row] = s;
 }
 
+// ------------------------------------------------------------------------------------------------
+// backward dQ without atomics (KFATT_DQ_SPLIT): the forward's structure with the log-sum-exp known.
+// One workgroup = 4 waves = 128 query rows; 64-key K / V tiles by LDS-DMA into a double-buffered
+// image; per tile S^T = K Q^T and dP^T = V dO^T (keys on registers, the lane's query on the column),
+// P^T = exp(scale S - lse), dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T with dS^T straight from the
+// registers as the B operand (the permuted k order, as P^T feeds PV in the forward). dQ is written
+// once, scaled, in bf16: no fp32 workspace, no atomics, no conversion pass. Costs the S and dP
+// products a second time (the dK / dV kernel computes them too).
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                            const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                            const float* __restrict__ lse, const float* __restrict__ delta,
+                                                            __bf16* __restrict__ dq, AttnShape a) {
+  constexpr int KS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int CH = D / 8;
+  constexpr int TILE = FK * D * 2;             // one K (or V) tile image
+  constexpr int NPC = TILE / 1024 / 4;         // LDS-DMA pieces (1 KiB) per wave per image
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K, V]
+
+  const int T = a.T;
+  const int nq = (T + FQ - 1) / FQ;
+  const int nwg = nq * a.H * a.B;
+  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  const int qblk = nq - 1 - (lid % nq);  // heaviest first within each head
+  const int bh = lid / nq, h = bh % a.H, b = bh / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
+
+  const __bf16* qb = q + base_off(a, TQ, b, h);
+  const __bf16* kb = k + base_off(a, TK, b, h);
+  const __bf16* vb = v + base_off(a, TV, b, h);
+  const __bf16* dob = dout + base_off(a, TDO, b, h);
+  const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2], dot = a.s[TDO][2];
+  const auto rq = slice_rsrc(qb, 2LL * T * qt), rdo = slice_rsrc(dob, 2LL * T * dot);
+  const i32x4 dk_desc = slice_desc(kb, 2LL * T * kt), dv_desc = slice_desc(vb, 2LL * T * vt);
+
+  // this lane's query: Q and dO rows as the B operands, lse and delta (rows past T: zeros)
+  bf16x8 qf[KS], dof[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    qf[kk] = __builtin_bit_cast(bf16x8, bload16(rq, 2 * (qrow * (int)qt + kk * 16 + 8 * hh)));
+    dof[kk] = __builtin_bit_cast(bf16x8, bload16(rdo, 2 * (qrow * (int)dot + kk * 16 + 8 * hh)));
+  }
+  const long long rowbase = ((long long)b * a.H + h) * T;
+  const float lse_q = qrow < T ? lse[rowbase + qrow] * kLog2e : 0.f;
+  const float del_q = qrow < T ? delta[rowbase + qrow] : 0.f;
+
+  const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
+  // K / V tile `tile` -> image buffer `buf`, each lane fetching the chunk the swizzle puts at its slot
+  auto stage_dma = [&](int tile, int buf) {
+    const int k0 = tile * FK;
+    char* kimg = smem + buf * 2 * TILE;
+    char* vimg = kimg + TILE;
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int pc = w * NPC + i;
+      const int byte = pc * 1024 + lane * 16;
+      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
+      const int ch = sc ^ swz<D>(row, 0);
+      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * ((k0 + row) * (int)kt + ch * 8));
+      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * ((k0 + row) * (int)vt + ch * 8));
+    }
+  };
+
+  const float c = a.scale * kLog2e;
+  f32x16 dqacc[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) dqacc[n] = (f32x16){};
+
+  if (ntiles > 0) stage_dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int j = 0; j < ntiles; ++j) {
+    const int k0 = j * FK;
+    if (j + 1 < ntiles) stage_dma(j + 1, (j + 1) & 1);  // buffer (j+1)&1 was last read before the barrier
+    const char* kimg = smem + (j & 1) * 2 * TILE;
+    const char* vimg = kimg + TILE;
+    if (!(CAUSAL && k0 > qw + 31)) {
+      f32x16 sacc[2] = {(f32x16){}, (f32x16){}}, dpacc[2] = {(f32x16){}, (f32x16){}};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          sacc[t] = mfma32(lds_row(kimg, img_off<D>(32 * t + r, 2 * kk + hh)), qf[kk], sacc[t]);
+          dpacc[t] = mfma32(lds_row(vimg, img_off<D>(32 * t + r, 2 * kk + hh)), dof[kk], dpacc[t]);
+        }
+      }
+      const bool need_mask = (CAUSAL && k0 + FK - 1 > qw) || k0 + FK > T;
+      uint32_t sf[2][2][4];  // [t][s][pair]: dS^T as the B operand of K^T dS^T
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) {
+          float p0 = fast_exp2(fmaf(sacc[t][e], c, -lse_q)), p1 = fast_exp2(fmaf(sacc[t][e + 1], c, -lse_q));
+          if (need_mask) {
+            const int key = k0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
+            if ((CAUSAL && key > qrow) || key >= T) p0 = 0.f;
+            if ((CAUSAL && key + 1 > qrow) || key + 1 >= T) p1 = 0.f;
+          }
+          sf[t][e >> 3][(e & 7) >> 1] = pack2(p0 * (dpacc[t][e] - del_q), p1 * (dpacc[t][e + 1] - del_q));
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 kf = tr_operand<D>(kimg, 32 * t + 16 * s2, 32 * n, lane);
+            const u32x4 sw = {sf[t][s2][0], sf[t][s2][1], sf[t][s2][2], sf[t][s2][3]};
+            dqacc[n] = mfma32(kf, __builtin_bit_cast(bf16x8, sw), dqacc[n]);
+          }
+        }
+      }
+    }
+    // the next tile's pieces (the only vector-memory operations in the loop) have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
+  if (qrow < T) {
+    __bf16* dqr = dq + base_off(a, TDQ, b, h) + qrow * a.s[TDQ][2];
+    const float sc = a.scale;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const u32x2 v2 = {pack2(dqacc[n][4 * g] * sc, dqacc[n][4 * g + 1] * sc),
+                          pack2(dqacc[n][4 * g + 2] * sc, dqacc[n][4 * g + 3] * sc)};
+        *reinterpret_cast<u32x2*>(dqr + 32 * n + 8 * g + 4 * hh) = v2;
+      }
+    }
+  }
+}
+
 // dS^T image [128 keys][64 queries]: 128-B rows of sixteen 8-B slots (4 queries each), slot ^ f(row),
 // f(row) = (row & 15) ^ (((row >> 1) & 1) << 3). The accumulator's stores (16 lanes = 16 consecutive
 // keys, one slot each) cover all 32 write banks (unswizzled: one slot column, 16-way); the dQ
@@ -381,7 +590,7 @@ constexpr int BK = 128, BQ = 64, QS = BQ / 32;
 
 // D = 128 holds dK^T, dV^T (128 registers) and V (32) for the whole sweep: one wave per SIMD
 // (512-register budget, no spills); D = 64 fits two
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DQS = false>
 __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                    const float* __restrict__ lse, const float* __restrict__ delta,
@@ -440,13 +649,19 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   const int qstart = CAUSAL ? k0 : 0;
   const int ntiles = (T - qstart + BQ - 1) / BQ;
 
-  u32x4 qreg[NQC], oreg[NQC];
+  constexpr bool kDma = KFATT_DMA && KFATT_BUF;
+  u32x4 qreg[kDma ? 1 : NQC], oreg[kDma ? 1 : NQC];
   float rreg = 0.f;
   const auto rq = slice_rsrc(qb, 2LL * T * qt), rdo = slice_rsrc(dob, 2LL * T * dot);
+  // (the selector through readfirstlane: a per-lane select of the base would make the compiler wrap
+  // the load in a waterfall loop over descriptor values)
+  const auto rrow = slice_rsrc(__builtin_amdgcn_readfirstlane(w) == 0 ? lseb : deltab, 4LL * T);
+  const i32x4 dq_desc = slice_desc(qb, 2LL * T * qt), ddo_desc = slice_desc(dob, 2LL * T * dot);
+  const i32x4 drow_desc = slice_desc(__builtin_amdgcn_readfirstlane(w) == 0 ? lseb : deltab, 4LL * T);
   auto stage_load = [&](int tile) {
     const int q0 = qstart + tile * BQ;
 #pragma unroll
-    for (int i = 0; i < NQC; ++i) {
+    for (int i = 0; i < (kDma ? 0 : NQC); ++i) {
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
       if constexpr (KFATT_BUF) {
         qreg[i] = bload16(rq, 2 * ((q0 + row) * (int)qt + ch * 8));
@@ -461,23 +676,50 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
         oreg[i] = xo;
       }
     }
-    if (tid < 2 * BQ) {
+    if (!kDma && tid < 2 * BQ) {  // waves 0 / 1: the tile's lse / delta (rows past T read 0)
       const int row = tid & (BQ - 1);
-      rreg = 0.f;
-      if (q0 + row < T) rreg = tid < BQ ? lseb[q0 + row] : deltab[q0 + row];
+      if constexpr (KFATT_BUF) {
+        rreg = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rrow, 4 * (q0 + row), 0, 0));
+      } else {
+        rreg = 0.f;
+        if (q0 + row < T) rreg = tid < BQ ? lseb[q0 + row] : deltab[q0 + row];
+      }
     }
   };
   auto stage_write = [&](int buf) {
     char* qi = qtiles + buf * 2 * QT;
     char* oi = qi + QT;
+    if constexpr (!kDma) {
+#pragma unroll
+      for (int i = 0; i < NQC; ++i) {
+        const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+        const int off = img_off<D>(row, ch);
+        *reinterpret_cast<u32x4*>(qi + off) = qreg[i];
+        *reinterpret_cast<u32x4*>(oi + off) = oreg[i];
+      }
+    }
+    if (!kDma && tid < 2 * BQ) rowc[buf * 2 * BQ + tid] = rreg;
+  };
+  // KFATT_DMA: the Q / dO tiles go global -> LDS by LDS-DMA (buffer_load ... lds), no staging
+  // registers. A wave instruction fills 1 KiB of the image linearly (lane L at +16 L), so each lane
+  // fetches the chunk that the swizzle puts there: image chunk sc of row `row` holds source chunk
+  // sc ^ swz(row, 0) (the swizzle is an XOR per row). Rows past T land as zeros (buffer range).
+  auto stage_dma = [&](int tile, int buf) {
+    const int q0 = qstart + tile * BQ;
+    char* qi = qtiles + buf * 2 * QT;
+    char* oi = qi + QT;
 #pragma unroll
     for (int i = 0; i < NQC; ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
-      const int off = img_off<D>(row, ch);
-      *reinterpret_cast<u32x4*>(qi + off) = qreg[i];
-      *reinterpret_cast<u32x4*>(oi + off) = oreg[i];
+      const int pc = w * NQC + i;                         // 1 KiB piece of the image
+      const int byte = pc * 1024 + lane * 16;
+      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
+      const int ch = sc ^ swz<D>(row, 0);
+      dma16(dq_desc, lds_addr(qi + pc * 1024), 2 * ((q0 + row) * (int)qt + ch * 8));
+      dma16(ddo_desc, lds_addr(oi + pc * 1024), 2 * ((q0 + row) * (int)dot + ch * 8));
     }
-    if (tid < 2 * BQ) rowc[buf * 2 * BQ + tid] = rreg;
+    // waves 0 / 1: the tile's 64 lse / delta values (no register staging: a pending load into a
+    // register made the compiler wait vmcnt(0) before the tile's first MFMA)
+    if (w < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + w * BQ)), 4 * (q0 + lane));
   };
 
   const float c = a.scale * kLog2e;
@@ -490,7 +732,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   }
 
   if (ntiles > 0) {
+    if constexpr (kDma) stage_dma(0, 0);
     stage_load(0);
+    if constexpr (kDma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stage_write(0);
   }
   __syncthreads();
@@ -498,7 +742,10 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   for (int it = 0; it < ntiles; ++it) {
     const int q0 = qstart + it * BQ;
     const bool more = it + 1 < ntiles;
-    if (more) stage_load(it + 1);
+    if (more) {
+      if constexpr (kDma) stage_dma(it + 1, (it + 1) & 1);
+      stage_load(it + 1);
+    }
     const char* qi = qtiles + (it & 1) * 2 * QT;
     const char* oi = qi + QT;
     const float* lse_s = rowc + (it & 1) * 2 * BQ;
@@ -545,10 +792,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
           sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
         }
         // dS^T image [key][q]: registers 4g..4g+3 are queries 32 j + 8 g + 4 hh .. +3 of this lane's key
+        if constexpr (!DQS) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u32x2 v2 = {sf[g >> 1][2 * (g & 1)], sf[g >> 1][2 * (g & 1) + 1]};
-          *reinterpret_cast<u32x2*>(dst + dst_off(32 * w + r, 8 * j + 2 * g + hh)) = v2;
+          for (int g = 0; g < 4; ++g) {
+            const u32x2 v2 = {sf[g >> 1][2 * (g & 1)], sf[g >> 1][2 * (g & 1) + 1]};
+            *reinterpret_cast<u32x2*>(dst + dst_off(32 * w + r, 8 * j + 2 * g + hh)) = v2;
+          }
         }
         // dV^T += dO^T . P and dK^T += Q^T . dS over this sub-tile's rows (permuted k order)
 #pragma unroll
@@ -564,17 +813,18 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
           }
         }
       }
-    } else {
+    } else if constexpr (!DQS) {
       // this wave's 32 rows of the dS^T image are zero (lane half hh clears slots 8 hh .. 8 hh + 7)
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl)
         *reinterpret_cast<u32x2*>(dst + dst_off(32 * w + r, 8 * hh + sl)) = (u32x2){0u, 0u};
     }
-    __syncthreads();
+    if constexpr (!DQS) __syncthreads();
 
     // dQ[q][d]: this wave's 32x32 output tiles (query sub-tile j, d tile n), all 128 keys: A = dS rows
     // from the [key][q] image by tr reads, B = K columns from the K image by tr reads
-    {
+    // (DQS: dQ is the atomic-free attn_bwd_dq_split kernel's)
+    if constexpr (!DQS) {
       const int g = lane >> 4, i = lane & 15, qq = i >> 2, p = i & 3;
 #pragma unroll
       for (int tt = 0; tt < DQT; ++tt) {
@@ -596,7 +846,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int qr = q0 + 32 * j + (e & 3) + 8 * (e >> 2) + 4 * hh;
-            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dqacc[e], rdq, 4 * (qr * (int)dq_st + 32 * dqn + r), 0, 0);
+            // (KFATT_ABL == 1, timing ablation only: every atomic out of range, dropped by the address unit)
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dqacc[e], rdq,
+                                                            4 * (qr * (int)dq_st + 32 * dqn + r) | (KFATT_ABL == 1 ? 0x70000000 : 0), 0, 0);
           }
         } else {
           float* dqb = dq_acc + b * dq_sb + h * dq_sh + 32 * dqn + r;
@@ -608,7 +860,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
         }
       }
     }
-    if (more) stage_write((it + 1) & 1);
+    if (more) {
+      // the next tile's LDS-DMA pieces (and the lse / delta load) were issued before this tile's
+      // DQT x 16 dQ atomics: waiting down to that many outstanding lands exactly them
+      if constexpr (kDma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQS ? 0 : DQT * 16) : "memory");
+      stage_write((it + 1) & 1);
+    }
     __syncthreads();
   }
 
@@ -697,8 +954,8 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
 }
 
 extern "C" long long kfamd_attn_bwd_workspace(int B, int H, int T, int D) {
-  // dq_acc f32 [B][T][H][D] + delta f32 [B][H][T]
-  return (long long)B * T * H * D * 4 + (long long)B * H * T * 4;
+  // delta f32 [B][H][T] (+ dq_acc f32 [B][T][H][D] in front of it when dQ goes through atomics)
+  return (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D * 4) + (long long)B * H * T * 4;
 }
 
 // strides: 8 tensors x (b, h, t): q, k, v, o, do, dq, dk, dv. workspace: kfamd_attn_bwd_workspace bytes
@@ -715,14 +972,37 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
   const long long nk = (long long)((T + BK - 1) / BK) * H * B;
   if (nk >= (1ll << 31)) return KFAMD_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  float* dq_acc = static_cast<float*>(workspace);
-  float* delta = dq_acc + (long long)B * T * H * D;
+  float* dq_acc = static_cast<float*>(workspace);  // (unused with KFATT_DQ_SPLIT)
+  float* delta = dq_acc + (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D);
   const long long dq_st = (long long)H * D, dq_sh = D, dq_sb = (long long)T * H * D;
   if (!slice_ok(T, s.s[TQ][2], 2) || !slice_ok(T, s.s[TDO][2], 2) || !slice_ok(T, dq_st, 4)) return KFAMD_EINVAL;
-  hipError_t e = hipMemsetAsync(dq_acc, 0, (size_t)B * T * H * D * 4, st);
-  if (e != hipSuccess) return static_cast<int>(e);
   const long long rows = (long long)B * H * T;
   const unsigned rblocks = (unsigned)((rows + 256 / (D / 8) - 1) / (256 / (D / 8)));
+  hipError_t e = hipSuccess;
+  if constexpr (KFATT_DQ_SPLIT) {
+    // dK / dV kernel without the dQ phase, then the atomic-free dQ kernel (no fp32 workspace)
+    const long long nq = (long long)((T + FQ - 1) / FQ) * H * B;
+    if (!slice_ok(T, s.s[TK][2], 2) || !slice_ok(T, s.s[TV][2], 2)) return KFAMD_EINVAL;
+    auto run = [&](auto delta_k, auto main_k, auto dq_k) {
+      hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
+                         static_cast<const __bf16*>(dout), delta, s);
+      hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                         static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
+                         static_cast<const float*>(lse), static_cast<const float*>(delta), dq_acc,
+                         static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s, dq_st, dq_sh, dq_sb);
+      hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                         static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
+                         static_cast<const float*>(lse), static_cast<const float*>(delta), static_cast<__bf16*>(dq), s);
+    };
+    if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true, true>, attn_bwd_dq_split<128, true>)
+                         : run(attn_bwd_delta<128>, attn_bwd<128, false, true>, attn_bwd_dq_split<128, false>);
+    else causal ? run(attn_bwd_delta<64>, attn_bwd<64, true, true>, attn_bwd_dq_split<64, true>)
+                : run(attn_bwd_delta<64>, attn_bwd<64, false, true>, attn_bwd_dq_split<64, false>);
+    e = hipGetLastError();
+    return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+  }
+  e = hipMemsetAsync(dq_acc, 0, (size_t)B * T * H * D * 4, st);
+  if (e != hipSuccess) return static_cast<int>(e);
   auto run = [&](auto delta_k, auto main_k, auto dq_k) {
     hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
                        static_cast<const __bf16*>(dout), delta, s);

@@ -25,10 +25,14 @@ def _variants():
     from kubeflow_rm_amd import _build as B
     prod = B.TU_FLAGS.get("attention_bf16.hip", [])
     return {
-        "prod": prod,  # the production flags (VGPR-form MFMA results)
+        "prod": prod,  # the production flags and knob defaults
         # the compiler's default AGPR form: S / dP shuttled through v_accvgpr moves
         "agprform": [],
-        "guarded": [*prod, "-DKFATT_BUF=0"],  # per-row `if (row < T)` loads and atomics
+        "guarded": [*prod, "-DKFATT_BUF=0", "-DKFATT_DMA=0", "-DKFATT_DQ_SPLIT=0"],  # per-row guards, atomics
+        "atomics": [*prod, "-DKFATT_DQ_SPLIT=0"],  # dQ by fp32 atomics inside the dK / dV kernel
+        "atomics_regstage": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_DMA=0"],  # ... Q / dO register-staged
+        "atomics_dropped": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_ABL=1"],  # timing only: atomics dropped
+        "fwd_dma": [*prod, "-DKFATT_FWD_DMA=1"],  # forward K / V by LDS-DMA
     }
 
 
