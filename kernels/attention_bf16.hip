@@ -146,14 +146,20 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_DMA
 #define KFATT_DMA 1  // backward Q / dO tiles by LDS-DMA (attn_bwd stage_dma)
 #endif
+#ifndef KFATT_FWD_SCHED
+#define KFATT_FWD_SCHED 0  // forward: LDS operand reads this many ahead of the MFMAs (0: compiler's schedule)
+#endif
+#ifndef KFATT_FWD_OFFS
+#define KFATT_FWD_OFFS 1  // forward: LDS read offsets precomputed per lane, buffers unrolled
+#endif
 #ifndef KFATT_FWD_DMA
 #define KFATT_FWD_DMA 0  // forward K / V tiles by LDS-DMA (attn_fwd stage_dma)
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
-__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, int byte_off, int soff = 0) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, soff, 0));
 }
 
 // LDS-DMA as inline asm (KFATT_DMA): the compiler, seeing a buffer_load ... lds builtin, waits
@@ -172,13 +178,17 @@ __device__ __forceinline__ i32x4 slice_desc(const void* base, long long bytes) {
 __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
-__device__ __forceinline__ void dma16(const i32x4& desc, unsigned lds, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc) : "memory");
+// voff: the lane's byte offset (VGPR); soff: a wave-uniform byte offset (SGPR: the tile's row offset,
+// so the per-lane part is computed once outside the loop)
+__device__ __forceinline__ void dma16(const i32x4& desc, unsigned lds, int voff, int soff = 0) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc),
+                  "s"(__builtin_amdgcn_readfirstlane(soff)) : "memory");
 }
-__device__ __forceinline__ void dma4(const i32x4& desc, unsigned lds, int voff) {  // lane L -> +4 L
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dword %1, %2, 0 offen lds"
-               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc) : "memory");
+__device__ __forceinline__ void dma4(const i32x4& desc, unsigned lds, int voff, int soff = 0) {  // lane L -> +4 L
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dword %1, %2, %3 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(desc),
+                  "s"(__builtin_amdgcn_readfirstlane(soff)) : "memory");
 }
 
 // The A operand of a product whose k index is an accumulator's row (the permuted order of
@@ -254,8 +264,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
       const int byte = pc * 1024 + lane * 16;
       const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
       const int ch = sc ^ swz<D>(row, 0);
-      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * ((k0 + row) * (int)kt + ch * 8));
-      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * ((k0 + row) * (int)vt + ch * 8));
+      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
+      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
     }
   };
   auto stage_load = [&](int tile) {
@@ -265,8 +275,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
       const int c = tid + 256 * i, row = c / CH, ch = c % CH;
       const int key = k0 + row;
       if constexpr (KFATT_BUF) {
-        kreg[i] = bload16(rk, 2 * (key * (int)kt + ch * 8));
-        vreg[i] = bload16(rv, 2 * (key * (int)vt + ch * 8));
+        // lane part in the voffset, the tile's row offset in the (scalar) soffset: no VALU per load
+        kreg[i] = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
+        vreg[i] = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
       } else {
         u32x4 xk = {0u, 0u, 0u, 0u}, xv = {0u, 0u, 0u, 0u};
         if (key < T) {
@@ -304,14 +315,32 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   stage_write(0);
   __syncthreads();
 
-  for (int j = 0; j < ntiles; ++j) {
+  // per-lane LDS offsets of every operand read, computed once (KFATT_FWD_OFFS): the row parts that
+  // vary per read (t, k-step, buffer) are compile-time and ride in the ds_read immediate, so the loop
+  // body carries no address arithmetic (it was ~80 VALU per 64-key tile, a third of the VALU stream)
+  int koff[KS], voff0[ND], voff1[ND];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) koff[kk] = img_off<D>(r, 2 * kk + hh);  // + 32 t rows: swz bits unchanged
+  {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+    const int r0 = 4 * hh + qq;  // + kbase (a multiple of 16): swz bits unchanged
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 32 * n + 16 * (g & 1) + 4 * pp;
+      voff0[n] = img_off<D>(r0, col >> 3) + 8 * (pp & 1);
+      voff1[n] = img_off<D>(r0 + 8, col >> 3) + 8 * (pp & 1);
+    }
+  }
+  // the tile loop unrolled over the two buffers: the buffer offset is compile-time too
+  auto tile_body = [&](int j, auto BUFC) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int k0 = j * FK;
     const bool more = j + 1 < ntiles;
     if (more) {
-      if constexpr (kDma) stage_dma(j + 1, (j + 1) & 1);
+      if constexpr (kDma) stage_dma(j + 1, 1 - BUF);
       stage_load(j + 1);
     }
-    const char* kimg = smem + (j & 1) * 2 * TILE;
+    const char* kimg = smem + BUF * 2 * TILE;
     const char* vimg = kimg + TILE;
     // a wave whose 32 rows all precede the tile's first key has nothing to do (causal)
     if (!(CAUSAL && k0 > qw + 31)) {
@@ -320,8 +349,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 kf = lds_row(kimg, img_off<D>(32 * t + r, 2 * kk + hh));
+          const bf16x8 kf = KFATT_FWD_OFFS ? lds_row(kimg + 32 * t * D * 2, koff[kk])
+                                           : lds_row(kimg, img_off<D>(32 * t + r, 2 * kk + hh));
           sacc[t] = mfma32(kf, qf[kk], sacc[t]);
+        }
+      }
+      if constexpr (KFATT_FWD_SCHED > 0) {
+        // software pipeline KFATT_FWD_SCHED K-row fragments ahead of the MFMAs (the default schedule
+        // reads two, waits for them, runs two MFMAs: the LDS latency exposed every 64 MFMA cycles)
+        constexpr int NM = 2 * KS, PF = KFATT_FWD_SCHED < NM ? KFATT_FWD_SCHED : NM;
+        __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+          if (m + PF < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
       }
       // masks: causal (key > query) on tiles that reach the wave's diagonal, key >= T on the tail
@@ -374,18 +415,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const bf16x8 vf = tr_operand<D>(vimg, 32 * t + 16 * s, 32 * n, lane);
+            const bf16x8 vf = KFATT_FWD_OFFS ? join(tr_read(vimg + (32 * t + 16 * s) * D * 2, voff0[n]),
+                                                    tr_read(vimg + (32 * t + 16 * s) * D * 2, voff1[n]))
+                                               : tr_operand<D>(vimg, 32 * t + 16 * s, 32 * n, lane);
             const u32x4 pw = {pf[t][s][0], pf[t][s][1], pf[t][s][2], pf[t][s][3]};
             oacc[n] = mfma32(vf, __builtin_bit_cast(bf16x8, pw), oacc[n]);
           }
         }
       }
+      if constexpr (KFATT_FWD_SCHED > 0) {
+        // the same for the PV product: two tr reads per V^T operand
+        constexpr int NM = 4 * ND, PF = KFATT_FWD_SCHED / 2 < NM ? KFATT_FWD_SCHED / 2 : NM;
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+          if (m + PF < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+      }
     }
     if (more) {
       if constexpr (kDma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces
-      stage_write((j + 1) & 1);
+      stage_write(1 - BUF);
     }
     __syncthreads();
+  };
+  for (int j = 0; j < ntiles; j += 2) {
+    tile_body(j, std::integral_constant<int, 0>{});
+    if (j + 1 < ntiles) tile_body(j + 1, std::integral_constant<int, 1>{});
   }
 
   // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
@@ -493,8 +550,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
       const int byte = pc * 1024 + lane * 16;
       const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
       const int ch = sc ^ swz<D>(row, 0);
-      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * ((k0 + row) * (int)kt + ch * 8));
-      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * ((k0 + row) * (int)vt + ch * 8));
+      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
+      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
     }
   };
 
@@ -507,10 +564,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int j = 0; j < ntiles; ++j) {
+  // per-lane LDS read offsets computed once; the tile loop unrolled over the two buffers (as the forward)
+  int koff[KS], voff0[ND], voff1[ND];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) koff[kk] = img_off<D>(r, 2 * kk + hh);
+  {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 32 * n + 16 * (g & 1) + 4 * pp;
+      voff0[n] = img_off<D>(4 * hh + qq, col >> 3) + 8 * (pp & 1);
+      voff1[n] = img_off<D>(4 * hh + qq + 8, col >> 3) + 8 * (pp & 1);
+    }
+  }
+  auto tile_body = [&](int j, auto BUFC) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int k0 = j * FK;
-    if (j + 1 < ntiles) stage_dma(j + 1, (j + 1) & 1);  // buffer (j+1)&1 was last read before the barrier
-    const char* kimg = smem + (j & 1) * 2 * TILE;
+    if (j + 1 < ntiles) stage_dma(j + 1, 1 - BUF);  // buffer 1 - BUF was last read before the barrier
+    const char* kimg = smem + BUF * 2 * TILE;
     const char* vimg = kimg + TILE;
     if (!(CAUSAL && k0 > qw + 31)) {
       f32x16 sacc[2] = {(f32x16){}, (f32x16){}}, dpacc[2] = {(f32x16){}, (f32x16){}};
@@ -518,8 +589,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          sacc[t] = mfma32(lds_row(kimg, img_off<D>(32 * t + r, 2 * kk + hh)), qf[kk], sacc[t]);
-          dpacc[t] = mfma32(lds_row(vimg, img_off<D>(32 * t + r, 2 * kk + hh)), dof[kk], dpacc[t]);
+          sacc[t] = mfma32(lds_row(kimg + 32 * t * D * 2, koff[kk]), qf[kk], sacc[t]);
+          dpacc[t] = mfma32(lds_row(vimg + 32 * t * D * 2, koff[kk]), dof[kk], dpacc[t]);
         }
       }
       const bool need_mask = (CAUSAL && k0 + FK - 1 > qw) || k0 + FK > T;
@@ -543,7 +614,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x8 kf = tr_operand<D>(kimg, 32 * t + 16 * s2, 32 * n, lane);
+            const bf16x8 kf = join(tr_read(kimg + (32 * t + 16 * s2) * D * 2, voff0[n]),
+                                   tr_read(kimg + (32 * t + 16 * s2) * D * 2, voff1[n]));
             const u32x4 sw = {sf[t][s2][0], sf[t][s2][1], sf[t][s2][2], sf[t][s2][3]};
             dqacc[n] = mfma32(kf, __builtin_bit_cast(bf16x8, sw), dqacc[n]);
           }
@@ -553,6 +625,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
     // the next tile's pieces (the only vector-memory operations in the loop) have landed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  };
+  for (int j = 0; j < ntiles; j += 2) {
+    tile_body(j, std::integral_constant<int, 0>{});
+    if (j + 1 < ntiles) tile_body(j + 1, std::integral_constant<int, 1>{});
   }
 
   // lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
@@ -714,12 +790,12 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
       const int byte = pc * 1024 + lane * 16;
       const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
       const int ch = sc ^ swz<D>(row, 0);
-      dma16(dq_desc, lds_addr(qi + pc * 1024), 2 * ((q0 + row) * (int)qt + ch * 8));
-      dma16(ddo_desc, lds_addr(oi + pc * 1024), 2 * ((q0 + row) * (int)dot + ch * 8));
+      dma16(dq_desc, lds_addr(qi + pc * 1024), 2 * (row * (int)qt + ch * 8), 2 * q0 * (int)qt);
+      dma16(ddo_desc, lds_addr(oi + pc * 1024), 2 * (row * (int)dot + ch * 8), 2 * q0 * (int)dot);
     }
     // waves 0 / 1: the tile's 64 lse / delta values (no register staging: a pending load into a
     // register made the compiler wait vmcnt(0) before the tile's first MFMA)
-    if (w < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + w * BQ)), 4 * (q0 + lane));
+    if (w < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + w * BQ)), 4 * lane, 4 * q0);
   };
 
   const float c = a.scale * kLog2e;

@@ -26,6 +26,7 @@ def _variants():
     prod = B.TU_FLAGS.get("attention_bf16.hip", [])
     return {
         "prod": prod,  # the production flags and knob defaults
+        "head": prod,  # git HEAD's attention source with the production flags
         # the compiler's default AGPR form: S / dP shuttled through v_accvgpr moves
         "agprform": [],
         "guarded": [*prod, "-DKFATT_BUF=0", "-DKFATT_DMA=0", "-DKFATT_DQ_SPLIT=0"],  # per-row guards, atomics
@@ -33,6 +34,11 @@ def _variants():
         "atomics_regstage": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_DMA=0"],  # ... Q / dO register-staged
         "atomics_dropped": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_ABL=1"],  # timing only: atomics dropped
         "fwd_dma": [*prod, "-DKFATT_FWD_DMA=1"],  # forward K / V by LDS-DMA
+        "fwd_r5q": [*prod, "-DKFATT_FWD_OFFS=0", "-DKFATT_FWD_SCHED=0"],  # the forward as of r5q
+        "fsched4": [*prod, "-DKFATT_FWD_OFFS=0", "-DKFATT_FWD_SCHED=4"],  # LDS reads pipelined 4 ahead
+        "offs": [*prod, "-DKFATT_FWD_SCHED=0"],  # precomputed LDS offsets, buffers unrolled
+        "offs_sched4": [*prod, "-DKFATT_FWD_SCHED=4"],
+        "offs_sched8": [*prod, "-DKFATT_FWD_SCHED=8"],
     }
 
 
@@ -48,8 +54,13 @@ def build(names):
     OUT.mkdir(parents=True, exist_ok=True)
     for n in names:
         obj = OUT / f"attention_bf16_{n}.o"
-        subprocess.run([B.HIPCC, *B.HIP_FLAGS, *VARIANTS[n], "-I", str(B.KERNEL_DIR), "-c",
-                        str(B.KERNEL_DIR / "attention_bf16.hip"), "-o", str(obj)], check=True)
+        src = B.KERNEL_DIR / "attention_bf16.hip"
+        if n == "head":  # the committed source (git HEAD), for an A/B against the working tree
+            src = OUT / "attention_bf16_head.hip"
+            src.write_text(subprocess.run(["git", "-C", str(ROOT), "show", "HEAD:kernels/attention_bf16.hip"],
+                                          capture_output=True, text=True, check=True).stdout)
+        subprocess.run([B.HIPCC, *B.HIP_FLAGS, *VARIANTS[n], "-I", str(B.KERNEL_DIR), "-c", str(src), "-o", str(obj)],
+                       check=True)
         lib = OUT / f"libkfamd_kernels_{n}.so"
         subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", str(lib), str(obj),
                         *map(str, others)], check=True)

@@ -1,0 +1,22 @@
+#!/bin/bash
+# forward: LDS operand reads software-pipelined ahead of the MFMAs (KFATT_FWD_SCHED) vs the
+# compiler's schedule; numerics first, then two alternating bench rounds (fwd-dominated shapes)
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r5u_attn_fsched
+mkdir -p $OUT
+cd $R
+VARS=${VARS:-prod fsched4 fsched8 fsched8_dma}
+for v in $VARS; do
+  KFAMD_KERNEL_LIB=$R/kubeflow_rm_amd/lib/attnab/libkfamd_kernels_$v.so timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_attention.py > $OUT/pytest_$v.log 2>&1
+  rc=$?; echo "$v pytest rc=$rc $(tail -1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || exit $rc
+done
+for r in 1 2; do
+  for v in $VARS; do
+    KFAMD_KERNEL_LIB=$R/kubeflow_rm_amd/lib/attnab/libkfamd_kernels_$v.so timeout -k 10 200 python -u tools/attn_bench.py > $OUT/bench_${v}_$r.jsonl 2> $OUT/bench_${v}_$r.err || exit $?
+    echo "== $v round $r"; python3 -c "
+import json
+for l in open('$OUT/bench_${v}_$r.jsonl'):
+    d=json.loads(l); print(d['shape'], d['pass'], d['ours_us'], d['sdpa_us'], d['ours_tflops'])"
+  done
+done
