@@ -253,19 +253,26 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
   const i32x4 dk_desc = slice_desc(kb, 2LL * T * kt), dv_desc = slice_desc(vb, 2LL * T * vt);
   // KFATT_DMA: K / V tiles by LDS-DMA (as the backward's stage_dma): no staging registers
+  constexpr int NPC = TILE / 1024 / 4;
+  // LDS-DMA pieces: the wave index as a uniform value, each piece's per-lane source offset computed
+  // once (image chunk sc of row `row` holds source chunk sc ^ swz(row, 0))
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int dvo_k[NPC], dvo_v[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; ++i) {
+    const int byte = (wu * NPC + i) * 1024 + lane * 16;
+    const int row = byte / (D * 2), ch = ((byte % (D * 2)) >> 4) ^ swz<D>(row, 0);
+    dvo_k[i] = 2 * (row * (int)kt + ch * 8);
+    dvo_v[i] = 2 * (row * (int)vt + ch * 8);
+  }
   auto stage_dma = [&](int tile, int buf) {
-    constexpr int NPC = TILE / 1024 / 4;
     const int k0 = tile * FK;
     char* kimg = smem + buf * 2 * TILE;
     char* vimg = kimg + TILE;
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
-      const int pc = w * NPC + i;
-      const int byte = pc * 1024 + lane * 16;
-      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
-      const int ch = sc ^ swz<D>(row, 0);
-      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
-      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
+      dma16(dk_desc, lds_addr(kimg + (wu * NPC + i) * 1024), dvo_k[i], 2 * k0 * (int)kt);
+      dma16(dv_desc, lds_addr(vimg + (wu * NPC + i) * 1024), dvo_v[i], 2 * k0 * (int)vt);
     }
   };
   auto stage_load = [&](int tile) {
@@ -464,11 +471,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
 }
 
 // ------------------------------------------------------------------------------------------------
-// backward prologue: delta[b][h][t] = sum_d dO * O (fp32)
+// backward prologue, per row [b][h][t]: nd = -sum_d dO * O and nl = -lse / scale (fp32), the two
+// row constants of the backward in the form its products start from: S - lse / scale and dP - delta
+// are the MFMA accumulators initialised with nl and nd (no negate / scale per element and tile)
 // ------------------------------------------------------------------------------------------------
 template <int D>
 __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__ o, const __bf16* __restrict__ dout,
-                                                      float* __restrict__ delta, AttnShape a) {
+                                                      const float* __restrict__ lse, float* __restrict__ nl,
+                                                      float* __restrict__ nd, AttnShape a) {
   constexpr int LPR = D / 8;        // lanes per row (16 B each)
   constexpr int RPB = 256 / LPR;    // rows per block
   const long long nrows = (long long)a.B * a.H * a.T;
@@ -486,7 +496,10 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
     for (int e = 0; e < 8; ++e) s = fmaf((float)xb[e], (float)yb[e], s);
   }
   s = kfw::group_sum<LPR>(s);
-  if (row < nrows && part == 0) delta[row] = s;
+  if (row < nrows && part == 0) {
+    nd[row] = -s;
+    nl[row] = -lse[row] / a.scale;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -535,23 +548,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
     dof[kk] = __builtin_bit_cast(bf16x8, bload16(rdo, 2 * (qrow * (int)dot + kk * 16 + 8 * hh)));
   }
   const long long rowbase = ((long long)b * a.H + h) * T;
-  const float lse_q = qrow < T ? lse[rowbase + qrow] * kLog2e : 0.f;
-  const float del_q = qrow < T ? delta[rowbase + qrow] : 0.f;
+  // (lse / delta arrive as the prologue's nl = -lse / scale and nd = -delta)
+  const float nlc = qrow < T ? lse[rowbase + qrow] * (a.scale * kLog2e) : 0.f;
+  const float nd_q = qrow < T ? delta[rowbase + qrow] : 0.f;
 
   const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
   // K / V tile `tile` -> image buffer `buf`, each lane fetching the chunk the swizzle puts at its slot
+  // LDS-DMA pieces: the wave index as a uniform value, each piece's per-lane source offset computed
+  // once (image chunk sc of row `row` holds source chunk sc ^ swz(row, 0))
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int dvo_k[NPC], dvo_v[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; ++i) {
+    const int byte = (wu * NPC + i) * 1024 + lane * 16;
+    const int row = byte / (D * 2), ch = ((byte % (D * 2)) >> 4) ^ swz<D>(row, 0);
+    dvo_k[i] = 2 * (row * (int)kt + ch * 8);
+    dvo_v[i] = 2 * (row * (int)vt + ch * 8);
+  }
   auto stage_dma = [&](int tile, int buf) {
     const int k0 = tile * FK;
     char* kimg = smem + buf * 2 * TILE;
     char* vimg = kimg + TILE;
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
-      const int pc = w * NPC + i;
-      const int byte = pc * 1024 + lane * 16;
-      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
-      const int ch = sc ^ swz<D>(row, 0);
-      dma16(dk_desc, lds_addr(kimg + pc * 1024), 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
-      dma16(dv_desc, lds_addr(vimg + pc * 1024), 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
+      dma16(dk_desc, lds_addr(kimg + (wu * NPC + i) * 1024), dvo_k[i], 2 * k0 * (int)kt);
+      dma16(dv_desc, lds_addr(vimg + (wu * NPC + i) * 1024), dvo_v[i], 2 * k0 * (int)vt);
     }
   };
 
@@ -599,13 +620,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int e = 0; e < 16; e += 2) {
-          float p0 = fast_exp2(fmaf(sacc[t][e], c, -lse_q)), p1 = fast_exp2(fmaf(sacc[t][e + 1], c, -lse_q));
+          float p0 = fast_exp2(fmaf(sacc[t][e], c, nlc)), p1 = fast_exp2(fmaf(sacc[t][e + 1], c, nlc));
           if (need_mask) {
             const int key = k0 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * hh;
             if ((CAUSAL && key > qrow) || key >= T) p0 = 0.f;
             if ((CAUSAL && key + 1 > qrow) || key + 1 >= T) p1 = 0.f;
           }
-          sf[t][e >> 3][(e & 7) >> 1] = pack2(p0 * (dpacc[t][e] - del_q), p1 * (dpacc[t][e + 1] - del_q));
+          sf[t][e >> 3][(e & 7) >> 1] = pack2(p0 * (dpacc[t][e] + nd_q), p1 * (dpacc[t][e + 1] + nd_q));
         }
       }
 #pragma unroll
@@ -780,26 +801,31 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   // registers. A wave instruction fills 1 KiB of the image linearly (lane L at +16 L), so each lane
   // fetches the chunk that the swizzle puts there: image chunk sc of row `row` holds source chunk
   // sc ^ swz(row, 0) (the swizzle is an XOR per row). Rows past T land as zeros (buffer range).
+  // LDS-DMA pieces: uniform wave index, per-lane source offsets computed once (as the forward's)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int dvo_q[kDma ? NQC : 1], dvo_o[kDma ? NQC : 1];
+#pragma unroll
+  for (int i = 0; i < (kDma ? NQC : 0); ++i) {
+    const int byte = (wu * NQC + i) * 1024 + lane * 16;
+    const int row = byte / (D * 2), ch = ((byte % (D * 2)) >> 4) ^ swz<D>(row, 0);
+    dvo_q[i] = 2 * (row * (int)qt + ch * 8);
+    dvo_o[i] = 2 * (row * (int)dot + ch * 8);
+  }
   auto stage_dma = [&](int tile, int buf) {
     const int q0 = qstart + tile * BQ;
     char* qi = qtiles + buf * 2 * QT;
     char* oi = qi + QT;
 #pragma unroll
     for (int i = 0; i < NQC; ++i) {
-      const int pc = w * NQC + i;                         // 1 KiB piece of the image
-      const int byte = pc * 1024 + lane * 16;
-      const int row = byte / (D * 2), sc = (byte % (D * 2)) >> 4;
-      const int ch = sc ^ swz<D>(row, 0);
-      dma16(dq_desc, lds_addr(qi + pc * 1024), 2 * (row * (int)qt + ch * 8), 2 * q0 * (int)qt);
-      dma16(ddo_desc, lds_addr(oi + pc * 1024), 2 * (row * (int)dot + ch * 8), 2 * q0 * (int)dot);
+      dma16(dq_desc, lds_addr(qi + (wu * NQC + i) * 1024), dvo_q[i], 2 * q0 * (int)qt);
+      dma16(ddo_desc, lds_addr(oi + (wu * NQC + i) * 1024), dvo_o[i], 2 * q0 * (int)dot);
     }
     // waves 0 / 1: the tile's 64 lse / delta values (no register staging: a pending load into a
     // register made the compiler wait vmcnt(0) before the tile's first MFMA)
-    if (w < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + w * BQ)), 4 * lane, 4 * q0);
+    if (wu < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + wu * BQ)), 4 * lane, 4 * q0);
   };
 
   const float c = a.scale * kLog2e;
-  const float inv_scale = 1.f / a.scale;
   f32x16 dkacc[ND], dvacc[ND];
 #pragma unroll
   for (int n = 0; n < ND; ++n) {
@@ -815,16 +841,32 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
   }
   __syncthreads();
 
-  for (int it = 0; it < ntiles; ++it) {
+  // per-lane LDS read offsets computed once; the q-tile loop unrolled over the two buffers so the
+  // buffer / sub-tile / k-step parts of every read ride in the ds_read immediate (as the forward)
+  int koff[KS], voff0[ND], voff1[ND];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) koff[kk] = img_off<D>(r, 2 * kk + hh);  // + 32 j / 32 w rows
+  {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 32 * n + 16 * (g & 1) + 4 * pp;
+      voff0[n] = img_off<D>(4 * hh + qq, col >> 3) + 8 * (pp & 1);
+      voff1[n] = img_off<D>(4 * hh + qq + 8, col >> 3) + 8 * (pp & 1);
+    }
+  }
+  const char* const kimg_w = kimg + 32 * w * D * 2;  // this wave's 32 key rows
+  auto tile_body = [&](int it, auto BUFC) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int q0 = qstart + it * BQ;
     const bool more = it + 1 < ntiles;
     if (more) {
-      if constexpr (kDma) stage_dma(it + 1, (it + 1) & 1);
+      if constexpr (kDma) stage_dma(it + 1, 1 - BUF);
       stage_load(it + 1);
     }
-    const char* qi = qtiles + (it & 1) * 2 * QT;
+    const char* qi = qtiles + BUF * 2 * QT;
     const char* oi = qi + QT;
-    const float* lse_s = rowc + (it & 1) * 2 * BQ;
+    const float* lse_s = rowc + BUF * 2 * BQ;
     const float* del_s = lse_s + BQ;
 
     // causal: every query of the tile precedes every key of the wave -> P = dS = 0
@@ -836,23 +878,23 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
         // one 32-row sub-tile at a time: its P / dS fragments are consumed before the next one's exist
         uint32_t pf[2][4], sf[2][4];
         f32x16 sacc, dpacc;
-        // row constants: -lse / scale and -delta for the query rows of this lane's registers
+        // row constants nl = -lse / scale and nd = -delta (the prologue's) for this lane's query rows
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_s + 32 * j + 8 * g + 4 * hh);
           const f32x4 d4 = *reinterpret_cast<const f32x4*>(del_s + 32 * j + 8 * g + 4 * hh);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sacc[4 * g + e] = -l4[e] * inv_scale;
-            dpacc[4 * g + e] = -d4[e];
+            sacc[4 * g + e] = l4[e];   // nl = -lse / scale
+            dpacc[4 * g + e] = d4[e];  // nd = -delta
           }
         }
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
-          const bf16x8 qa = lds_row(qi, img_off<D>(32 * j + r, 2 * kk + hh));
-          const bf16x8 kbf = lds_row(kimg, img_off<D>(32 * w + r, 2 * kk + hh));
+          const bf16x8 qa = lds_row(qi + 32 * j * D * 2, koff[kk]);
+          const bf16x8 kbf = lds_row(kimg_w, koff[kk]);
           sacc = mfma32(qa, kbf, sacc);
-          const bf16x8 oa = lds_row(oi, img_off<D>(32 * j + r, 2 * kk + hh));
+          const bf16x8 oa = lds_row(oi + 32 * j * D * 2, koff[kk]);
           dpacc = mfma32(oa, vf[kk], dpacc);
         }
         // P and dS; rows q = q0 + 32 j + (e & 3) + 8 (e >> 2) + 4 hh, column = this lane's key
@@ -882,9 +924,11 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
           for (int sx = 0; sx < 2; ++sx) {
             const u32x4 pw = {pf[sx][0], pf[sx][1], pf[sx][2], pf[sx][3]};
             const u32x4 sw = {sf[sx][0], sf[sx][1], sf[sx][2], sf[sx][3]};
-            const bf16x8 doa = tr_operand<D>(oi, 32 * j + 16 * sx, 32 * n, lane);
+            const bf16x8 doa = join(tr_read(oi + (32 * j + 16 * sx) * D * 2, voff0[n]),
+                                    tr_read(oi + (32 * j + 16 * sx) * D * 2, voff1[n]));
             dvacc[n] = mfma32(doa, __builtin_bit_cast(bf16x8, pw), dvacc[n]);
-            const bf16x8 qa = tr_operand<D>(qi, 32 * j + 16 * sx, 32 * n, lane);
+            const bf16x8 qa = join(tr_read(qi + (32 * j + 16 * sx) * D * 2, voff0[n]),
+                                   tr_read(qi + (32 * j + 16 * sx) * D * 2, voff1[n]));
             dkacc[n] = mfma32(qa, __builtin_bit_cast(bf16x8, sw), dkacc[n]);
           }
         }
@@ -940,9 +984,13 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
       // the next tile's LDS-DMA pieces (and the lse / delta load) were issued before this tile's
       // DQT x 16 dQ atomics: waiting down to that many outstanding lands exactly them
       if constexpr (kDma) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DQS ? 0 : DQT * 16) : "memory");
-      stage_write((it + 1) & 1);
+      stage_write(1 - BUF);
     }
     __syncthreads();
+  };
+  for (int it = 0; it < ntiles; it += 2) {
+    tile_body(it, std::integral_constant<int, 0>{});
+    if (it + 1 < ntiles) tile_body(it + 1, std::integral_constant<int, 1>{});
   }
 
   // epilogue: dK = scale * (dK^T)^T, dV; lane = key, rows d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
@@ -1030,8 +1078,8 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
 }
 
 extern "C" long long kfamd_attn_bwd_workspace(int B, int H, int T, int D) {
-  // delta f32 [B][H][T] (+ dq_acc f32 [B][T][H][D] in front of it when dQ goes through atomics)
-  return (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D * 4) + (long long)B * H * T * 4;
+  // nl, nd f32 [B][H][T] (+ dq_acc f32 [B][T][H][D] in front of them when dQ goes through atomics)
+  return (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D * 4) + 2LL * B * H * T * 4;
 }
 
 // strides: 8 tensors x (b, h, t): q, k, v, o, do, dq, dk, dv. workspace: kfamd_attn_bwd_workspace bytes
@@ -1049,7 +1097,9 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
   if (nk >= (1ll << 31)) return KFAMD_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* dq_acc = static_cast<float*>(workspace);  // (unused with KFATT_DQ_SPLIT)
-  float* delta = dq_acc + (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D);
+  // the prologue's row constants: nl = -lse / scale and nd = -delta, [B][H][T] each
+  float* nl = dq_acc + (KFATT_DQ_SPLIT ? 0LL : (long long)B * T * H * D);
+  float* nd = nl + (long long)B * H * T;
   const long long dq_st = (long long)H * D, dq_sh = D, dq_sb = (long long)T * H * D;
   if (!slice_ok(T, s.s[TQ][2], 2) || !slice_ok(T, s.s[TDO][2], 2) || !slice_ok(T, dq_st, 4)) return KFAMD_EINVAL;
   const long long rows = (long long)B * H * T;
@@ -1061,14 +1111,14 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
     if (!slice_ok(T, s.s[TK][2], 2) || !slice_ok(T, s.s[TV][2], 2)) return KFAMD_EINVAL;
     auto run = [&](auto delta_k, auto main_k, auto dq_k) {
       hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
-                         static_cast<const __bf16*>(dout), delta, s);
+                         static_cast<const __bf16*>(dout), static_cast<const float*>(lse), nl, nd, s);
       hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(256), 0, st, static_cast<const __bf16*>(q),
                          static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
-                         static_cast<const float*>(lse), static_cast<const float*>(delta), dq_acc,
+                         static_cast<const float*>(nl), static_cast<const float*>(nd), dq_acc,
                          static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s, dq_st, dq_sh, dq_sb);
       hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
                          static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
-                         static_cast<const float*>(lse), static_cast<const float*>(delta), static_cast<__bf16*>(dq), s);
+                         static_cast<const float*>(nl), static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
     };
     if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true, true>, attn_bwd_dq_split<128, true>)
                          : run(attn_bwd_delta<128>, attn_bwd<128, false, true>, attn_bwd_dq_split<128, false>);
@@ -1081,10 +1131,10 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
   if (e != hipSuccess) return static_cast<int>(e);
   auto run = [&](auto delta_k, auto main_k, auto dq_k) {
     hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
-                       static_cast<const __bf16*>(dout), delta, s);
+                       static_cast<const __bf16*>(dout), static_cast<const float*>(lse), nl, nd, s);
     hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(256), 0, st, static_cast<const __bf16*>(q),
                        static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
-                       static_cast<const float*>(lse), static_cast<const float*>(delta), dq_acc,
+                       static_cast<const float*>(nl), static_cast<const float*>(nd), dq_acc,
                        static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s, dq_st, dq_sh, dq_sb);
     hipLaunchKernelGGL(dq_k, dim3(rblocks), dim3(256), 0, st, static_cast<const float*>(dq_acc),
                        static_cast<__bf16*>(dq), s, dq_st, dq_sh, dq_sb);
