@@ -149,6 +149,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_FWD_SCHED
 #define KFATT_FWD_SCHED 0  // forward: LDS operand reads this many ahead of the MFMAs (0: compiler's schedule)
 #endif
+#ifndef KFATT_DKDV8
+#define KFATT_DKDV8 1  // D = 128 dK / dV with 8 waves (two per SIMD), attn_bwd_dkdv8 (profiles/r5w_attn_dkdv8)
+#endif
 #ifndef KFATT_FWD_OFFS
 #define KFATT_FWD_OFFS 1  // forward: LDS read offsets precomputed per lane, buffers unrolled
 #endif
@@ -685,6 +688,222 @@ __device__ __forceinline__ int dst_off(int row, int slot8) {
 // ------------------------------------------------------------------------------------------------
 constexpr int BK = 128, BQ = 64, QS = BQ / 32;
 
+// ------------------------------------------------------------------------------------------------
+// dK / dV with two waves per SIMD (KFATT_DKDV8, used with the split dQ kernel): 8 waves = 4 key
+// groups of 32 keys x 2 query halves. Wave (w, jh) takes rows 32 jh .. 32 jh + 31 of every 64-row
+// query tile for the keys of group w, so the two waves of a SIMD interleave their LDS waits and
+// barriers with each other's MFMAs (the 4-wave kernel runs one wave per SIMD at D = 128 and waits
+// half its cycles). K and V both sit in LDS (V rows are the dP product's B operand) to keep a wave
+// within 256 registers; the two halves' partial dK^T / dV^T are summed through LDS at the end.
+// ------------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                         const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                         const float* __restrict__ nl, const float* __restrict__ nd,
+                                                         __bf16* __restrict__ dk, __bf16* __restrict__ dv, AttnShape a) {
+  constexpr int KS = D / 16;
+  constexpr int ND = D / 32;
+  constexpr int CH = D / 8;
+  constexpr int KIMG = BK * D * 2;          // K (and V) image: [128 keys][D]
+  constexpr int QT = BQ * D * 2;            // one Q (or dO) tile image: [64][D]
+  constexpr int NPC = QT / 1024 / 8;        // LDS-DMA pieces per wave per tile image
+  static_assert(NPC >= 1, "head dim");
+  static_assert(4 * QT >= 4 * ND * 4 * 1024, "partial-sum staging fits the Q / dO region");
+  __shared__ __attribute__((aligned(16))) char smem[2 * KIMG + 4 * QT + 4 * BQ * 4];
+  char* const kimg = smem;
+  char* const vimg = smem + KIMG;
+  char* const qtiles = smem + 2 * KIMG;     // [buf][Q, dO]
+  float* const rowc = reinterpret_cast<float*>(qtiles + 4 * QT);  // [buf][nl(64), nd(64)]
+
+  const int T = a.T;
+  const int nk = (T + BK - 1) / BK;
+  const int nwg = nk * a.H * a.B;
+  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  const int kblk = lid % nk;
+  const int bh = lid / nk, h = bh % a.H, b = bh / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // 0..7, uniform
+  const int w = wv & 3, jh = wv >> 2;                       // key group, query half
+  const int k0 = kblk * BK, kw = k0 + 32 * w, key = kw + r;
+
+  const __bf16* qb = q + base_off(a, TQ, b, h);
+  const __bf16* kb = k + base_off(a, TK, b, h);
+  const __bf16* vb = v + base_off(a, TV, b, h);
+  const __bf16* dob = dout + base_off(a, TDO, b, h);
+  const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2], dot = a.s[TDO][2];
+  const float* nlb = nl + ((long long)b * a.H + h) * T;
+  const float* ndb = nd + ((long long)b * a.H + h) * T;
+  const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
+
+  // K and V images of the block's 128 keys (rows past T: zeros)
+#pragma unroll
+  for (int i = 0; i < BK * CH / 512; ++i) {
+    const int c = tid + 512 * i, row = c / CH, ch = c % CH;
+    *reinterpret_cast<u32x4*>(kimg + img_off<D>(row, ch)) = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * k0 * (int)kt);
+    *reinterpret_cast<u32x4*>(vimg + img_off<D>(row, ch)) = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * k0 * (int)vt);
+  }
+
+  const int qstart = CAUSAL ? k0 : 0;
+  const int ntiles = (T - qstart + BQ - 1) / BQ;
+
+  const i32x4 dq_desc = slice_desc(qb, 2LL * T * qt), ddo_desc = slice_desc(dob, 2LL * T * dot);
+  const i32x4 drow_desc = slice_desc(wv == 0 ? nlb : ndb, 4LL * T);
+  int dvo_q[NPC], dvo_o[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; ++i) {
+    const int byte = (wv * NPC + i) * 1024 + lane * 16;
+    const int row = byte / (D * 2), ch = ((byte % (D * 2)) >> 4) ^ swz<D>(row, 0);
+    dvo_q[i] = 2 * (row * (int)qt + ch * 8);
+    dvo_o[i] = 2 * (row * (int)dot + ch * 8);
+  }
+  auto stage_dma = [&](int tile, int buf) {
+    const int q0 = qstart + tile * BQ;
+    char* qi = qtiles + buf * 2 * QT;
+    char* oi = qi + QT;
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      dma16(dq_desc, lds_addr(qi + (wv * NPC + i) * 1024), dvo_q[i], 2 * q0 * (int)qt);
+      dma16(ddo_desc, lds_addr(oi + (wv * NPC + i) * 1024), dvo_o[i], 2 * q0 * (int)dot);
+    }
+    if (wv < 2) dma4(drow_desc, lds_addr(reinterpret_cast<const char*>(rowc + buf * 2 * BQ + wv * BQ)), 4 * lane, 4 * q0);
+  };
+
+  int koff[KS], voff0[ND], voff1[ND];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) koff[kk] = img_off<D>(r, 2 * kk + hh);
+  {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 32 * n + 16 * (g & 1) + 4 * pp;
+      voff0[n] = img_off<D>(4 * hh + qq, col >> 3) + 8 * (pp & 1);
+      voff1[n] = img_off<D>(4 * hh + qq + 8, col >> 3) + 8 * (pp & 1);
+    }
+  }
+  const char* const kimg_w = kimg + 32 * w * D * 2;
+  const char* const vimg_w = vimg + 32 * w * D * 2;
+
+  const float c = a.scale * kLog2e;
+  f32x16 dkacc[ND], dvacc[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) {
+    dkacc[n] = (f32x16){};
+    dvacc[n] = (f32x16){};
+  }
+
+  if (ntiles > 0) stage_dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  auto tile_body = [&](int it, auto BUFC) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(BUFC)::value;
+    const int q0 = qstart + it * BQ;
+    if (it + 1 < ntiles) stage_dma(it + 1, 1 - BUF);
+    const char* qi = qtiles + BUF * 2 * QT + 32 * jh * D * 2;  // this wave's 32 query rows
+    const char* oi = qi + QT;
+    const float* nl_s = rowc + BUF * 2 * BQ + 32 * jh;
+    const float* nd_s = nl_s + BQ;
+    const int qw = q0 + 32 * jh;
+    // causal: every query of the half precedes every key of the wave -> P = dS = 0
+    if (!(CAUSAL && qw + 31 < kw)) {
+      const bool need_mask = (CAUSAL && qw < kw + 31) || qw + 32 > T || key >= T;
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(nl_s + 8 * g + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(nd_s + 8 * g + 4 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sacc[4 * g + e] = l4[e];
+          dpacc[4 * g + e] = d4[e];
+        }
+      }
+      // S^T-free form as the 4-wave kernel: rows = this wave's queries, column = the lane's key
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        sacc = mfma32(lds_row(qi, koff[kk]), lds_row(kimg_w, koff[kk]), sacc);
+        dpacc = mfma32(lds_row(oi, koff[kk]), lds_row(vimg_w, koff[kk]), dpacc);
+      }
+      uint32_t pf[2][4], sf[2][4];
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        float p0 = fast_exp2(sacc[e] * c), p1 = fast_exp2(sacc[e + 1] * c);
+        if (need_mask) {
+          const int qa0 = qw + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if ((CAUSAL && qa0 < key) || qa0 >= T || key >= T) p0 = 0.f;
+          if ((CAUSAL && qa0 + 1 < key) || qa0 + 1 >= T || key >= T) p1 = 0.f;
+        }
+        pf[e >> 3][(e & 7) >> 1] = pack2(p0, p1);
+        sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
+      }
+      // dV^T += dO^T . P and dK^T += Q^T . dS over this half's rows (permuted k order)
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+#pragma unroll
+        for (int sx = 0; sx < 2; ++sx) {
+          const u32x4 pw = {pf[sx][0], pf[sx][1], pf[sx][2], pf[sx][3]};
+          const u32x4 sw = {sf[sx][0], sf[sx][1], sf[sx][2], sf[sx][3]};
+          const bf16x8 doa = join(tr_read(oi + 16 * sx * D * 2, voff0[n]), tr_read(oi + 16 * sx * D * 2, voff1[n]));
+          dvacc[n] = mfma32(doa, __builtin_bit_cast(bf16x8, pw), dvacc[n]);
+          const bf16x8 qa = join(tr_read(qi + 16 * sx * D * 2, voff0[n]), tr_read(qi + 16 * sx * D * 2, voff1[n]));
+          dkacc[n] = mfma32(qa, __builtin_bit_cast(bf16x8, sw), dkacc[n]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces (the loop's only VMEM)
+    __syncthreads();
+  };
+  for (int it = 0; it < ntiles; it += 2) {
+    tile_body(it, std::integral_constant<int, 0>{});
+    if (it + 1 < ntiles) tile_body(it + 1, std::integral_constant<int, 1>{});
+  }
+
+  // the two query halves' partial sums: half 1 stages its accumulators (f32, lane-major) in the
+  // Q / dO region, half 0 adds them and stores; dK first, then dV
+  float* const part = reinterpret_cast<float*>(qtiles);
+  auto reduce = [&](f32x16 (&acc)[ND]) __attribute__((always_inline)) {
+    if (jh == 1) {
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(part + (((w * ND + n) * 4 + g) * 64 + lane) * 4) =
+              (f32x4){acc[n][4 * g], acc[n][4 * g + 1], acc[n][4 * g + 2], acc[n][4 * g + 3]};
+    }
+    __syncthreads();
+    if (jh == 0) {
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(part + (((w * ND + n) * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[n][4 * g + e] += x[e];
+        }
+    }
+    __syncthreads();
+  };
+  reduce(dkacc);
+  reduce(dvacc);
+  // lane = key, rows d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
+  if (jh == 0 && key < T) {
+    __bf16* dkr = dk + base_off(a, TDK, b, h) + key * a.s[TDK][2];
+    __bf16* dvr = dv + base_off(a, TDV, b, h) + key * a.s[TDV][2];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * n + 8 * g + 4 * hh;
+        const float sc = a.scale;
+        *reinterpret_cast<u32x2*>(dkr + d) =
+            (u32x2){pack2(dkacc[n][4 * g] * sc, dkacc[n][4 * g + 1] * sc), pack2(dkacc[n][4 * g + 2] * sc, dkacc[n][4 * g + 3] * sc)};
+        *reinterpret_cast<u32x2*>(dvr + d) =
+            (u32x2){pack2(dvacc[n][4 * g], dvacc[n][4 * g + 1]), pack2(dvacc[n][4 * g + 2], dvacc[n][4 * g + 3])};
+      }
+    }
+  }
+}
+
 // D = 128 holds dK^T, dV^T (128 registers) and V (32) for the whole sweep: one wave per SIMD
 // (512-register budget, no spills); D = 64 fits two
 template <int D, bool CAUSAL, bool DQS = false>
@@ -1120,7 +1339,22 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
                          static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
                          static_cast<const float*>(nl), static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
     };
-    if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true, true>, attn_bwd_dq_split<128, true>)
+    if (KFATT_DKDV8 && D == 128) {
+      auto run8 = [&](auto delta_k, auto main_k, auto dq_k) {
+        hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(lse), nl, nd, s);
+        hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(512), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s);
+        hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
+      };
+      causal ? run8(attn_bwd_delta<128>, attn_bwd_dkdv8<128, true>, attn_bwd_dq_split<128, true>)
+             : run8(attn_bwd_delta<128>, attn_bwd_dkdv8<128, false>, attn_bwd_dq_split<128, false>);
+    } else if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true, true>, attn_bwd_dq_split<128, true>)
                          : run(attn_bwd_delta<128>, attn_bwd<128, false, true>, attn_bwd_dq_split<128, false>);
     else causal ? run(attn_bwd_delta<64>, attn_bwd<64, true, true>, attn_bwd_dq_split<64, true>)
                 : run(attn_bwd_delta<64>, attn_bwd<64, false, true>, attn_bwd_dq_split<64, false>);
