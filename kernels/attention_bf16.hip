@@ -152,6 +152,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_DKDV8
 #define KFATT_DKDV8 1  // D = 128 dK / dV with 8 waves (two per SIMD), attn_bwd_dkdv8 (profiles/r5w_attn_dkdv8)
 #endif
+#ifndef KFATT_DKDV8_64
+#define KFATT_DKDV8_64 1  // D = 64 with the 8-wave dK / dV kernel too (16x12x2048x64: 516 -> 485 us)
+#endif
 #ifndef KFATT_FWD_OFFS
 #define KFATT_FWD_OFFS 1  // forward: LDS read offsets precomputed per lane, buffers unrolled
 #endif
@@ -697,7 +700,7 @@ constexpr int BK = 128, BQ = 64, QS = BQ / 32;
 // within 256 registers; the two halves' partial dK^T / dV^T are summed through LDS at the end.
 // ------------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                          const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                          const float* __restrict__ nl, const float* __restrict__ nd,
                                                          __bf16* __restrict__ dk, __bf16* __restrict__ dv, AttnShape a) {
@@ -1356,7 +1359,22 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
              : run8(attn_bwd_delta<128>, attn_bwd_dkdv8<128, false>, attn_bwd_dq_split<128, false>);
     } else if (D == 128) causal ? run(attn_bwd_delta<128>, attn_bwd<128, true, true>, attn_bwd_dq_split<128, true>)
                          : run(attn_bwd_delta<128>, attn_bwd<128, false, true>, attn_bwd_dq_split<128, false>);
-    else causal ? run(attn_bwd_delta<64>, attn_bwd<64, true, true>, attn_bwd_dq_split<64, true>)
+    else if (KFATT_DKDV8_64) {
+      auto run8 = [&](auto delta_k, auto main_k, auto dq_k) {
+        hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(lse), nl, nd, s);
+        hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(512), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s);
+        hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
+      };
+      causal ? run8(attn_bwd_delta<64>, attn_bwd_dkdv8<64, true>, attn_bwd_dq_split<64, true>)
+             : run8(attn_bwd_delta<64>, attn_bwd_dkdv8<64, false>, attn_bwd_dq_split<64, false>);
+    } else causal ? run(attn_bwd_delta<64>, attn_bwd<64, true, true>, attn_bwd_dq_split<64, true>)
                 : run(attn_bwd_delta<64>, attn_bwd<64, false, true>, attn_bwd_dq_split<64, false>);
     e = hipGetLastError();
     return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
