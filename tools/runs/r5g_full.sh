@@ -1,7 +1,7 @@
 # round 5 checkpoint: the whole GPU suite, smoke(), the default bench line, the gpt step A/B
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r5g
+OUT=$R/gpurun_out/${RUN_TAG:-r5g}
 mkdir -p $OUT
 cd $R
 timeout -k 10 900 python -u -m pytest -m gpu -q --timeout 240 --timeout-method thread tests/ > $OUT/pytest_gpu.log 2>&1
