@@ -155,6 +155,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_DKDV8_64
 #define KFATT_DKDV8_64 1  // D = 64 with the 8-wave dK / dV kernel too (16x12x2048x64: 516 -> 485 us)
 #endif
+#ifndef KFATT_DQ_DELTA
+#define KFATT_DQ_DELTA 1  // the dQ kernel computes delta (runs first; no separate prologue kernel): gpt-1b bwd -5 %
+#endif
 #ifndef KFATT_FWD_OFFS
 #define KFATT_FWD_OFFS 1  // forward: LDS read offsets precomputed per lane, buffers unrolled
 #endif
@@ -517,11 +520,16 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
 // once, scaled, in bf16: no fp32 workspace, no atomics, no conversion pass. Costs the S and dP
 // products a second time (the dK / dV kernel computes them too).
 // ------------------------------------------------------------------------------------------------
-template <int D, bool CAUSAL>
+// DELTA (KFATT_DQ_DELTA): this kernel runs first and is also the backward's prologue: each lane's
+// query row computes delta = sum_d dO * O from the dO fragments it holds anyway plus one pass over O,
+// and writes nl / nd for the dK / dV kernel (lse, delta arrive raw; the separate prologue is gone)
+template <int D, bool CAUSAL, bool DELTA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                             const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
-                                                            __bf16* __restrict__ dq, AttnShape a) {
+                                                            __bf16* __restrict__ dq, AttnShape a,
+                                                            const __bf16* __restrict__ o, float* __restrict__ nl_out,
+                                                            float* __restrict__ nd_out) {
   constexpr int KS = D / 16;
   constexpr int ND = D / 32;
   constexpr int CH = D / 8;
@@ -554,9 +562,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
     dof[kk] = __builtin_bit_cast(bf16x8, bload16(rdo, 2 * (qrow * (int)dot + kk * 16 + 8 * hh)));
   }
   const long long rowbase = ((long long)b * a.H + h) * T;
-  // (lse / delta arrive as the prologue's nl = -lse / scale and nd = -delta)
-  const float nlc = qrow < T ? lse[rowbase + qrow] * (a.scale * kLog2e) : 0.f;
-  const float nd_q = qrow < T ? delta[rowbase + qrow] : 0.f;
+  float nlc, nd_q;
+  if constexpr (DELTA) {
+    const auto ro = slice_rsrc(o + base_off(a, TO, b, h), 2LL * T * a.s[TO][2]);
+    float dd = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8 of = __builtin_bit_cast(bf16x8, bload16(ro, 2 * (qrow * (int)a.s[TO][2] + kk * 16 + 8 * hh)));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dd = fmaf((float)of[e], (float)dof[kk][e], dd);
+    }
+    const float delta_q = kfw::sum_halves(dd);  // the row's other half of d (lane ^ 32)
+    const float lq = qrow < T ? lse[rowbase + qrow] : 0.f;
+    nlc = -lq * kLog2e;
+    nd_q = -delta_q;
+    if (hh == 0 && qrow < T) {
+      nl_out[rowbase + qrow] = -lq / a.scale;
+      nd_out[rowbase + qrow] = nd_q;
+    }
+  } else {
+    // (lse / delta arrive as the prologue's nl = -lse / scale and nd = -delta)
+    nlc = qrow < T ? lse[rowbase + qrow] * (a.scale * kLog2e) : 0.f;
+    nd_q = qrow < T ? delta[rowbase + qrow] : 0.f;
+  }
 
   const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
   // K / V tile `tile` -> image buffer `buf`, each lane fetching the chunk the swizzle puts at its slot
@@ -1340,9 +1368,27 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
                          static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s, dq_st, dq_sh, dq_sb);
       hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
                          static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<const __bf16*>(dout),
-                         static_cast<const float*>(nl), static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
+                         static_cast<const float*>(nl), static_cast<const float*>(nd), static_cast<__bf16*>(dq), s,
+                         static_cast<const __bf16*>(nullptr), static_cast<float*>(nullptr), static_cast<float*>(nullptr));
     };
-    if (KFATT_DKDV8 && D == 128) {
+    if (KFATT_DQ_DELTA && (D == 128 ? KFATT_DKDV8 : KFATT_DKDV8_64)) {
+      // the dQ kernel first, as the prologue too (nl / nd), then the 8-wave dK / dV kernel
+      auto runq = [&](auto dq_k, auto main_k) {
+        hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(lse),
+                           static_cast<const float*>(nullptr), static_cast<__bf16*>(dq), s,
+                           static_cast<const __bf16*>(o), nl, nd);
+        hipLaunchKernelGGL(main_k, dim3((unsigned)nk), dim3(512), 0, st, static_cast<const __bf16*>(q),
+                           static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
+                           static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s);
+      };
+      if (D == 128) causal ? runq(attn_bwd_dq_split<128, true, true>, attn_bwd_dkdv8<128, true>)
+                           : runq(attn_bwd_dq_split<128, false, true>, attn_bwd_dkdv8<128, false>);
+      else causal ? runq(attn_bwd_dq_split<64, true, true>, attn_bwd_dkdv8<64, true>)
+                  : runq(attn_bwd_dq_split<64, false, true>, attn_bwd_dkdv8<64, false>);
+    } else if (KFATT_DKDV8 && D == 128) {
       auto run8 = [&](auto delta_k, auto main_k, auto dq_k) {
         hipLaunchKernelGGL(delta_k, dim3(rblocks), dim3(256), 0, st, static_cast<const __bf16*>(o),
                            static_cast<const __bf16*>(dout), static_cast<const float*>(lse), nl, nd, s);
@@ -1353,7 +1399,8 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
         hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
                            static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
                            static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
-                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s,
+                           static_cast<const __bf16*>(nullptr), static_cast<float*>(nullptr), static_cast<float*>(nullptr));
       };
       causal ? run8(attn_bwd_delta<128>, attn_bwd_dkdv8<128, true>, attn_bwd_dq_split<128, true>)
              : run8(attn_bwd_delta<128>, attn_bwd_dkdv8<128, false>, attn_bwd_dq_split<128, false>);
@@ -1370,7 +1417,8 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
         hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
                            static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
                            static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
-                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s);
+                           static_cast<const float*>(nd), static_cast<__bf16*>(dq), s,
+                           static_cast<const __bf16*>(nullptr), static_cast<float*>(nullptr), static_cast<float*>(nullptr));
       };
       causal ? run8(attn_bwd_delta<64>, attn_bwd_dkdv8<64, true>, attn_bwd_dq_split<64, true>)
              : run8(attn_bwd_delta<64>, attn_bwd_dkdv8<64, false>, attn_bwd_dq_split<64, false>);

@@ -27,6 +27,7 @@ def _variants():
     return {
         "prod": prod,  # the production flags and knob defaults
         "head": prod,  # git HEAD's attention source with the production flags
+        "sepdelta": [*prod, "-DKFATT_DQ_DELTA=0"],  # the separate delta prologue kernel
         "dkdv4_64": [*prod, "-DKFATT_DKDV8_64=0"],  # D = 64 with the 4-wave dK / dV kernel
         "dkdv4": [*prod, "-DKFATT_DKDV8=0"],  # D = 128 dK / dV with the 4-wave kernel (one wave per SIMD)
         # the compiler's default AGPR form: S / dP shuttled through v_accvgpr moves
