@@ -2,7 +2,7 @@
 
 Every check compares the bf16 kernel with ``F.scaled_dot_product_attention`` evaluated in fp32 on
 the same bf16-rounded inputs: the output, the forward's log-sum-exp, and dq / dk / dv for a random
-upstream gradient. Shapes cover T in {128, 1000, 2048, 4096} (1000: partial query and key tiles),
+upstream gradient. Shapes cover T in {40, 65, 128, 1000, 2048, 4096} (40 / 65 / 1000: partial query and key tiles),
 odd batch / head counts, head dims 64 and 128, causal and not. The online-softmax rescale is forced
 by a spiked key (cdna_hip_programming.md §5.4 rule 26), and the fused-QKV entry point is checked
 against the view entry point (same numbers, gradients in the QKV layout).
@@ -49,6 +49,8 @@ SHAPES = [
     (1, 1, 4096, 128, True),
     (2, 3, 1000, 128, False),
     (1, 2, 256, 64, False),
+    (1, 2, 40, 128, True),   # shorter than one key tile and than one 128-row block
+    (2, 1, 65, 64, False),   # one row / key past a tile
 ]
 
 

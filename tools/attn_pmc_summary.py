@@ -17,8 +17,8 @@ def load(dirs):
         for f in Path(d).rglob("*counter_collection.csv"):
             for r in csv.DictReader(open(f)):
                 name = r.get("Kernel_Name", "")
-                for key in ("attn_bwd_dq_split", "attn_bwd_delta", "attn_bwd_dq<", "attn_bwd", "attn_fwd"):
-                    if key.rstrip("<") in name and (key != "attn_bwd" or ("dq" not in name and "delta" not in name)):
+                for key in ("attn_bwd_dq_split", "attn_bwd_dkdv8", "attn_bwd_delta", "attn_bwd_dq<", "attn_bwd", "attn_fwd"):
+                    if key.rstrip("<") in name and (key != "attn_bwd" or ("dq" not in name and "delta" not in name and "dkdv" not in name)):
                         tot[key.rstrip("<")][r["Counter_Name"]] += float(r["Counter_Value"])
                         break
     return tot
