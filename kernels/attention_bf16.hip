@@ -146,9 +146,6 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_DMA
 #define KFATT_DMA 1  // backward Q / dO tiles by LDS-DMA (attn_bwd stage_dma)
 #endif
-#ifndef KFATT_FWD_SCHED
-#define KFATT_FWD_SCHED 0  // forward: LDS operand reads this many ahead of the MFMAs (0: compiler's schedule)
-#endif
 #ifndef KFATT_DKDV8
 #define KFATT_DKDV8 1  // D = 128 dK / dV with 8 waves (two per SIMD), attn_bwd_dkdv8 (profiles/r5w_attn_dkdv8)
 #endif
@@ -370,17 +367,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
           sacc[t] = mfma32(kf, qf[kk], sacc[t]);
         }
       }
-      if constexpr (KFATT_FWD_SCHED > 0) {
-        // software pipeline KFATT_FWD_SCHED K-row fragments ahead of the MFMAs (the default schedule
-        // reads two, waits for them, runs two MFMAs: the LDS latency exposed every 64 MFMA cycles)
-        constexpr int NM = 2 * KS, PF = KFATT_FWD_SCHED < NM ? KFATT_FWD_SCHED : NM;
-        __builtin_amdgcn_sched_group_barrier(0x100, PF, 0);
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-          if (m + PF < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-      }
       // masks: causal (key > query) on tiles that reach the wave's diagonal, key >= T on the tail
       const bool causal_mask = CAUSAL && k0 + FK - 1 > qw;
       if (causal_mask || k0 + FK > T) {
@@ -437,16 +423,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
             const u32x4 pw = {pf[t][s][0], pf[t][s][1], pf[t][s][2], pf[t][s][3]};
             oacc[n] = mfma32(vf, __builtin_bit_cast(bf16x8, pw), oacc[n]);
           }
-        }
-      }
-      if constexpr (KFATT_FWD_SCHED > 0) {
-        // the same for the PV product: two tr reads per V^T operand
-        constexpr int NM = 4 * ND, PF = KFATT_FWD_SCHED / 2 < NM ? KFATT_FWD_SCHED / 2 : NM;
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-          if (m + PF < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         }
       }
     }

@@ -37,11 +37,6 @@ def _variants():
         "atomics_regstage": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_DMA=0"],  # ... Q / dO register-staged
         "atomics_dropped": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_ABL=1"],  # timing only: atomics dropped
         "fwd_dma": [*prod, "-DKFATT_FWD_DMA=1"],  # forward K / V by LDS-DMA
-        "fwd_r5q": [*prod, "-DKFATT_FWD_OFFS=0", "-DKFATT_FWD_SCHED=0"],  # the forward as of r5q
-        "fsched4": [*prod, "-DKFATT_FWD_OFFS=0", "-DKFATT_FWD_SCHED=4"],  # LDS reads pipelined 4 ahead
-        "offs": [*prod, "-DKFATT_FWD_SCHED=0"],  # precomputed LDS offsets, buffers unrolled
-        "offs_sched4": [*prod, "-DKFATT_FWD_SCHED=4"],
-        "offs_sched8": [*prod, "-DKFATT_FWD_SCHED=8"],
     }
 
 
