@@ -41,8 +41,12 @@ def main():
     model = gpt.build(args.model, device=dev)
     # native: the framework's multi-tensor AdamW kernel; torch: torch's fused AdamW (separate moments)
     from kubeflow_rm_amd.optim import AdamW
-    opts = {"native": AdamW(model.parameters(), lr=1e-4),
-            "torch": torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)}
+    make_opt = {"native": lambda: AdamW(model.parameters(), lr=1e-4),
+                "torch": lambda: torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)}
+    # every run starts from the same weights with fresh optimizer state, so the two backends' losses
+    # after warmup + steps updates on the same batch are comparable (a convergence check next to the
+    # timing; the copy and the optimizer set-up are outside the timed region)
+    init = [p.detach().clone() for p in model.parameters()]
     g = torch.Generator(device=dev).manual_seed(0)
     V = model.cfg.vocab_size
     idx = torch.randint(0, V, (args.batch, args.seq), generator=g, device=dev)
@@ -59,13 +63,17 @@ def main():
 
     def run(backend, n):
         ctx = ops.torch_reference() if backend == "torch" else _null()
+        with torch.no_grad():
+            for p, p0 in zip(model.parameters(), init):
+                p.copy_(p0)
+        opt = make_opt[backend]()
         with ctx:
             for _ in range(args.warmup):
-                step(opts[backend])
+                step(opt)
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             for _ in range(n):
-                loss = step(opts[backend])
+                loss = step(opt)
             torch.cuda.synchronize(dev)
             return (time.perf_counter() - t0) / n, float(loss.item())
 
