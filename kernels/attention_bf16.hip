@@ -76,6 +76,33 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// Work order (KFATT_LPT). A causal pass's blocks differ in work: query block i of the forward sees
+// i + 1 key tiles, key block i of the backward sees the queries from i on. The hardware deals
+// workgroups to the 8 XCDs round-robin (bid % 8) and each XCD starts its share in bid order, so a
+// head-major order left the heaviest blocks of an XCD's last heads to start when the rest was done
+// (makespan 1.5x the mean at 8 heads x 16 blocks on an XCD's 64 slots). Here XCD x owns heads
+// [x BH/8, (x+1) BH/8) and walks them in groups of G heads, the fewest whose blocks fill its slots:
+// the heaviest rank of every head of the group first (longest-processing-time order), the group's
+// K / V shared in the XCD's L2. rank 0 = the heaviest block. Other head counts: the plain order.
+#ifndef KFATT_LPT
+#define KFATT_LPT 1
+#endif
+struct BlockId {
+  int bh, rank;
+};
+__device__ __forceinline__ BlockId block_order(int bid, int nblk, int BH, int slots) {
+  if (KFATT_LPT && (BH & 7) == 0) {
+    const int hpx = BH >> 3, xcd = bid & 7, i = bid >> 3;
+    int G = 1;
+    while (G < hpx && (G * nblk < slots || hpx % G != 0)) ++G;
+    const int gs = G * nblk, g = i / gs, j = i - g * gs;
+    return {xcd * hpx + g * G + j % G, j / G};
+  }
+  const int nwg = nblk * BH;
+  const int lid = (nwg & 7) == 0 ? xcd_remap(bid, nwg) : bid;
+  return {lid / nblk, lid % nblk};
+}
+
 template <int D>
 __device__ __forceinline__ int swz(int row, int ch) {
   if constexpr (D == 128) {
@@ -230,10 +257,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K, V]
 
   const int nq = (a.T + FQ - 1) / FQ;
-  const int nwg = nq * a.H * a.B;
-  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
-  const int qblk = nq - 1 - (lid % nq);  // heaviest (most keys) first within each head
-  const int bh = lid / nq, h = bh % a.H, b = bh / a.H;
+  const BlockId bo = block_order(blockIdx.x, nq, a.H * a.B, 64);  // 2 workgroups per CU
+  const int qblk = nq - 1 - bo.rank;  // the heaviest (most keys) first
+  const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
@@ -515,10 +541,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
 
   const int T = a.T;
   const int nq = (T + FQ - 1) / FQ;
-  const int nwg = nq * a.H * a.B;
-  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
-  const int qblk = nq - 1 - (lid % nq);  // heaviest first within each head
-  const int bh = lid / nq, h = bh % a.H, b = bh / a.H;
+  const BlockId bo = block_order(blockIdx.x, nq, a.H * a.B, 64);
+  const int qblk = nq - 1 - bo.rank;  // the heaviest first
+  const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
 
@@ -724,10 +749,9 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
 
   const int T = a.T;
   const int nk = (T + BK - 1) / BK;
-  const int nwg = nk * a.H * a.B;
-  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
-  const int kblk = lid % nk;
-  const int bh = lid / nk, h = bh % a.H, b = bh / a.H;
+  const BlockId bo = block_order(blockIdx.x, nk, a.H * a.B, D == 64 ? 64 : 32);
+  const int kblk = bo.rank;  // block 0 (all queries) first
+  const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // 0..7, uniform
   const int w = wv & 3, jh = wv >> 2;                       // key group, query half
@@ -937,10 +961,9 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd(const __bf16* 
 
   const int T = a.T;
   const int nk = (T + BK - 1) / BK;
-  const int nwg = nk * a.H * a.B;
-  const int lid = (nwg & 7) == 0 ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
-  const int kblk = lid % nk;               // block 0 (all queries) first within each head
-  const int bh = lid / nk, h = bh % a.H, b = bh / a.H;
+  const BlockId bo = block_order(blockIdx.x, nk, a.H * a.B, D == 128 ? 32 : 64);
+  const int kblk = bo.rank;  // block 0 (all queries) first
+  const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int k0 = kblk * BK, kw = k0 + 32 * w, key = kw + r;
 

@@ -37,6 +37,7 @@ def _variants():
         "atomics_regstage": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_DMA=0"],  # ... Q / dO register-staged
         "atomics_dropped": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_ABL=1"],  # timing only: atomics dropped
         "fwd_dma": [*prod, "-DKFATT_FWD_DMA=1"],  # forward K / V by LDS-DMA
+        "nolpt": [*prod, "-DKFATT_LPT=0"],  # head-major block order (no longest-first across heads)
     }
 
 
