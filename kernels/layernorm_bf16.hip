@@ -9,6 +9,7 @@
 //  * Backward: dx per row (same wave-per-row structure), dgamma/dbeta by a column-strip
 //    partial-sum kernel + a finalize kernel (deterministic, no float atomics).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include "kfamd_kernels.h"
 #include "wave_ops.h"
@@ -373,6 +374,91 @@ __global__ __launch_bounds__(256) void ln_bwd_dx_block(const __bf16* __restrict_
   }
 }
 
+// ---- backward, fused: dx and the dgamma / dbeta partials in one pass -----------------------------
+// kFusedWaves waves per block walk a contiguous chunk of rows, one row per wave at a time, as
+// ln_bwd_dx_wave does; each lane also keeps its columns' sums of dy * xhat and dy in registers
+// across its rows, so dy and x are read once for all three gradients (the split path reads them a
+// second time in ln_bwd_dgb_partial: 16.9 of 46.8 us per gpt-1b LayerNorm backward,
+// profiles/r5zc_ln_bwd). At the end the block's waves meet in LDS, 64 W columns at a time, summed
+// in wave order (deterministic), and one [2][hidden] partial row per block goes to the workspace for
+// ln_bwd_dgb_finalize. Widths up to 32 columns per lane (hidden <= 2048 at W = 8): the sums take
+// 2 x VPL x W registers beside the row.
+constexpr int kFusedWaves = 8, kFusedBlocks = 256;
+
+template <int VPL, int W>
+__global__ __launch_bounds__(64 * kFusedWaves) void ln_bwd_fused(const __bf16* __restrict__ dy,
+                                                                const __bf16* __restrict__ x,
+                                                                const __bf16* __restrict__ gamma,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const __bf16* __restrict__ dres,
+                                                                __bf16* __restrict__ dx, float* __restrict__ ws,
+                                                                int rows, int rpb) {
+  using vec_t = __bf16 __attribute__((ext_vector_type(W)));
+  constexpr int H = VPL * 64 * W, CW = 64 * W;
+  static_assert(VPL * W <= 32, "ln_bwd_fused: at most 32 columns per lane");
+  __shared__ __attribute__((aligned(16))) float red[kFusedWaves][CW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  const vec_t* g8 = reinterpret_cast<const vec_t*>(gamma);
+  float ag[VPL][W], ab[VPL][W];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int e = 0; e < W; ++e) ag[j][e] = ab[j][e] = 0.f;
+  for (int row = r0 + wv; row < r1; row += kFusedWaves) {
+    const vec_t* xr = reinterpret_cast<const vec_t*>(x + (long long)row * H);
+    const vec_t* dyr = reinterpret_cast<const vec_t*>(dy + (long long)row * H);
+    const float mu = mean[row], rs = rstd[row];
+    float xh[VPL][W], gd[VPL][W];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const vec_t xv = xr[j * 64 + lane], dv = dyr[j * 64 + lane], gv = g8[j * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < W; ++e) {
+        const float d = (float)dv[e];
+        xh[j][e] = ((float)xv[e] - mu) * rs;
+        gd[j][e] = d * (float)gv[e];
+        s1 += gd[j][e] * xh[j][e];
+        s2 += gd[j][e];
+        ag[j][e] = fmaf(d, xh[j][e], ag[j][e]);
+        ab[j][e] += d;
+      }
+    }
+    const float c1 = wave_sum(s1) * (1.f / H), c2 = wave_sum(s2) * (1.f / H);
+    vec_t* dxr = reinterpret_cast<vec_t*>(dx + (long long)row * H);
+    const vec_t* rr = dres ? reinterpret_cast<const vec_t*>(dres + (long long)row * H) : nullptr;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      vec_t rv = {};
+      if (rr) rv = rr[j * 64 + lane];
+      vec_t o;
+#pragma unroll
+      for (int e = 0; e < W; ++e) o[e] = (__bf16)(fmaf(rs, gd[j][e] - xh[j][e] * c1 - c2, (float)rv[e]));
+      dxr[j * 64 + lane] = o;
+    }
+  }
+  float* og = ws + (long long)blockIdx.x * H;
+  float* ob = ws + ((long long)gridDim.x + blockIdx.x) * H;
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+#pragma unroll
+      for (int e = 0; e < W; ++e) red[wv][lane * W + e] = which ? ab[j][e] : ag[j][e];
+      __syncthreads();
+      for (int c = threadIdx.x; c < CW; c += 64 * kFusedWaves) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kFusedWaves; ++w) t += red[w][c];
+        (which ? ob : og)[j * CW + c] = t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---- backward: dgamma / dbeta partials over row chunks ---------------------------------------
 // Block: 64 column lanes x 4 row lanes; each column lane owns one column of the strip, so a
 // wave reads 64 consecutive bf16 (128 B) of one row per step; partials land in ws[chunk][col].
@@ -555,7 +641,7 @@ extern "C" int kfamd_rmsnorm_fwd_bf16(const void* x, const void* gamma, void* y,
 
 extern "C" long long kfamd_layernorm_bwd_workspace(int rows, int hidden) {
   const long long nch = (rows + kRowsPerChunk - 1) / kRowsPerChunk;
-  return 2LL * nch * hidden * (long long)sizeof(float);
+  return 2LL * (nch > kFusedBlocks ? nch : kFusedBlocks) * hidden * (long long)sizeof(float);
 }
 
 // dgamma / dbeta: fp32, or bf16 (the parameter dtype) when dgb_bf16; sums accumulate in fp32 either way.
@@ -575,6 +661,32 @@ extern "C" int kfamd_layernorm_bwd_bf16_v3(const void* dy, const void* dres, con
   const __bf16* rp = static_cast<const __bf16*>(dres);
   const int vpl = vpl_for(hidden);
   const bool vec = vpl && a16(dy) && a16(x) && a16(gamma) && a16(dx) && (!dres || a16(dres));
+  const int v4 = vec ? 0 : vpl4_for(hidden);
+  const bool vec4 = v4 && a8(dy) && a8(x) && a8(gamma) && a8(dx) && (!dres || a8(dres));
+  // dx + dgamma / dbeta in one pass (ln_bwd_fused) where the sums fit beside the row: hidden <= 2048
+  // (W = 8) or 256 x {1, 3, 5} (W = 4); KFAMD_LN_BWD_SPLIT=1 forces the split path (A/B runs)
+  static const bool force_split = [] { const char* e = getenv("KFAMD_LN_BWD_SPLIT"); return e && *e == '1'; }();
+  const bool fused = (dgamma || dbeta) && !force_split && ((vec && vpl <= 4) || vec4);
+  if (fused) {
+    int nblk = (rows + kFusedWaves - 1) / kFusedWaves;
+    if (nblk > kFusedBlocks) nblk = kFusedBlocks;
+    const int rpb = (rows + nblk - 1) / nblk;
+    nblk = (rows + rpb - 1) / rpb;
+    const dim3 grid(nblk), block(64 * kFusedWaves);
+    const int key = vec ? vpl : 100 + v4;
+    switch (key) {
+#define KFAMD_LN_FUSED(K, V, WW) \
+  case K: hipLaunchKernelGGL((ln_bwd_fused<V, WW>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, workspace, rows, rpb); break;
+      KFAMD_LN_FUSED(1, 1, 8) KFAMD_LN_FUSED(2, 2, 8) KFAMD_LN_FUSED(3, 3, 8) KFAMD_LN_FUSED(4, 4, 8)
+      KFAMD_LN_FUSED(101, 1, 4) KFAMD_LN_FUSED(103, 3, 4) KFAMD_LN_FUSED(105, 5, 4)
+#undef KFAMD_LN_FUSED
+    }
+    const dim3 fg((hidden + kColsPerBlock - 1) / kColsPerBlock);
+    if (dgb_bf16) hipLaunchKernelGGL(ln_bwd_dgb_finalize<true>, fg, dim3(256), 0, s, workspace, dgamma, dbeta, nblk, hidden);
+    else hipLaunchKernelGGL(ln_bwd_dgb_finalize<false>, fg, dim3(256), 0, s, workspace, dgamma, dbeta, nblk, hidden);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+  }
   if (vec) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (vpl) {
@@ -583,7 +695,7 @@ extern "C" int kfamd_layernorm_bwd_bf16_v3(const void* dy, const void* dres, con
       KFAMD_FOR_EACH_VPL(KFAMD_LN_BWD_CASE)
 #undef KFAMD_LN_BWD_CASE
     }
-  } else if (const int v4 = vpl4_for(hidden); v4 && a8(dy) && a8(x) && a8(gamma) && a8(dx) && (!dres || a8(dres))) {
+  } else if (vec4) {
     dim3 grid((rows + 3) / 4), block(256);
     switch (v4) {
       case 1: hipLaunchKernelGGL((ln_bwd_dx_wave<1, 4>), grid, block, 0, s, dyp, xp, gp, mean, rstd, rp, dxp, rows); break;

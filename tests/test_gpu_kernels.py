@@ -146,6 +146,27 @@ def test_layernorm_fwd_bwd(rows, H):
     assert (b.grad.float() - br.grad).abs().max().item() < 2e-2 * (br.grad.abs().max().item() + 1)
 
 
+@pytest.mark.parametrize("rows,H", [(8192, 2048), (3001, 2048), (5000, 1024), (777, 768), (2049, 1536), (300, 1280)])
+def test_layernorm_backward_fused_with_residual(rows, H):
+    """The one-pass backward (layernorm_bf16.hip ln_bwd_fused: dx, the residual gradient folded into
+    its store, and the dgamma / dbeta partials from the same reads) at model widths and row counts
+    that give every wave several rows and the last block a short chunk; vs fp32 autograd."""
+    from kubeflow_rm_amd.ops import layernorm as LN
+    x = (_rand(rows, H, seed=61, scale=2.0).float() + 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = _rand(H, seed=62).requires_grad_(True)
+    b = _rand(H, seed=63).requires_grad_(True)
+    y, r = LN.layer_norm_residual(x, w, b, 1e-5)
+    gy, gr = _rand(rows, H, seed=64), _rand(rows, H, seed=65)
+    torch.autograd.backward((y, r), (gy, gr))
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+    torch.autograd.backward((yr, xr * 1.0), (gy.float(), gr.float()))
+    assert (x.grad.float() - xr.grad).abs().max().item() < 5e-2 * (xr.grad.abs().max().item() + 1)
+    # dgamma / dbeta sum `rows` products: bf16 output rounding on values of size ~sqrt(rows)
+    assert (w.grad.float() - wr.grad).abs().max().item() < 1e-2 * (wr.grad.abs().max().item() + 1)
+    assert (b.grad.float() - br.grad).abs().max().item() < 1e-2 * (br.grad.abs().max().item() + 1)
+
+
 @pytest.mark.parametrize("rows,H,rms", [(6001, 4096, False), (8192, 4096, False), (12289, 1024, False),
                                         (6001, 4096, True), (8192, 8192, False), (37, 8192, False),
                                         (4099, 8192, True), (20000, 8192, False), (32768, 512, False)])
