@@ -189,6 +189,15 @@ extern "C" int kfamd_act_grad_bf16_v2(const void* dy, const void* z, void* g, vo
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
 
+extern "C" int kfamd_colsum_finalize(const float* ws, void* db, int db_bf16, int nblk, int cols, void* stream) {
+  if (!ws || !db || nblk <= 0 || cols <= 0) return KFAMD_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (db_bf16) hipLaunchKernelGGL(colsum_finalize<true>, dim3((cols + 63) / 64), dim3(256), 0, s, ws, db, nblk, cols);
+  else hipLaunchKernelGGL(colsum_finalize<false>, dim3((cols + 63) / 64), dim3(256), 0, s, ws, db, nblk, cols);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
+}
+
 extern "C" int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float* workspace, int rows,
                                    int cols, int act, void* stream) {
   return kfamd_act_grad_bf16_v2(dy, z, g, db, 0, workspace, rows, cols, act, stream);

@@ -73,6 +73,52 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   }
 }
 
+// act'(z) for the DACT epilogue (the backward of act at the pre-activation z; relu takes z too)
+__device__ __forceinline__ float dact_fn(float z, int act) {
+  switch (act) {
+    case KFAMD_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case KFAMD_ACT_GELU_TANH: {
+      // gelu_tanh(z) = z s(2u), u = c (z + 0.044715 z^3): d/dz = s + z s (1 - s) 2u'
+      const float z2 = z * z;
+      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-1.5957691216057308f * (z + 0.044715f * z2 * z)));
+      return sg + z * sg * (1.f - sg) * 1.5957691216057308f * (1.f + 3.f * 0.044715f * z2);
+    }
+    case KFAMD_ACT_SILU: {
+      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-z));
+      return sg * (1.f + z * (1.f - sg));
+    }
+    default: return 1.f;
+  }
+}
+
+// act'(z) on a pair of values: the polynomial parts as packed f32 ops (v_pk_mul / v_pk_fma: two
+// lanes' worth per instruction), the exp / rcp per value. gelu_tanh with 2u = z (A + B z^2):
+// act' = s (1 + z (1 - s) (A + 3 B z^2)), s = sigmoid(2u), log2(e) folded into exp's argument.
+typedef float kf32x2 __attribute__((ext_vector_type(2)));
+template <int ACT>
+__device__ __forceinline__ kf32x2 dact2(kf32x2 z) {
+  if constexpr (ACT == KFAMD_ACT_RELU) {
+    return kf32x2{z.x > 0.f ? 1.f : 0.f, z.y > 0.f ? 1.f : 0.f};
+  } else if constexpr (ACT == KFAMD_ACT_GELU_TANH) {
+    constexpr float A = 1.5957691216057308f, B = 1.5957691216057308f * 0.044715f, L2E = 1.4426950408889634f;
+    const kf32x2 z2 = z * z;
+    const kf32x2 q = z * __builtin_elementwise_fma(z2, kf32x2{-B * L2E, -B * L2E}, kf32x2{-A * L2E, -A * L2E});
+    const kf32x2 s{__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(q.x)),
+                   __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(q.y))};
+    const kf32x2 r = __builtin_elementwise_fma(z2, kf32x2{3.f * B, 3.f * B}, kf32x2{A, A});
+    const kf32x2 w = __builtin_elementwise_fma((kf32x2{1.f, 1.f} - s) * z, r, kf32x2{1.f, 1.f});
+    return s * w;
+  } else if constexpr (ACT == KFAMD_ACT_SILU) {
+    constexpr float L2E = 1.4426950408889634f;
+    const kf32x2 q = z * kf32x2{-L2E, -L2E};
+    const kf32x2 s{__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(q.x)),
+                   __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(q.y))};
+    return s * __builtin_elementwise_fma((kf32x2{1.f, 1.f} - s), z, kf32x2{1.f, 1.f});
+  } else {
+    return kf32x2{1.f, 1.f};
+  }
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -220,8 +266,14 @@ struct Reader {
 // released with an agent-scope flag = epoch) and runs the epilogue; a partial that does not arrive
 // within the deadline is recomputed by the owner itself, so a non-co-resident grid is slow, never
 // hung or wrong.
+// DACT (a linear layer's backward through its activation, gemm_bf16_w4_t.hip kfamd_w4_dgrad_act):
+// C = (A·B) * act'(R), R = the pre-activation the forward stored, and when W is given the column
+// sums of the bf16 C per 128-row slab (W[M / 128][N], the next layer's bias-gradient partials):
+// the elementwise act-grad pass (act_grad_bf16.hip) folded into the dgrad GEMM's epilogue, which
+// reads R where that pass read both dY and R and wrote G. Whole interior tiles only (the host
+// requires M and N multiples of 256 and 16-B rows), on the full-line residual epilogue.
 template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, int SPLIT = 0,
-          bool DIAG = false, int ABL = 0, bool SK = false, bool PO = false>
+          bool DIAG = false, int ABL = 0, bool SK = false, bool PO = false, bool DACT = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
@@ -263,6 +315,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(SPLIT != 2 || BM == 256, "split-K fixup: 256 tile");
   static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
   static_assert(!PO || (BM == 256 && !SPLIT && !SK && !DIAG), "persistent overlapped: 256 tile, whole K");
+  static_assert(!DACT || (HAS_RES && !HAS_BIAS && !HAS_AUX && ACT != KFAMD_ACT_NONE && BM == 256 && !SPLIT && !SK && !PO),
+                "act-grad epilogue: the pre-activation as R, 256 tile, whole K");
   // PO: the epilogue's LDS staging lives in the ring's fifth slot, which the next tile's prologue
   // (tiles 0 and 1 into slots 0-3) leaves alone, so that prologue can be issued before the epilogue
   constexpr int kEpiBase = PO ? (kSlots - 1) * TILE : 0;
@@ -896,7 +950,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += (float)bb[r];
     }
-    if (ACT != KFAMD_ACT_NONE) {
+    if (ACT != KFAMD_ACT_NONE && !DACT) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
     }
@@ -908,30 +962,102 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     const int rr = elane >> 3, rc = elane & 7;
     const int ra0 = rr * 256 + 16 * ((2 * rc) ^ rr), ra1 = rr * 256 + 16 * ((2 * rc + 1) ^ rr);
     const int rb0 = (rr + 8) * 256 + 16 * ((2 * rc) ^ (rr + 8)), rb1 = (rr + 8) * 256 + 16 * ((2 * rc + 1) ^ (rr + 8));
+    // DACT: this lane's column sums (rows rr and rr + 8 of every fragment row), 8 columns per span
+    float csum[DACT ? NR / 4 : 1][8];
+#pragma unroll
+    for (int h = 0; h < (DACT ? NR / 4 : 1); ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) csum[h][e] = 0.f;
+    // R (residual / pre-activation) rows of span sp = (fragment row i, 64-column half n / 4), issued
+    // KFW4_RES_PD spans ahead of their use: one span's loads per use left the HBM latency exposed
+    // once per span, 16 times per wave and tile (profiles/r5zg_dact2)
+#ifndef KFW4_RES_PD
+#define KFW4_RES_PD 2
+#endif
+    constexpr int SPW = NR / 4, NS = NR * SPW, PD = KFW4_RES_PD;
+    bf16x8 rbuf[PD + 1][2];
+    auto rload = [&](int sp) __attribute__((always_inline)) {
+      const int i = sp / SPW, n = (sp % SPW) * 4;
+      const __bf16* rrow = R + ((long long)(m0 + wm * WT + i * 16 + rr) * ldr + n0 + wn * WT + rc * 8);
+      rbuf[sp % (PD + 1)][0] = *reinterpret_cast<const bf16x8*>(rrow + n * 16);
+      rbuf[sp % (PD + 1)][1] = *reinterpret_cast<const bf16x8*>(rrow + 8 * ldr + n * 16);
+    };
+#pragma unroll
+    for (int sp = 0; sp < PD && sp < NS; ++sp) rload(sp);
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const long long row = m0 + wm * WT + i * 16 + rr;
       __bf16* xrow = C + (row * ldc + n0 + wn * WT + rc * 8);
-      const __bf16* rrow = R + (row * ldr + n0 + wn * WT + rc * 8);
 #pragma unroll
       for (int n = 0; n < NR; n += 4) {
-        const bf16x8 RX = *reinterpret_cast<const bf16x8*>(rrow + n * 16);
-        const bf16x8 RY = *reinterpret_cast<const bf16x8*>(rrow + 8 * ldr + n * 16);
+        const int sp = i * SPW + n / 4;
+        if (sp + PD < NS) rload(sp + PD);
+        const bf16x8 RX = rbuf[sp % (PD + 1)][0];
+        const bf16x8 RY = rbuf[sp % (PD + 1)][1];
 #pragma unroll
         for (int nn = 0; nn < 4; ++nn)
           *reinterpret_cast<f32x4*>(stage + elr * 256 + 16 * ((4 * nn + elh) ^ elr)) = pre_res(UNIT, i, n + nn);
         const f32x4 xa = *reinterpret_cast<const f32x4*>(stage + ra0), xb = *reinterpret_cast<const f32x4*>(stage + ra1);
         const f32x4 ya = *reinterpret_cast<const f32x4*>(stage + rb0), yb = *reinterpret_cast<const f32x4*>(stage + rb1);
         bf16x8 X, Y;
+        if constexpr (DACT) {
+          // pairs: the packed-f32 act' (dact2), the product, one v_cvt_pk_bf16_f32 per pair; the
+          // column sums add the fp32 products (the act-grad pass summed the bf16-rounded ones)
+          typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+          float* cs = csum[n / 4];
+          auto pair = [&](int e, float x0, float x1, float y0, float y1) __attribute__((always_inline)) {
+            const kf32x2 gx = kf32x2{x0, x1} * dact2<ACT>(kf32x2{(float)RX[e], (float)RX[e + 1]});
+            const kf32x2 gy = kf32x2{y0, y1} * dact2<ACT>(kf32x2{(float)RY[e], (float)RY[e + 1]});
+            const bf16x2_t bx = __builtin_convertvector(gx, bf16x2_t), by = __builtin_convertvector(gy, bf16x2_t);
+            X[e] = bx[0];
+            X[e + 1] = bx[1];
+            Y[e] = by[0];
+            Y[e + 1] = by[1];
+            const kf32x2 c2 = kf32x2{cs[e], cs[e + 1]} + gx + gy;
+            cs[e] = c2.x;
+            cs[e + 1] = c2.y;
+          };
+          pair(0, xa[0], xa[1], ya[0], ya[1]);
+          pair(2, xa[2], xa[3], ya[2], ya[3]);
+          pair(4, xb[0], xb[1], yb[0], yb[1]);
+          pair(6, xb[2], xb[3], yb[2], yb[3]);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          X[r] = (__bf16)(xa[r] + (float)RX[r]);
-          X[4 + r] = (__bf16)(xb[r] + (float)RX[4 + r]);
-          Y[r] = (__bf16)(ya[r] + (float)RY[r]);
-          Y[4 + r] = (__bf16)(yb[r] + (float)RY[4 + r]);
+          for (int r = 0; r < 4; ++r) {
+            X[r] = (__bf16)(xa[r] + (float)RX[r]);
+            X[4 + r] = (__bf16)(xb[r] + (float)RX[4 + r]);
+            Y[r] = (__bf16)(ya[r] + (float)RY[r]);
+            Y[4 + r] = (__bf16)(yb[r] + (float)RY[4 + r]);
+          }
         }
         *reinterpret_cast<bf16x8*>(xrow + n * 16) = X;
         *reinterpret_cast<bf16x8*>(xrow + 8 * ldc + n * 16) = Y;
+      }
+    }
+    if constexpr (DACT) {
+      if (W != nullptr) {
+        // sum over the 8 lanes of one column run (lane bits 3-5: row_ror:8 within a row, then the
+        // row pairs and halves by v_permlane16 / 32 swaps); lanes 0-7 store the slab's partials
+#pragma unroll
+        for (int h = 0; h < NR / 4; ++h) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float v = csum[h][e];
+            v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+            auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            v = __uint_as_float(s16[0]) + __uint_as_float(s16[1]);
+            auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            csum[h][e] = __uint_as_float(s32[0]) + __uint_as_float(s32[1]);
+          }
+        }
+        if (rr == 0) {
+          float* wrow = W + ((long long)(m0 / 128) + wm) * N + n0 + wn * WT + rc * 8;
+#pragma unroll
+          for (int h = 0; h < NR / 4; ++h) {
+            *reinterpret_cast<f32x4*>(wrow + 64 * h) = f32x4{csum[h][0], csum[h][1], csum[h][2], csum[h][3]};
+            *reinterpret_cast<f32x4*>(wrow + 64 * h + 4) = f32x4{csum[h][4], csum[h][5], csum[h][6], csum[h][7]};
+          }
+        }
       }
     }
   };
@@ -942,7 +1068,10 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #endif
   // uniform branches: interior tiles store unmasked straight-line 16-B stores, shifted edge tiles
   // mask per lane, an odd output takes the og path; only the path that runs is fetched
-  if (og == 8 && vec_in) {
+  if constexpr (DACT) {  // interior tiles only (host contract): one path
+    if (alpha == 1.f) emit_fullline_res(T{});
+    else emit_fullline_res(F{});
+  } else if (og == 8 && vec_in) {
     if (m0 == m_lo && n0 == n_lo) {
       if constexpr (KFW4_FULLLINE && HAS_RES && !HAS_AUX && !SK) {  // (the stream-K owner adds partials in finish())
         if (res16) {

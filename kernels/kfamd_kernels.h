@@ -117,6 +117,17 @@ int kfamd_act_grad_bf16(const void* dy, const void* z, void* g, float* db, float
 // the same with db written as bf16 when db_bf16 (fp32 accumulation)
 int kfamd_act_grad_bf16_v2(const void* dy, const void* z, void* g, void* db, int db_bf16, float* workspace, int rows,
                            int cols, int act, void* stream);
+// db[c] = sum over b < nblk of ws[b][c] (fp32 partials; db fp32, or bf16 when db_bf16)
+int kfamd_colsum_finalize(const float* ws, void* db, int db_bf16, int nblk, int cols, void* stream);
+// A linear layer's dgrad through the previous layer's activation, one GEMM (gemm_w4.h DACT):
+// G[M][N] = (dY[M][K] . W[K][N]) * act'(Z[M][N]) (dY K-contiguous with row stride lda, W row-major
+// [K][N] with row stride ldb, Z / G row strides ldz / ldg), and when db is given the column sums of G
+// (the previous layer's bias gradient; ws: kfamd_w4_dgrad_act_workspace bytes). M, N multiples of
+// 256, K of 64, 16-B rows; KFAMD_EINVAL otherwise (callers fall back to the GEMM + act-grad pass).
+long long kfamd_w4_dgrad_act_workspace(int M, int N);
+int kfamd_w4_dgrad_act(const void* dy, const void* w, void* g, const void* z, int M, int N, int K, long long lda,
+                       long long ldb, long long ldg, long long ldz, int act, float* ws, void* db, int db_bf16,
+                       void* stream);
 
 // LayerNorm forward over the last dim (hidden). x,y: [rows][hidden] bf16 (row stride = hidden).
 // gamma/beta: [hidden] bf16 (beta may be null). mean/rstd: optional fp32 [rows] (saved for bwd).

@@ -128,13 +128,21 @@ class Block(torch.nn.Module):
         y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
         return self.proj(y.transpose(1, 2).reshape(B, T, h * hd), residual=residual)
 
+    def mlp(self, h, residual):
+        # without TP, fc1 + fc2 are one autograd node on the HIP path (ops.mlp): fc2's dgrad applies
+        # fc1's gelu backward in its GEMM epilogue
+        if h.is_cuda and ops.native_enabled() and tpl._world(self.tp_group) == 1:
+            return ops.mlp(h, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, act=self.fc1.act,
+                           residual=residual)
+        return self.fc2(self.fc1(h), residual=residual)
+
     def forward(self, x):
         # both residual adds ride in the output projections' GEMM epilogues (without TP); the
         # residual gradient joins the LayerNorm backward's dx store (LayerNorm.with_residual)
         h, r = self.ln1.with_residual(x)
         x = self.attention(h, residual=r)
         h, r = self.ln2.with_residual(x)
-        return self.fc2(self.fc1(h), residual=r)
+        return self.mlp(h, r)
 
 
 class GPT(torch.nn.Module):

@@ -7,6 +7,8 @@ replacement used by :mod:`kubeflow_rm_amd.models` and the TP layers.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -570,6 +572,99 @@ class _Linear(torch.autograd.Function):
         # y = ... + residual: the residual's gradient is gy itself
         gr = gy if ctx.needs_input_grad[4] else None
         return gx, gw, gb, None, gr
+
+
+# An MLP's fc2 dgrad and fc1's activation backward (+ fc1's bias-gradient partials) in one GEMM
+# (gemm_w4.h DACT, kernels/tu/w4_dgrad_act.hip) instead of the GEMM, then act_grad's pass over its
+# output and the pre-activation. False: the two-step form (A/B runs, profiles/r5ze_mlp).
+FUSED_DGRAD_ACT = os.environ.get("KFAMD_FUSED_DGRAD_ACT", "1") != "0"
+
+
+def dgrad_act(gy2: torch.Tensor, weight: torch.Tensor, z: torch.Tensor, act: str, need_bias_grad: bool,
+              db_dtype: torch.dtype = torch.float32):
+    """(g, db): g = (gy2 @ weight) * act'(z) — the gradient at the pre-activation z of the layer
+    feeding ``weight``'s layer — and db = column sums of g, from one GEMM whose epilogue reads z; or
+    None when the shape is outside that kernel's contract (M, N multiples of 256, K of 64, 16-B
+    rows), and the caller takes ``mm`` + ``act_grad``."""
+    if not FUSED_DGRAD_ACT or act not in ACTS or act == "none":
+        return None
+    M, K = gy2.shape
+    N = weight.shape[1]
+    if (weight.dim() != 2 or weight.shape[0] != K or tuple(z.shape) != (M, N) or gy2.dtype != torch.bfloat16
+            or weight.dtype != torch.bfloat16 or z.dtype != torch.bfloat16
+            or not (gy2.is_contiguous() and weight.is_contiguous() and z.is_contiguous())):
+        return None
+    L = _lib.lib()
+    g = torch.empty(M, N, dtype=torch.bfloat16, device=gy2.device)
+    db = ws = None
+    db_bf16 = db_dtype == torch.bfloat16
+    if need_bias_grad:
+        db = torch.empty(N, dtype=torch.bfloat16 if db_bf16 else torch.float32, device=gy2.device)
+        ws = torch.empty(L.kfamd_w4_dgrad_act_workspace(M, N) // 4, dtype=torch.float32, device=gy2.device)
+    rc = L.kfamd_w4_dgrad_act(gy2.data_ptr(), weight.data_ptr(), g.data_ptr(), z.data_ptr(), M, N, K, K, N, N, N,
+                              ACTS[act], ws.data_ptr() if ws is not None else None,
+                              db.data_ptr() if db is not None else None, int(db_bf16), _stream_ptr(gy2))
+    if rc < 0:
+        return None
+    _lib.check(rc, f"dgrad_act[{M}x{N}x{K}]")
+    return g, db
+
+
+class _MLP(torch.autograd.Function):
+    """out = act(x W1^T + b1) W2^T + b2 (+ residual) as one autograd node, so that fc2's dgrad can
+    apply fc1's activation backward in its epilogue (dgrad_act): the backward runs fc2's bias and
+    weight gradients, ONE GEMM for dH * act'(z1) (+ fc1's bias-gradient partials), then fc1's dgrad
+    and wgrad. The forward is the two linears' (gemm_nt_preact, gemm_nt with bias / residual)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, act, residual):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        y1, z1 = gemm_nt_preact(x2, w1, b1, act)
+        res = residual.reshape(-1, w2.shape[0]).contiguous() if residual is not None else None
+        out = gemm_nt(y1, w2, bias=b2, residual=res)
+        ctx.save_for_backward(x2, w1, b1, w2, b2, y1, z1)
+        ctx.act = act
+        ctx.xshape = x.shape
+        return out.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w1, b1, w2, b2, y1, z1 = ctx.saved_tensors
+        gy2 = gy.reshape(-1, w2.shape[0])
+        if not gy2.is_contiguous():
+            gy2 = gy2.contiguous()
+        ni = ctx.needs_input_grad
+        need_db2 = b2 is not None and ni[4]
+        need_db1 = b1 is not None and ni[2]
+        _, db2 = act_grad(gy2, None, "none", need_db2,
+                          db_dtype=torch.bfloat16 if need_db2 and b2.dtype == torch.bfloat16 else torch.float32)
+        gw2 = mm(gy2, y1, trans_a=True) if ni[3] else None
+        db1_dtype = torch.bfloat16 if need_db1 and b1.dtype == torch.bfloat16 else torch.float32
+        fused = dgrad_act(gy2, w2, z1, ctx.act, need_db1, db1_dtype)
+        if fused is None:
+            g1, db1 = act_grad(mm(gy2, w2), z1, ctx.act, need_db1, db_dtype=db1_dtype)
+        else:
+            g1, db1 = fused
+        gx = mm(g1, w1).reshape(ctx.xshape) if ni[0] else None
+        gw1 = mm(g1, x2, trans_a=True) if ni[1] else None
+        gb1 = db1.to(b1.dtype) if need_db1 else None
+        gb2 = db2.to(b2.dtype) if need_db2 else None
+        return gx, gw1, gb1, gw2, gb2, None, (gy if ni[6] else None)
+
+
+def mlp(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor | None, w2: torch.Tensor, b2: torch.Tensor | None,
+        act: str = "gelu_tanh", residual: torch.Tensor | None = None) -> torch.Tensor:
+    """Autograd-aware ``F.linear(act(F.linear(x, w1, b1)), w2, b2) (+ residual)`` (act: gelu_tanh,
+    silu or relu) on the MFMA kernels, fc2's dgrad fused with fc1's activation backward."""
+    if act not in ("gelu", "gelu_tanh", "silu", "relu"):
+        raise ValueError(f"mlp: unsupported activation {act!r}")
+    if act == "relu":
+        # relu's backward reads the activation output; the pre-activation form covers gelu / silu
+        return linear(linear(x, w1, b1, act="relu"), w2, b2, residual=residual)
+    return _MLP.apply(x, w1, b1, w2, b2, act, residual)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,

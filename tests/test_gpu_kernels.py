@@ -697,3 +697,79 @@ def test_split_heads_backward_packs_qkv_grad(B, T, h, hd):
     assert torch.equal(gq[:, :, 0], torch.ones_like(gq[:, :, 0]))
     assert torch.equal(gq[:, :, 1], torch.full_like(gq[:, :, 1], 2))
     assert not gq[:, :, 2].any()
+
+
+def _dact_ref(z, act):
+    zf = z.float().requires_grad_(True)
+    F = torch.nn.functional
+    if act == "relu":
+        y = F.relu(zf)
+    elif act == "silu":
+        y = F.silu(zf)
+    else:
+        y = F.gelu(zf, approximate="tanh")
+    (d,) = torch.autograd.grad(y.sum(), zf)
+    return d
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "silu", "relu"])
+@pytest.mark.parametrize("M,K,N", [(512, 256, 768), (256, 2048, 1024), (1024, 512, 256)])
+def test_dgrad_act_matches_fp32(act, M, K, N):
+    """The act-grad GEMM epilogue (gemm_w4.h DACT): g = (gy @ W) * act'(z) against fp32, and the
+    bias-gradient column sums (fp32 sums of the unrounded products) against the sums of the
+    kernel's own bf16 g."""
+    from kubeflow_rm_amd import ops
+    gy, w = _rand(M, K, seed=71), _rand(K, N, seed=72, scale=0.05)
+    z = _rand(M, N, seed=73, scale=2.0)
+    out = ops.dgrad_act(gy, w, z, act, True, torch.float32)
+    assert out is not None, "the fused kernel refused a 256-multiple shape"
+    g, db = out
+    ref = (gy.float() @ w.float()) * _dact_ref(z, act)
+    err = (g.float() - ref).abs().max().item()
+    assert err <= 2e-2 * (ref.abs().max().item() + 1e-3), err
+    # the kernel sums the fp32 products before their bf16 rounding: within the rounding of g
+    col = g.float().sum(0)
+    assert (db - col).abs().max().item() <= 1e-3 * g.float().abs().sum(0).max().item() + 1e-3
+    # bf16 bias gradient, no bias gradient
+    g2, db2 = ops.dgrad_act(gy, w, z, act, True, torch.bfloat16)
+    assert db2.dtype == torch.bfloat16 and torch.equal(g2, g)
+    g3, db3 = ops.dgrad_act(gy, w, z, act, False)
+    assert db3 is None and torch.equal(g3, g)
+
+
+def test_dgrad_act_refuses_odd_shapes():
+    from kubeflow_rm_amd import ops
+    gy, w, z = _rand(300, 256, seed=74), _rand(256, 512, seed=75), _rand(300, 512, seed=76)
+    assert ops.dgrad_act(gy, w, z, "gelu_tanh", True) is None
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("act", ["gelu_tanh", "silu"])
+def test_mlp_matches_fp32(fused, act):
+    """ops.mlp (fc1 + act + fc2 + residual as one autograd node) forward and every gradient vs fp32
+    autograd, with fc2's dgrad fused with the activation backward (default) and in two steps."""
+    from kubeflow_rm_amd import ops
+    from kubeflow_rm_amd.ops import gemm as G
+    B, T, D, Fd = 2, 256, 512, 1024
+    x = _rand(B, T, D, seed=81).requires_grad_(True)
+    w1, b1 = _rand(Fd, D, seed=82, scale=0.05).requires_grad_(True), _rand(Fd, seed=83).requires_grad_(True)
+    w2, b2 = _rand(D, Fd, seed=84, scale=0.05).requires_grad_(True), _rand(D, seed=85).requires_grad_(True)
+    r = _rand(B, T, D, seed=86).requires_grad_(True)
+    gy = _rand(B, T, D, seed=87)
+    old = G.FUSED_DGRAD_ACT
+    G.FUSED_DGRAD_ACT = fused
+    try:
+        y = ops.mlp(x, w1, b1, w2, b2, act=act, residual=r)
+        y.backward(gy)
+    finally:
+        G.FUSED_DGRAD_ACT = old
+    ts = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2, b2, r)]
+    F = torch.nn.functional
+    h = F.linear(ts[0], ts[1], ts[2])
+    h = F.gelu(h, approximate="tanh") if act == "gelu_tanh" else F.silu(h)
+    yr = F.linear(h, ts[3], ts[4]) + ts[5]
+    yr.backward(gy.float())
+    assert (y.float() - yr).abs().max().item() < 3e-2 * (yr.abs().max().item() + 1)
+    for got, ref in zip((x.grad, w1.grad, b1.grad, w2.grad, b2.grad, r.grad), (t.grad for t in ts)):
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 3e-2 * (ref.abs().max().item() + 1e-3) + 1e-2, err
