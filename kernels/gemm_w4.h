@@ -266,6 +266,19 @@ struct Reader {
 // released with an agent-scope flag = epoch) and runs the epilogue; a partial that does not arrive
 // within the deadline is recomputed by the owner itself, so a non-co-resident grid is slow, never
 // hung or wrong.
+// GRP: a second problem in the same launch (W4Grp: its own A, B, C, M, N and leading dimensions; the
+// same K, layouts and epilogue): blocks [0, tiles of problem 1) take problem 1, the rest problem 2,
+// after the XCD remap over both. For two GEMMs that under-fill the chip alone, e.g. a transformer
+// block's QKV and output-projection weight gradients (192 + 64 tiles of 256 x 256 at gpt-1b:
+// one full wave of 256 CUs together; kfamd_w4_wgrad_pair, gemm_bf16_w4_t.hip).
+struct W4Grp {
+  const __bf16* A;
+  const __bf16* B;
+  __bf16* C;
+  int M, N;
+  long long lda, ldb, ldc;
+};
+
 // DACT (a linear layer's backward through its activation, gemm_bf16_w4_t.hip kfamd_w4_dgrad_act):
 // C = (A·B) * act'(R), R = the pre-activation the forward stored, and when W is given the column
 // sums of the bf16 C per 128-row slab (W[M / 128][N], the next layer's bias-gradient partials):
@@ -273,7 +286,7 @@ struct Reader {
 // reads R where that pass read both dY and R and wrote G. Whole interior tiles only (the host
 // requires M and N multiples of 256 and 16-B rows), on the full-line residual epilogue.
 template <int ACT, bool HAS_BIAS, bool HAS_RES, bool HAS_AUX, int LA, int LB, int BM, int SPLIT = 0,
-          bool DIAG = false, int ABL = 0, bool SK = false, bool PO = false, bool DACT = false>
+          bool DIAG = false, int ABL = 0, bool SK = false, bool PO = false, bool DACT = false, bool GRP = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kThreads, kThreads),
                           amdgpu_waves_per_eu(BM == 256 ? 1 : 2, BM == 256 ? 1 : 2)))
 void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
@@ -281,7 +294,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
              int K, long long lda, long long ldb, long long ldc, long long ldr, long long sa, long long sb,
              long long sc, long long sr, float alpha, unsigned long long* __restrict__ diag,
              float* __restrict__ W = nullptr, int kper = 0, unsigned* __restrict__ sk_flags = nullptr,
-             unsigned sk_epoch = 0) {
+             unsigned sk_epoch = 0, W4Grp g2 = W4Grp{}) {
   constexpr int BN = BM, WT = BM / 2, NR = WT / 16;    // wave tile WT x WT = NR x NR MFMA blocks
   constexpr int TILE = BM * kBK * 2;                   // bytes per operand tile
   constexpr int PIECES = BM / 32;                      // 1 KiB DMA pieces per wave per operand tile
@@ -315,6 +328,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(SPLIT != 2 || BM == 256, "split-K fixup: 256 tile");
   static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
   static_assert(!PO || (BM == 256 && !SPLIT && !SK && !DIAG), "persistent overlapped: 256 tile, whole K");
+  static_assert(!GRP || (!SPLIT && !SK && !PO && !DACT && !HAS_BIAS && !HAS_RES && !HAS_AUX && !DIAG),
+                "grouped pair: plain epilogue, one tile per block");
   static_assert(!DACT || (HAS_RES && !HAS_BIAS && !HAS_AUX && ACT != KFAMD_ACT_NONE && BM == 256 && !SPLIT && !SK && !PO),
                 "act-grad epilogue: the pre-activation as R, 256 tile, whole K");
   // PO: the epilogue's LDS staging lives in the ring's fifth slot, which the next tile's prologue
@@ -331,8 +346,28 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
     rt_start = __builtin_amdgcn_s_memrealtime();
   }
 
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
+  int wg;
+  if constexpr (GRP) {
+    const int t1 = nwg, t2 = ((g2.M + BM - 1) / BM) * ((g2.N + BN - 1) / BN);
+    wg = xcd_remap(blockIdx.x, t1 + t2);
+    if (wg >= t1) {  // problem 2 (uniform per block)
+      wg -= t1;
+      A = g2.A;
+      B = g2.B;
+      C = g2.C;
+      M = g2.M;
+      N = g2.N;
+      lda = g2.lda;
+      ldb = g2.ldb;
+      ldc = g2.ldc;
+      tiles_m = (M + BM - 1) / BM;
+      tiles_n = (N + BN - 1) / BN;
+      nwg = t2;
+    }
+  } else {
+    wg = xcd_remap(blockIdx.x, nwg);
+  }
 #ifndef KFW4_SK_AB
 #define KFW4_SK_AB 0  // stream-K timing ablations (tools/sk_ab.py builds): 1 no partial traffic, 2 no owner wait
 #endif

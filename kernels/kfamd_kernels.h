@@ -124,6 +124,11 @@ int kfamd_colsum_finalize(const float* ws, void* db, int db_bf16, int nblk, int 
 // [K][N] with row stride ldb, Z / G row strides ldz / ldg), and when db is given the column sums of G
 // (the previous layer's bias gradient; ws: kfamd_w4_dgrad_act_workspace bytes). M, N multiples of
 // 256, K of 64, 16-B rows; KFAMD_EINVAL otherwise (callers fall back to the GEMM + act-grad pass).
+// Two weight gradients in one launch: C_i[M_i][N] = A_i^T . B_i, A_i [K][M_i] (row stride lda_i), B_i
+// [K][N] (ldb_i), C_i row stride ldc_i (kernels/tu/w4_wgrad_pair.hip).
+int kfamd_w4_wgrad_pair(const void* A1, const void* B1, void* C1, int M1, long long lda1, long long ldb1,
+                        long long ldc1, const void* A2, const void* B2, void* C2, int M2, long long lda2,
+                        long long ldb2, long long ldc2, int N, int K, void* stream);
 long long kfamd_w4_dgrad_act_workspace(int M, int N);
 int kfamd_w4_dgrad_act(const void* dy, const void* w, void* g, const void* z, int M, int N, int K, long long lda,
                        long long ldb, long long ldg, long long ldz, int act, float* ws, void* db, int db_bf16,

@@ -120,6 +120,11 @@ class Block(torch.nn.Module):
     def attention(self, x, residual=None):
         B, T, _ = x.shape
         h, hd = self.local_heads, self.cfg.head_dim
+        if x.is_cuda and ops.native_enabled() and ops.attention_supported(x, hd) and tpl._world(self.tp_group) == 1:
+            # one autograd node on the HIP path (ops.attn_block): its backward runs the QKV and
+            # output-projection weight gradients as one GEMM launch
+            return ops.attn_block(x, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias, h, hd,
+                                  residual=residual)
         qkv = self.qkv(x)  # [B, T, 3 * h * hd] — the column shard is [q_h | k_h | v_h] per rank
         if ops.native_enabled() and ops.attention_supported(qkv, hd):
             y = ops.attention_qkv(qkv.contiguous(), h, hd, causal=True)  # [B, T, h * hd]

@@ -1,9 +1,9 @@
 """Torch-facing wrappers of the hand-written gfx950 kernels (no silent eager fallback)."""
 from ._lib import NativeLibraryError, available, build_info, lib  # noqa: F401
-from .gemm import act_grad, dgrad_act, flops, gemm_nt, gemm_nt_preact, linear, matmul, mlp, mm  # noqa: F401
+from .gemm import act_grad, dgrad_act, flops, gemm_nt, gemm_nt_preact, linear, matmul, mlp, mm, wgrad_pair  # noqa: F401
 from .layernorm import layer_norm, layer_norm_fwd, layer_norm_residual, rms_norm, rms_norm_fwd  # noqa: F401
 from .xent import cross_entropy  # noqa: F401
-from .attention import attention_qkv, flash_attention, split_heads  # noqa: F401
+from .attention import attention_qkv, attn_block, flash_attention, split_heads  # noqa: F401
 from .attention import supported as attention_supported  # noqa: F401
 from .allreduce import OneShotAllReduce  # noqa: F401
 from .graph import GraphedCallable  # noqa: F401

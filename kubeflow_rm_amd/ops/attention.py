@@ -120,6 +120,79 @@ class _FlashAttnQKV(torch.autograd.Function):
         return dqkv.view(B, T, 3 * h * hd), None, None, None, None
 
 
+class _AttnBlock(torch.autograd.Function):
+    """x -> qkv = x Wqkv^T + bqkv -> flash attention -> o Wproj^T + bproj (+ residual), one autograd
+    node. Its backward orders the work across the three: the projection's dgrad, the attention
+    backward, the QKV dgrad, and then both weight gradients in ONE launch (gemm.wgrad_pair: 192 + 64
+    tiles at gpt-1b, where apart the QKV wgrad filled 75 % of the CUs and the projection's ran
+    split-K). The forward is the separate layers' (gemm_nt with bias, _fwd, gemm_nt with bias and
+    residual)."""
+
+    @staticmethod
+    def forward(ctx, x, wqkv, bqkv, wproj, bproj, h, hd, causal, scale, residual):
+        from .gemm import gemm_nt
+        B, T, D = x.shape
+        x2 = x.reshape(B * T, D)
+        if x2.stride(-1) != 1 or x2.stride(0) != D:
+            x2 = x2.contiguous()
+        qkv = gemm_nt(x2, wqkv, bias=bqkv).view(B, T, 3, h, hd)
+        o = torch.empty(B, T, h, hd, device=x.device, dtype=x.dtype)
+        lse = _fwd(*(_bhtd(qkv[:, :, i]) for i in range(3)), _bhtd(o), causal, scale)
+        o2 = o.view(B * T, h * hd)
+        res = residual.reshape(B * T, wproj.shape[0]).contiguous() if residual is not None else None
+        out = gemm_nt(o2, wproj, bias=bproj, residual=res)
+        ctx.save_for_backward(x2, wqkv, bqkv, wproj, bproj, qkv, o, lse)
+        ctx.dims, ctx.causal, ctx.scale = (B, T, D, h, hd), causal, scale
+        return out.view(B, T, wproj.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .gemm import act_grad, mm, wgrad_pair
+        x2, wqkv, bqkv, wproj, bproj, qkv, o, lse = ctx.saved_tensors
+        B, T, D, h, hd = ctx.dims
+        ni = ctx.needs_input_grad
+        gy2 = gy.reshape(B * T, wproj.shape[0])
+        if not gy2.is_contiguous():
+            gy2 = gy2.contiguous()
+
+        def bias_grad(g, bias, need):
+            if not need:
+                return None
+            _, db = act_grad(g, None, "none", True,
+                             db_dtype=torch.bfloat16 if bias.dtype == torch.bfloat16 else torch.float32)
+            return db.to(bias.dtype)
+        gbp = bias_grad(gy2, bproj, bproj is not None and ni[4])
+        o2 = o.view(B * T, h * hd)
+        do = mm(gy2, wproj).view(B, T, h, hd)  # the projection's dgrad
+        dqkv = torch.empty(B, T, 3, h, hd, device=qkv.device, dtype=qkv.dtype)
+        _bwd(*(_bhtd(qkv[:, :, i]) for i in range(3)), _bhtd(o), _bhtd(do), lse,
+             *(_bhtd(dqkv[:, :, i]) for i in range(3)), ctx.causal, ctx.scale)
+        dqkv2 = dqkv.view(B * T, 3 * h * hd)
+        gbq = bias_grad(dqkv2, bqkv, bqkv is not None and ni[2])
+        dx = mm(dqkv2, wqkv).view(B, T, D) if ni[0] else None
+        gwq = gwp = None
+        pair = wgrad_pair(dqkv2, x2, gy2, o2) if ni[1] and ni[3] else None
+        if pair is not None:
+            gwq, gwp = pair
+        else:
+            gwq = mm(dqkv2, x2, trans_a=True) if ni[1] else None
+            gwp = mm(gy2, o2, trans_a=True) if ni[3] else None
+        return dx, gwq, gbq, gwp, gbp, None, None, None, None, (gy if ni[9] else None)
+
+
+def attn_block(x: torch.Tensor, wqkv: torch.Tensor, bqkv: torch.Tensor | None, wproj: torch.Tensor,
+               bproj: torch.Tensor | None, h: int, hd: int, residual: torch.Tensor | None = None,
+               causal: bool = True, scale: float | None = None) -> torch.Tensor:
+    """A transformer block's attention half on the HIP kernels: ``proj(attn(qkv(x))) (+ residual)``,
+    x ``[B, T, D]``, wqkv ``[3 h hd, D]`` (q | k | v rows, heads inside each), wproj ``[D_out, h hd]``."""
+    if x.dim() != 3 or wqkv.shape[0] != 3 * h * hd or wproj.shape[1] != h * hd:
+        raise ValueError("attn_block: x [B, T, D], wqkv [3 h hd, D], wproj [D_out, h hd] expected")
+    if not supported(x, hd):
+        raise ValueError(f"attn_block: bf16 CUDA input with head dim in {HEAD_DIMS} expected")
+    return _AttnBlock.apply(x, wqkv, bqkv, wproj, bproj, h, hd, causal,
+                            scale if scale is not None else 1.0 / math.sqrt(hd), residual)
+
+
 def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
                     scale: float | None = None) -> torch.Tensor:
     """softmax(scale * q k^T (+ causal mask)) v for [B, H, T, D] bf16 views (D = 64 / 128)."""

@@ -610,6 +610,32 @@ def dgrad_act(gy2: torch.Tensor, weight: torch.Tensor, z: torch.Tensor, act: str
     return g, db
 
 
+def wgrad_pair(g1: torch.Tensor, x1: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, force: bool = False):
+    """(g1^T x1, g2^T x2) — two weight gradients (g_i [K][M_i], x_i [K][N]) as one launch of the w4
+    kernel (kernels/tu/w4_wgrad_pair.hip) when together they fill the chip's 256 CUs far better than
+    apart (a transformer block's QKV + output projection: 192 + 64 tiles at gpt-1b); else None and
+    the caller runs two ``mm``s (which split K where a problem alone under-fills the chip).
+    ``force``: launch whenever the shapes fit the kernel (tests)."""
+    if any(t.dim() != 2 or t.dtype != torch.bfloat16 or t.stride(-1) != 1 for t in (g1, x1, g2, x2)):
+        return None
+    K, M1 = g1.shape
+    M2, N = g2.shape[1], x1.shape[1]
+    if g2.shape[0] != K or tuple(x1.shape) != (K, N) or tuple(x2.shape) != (K, N) or min(M1, M2, N) < 256:
+        return None
+    t1, t2 = -(-M1 // 256) * -(-N // 256), -(-M2 // 256) * -(-N // 256)
+    if not force and not (t1 < _NUM_CUS and t2 < _NUM_CUS and _NUM_CUS * 3 // 4 <= t1 + t2 <= _NUM_CUS):
+        return None
+    o1 = torch.empty(M1, N, dtype=torch.bfloat16, device=g1.device)
+    o2 = torch.empty(M2, N, dtype=torch.bfloat16, device=g1.device)
+    rc = _lib.lib().kfamd_w4_wgrad_pair(g1.data_ptr(), x1.data_ptr(), o1.data_ptr(), M1, g1.stride(0), x1.stride(0), N,
+                                        g2.data_ptr(), x2.data_ptr(), o2.data_ptr(), M2, g2.stride(0), x2.stride(0), N,
+                                        N, K, _stream_ptr(g1))
+    if rc < 0:
+        return None
+    _lib.check(rc, f"wgrad_pair[{M1}+{M2}x{N}x{K}]")
+    return o1, o2
+
+
 class _MLP(torch.autograd.Function):
     """out = act(x W1^T + b1) W2^T + b2 (+ residual) as one autograd node, so that fc2's dgrad can
     apply fc1's activation backward in its epilogue (dgrad_act): the backward runs fc2's bias and

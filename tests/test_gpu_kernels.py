@@ -773,3 +773,43 @@ def test_mlp_matches_fp32(fused, act):
     for got, ref in zip((x.grad, w1.grad, b1.grad, w2.grad, b2.grad, r.grad), (t.grad for t in ts)):
         err = (got.float() - ref).abs().max().item()
         assert err <= 3e-2 * (ref.abs().max().item() + 1e-3) + 1e-2, err
+
+
+@pytest.mark.parametrize("K,M1,M2,N", [(512, 768, 256, 512), (1000, 6144, 2048, 2048), (384, 296, 520, 264)])
+def test_wgrad_pair_matches_fp32(K, M1, M2, N):
+    """Two weight gradients in one launch (gemm_w4.h GRP): each against its fp32 product, including
+    edge tiles (M / N not multiples of 256) and a K that is not a multiple of 64."""
+    from kubeflow_rm_amd import ops
+    g1, x1 = _rand(K, M1, seed=91), _rand(K, N, seed=92)
+    g2, x2 = _rand(K, M2, seed=93), _rand(K, N, seed=94)
+    out = ops.wgrad_pair(g1, x1, g2, x2, force=True)
+    assert out is not None
+    for got, (g, x) in zip(out, ((g1, x1), (g2, x2))):
+        _assert_close(got, g.float().t() @ x.float(), K)
+
+
+@pytest.mark.parametrize("B,T,D,h,hd", [(1, 512, 2048, 16, 128), (2, 128, 512, 4, 64)])
+def test_attn_block_matches_fp32(B, T, D, h, hd):
+    """ops.attn_block (QKV projection + flash attention + output projection + residual as one autograd
+    node; at D = 2048 both weight gradients in one launch, at D = 512 the separate path) forward and
+    every gradient against fp32 autograd with F.scaled_dot_product_attention."""
+    from kubeflow_rm_amd import ops
+    F = torch.nn.functional
+    x = _rand(B, T, D, seed=101).requires_grad_(True)
+    wq, bq = _rand(3 * h * hd, D, seed=102, scale=0.03).requires_grad_(True), _rand(3 * h * hd, seed=103).requires_grad_(True)
+    wp, bp = _rand(D, h * hd, seed=104, scale=0.03).requires_grad_(True), _rand(D, seed=105).requires_grad_(True)
+    r = _rand(B, T, D, seed=106).requires_grad_(True)
+    gy = _rand(B, T, D, seed=107)
+    y = ops.attn_block(x, wq, bq, wp, bp, h, hd, residual=r)
+    y.backward(gy)
+    ts = [t.detach().float().requires_grad_(True) for t in (x, wq, bq, wp, bp, r)]
+    qkv = F.linear(ts[0], ts[1], ts[2]).view(B, T, 3, h, hd)
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    o = F.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, h * hd)
+    yr = F.linear(o, ts[3], ts[4]) + ts[5]
+    yr.backward(gy.float())
+    assert (y.float() - yr).abs().max().item() < 3e-2 * (yr.abs().max().item() + 1)
+    for name, got, ref in zip(("x", "wqkv", "bqkv", "wproj", "bproj", "res"),
+                              (x.grad, wq.grad, bq.grad, wp.grad, bp.grad, r.grad), (t.grad for t in ts)):
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 3e-2 * (ref.abs().max().item() + 1e-3) + 1e-2, (name, err)
