@@ -73,24 +73,6 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   }
 }
 
-// act'(z) for the DACT epilogue (the backward of act at the pre-activation z; relu takes z too)
-__device__ __forceinline__ float dact_fn(float z, int act) {
-  switch (act) {
-    case KFAMD_ACT_RELU: return z > 0.f ? 1.f : 0.f;
-    case KFAMD_ACT_GELU_TANH: {
-      // gelu_tanh(z) = z s(2u), u = c (z + 0.044715 z^3): d/dz = s + z s (1 - s) 2u'
-      const float z2 = z * z;
-      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-1.5957691216057308f * (z + 0.044715f * z2 * z)));
-      return sg + z * sg * (1.f - sg) * 1.5957691216057308f * (1.f + 3.f * 0.044715f * z2);
-    }
-    case KFAMD_ACT_SILU: {
-      const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-z));
-      return sg * (1.f + z * (1.f - sg));
-    }
-    default: return 1.f;
-  }
-}
-
 // act'(z) on a pair of values: the polynomial parts as packed f32 ops (v_pk_mul / v_pk_fma: two
 // lanes' worth per instruction), the exp / rcp per value. gelu_tanh with 2u = z (A + B z^2):
 // act' = s (1 + z (1 - s) (A + 3 B z^2)), s = sigmoid(2u), log2(e) folded into exp's argument.
@@ -117,6 +99,26 @@ __device__ __forceinline__ kf32x2 dact2(kf32x2 z) {
   } else {
     return kf32x2{1.f, 1.f};
   }
+}
+
+// act(z) on a pair (the forward epilogue, KFW4_ACT_PK): gelu_tanh / silu as z * sigmoid(.), the
+// polynomial parts packed as in dact2
+#ifndef KFW4_ACT_PK
+#define KFW4_ACT_PK 1
+#endif
+template <int ACT>
+__device__ __forceinline__ kf32x2 act2(kf32x2 z) {
+  constexpr float L2E = 1.4426950408889634f;
+  kf32x2 q;
+  if constexpr (ACT == KFAMD_ACT_GELU_TANH) {
+    constexpr float A = 1.5957691216057308f, B = 1.5957691216057308f * 0.044715f;
+    q = z * __builtin_elementwise_fma(z * z, kf32x2{-B * L2E, -B * L2E}, kf32x2{-A * L2E, -A * L2E});
+  } else {
+    q = z * kf32x2{-L2E, -L2E};
+  }
+  const kf32x2 e{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const kf32x2 d = e + kf32x2{1.f, 1.f};
+  return z * kf32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -789,7 +791,13 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
       for (int r = 0; r < 4; ++r) p[r] = (__bf16)v[r];
       pre_out = __builtin_bit_cast(uint2, p);
     }
-    if (ACT != KFAMD_ACT_NONE) {
+    if constexpr (KFW4_ACT_PK && (ACT == KFAMD_ACT_GELU_TANH || ACT == KFAMD_ACT_SILU)) {
+      const kf32x2 lo = act2<ACT>(kf32x2{v[0], v[1]}), hi = act2<ACT>(kf32x2{v[2], v[3]});
+      v[0] = lo.x;
+      v[1] = lo.y;
+      v[2] = hi.x;
+      v[3] = hi.y;
+    } else if (ACT != KFAMD_ACT_NONE) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = act_fn(v[r], ACT);
     }

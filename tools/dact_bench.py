@@ -29,10 +29,12 @@ def main():
     ap.add_argument("--shapes", default="8192x2048x8192,32768x768x3072")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--preact", default="8192x8192x2048,32768x3072x768",
+                    help="MxNxK: the forward GEMM with bias + gelu + pre-activation output vs bias only")
     ap.add_argument("--res", default="8192x2048x2048,8192x2048x8192",
                     help="MxNxK: the forward GEMM with bias + residual epilogue vs bias only")
     a = ap.parse_args()
-    for shp in a.shapes.split(","):
+    for shp in [x for x in a.shapes.split(",") if x]:
         M, K, N = map(int, shp.split("x"))
         g = torch.Generator(device="cuda").manual_seed(0)
         gy = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
@@ -52,6 +54,21 @@ def main():
         print(json.dumps({"shape": shp, **{k + "_us": round(statistics.median(v), 1) for k, v in res.items()}}),
               flush=True)
 
+    for shp in [x for x in a.preact.split(",") if x]:
+        M, N, K = map(int, shp.split("x"))
+        g = torch.Generator(device="cuda").manual_seed(2)
+        x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+        fns = {"gelu_preact": lambda: ops.gemm_nt_preact(x, w, b, "gelu_tanh"), "bias": lambda: ops.gemm_nt(x, w, bias=b)}
+        for f in fns.values():
+            timeit(f, 2)
+        res = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, f in fns.items():
+                res[k].append(timeit(f, a.iters))
+        print(json.dumps({"preact": shp, **{k + "_us": round(statistics.median(v), 1) for k, v in res.items()}}),
+              flush=True)
     for shp in [x for x in a.res.split(",") if x]:
         M, N, K = map(int, shp.split("x"))
         g = torch.Generator(device="cuda").manual_seed(1)
