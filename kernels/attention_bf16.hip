@@ -185,6 +185,12 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_FWD_OFFS
 #define KFATT_FWD_OFFS 1  // forward: LDS read offsets precomputed per lane, buffers unrolled
 #endif
+#ifndef KFATT_FWD_PAIR
+#define KFATT_FWD_PAIR 1  // causal forward: heavy + light query block per workgroup (attn_fwd PAIR, profiles/r5zm_fpair)
+#endif
+#ifndef KFATT_DQ_PAIR
+#define KFATT_DQ_PAIR 0  // the same for the dQ kernel (attn_bwd_dq_split PAIR)
+#endif
 #ifndef KFATT_FWD_DMA
 #define KFATT_FWD_DMA 0  // forward K / V tiles by LDS-DMA (attn_fwd stage_dma)
 #endif
@@ -245,7 +251,9 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* smem, int kbase, int co
 // ------------------------------------------------------------------------------------------------
 constexpr int FQ = 128, FK = 64;
 
-template <int D, bool CAUSAL>
+// PAIR (causal, an even number of query blocks, KFATT_FWD_PAIR): one workgroup runs query blocks
+// nq - 1 - i and i one after the other, nq + 1 key tiles for every workgroup, half the grid
+template <int D, bool CAUSAL, bool PAIR = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, __bf16* __restrict__ o,
                                                    float* __restrict__ lse, AttnShape a) {
@@ -257,9 +265,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K, V]
 
   const int nq = (a.T + FQ - 1) / FQ;
-  const BlockId bo = block_order(blockIdx.x, nq, a.H * a.B, 64);  // 2 workgroups per CU
-  const int qblk = nq - 1 - bo.rank;  // the heaviest (most keys) first
+  const BlockId bo = block_order(blockIdx.x, PAIR ? nq / 2 : nq, a.H * a.B, 64);  // 2 workgroups per CU
   const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
+#pragma unroll 1
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  if (PAIR && pass) __syncthreads();  // the first block's last tile reads are done before the LDS is refilled
+  const int qblk = pass ? bo.rank : nq - 1 - bo.rank;  // the heaviest (most keys) first
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
@@ -479,6 +490,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
     }
     if (hh == 0) lse[((long long)b * a.H + h) * T + qrow] = m * a.scale + logf(lt);
   }
+  }  // pass
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -525,7 +537,8 @@ __global__ __launch_bounds__(256) void attn_bwd_delta(const __bf16* __restrict__
 // DELTA (KFATT_DQ_DELTA): this kernel runs first and is also the backward's prologue: each lane's
 // query row computes delta = sum_d dO * O from the dO fragments it holds anyway plus one pass over O,
 // and writes nl / nd for the dK / dV kernel (lse, delta arrive raw; the separate prologue is gone)
-template <int D, bool CAUSAL, bool DELTA = false>
+// PAIR: as attn_fwd's (query blocks nq - 1 - i and i in one workgroup; KFATT_DQ_PAIR)
+template <int D, bool CAUSAL, bool DELTA = false, bool PAIR = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                             const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
@@ -541,9 +554,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
 
   const int T = a.T;
   const int nq = (T + FQ - 1) / FQ;
-  const BlockId bo = block_order(blockIdx.x, nq, a.H * a.B, 64);
-  const int qblk = nq - 1 - bo.rank;  // the heaviest first
+  const BlockId bo = block_order(blockIdx.x, PAIR ? nq / 2 : nq, a.H * a.B, 64);
   const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
+#pragma unroll 1
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+  if (PAIR && pass) __syncthreads();  // the first block's last LDS reads are done before the refill
+  const int qblk = pass ? bo.rank : nq - 1 - bo.rank;  // the heaviest first
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
 
@@ -701,6 +717,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
       }
     }
   }
+  }  // pass
 }
 
 // dS^T image [128 keys][64 queries]: 128-B rows of sixteen 8-B slots (4 queries each), slot ^ f(row),
@@ -1320,8 +1337,20 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
                        static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),
                        static_cast<float*>(lse), s);
   };
-  if (D == 128) causal ? go(attn_fwd<128, true>) : go(attn_fwd<128, false>);
-  else causal ? go(attn_fwd<64, true>) : go(attn_fwd<64, false>);
+  const int nq = (T + FQ - 1) / FQ;
+  if (KFATT_FWD_PAIR && causal && nq % 2 == 0) {
+    auto go2 = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)(nwg / 2)), dim3(256), 0, st, static_cast<const __bf16*>(q),
+                         static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),
+                         static_cast<float*>(lse), s);
+    };
+    if (D == 128) go2(attn_fwd<128, true, true>);
+    else go2(attn_fwd<64, true, true>);
+  } else if (D == 128) {
+    causal ? go(attn_fwd<128, true>) : go(attn_fwd<128, false>);
+  } else {
+    causal ? go(attn_fwd<64, true>) : go(attn_fwd<64, false>);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KFAMD_OK : static_cast<int>(e);
 }
@@ -1372,8 +1401,9 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
     };
     if (KFATT_DQ_DELTA && (D == 128 ? KFATT_DKDV8 : KFATT_DKDV8_64)) {
       // the dQ kernel first, as the prologue too (nl / nd), then the 8-wave dK / dV kernel
+      const bool pair = KFATT_DQ_PAIR && causal && ((T + FQ - 1) / FQ) % 2 == 0;
       auto runq = [&](auto dq_k, auto main_k) {
-        hipLaunchKernelGGL(dq_k, dim3((unsigned)nq), dim3(256), 0, st, static_cast<const __bf16*>(q),
+        hipLaunchKernelGGL(dq_k, dim3((unsigned)(pair ? nq / 2 : nq)), dim3(256), 0, st, static_cast<const __bf16*>(q),
                            static_cast<const __bf16*>(k), static_cast<const __bf16*>(v),
                            static_cast<const __bf16*>(dout), static_cast<const float*>(lse),
                            static_cast<const float*>(nullptr), static_cast<__bf16*>(dq), s,
@@ -1383,8 +1413,10 @@ extern "C" int kfamd_attn_bwd_bf16(const void* q, const void* k, const void* v, 
                            static_cast<const __bf16*>(dout), static_cast<const float*>(nl),
                            static_cast<const float*>(nd), static_cast<__bf16*>(dk), static_cast<__bf16*>(dv), s);
       };
-      if (D == 128) causal ? runq(attn_bwd_dq_split<128, true, true>, attn_bwd_dkdv8<128, true>)
-                           : runq(attn_bwd_dq_split<128, false, true>, attn_bwd_dkdv8<128, false>);
+      if (pair) D == 128 ? runq(attn_bwd_dq_split<128, true, true, true>, attn_bwd_dkdv8<128, true>)
+                         : runq(attn_bwd_dq_split<64, true, true, true>, attn_bwd_dkdv8<64, true>);
+      else if (D == 128) causal ? runq(attn_bwd_dq_split<128, true, true>, attn_bwd_dkdv8<128, true>)
+                                : runq(attn_bwd_dq_split<128, false, true>, attn_bwd_dkdv8<128, false>);
       else causal ? runq(attn_bwd_dq_split<64, true, true>, attn_bwd_dkdv8<64, true>)
                   : runq(attn_bwd_dq_split<64, false, true>, attn_bwd_dkdv8<64, false>);
     } else if (KFATT_DKDV8 && D == 128) {

@@ -38,6 +38,8 @@ def _variants():
         "atomics_dropped": [*prod, "-DKFATT_DQ_SPLIT=0", "-DKFATT_ABL=1"],  # timing only: atomics dropped
         "fwd_dma": [*prod, "-DKFATT_FWD_DMA=1"],  # forward K / V by LDS-DMA
         "nolpt": [*prod, "-DKFATT_LPT=0"],  # head-major block order (no longest-first across heads)
+        "nofpair": [*prod, "-DKFATT_FWD_PAIR=0"],  # causal forward: one query block per workgroup
+        "dqpair": [*prod, "-DKFATT_DQ_PAIR=1"],  # dQ kernel: heavy + light query block per workgroup
     }
 
 
