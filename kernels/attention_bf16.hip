@@ -188,6 +188,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_FWD_PAIR
 #define KFATT_FWD_PAIR 1  // causal forward: heavy + light query block per workgroup (attn_fwd PAIR, profiles/r5zm_fpair)
 #endif
+#ifndef KFATT_FWD_NW
+#define KFATT_FWD_NW 4  // forward workgroup: 4 waves (two workgroups per CU) or 8 (one; A/B runs)
+#endif
 #ifndef KFATT_DQ_PAIR
 #define KFATT_DQ_PAIR 0  // the same for the dQ kernel (attn_bwd_dq_split PAIR)
 #endif
@@ -253,19 +256,20 @@ constexpr int FQ = 128, FK = 64;
 
 // PAIR (causal, an even number of query blocks, KFATT_FWD_PAIR): one workgroup runs query blocks
 // nq - 1 - i and i one after the other, nq + 1 key tiles for every workgroup, half the grid
-template <int D, bool CAUSAL, bool PAIR = false>
-__global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+template <int D, bool CAUSAL, bool PAIR = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, __bf16* __restrict__ o,
                                                    float* __restrict__ lse, AttnShape a) {
   constexpr int KS = D / 16;           // k-steps of the QK^T product
   constexpr int ND = D / 32;           // 32-wide d tiles of O
   constexpr int CH = D / 8;            // 16-B chunks per row
-  constexpr int NCH = FK * CH / 256;   // chunks per thread per K (and per V) tile
+  constexpr int NT = 64 * NW, FQW = 32 * NW;  // threads, query rows per workgroup (NW waves x 32)
+  constexpr int NCH = FK * CH / NT;    // chunks per thread per K (and per V) tile
   constexpr int TILE = FK * D * 2;     // bytes of one K (or V) tile image
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][K, V]
 
-  const int nq = (a.T + FQ - 1) / FQ;
-  const BlockId bo = block_order(blockIdx.x, PAIR ? nq / 2 : nq, a.H * a.B, 64);  // 2 workgroups per CU
+  const int nq = (a.T + FQW - 1) / FQW;
+  const BlockId bo = block_order(blockIdx.x, PAIR ? nq / 2 : nq, a.H * a.B, NW == 4 ? 64 : 32);  // workgroups per XCD
   const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
 #pragma unroll 1
   for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
   const int qblk = pass ? bo.rank : nq - 1 - bo.rank;  // the heaviest (most keys) first
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
-  const int q0 = qblk * FQ, qw = q0 + 32 * w, qrow = qw + r;
+  const int q0 = qblk * FQW, qw = q0 + 32 * w, qrow = qw + r;
   const int T = a.T;
 
   const __bf16* qb = q + base_off(a, TQ, b, h);
@@ -289,14 +293,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
     qf[kk] = __builtin_bit_cast(bf16x8, x);
   }
 
-  const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQ) / FK) : (T + FK - 1) / FK;
+  const int ntiles = CAUSAL ? min((T + FK - 1) / FK, (q0 + FQW) / FK) : (T + FK - 1) / FK;
 
   constexpr bool kDma = KFATT_FWD_DMA && KFATT_BUF;
   u32x4 kreg[kDma ? 1 : NCH], vreg[kDma ? 1 : NCH];
   const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
   const i32x4 dk_desc = slice_desc(kb, 2LL * T * kt), dv_desc = slice_desc(vb, 2LL * T * vt);
   // KFATT_DMA: K / V tiles by LDS-DMA (as the backward's stage_dma): no staging registers
-  constexpr int NPC = TILE / 1024 / 4;
+  constexpr int NPC = TILE / 1024 / NW;
   // LDS-DMA pieces: the wave index as a uniform value, each piece's per-lane source offset computed
   // once (image chunk sc of row `row` holds source chunk sc ^ swz(row, 0))
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
     const int k0 = tile * FK;
 #pragma unroll
     for (int i = 0; i < (kDma ? 0 : NCH); ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int c = tid + NT * i, row = c / CH, ch = c % CH;
       const int key = k0 + row;
       if constexpr (KFATT_BUF) {
         // lane part in the voffset, the tile's row offset in the (scalar) soffset: no VALU per load
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd(const __bf16* __restrict__ q,
     char* vimg = kimg + TILE;
 #pragma unroll
     for (int i = 0; i < (kDma ? 0 : NCH); ++i) {
-      const int c = tid + 256 * i, row = c / CH, ch = c % CH;
+      const int c = tid + NT * i, row = c / CH, ch = c % CH;
       const int off = img_off<D>(row, ch);
       *reinterpret_cast<u32x4*>(kimg + off) = kreg[i];
       *reinterpret_cast<u32x4*>(vimg + off) = vreg[i];
@@ -1338,7 +1342,20 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
                        static_cast<float*>(lse), s);
   };
   const int nq = (T + FQ - 1) / FQ;
-  if (KFATT_FWD_PAIR && causal && nq % 2 == 0) {
+  if constexpr (KFATT_FWD_NW == 8) {  // 8 waves x 32 rows per workgroup (A/B knob)
+    const int nq8 = (T + 255) / 256;
+    const bool pair = KFATT_FWD_PAIR && causal && nq8 % 2 == 0;
+    const long long g8 = (long long)(pair ? nq8 / 2 : nq8) * H * B;
+    auto go8 = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)g8), dim3(512), 0, st, static_cast<const __bf16*>(q),
+                         static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),
+                         static_cast<float*>(lse), s);
+    };
+    if (D == 128) pair ? go8(attn_fwd<128, true, true, 8>) : causal ? go8(attn_fwd<128, true, false, 8>)
+                                                                    : go8(attn_fwd<128, false, false, 8>);
+    else pair ? go8(attn_fwd<64, true, true, 8>) : causal ? go8(attn_fwd<64, true, false, 8>)
+                                                          : go8(attn_fwd<64, false, false, 8>);
+  } else if (KFATT_FWD_PAIR && causal && nq % 2 == 0) {
     auto go2 = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((unsigned)(nwg / 2)), dim3(256), 0, st, static_cast<const __bf16*>(q),
                          static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),

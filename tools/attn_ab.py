@@ -40,6 +40,7 @@ def _variants():
         "nolpt": [*prod, "-DKFATT_LPT=0"],  # head-major block order (no longest-first across heads)
         "nofpair": [*prod, "-DKFATT_FWD_PAIR=0"],  # causal forward: one query block per workgroup
         "dqpair": [*prod, "-DKFATT_DQ_PAIR=1"],  # dQ kernel: heavy + light query block per workgroup
+        "fwd8": [*prod, "-DKFATT_FWD_NW=8"],  # forward: one 8-wave workgroup (256 query rows) per CU
     }
 
 
