@@ -3,7 +3,7 @@
 # its own bounded run, then a per-kernel summary (tools/attn_pmc_summary.py)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r5t_attn_pmc
+OUT=$R/gpurun_out/${TAG:-r5t_attn_pmc}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $OUT/pmc1 -o run -- python3 $R/tools/attn_prof.py 4x16x2048x128 3 > $OUT/pmc1.log 2>&1 || exit $?
