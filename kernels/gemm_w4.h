@@ -283,7 +283,7 @@ struct W4Grp {
 
 // DACT (a linear layer's backward through its activation, gemm_bf16_w4_t.hip kfamd_w4_dgrad_act):
 // C = (A·B) * act'(R), R = the pre-activation the forward stored, and when W is given the column
-// sums of the bf16 C per 128-row slab (W[M / 128][N], the next layer's bias-gradient partials):
+// sums of C per wave-row slab (W[M / (BM / 2)][N], the next layer's bias-gradient partials):
 // the elementwise act-grad pass (act_grad_bf16.hip) folded into the dgrad GEMM's epilogue, which
 // reads R where that pass read both dY and R and wrote G. Whole interior tiles only (the host
 // requires M and N multiples of 256 and 16-B rows), on the full-line residual epilogue.
@@ -332,7 +332,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(!PO || (BM == 256 && !SPLIT && !SK && !DIAG), "persistent overlapped: 256 tile, whole K");
   static_assert(!GRP || (!SPLIT && !SK && !PO && !DACT && !HAS_BIAS && !HAS_RES && !HAS_AUX && !DIAG),
                 "grouped pair: plain epilogue, one tile per block");
-  static_assert(!DACT || (HAS_RES && !HAS_BIAS && !HAS_AUX && ACT != KFAMD_ACT_NONE && BM == 256 && !SPLIT && !SK && !PO),
+  static_assert(!DACT || (HAS_RES && !HAS_BIAS && !HAS_AUX && ACT != KFAMD_ACT_NONE && !SPLIT && !SK && !PO),
                 "act-grad epilogue: the pre-activation as R, 256 tile, whole K");
   // PO: the epilogue's LDS staging lives in the ring's fifth slot, which the next tile's prologue
   // (tiles 0 and 1 into slots 0-3) leaves alone, so that prologue can be issued before the epilogue
@@ -1094,7 +1094,7 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
           }
         }
         if (rr == 0) {
-          float* wrow = W + ((long long)(m0 / 128) + wm) * N + n0 + wn * WT + rc * 8;
+          float* wrow = W + ((long long)(m0 / WT) + wm) * N + n0 + wn * WT + rc * 8;
 #pragma unroll
           for (int h = 0; h < NR / 4; ++h) {
             *reinterpret_cast<f32x4*>(wrow + 64 * h) = f32x4{csum[h][0], csum[h][1], csum[h][2], csum[h][3]};
