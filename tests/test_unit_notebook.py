@@ -94,23 +94,32 @@ def _rfc(delta_min=0.0):
     return (dt.datetime.now(dt.timezone.utc) + dt.timedelta(minutes=delta_min)).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
+class _Now:
+    """A timestamp `minutes` from now, taken when the test runs (not at collection: in a long serial
+    run the gap between the two pushed the 3-minutes-ago case past the 5-minute deadline)."""
+
+    def __init__(self, minutes=0.0):
+        self.minutes = minutes
+
+
 IDLE_CASES = [
     ("No existing Annotations", {}, 1440, False),
     ("Basic case", {"annotations": {}}, 1440, False),
-    ("Stop Annotation already set", {"annotations": {STOP: _rfc()}}, 1440, False),
+    ("Stop Annotation already set", {"annotations": {STOP: _Now()}}, 1440, False),
     ("LAST_ACTIVITY_ANNOTATION is not set", {"annotations": {}}, 1440, False),
     ("LAST_ACTIVITY_ANNOTATION is not RF3339", {"annotations": {LAST: "should-fail"}}, 1440, False),
     ("LAST_ACTIVITY_ANNOTATION is old", {"annotations": {LAST: "2021-08-30T15:37:36.990063Z"}}, 1440, True),
     ("LAST_ACTIVITY_ANNOTATION is too old", {"annotations": {LAST: "1900-08-30T15:37:36.990063Z"}}, 1440, True),
-    ("LAST_ACTIVITY_ANNOTATION is the current time", {"annotations": {LAST: _rfc()}}, 5, False),
-    ("1 minute MORE than the deadline", {"annotations": {LAST: _rfc(-6)}}, 5, True),
-    ("1 minute LESS than the deadline", {"annotations": {LAST: _rfc(-3)}}, 5, False),
+    ("LAST_ACTIVITY_ANNOTATION is the current time", {"annotations": {LAST: _Now()}}, 5, False),
+    ("1 minute MORE than the deadline", {"annotations": {LAST: _Now(-6)}}, 5, True),
+    ("1 minute LESS than the deadline", {"annotations": {LAST: _Now(-3)}}, 5, False),
 ]
 
 
 @pytest.mark.parametrize("name,meta,minutes,want", IDLE_CASES, ids=[c[0] for c in IDLE_CASES])
 def test_notebook_is_idle(native, name, meta, minutes, want):
-    nb = {"metadata": meta}
+    ann = {k: _rfc(v.minutes) if isinstance(v, _Now) else v for k, v in meta.get("annotations", {}).items()}
+    nb = {"metadata": {**meta, "annotations": ann}} if "annotations" in meta else {"metadata": meta}
     assert native.call("notebook_is_idle", notebook=nb, cull_idle_minutes=minutes) is want
 
 
