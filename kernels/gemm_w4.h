@@ -330,8 +330,8 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   static_assert(SPLIT != 2 || BM == 256, "split-K fixup: 256 tile");
   static_assert(!SK || (!HAS_AUX && BM == 256 && !SPLIT), "stream-K: 256 tile, no pre-activation output");
   static_assert(!PO || (BM == 256 && !SPLIT && !SK && !DIAG), "persistent overlapped: 256 tile, whole K");
-  static_assert(!GRP || (!SPLIT && !SK && !PO && !DACT && !HAS_BIAS && !HAS_RES && !HAS_AUX && !DIAG),
-                "grouped pair: plain epilogue, one tile per block");
+  static_assert(!GRP || (SPLIT != 1 && !SK && !PO && !DACT && !HAS_BIAS && !HAS_RES && !HAS_AUX && !DIAG),
+                "grouped pair: plain epilogue, whole K or the in-kernel split-K fixup");
   static_assert(!DACT || (HAS_RES && !HAS_BIAS && !HAS_AUX && ACT != KFAMD_ACT_NONE && !SPLIT && !SK && !PO),
                 "act-grad epilogue: the pre-activation as R, 256 tile, whole K");
   // PO: the epilogue's LDS staging lives in the ring's fifth slot, which the next tile's prologue
@@ -350,10 +350,13 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 
   int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, nwg = tiles_m * tiles_n;
   int wg;
+  int grp_base = 0, nwg_all = nwg;  // GRP: this problem's first tile / both problems' tiles (split-K slots)
   if constexpr (GRP) {
     const int t1 = nwg, t2 = ((g2.M + BM - 1) / BM) * ((g2.N + BN - 1) / BN);
+    nwg_all = t1 + t2;
     wg = xcd_remap(blockIdx.x, t1 + t2);
     if (wg >= t1) {  // problem 2 (uniform per block)
+      grp_base = t1;
       wg -= t1;
       A = g2.A;
       B = g2.B;
@@ -1393,9 +1396,9 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
 #endif
     constexpr int kFixPol = (KFW4_FIX_AB & 4) ? 0 : 16;  // sc1
     const int el = lane_id_fresh();
-    const long long tile_id = (long long)blockIdx.y * nwg + wg;
+    const long long tile_id = (long long)blockIdx.y * nwg_all + grp_base + wg;
     constexpr long long kPerTile = (long long)BM * BN;  // floats
-    const long long zstride = (long long)gridDim.y * nwg * kPerTile;
+    const long long zstride = (long long)gridDim.y * nwg_all * kPerTile;
     const unsigned lane_off = (unsigned)(wid * (NR * NR * 1024) + el * 16);
     {
       __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(

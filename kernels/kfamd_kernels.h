@@ -129,6 +129,12 @@ int kfamd_colsum_finalize(const float* ws, void* db, int db_bf16, int nblk, int 
 int kfamd_w4_wgrad_pair(const void* A1, const void* B1, void* C1, int M1, long long lda1, long long ldb1,
                         long long ldc1, const void* A2, const void* B2, void* C2, int M2, long long lda2,
                         long long ldb2, long long ldc2, int N, int K, void* stream);
+// the same with problem 2's own width N2 and, for splits > 1, K split in kper pieces with the in-kernel
+// fixup (W: splits x tiles fp32 256 x 256 partials, cnt: tiles arrival counters, zero on entry and exit)
+int kfamd_w4_wgrad_pair_v2(const void* A1, const void* B1, void* C1, int M1, long long lda1, long long ldb1,
+                           long long ldc1, const void* A2, const void* B2, void* C2, int M2, long long lda2,
+                           long long ldb2, long long ldc2, int N, int N2, int K, int splits, int kper, float* W,
+                           unsigned* cnt, void* stream);
 long long kfamd_w4_dgrad_act_workspace(int M, int N);
 int kfamd_w4_dgrad_act(const void* dy, const void* w, void* g, const void* z, int M, int N, int K, long long lda,
                        long long ldb, long long ldg, long long ldz, int act, float* ws, void* db, int db_bf16,

@@ -56,6 +56,8 @@ _SIGNATURES = {
     "kfamd_w4_dgrad_act_workspace": (c_ll, [c_int, c_int]),
     "kfamd_w4_wgrad_pair": (c_int, [c_vp, c_vp, c_vp, c_int, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_ll, c_ll,
                                     c_ll, c_int, c_int, c_vp]),
+    "kfamd_w4_wgrad_pair_v2": (c_int, [c_vp, c_vp, c_vp, c_int, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_ll,
+                                       c_ll, c_ll, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "kfamd_w4_dgrad_act": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_int, c_vp,
                                    c_vp, c_int, c_vp]),
     "kfamd_layernorm_fwd_bf16": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_vp]),

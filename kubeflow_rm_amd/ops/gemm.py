@@ -610,37 +610,74 @@ def dgrad_act(gy2: torch.Tensor, weight: torch.Tensor, z: torch.Tensor, act: str
     return g, db
 
 
-def wgrad_pair(g1: torch.Tensor, x1: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, force: bool = False):
-    """(g1^T x1, g2^T x2) — two weight gradients (g_i [K][M_i], x_i [K][N]) as one launch of the w4
+_pair_ws: dict = {}  # (device, stream) -> [W fp32 partial tiles, arrival counters]
+WGRAD_PAIR = os.environ.get("KFAMD_WGRAD_PAIR", "1") != "0"  # False: always two mm's (A/B runs)
+
+
+def pair_plan(M1: int, N1: int, M2: int, N2: int, K: int) -> tuple[int, int] | None:
+    """(splits, kper) for one launch of two weight gradients ([M_i][N_i] over K), or None when apart
+    is better: together they stay within one wave of the 256 CUs and each alone under-fills it;
+    below three quarters of a wave the K range splits (in-kernel fixup) until the blocks fill it."""
+    t1, t2 = -(-M1 // 256) * -(-N1 // 256), -(-M2 // 256) * -(-N2 // 256)
+    if not WGRAD_PAIR or t1 >= _NUM_CUS or t2 >= _NUM_CUS or t1 + t2 > _NUM_CUS:
+        return None
+    if t1 + t2 >= _NUM_CUS * 3 // 4:
+        return 1, 0
+    splits = min(_NUM_CUS // (t1 + t2), -(-K // 64) // _FIXK_MIN_KT, 64)
+    if splits < 2:
+        return None
+    kper = _round_up(-(-K // splits), 64)
+    splits = -(-K // kper)
+    return (splits, kper) if splits >= 2 else None
+
+
+def wgrad_pair(g1: torch.Tensor, x1: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, force: bool = False,
+               plan: tuple[int, int] | None = None):
+    """(g1^T x1, g2^T x2) — two weight gradients (g_i [K][M_i], x_i [K][N_i]) as one launch of the w4
     kernel (kernels/tu/w4_wgrad_pair.hip) when together they fill the chip's 256 CUs far better than
-    apart (a transformer block's QKV + output projection: 192 + 64 tiles at gpt-1b); else None and
-    the caller runs two ``mm``s (which split K where a problem alone under-fills the chip).
-    ``force``: launch whenever the shapes fit the kernel (tests)."""
+    apart (pair_plan): a transformer block's QKV + output projection at gpt-1b (192 + 64 tiles), or
+    an MLP's / attention block's pair at small widths with K split by the in-kernel fixup (gpt-small:
+    36 + 36 and 27 + 9 tiles). Else None and the caller runs two ``mm``s. ``force`` launches whenever
+    the shapes fit the kernel, with ``plan`` (default: whole K) — tests."""
     if any(t.dim() != 2 or t.dtype != torch.bfloat16 or t.stride(-1) != 1 for t in (g1, x1, g2, x2)):
         return None
     K, M1 = g1.shape
-    M2, N = g2.shape[1], x1.shape[1]
-    if g2.shape[0] != K or tuple(x1.shape) != (K, N) or tuple(x2.shape) != (K, N) or min(M1, M2, N) < 256:
+    M2, N1, N2 = g2.shape[1], x1.shape[1], x2.shape[1]
+    if g2.shape[0] != K or x1.shape[0] != K or x2.shape[0] != K or min(M1, M2, N1, N2) < 256:
         return None
-    t1, t2 = -(-M1 // 256) * -(-N // 256), -(-M2 // 256) * -(-N // 256)
-    if not force and not (t1 < _NUM_CUS and t2 < _NUM_CUS and _NUM_CUS * 3 // 4 <= t1 + t2 <= _NUM_CUS):
+    plan = (plan or (1, 0)) if force else pair_plan(M1, N1, M2, N2, K)
+    if plan is None:
         return None
-    o1 = torch.empty(M1, N, dtype=torch.bfloat16, device=g1.device)
-    o2 = torch.empty(M2, N, dtype=torch.bfloat16, device=g1.device)
-    rc = _lib.lib().kfamd_w4_wgrad_pair(g1.data_ptr(), x1.data_ptr(), o1.data_ptr(), M1, g1.stride(0), x1.stride(0), N,
-                                        g2.data_ptr(), x2.data_ptr(), o2.data_ptr(), M2, g2.stride(0), x2.stride(0), N,
-                                        N, K, _stream_ptr(g1))
+    splits, kper = plan
+    o1 = torch.empty(M1, N1, dtype=torch.bfloat16, device=g1.device)
+    o2 = torch.empty(M2, N2, dtype=torch.bfloat16, device=g1.device)
+    W = cnt = None
+    if splits > 1:
+        tiles = -(-M1 // 256) * -(-N1 // 256) + -(-M2 // 256) * -(-N2 // 256)
+        key = (g1.device, _stream_ptr(g1))
+        ws = _pair_ws.get(key)
+        need = splits * tiles * 256 * 256
+        if ws is None or ws[0].numel() < need or ws[1].numel() < tiles:
+            old = (ws[0].numel(), ws[1].numel()) if ws is not None else (0, 0)
+            ws = [torch.empty(max(need, old[0]), dtype=torch.float32, device=g1.device),
+                  torch.zeros(max(tiles, old[1], 256), dtype=torch.int32, device=g1.device)]
+            _pair_ws[key] = ws
+        W, cnt = ws[0].data_ptr(), ws[1].data_ptr()
+    rc = _lib.lib().kfamd_w4_wgrad_pair_v2(g1.data_ptr(), x1.data_ptr(), o1.data_ptr(), M1, g1.stride(0), x1.stride(0),
+                                           N1, g2.data_ptr(), x2.data_ptr(), o2.data_ptr(), M2, g2.stride(0),
+                                           x2.stride(0), N2, N1, N2, K, splits, kper, W, cnt, _stream_ptr(g1))
     if rc < 0:
         return None
-    _lib.check(rc, f"wgrad_pair[{M1}+{M2}x{N}x{K}]")
+    _lib.check(rc, f"wgrad_pair[{M1}x{N1}+{M2}x{N2}x{K}/{splits}]")
     return o1, o2
 
 
 class _MLP(torch.autograd.Function):
     """out = act(x W1^T + b1) W2^T + b2 (+ residual) as one autograd node, so that fc2's dgrad can
-    apply fc1's activation backward in its epilogue (dgrad_act): the backward runs fc2's bias and
-    weight gradients, ONE GEMM for dH * act'(z1) (+ fc1's bias-gradient partials), then fc1's dgrad
-    and wgrad. The forward is the two linears' (gemm_nt_preact, gemm_nt with bias / residual)."""
+    apply fc1's activation backward in its epilogue (dgrad_act): the backward runs fc2's bias
+    gradient, ONE GEMM for dH * act'(z1) (+ fc1's bias-gradient partials), fc1's dgrad, then both
+    weight gradients (one launch where they under-fill the chip, wgrad_pair). The forward is the two
+    linears' (gemm_nt_preact, gemm_nt with bias / residual)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, act, residual):
@@ -667,7 +704,6 @@ class _MLP(torch.autograd.Function):
         need_db1 = b1 is not None and ni[2]
         _, db2 = act_grad(gy2, None, "none", need_db2,
                           db_dtype=torch.bfloat16 if need_db2 and b2.dtype == torch.bfloat16 else torch.float32)
-        gw2 = mm(gy2, y1, trans_a=True) if ni[3] else None
         db1_dtype = torch.bfloat16 if need_db1 and b1.dtype == torch.bfloat16 else torch.float32
         fused = dgrad_act(gy2, w2, z1, ctx.act, need_db1, db1_dtype)
         if fused is None:
@@ -675,7 +711,14 @@ class _MLP(torch.autograd.Function):
         else:
             g1, db1 = fused
         gx = mm(g1, w1).reshape(ctx.xshape) if ni[0] else None
-        gw1 = mm(g1, x2, trans_a=True) if ni[1] else None
+        # both weight gradients in one launch where apart they would under-fill the chip (small
+        # widths: K split in-kernel, wgrad_pair); else one mm each
+        pair = wgrad_pair(g1, x2, gy2, y1) if ni[1] and ni[3] else None
+        if pair is not None:
+            gw1, gw2 = pair
+        else:
+            gw1 = mm(g1, x2, trans_a=True) if ni[1] else None
+            gw2 = mm(gy2, y1, trans_a=True) if ni[3] else None
         gb1 = db1.to(b1.dtype) if need_db1 else None
         gb2 = db2.to(b2.dtype) if need_db2 else None
         return gx, gw1, gb1, gw2, gb2, None, (gy if ni[6] else None)

@@ -775,14 +775,18 @@ def test_mlp_matches_fp32(fused, act):
         assert err <= 3e-2 * (ref.abs().max().item() + 1e-3) + 1e-2, err
 
 
-@pytest.mark.parametrize("K,M1,M2,N", [(512, 768, 256, 512), (1000, 6144, 2048, 2048), (384, 296, 520, 264)])
-def test_wgrad_pair_matches_fp32(K, M1, M2, N):
+@pytest.mark.parametrize("K,M1,M2,N,N2,plan", [(512, 768, 256, 512, 512, None), (1000, 6144, 2048, 2048, 2048, None),
+                                                (384, 296, 520, 264, 264, None), (4096, 768, 256, 256, 768, (3, 1408)),
+                                                (4000, 3072, 768, 768, 3072, (2, 2048)),
+                                                (2112, 520, 296, 264, 520, (5, 448))])
+def test_wgrad_pair_matches_fp32(K, M1, M2, N, N2, plan):
     """Two weight gradients in one launch (gemm_w4.h GRP): each against its fp32 product, including
-    edge tiles (M / N not multiples of 256) and a K that is not a multiple of 64."""
+    edge tiles (M / N not multiples of 256), a K that is not a multiple of 64, a second problem of
+    its own width, and K split with the in-kernel fixup (SPLIT == 2) across both problems' tiles."""
     from kubeflow_rm_amd import ops
     g1, x1 = _rand(K, M1, seed=91), _rand(K, N, seed=92)
-    g2, x2 = _rand(K, M2, seed=93), _rand(K, N, seed=94)
-    out = ops.wgrad_pair(g1, x1, g2, x2, force=True)
+    g2, x2 = _rand(K, M2, seed=93), _rand(K, N2, seed=94)
+    out = ops.wgrad_pair(g1, x1, g2, x2, force=True, plan=plan)
     assert out is not None
     for got, (g, x) in zip(out, ((g1, x1), (g2, x2))):
         _assert_close(got, g.float().t() @ x.float(), K)
