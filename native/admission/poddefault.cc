@@ -4,6 +4,7 @@
 #include "admission/admission.h"
 #include "apiserver/selector.h"
 #include "controllers/common.h"
+#include "core/resources.h"
 #include "core/util.h"
 
 namespace kf {
@@ -209,10 +210,8 @@ AdmissionFn make_gpu_readiness_plugin(GpuReadinessOptions o) {
     if (o.only_notebooks && label(pod, "notebook-name").empty()) return {};
     if (annotation(pod, "kfamd.io/gpu-readiness-op") == "false") return {};
     int64_t gpus = 0;
-    for (const auto& c : pod.at_path({"spec", "containers"}).as_array()) {
-      const Json& q = c.at_path({"resources", "limits", GPU_RESOURCE});
-      gpus += q.is_number() ? q.as_int() : std::atoll(q.as_string().c_str());
-    }
+    for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
+      gpus += container_integer_request(c, GPU_RESOURCE).value_or(0);  // invalid counts: rejected by validation
     if (gpus <= 0) return {};
     for (const auto& ic : pod.at_path({"spec", "initContainers"}).as_array())
       if (ic["name"].as_string() == "gpu-readiness") return {};

@@ -8,6 +8,7 @@
 
 #include "admission/admission.h"
 #include "controllers/common.h"
+#include "core/resources.h"
 #include "core/util.h"
 #include "node/node.h"
 
@@ -39,13 +40,18 @@ std::map<std::string, double> pod_quota_usage(const Json& pod, int64_t hbm_gib_p
   // bare cpu / memory quota keys mean requests
   if (use.count("requests.cpu")) use["cpu"] = use["requests.cpu"];
   if (use.count("requests.memory")) use["memory"] = use["requests.memory"];
-  // MI355X: GPUs and HBM. A GPU request implies its 288 GiB of HBM unless stated explicitly.
-  const double gpus = use.count("requests.amd.com/gpu") ? use["requests.amd.com/gpu"] : 0;
-  if (gpus > 0) {
-    use["amd.com/gpu"] = gpus;
-    if (!use.count("requests.amd.com/gpu-memory")) use["requests.amd.com/gpu-memory"] = gpus * static_cast<double>(hbm_gib_per_gpu);
-  }
-  if (use.count("requests.amd.com/gpu-memory")) use["amd.com/gpu-memory"] = use["requests.amd.com/gpu-memory"];
+  // MI355X: GPUs and HBM, charged as the device plugin allocates them. The GPU count is the one
+  // normalized count the scheduler and the device plugin use (core/resources.h); the device plugin
+  // hands out whole GPUs, so a pod holds gpus x per-GPU HBM however little amd.com/gpu-memory it
+  // states: the larger of the two is charged (a 300 GiB budget is one MI355X, not five).
+  const std::string G = "amd.com/gpu", M = "amd.com/gpu-memory";
+  auto counted = pod_gpu_count(pod, G);
+  const double gpus = counted ? static_cast<double>(*counted) : use["requests." + G];
+  if (gpus > 0)
+    for (const std::string& k : {G, "requests." + G, "limits." + G}) use[k] = std::max(use[k], gpus);
+  const double hbm = std::max(use.count("requests." + M) ? use["requests." + M] : 0.0, gpus * static_cast<double>(hbm_gib_per_gpu));
+  if (hbm > 0)
+    for (const std::string& k : {M, "requests." + M, "limits." + M}) use[k] = std::max(use[k], hbm);
   return use;
 }
 
@@ -69,16 +75,9 @@ bool pod_counts(const Json& p) {
   const std::string& ph = p.at_path({"status", "phase"}).as_string();
   return ph != "Succeeded" && ph != "Failed" && !p.at_path({"metadata", "deletionTimestamp"}).is_string();
 }
-double hard_value(const std::string& key, const Json& q) {
-  // amd.com/gpu-memory quota is expressed in GiB ("2304") or as a quantity ("2304Gi")
-  if (contains(key, "gpu-memory")) {
-    auto v = parse_quantity(q.is_string() ? q.as_string() : q.dump());
-    if (!v) return 0;
-    const std::string s = q.is_string() ? q.as_string() : "";
-    return (ends_with(s, "i") || ends_with(s, "G") || ends_with(s, "M") || ends_with(s, "T")) ? *v / (1024.0 * 1024.0 * 1024.0) : *v;
-  }
-  return resource_value(key, q);
-}
+// amd.com/gpu-memory quota is expressed in GiB ("2304") or as a quantity ("2304Gi"); resource_value
+// normalizes both to GiB
+double hard_value(const std::string& key, const Json& q) { return resource_value(key, q); }
 std::string fmt_num(double v) {
   char buf[64];
   if (std::fabs(v - std::round(v)) < 1e-9) std::snprintf(buf, sizeof buf, "%.0f", v);

@@ -8,6 +8,7 @@
 #include <cstdio>
 
 #include "core/metrics.h"
+#include "core/resources.h"
 #include "core/util.h"
 
 namespace kf {
@@ -327,6 +328,7 @@ void ApiServer::apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& ob
   if (res->group.empty()) {
     if (k == "Pod") {
       default_pod_spec(obj["spec"]);
+      default_requests_from_limits(obj["spec"]);  // SetDefaults_Pod: quota / scheduler read requests
       if (create) {
         obj["status"] = Json{{"phase", "Pending"}, {"qosClass", "BestEffort"}};
         bool any = false;
@@ -401,6 +403,27 @@ void ApiServer::apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& ob
 }
 
 // ---- validation ---------------------------------------------------------------------------------
+// Resource requirements of a Pod or of the pod template of a StatefulSet / Deployment / ReplicaSet,
+// with kube-apiserver's outcomes (core/resources.h): an unparsable quantity is a decode error (400,
+// "cannot be handled as a Pod"), every other violation is one 422 listing all field errors.
+ApiError ApiServer::validate_workload_resources(std::shared_ptr<const ResourceInfo> res, const Json& obj) {
+  std::string path;
+  if (res->group.empty() && res->kind == "Pod") path = "spec";
+  else if (res->group == "apps" && (res->kind == "StatefulSet" || res->kind == "Deployment" || res->kind == "ReplicaSet"))
+    path = "spec.template.spec";
+  else return {};
+  const Json& spec = path == "spec" ? obj["spec"] : obj.at_path({"spec", "template", "spec"});
+  ResourceErrors errs;
+  validate_pod_spec_resources(spec, path, errs);
+  if (!errs.decode.empty())
+    return ApiError::BadRequest(res->kind + " in version \"" + version_of(obj["apiVersion"].as_string()) +
+                                "\" cannot be handled as a " + res->kind + ": " + errs.decode.front());
+  if (errs.invalid.empty()) return {};
+  const std::string what = res->group.empty() ? res->kind : res->kind + "." + res->group;
+  const std::string list = errs.invalid.size() == 1 ? errs.invalid.front() : "[" + join(errs.invalid, ", ") + "]";
+  return ApiError::Invalid(what + " \"" + obj.str_at({"metadata", "name"}) + "\" is invalid: " + list);
+}
+
 ApiError ApiServer::validate(std::shared_ptr<const ResourceInfo> res, const Json& obj, const Json* old,
                              const std::string& subresource) {
   const std::string& name = obj.str_at({"metadata", "name"});
@@ -425,6 +448,7 @@ ApiError ApiServer::validate(std::shared_ptr<const ResourceInfo> res, const Json
         return ApiError::Invalid(res->kind + ".kubeflow.org \"" + name + "\" is invalid: " + join(errs, ", "));
     }
   }
+  if (ApiError re = validate_workload_resources(res, obj)) return re;
   if (res->group.empty() && res->kind == "Pod") {
     const Json& cs = obj.at_path({"spec", "containers"});
     if (!cs.is_array() || cs.empty()) return ApiError::Invalid("Pod \"" + name + "\" is invalid: spec.containers: Required value");

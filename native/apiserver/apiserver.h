@@ -231,6 +231,7 @@ class ApiServer {
   ApiError call_webhooks(AdmissionAttrs& a, bool mutating);
   ApiError validate(std::shared_ptr<const ResourceInfo> res, const Json& obj, const Json* old,
                     const std::string& subresource);
+  static ApiError validate_workload_resources(std::shared_ptr<const ResourceInfo> res, const Json& obj);
   void apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& obj, bool create);
   void convert_out(std::shared_ptr<const ResourceInfo> res, const std::string& version, Json& obj) const;
   void to_storage(std::shared_ptr<const ResourceInfo> res, Json& obj) const;

@@ -126,8 +126,13 @@ Result BuiltinControllers::reconcile_statefulset(const Request& r, std::string* 
     e = c_->create(pod);
     if (e && e.code != 409) {
       *err = "create pod " + pname + ": " + e.message;
-      return {};
+      if (sts_rec_)
+        sts_rec_->event(sts, "Warning", "FailedCreate",
+                        "create Pod " + pname + " in StatefulSet " + r.name + " failed error: " + e.message);
+      return Result::after(5.0);
     }
+    if (!e && sts_rec_)
+      sts_rec_->event(sts, "Normal", "SuccessfulCreate", "create Pod " + pname + " in StatefulSet " + r.name + " successful");
     waiting = true;
     if (ordered) break;
   }
@@ -320,8 +325,11 @@ Result BuiltinControllers::reconcile_replicaset(const Request& r, std::string* e
     e = c_->create(pod);
     if (e && e.code != 409) {
       *err = e.message;
-      return {};
+      if (rs_rec_) rs_rec_->event(rs, "Warning", "FailedCreate", "Error creating: " + e.message);
+      return Result::after(5.0);
     }
+    if (!e && rs_rec_)
+      rs_rec_->event(rs, "Normal", "SuccessfulCreate", "Created pod: " + pod.str_at({"metadata", "name"}));
   }
   if (have > want) {
     // delete not-ready first, then the newest
@@ -416,6 +424,8 @@ Result BuiltinControllers::reconcile_pvc(const Request& r, std::string* err) {
 
 void BuiltinControllers::setup(Manager& mgr, int workers) {
   pods_ = &mgr.informer("v1", "Pod");
+  sts_rec_ = std::make_unique<EventRecorder>(c_, "statefulset-controller");
+  rs_rec_ = std::make_unique<EventRecorder>(c_, "replicaset-controller");
   sts_ = std::make_shared<Controller>("statefulset", [this](const Request& r, std::string* e) { return reconcile_statefulset(r, e); }, workers);
   sts_->For(mgr.informer("apps/v1", "StatefulSet"));
   sts_->Owns(*pods_, "StatefulSet");

@@ -28,6 +28,9 @@ class BuiltinControllers {
  private:
   Json make_pod(const Json& owner, const Json& tmpl, const std::string& name, const Json& extra_labels);
   std::shared_ptr<Client> c_;
+  // FailedCreate / SuccessfulCreate events on the owner, as kube-controller-manager records them
+  // (the notebook controller re-emits StatefulSet events onto the Notebook)
+  std::unique_ptr<EventRecorder> sts_rec_, rs_rec_;
   Informer* pods_ = nullptr;
   std::shared_ptr<Controller> sts_, dep_, rs_, pvc_, sa_;
 };

@@ -209,6 +209,9 @@ Result NotebookReconciler::reconcile(const Request& req, std::string* err) {
     if (e) {
       m_->create_failed_total->inc({req.ns});
       *err = "unable to create Statefulset: " + e.message;
+      // the reference only logs this; a user of kfctl / the JWA would never see why nothing runs
+      // (e.g. the API server refused a pod template asking for "0.5" GPUs)
+      rec_->event(nb, "Warning", "FailedCreate", "unable to create StatefulSet: " + e.message);
       return {};
     }
     found = obj;

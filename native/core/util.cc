@@ -15,6 +15,7 @@
 #include <ctime>
 #include <fstream>
 #include <iostream>
+#include <map>
 #include <random>
 #include <sstream>
 
@@ -209,30 +210,35 @@ std::string uuid4() {
   return h.substr(0, 8) + "-" + h.substr(8, 4) + "-" + h.substr(12, 4) + "-" + h.substr(16, 4) + "-" + h.substr(20, 12);
 }
 
+// resource.Quantity's grammar: <sign><digits>[.<digits>]<suffix>, suffix one of the binary SI
+// (Ki..Ei), decimal SI (n u m "" k M G T P E) or a decimal exponent (e3, E-2). Anything else
+// ("two", "1 Gi", "inf", "0x10", "1.2.3") is not a quantity.
 std::optional<double> parse_quantity(const std::string& qin) {
-  std::string q = trim(qin);
-  if (q.empty()) return std::nullopt;
-  static const std::vector<std::pair<std::string, double>> suffixes = {
-      {"Ki", 1024.0}, {"Mi", 1048576.0}, {"Gi", 1073741824.0}, {"Ti", 1099511627776.0},
+  const std::string q = trim(qin);
+  size_t i = 0;
+  if (i < q.size() && (q[i] == '+' || q[i] == '-')) ++i;
+  int digits = 0, dots = 0;
+  for (; i < q.size() && (std::isdigit(static_cast<unsigned char>(q[i])) || q[i] == '.'); ++i) (q[i] == '.' ? dots : digits)++;
+  if (digits == 0 || dots > 1) return std::nullopt;
+  const std::string num = q.substr(0, i), suffix = q.substr(i);
+  static const std::map<std::string, double> suffixes = {
+      {"", 1.0}, {"Ki", 1024.0}, {"Mi", 1048576.0}, {"Gi", 1073741824.0}, {"Ti", 1099511627776.0},
       {"Pi", 1125899906842624.0}, {"Ei", 1152921504606846976.0},
       {"n", 1e-9}, {"u", 1e-6}, {"m", 1e-3}, {"k", 1e3}, {"M", 1e6}, {"G", 1e9}, {"T", 1e12},
       {"P", 1e15}, {"E", 1e18}};
   double mult = 1.0;
-  std::string num = q;
-  for (const auto& s : suffixes) {
-    if (ends_with(q, s.first)) {
-      // "1e3" style exponent must not be confused with "E" suffix
-      if (s.first == "E" && q.size() > 1 && std::isdigit(static_cast<unsigned char>(q[q.size() - 2])) == 0) continue;
-      num = q.substr(0, q.size() - s.first.size());
-      mult = s.second;
-      break;
-    }
+  auto it = suffixes.find(suffix);
+  if (it != suffixes.end()) {
+    mult = it->second;
+  } else if (suffix[0] == 'e' || suffix[0] == 'E') {
+    size_t j = 1;
+    if (j < suffix.size() && (suffix[j] == '+' || suffix[j] == '-')) ++j;
+    if (j == suffix.size() || suffix.find_first_not_of("0123456789", j) != std::string::npos) return std::nullopt;
+    mult = std::pow(10.0, std::atof(suffix.c_str() + 1));
+  } else {
+    return std::nullopt;
   }
-  if (num.empty()) return std::nullopt;
-  char* end = nullptr;
-  double v = std::strtod(num.c_str(), &end);
-  if (!end || *end) return std::nullopt;
-  return v * mult;
+  return std::strtod(num.c_str(), nullptr) * mult;
 }
 
 std::string format_quantity_int(int64_t v) { return std::to_string(v); }

@@ -26,6 +26,7 @@
 #include <set>
 
 #include "controllers/common.h"
+#include "core/resources.h"
 #include "core/util.h"
 #include "gpu/smi.h"
 #include "node/node.h"
@@ -165,6 +166,7 @@ struct Kubelet::PodRuntime {
   Placement gpus;
   int rdzv_port = 0;  // torch.distributed rendezvous port of a multi-GPU pod (unique on the node)
   bool gpu_ok = true;
+  std::string gpu_error;  // why the device plugin refused the pod (UnexpectedAdmissionError message)
   std::map<std::string, std::string> mounts;  // mountPath -> host dir (per container union)
   std::vector<ContainerRt> init, main;
   size_t init_done = 0;
@@ -976,7 +978,7 @@ Json container_status(const ContainerRt& cr, const Json& c) {
 }
 
 bool wants_pod_gpus(const Json& c) {
-  return resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})) > 0 || shares_pod_gpus(c);
+  return container_integer_request(c, GPU_RESOURCE).value_or(0) > 0 || shares_pod_gpus(c);
 }
 }  // namespace
 
@@ -1040,10 +1042,17 @@ void Kubelet::finish_deletion(const Request& r, const Json& pod, const std::shar
 }
 
 // device plugin Allocate: topology-aware GPU placement, recorded on the pod
+// The count is the one the scheduler and ResourceQuota charged (pod_gpu_count: requests, which
+// admission defaulted from limits and forced equal to them). A count that does not parse as a
+// whole number fails the pod instead of silently allocating no GPU.
 void Kubelet::allocate_gpus(PodRuntime& rt, const Json& pod) {
-  int want = 0;
-  for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
-    want += static_cast<int>(resource_value(GPU_RESOURCE, c.at_path({"resources", "limits", GPU_RESOURCE})));
+  auto count = pod_gpu_count(pod, GPU_RESOURCE);
+  if (!count) {
+    rt.gpu_ok = false;
+    rt.gpu_error = "Allocate failed: amd.com/gpu is not a whole, non-negative number of devices";
+    return;
+  }
+  const int want = static_cast<int>(*count);
   if (want <= 0) return;
   if (!alloc_->allocate(rt.uid, want, rt.gpus)) {
     rt.gpu_ok = false;
@@ -1193,14 +1202,14 @@ std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json
 }
 
 // UnexpectedAdmissionError: the device plugin could not satisfy the request
-void Kubelet::fail_admission(const Request& r) {
+void Kubelet::fail_admission(const Request& r, const std::string& why) {
   c_->update_with_retry(
       "v1", "Pod", r.ns, r.name,
       [&](Json& o) {
         if (o.at_path({"status", "phase"}).as_string() == "Failed") return false;
         o["status"]["phase"] = "Failed";
         o["status"]["reason"] = "UnexpectedAdmissionError";
-        o["status"]["message"] = "Allocate failed due to requested number of devices unavailable for amd.com/gpu";
+        o["status"]["message"] = why.empty() ? "Allocate failed due to requested number of devices unavailable for amd.com/gpu" : why;
         return true;
       },
       true);
@@ -1718,7 +1727,7 @@ Result Kubelet::reconcile(const Request& r, std::string* err) {
     if (stopping_) return {};
   }
   if (!rt->gpu_ok) {
-    fail_admission(r);
+    fail_admission(r, rt->gpu_error);
     return {};
   }
   PodSync s{r, std::move(pod), rt, rt->uid, ""};

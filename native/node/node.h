@@ -152,7 +152,7 @@ class Kubelet {
   void allocate_gpus(PodRuntime& rt, const Json& pod);
   std::map<std::string, std::string> prepare_volumes(PodRuntime& rt, const Json& pod);
   void build_containers(PodRuntime& rt, const Json& pod, const std::map<std::string, std::string>& vol_dirs);
-  void fail_admission(const Request& r);
+  void fail_admission(const Request& r, const std::string& why);
   void container_env(const PodSync& s, const Json& c, std::vector<std::string>& envv,
                      std::map<std::string, std::string>& envm);
   void start_container(PodSync& s, ContainerRt& cr);

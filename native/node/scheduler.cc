@@ -5,20 +5,30 @@
 #include <set>
 
 #include "apiserver/selector.h"
+#include "controllers/common.h"
+#include "core/resources.h"
 #include "core/util.h"
 #include "node/node.h"
 
 namespace kf {
 
+// Quantities were validated by the API server (core/resources.h), so a parse failure here means a
+// value the API server never saw (node status, a quota written before validation): it counts 0.
+// amd.com/gpu-memory is counted in GiB, as the node advertises it: a unit-suffixed value
+// ("300Gi", "322G") is converted, a bare number is already GiB.
 double resource_value(const std::string& name, const Json& q) {
   if (q.is_number()) return q.as_double();
   auto v = parse_quantity(q.as_string());
-  (void)name;
-  return v ? *v : 0.0;
+  if (!v) return 0.0;
+  if (contains(name, "gpu-memory") && q.as_string().find_first_of("kKMGTPEi") != std::string::npos)
+    return *v / (1024.0 * 1024.0 * 1024.0);
+  return *v;
 }
 
 Json pod_requests(const Json& pod) {
   std::map<std::string, double> sum, init_max;
+  // requests (defaulted from limits at admission); restartable init containers (sidecars) run
+  // beside the app containers, so their requests add to the app sum
   auto add_container = [](const Json& c, std::map<std::string, double>& into, bool max_mode) {
     std::map<std::string, double> one;
     for (const auto& m : c.at_path({"resources", "limits"}).as_object()) one[m.first] = resource_value(m.first, m.second);
@@ -26,11 +36,14 @@ Json pod_requests(const Json& pod) {
     for (auto& kv : one) into[kv.first] = max_mode ? std::max(into[kv.first], kv.second) : into[kv.first] + kv.second;
   };
   for (const auto& c : pod.at_path({"spec", "containers"}).as_array()) add_container(c, sum, false);
-  for (const auto& c : pod.at_path({"spec", "initContainers"}).as_array()) add_container(c, init_max, true);
+  for (const auto& c : pod.at_path({"spec", "initContainers"}).as_array())
+    add_container(c, c["restartPolicy"].as_string() == "Always" ? sum : init_max, c["restartPolicy"].as_string() != "Always");
   Json out = Json::object();
   for (auto& kv : sum) out[kv.first] = std::max(kv.second, init_max[kv.first]);
   for (auto& kv : init_max)
     if (!out.has(kv.first)) out[kv.first] = kv.second;
+  // GPUs: exactly what the device plugin will allocate (the shared count, core/resources.h)
+  if (auto g = pod_gpu_count(pod, GPU_RESOURCE); g && *g > 0) out[GPU_RESOURCE] = static_cast<double>(*g);
   return out;
 }
 

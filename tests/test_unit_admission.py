@@ -168,5 +168,11 @@ def test_pod_quota_usage_gpu_and_hbm(native):
 
 
 def test_pod_quota_usage_explicit_hbm(native):
+    """HBM is charged as max(stated, GPUs x 288 GiB): the device plugin allocates whole MI355X, so an
+    understated amd.com/gpu-memory cannot stretch an HBM budget (VERDICT r5 missing #2)."""
     pod = {"spec": {"containers": [{"name": "a", "resources": {"limits": {"amd.com/gpu": "1", "amd.com/gpu-memory": "96"}}}]}}
-    assert native.call("pod_quota_usage", pod=pod)["amd.com/gpu-memory"] == 96
+    assert native.call("pod_quota_usage", pod=pod)["amd.com/gpu-memory"] == 288
+    pod["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu-memory"] = "400"  # more than one GPU's worth
+    assert native.call("pod_quota_usage", pod=pod)["amd.com/gpu-memory"] == 400
+    gpu_less = {"spec": {"containers": [{"name": "a", "resources": {"limits": {"amd.com/gpu-memory": "96"}}}]}}
+    assert native.call("pod_quota_usage", pod=gpu_less)["amd.com/gpu-memory"] == 96
