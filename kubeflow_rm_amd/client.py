@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import json
 import os
+import re
+import sys
 import threading
 import time
 import urllib.parse
@@ -47,6 +49,18 @@ def _split_api_version(api_version: str) -> tuple[str, str]:
 
 # Sanitizer builds of the control plane (tools/sanitize.sh) run 5-15x slower: every wait scales.
 _TIMEOUT_SCALE = float(os.environ.get("KFAMD_TIMEOUT_SCALE", "1"))
+_WARN_VALUE = re.compile(r'\d{3} [^ ]+ "((?:[^"\\]|\\.)*)"')
+
+
+def parse_warning_header(value: str) -> list[str]:
+    """RFC 7234 Warning header values (``299 - "unknown field \"spec.x\""``, comma-joined when the
+    server sent several) -> the warning texts, in order."""
+    return [json.loads(f'"{m.group(1)}"') for m in _WARN_VALUE.finditer(value or "")]
+
+
+def print_warning(text: str) -> None:
+    """kubectl's default warning handler: one ``Warning: <text>`` line on stderr."""
+    print(f"Warning: {text}", file=sys.stderr)
 
 
 _SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
@@ -93,6 +107,10 @@ class KubeClient:
                 self.headers["Impersonate-Group"] = ",".join(impersonate_groups)
         self._res: dict[tuple[str, str], tuple[str, bool]] = {}
         self._lock = threading.Lock()
+        # server warnings (unknown / pruned fields, deprecations): kept in ``warnings`` and passed to
+        # ``warning_handler`` (the CLIs set print_warning, as kubectl prints them)
+        self.warnings: list[str] = []
+        self.warning_handler: Callable[[str], None] | None = None
 
     # ---- plumbing ----------------------------------------------------------------------------
     def _req(self, method: str, path: str, body: Any = None, params: dict | None = None,
@@ -104,6 +122,11 @@ class KubeClient:
             headers["Content-Type"] = content_type
         r = self.session.request(method, self.base + path, data=data, params=params, headers=headers,
                                  timeout=timeout or self.timeout)
+        if "Warning" in r.headers:
+            for w in parse_warning_header(r.headers["Warning"]):
+                self.warnings.append(w)
+                if self.warning_handler:
+                    self.warning_handler(w)
         if raw:
             if r.status_code >= 400:
                 raise ApiException(r.status_code, r.reason, _safe_json(r.text))

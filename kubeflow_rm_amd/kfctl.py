@@ -21,7 +21,7 @@ import time
 from pathlib import Path
 
 from . import kustomize
-from .client import ApiException, KubeClient
+from .client import ApiException, KubeClient, print_warning
 
 ORDER = ["Namespace", "CustomResourceDefinition", "ClusterRole", "ClusterRoleBinding", "ServiceAccount", "Role",
          "RoleBinding", "ConfigMap", "Secret", "PersistentVolumeClaim", "Service", "Deployment", "StatefulSet",
@@ -138,6 +138,7 @@ def main(argv: list[str] | None = None) -> int:
         return kubectl.run(args.cmd, args)
     if args.cmd in ("apply", "delete"):
         client = KubeClient(args.server)
+        client.warning_handler = print_warning
         try:
             if args.filename:
                 objs = kubectl.load_docs(args.filename)

@@ -26,7 +26,7 @@ import sys
 import time
 from typing import Any, Callable
 
-from .client import ApiException, KubeClient
+from .client import ApiException, KubeClient, print_warning
 
 # short names kubectl knows for kinds whose discovery here carries none
 _EXTRA_SHORT = {"statefulsets": ["sts"], "deployments": ["deploy"], "replicasets": ["rs"], "daemonsets": ["ds"],
@@ -779,6 +779,8 @@ def run(verb: str, args, client: KubeClient | None = None) -> int:
             sys.stderr.write(str(e) + "\n")
             return 1
     client = client or KubeClient(getattr(args, "server", None))
+    if client.warning_handler is None:
+        client.warning_handler = print_warning
     if getattr(args, "namespace", None) is None and verb not in ("logs", "exec"):
         args.namespace = None if getattr(args, "all_namespaces", False) else "default"
     try:

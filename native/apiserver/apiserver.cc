@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 
+#include "apiserver/schemas.h"
 #include "core/metrics.h"
 #include "core/resources.h"
 #include "core/util.h"
@@ -185,6 +186,11 @@ void ApiServer::bootstrap() {
   for (Json crd : builtin_crds()) {
     Json existing;
     if (get("apiextensions.k8s.io/v1", "CustomResourceDefinition", "", crd.str_at({"metadata", "name"}), existing).ok()) {
+      if (existing["spec"] != crd["spec"]) {  // a data dir from an older build: serve this build's schemas
+        existing["spec"] = crd["spec"];
+        if (ApiError e = update(existing, sys))
+          KF_ERROR("apiserver", "bootstrap CRD update failed", Json{{"crd", crd.str_at({"metadata", "name"})}, {"error", e.message}});
+      }
       reg_.add_crd(existing);
       continue;
     }
@@ -400,6 +406,27 @@ void ApiServer::apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& ob
     if (spec.at_path({"template", "spec"}).is_object()) default_pod_spec(spec["template"]["spec"]);
     if (create && !obj.has("status")) obj["status"] = Json::object();
   }
+}
+
+// ---- structural schemas (CRDs) ----------------------------------------------------------------------
+ApiError ApiServer::structural(std::shared_ptr<const ResourceInfo> res, Json& obj, const WriteOptions& o, bool report) {
+  if (!res->is_crd) return {};
+  auto it = res->schemas.find(version_of(obj["apiVersion"].as_string()));
+  if (it == res->schemas.end()) it = res->schemas.find(res->storage_version);
+  if (it == res->schemas.end()) return {};
+  std::vector<std::string> pruned;
+  prune_unknown_fields(it->second, obj, report ? &pruned : nullptr);
+  apply_schema_defaults(it->second, obj);
+  if (pruned.empty()) return {};
+  if (o.field_validation == "Strict") {
+    std::vector<std::string> msgs;
+    for (const auto& p : pruned) msgs.push_back("unknown field \"" + p + "\"");
+    return ApiError::BadRequest(res->kind + " in version \"" + version_of(obj["apiVersion"].as_string()) +
+                                "\" cannot be handled as a " + res->kind + ": strict decoding error: " + join(msgs, ", "));
+  }
+  if (o.field_validation != "Ignore" && o.warnings)
+    for (const auto& p : pruned) o.warnings->push_back("unknown field \"" + p + "\"");
+  return {};
 }
 
 // ---- validation ---------------------------------------------------------------------------------
@@ -693,6 +720,7 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
     return {};
   }
 
+  if (ApiError se = structural(res, obj, o, true)) return se;
   apply_defaults(res, obj, true);
   AdmissionAttrs a;
   a.operation = "CREATE";
@@ -714,6 +742,7 @@ ApiError ApiServer::r_create(std::shared_ptr<const ResourceInfo> res, const std:
   err = run_admission(a, true);
   if (err) return err;
   apply_defaults(res, obj, false);  // mutating admission may add containers: default them too
+  structural(res, obj, o, false);    // ... and fields a webhook added are pruned too (silently)
   to_storage(res, obj);
   obj["metadata"]["namespace"] = ns;
   if (!res->namespaced) obj["metadata"].erase("namespace");
@@ -874,6 +903,7 @@ ApiError ApiServer::r_update(std::shared_ptr<const ResourceInfo> res, const std:
   md["generation"] = omd["generation"].as_int(1);
   next["apiVersion"] = res->api_version(version);
   next["kind"] = res->kind;
+  if (ApiError se = structural(res, next, o, subresource.empty())) return se;
   if (subresource.empty()) apply_defaults(res, next, false);
 
   AdmissionAttrs a;
@@ -890,6 +920,7 @@ ApiError ApiServer::r_update(std::shared_ptr<const ResourceInfo> res, const std:
   ApiError err = run_admission(a, true);
   if (err) return err;
   if (subresource.empty()) apply_defaults(res, next, false);
+  structural(res, next, o, false);
   to_storage(res, next);
   err = validate(res, next, &old, subresource);
   if (err) return err;

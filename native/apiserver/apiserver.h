@@ -70,6 +70,10 @@ struct WriteOptions {
   bool dry_run = false;
   UserInfo user;
   std::string field_manager;
+  // ?fieldValidation= for fields a structural CRD schema does not know: "Ignore" (prune silently),
+  // "Warn" (the default: prune and return a Warning header per field) or "Strict" (400)
+  std::string field_validation;
+  std::vector<std::string>* warnings = nullptr;  // where "Warn" appends (HTTP: Warning headers)
 };
 
 struct DeleteOptions {
@@ -232,6 +236,9 @@ class ApiServer {
   ApiError validate(std::shared_ptr<const ResourceInfo> res, const Json& obj, const Json* old,
                     const std::string& subresource);
   static ApiError validate_workload_resources(std::shared_ptr<const ResourceInfo> res, const Json& obj);
+  // structural CRD semantics on a write: prune unknown fields (reported per o.field_validation
+  // when `report`), then apply schema defaults
+  static ApiError structural(std::shared_ptr<const ResourceInfo> res, Json& obj, const WriteOptions& o, bool report);
   void apply_defaults(std::shared_ptr<const ResourceInfo> res, Json& obj, bool create);
   void convert_out(std::shared_ptr<const ResourceInfo> res, const std::string& version, Json& obj) const;
   void to_storage(std::shared_ptr<const ResourceInfo> res, Json& obj) const;
@@ -253,6 +260,24 @@ class ApiServer {
   void bootstrap_rbac();
   bool check_namespace(std::shared_ptr<const ResourceInfo> res, const std::string& ns, bool creating, ApiError& err);
   std::string alloc_cluster_ip();
+  // one parsed /api|/apis request (apiserver_http.cc: handle_http -> connect subresources | http_crud)
+  struct HttpTarget {
+    std::string group, version, ns, plural, name, sub, verb;
+    std::vector<std::string> rest;  // path segments from the resource on
+    std::shared_ptr<const ResourceInfo> res;
+    UserInfo user;
+    bool watch = false;
+  };
+  void http_faults(HttpRequest& req, HttpResponse& resp);
+  void http_group_discovery(HttpResponse& resp, const std::string& group);
+  bool http_connect_subresource(HttpRequest& req, HttpResponse& resp, const HttpTarget& t);
+  void http_token_request(HttpRequest& req, HttpResponse& resp, const HttpTarget& t);
+  void http_exec(HttpRequest& req, HttpResponse& resp, const HttpTarget& t);
+  void http_crud(HttpRequest& req, HttpResponse& resp, const HttpTarget& t);
+  ApiError http_write(HttpRequest& req, const HttpTarget& t, Json& body, const WriteOptions& wo, Json& out, int& code);
+  ApiError http_delete(HttpRequest& req, const HttpTarget& t, const WriteOptions& wo, Json& out);
+  static ListOptions list_options(HttpRequest& req);
+  static Json scale_view(const HttpTarget& t, const Json& obj);
   void http_discovery(HttpRequest& req, HttpResponse& resp, const std::vector<std::string>& segs);
   void http_watch(std::shared_ptr<const ResourceInfo> res, const std::string& version, const std::string& ns,
                   const ListOptions& lo, HttpResponse& resp);

@@ -184,18 +184,7 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
     return;
   }
   if (path == "/debug/faults") {
-    if (req.method == "DELETE") {
-      clear_faults();
-      resp.json(200, "{}");
-      return;
-    }
-    Json b;
-    if (!Json::try_parse(req.body, b)) {
-      resp.json(400, R"({"error":"body must be JSON {\"spec\": \"kind:plural:count[:arg]\"}"})");
-      return;
-    }
-    std::string err = inject_fault(b["spec"].as_string());
-    resp.json(err.empty() ? 200 : 400, Json{{"error", err}}.dump());
+    http_faults(req, resp);
     return;
   }
   auto segs = split(path, '/', true);
@@ -208,89 +197,264 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
     return;
   }
   if (segs.size() == 1 || (segs[0] == "api" && segs.size() == 2) || (segs[0] == "apis" && segs.size() <= 3)) {
-    if (segs[0] == "apis" && segs.size() == 2) {
-      // group discovery
-      Json vs = Json::array();
-      std::string pref;
-      for (const auto& r : reg_.all())
-        if (r->group == segs[1]) {
-          for (const auto& v : r->versions) {
-            Json e{{"groupVersion", segs[1] + "/" + v}, {"version", v}};
-            bool dup = false;
-            for (const auto& x : vs.as_array()) dup = dup || x == e;
-            if (!dup) vs.push_back(e);
-          }
-          pref = r->storage_version;
-        }
-      if (vs.empty()) {
-        send_error(resp, ApiError::NotFound("group", segs[1]));
-        return;
-      }
-      resp.json(200, Json{{"kind", "APIGroup"}, {"apiVersion", "v1"}, {"name", segs[1]}, {"versions", vs},
-                          {"preferredVersion", Json{{"groupVersion", segs[1] + "/" + pref}, {"version", pref}}}}.dump());
-      return;
-    }
-    http_discovery(req, resp, segs);
+    if (segs[0] == "apis" && segs.size() == 2) http_group_discovery(resp, segs[1]);
+    else http_discovery(req, resp, segs);
     return;
   }
-  std::string group, version;
+  HttpTarget t;
   size_t i;
   if (segs[0] == "api") {
-    version = segs[1];
+    t.version = segs[1];
     i = 2;
   } else {
-    group = segs[1];
-    version = segs[2];
+    t.group = segs[1];
+    t.version = segs[2];
     i = 3;
   }
-  std::string ns, plural, name, sub;
-  std::vector<std::string> rest(segs.begin() + static_cast<long>(i), segs.end());
-  if (rest.size() >= 2 && rest[0] == "namespaces" && group.empty() && rest.size() >= 3) {
-    ns = rest[1];
-    rest.erase(rest.begin(), rest.begin() + 2);
-  } else if (rest.size() >= 3 && rest[0] == "namespaces" && !group.empty()) {
-    ns = rest[1];
-    rest.erase(rest.begin(), rest.begin() + 2);
+  t.rest.assign(segs.begin() + static_cast<long>(i), segs.end());
+  if (t.rest.size() >= 3 && t.rest[0] == "namespaces") {
+    t.ns = t.rest[1];
+    t.rest.erase(t.rest.begin(), t.rest.begin() + 2);
   }
-  if (rest.empty()) {
+  if (t.rest.empty()) {
     send_error(resp, ApiError::NotFound("resource", path));
     return;
   }
-  plural = rest[0];
-  if (rest.size() > 1) name = rest[1];
-  if (rest.size() > 2) sub = rest[2];
-  auto res = reg_.by_plural(group, plural);
-  if (!res || !res->serves(version)) {
-    send_error(resp, ApiError::NotFound("the server could not find the requested resource", plural));
+  t.plural = t.rest[0];
+  if (t.rest.size() > 1) t.name = t.rest[1];
+  if (t.rest.size() > 2) t.sub = t.rest[2];
+  t.res = reg_.by_plural(t.group, t.plural);
+  if (!t.res || !t.res->serves(t.version)) {
+    send_error(resp, ApiError::NotFound("the server could not find the requested resource", t.plural));
     return;
   }
-  UserInfo user;
-  if (!authenticate(req, user)) {
+  if (!authenticate(req, t.user)) {
     resp.json(401, ApiError{401, "Unauthorized", "Unauthorized"}.status_json().dump());
     return;
   }
-  bool watch = req.q("watch") == "true" || req.q("watch") == "1";
-  std::string verb = verb_for(req.method, !name.empty(), watch);
+  t.watch = req.q("watch") == "true" || req.q("watch") == "1";
+  t.verb = verb_for(req.method, !t.name.empty(), t.watch);
   // pods/exec runs a command in the container whatever the HTTP method (kubectl upgrades a GET to a
   // stream): authorize it as "create", as Kubernetes does since CVE-2018-1002105's follow-ups, so a role
   // with only get on pods/* cannot run commands
-  if (group.empty() && plural == "pods" && (sub == "exec" || sub == "attach")) verb = "create";
-  std::string authz_sub = sub;
+  if (t.group.empty() && t.plural == "pods" && (t.sub == "exec" || t.sub == "attach")) t.verb = "create";
   if (cfg_.authz_rbac) {
     std::string reason;
-    if (!authorize(user, verb, group, plural, authz_sub, ns, name, &reason)) {
-      send_error(resp, ApiError::Forbidden(plural + (group.empty() ? "" : "." + group) + " \"" + name + "\" is forbidden: User \"" +
-                                           user.username + "\" cannot " + verb + " resource \"" + plural + "\" in API group \"" +
-                                           group + "\"" + (ns.empty() ? "" : " in the namespace \"" + ns + "\"")),
-                 res->kind, name);
+    if (!authorize(t.user, t.verb, t.group, t.plural, t.sub, t.ns, t.name, &reason)) {
+      send_error(resp, ApiError::Forbidden(t.plural + (t.group.empty() ? "" : "." + t.group) + " \"" + t.name +
+                                           "\" is forbidden: User \"" + t.user.username + "\" cannot " + t.verb +
+                                           " resource \"" + t.plural + "\" in API group \"" + t.group + "\"" +
+                                           (t.ns.empty() ? "" : " in the namespace \"" + t.ns + "\"")),
+                 t.res->kind, t.name);
       return;
     }
   }
-  double t0 = now_seconds();
+  if (http_connect_subresource(req, resp, t)) return;
+  if (!t.sub.empty() && t.sub != "status" && t.sub != "scale" && !(t.group.empty() && t.plural == "pods" && t.sub == "binding")) {
+    send_error(resp, ApiError::NotFound("subresource", t.sub));
+    return;
+  }
+  http_crud(req, resp, t);
+}
+
+void ApiServer::http_faults(HttpRequest& req, HttpResponse& resp) {
+  if (req.method == "DELETE") {
+    clear_faults();
+    resp.json(200, "{}");
+    return;
+  }
+  Json b;
+  if (!Json::try_parse(req.body, b)) {
+    resp.json(400, R"({"error":"body must be JSON {\"spec\": \"kind:plural:count[:arg]\"}"})");
+    return;
+  }
+  std::string err = inject_fault(b["spec"].as_string());
+  resp.json(err.empty() ? 200 : 400, Json{{"error", err}}.dump());
+}
+
+void ApiServer::http_group_discovery(HttpResponse& resp, const std::string& group) {
+  Json vs = Json::array();
+  std::string pref;
+  for (const auto& r : reg_.all())
+    if (r->group == group) {
+      for (const auto& v : r->versions) {
+        Json e{{"groupVersion", group + "/" + v}, {"version", v}};
+        bool dup = false;
+        for (const auto& x : vs.as_array()) dup = dup || x == e;
+        if (!dup) vs.push_back(e);
+      }
+      pref = r->storage_version;
+    }
+  if (vs.empty()) {
+    send_error(resp, ApiError::NotFound("group", group));
+    return;
+  }
+  resp.json(200, Json{{"kind", "APIGroup"}, {"apiVersion", "v1"}, {"name", group}, {"versions", vs},
+                      {"preferredVersion", Json{{"groupVersion", group + "/" + pref}, {"version", pref}}}}.dump());
+}
+
+// the connect-style subresources (pods/log, pods/exec, serviceaccounts/token, services/proxy):
+// true when one of them handled the request
+bool ApiServer::http_connect_subresource(HttpRequest& req, HttpResponse& resp, const HttpTarget& t) {
+  const bool core = t.res->group.empty();
+  if (core && t.plural == "pods" && t.sub == "log") {
+    std::string out;
+    if (!log_provider_ || !log_provider_(t.ns, t.name, req.q("container"), std::atoll(req.q("tailLines", "-1").c_str()), out)) {
+      Json p;
+      if (ApiError e = r_get(t.res, t.version, t.ns, t.name, p)) {
+        send_error(resp, e, "Pod", t.name);
+        return true;
+      }
+      resp.json(400, ApiError::BadRequest("container logs are not available for pod " + t.name).status_json().dump());
+      return true;
+    }
+    resp.text(200, out);
+    return true;
+  }
+  if (core && t.plural == "serviceaccounts" && t.sub == "token") {
+    http_token_request(req, resp, t);
+    return true;
+  }
+  if (core && t.plural == "pods" && t.sub == "exec") {
+    http_exec(req, resp, t);
+    return true;
+  }
+  if (core && t.plural == "services" && t.sub == "proxy") {
+    std::string r;
+    for (size_t k = 3; k < t.rest.size(); ++k) r += (k > 3 ? "/" : "") + t.rest[k];
+    if (ends_with(req.path, "/") && !r.empty()) r += "/";
+    http_proxy(req, resp, t.ns, t.name, r);
+    return true;
+  }
+  return false;
+}
+
+// TokenRequest (authentication.k8s.io/v1): a bound token for the ServiceAccount; authorized as
+// "create serviceaccounts/token"
+void ApiServer::http_token_request(HttpRequest& req, HttpResponse& resp, const HttpTarget& t) {
+  if (req.method != "POST") {
+    resp.json(405, ApiError{405, "MethodNotAllowed", "TokenRequest takes POST"}.status_json().dump());
+    return;
+  }
+  Json body;
+  if (!req.body.empty() && !Json::try_parse(req.body, body)) {
+    resp.json(400, ApiError::BadRequest("invalid TokenRequest body").status_json().dump());
+    return;
+  }
+  std::string token;
+  double exp = 0;
+  if (ApiError e = issue_sa_token(t.ns, t.name, body.at_path({"spec", "expirationSeconds"}).as_int(3600), token, exp)) {
+    send_error(resp, e, "ServiceAccount", t.name);
+    return;
+  }
+  Json spec = body["spec"].is_object() ? body["spec"] : Json::object();
+  resp.json(201, Json{{"apiVersion", "authentication.k8s.io/v1"}, {"kind", "TokenRequest"},
+                      {"metadata", Json{{"name", t.name}, {"namespace", t.ns}}}, {"spec", spec},
+                      {"status", Json{{"token", token},
+                                      {"expirationTimestamp", rfc3339_from_ms(static_cast<int64_t>(exp * 1000))}}}}
+                     .dump());
+}
+
+// kubectl exec without a TTY or stdin: ?command=a&command=b[&container=c][&timeoutSeconds=n];
+// reply {"exitCode": n, "output": "<stdout+stderr>"} (authorized as create pods/exec)
+void ApiServer::http_exec(HttpRequest& req, HttpResponse& resp, const HttpTarget& t) {
+  if (req.method != "POST" && req.method != "GET") {
+    resp.json(405, ApiError{405, "MethodNotAllowed", "exec takes POST"}.status_json().dump());
+    return;
+  }
+  auto it = req.query.find("command");
+  if (it == req.query.end() || it->second.empty()) {
+    resp.json(400, ApiError::BadRequest("you must specify at least one command for the container").status_json().dump());
+    return;
+  }
+  Json p;
+  if (ApiError e = r_get(t.res, t.version, t.ns, t.name, p)) {
+    send_error(resp, e, "Pod", t.name);
+    return;
+  }
+  // each exec holds an API server worker for its duration: at most kMaxConcurrentExec at once, so
+  // long execs can never starve controllers and watches of workers
+  static std::atomic<int> active_exec{0};
+  constexpr int kMaxConcurrentExec = 4;
+  if (active_exec.fetch_add(1) >= kMaxConcurrentExec) {
+    active_exec.fetch_sub(1);
+    resp.json(429, ApiError{429, "TooManyRequests", "too many concurrent exec sessions, retry later"}.status_json().dump());
+    return;
+  }
+  struct ExecSlot {
+    std::atomic<int>& n;
+    ~ExecSlot() { n.fetch_sub(1); }
+  } exec_slot{active_exec};
+  int code = 0;
+  std::string out, err;
+  const double timeout = std::min(3600.0, std::max(1.0, std::atof(req.q("timeoutSeconds", "30").c_str())));
+  if (!exec_provider_ || !exec_provider_(t.ns, t.name, req.q("container"), it->second, timeout, code, out, err)) {
+    resp.json(400, ApiError::BadRequest(err.empty() ? "exec is not available for pod " + t.name : err).status_json().dump());
+    return;
+  }
+  resp.json(200, Json{{"exitCode", static_cast<int64_t>(code)}, {"output", out}}.dump());
+}
+
+// the REST verbs on a resource / collection / status / scale / binding
+void ApiServer::http_crud(HttpRequest& req, HttpResponse& resp, const HttpTarget& t) {
+  const double t0 = now_seconds();
+  std::vector<std::string> warnings;
   WriteOptions wo;
-  wo.user = user;
+  wo.user = t.user;
   wo.dry_run = req.q("dryRun") == "All";
   wo.field_manager = req.q("fieldManager");
+  wo.field_validation = req.q("fieldValidation", "Warn");
+  wo.warnings = &warnings;
+  if (wo.field_validation != "Ignore" && wo.field_validation != "Warn" && wo.field_validation != "Strict") {
+    send_error(resp, ApiError::BadRequest("fieldValidation must be one of Ignore, Warn or Strict"));
+    return;
+  }
+  ApiError err;
+  Json out;
+  int code = 200;
+  if (req.method == "GET") {
+    if (t.watch) {
+      http_watch(t.res, t.version, t.ns, list_options(req), resp);
+      return;
+    }
+    if (!t.name.empty()) {
+      err = r_get(t.res, t.version, t.ns, t.name, out);
+      if (!err && t.sub == "scale") out = scale_view(t, out);
+    } else {
+      err = r_list(t.res, t.version, t.ns, list_options(req), out);
+    }
+  } else if (req.method == "POST" || req.method == "PUT" || req.method == "PATCH") {
+    Json body;
+    if (!Json::try_parse(req.body, body)) {
+      send_error(resp, ApiError::BadRequest(req.method == "PATCH" ? "invalid JSON patch body (YAML apply bodies must be sent as JSON)"
+                                                                  : "invalid JSON body"));
+      return;
+    }
+    err = http_write(req, t, body, wo, out, code);
+  } else if (req.method == "DELETE") {
+    err = http_delete(req, t, wo, out);
+  } else {
+    send_error(resp, ApiError{405, "MethodNotAllowed", "method not allowed"});
+    return;
+  }
+  Registry::global()
+      .histogram("apiserver_http_request_duration_seconds", "kube-lite HTTP request latency", {"verb", "resource"},
+                 HistogramVec::exponential(0.0001, 2, 18))
+      ->observe({t.verb, t.plural}, now_seconds() - t0);
+  if (!warnings.empty()) {
+    // RFC 7234 warn-code 299, one warn-value per unknown field (kubectl prints each as "Warning: ...")
+    std::vector<std::string> vals;
+    for (const auto& w : warnings) vals.push_back("299 - " + Json(w).dump());
+    resp.headers["Warning"] = join(vals, ", ");
+  }
+  if (err) {
+    send_error(resp, err, t.res->kind, t.name);
+    return;
+  }
+  resp.json(code, out.dump());
+}
+
+ListOptions ApiServer::list_options(HttpRequest& req) {
   ListOptions lo;
   lo.label_selector = req.q("labelSelector");
   lo.field_selector = req.q("fieldSelector");
@@ -299,209 +463,84 @@ void ApiServer::handle_http(HttpRequest& req, HttpResponse& resp) {
   lo.continue_token = req.q("continue");
   lo.timeout_seconds = std::atoi(req.q("timeoutSeconds", "0").c_str());
   lo.allow_bookmarks = req.q("allowWatchBookmarks") == "true";
+  return lo;
+}
 
-  // subresources handled specially
-  if (res->group.empty() && plural == "pods" && sub == "log") {
-    std::string out;
-    if (!log_provider_ || !log_provider_(ns, name, req.q("container"), std::atoll(req.q("tailLines", "-1").c_str()), out)) {
-      Json p;
-      if (ApiError e = r_get(res, version, ns, name, p)) {
-        send_error(resp, e, "Pod", name);
-        return;
-      }
-      resp.json(400, ApiError::BadRequest("container logs are not available for pod " + name).status_json().dump());
-      return;
-    }
-    resp.text(200, out);
-    return;
-  }
-  if (res->group.empty() && plural == "serviceaccounts" && sub == "token") {
-    // TokenRequest (authentication.k8s.io/v1): a bound token for the ServiceAccount; authorized
-    // above as "create serviceaccounts/token"
-    if (req.method != "POST") {
-      resp.json(405, ApiError{405, "MethodNotAllowed", "TokenRequest takes POST"}.status_json().dump());
-      return;
-    }
-    Json body;
-    if (!req.body.empty() && !Json::try_parse(req.body, body)) {
-      resp.json(400, ApiError::BadRequest("invalid TokenRequest body").status_json().dump());
-      return;
-    }
-    std::string token;
-    double exp = 0;
-    if (ApiError e = issue_sa_token(ns, name, body.at_path({"spec", "expirationSeconds"}).as_int(3600), token, exp)) {
-      send_error(resp, e, "ServiceAccount", name);
-      return;
-    }
-    Json spec = body["spec"].is_object() ? body["spec"] : Json::object();
-    resp.json(201, Json{{"apiVersion", "authentication.k8s.io/v1"}, {"kind", "TokenRequest"},
-                        {"metadata", Json{{"name", name}, {"namespace", ns}}}, {"spec", spec},
-                        {"status", Json{{"token", token},
-                                        {"expirationTimestamp", rfc3339_from_ms(static_cast<int64_t>(exp * 1000))}}}}
-                       .dump());
-    return;
-  }
-  if (res->group.empty() && plural == "pods" && sub == "exec") {
-    // kubectl exec without a TTY or stdin: ?command=a&command=b[&container=c][&timeoutSeconds=n];
-    // reply {"exitCode": n, "output": "<stdout+stderr>"} (authorized above as create pods/exec)
-    if (req.method != "POST" && req.method != "GET") {
-      resp.json(405, ApiError{405, "MethodNotAllowed", "exec takes POST"}.status_json().dump());
-      return;
-    }
-    auto it = req.query.find("command");
-    if (it == req.query.end() || it->second.empty()) {
-      resp.json(400, ApiError::BadRequest("you must specify at least one command for the container").status_json().dump());
-      return;
-    }
-    Json p;
-    if (ApiError e = r_get(res, version, ns, name, p)) {
-      send_error(resp, e, "Pod", name);
-      return;
-    }
-    // each exec holds an API server worker for its duration: at most kMaxConcurrentExec at once, so
-    // long execs can never starve controllers and watches of workers
-    static std::atomic<int> active_exec{0};
-    constexpr int kMaxConcurrentExec = 4;
-    if (active_exec.fetch_add(1) >= kMaxConcurrentExec) {
-      active_exec.fetch_sub(1);
-      resp.json(429, ApiError{429, "TooManyRequests", "too many concurrent exec sessions, retry later"}.status_json().dump());
-      return;
-    }
-    struct ExecSlot {
-      std::atomic<int>& n;
-      ~ExecSlot() { n.fetch_sub(1); }
-    } exec_slot{active_exec};
-    int code = 0;
-    std::string out, err;
-    // bounded: the request holds one API server worker for its duration
-    const double timeout = std::min(3600.0, std::max(1.0, std::atof(req.q("timeoutSeconds", "30").c_str())));
-    if (!exec_provider_ || !exec_provider_(ns, name, req.q("container"), it->second, timeout, code, out, err)) {
-      resp.json(400, ApiError::BadRequest(err.empty() ? "exec is not available for pod " + name : err).status_json().dump());
-      return;
-    }
-    resp.json(200, Json{{"exitCode", static_cast<int64_t>(code)}, {"output", out}}.dump());
-    return;
-  }
-  if (res->group.empty() && plural == "services" && sub == "proxy") {
-    std::string r;
-    for (size_t k = 3; k < rest.size(); ++k) r += (k > 3 ? "/" : "") + rest[k];
-    if (ends_with(path, "/") && !r.empty()) r += "/";
-    http_proxy(req, resp, ns, name, r);
-    return;
-  }
-  if (!sub.empty() && sub != "status" && sub != "scale" && !(res->group.empty() && plural == "pods" && sub == "binding")) {
-    send_error(resp, ApiError::NotFound("subresource", sub));
-    return;
-  }
-  ApiError err;
-  Json out;
-  int code = 200;
-  if (req.method == "GET") {
-    if (watch) {
-      http_watch(res, version, ns, lo, resp);
-      return;
-    }
-    if (!name.empty()) {
-      err = r_get(res, version, ns, name, out);
-      if (!err && sub == "scale")
-        out = Json{{"apiVersion", "autoscaling/v1"}, {"kind", "Scale"},
-                   {"metadata", Json{{"name", name}, {"namespace", ns}}},
-                   {"spec", Json{{"replicas", out.at_path({"spec", "replicas"})}}},
-                   {"status", Json{{"replicas", out.at_path({"status", "replicas"})}}}};
-    } else {
-      err = r_list(res, version, ns, lo, out);
-    }
-  } else if (req.method == "POST") {
-    if (!Json::try_parse(req.body, out)) {
-      send_error(resp, ApiError::BadRequest("invalid JSON body"));
-      return;
-    }
-    if (sub == "binding") {
-      // pods/{name}/binding: set spec.nodeName
+Json ApiServer::scale_view(const HttpTarget& t, const Json& obj) {
+  return Json{{"apiVersion", "autoscaling/v1"}, {"kind", "Scale"},
+              {"metadata", Json{{"name", t.name}, {"namespace", t.ns}}},
+              {"spec", Json{{"replicas", obj.at_path({"spec", "replicas"})}}},
+              {"status", Json{{"replicas", obj.at_path({"status", "replicas"})}}}};
+}
+
+ApiError ApiServer::http_write(HttpRequest& req, const HttpTarget& t, Json& body, const WriteOptions& wo, Json& out,
+                               int& code) {
+  if (req.method == "POST") {
+    code = 201;
+    if (t.sub == "binding") {  // pods/{name}/binding: set spec.nodeName
       Json pod;
-      err = r_get(res, version, ns, name, pod);
-      if (!err) {
-        pod["spec"]["nodeName"] = out.at_path({"target", "name"});
-        WriteOptions sys = wo;
-        err = r_update(res, version, ns, name, pod, sys, "");
-        out = ApiError{}.status_json();
-        code = 201;
-      }
-    } else {
-      err = r_create(res, version, ns, out, wo);
-      code = res->virtual_only ? 201 : 201;
+      ApiError err = r_get(t.res, t.version, t.ns, t.name, pod);
+      if (err) return err;
+      pod["spec"]["nodeName"] = body.at_path({"target", "name"});
+      err = r_update(t.res, t.version, t.ns, t.name, pod, wo, "");
+      out = ApiError{}.status_json();
+      return err;
     }
-  } else if (req.method == "PUT") {
-    if (!Json::try_parse(req.body, out)) {
-      send_error(resp, ApiError::BadRequest("invalid JSON body"));
-      return;
-    }
-    err = r_update(res, version, ns, name, out, wo, sub);
-  } else if (req.method == "PATCH") {
-    Json p;
-    if (!Json::try_parse(req.body, p)) {
-      send_error(resp, ApiError::BadRequest("invalid JSON patch body (YAML apply bodies must be sent as JSON)"));
-      return;
-    }
-    std::string ct = to_lower(req.header("Content-Type", "application/merge-patch+json"));
-    if (contains(ct, "apply-patch")) {
-      // server-side apply (simplified): create if missing, else merge
-      Json cur;
-      if (r_get(res, version, ns, name, cur).code == 404) {
-        p["metadata"]["name"] = name;
-        err = r_create(res, version, ns, p, wo);
-        out = p;
-        code = 201;
-      } else {
-        err = r_patch(res, version, ns, name, "merge", p, out, wo, sub);
-      }
-    } else {
-      err = r_patch(res, version, ns, name, ct, p, out, wo, sub);
-    }
-  } else if (req.method == "DELETE") {
-    DeleteOptions d;
-    d.user = user;
-    d.dry_run = wo.dry_run;
-    d.propagation = req.q("propagationPolicy");
-    d.grace_seconds = req.has_q("gracePeriodSeconds") ? std::atoll(req.q("gracePeriodSeconds").c_str()) : -1;
-    Json body;
-    if (!req.body.empty() && Json::try_parse(req.body, body)) {
-      if (body["propagationPolicy"].is_string()) d.propagation = body["propagationPolicy"].as_string();
-      if (body["gracePeriodSeconds"].is_number()) d.grace_seconds = body["gracePeriodSeconds"].as_int();
-      if (body["dryRun"].is_array() && !body["dryRun"].empty()) d.dry_run = true;
-      d.precondition_uid = body.at_path({"preconditions", "uid"}).as_string();
-      d.precondition_rv = body.at_path({"preconditions", "resourceVersion"}).as_string();
-    }
-    if (!name.empty()) {
-      Json deleted;
-      err = r_delete(res, ns, name, d, &deleted);
-      if (!err) {
-        out = deleted;
-        if (!out.is_null()) convert_out(res, version, out);
-      }
-    } else {
-      Json lst;
-      err = r_list(res, version, ns, lo, lst);
-      if (!err) {
-        for (const auto& item : lst["items"].as_array())
-          r_delete(res, item.str_at({"metadata", "namespace"}), item.str_at({"metadata", "name"}), d);
-        out = ApiError{}.status_json();
-      }
-    }
-  } else {
-    send_error(resp, ApiError{405, "MethodNotAllowed", "method not allowed"});
-    return;
+    ApiError err = r_create(t.res, t.version, t.ns, body, wo);
+    out = body;
+    return err;
   }
+  if (req.method == "PUT") {
+    ApiError err = r_update(t.res, t.version, t.ns, t.name, body, wo, t.sub);
+    out = body;
+    return err;
+  }
+  const std::string ct = to_lower(req.header("Content-Type", "application/merge-patch+json"));
+  if (contains(ct, "apply-patch")) {
+    // server-side apply (simplified): create if missing, else merge
+    Json cur;
+    if (r_get(t.res, t.version, t.ns, t.name, cur).code == 404) {
+      body["metadata"]["name"] = t.name;
+      code = 201;
+      ApiError err = r_create(t.res, t.version, t.ns, body, wo);
+      out = body;
+      return err;
+    }
+    return r_patch(t.res, t.version, t.ns, t.name, "merge", body, out, wo, t.sub);
+  }
+  return r_patch(t.res, t.version, t.ns, t.name, ct, body, out, wo, t.sub);
+}
 
-  Registry::global()
-      .histogram("apiserver_http_request_duration_seconds", "kube-lite HTTP request latency", {"verb", "resource"},
-                 HistogramVec::exponential(0.0001, 2, 18))
-      ->observe({verb, plural}, now_seconds() - t0);
-  if (err) {
-    send_error(resp, err, res->kind, name);
-    return;
+ApiError ApiServer::http_delete(HttpRequest& req, const HttpTarget& t, const WriteOptions& wo, Json& out) {
+  DeleteOptions d;
+  d.user = t.user;
+  d.dry_run = wo.dry_run;
+  d.propagation = req.q("propagationPolicy");
+  d.grace_seconds = req.has_q("gracePeriodSeconds") ? std::atoll(req.q("gracePeriodSeconds").c_str()) : -1;
+  Json body;
+  if (!req.body.empty() && Json::try_parse(req.body, body)) {
+    if (body["propagationPolicy"].is_string()) d.propagation = body["propagationPolicy"].as_string();
+    if (body["gracePeriodSeconds"].is_number()) d.grace_seconds = body["gracePeriodSeconds"].as_int();
+    if (body["dryRun"].is_array() && !body["dryRun"].empty()) d.dry_run = true;
+    d.precondition_uid = body.at_path({"preconditions", "uid"}).as_string();
+    d.precondition_rv = body.at_path({"preconditions", "resourceVersion"}).as_string();
   }
-  resp.json(code, out.dump());
+  if (!t.name.empty()) {
+    Json deleted;
+    ApiError err = r_delete(t.res, t.ns, t.name, d, &deleted);
+    if (!err) {
+      out = deleted;
+      if (!out.is_null()) convert_out(t.res, t.version, out);
+    }
+    return err;
+  }
+  Json lst;
+  ApiError err = r_list(t.res, t.version, t.ns, list_options(req), lst);
+  if (err) return err;
+  for (const auto& item : lst["items"].as_array())
+    r_delete(t.res, item.str_at({"metadata", "namespace"}), item.str_at({"metadata", "name"}), d);
+  out = ApiError{}.status_json();
+  return {};
 }
 
 }  // namespace kf

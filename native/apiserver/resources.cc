@@ -1,6 +1,14 @@
 // resources.cc — see resources.h.
 #include "apiserver/resources.h"
 
+#include <climits>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <regex>
+
+#include "apiserver/schemas.h"
 #include "core/util.h"
 
 namespace kf {
@@ -176,62 +184,118 @@ void ResourceRegistry::remove_crd(const Json& crd) {
 }
 
 // ---------------------------------------------------------------------------------------------
+namespace {
+const char* json_type_name(const Json& v) {
+  if (v.is_null()) return "null";
+  if (v.is_bool()) return "boolean";
+  if (v.is_int()) return "integer";
+  if (v.is_number()) return "number";
+  if (v.is_string()) return "string";
+  if (v.is_array()) return "array";
+  return "object";
+}
+
+// `pattern` as kube-apiserver evaluates it (ECMA-262 regex), compiled once per pattern; the
+// Quantity pattern is checked with the Quantity parser itself
+bool matches_pattern(const std::string& pattern, const std::string& s) {
+  if (pattern == kQuantityPattern) return parse_quantity(s).has_value() && s == trim(s);
+  static std::mutex mu;
+  static std::map<std::string, std::shared_ptr<const std::regex>> cache;
+  std::shared_ptr<const std::regex> re;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto& slot = cache[pattern];
+    if (!slot) {
+      try {
+        slot = std::make_shared<const std::regex>(pattern, std::regex::ECMAScript);
+      } catch (const std::regex_error&) {
+        slot = std::make_shared<const std::regex>(".*");  // an invalid pattern never rejects
+      }
+    }
+    re = slot;
+  }
+  return std::regex_search(s, *re);
+}
+}  // namespace
+
+// OpenAPI v3 validation with kube-apiserver's messages ("<path> in body must be of type integer:
+// \"string\"", "should match '<pattern>'", "Unsupported value", "Required value")
 std::vector<std::string> validate_schema(const Json& schema, const Json& value, const std::string& path) {
   std::vector<std::string> errs;
   if (!schema.is_object()) return errs;
   const std::string here = path.empty() ? "<root>" : path;
-  if (value.is_null()) {
-    if (schema["nullable"].as_bool()) return errs;
-  }
-  const std::string& type = schema["type"].as_string();
-  auto type_ok = [&]() {
-    if (type.empty()) return true;
-    if (type == "object") return value.is_object();
-    if (type == "array") return value.is_array();
-    if (type == "string") return value.is_string() || (schema["x-kubernetes-int-or-string"].as_bool() && value.is_number());
-    if (type == "integer") return value.is_int() || (schema["x-kubernetes-int-or-string"].as_bool() && value.is_string());
-    if (type == "number") return value.is_number();
-    if (type == "boolean") return value.is_bool();
-    return true;
+  if (value.is_null() && schema["nullable"].as_bool()) return errs;
+  auto type_error = [&](const std::string& want) {
+    errs.push_back(here + ": Invalid value: \"" + json_type_name(value) + "\": " + here + " in body must be of type " + want +
+                   ": \"" + json_type_name(value) + "\"");
   };
-  if (schema["x-kubernetes-int-or-string"].as_bool() && (value.is_string() || value.is_number())) return errs;
-  if (!type_ok()) {
-    errs.push_back(here + ": Invalid value: expected " + type);
-    return errs;
+  const bool int_or_string = schema["x-kubernetes-int-or-string"].as_bool();
+  const std::string& type = schema["type"].as_string();
+  if (int_or_string) {
+    if (!value.is_int() && !value.is_string()) {
+      type_error("integer or string");
+      return errs;
+    }
+  } else if (!type.empty()) {
+    bool ok = true;
+    if (type == "object") ok = value.is_object();
+    else if (type == "array") ok = value.is_array();
+    else if (type == "string") ok = value.is_string();
+    else if (type == "integer") ok = value.is_int();
+    else if (type == "number") ok = value.is_number();
+    else if (type == "boolean") ok = value.is_bool();
+    if (!ok) {
+      type_error(type);
+      return errs;
+    }
   }
+  if (value.is_int()) {
+    const std::string& fmt = schema["format"].as_string();
+    const int64_t v = value.as_int();
+    if (fmt == "int32" && (v < INT32_MIN || v > INT32_MAX))
+      errs.push_back(here + ": Invalid value: " + value.dump() + ": " + here + " in body must be of type int32: \"" + value.dump() + "\"");
+  }
+  if (value.is_string() && schema["pattern"].is_string() && !matches_pattern(schema["pattern"].as_string(), value.as_string()))
+    errs.push_back(here + ": Invalid value: \"" + value.as_string() + "\": " + here + " in body should match '" +
+                   schema["pattern"].as_string() + "'");
   if (schema.has("enum")) {
     bool found = false;
-    for (const auto& e : schema["enum"].as_array()) found = found || e == value;
-    if (!found) errs.push_back(here + ": Unsupported value: " + value.dump());
+    std::vector<std::string> allowed;
+    for (const auto& e : schema["enum"].as_array()) {
+      found = found || e == value;
+      allowed.push_back(e.dump());
+    }
+    if (!found) errs.push_back(here + ": Unsupported value: " + value.dump() + ": supported values: " + join(allowed, ", "));
   }
   if (value.is_number()) {
     if (schema.has("minimum") && value.as_double() < schema["minimum"].as_double())
-      errs.push_back(here + ": Invalid value: must be >= " + schema["minimum"].dump());
+      errs.push_back(here + ": Invalid value: " + value.dump() + ": " + here + " in body should be greater than or equal to " +
+                     schema["minimum"].dump());
     if (schema.has("maximum") && value.as_double() > schema["maximum"].as_double())
-      errs.push_back(here + ": Invalid value: must be <= " + schema["maximum"].dump());
+      errs.push_back(here + ": Invalid value: " + value.dump() + ": " + here + " in body should be less than or equal to " +
+                     schema["maximum"].dump());
   }
   if (value.is_object()) {
     for (const auto& req : schema["required"].as_array())
-      if (!value.has(req.as_string())) errs.push_back(here + "." + req.as_string() + ": Required value");
+      if (!value.has(req.as_string())) errs.push_back((path.empty() ? req.as_string() : here + "." + req.as_string()) + ": Required value");
     const Json& props = schema["properties"];
     for (const auto& m : value.as_object()) {
+      if (path.empty() && m.first == "metadata") continue;
       const Json* ps = props.find(m.first);
       std::string sub = path.empty() ? m.first : path + "." + m.first;
-      if (ps) {
-        auto e = validate_schema(*ps, m.second, sub);
-        errs.insert(errs.end(), e.begin(), e.end());
-      } else if (schema["additionalProperties"].is_object()) {
-        auto e = validate_schema(schema["additionalProperties"], m.second, sub);
-        errs.insert(errs.end(), e.begin(), e.end());
-      }
+      const Json* sch = ps ? ps : (schema["additionalProperties"].is_object() ? &schema["additionalProperties"] : nullptr);
+      if (!sch) continue;
+      auto e = validate_schema(*sch, m.second, sub);
+      errs.insert(errs.end(), e.begin(), e.end());
     }
   }
   if (value.is_array()) {
     if (schema.has("minItems") && static_cast<int64_t>(value.size()) < schema["minItems"].as_int())
-      errs.push_back(here + ": Invalid value: " + std::to_string(value.size()) + ": " + here +
-                     " in body should have at least " + std::to_string(schema["minItems"].as_int()) + " items");
+      errs.push_back(here + ": Invalid value: " + std::to_string(value.size()) + ": " + here + " in body should have at least " +
+                     std::to_string(schema["minItems"].as_int()) + " items");
     if (schema.has("maxItems") && static_cast<int64_t>(value.size()) > schema["maxItems"].as_int())
-      errs.push_back(here + ": Too many: must have at most " + std::to_string(schema["maxItems"].as_int()) + " items");
+      errs.push_back(here + ": Too many: " + std::to_string(value.size()) + ": must have at most " +
+                     std::to_string(schema["maxItems"].as_int()) + " items");
     if (schema["items"].is_object()) {
       for (size_t i = 0; i < value.size(); ++i) {
         auto e = validate_schema(schema["items"], value[i], path + "[" + std::to_string(i) + "]");
@@ -244,17 +308,6 @@ std::vector<std::string> validate_schema(const Json& schema, const Json& value, 
 
 // ---------------------------------------------------------------------------------------------
 namespace {
-Json obj_schema(Json props, std::vector<std::string> required = {}) {
-  Json s{{"type", "object"}, {"x-kubernetes-preserve-unknown-fields", true}};
-  if (props.is_object()) s["properties"] = std::move(props);
-  if (!required.empty()) {
-    Json r = Json::array();
-    for (auto& x : required) r.push_back(x);
-    s["required"] = r;
-  }
-  return s;
-}
-
 Json crd(const std::string& group, const std::string& kind, const std::string& plural, const std::string& scope,
          const std::vector<std::pair<std::string, bool>>& versions, bool status, const Json& schema,
          std::vector<std::string> shorts = {}, std::vector<std::string> categories = {}) {
@@ -286,28 +339,16 @@ Json crd(const std::string& group, const std::string& kind, const std::string& p
 
 std::vector<Json> builtin_crds() {
   std::vector<Json> out;
-  // Notebook (notebook-controller/config/crd/bases/kubeflow.org_notebooks.yaml + validation_patches.yaml):
-  // containers required [name,image], minItems 1; storage version v1; all three served.
-  Json container{{"type", "object"}, {"required", Json::array({"name", "image"})},
-                 {"x-kubernetes-preserve-unknown-fields", true}};
-  Json containers{{"type", "array"}, {"minItems", 1}, {"items", container}};
-  Json nb_schema = obj_schema(Json{
-      {"spec", obj_schema(Json{{"template", obj_schema(Json{{"spec", obj_schema(Json{{"containers", containers}})}})}})},
-      {"status", obj_schema(Json())}});
+  // Structural schemas (apiserver/schemas.cc): full core/v1 PodSpec under Notebook
+  // spec.template.spec (all three versions, storage v1) and PVCViewer spec.podSpec, the PodDefault
+  // merge fields, Profile owner / plugins / quota, Tensorboard logspath; unknown fields are pruned.
   out.push_back(crd("kubeflow.org", "Notebook", "notebooks", "Namespaced",
-                    {{"v1", true}, {"v1alpha1", false}, {"v1beta1", false}}, true, nb_schema, {}, {"kubeflow"}));
-  // Profile (cluster-scoped), storage v1
-  out.push_back(crd("kubeflow.org", "Profile", "profiles", "Cluster", {{"v1", true}, {"v1beta1", false}}, true,
-                    obj_schema(Json{{"spec", obj_schema(Json())}, {"status", obj_schema(Json())}})));
-  // Tensorboard: spec.logspath required
-  out.push_back(crd("tensorboard.kubeflow.org", "Tensorboard", "tensorboards", "Namespaced", {{"v1alpha1", true}},
-                    true, obj_schema(Json{{"spec", obj_schema(Json(), {"logspath"})}, {"status", obj_schema(Json())}})));
-  // PVCViewer: spec.pvc + rwoScheduling required
-  out.push_back(crd("kubeflow.org", "PVCViewer", "pvcviewers", "Namespaced", {{"v1alpha1", true}}, true,
-                    obj_schema(Json{{"spec", obj_schema(Json(), {"pvc", "rwoScheduling"})}, {"status", obj_schema(Json())}})));
-  // PodDefault: spec.selector required
-  out.push_back(crd("kubeflow.org", "PodDefault", "poddefaults", "Namespaced", {{"v1alpha1", true}}, false,
-                    obj_schema(Json{{"spec", obj_schema(Json(), {"selector"})}})));
+                    {{"v1", true}, {"v1alpha1", false}, {"v1beta1", false}}, true, notebook_schema(), {}, {"kubeflow"}));
+  out.push_back(crd("kubeflow.org", "Profile", "profiles", "Cluster", {{"v1", true}, {"v1beta1", false}}, true, profile_schema()));
+  out.push_back(crd("tensorboard.kubeflow.org", "Tensorboard", "tensorboards", "Namespaced", {{"v1alpha1", true}}, true,
+                    tensorboard_schema()));
+  out.push_back(crd("kubeflow.org", "PVCViewer", "pvcviewers", "Namespaced", {{"v1alpha1", true}}, true, pvcviewer_schema()));
+  out.push_back(crd("kubeflow.org", "PodDefault", "poddefaults", "Namespaced", {{"v1alpha1", true}}, false, poddefault_schema()));
   // Istio (what the reconcilers own / create)
   out.push_back(crd("networking.istio.io", "VirtualService", "virtualservices", "Namespaced",
                     {{"v1alpha3", true}, {"v1beta1", false}, {"v1", false}}, true, Json(), {"vs"}));

@@ -18,6 +18,7 @@
 
 #include "admission/admission.h"
 #include "apiserver/resources.h"
+#include "apiserver/schemas.h"
 #include "apiserver/selector.h"
 #include "capi/registry.h"
 #include "controllers/common.h"
@@ -119,6 +120,15 @@ void register_core(CapiRegistry& R) {
     return out;
   });
   R.add("dump_yaml", [](const Json& a) -> Json { return dump_yaml(a["value"]); });
+  R.add("prune_unknown_fields", [](const Json& a) -> Json {
+    Json v = a["value"];
+    std::vector<std::string> pruned;
+    prune_unknown_fields(a["schema"], v, &pruned);
+    apply_schema_defaults(a["schema"], v);
+    Json p = Json::array();
+    for (const auto& x : pruned) p.push_back(x);
+    return Json{{"value", v}, {"pruned", p}};
+  });
   R.add("builtin_crds", [](const Json&) -> Json {
     Json out = Json::array();
     for (const auto& c : builtin_crds()) out.push_back(c);
