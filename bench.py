@@ -24,7 +24,10 @@ xGMI). Reported with p50 / p90 and the per-phase p50 breakdown; the same for the
 the torch-ready server (imports torch + runs a GEMM before Ready) and that server forked from the
 kubelet's pre-imported interpreter (``--pod-zygote``). Then the control-plane latencies of
 BASELINE configs 3 and 5 (Profile with GPU quota ready; TensorBoard and PVCViewer ready) on the same
-native control plane.
+native control plane, and configs 4 and 5 as stated (``config4_*`` / ``config5_*``): one Notebook
+holding all N GPUs runs the RCCL all-reduce smoke inside its pod (``--rccl``; ``--rccl-single`` at
+N = 1), then a TensorBoard and a PVCViewer attach to that notebook's RWO workspace PVC and are
+co-scheduled onto its node.
 """
 from __future__ import annotations
 
@@ -97,7 +100,7 @@ def _cs_keys(prefix: str, cs: dict) -> dict:
 
 def run_cold_starts(ex, args, world: int) -> None:
     """Rank 0: the four cold-start variants and the control-plane latencies, each its own extra."""
-    from kubeflow_rm_amd.bench_coldstart import measure_cold_start, measure_control_plane
+    from kubeflow_rm_amd.bench_coldstart import measure_cold_start, measure_control_plane, measure_gpu_notebook_configs
 
     def stub(e):
         cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world, timeout=30, deadline=e.deadline())
@@ -136,6 +139,11 @@ def run_cold_starts(ex, args, world: int) -> None:
         timeout=30, deadline=e.deadline()))), est_s=25, timeout_s=90)
     # BASELINE configs 3 and 5: Profile with GPU quota, TensorBoard + PVCViewer on a PVC
     ex.run("control_plane", lambda e: {"control_plane": measure_control_plane(runs=5)}, est_s=5, timeout_s=60)
+    # BASELINE configs 4 and 5 as stated: one notebook holding all N GPUs runs the RCCL all-reduce
+    # smoke in its pod (config4_*), then a TensorBoard and a PVCViewer attach to its RWO workspace
+    # PVC and are co-scheduled onto its node (config5_*)
+    ex.run("gpu_notebook_configs", lambda e: measure_gpu_notebook_configs(
+        gpus_per_notebook=world, timeout=max(10.0, min(90.0, e.deadline() - time.time()))), est_s=10, timeout_s=120)
 
 
 def self_launch(args) -> int:

@@ -363,6 +363,84 @@ def measure_control_plane(runs: int = 5, gpus: int | None = None, timeout: float
             "pvcviewer_ready_p50_s": p50(pv), "note": "process pods (no container runtime)"}
 
 
+def measure_gpu_notebook_configs(gpus_per_notebook: int = 1, gpus: int | None = None, timeout: float = 120.0,
+                                 namespace: str = "bench-cfg") -> dict:
+    """BASELINE configs 4 and 5 exactly as stated, on ONE notebook that requests every GPU:
+
+    * config 4 — "Notebook CR requesting 8 GPUs: RCCL all-reduce smoke over xGMI inside the pod": the
+      Notebook carries ``kfamd.io/gpu-readiness-args: --rccl`` (``--rccl-single`` when it has one GPU),
+      so the pod's readiness op builds an RCCL communicator over the pod's devices and sweeps an
+      all-reduce 8 B - 64 MiB before the pod is Ready. Reported: Ready time, ``comm_init_ms``, busbw at
+      the largest size, correctness, and the devices the device plugin allocated.
+    * config 5 — "TensorBoard + PVCViewer attached to the 8-GPU notebook": a Tensorboard
+      (``pvc://<nb>-workspace/logs``) and a PVCViewer on that notebook's ReadWriteOnce workspace PVC
+      (the JWA's ``{notebook-name}-workspace``), both co-scheduled onto the notebook's node through the
+      RWO affinity (tensorboard_controller.go:207-231 with RWO_PVC_SCHEDULING, pvcviewer_controller.go:372-445).
+      Reported: their Ready times and the node affinity they got.
+    """
+    name = "cfg-nb"
+    pvc = f"{name}-workspace"
+    out: dict = {"gpus_per_notebook": gpus_per_notebook}
+    with LocalCluster(gpus=gpus, env={"RWO_PVC_SCHEDULING": "true"}) as cl:
+        c = cl.client
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": namespace}})
+        c.create({"apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": pvc, "namespace": namespace},
+                  "spec": {"accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "10Gi"}}}})
+        rccl = "--rccl-single" if gpus_per_notebook == 1 else "--rccl"
+        ctr = {"name": name, "image": "kfamd/jupyter-pytorch-rocm:latest",
+               "resources": {"limits": {"amd.com/gpu": str(gpus_per_notebook)}},
+               "volumeMounts": [{"name": "workspace", "mountPath": "/home/jovyan"}]}
+        nb = {"apiVersion": "kubeflow.org/v1", "kind": "Notebook",
+              "metadata": {"name": name, "namespace": namespace, "annotations": {"kfamd.io/gpu-readiness-args": rccl}},
+              "spec": {"template": {"spec": {"containers": [ctr],
+                                             "volumes": [{"name": "workspace", "persistentVolumeClaim": {"claimName": pvc}}]}}}}
+        t0 = time.time()
+        c.create(nb)
+        obj = _wait_ready(c, name, namespace, timeout)
+        out["config4_ready_s"] = time.time() - t0
+        st = obj.get("status") or {}
+        rep = st.get("gpuReadiness") or {}
+        ar = rep.get("allreduce") or {}
+        sweep = ar.get("sweep") or []
+        out.update({"config4_readiness_args": rccl, "config4_gpus": st.get("gpus"), "config4_readiness_ok": rep.get("ok"),
+                    "config4_rccl_devices": ar.get("devices"), "config4_rccl_comm_init_ms": ar.get("comm_init_ms"),
+                    "config4_rccl_correct": ar.get("correct"), "config4_rccl_load_ms": rep.get("rccl_load_ms"),
+                    "config4_rccl_busbw_GBps": sweep[-1].get("busbw_GBps") if sweep else None,
+                    "config4_rccl_algbw_GBps": sweep[-1].get("algbw_GBps") if sweep else None,
+                    "config4_rccl_bytes": sweep[-1].get("bytes") if sweep else None,
+                    "config4_rccl_sweep": [{k: s.get(k) for k in ("bytes", "us", "algbw_GBps", "busbw_GBps")} for s in sweep]})
+        pod = c.get("v1", "Pod", f"{name}-0", namespace)
+        node = (pod.get("spec") or {}).get("nodeName")
+        t0 = time.time()
+        c.create({"apiVersion": "tensorboard.kubeflow.org/v1alpha1", "kind": "Tensorboard",
+                  "metadata": {"name": "tb", "namespace": namespace}, "spec": {"logspath": f"pvc://{pvc}/logs"}})
+        c.wait_for("tensorboard.kubeflow.org/v1alpha1", "Tensorboard", "tb", namespace,
+                   lambda o: (o.get("status") or {}).get("readyReplicas") == 1, timeout=timeout, interval=0.005)
+        out["config5_tensorboard_ready_s"] = time.time() - t0
+        t0 = time.time()
+        c.create({"apiVersion": "kubeflow.org/v1alpha1", "kind": "PVCViewer", "metadata": {"name": "viewer", "namespace": namespace},
+                  "spec": {"pvc": pvc, "rwoScheduling": True}})
+        c.wait_for("kubeflow.org/v1alpha1", "PVCViewer", "viewer", namespace,
+                   lambda o: (o.get("status") or {}).get("ready") is True, timeout=timeout, interval=0.005)
+        out["config5_pvcviewer_ready_s"] = time.time() - t0
+
+        def affinity_nodes(kind_path, dep_name):
+            dep = c.get("apps/v1", "Deployment", dep_name, namespace)
+            aff = (((dep["spec"]["template"]["spec"].get("affinity") or {}).get("nodeAffinity") or {})
+                   .get("preferredDuringSchedulingIgnoredDuringExecution") or [])
+            vals = [v for t in aff for e in (t.get("preference") or {}).get("matchExpressions") or [] for v in e.get("values") or []]
+            pods = c.list("v1", "Pod", namespace, label_selector=kind_path)["items"]
+            return vals, sorted({(p.get("spec") or {}).get("nodeName") for p in pods})
+
+        tb_aff, tb_nodes = affinity_nodes("app=tb", "tb")
+        pv_aff, pv_nodes = affinity_nodes("app.kubernetes.io/instance=pvcviewer-viewer", "pvcviewer-viewer")
+        out.update({"config5_notebook_node": node, "config5_pvc": pvc,
+                    "config5_tensorboard_affinity_nodes": tb_aff, "config5_tensorboard_pod_nodes": tb_nodes,
+                    "config5_pvcviewer_affinity_nodes": pv_aff, "config5_pvcviewer_pod_nodes": pv_nodes,
+                    "config5_coscheduled": bool(tb_aff == [node] and pv_aff == [node] and tb_nodes == [node] and pv_nodes == [node])})
+    return out
+
+
 def main() -> int:
     p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     p.add_argument("--runs", type=int, default=5)

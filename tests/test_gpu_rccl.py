@@ -196,3 +196,17 @@ def test_bench_force_dist_runs_the_multi_gpu_path_under_torchrun(tmp_path):
     assert all(r["correct"] for r in d["allreduce_oneshot_bf16"] + d["allreduce_twoshot_bf16"])
     assert d["ab_ours_tflops_median"] > 0 and d["ab_hipblaslt_tflops_median"] > 0
     assert d["cold_start_runs"] == 1
+
+
+def test_config4_in_pod_rccl_and_config5_attach_on_the_gpu_notebook():
+    """BASELINE configs 4 and 5 as bench.py runs them (config4_* / config5_* keys), on this box's
+    GPUs: the notebook holding every GPU runs the RCCL stage inside its pod (``--rccl-single`` on one
+    GPU) before Ready, and a TensorBoard + PVCViewer attach to its RWO workspace PVC on its node."""
+    from kubeflow_rm_amd.bench_coldstart import measure_gpu_notebook_configs
+    n = torch.cuda.device_count()
+    r = measure_gpu_notebook_configs(gpus_per_notebook=n, timeout=90)
+    assert r["config4_readiness_ok"] is True, r
+    assert r["config4_rccl_devices"] == n and r["config4_rccl_correct"] is True, r
+    assert r["config4_rccl_comm_init_ms"] > 0 and len(r["config4_rccl_sweep"]) >= 5
+    assert r["config4_rccl_bytes"] == 16 << 20 and r["config4_rccl_algbw_GBps"] > 0
+    assert r["config5_coscheduled"] is True, r
