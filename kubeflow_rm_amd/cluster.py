@@ -36,14 +36,17 @@ def kflite_binary() -> Path:
 class LocalCluster:
     def __init__(self, data_dir: str | None = None, env: dict | None = None, args: list[str] | None = None,
                  controllers: str = "all", gpus: int | None = 8, startup_timeout: float = 30.0,
-                 ca_file: str | None = None, zygote: bool = False, users: list[str] | dict | None = None):
+                 ca_file: str | None = None, zygote: bool | None = False, users: list[str] | dict | None = None):
         self._tmp = None
         # end users with bearer tokens (kflite --token-auth-file): the gateway authenticates them and
         # sets the userid header from the token (never from the client); ``user_headers(name)``
         self.users: dict[str, str] = {}
         for u in (users or []):
             self.users[u] = (users[u] if isinstance(users, dict) else "") or "tok-" + secrets.token_hex(16)
-        self.zygote = zygote  # kubelet --pod-zygote: Python containers fork from a pre-imported interpreter
+        # kubelet --pod-zygote (kflite's default): Python containers fork from a pre-imported
+        # interpreter. False here by default: a test / dev cluster skips the per-node torch import
+        # unless it asks for it; None = kflite's default
+        self.zygote = zygote
         if data_dir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="kflite-")
             data_dir = self._tmp.name
@@ -84,8 +87,8 @@ class LocalCluster:
             tf.write_text(json.dumps({t: {"username": u, "groups": ["system:authenticated"]} for u, t in self.users.items()}))
             os.chmod(tf, 0o600)
             cmd += ["--token-auth-file", str(tf)]
-        if self.zygote and "--pod-zygote" not in self.args:
-            cmd += ["--pod-zygote"]
+        if self.zygote is not None and not any(a.startswith("--pod-zygote") for a in self.args):
+            cmd += ["--pod-zygote" if self.zygote else "--pod-zygote=false"]
         cmd += self.args
         self.log_path = Path(self.data_dir) / "kflite.log"
         self._log = open(self.log_path, "ab")

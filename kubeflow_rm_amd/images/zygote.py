@@ -118,6 +118,20 @@ def _size_thread_pools(env: dict) -> None:
             pass
 
 
+def _join_netns(path: str) -> None:
+    """Enter the pod's network namespace (kubelet --pod-netns) before any of the container's code
+    runs; a container that cannot be isolated must not run at all (the exception exits the child)."""
+    import ctypes
+    fd = os.open(path, os.O_RDONLY | os.O_CLOEXEC)
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        if libc.setns(fd, 0x40000000) != 0:  # CLONE_NEWNET
+            err = ctypes.get_errno()
+            raise OSError(err, f"setns({path}): {os.strerror(err)}")
+    finally:
+        os.close(fd)
+
+
 def _child(req: dict, closefds: list[int]) -> None:
     """Runs in the forked process: become the container, run its module, never return."""
     code = 1
@@ -129,6 +143,8 @@ def _child(req: dict, closefds: list[int]) -> None:
             except OSError:
                 pass
         signal.set_wakeup_fd(-1)
+        if req.get("netns"):
+            _join_netns(req["netns"])
         os.setsid()
         for s in (signal.SIGTERM, signal.SIGCHLD, signal.SIGHUP, signal.SIGPIPE, signal.SIGQUIT):
             signal.signal(s, signal.SIG_DFL)

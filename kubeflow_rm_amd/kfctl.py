@@ -170,7 +170,7 @@ def main(argv: list[str] | None = None) -> int:
         return 0
     if args.cmd == "up":
         from .cluster import LocalCluster
-        cl = LocalCluster(data_dir=args.data_dir).start()
+        cl = LocalCluster(data_dir=args.data_dir, zygote=None).start()
         print(f"kube-lite API {cl.url}  gateway {cl.gateway}  kfam {cl.kfam}  (Ctrl-C to stop)", flush=True)
         try:
             while True:

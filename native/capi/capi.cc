@@ -32,6 +32,7 @@
 #include "gpu/smi.h"
 #include "gpu/topology.h"
 #include "node/authz.h"
+#include "node/netpol.h"
 
 namespace kf {
 namespace {
@@ -120,6 +121,25 @@ void register_core(CapiRegistry& R) {
     return out;
   });
   R.add("dump_yaml", [](const Json& a) -> Json { return dump_yaml(a["value"]); });
+  R.add("evaluate_netpol", [](const Json& a) -> Json {
+    std::vector<Json> pols(a["policies"].as_array().begin(), a["policies"].as_array().end());
+    auto strmap = [](const Json& j) {
+      std::map<std::string, std::string> m;
+      for (const auto& kv : j.as_object()) m[kv.first] = kv.second.as_string();
+      return m;
+    };
+    NetpolSource src;
+    const Json& s = a["source"];
+    src.pod = s["pod"].as_bool();
+    src.ns = s["ns"].as_string();
+    src.pod_labels = strmap(s["pod_labels"]);
+    src.ns_labels = strmap(s["ns_labels"]);
+    src.ip = s["ip"].as_string();
+    const NetpolDecision d = evaluate_netpol(pols, a["namespace"].as_string(), strmap(a["pod_labels"]),
+                                             static_cast<int>(a["port"].as_int()), a["port_name"].as_string(),
+                                             a["protocol"].as_string_or("TCP"), src);
+    return Json{{"allowed", d.allowed}, {"isolated", d.isolated}, {"policy", d.policy}, {"reason", d.reason}};
+  });
   R.add("prune_unknown_fields", [](const Json& a) -> Json {
     Json v = a["value"];
     std::vector<std::string> pruned;

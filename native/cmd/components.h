@@ -25,7 +25,8 @@ struct ComponentFlags {
   std::string pod_cidr_prefix = "127.20";
   std::string sysfs_root;  // GPU discovery root ("" = /sys)
   bool numa_pinning = true;
-  bool pod_zygote = false;
+  bool pod_zygote = true;
+  std::string pod_netns = "auto";  // per-pod network namespaces (node/netns.h)
   std::string image_recipes;
   // gateway (Istio ingress equivalent)
   std::string gateway_addr = "127.0.0.1";

@@ -120,7 +120,15 @@ bool CullingReconciler::fetch(const std::string& nm, const std::string& ns, cons
           "/api/" + what;
   Headers h;
   const std::string mesh = o_.mesh_url_fn ? o_.mesh_url_fn() : o_.mesh_url;
+  // through the mesh (with the culler's workload identity) only into mesh members: in any other
+  // namespace the reference's plain GET comes from the controller's own namespace, which is what
+  // ODH's <nb>-ctrl-np admits on :8888
+  bool member = false;
   if (!o_.dev && !mesh.empty()) {
+    Json n;
+    member = !c_->get("v1", "Namespace", "", ns, n) && n.at_path({"metadata", "labels", "istio-injection"}).as_string() == "enabled";
+  }
+  if (member) {
     h["Host"] = nm + "." + ns + ".svc." + o_.cluster_domain;
     std::string token;
     if (o_.peer_token_fn) token = o_.peer_token_fn();

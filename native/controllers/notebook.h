@@ -71,7 +71,8 @@ struct CullingOptions {
   // mesh_url with Host <nb>.<ns>.svc.<domain> and the culler's ServiceAccount token, so the
   // profile's ns-owner-access-istio policy admits it as the notebook-controller principal
   // (profile_controller.go:419-556, the "*/api/kernels" rule). MESH_URL / MESH_TOKEN_FILE in split
-  // mode; kflite wires both in-process.
+  // mode; kflite wires both in-process. Only for mesh members (istio-injection=enabled): elsewhere
+  // the GET goes straight to the Service, from the controller's own namespace.
   std::string mesh_url;
   std::string mesh_token_file;
   std::function<std::string()> mesh_url_fn, peer_token_fn;

@@ -199,7 +199,8 @@ AdmissionFn make_odh_notebook_webhook(std::shared_ptr<Client> c, OdhOptions o) {
                 {"metadata", Json{{"name", "workbench-trusted-ca-bundle"}, {"namespace", ns},
                                   {"labels", Json{{"opendatahub.io/managed-by", "workbenches"}}}}},
                 {"data", Json{{"ca-bundle.crt", odh_cm.at_path({"data", "ca-bundle.crt"}).as_string()}}}};
-        have = !c->create(cm);
+        const ApiError ce = c->create(cm);
+        have = !ce || ce.code == 409;  // the reconciler may have created it meanwhile
       }
       if (have) odh_inject_cert_config(nb, "workbench-trusted-ca-bundle");
     }

@@ -770,7 +770,7 @@ void HttpServer::serve_conn(int fd, std::string remote) {
     if (!read_headers(rd, req.headers)) return;
     if (!read_body(rd, req.headers, req.body, false)) return;
     size_t qm = req.target.find('?');
-    req.path = url_decode(qm == std::string::npos ? req.target : req.target.substr(0, qm));
+    req.path = url_decode_path(qm == std::string::npos ? req.target : req.target.substr(0, qm));
     if (qm != std::string::npos) {
       req.raw_query = req.target.substr(qm + 1);
       parse_query(req.raw_query, req.query);

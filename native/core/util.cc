@@ -90,6 +90,25 @@ std::string url_decode(const std::string& s) {
   return out;
 }
 
+std::string url_decode_path(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && std::isxdigit(static_cast<unsigned char>(s[i + 1])) &&
+        std::isxdigit(static_cast<unsigned char>(s[i + 2]))) {
+      out += static_cast<char>(std::strtol(s.substr(i + 1, 2).c_str(), nullptr, 16));
+      i += 2;
+    } else {
+      out += s[i];  // '+' is a plus sign in a path (form encoding applies to queries only)
+    }
+  }
+  return out;
+}
+
+bool path_has_escaped_slash(const std::string& raw_path) {
+  const std::string l = to_lower(raw_path);
+  return l.find("%2f") != std::string::npos || l.find("%5c") != std::string::npos;
+}
+
 std::string url_encode(const std::string& s) {
   static const char* hex = "0123456789ABCDEF";
   std::string out;

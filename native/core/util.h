@@ -25,7 +25,12 @@ bool contains(const std::string& s, const std::string& p);
 std::string to_lower(std::string s);
 std::string to_upper(std::string s);
 std::string replace_all(std::string s, const std::string& from, const std::string& to);
-std::string url_decode(const std::string& s);
+std::string url_decode(const std::string& s);  // form encoding (queries): '+' is a space
+// a request path: percent-decoding only ('+' stays '+')
+std::string url_decode_path(const std::string& s);
+// an encoded '/' or '\' (%2F, %5C) in a raw path: the gateway refuses these (Istio's REJECT_REQUEST
+// for escaped slashes) rather than let routing and authorization disagree on segments
+bool path_has_escaped_slash(const std::string& raw_path);
 std::string url_encode(const std::string& s);
 std::string base64_encode(const std::string& in);
 std::string base64_decode(const std::string& in);

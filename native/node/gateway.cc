@@ -1,11 +1,16 @@
 // gateway.cc — Istio-ingress-equivalent HTTP gateway and policy enforcement point (see node.h).
 #include <unistd.h>
 
+#include <openssl/crypto.h>
+#include <openssl/evp.h>
+#include <openssl/hmac.h>
+
 #include <algorithm>
 #include <cstdlib>
 
 #include "core/util.h"
 #include "node/authz.h"
+#include "node/netpol.h"
 #include "node/node.h"
 
 namespace kf {
@@ -13,9 +18,27 @@ namespace kf {
 namespace {
 constexpr const char* kPeerTokenHeader = "X-Kfamd-Peer-Token";
 constexpr const char* kProxySecretHeader = "X-Kfamd-Auth-Proxy-Secret";
-// the ingress / mesh listener's "already authorized" stamp for the pods' inbound listeners (what the
-// peer's mTLS identity of the ingress gateway is to an Istio sidecar); never taken from a client
+// the ingress / mesh listener's proof that it authorized a request, for the pods' inbound listeners
+// (what the peer's mTLS identity of the ingress gateway is to an Istio sidecar): claims (method, path,
+// destination namespace, expiry, the caller's principal / namespace / pod labels) + an HMAC-SHA256
+// under a node secret. Bound to one request shape for 30 s, never taken from a client.
 constexpr const char* kHopHeader = "X-Kfamd-Hop";
+constexpr int64_t kHopTtlMs = 30000;
+constexpr const char* kMeshPolicyName = "istio-mesh";
+
+std::string hmac_hex(const std::string& key, const std::string& msg) {
+  unsigned char md[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  HMAC(EVP_sha256(), key.data(), static_cast<int>(key.size()), reinterpret_cast<const unsigned char*>(msg.data()),
+       msg.size(), md, &len);
+  static const char* hex = "0123456789abcdef";
+  std::string out;
+  for (unsigned i = 0; i < len; ++i) {
+    out += hex[md[i] >> 4];
+    out += hex[md[i] & 15];
+  }
+  return out;
+}
 
 // "<svc>.<ns>.svc[.<domain>]" (or "<svc>.<ns>") -> (svc, ns); false for anything else
 bool split_service_host(const std::string& host_port, std::string& svc, std::string& ns) {
@@ -55,6 +78,71 @@ void Gateway::setup(Manager& mgr) {
   routes_ = &mgr.informer("route.openshift.io/v1", "Route");
   policies_ = &mgr.informer("security.istio.io/v1beta1", "AuthorizationPolicy");
   services_ = &mgr.informer("v1", "Service");
+  netpols_ = &mgr.informer("networking.k8s.io/v1", "NetworkPolicy");
+  namespaces_ = &mgr.informer("v1", "Namespace");
+  mesh_np_ = std::make_shared<Controller>("istio-mesh-networkpolicy",
+                                          [this](const Request& r, std::string* e) { return reconcile_mesh_policy(r, e); });
+  mesh_np_->For(*namespaces_);
+  mesh_np_->Watches(*netpols_, [](const std::string&, const Json& np) {
+    std::vector<Request> out;
+    if (np.str_at({"metadata", "name"}) == kMeshPolicyName) out.push_back({"", np.str_at({"metadata", "namespace"})});
+    return out;
+  });
+  mgr.add(mesh_np_);
+}
+
+// OpenShift Service Mesh's member-namespace NetworkPolicy (Maistra's "istio-mesh"): every pod of a
+// mesh-injected namespace accepts the mesh — other member namespaces, the ingress gateway's
+// namespace and the control plane — so that a workload's own NetworkPolicies (ODH's <nb>-ctrl-np
+// admits only the controller namespace on :8888) add to, and never cut off, mesh traffic. Policies
+// are additive: a pod of an injected namespace is reachable from anything any policy allows.
+Result Gateway::reconcile_mesh_policy(const Request& r, std::string* err) {
+  Json n, live;
+  const bool member = namespaces_->get("", r.name, n) && !n.at_path({"metadata", "deletionTimestamp"}).is_string() &&
+                      n.at_path({"metadata", "labels", "istio-injection"}).as_string() == "enabled";
+  const ApiError ge = c_->get("networking.k8s.io/v1", "NetworkPolicy", r.name, kMeshPolicyName, live);
+  if (!member) {
+    if (!ge && live.at_path({"metadata", "labels", "app.kubernetes.io/managed-by"}).as_string() == "kfamd-mesh")
+      c_->remove("networking.k8s.io/v1", "NetworkPolicy", r.name, kMeshPolicyName);
+    return {};
+  }
+  Json mesh_ns = Json::array({o_.ingress_namespace, o_.root_namespace, o_.control_plane_namespace, "kubeflow"});
+  Json members = Json::object();
+  members["namespaceSelector"] = Json{{"matchLabels", Json{{"istio-injection", "enabled"}}}};
+  Json expr{{"key", "kubernetes.io/metadata.name"}, {"operator", "In"}, {"values", mesh_ns}};
+  Json infra = Json::object();
+  infra["namespaceSelector"] = Json{{"matchExpressions", Json::array({expr})}};
+  Json rule = Json::object();
+  rule["from"] = Json::array({members, infra});
+  Json spec = Json::object();
+  spec["podSelector"] = Json::object();
+  spec["policyTypes"] = Json::array({"Ingress"});
+  spec["ingress"] = Json::array({rule});
+  if (!ge && live["spec"] == spec) return {};
+  ApiError e;
+  if (ge.code == 404) {
+    Json np{{"apiVersion", "networking.k8s.io/v1"},
+            {"kind", "NetworkPolicy"},
+            {"metadata", Json{{"name", kMeshPolicyName}, {"namespace", r.name},
+                              {"labels", Json{{"app.kubernetes.io/managed-by", "kfamd-mesh"}}}}},
+            {"spec", spec}};
+    e = c_->create(np);
+  } else if (!ge) {
+    live["spec"] = spec;
+    e = c_->update(live);
+  } else {
+    e = ge;
+  }
+  if (e && e.code != 409) *err = e.message;
+  return {};
+}
+
+// pods of `ns` have inbound listeners: every pod when pods get network namespaces, else the
+// mesh-injected namespaces' (and NetworkPolicy-selected pods, which do not need the hop proof)
+bool Gateway::dest_has_listener(const std::string& ns) {
+  if (o_.pods_have_listeners) return true;
+  Json n;
+  return namespaces_ && namespaces_->get("", ns, n) && n.at_path({"metadata", "labels", "istio-injection"}).as_string() == "enabled";
 }
 
 bool Gateway::start(const std::string& addr, int port, std::string* err) {
@@ -152,9 +240,72 @@ void Gateway::peer_identity(const HttpRequest& req, std::string& principal, std:
   }
 }
 
+std::string Gateway::stamp_hop(const std::string& method, const std::string& path, const std::string& dest_ns,
+                               const HopClaims& who) const {
+  Json labels = Json::object();
+  for (const auto& kv : who.source_labels) labels[kv.first] = kv.second;
+  const Json claims{{"m", method}, {"p", path}, {"ns", dest_ns}, {"exp", now_unix_ms() + kHopTtlMs},
+                    {"pr", who.principal}, {"sns", who.source_ns}, {"spod", who.source_pod}, {"sl", labels}};
+  const std::string payload = base64_encode(claims.dump());
+  return payload + "." + hmac_hex(hop_secret_, payload);
+}
+
+bool Gateway::verify_hop(const std::string& value, const std::string& method, const std::string& path,
+                         const std::string& dest_ns, HopClaims& out) const {
+  const size_t dot = value.rfind('.');
+  if (value.empty() || dot == std::string::npos) return false;
+  const std::string payload = value.substr(0, dot), mac = value.substr(dot + 1), want = hmac_hex(hop_secret_, payload);
+  if (mac.size() != want.size() || CRYPTO_memcmp(mac.data(), want.data(), want.size()) != 0) return false;
+  Json c;
+  if (!Json::try_parse(base64_decode(payload), c)) return false;
+  const int64_t now = now_unix_ms(), exp = c["exp"].as_int();
+  if (c["m"].as_string() != method || c["p"].as_string() != path || c["ns"].as_string() != dest_ns || exp < now ||
+      exp > now + kHopTtlMs)
+    return false;
+  out.principal = c["pr"].as_string();
+  out.source_ns = c["sns"].as_string();
+  out.source_pod = c["spod"].as_bool();
+  for (const auto& kv : c["sl"].as_object()) out.source_labels[kv.first] = kv.second.as_string();
+  return true;
+}
+
+// the source of a request the mesh listener received: the pod behind an egress relay (netns mode:
+// its namespace + labels), else the ServiceAccount token's namespace
+Gateway::HopClaims Gateway::mesh_caller(const HttpRequest& req) {
+  HopClaims who;
+  peer_identity(req, who.principal, who.source_ns);
+  PodSource ps;
+  if (lookup_pod_source(req.remote_addr, ps)) {
+    who.source_pod = true;
+    who.source_labels = ps.labels;
+    if (who.source_ns.empty() || who.source_ns != ps.ns) who.principal.clear();  // a token of another namespace proves nothing
+    who.source_ns = ps.ns;
+  } else {
+    who.source_pod = !who.source_ns.empty();
+  }
+  return who;
+}
+
+std::map<std::string, std::string> Gateway::namespace_labels(const std::string& ns) {
+  std::map<std::string, std::string> out;
+  Json n;
+  if (namespaces_ && namespaces_->get("", ns, n))
+    for (const auto& kv : n.at_path({"metadata", "labels"}).as_object()) out[kv.first] = kv.second.as_string();
+  if (out.empty()) out["kubernetes.io/metadata.name"] = ns;
+  return out;
+}
+
+// A pod's inbound listener: NetworkPolicy for every pod that has one, Istio AuthorizationPolicy on
+// the pod's own labels for mesh-injected pods (the gateway decided on the Service
+// selector; re-evaluated here with the principal it carried), then the app.
 void Gateway::handle_inbound(const InboundTarget& t, HttpRequest& req, HttpResponse& resp) {
+  if (path_has_escaped_slash(req.target.substr(0, req.target.find('?')))) {
+    resp.text(400, "Bad Request: escaped slashes are not allowed in the path\n");
+    return;
+  }
   const std::string path = normalize_authz_path(req.path);
-  const bool hopped = !hop_secret_.empty() && req.header(kHopHeader) == hop_secret_;
+  HopClaims who;
+  const bool hopped = verify_hop(req.header(kHopHeader), req.method, path, t.ns, who);
   Headers h;
   for (const auto& kv : req.headers) {
     const std::string k = to_lower(kv.first);
@@ -162,10 +313,32 @@ void Gateway::handle_inbound(const InboundTarget& t, HttpRequest& req, HttpRespo
     if (k == to_lower(kPeerTokenHeader) || k == to_lower(kHopHeader)) continue;
     h[kv.first] = kv.second;
   }
-  if (!hopped && o_.enforce) {
-    std::string principal, source_ns, why;
-    peer_identity(req, principal, source_ns);
-    if (!authorize_workload(t.ns, t.labels, t.port, req, path, h, principal, source_ns, &why)) {
+  if (!hopped) {
+    // dialed directly: the pod network (netns mode) lets only node processes reach this address, so
+    // an unattributed caller is the control plane; a ServiceAccount token names its namespace
+    peer_identity(req, who.principal, who.source_ns);
+    who.source_pod = true;
+    if (who.source_ns.empty()) who.source_ns = o_.control_plane_namespace;
+  }
+  if (netpols_) {
+    NetpolSource src;
+    src.pod = who.source_pod;
+    src.ns = who.source_ns;
+    src.pod_labels = who.source_labels;
+    src.ns_labels = namespace_labels(who.source_ns);
+    src.ip = req.remote_addr.substr(0, req.remote_addr.rfind(':'));
+    const NetpolDecision d = evaluate_netpol(netpols_->list(t.ns), t.ns, t.labels, t.port, t.port_name, "TCP", src);
+    if (d.isolated) decisions_->inc({"netpol", d.allowed ? "allow" : "deny"});
+    if (!d.allowed) {
+      resp.headers["X-Kfamd-Netpol"] = d.reason + " (" + d.policy + ")";
+      resp.text(403, "NetworkPolicy: connection refused");
+      return;
+    }
+  }
+  if (t.mesh && o_.enforce) {
+    std::string why;
+    const std::string principal = hopped || !who.principal.empty() ? who.principal : "";
+    if (!authorize_workload(t.ns, t.labels, t.port, req, path, h, principal, hopped || !principal.empty() ? who.source_ns : "", &why)) {
       decisions_->inc({"sidecar", "deny"});
       resp.headers["X-Kfamd-Authz"] = why;
       resp.text(403, "RBAC: access denied");
@@ -175,6 +348,11 @@ void Gateway::handle_inbound(const InboundTarget& t, HttpRequest& req, HttpRespo
   }
   const std::string url = "http://" + t.app_ip + ":" + std::to_string(t.port) + encode_request_path(path) +
                           (req.raw_query.empty() ? "" : "?" + req.raw_query);
+  NetnsScope in(t.netns.get());  // the connection to the app is made inside the pod's namespace
+  if (!in.ok()) {
+    resp.text(503, "upstream connect error: cannot enter the pod's network namespace\n");
+    return;
+  }
   forward(req, resp, url, std::move(h), 300000);
 }
 
@@ -235,6 +413,10 @@ bool Gateway::match(const std::vector<Json>& vss, const std::string& gateway, co
 
 void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   const std::string host = req.header("Host");
+  if (path_has_escaped_slash(req.target.substr(0, req.target.find('?')))) {
+    resp.text(400, "Bad Request: escaped slashes are not allowed in the path\n");
+    return;
+  }
   // routing, authorization and the upstream request all see one normalized path (Istio BASE)
   const std::string path = normalize_authz_path(req.path);
   Route rt;
@@ -307,7 +489,17 @@ void Gateway::handle(HttpRequest& req, HttpResponse& resp) {
   }
   if (!routed_by_route && o_.enforce) {
     decisions_->inc({"ingress", "allow"});
-    h[kHopHeader] = hop_secret_;  // the destination pod's inbound listener takes this decision
+    // the destination pod's inbound listener takes this decision (when it has one: a pod without one
+    // must not even see the proof)
+    std::string svc, dns;
+    if (split_service_host(rt.dest_host, svc, dns) && dest_has_listener(dns)) {
+      HopClaims who;
+      who.principal = o_.ingress_principal;
+      who.source_ns = o_.ingress_namespace;
+      who.source_pod = true;
+      who.source_labels = {{"istio", "ingressgateway"}};
+      h[kHopHeader] = stamp_hop(req.method, normalize_authz_path(target_path), dns, who);
+    }
   }
   forward(req, resp, url, std::move(h), static_cast<int>(rt.timeout_s * 1000));
 }
@@ -319,8 +511,12 @@ void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
     resp.text(404, "mesh: Host must name a Service (<svc>.<ns>.svc[.<domain>]), got " + host + "\n");
     return;
   }
-  std::string principal, source_ns;
-  peer_identity(req, principal, source_ns);
+  if (path_has_escaped_slash(req.target.substr(0, req.target.find('?')))) {
+    resp.text(400, "Bad Request: escaped slashes are not allowed in the path\n");
+    return;
+  }
+  const HopClaims who = mesh_caller(req);
+  const std::string principal = who.principal, source_ns = who.source_ns;
   Headers h;
   for (const auto& kv : req.headers) {
     std::string k = to_lower(kv.first);
@@ -340,7 +536,7 @@ void Gateway::handle_mesh(HttpRequest& req, HttpResponse& resp) {
   }
   if (o_.enforce) {
     decisions_->inc({"mesh", "allow"});
-    h[kHopHeader] = hop_secret_;
+    if (dest_has_listener(ns)) h[kHopHeader] = stamp_hop(req.method, path, ns, who);
   }
   const std::string url = "http://" + svc + "." + ns + ".svc." + o_.cluster_domain + ":" + std::to_string(port) +
                           encode_request_path(path) +

@@ -30,6 +30,7 @@
 #include "core/util.h"
 #include "gpu/smi.h"
 #include "node/node.h"
+#include "node/netpol.h"
 #include "node/prober.h"
 
 extern char** environ;
@@ -166,7 +167,8 @@ struct Kubelet::PodRuntime {
   Placement gpus;
   int rdzv_port = 0;  // torch.distributed rendezvous port of a multi-GPU pod (unique on the node)
   bool gpu_ok = true;
-  std::string gpu_error;  // why the device plugin refused the pod (UnexpectedAdmissionError message)
+  std::string gpu_error;
+  std::shared_ptr<PodNetns> netns;  // kubelet --pod-netns: the pod's own network namespace  // why the device plugin refused the pod (UnexpectedAdmissionError message)
   std::map<std::string, std::string> mounts;  // mountPath -> host dir (per container union)
   std::vector<ContainerRt> init, main;
   size_t init_done = 0;
@@ -323,7 +325,8 @@ Json Kubelet::node_object() const {
   return Json{{"apiVersion", "v1"},
               {"kind", "Node"},
               {"metadata", Json{{"name", cfg_.node_name}, {"labels", labels},
-                                {"annotations", Json{{"amd.com/gpu-topology", topo.to_json().dump()}}}}},
+                                {"annotations", Json{{"amd.com/gpu-topology", topo.to_json().dump()},
+                                                     {"kfamd.io/pod-network", netns_ ? "netns" : "host"}}}}},
               {"spec", Json{{"providerID", "kflite://" + cfg_.node_name}}},
               {"status", Json{{"capacity", cap},
                               {"allocatable", cap},
@@ -339,6 +342,18 @@ Json Kubelet::node_object() const {
 }
 
 void Kubelet::start() {
+  // pod network namespaces need the privilege to create them and an enforcement point to reach the
+  // apps through (the gateway's inbound handler)
+  std::string why;
+  const bool capable = cfg_.pod_netns != "off" && pod_netns_supported(&why);
+  netns_ = capable && inbound_;
+  if (netns_) relay_ = std::make_unique<EgressRelay>();
+  if (cfg_.pod_netns == "on" && !netns_)
+    KF_ERROR("kubelet", "--pod-netns=on but pods cannot get a network namespace; they fail admission",
+             Json{{"reason", capable ? "no policy enforcer (gateway) on this node" : why}});
+  else if (cfg_.pod_netns == "auto" && !netns_)
+    KF_WARN("kubelet", "pods share the host network namespace (private-address convention only)",
+            Json{{"reason", capable ? "no policy enforcer (gateway) on this node" : why}});
   Json node = node_object();
   Json existing;
   if (c_->get("v1", "Node", "", cfg_.node_name, existing).code == 404) {
@@ -473,6 +488,7 @@ void Kubelet::stop() {
     std::lock_guard<std::mutex> pl(rt->op_mu);
     terminate_pod(*rt, 0);
   }
+  if (relay_) relay_->stop();
   stop_zygotes();
 }
 
@@ -497,8 +513,10 @@ struct ScopedThreadAffinity {
   }
 };
 
+// `ns`: the pod's network namespace; the child starts in it (posix_spawn from a thread inside it)
 pid_t spawn(const std::vector<std::string>& argv, const std::vector<std::string>& env, const std::string& cwd,
-            const std::string& log_path, std::string* err, const std::vector<int>& cpus = {}) {
+            const std::string& log_path, std::string* err, const std::vector<int>& cpus = {},
+            const PodNetns* ns = nullptr) {
   ScopedThreadAffinity pin(cpus);
   posix_spawn_file_actions_t fa;
   posix_spawnattr_t at;
@@ -521,7 +539,11 @@ pid_t spawn(const std::vector<std::string>& argv, const std::vector<std::string>
   ev.push_back(nullptr);
   std::string exe = which(argv[0]);
   pid_t pid = -1;
-  int rc = exe.empty() ? ENOENT : posix_spawn(&pid, exe.c_str(), &fa, &at, av.data(), ev.data());
+  int rc;
+  {
+    NetnsScope in(ns);
+    rc = !in.ok() ? errno : exe.empty() ? ENOENT : posix_spawn(&pid, exe.c_str(), &fa, &at, av.data(), ev.data());
+  }
   posix_spawn_file_actions_destroy(&fa);
   posix_spawnattr_destroy(&at);
   if (rc != 0) {
@@ -602,7 +624,7 @@ bool reap(pid_t pid, int& exit_code, std::string& reason) {
 // there or refuses (the caller then spawns a fresh interpreter).
 pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv, const std::vector<std::string>& env,
                    const std::string& cwd, const std::string& log_path, const std::vector<int>& cpus, int* zfd,
-                   std::string* err) {
+                   std::string* err, const std::string& netns_path = "") {
   const int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (fd < 0) return -1;
   sockaddr_un a{};
@@ -620,6 +642,7 @@ pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv
   for (size_t i = 1; i < argv.size(); ++i) req["argv"].push_back(argv[i]);
   for (const auto& e : env) req["env"].push_back(e);
   for (int c : cpus) req["cpus"].push_back(static_cast<int64_t>(c));
+  if (!netns_path.empty()) req["netns"] = netns_path;  // the child joins the pod's namespace first
   const std::string line = req.dump() + "\n";
   size_t off = 0;
   while (off < line.size()) {
@@ -793,9 +816,10 @@ void Kubelet::terminate_pod(PodRuntime& rt, int64_t grace_s) {
       c.finished_at = ms_now();
       c.pid = -1;
     }
-  // the pod's inbound listeners go with it (the pod IP may be handed out again)
+  // the pod's inbound listeners and egress relays go with it (the pod IP may be handed out again)
   for (auto& srv : rt.inbound) srv->stop();
   rt.inbound.clear();
+  if (relay_) relay_->remove_pod(rt.uid);
 }
 
 bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::string& container,
@@ -839,7 +863,7 @@ bool Kubelet::exec(const std::string& ns, const std::string& pod, const std::str
   }
   const std::string out_path = dir + "/exec-" + random_hex(6) + ".out";
   std::string serr;
-  const pid_t pid = spawn(argv, envv, cwd, out_path, &serr, cpus);
+  const pid_t pid = spawn(argv, envv, cwd, out_path, &serr, cpus, rt->netns.get());
   if (pid < 0) {
     err = serr;
     ::unlink(out_path.c_str());
@@ -1146,28 +1170,46 @@ bool Kubelet::wants_sidecar(const Json& pod) {
   return label(ns, "istio-injection") == "enabled";
 }
 
-// the pod's inbound listeners: pod_ip:port for every containerPort, each request through the
-// enforcer, then to app_ip:port
-void Kubelet::start_inbound(PodRuntime& rt, const Json& pod) {
+// an ingress NetworkPolicy of the pod's namespace selects it (its traffic must pass an enforcement
+// point even without a mesh sidecar: ODH's <nb>-ctrl-np / <nb>-oauth-np)
+bool Kubelet::selected_by_netpol(const Json& pod) {
+  Json nps;
+  if (c_->list("networking.k8s.io/v1", "NetworkPolicy", pod.str_at({"metadata", "namespace"}), ListOptions(), nps)) return false;
+  NetpolSource none;
+  std::map<std::string, std::string> labels;
+  for (const auto& kv : pod.at_path({"metadata", "labels"}).as_object()) labels[kv.first] = kv.second.as_string();
+  std::vector<Json> items(nps["items"].as_array().begin(), nps["items"].as_array().end());
+  return evaluate_netpol(items, pod.str_at({"metadata", "namespace"}), labels, 0, "", "TCP", none).isolated;
+}
+
+// the pod's inbound listeners: pod_ip:port (host namespace) for every TCP containerPort, each
+// request through the enforcer (NetworkPolicy; Istio AuthorizationPolicy when `mesh`), then to the
+// app: app_ip:port on the host, or inside the pod's network namespace
+void Kubelet::start_inbound(PodRuntime& rt, const Json& pod, bool mesh) {
   InboundTarget base;
   base.ns = rt.ns;
   base.name = rt.name;
   base.app_ip = rt.app_ip;
+  base.pod_ip = rt.ip;
+  base.mesh = mesh;
+  base.netns = rt.netns;
   for (const auto& kv : pod.at_path({"metadata", "labels"}).as_object()) base.labels[kv.first] = kv.second.as_string();
-  std::set<int> ports;
-  for (const auto& c : pod.at_path({"spec", "containers"}).as_array())
-    for (const auto& p : c["ports"].as_array())
-      if (p["protocol"].as_string_or("TCP") == "TCP" && p["containerPort"].as_int() > 0)
-        ports.insert(static_cast<int>(p["containerPort"].as_int()));
-  for (int port : ports) {
+  std::map<int, std::string> ports;  // port -> name
+  for (const char* list : {"containers", "initContainers"})
+    for (const auto& c : pod.at_path({"spec", list}).as_array())
+      for (const auto& p : c["ports"].as_array())
+        if (p["protocol"].as_string_or("TCP") == "TCP" && p["containerPort"].as_int() > 0)
+          ports.emplace(static_cast<int>(p["containerPort"].as_int()), p["name"].as_string());
+  for (const auto& port : ports) {
     InboundTarget t = base;
-    t.port = port;
+    t.port = port.first;
+    t.port_name = port.second;
     auto srv = std::make_unique<HttpServer>();
     InboundHandler h = inbound_;
     srv->set_handler([h, t](HttpRequest& req, HttpResponse& resp) { h(t, req, resp); });
     std::string err;
-    if (!srv->listen(rt.ip, port, &err)) {
-      rec_->event(pod, "Warning", "FailedInbound", "inbound listener " + rt.ip + ":" + std::to_string(port) + ": " + err);
+    if (!srv->listen(rt.ip, port.first, &err)) {
+      rec_->event(pod, "Warning", "FailedInbound", "inbound listener " + rt.ip + ":" + std::to_string(port.first) + ": " + err);
       continue;
     }
     srv->start();
@@ -1175,7 +1217,42 @@ void Kubelet::start_inbound(PodRuntime& rt, const Json& pod) {
   }
 }
 
-// admission of a new pod: sandbox dir, pod IP, GPUs, volumes, containers; registered on the node
+// the pod's network: its own namespace with inbound listeners and egress relays (--pod-netns), else
+// the host namespace, with the private-address convention when an enforcement point is needed
+bool Kubelet::setup_pod_network(PodRuntime& rt, const Json& pod) {
+  const bool mesh = wants_sidecar(pod);
+  if (netns_) {
+    std::string err;
+    rt.netns = PodNetns::create(&err);
+    if (!rt.netns) {
+      rt.gpu_ok = false;  // fails admission: a pod is never started outside its isolation
+      rt.gpu_error = "FailedCreatePodSandBox: network namespace: " + err;
+      rec_->event(pod, "Warning", "FailedCreatePodSandBox", "network namespace: " + err);
+      return false;
+    }
+    PodSource src;
+    src.ns = rt.ns;
+    src.name = rt.name;
+    for (const auto& kv : pod.at_path({"metadata", "labels"}).as_object()) src.labels[kv.first] = kv.second.as_string();
+    const auto eps = cfg_.egress_endpoints ? cfg_.egress_endpoints() : std::vector<std::string>{};
+    for (const auto& f : relay_->add_pod(rt.uid, *rt.netns, eps, src))
+      rec_->event(pod, "Warning", "FailedEgress", "egress relay for " + f + " could not be bound in the pod's namespace");
+    start_inbound(rt, pod, mesh);
+    return true;
+  }
+  if (cfg_.pod_netns == "on") {
+    rt.gpu_ok = false;
+    rt.gpu_error = "FailedCreatePodSandBox: --pod-netns=on and this node cannot isolate pods";
+    return false;
+  }
+  if (inbound_ && (mesh || selected_by_netpol(pod))) {
+    rt.app_ip = cfg_.app_ip_prefix + rt.ip.substr(cfg_.pod_ip_prefix.size());
+    start_inbound(rt, pod, mesh);
+  }
+  return true;
+}
+
+// admission of a new pod: sandbox dir, pod IP, network, GPUs, volumes, containers; registered on the node
 std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json& pod) {
   auto rt = std::make_shared<PodRuntime>();
   rt->uid = pod.str_at({"metadata", "uid"});
@@ -1183,18 +1260,17 @@ std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json
   rt->name = r.name;
   rt->dir = cfg_.root_dir + "/pods/" + r.ns + "_" + r.name + "_" + rt->uid.substr(0, 8);
   make_dirs(rt->dir + "/rootfs");
-  const bool sidecar = wants_sidecar(pod);
   {
     std::lock_guard<std::mutex> g(mu_);
     uint32_t n = next_ip_++;
-    const std::string host = "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
-    rt->ip = cfg_.pod_ip_prefix + host;
-    rt->app_ip = sidecar ? cfg_.app_ip_prefix + host : rt->ip;
+    rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
+    rt->app_ip = rt->ip;
   }
   rt->start_time = ms_now();
-  allocate_gpus(*rt, pod);
-  build_containers(*rt, pod, prepare_volumes(*rt, pod));
-  if (sidecar) start_inbound(*rt, pod);
+  if (setup_pod_network(*rt, pod)) {
+    allocate_gpus(*rt, pod);
+    build_containers(*rt, pod, prepare_volumes(*rt, pod));
+  }
   std::lock_guard<std::mutex> g(mu_);
   pods_[rt->uid] = rt;
   key_to_uid_[r.ns + "/" + r.name] = rt->uid;
@@ -1365,7 +1441,7 @@ void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
   }
   if (zy.pid > 0 && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
     std::string zerr;
-    pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr);
+    pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr, rt.netns ? rt.netns->path() : "");
     if (pid > 0) {
       std::ofstream lf(cr.log_path, std::ios::app);
       lf << "# kflite: forked from zygote " << zy.pid << " (preloaded " << zygote << ")\n";
@@ -1378,7 +1454,7 @@ void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
       "kubelet_container_starts_total", "container processes started, by how: zygote fork or fresh exec", {"mode"});
   if (pid > 0) starts->inc({"zygote"});
   if (pid < 0) {
-    pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus);
+    pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus, rt.netns.get());
     if (pid > 0) starts->inc({"fresh"});
   }
   if (pid < 0) {
@@ -1433,15 +1509,21 @@ std::function<bool()> Kubelet::make_probe(const PodSync& s, const Json& probe, c
     std::string url = "http://" + host + ":" + std::to_string(port_of(hg["port"])) + hg["path"].as_string_or("/");
     Headers h;
     for (const auto& hh : hg["httpHeaders"].as_array()) h[hh["name"].as_string()] = hh["value"].as_string();
-    return [url, h, timeout] {
-      HttpResult res = http_request("GET", url, "", h, timeout);
+    std::shared_ptr<const PodNetns> ns = rt.netns;  // probes connect inside the pod's namespace
+    return [url, h, timeout, ns] {
+      NetnsScope in(ns.get());
+      HttpResult res = in.ok() ? http_request("GET", url, "", h, timeout) : HttpResult{};
       return res.status >= 200 && res.status < 400;
     };
   }
   if (probe["tcpSocket"].is_object()) {
     const std::string ip = rt.app_ip;
     const int port = port_of(probe.at_path({"tcpSocket", "port"}));
-    return [ip, port, timeout] { return tcp_connect(ip, port, timeout); };
+    std::shared_ptr<const PodNetns> ns = rt.netns;
+    return [ip, port, timeout, ns] {
+      NetnsScope in(ns.get());
+      return in.ok() && tcp_connect(ip, port, timeout);
+    };
   }
   if (probe["exec"].is_object()) {
     std::vector<std::string> argv;
@@ -1451,8 +1533,9 @@ std::function<bool()> Kubelet::make_probe(const PodSync& s, const Json& probe, c
     std::map<std::string, std::string> envm;
     container_env(s, c, envv, envm);
     const std::string cwd = rt.dir + "/rootfs", log = rt.dir + "/probe.log";
-    return [argv, envv, cwd, log, timeout] {
-      pid_t pid = spawn(argv, envv, cwd, log, nullptr);
+    std::shared_ptr<const PodNetns> ns = rt.netns;
+    return [argv, envv, cwd, log, timeout, ns] {
+      pid_t pid = spawn(argv, envv, cwd, log, nullptr, {}, ns.get());
       if (pid < 0) return false;
       return wait_probe_process(pid, timeout) == 0;
     };

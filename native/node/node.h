@@ -40,6 +40,7 @@
 #include "core/http.h"
 #include "core/metrics.h"
 #include "gpu/topology.h"
+#include "node/netns.h"
 #include "runtime/runtime.h"
 
 namespace kf {
@@ -94,20 +95,31 @@ struct KubeletConfig {
   bool numa_pinning = true;  // pin GPU pods' processes to their devices' NUMA-local CPUs
   // start a pre-imported interpreter (kubeflow_rm_amd/images/zygote.py) per image recipe that names
   // one, and fork Python containers from it instead of exec'ing a fresh interpreter
-  bool pod_zygote = false;
+  bool pod_zygote = true;
+  // per-pod network namespaces (node/netns.h): "auto" (when the node can create them and a policy
+  // enforcer is wired), "on" (required: pods fail admission without one), "off" (private-address
+  // convention only)
+  std::string pod_netns = "auto";
+  // the node endpoints ("127.0.0.1:<port>") relayed into every pod namespace: API server, ingress
+  // gateway, mesh listener, KFAM (evaluated when a pod is admitted: ports may be ephemeral)
+  std::function<std::vector<std::string>()> egress_endpoints;
 };
 
 struct ContainerRt;  // one container's process state (kubelet.cc)
 
-// A pod's inbound enforcement point (the Istio sidecar's inbound listener): the kubelet binds
-// pod_ip:port for every declared containerPort of a mesh-injected pod, the app listens on the pod's
-// private app_ip, and each request is handed to the gateway's policy check (Gateway::handle_inbound)
-// before it is proxied to app_ip:port. Kubelet probes go to app_ip directly (exempt, as Istio's
-// rewritten probes are).
+// A pod's inbound enforcement point (the CNI's NetworkPolicy hook + the Istio sidecar's inbound
+// listener): the kubelet binds pod_ip:port (host namespace) for every declared TCP containerPort —
+// of every pod when pods have their own network namespace (node/netns.h), else of mesh-injected and
+// NetworkPolicy-selected pods, whose apps then listen on a private app_ip — and each request is
+// handed to the gateway's policy check (Gateway::handle_inbound) before it is proxied to the app.
+// Kubelet probes go to the app directly (exempt, as Istio's rewritten probes are).
 struct InboundTarget {
-  std::string ns, name, app_ip;
+  std::string ns, name, app_ip, pod_ip;
   int port = 0;
+  std::string port_name;  // the containerPort's name (NetworkPolicy named ports)
   std::map<std::string, std::string> labels;
+  bool mesh = false;                      // Istio sidecar semantics (AuthorizationPolicies) too
+  std::shared_ptr<const PodNetns> netns;  // the app's namespace (nullptr: app_ip on the host)
 };
 using InboundHandler = std::function<void(const InboundTarget&, HttpRequest&, HttpResponse&)>;
 
@@ -126,6 +138,7 @@ class Kubelet {
   bool exec(const std::string& ns, const std::string& pod, const std::string& container,
             const std::vector<std::string>& argv, double timeout_s, int& exit_code, std::string& output, std::string& err);
   GpuAllocator& gpus() { return *alloc_; }
+  bool pod_netns() const { return netns_; }
   const std::string& node_name() const { return cfg_.node_name; }
   // pods of mesh-injected namespaces (label istio-injection=enabled, pod annotation
   // sidecar.istio.io/inject not "false") get an inbound listener per containerPort (set before start)
@@ -165,8 +178,12 @@ class Kubelet {
   void publish_readiness(PodSync& s);
   ApiError write_status(PodSync& s);
   bool wants_sidecar(const Json& pod);
-  void start_inbound(PodRuntime& rt, const Json& pod);
+  bool selected_by_netpol(const Json& pod);
+  void start_inbound(PodRuntime& rt, const Json& pod, bool mesh);
+  bool setup_pod_network(PodRuntime& rt, const Json& pod);
   InboundHandler inbound_;
+  bool netns_ = false;                  // pods get their own network namespace (decided at start())
+  std::unique_ptr<EgressRelay> relay_;  // their egress to the node endpoints
   std::shared_ptr<Client> c_;
   KubeletConfig cfg_;
   std::unique_ptr<GpuAllocator> alloc_;
@@ -226,6 +243,10 @@ struct GatewayOptions {
   std::string auth_cookie = "kfamd-token";  // browser sessions: the bearer token as a cookie
   bool enforce = true;                      // evaluate AuthorizationPolicies (ALLOW/DENY)
   int mesh_port = -1;                       // in-cluster listener (-1 = off, 0 = ephemeral)
+  // NetworkPolicy source of a connection made straight to a pod's inbound listener by a node process
+  // (the culler, the API server's service proxy): the control plane's namespace
+  std::string control_plane_namespace = "kubeflow";
+  bool pods_have_listeners = false;  // every pod has an inbound listener (kubelet --pod-netns)
 };
 
 class Gateway {
@@ -242,11 +263,14 @@ class Gateway {
   // mesh (the destination sidecars' job, done node-wide like Istio ambient's ztunnel): Host names a
   // Service, the caller's identity is its ServiceAccount token in X-Kfamd-Peer-Token
   void handle_mesh(HttpRequest& req, HttpResponse& resp);
-  // a pod's inbound listener (InboundTarget): requests the ingress / mesh listener already
-  // authorized carry this node's hop secret and pass; any other caller (a process dialing the pod IP
-  // directly) is evaluated against the pod's namespace policies with its own identity (ServiceAccount
-  // token in X-Kfamd-Peer-Token, else none); then proxied to the app
+  // a pod's inbound listener (InboundTarget): NetworkPolicy (ingress rules against the caller's
+  // namespace / pod labels / address) for every pod with a listener, then, for mesh-injected pods,
+  // the namespace's AuthorizationPolicies on the pod's own labels. Requests the ingress / mesh
+  // listener authorized carry a signed proof naming the caller (X-Kfamd-Hop); any other caller is
+  // evaluated with its own identity (ServiceAccount token in X-Kfamd-Peer-Token, else none). Then
+  // proxied to the app (inside the pod's network namespace when it has one).
   void handle_inbound(const InboundTarget& t, HttpRequest& req, HttpResponse& resp);
+  void set_pods_have_listeners(bool v) { o_.pods_have_listeners = v; }
 
   struct Route {
     std::string prefix, rewrite, dest_host;
@@ -276,7 +300,22 @@ class Gateway {
                           const HttpRequest& req, const std::string& path, const Headers& fwd,
                           const std::string& principal, const std::string& source_ns, std::string* why);
   void peer_identity(const HttpRequest& req, std::string& principal, std::string& source_ns);
-  std::string hop_secret_;  // stamped on requests this gateway authorized (X-Kfamd-Hop)
+  // the caller a signed hop proof names (kHopHeader in gateway.cc)
+  struct HopClaims {
+    std::string principal, source_ns;
+    bool source_pod = false;
+    std::map<std::string, std::string> source_labels;
+  };
+  std::string stamp_hop(const std::string& method, const std::string& path, const std::string& dest_ns,
+                        const HopClaims& who) const;
+  bool verify_hop(const std::string& value, const std::string& method, const std::string& path,
+                  const std::string& dest_ns, HopClaims& out) const;
+  HopClaims mesh_caller(const HttpRequest& req);
+  std::map<std::string, std::string> namespace_labels(const std::string& ns);
+  bool dest_has_listener(const std::string& ns);
+  Result reconcile_mesh_policy(const Request& r, std::string* err);
+  std::shared_ptr<Controller> mesh_np_;
+  std::string hop_secret_;  // HMAC key of the hop proofs
   void forward(HttpRequest& req, HttpResponse& resp, const std::string& url, Headers h, int timeout_ms);
 
   std::shared_ptr<Client> c_;
@@ -285,6 +324,8 @@ class Gateway {
   Informer* routes_ = nullptr;
   Informer* policies_ = nullptr;
   Informer* services_ = nullptr;
+  Informer* netpols_ = nullptr;
+  Informer* namespaces_ = nullptr;
   std::unique_ptr<HttpServer> srv_, mesh_;
   std::shared_ptr<CounterVec> upgrades_, streams_, decisions_;
   // host an OpenShift router gives a Route without spec.host: <name>-<namespace>.<domain>

@@ -33,7 +33,10 @@ def _ready(o):
 @pytest.fixture(scope="module")
 def c(cluster):
     cl = cluster.client
-    cl.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "e2e"}})
+    # a mesh member, like every Kubeflow profile namespace (profile_controller.go:71): the ODH
+    # controller's <nb>-ctrl-np admits only its own namespace on :8888, and the member namespace's
+    # mesh policy (istio-mesh) is what admits the ingress gateway
+    cl.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "e2e", "labels": {"istio-injection": "enabled"}}})
     return cl
 
 

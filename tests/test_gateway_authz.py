@@ -161,6 +161,11 @@ def test_mesh_admits_the_culler_principal_and_same_namespace_only(cl):
     assert cl.mesh
     nbc = _sa_token(c, "kubeflow", "notebook-controller-service-account")
     same_ns = _sa_token(c, "alice", "default-editor")
+    # bob-team is another mesh member (a profile namespace): L4 admits it, Istio decides
+    try:
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "bob-team", "labels": {"istio-injection": "enabled"}}})
+    except ApiException as e:
+        assert e.status == 409
     other = _sa_token(c, "bob-team", "default")
     assert _mesh(cl) == 403                                  # plaintext caller: no principal
     assert _mesh(cl, other) == 403                           # another namespace's workload

@@ -138,7 +138,7 @@ def test_gpu_pod_pinned_to_numa_local_cpus_and_partition_hbm_quota(tmp_path):
         assert labels["amd.com/gpu.compute-partitioning-mode"] == "cpx"
         assert labels["amd.com/gpu.memory-partitioning-mode"] == "nps2"
         assert labels["amd.com/gpu.hbm-gib-per-device"] == "36"
-        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "pin"}})
+        c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "pin", "labels": {"istio-injection": "enabled"}}})
         c.create({"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q", "namespace": "pin"},
                   "spec": {"hard": {"amd.com/gpu-memory": "1000"}}})
         # fill package 0 (8 partitions, NUMA 0) so the notebook lands on package 1 (NUMA 1)
