@@ -77,13 +77,15 @@ def parse_args():
     return p.parse_args()
 
 
-COLD_START_NOTE = ("process pods (no container runtime); notebook server = stub recipe (no torch import); "
-                   "cold_start_torch_ready_* = same path with a server that imports torch + runs a GEMM on the GPU "
-                   "before Ready (fresh interpreter); cold_start_torch_ready_zygote_* = that server forked from the "
-                   "kubelet's pre-imported interpreter (torch imported once per node); cold_start_odh_* = ODH path "
-                   "with the OAuth proxy + reconciliation lock; the GPU readiness op runs as a native sidecar "
-                   "overlapping the server start. *_failures = runs not Ready within the per-run timeout, with "
-                   "pod diagnostics in cold_start_failures")
+COLD_START_NOTE = ("process pods (no container runtime). cold_start_* = the product's default path: the "
+                   "jupyter-pytorch-rocm notebook server (imports torch, runs a GEMM on its GPU before Ready) forked "
+                   "from the kubelet's pre-imported interpreter (--pod-zygote, on by default), a 1-GPU pod taking "
+                   "the zygote's warm child of its GPU (HIP + device context already up); cold_start_stub_* = a "
+                   "server that imports nothing (control plane + readiness op alone); cold_start_torch_ready_fresh_* "
+                   "= the torch server in a fresh interpreter (--pod-zygote=false); cold_start_odh_* = ODH path with "
+                   "the OAuth proxy + reconciliation lock. The GPU readiness op runs as a native sidecar overlapping "
+                   "the server start. *_failures = runs not Ready within the per-run timeout, with pod diagnostics "
+                   "in cold_start_failures")
 
 
 def _cs_keys(prefix: str, cs: dict) -> dict:
@@ -91,6 +93,8 @@ def _cs_keys(prefix: str, cs: dict) -> dict:
            f"{prefix}_phases_p50_s": cs.get("phases_p50_s"), f"{prefix}_failures": len(cs.get("failures") or [])}
     if cs.get("server_warmup_p50_ms"):
         out[f"{prefix}_server_p50_ms"] = cs["server_warmup_p50_ms"]
+    if cs.get("warm_children") is not None:
+        out[f"{prefix}_warm_children"] = cs["warm_children"]
     if cs.get("truncated"):
         out[f"{prefix}_truncated"] = True
     if cs.get("failures"):
@@ -99,11 +103,19 @@ def _cs_keys(prefix: str, cs: dict) -> dict:
 
 
 def run_cold_starts(ex, args, world: int) -> None:
-    """Rank 0: the four cold-start variants and the control-plane latencies, each its own extra."""
+    """Rank 0: the cold-start variants and the control-plane latencies, each its own extra."""
     from kubeflow_rm_amd.bench_coldstart import measure_cold_start, measure_control_plane, measure_gpu_notebook_configs
 
-    def stub(e):
-        cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world, timeout=30, deadline=e.deadline())
+    def merge_failures(e, out):
+        f = out.pop("cold_start_failures", None)
+        if f:
+            e.data.setdefault("cold_start_failures", {}).update(f)
+        return out
+
+    def default_path(e):
+        # the product's default: torch-ready server, kubelet --pod-zygote (kflite's default), warm GPU child
+        cs = measure_cold_start(runs=args.coldstart_runs, gpus_per_notebook=world, server="torch-ready",
+                                namespace="bench", zygote=True, timeout=30, deadline=e.deadline())
         out = _cs_keys("cold_start", cs)
         out.update({"cold_start_gpus_per_notebook": world, "cold_start_readiness": cs.get("readiness"),
                     "cold_start_note": COLD_START_NOTE})
@@ -116,23 +128,17 @@ def run_cold_starts(ex, args, world: int) -> None:
         out["reconcile_by_controller"] = cs.get("reconcile")
         return out
 
-    def merge_failures(e, out):
-        f = out.pop("cold_start_failures", None)
-        if f:
-            e.data.setdefault("cold_start_failures", {}).update(f)
-        return out
-
-    ex.run("cold_start_stub", lambda e: merge_failures(e, stub(e)), est_s=10, timeout_s=90)
+    ex.run("cold_start", lambda e: merge_failures(e, default_path(e)), est_s=20, timeout_s=150)
+    # the control plane + readiness op alone (a server that imports nothing)
+    ex.run("cold_start_stub", lambda e: merge_failures(e, _cs_keys("cold_start_stub", measure_cold_start(
+        runs=args.coldstart_runs, gpus_per_notebook=world, namespace="bench-stub", timeout=30,
+        deadline=e.deadline()))), est_s=10, timeout_s=90)
     if args.coldstart_torch_runs > 0:
-        # the torch-ready server, fresh interpreter (the jupyter-pytorch-rocm image's cold start)
-        ex.run("cold_start_torch_ready", lambda e: merge_failures(e, _cs_keys("cold_start_torch_ready", measure_cold_start(
-            runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready", namespace="bench-torch",
-            timeout=30, deadline=e.deadline()))), est_s=15, timeout_s=120)
-        # the same server forked from the node's pre-imported interpreter (kubelet --pod-zygote)
-        ex.run("cold_start_torch_ready_zygote", lambda e: merge_failures(e, _cs_keys(
-            "cold_start_torch_ready_zygote", measure_cold_start(
-                runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready", namespace="bench-zygote",
-                zygote=True, timeout=30, deadline=e.deadline()))), est_s=20, timeout_s=120)
+        # the torch-ready server in a fresh interpreter (--pod-zygote=false)
+        ex.run("cold_start_torch_ready_fresh", lambda e: merge_failures(e, _cs_keys(
+            "cold_start_torch_ready_fresh", measure_cold_start(
+                runs=args.coldstart_torch_runs, gpus_per_notebook=world, server="torch-ready", namespace="bench-torch",
+                timeout=30, deadline=e.deadline()))), est_s=15, timeout_s=120)
     # the fork's own spawn path: ODH webhook lock + OAuth proxy + two reconciles
     ex.run("cold_start_odh", lambda e: merge_failures(e, _cs_keys("cold_start_odh", measure_cold_start(
         runs=max(3, args.coldstart_runs // 2), gpus_per_notebook=world, odh_oauth=True, namespace="bench-odh",

@@ -258,6 +258,7 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                 if not isinstance(rep, dict):
                     continue
                 stages = {"hip_init_ms": rep.get("hip_init_ms"), "total_ms": rep.get("total_ms"),
+                          "warm_op": 1.0 if rep.get("warm_op_ms") is not None else 0.0,
                           **{f"{k}_ms": v for k, v in (rep.get("stages_ms") or {}).items()},
                           **{f"gemm_{k}": v for k, v in (rep.get("gemm0_stages_ms") or {}).items()}}
             ctl_phases = None
@@ -286,7 +287,14 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
                             warm["initialized_to_start_ms"] = round((t_cs - t_init) * 1e3, 1)
                 except Exception:  # noqa: BLE001 - diagnostics only
                     pass
+            warm_child = None
+            if zygote:  # did the container take the zygote's warm GPU child? (the kubelet's log line)
+                try:
+                    warm_child = "# kflite: warm child of zygote" in c.pod_logs(f"{name}-0", namespace, container=name)
+                except Exception:  # noqa: BLE001 - diagnostics only
+                    pass
             out_runs.append({"cold_start_s": t1 - t0, "phases": phases, "readiness_stages": stages, "server_warmup": warm,
+                             "warm_child": warm_child,
                              "controller_phases_ms": ctl_phases,
                              "gpus": (obj.get("status") or {}).get("gpus"),
                              "gpuReadiness": (obj.get("status") or {}).get("gpuReadiness")})
@@ -310,6 +318,8 @@ def measure_cold_start(runs: int = 5, gpus_per_notebook: int = 1, gpus: int | No
     if wk:
         res["server_warmup_p50_ms"] = {k: _pct([r["server_warmup"][k] for r in out_runs if (r.get("server_warmup") or {}).get(k)
                                                 is not None], 0.5) for k in wk if k.endswith("_ms")}
+    if zygote:
+        res["warm_children"] = sum(1 for r in out_runs if r.get("warm_child"))
     rd = [r["gpuReadiness"] for r in out_runs if r.get("gpuReadiness")]
     if rd:
         res["readiness"] = rd[-1]

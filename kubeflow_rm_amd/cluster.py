@@ -126,6 +126,7 @@ class LocalCluster:
             socks = sorted(str(p) for p in root.glob("zygote-*.sock"))
             logs = sorted(root.glob("zygote-*.log"))
             if socks and len(socks) >= len(logs):
+                self.wait_warm(max(0.0, deadline - time.time()))
                 return socks
             for lg in logs:
                 t = lg.read_text(errors="replace")
@@ -133,6 +134,32 @@ class LocalCluster:
                     raise RuntimeError(f"zygote failed: {t[-2000:]}")
             time.sleep(0.05)
         raise TimeoutError("zygote did not come up")
+
+    def wait_warm(self, timeout: float = 30.0) -> dict:
+        """Block until every zygote started with warm GPU children has reported each of them ready or
+        failed (zygote.py: "[zygote] warm child <pid> for device <d> ready|failed"); a zygote without
+        warm devices returns at once. Returns {device: "ready" | "failed"} of the last report each."""
+        import re
+        root = Path(self.data_dir) / "kubelet"
+        deadline = time.time() + timeout
+        state: dict = {}
+        while True:
+            want = set()
+            for lg in root.glob("zygote-*.log"):
+                t = lg.read_text(errors="replace")
+                for dev, what in re.findall(r"warm child \d+ for device (\d+) (ready|failed)", t):
+                    state[int(dev)] = what
+            try:
+                cmdlines = [open(f"/proc/{p}/cmdline", "rb").read().split(b"\0") for p in os.listdir("/proc") if p.isdigit()]
+            except OSError:
+                cmdlines = []
+            for cl in cmdlines:
+                if b"kubeflow_rm_amd.images.zygote" in cl and b"--warm-devices" in cl and str(root).encode() in b" ".join(cl):
+                    i = cl.index(b"--warm-devices")
+                    want |= {int(x) for x in cl[i + 1].decode().split(",") if x}
+            if want <= set(state) or time.time() > deadline:
+                return state
+            time.sleep(0.05)
 
     def stop(self) -> None:
         if self.proc and self.proc.poll() is None:

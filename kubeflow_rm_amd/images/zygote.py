@@ -17,7 +17,17 @@ Protocol (one AF_UNIX stream connection per container start, JSON lines):
   zygote  -> kubelet  {"exit": 0, "signal": 0}      when the process ends, then close
 
 The connection stays open for the life of the container: it is how the kubelet (which is not the
-process's parent) learns the exit status. The kubelet kills the process group (the child calls
+process's parent) learns the exit status.
+
+Warm GPU children (``--warm-devices 0,1,...``, ``--warm-modules``): per node GPU, the zygote keeps one
+forked child that has already brought up HIP, torch's device context, the first GPU operation and the
+framework's GEMM code object on that device alone (ROCR_VISIBLE_DEVICES=<d>, HIP_VISIBLE_DEVICES=0,
+exactly the env the device plugin gives a 1-GPU pod on <d>), and then waits. A 1-GPU container
+request that names ``"warm_device": d``, runs a module of ``--warm-modules`` and whose HIP-relevant env
+matches the warm child's takes it: the child becomes the container (same steps as a fresh fork) and
+the zygote forks the next warm child for <d>. The ~200 ms of HIP + device bring-up then happen
+before the pod exists instead of on its cold-start path. Warm children die with the zygote until
+claimed; nothing of a tenant ever runs in one before it is claimed, and each is used once. The kubelet kills the process group (the child calls
 setsid). Safety: the zygote refuses to serve if its preload opened the GPU driver (/dev/kfd): a
 fork of a process with a live HIP context is undefined. It also refuses if the preload left any
 native thread besides the main one: fork() copies only the calling thread, so a lock another thread
@@ -38,6 +48,7 @@ import importlib
 import json
 import os
 import runpy
+import select
 import selectors
 import signal
 import socket
@@ -132,8 +143,88 @@ def _join_netns(path: str) -> None:
         os.close(fd)
 
 
-def _child(req: dict, closefds: list[int]) -> None:
-    """Runs in the forked process: become the container, run its module, never return."""
+# env read when HIP / ROCr / comgr initialise: a warm child serves a request only if these match
+_HIP_ENV_PREFIXES = ("ROCR_", "HIP_", "HSA_", "GPU_", "CUDA_", "AMD_", "PYTORCH_")
+_HIP_ENV_IGNORE = {"AMD_COMGR_CACHE_DIR", "AMD_COMGR_CACHE"}
+
+
+def _hip_env(env: dict) -> dict:
+    return {k: v for k, v in env.items() if k.startswith(_HIP_ENV_PREFIXES) and k not in _HIP_ENV_IGNORE}
+
+
+def _warm_env(dev: int) -> dict:
+    """The env a warm child initialises the GPU under: the zygote's (the kubelet's pass-through
+    HSA_* / ROCm settings) plus the device plugin's 1-GPU view of device `dev`."""
+    env = {k: v for k, v in os.environ.items() if k not in _POOL_ENV}
+    for k in [k for k in env if k.startswith(_HIP_ENV_PREFIXES)]:
+        if k.endswith("VISIBLE_DEVICES") or k == "GPU_DEVICE_ORDINAL":
+            del env[k]
+    env.update({"ROCR_VISIBLE_DEVICES": str(dev), "HIP_VISIBLE_DEVICES": "0",
+                # no comgr cache while warming: the cache dir is per tenant and this child has none yet
+                "AMD_COMGR_CACHE": "0"})
+    return env
+
+
+def _warm_child(dev: int, ctl: socket.socket, closefds: list[int]) -> None:
+    """Runs in a forked warm child: bring the GPU up, report, wait for a container request on `ctl`,
+    then become that container (_child). Never returns."""
+    try:
+        gc.enable()
+        for fd in closefds:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        signal.set_wakeup_fd(-1)
+        try:
+            import ctypes
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGKILL, 0, 0, 0)  # dies with the zygote until claimed
+        except (OSError, AttributeError):
+            pass
+        env = _warm_env(dev)
+        os.environ.clear()
+        os.environ.update(env)
+        t0 = time.perf_counter()
+        import torch
+        torch.cuda.init()
+        x = torch.zeros(1 << 20, device="cuda")
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        steps = {"device_ms": round((t1 - t0) * 1e3, 1)}
+        try:  # the notebook server's first GEMM shape: its code object is resident before the pod exists
+            from kubeflow_rm_amd import ops
+            a = torch.ones(1024, 1024, device="cuda", dtype=torch.bfloat16)
+            ops.gemm_nt(a, a)
+            torch.cuda.synchronize()
+            steps["kernels_ms"] = round((time.perf_counter() - t1) * 1e3, 1)
+        except Exception as e:  # noqa: BLE001 - the container loads them itself then
+            steps["kernels_error"] = f"{type(e).__name__}: {e}"
+        del x
+        ctl.sendall((json.dumps({"ready": True, "device": dev, "env": _hip_env(env), **steps}) + "\n").encode())
+        buf = b""
+        while not buf.endswith(b"\n"):
+            chunk = ctl.recv(65536)
+            if not chunk:
+                os._exit(0)  # the zygote went away or retired this child
+            buf += chunk
+        req = json.loads(buf)
+    except BaseException as e:  # noqa: BLE001 - a child that cannot warm up says so and leaves
+        try:
+            ctl.sendall((json.dumps({"ready": False, "error": f"{type(e).__name__}: {e}"}) + "\n").encode())
+        except OSError:
+            pass
+        os._exit(1)
+    try:
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, 0, 0, 0, 0)  # claimed: lives like any container
+    except (OSError, AttributeError):
+        pass
+    _child(req, [ctl.fileno()], warm=True)
+
+
+def _child(req: dict, closefds: list[int], warm: bool = False) -> None:
+    """Runs in the forked process (or a claimed warm child): become the container, run its module,
+    never return."""
     code = 1
     try:
         gc.enable()
@@ -152,10 +243,12 @@ def _child(req: dict, closefds: list[int]) -> None:
         signal.pthread_sigmask(signal.SIG_SETMASK, [])
         cpus = [c for c in req.get("cpus") or [] if isinstance(c, int)]
         if cpus:
-            try:
-                os.sched_setaffinity(0, cpus)
-            except OSError:
-                pass
+            # a warm child already runs the GPU runtime's threads: every thread gets the mask
+            for tid in (os.listdir("/proc/self/task") if warm else ["0"]):
+                try:
+                    os.sched_setaffinity(int(tid), cpus)
+                except OSError:
+                    pass
         fd = os.open(req["log"], os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
         nul = os.open(os.devnull, os.O_RDONLY)
         os.dup2(nul, 0)
@@ -199,7 +292,8 @@ def _child(req: dict, closefds: list[int]) -> None:
 _PRELOADED: set[str] = set()
 
 
-def serve(sock_path: str, preload: list[str]) -> int:
+def serve(sock_path: str, preload: list[str], warm_devices: list[int] | None = None,
+          warm_modules: list[str] | None = None) -> int:
     t0 = time.perf_counter()
     # pre-fork server idiom (Python docs, gc.freeze): no collections while the preload allocates (no
     # freed holes in shared pages), then every preloaded object moves to the permanent generation, so a
@@ -248,6 +342,107 @@ def serve(sock_path: str, preload: list[str]) -> int:
     sel.register(lsock, selectors.EVENT_READ, "listen")
     sel.register(rd, selectors.EVENT_READ, "sigchld")
     children: dict[int, socket.socket] = {}
+    warm_devices = list(warm_devices or [])
+    warm_modules = set(warm_modules or [])
+    # device -> {"pid", "sock", "ready": bool, "env": {...}}; at most one per device
+    warm: dict[int, dict] = {}
+    warm_failures: dict[int, int] = {}
+    warm_due: dict[int, float] = {}  # device -> when to fork its next warm child (after a claim)
+
+    def start_warm(dev: int) -> None:
+        if dev in warm or warm_failures.get(dev, 0) >= 3 or stop:
+            return
+        if len(_native_threads()) > 1:
+            return
+        parent, child = socket.socketpair()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        pid = os.fork()
+        if pid == 0:
+            parent.close()
+            _warm_child(dev, child, [lsock.fileno(), rd, wr] + [c.fileno() for c in children.values()] +
+                        [w["sock"].fileno() for w in warm.values()])
+        child.close()
+        warm[dev] = {"pid": pid, "sock": parent, "ready": False, "started": time.perf_counter()}
+        sel.register(parent, selectors.EVENT_READ, ("warm", dev))
+
+    def warm_message(dev: int) -> None:
+        w = warm.get(dev)
+        if w is None:
+            return
+        try:
+            line = w["sock"].recv(65536)
+        except OSError:
+            line = b""
+        msg = {}
+        try:
+            msg = json.loads(line) if line else {}
+        except ValueError:
+            pass
+        if msg.get("ready"):
+            w["ready"] = True
+            w["env"] = msg.get("env") or {}
+            warm_failures[dev] = 0
+            print(f"[zygote] warm child {w['pid']} for device {dev} ready in "
+                  f"{(time.perf_counter() - w['started']) * 1e3:.0f} ms {msg}", flush=True)
+            return
+        print(f"[zygote] warm child {w['pid']} for device {dev} failed: {msg.get('error') or 'exited'}", flush=True)
+        retire(dev)
+        warm_failures[dev] = warm_failures.get(dev, 0) + 1
+
+    def retire(dev: int) -> None:
+        w = warm.pop(dev, None)
+        if w is None:
+            return
+        try:
+            sel.unregister(w["sock"])
+        except (KeyError, ValueError):
+            pass
+        w["sock"].close()  # an unclaimed child exits on EOF
+
+    def claim(dev: int, req: dict, conn: socket.socket) -> bool:
+        """Hand `req` to the warm child of `dev` if it is ready (waiting up to 0.3 s for one that is
+        still warming) and its GPU env matches the request's."""
+        w = warm.get(dev)
+        if w is None:
+            return False
+        deadline = time.perf_counter() + 0.3
+        while not w["ready"] and time.perf_counter() < deadline:
+            r, _, _ = select.select([w["sock"]], [], [], max(0.0, deadline - time.perf_counter()))
+            if r:
+                warm_message(dev)
+                w = warm.get(dev)
+                if w is None:
+                    return False
+        if not w["ready"]:
+            return False
+        env = dict(kv.split("=", 1) for kv in req.get("env") or [] if "=" in kv)
+        if _hip_env(env) != w["env"]:
+            print(f"[zygote] warm child for device {dev} not used: GPU env differs "
+                  f"({sorted(set(_hip_env(env).items()) ^ set(w['env'].items()))[:6]})", flush=True)
+            return False
+        try:
+            w["sock"].sendall((json.dumps(req) + "\n").encode())
+        except OSError:
+            retire(dev)
+            return False
+        pid = w["pid"]
+        try:
+            sel.unregister(w["sock"])
+        except (KeyError, ValueError):
+            pass
+        w["sock"].close()
+        del warm[dev]
+        children[pid] = conn
+        conn.settimeout(None)
+        try:
+            conn.sendall((json.dumps({"pid": pid, "warm": True}) + "\n").encode())
+        except OSError:
+            pass
+        # the next one warms up once this container's own GPU start is past (no KFD contention on its
+        # cold-start path)
+        warm_due[dev] = time.perf_counter() + 0.3
+        return True
 
     def reap():
         while True:
@@ -290,6 +485,10 @@ def serve(sock_path: str, preload: list[str]) -> int:
                 pass
             conn.close()
             return
+        dev = req.get("warm_device")
+        if (isinstance(dev, int) and dev in warm and len(argv) >= 2 and argv[1] in warm_modules
+                and claim(dev, req, conn)):
+            return
         sys.stdout.flush()
         sys.stderr.flush()
         threads = _native_threads()
@@ -304,7 +503,8 @@ def serve(sock_path: str, preload: list[str]) -> int:
             return
         pid = os.fork()
         if pid == 0:
-            _child(req, [lsock.fileno(), rd, wr] + [c.fileno() for c in children.values()] + [conn.fileno()])
+            _child(req, [lsock.fileno(), rd, wr] + [c.fileno() for c in children.values()] + [conn.fileno()] +
+                   [w["sock"].fileno() for w in warm.values()])
         children[pid] = conn
         conn.settimeout(None)
         try:
@@ -312,8 +512,15 @@ def serve(sock_path: str, preload: list[str]) -> int:
         except OSError:
             pass
 
+    for d in warm_devices:
+        start_warm(d)
     while not stop:
-        for key, _ in sel.select(timeout=1.0):
+        now = time.perf_counter()
+        timeout = min([1.0] + [max(0.0, t - now) for t in warm_due.values()])
+        for key, _ in sel.select(timeout=timeout):
+            if isinstance(key.data, tuple):  # a warm child's report (or its exit)
+                warm_message(key.data[1])
+                continue
             if key.data == "listen":
                 try:
                     conn, _ = lsock.accept()
@@ -327,6 +534,13 @@ def serve(sock_path: str, preload: list[str]) -> int:
                 except (BlockingIOError, OSError):
                     pass
         reap()
+        now = time.perf_counter()
+        for d in warm_devices:  # a claimed / retired / failed warm child is replaced (at most 3 failures in a row)
+            if d not in warm and warm_due.get(d, 0.0) <= now:
+                warm_due.pop(d, None)
+                start_warm(d)
+    for d in list(warm):
+        retire(d)
     try:
         os.unlink(sock_path)
     except OSError:
@@ -338,10 +552,14 @@ def main(argv=None) -> int:
     p = argparse.ArgumentParser(description="pre-imported interpreter for process pods")
     p.add_argument("--socket", required=True)
     p.add_argument("--preload", default="", help="comma-separated modules to import before serving")
+    p.add_argument("--warm-devices", default="", help="comma-separated node GPU ids to keep a warm child for")
+    p.add_argument("--warm-modules", default="kubeflow_rm_amd.images.notebook_server",
+                   help="comma-separated container modules a warm child may become")
     a = p.parse_args(argv)
     for k in _POOL_ENV:  # the containers get their own env; these only shape the preload
         os.environ[k] = "1"
-    return serve(a.socket, [m for m in a.preload.split(",") if m])
+    return serve(a.socket, [m for m in a.preload.split(",") if m],
+                 [int(d) for d in a.warm_devices.split(",") if d.strip()], [m for m in a.warm_modules.split(",") if m])
 
 
 if __name__ == "__main__":

@@ -26,6 +26,7 @@ struct ComponentFlags {
   std::string sysfs_root;  // GPU discovery root ("" = /sys)
   bool numa_pinning = true;
   bool pod_zygote = true;
+  bool pod_warm_gpus = true;
   std::string pod_netns = "auto";  // per-pod network namespaces (node/netns.h)
   std::string image_recipes;
   // gateway (Istio ingress equivalent)

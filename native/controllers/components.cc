@@ -31,6 +31,9 @@ void ComponentFlags::register_flags(Flags& f) {
   f.add_bool("pod-zygote", &pod_zygote, true,
              "fork Python pod containers from a pre-imported interpreter per image recipe (torch preloaded; "
              "a container whose recipe has none, or that the zygote refuses, starts a fresh interpreter)");
+  f.add_bool("pod-warm-gpus", &pod_warm_gpus, true,
+             "keep one warm child per GPU in torch zygotes (HIP + device context initialised before a 1-GPU pod "
+             "on that GPU starts)");
   f.add_string("pod-netns", &pod_netns, "auto",
                "per-pod network namespaces: auto (when the node can create them), on (required), off");
   f.add_string("gateway-address", &gateway_addr, "127.0.0.1", "ingress gateway bind address");
@@ -289,6 +292,7 @@ void Components::Impl::setup_kubelet(Manager& mgr) {
   kc.sysfs_root = f.sysfs_root;
   kc.numa_pinning = f.numa_pinning;
   kc.pod_zygote = f.pod_zygote;
+  kc.pod_warm_gpus = f.pod_warm_gpus;
   kc.pod_netns = f.pod_netns;
   kc.recipes_file = f.image_recipes;
   const Impl* self = this;

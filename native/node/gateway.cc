@@ -140,7 +140,7 @@ Result Gateway::reconcile_mesh_policy(const Request& r, std::string* err) {
 // pods of `ns` have inbound listeners: every pod when pods get network namespaces, else the
 // mesh-injected namespaces' (and NetworkPolicy-selected pods, which do not need the hop proof)
 bool Gateway::dest_has_listener(const std::string& ns) {
-  if (o_.pods_have_listeners) return true;
+  if (pods_have_listeners_) return true;
   Json n;
   return namespaces_ && namespaces_->get("", ns, n) && n.at_path({"metadata", "labels", "istio-injection"}).as_string() == "enabled";
 }

@@ -373,6 +373,7 @@ void Kubelet::start() {
     return true;
   });
   if (cfg_.pod_zygote) start_zygotes();
+  start_warm_ops();
   running_ = true;
   hb_ = std::thread([this] {
     set_thread_name("kubelet-hb");
@@ -445,6 +446,7 @@ void Kubelet::heartbeat_loop() {
     for (int i = 0; i < 100 && running_; ++i) {
       ::usleep(100000);
       if (cfg_.pod_zygote && i % 10 == 9 && running_) supervise_zygotes();
+      if (running_) supervise_warm_ops();
     }
     if (!running_) break;
     c_->update_with_retry(
@@ -490,6 +492,7 @@ void Kubelet::stop() {
   }
   if (relay_) relay_->stop();
   stop_zygotes();
+  stop_warm_ops();
 }
 
 // ---- process management ---------------------------------------------------------------------------
@@ -624,7 +627,7 @@ bool reap(pid_t pid, int& exit_code, std::string& reason) {
 // there or refuses (the caller then spawns a fresh interpreter).
 pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv, const std::vector<std::string>& env,
                    const std::string& cwd, const std::string& log_path, const std::vector<int>& cpus, int* zfd,
-                   std::string* err, const std::string& netns_path = "") {
+                   std::string* err, const std::string& netns_path = "", int warm_device = -1, bool* warm = nullptr) {
   const int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (fd < 0) return -1;
   sockaddr_un a{};
@@ -643,6 +646,7 @@ pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv
   for (const auto& e : env) req["env"].push_back(e);
   for (int c : cpus) req["cpus"].push_back(static_cast<int64_t>(c));
   if (!netns_path.empty()) req["netns"] = netns_path;  // the child joins the pod's namespace first
+  if (warm_device >= 0) req["warm_device"] = warm_device;  // a warm child of that GPU may take it
   const std::string line = req.dump() + "\n";
   size_t off = 0;
   while (off < line.size()) {
@@ -671,6 +675,7 @@ pid_t zygote_spawn(const std::string& sock, const std::vector<std::string>& argv
     return -1;
   }
   *zfd = fd;
+  if (warm) *warm = r["warm"].as_bool();
   return static_cast<pid_t>(r["pid"].as_int());
 }
 
@@ -717,9 +722,18 @@ bool Kubelet::spawn_zygote(Zygote& z) {
   }
   env.push_back("PYTHONPATH=" + cfg_.repo_root);
   env.push_back("PYTHONUNBUFFERED=1");
+  std::vector<std::string> argv{cfg_.python, "-m", "kubeflow_rm_amd.images.zygote", "--socket", z.sock, "--preload", z.preload};
+  // warm GPU children (zygote.py): one per node GPU, HIP + device context + first op done before a
+  // 1-GPU pod on that device is admitted; real GPUs only, torch zygotes only
+  if (cfg_.pod_warm_gpus && contains(z.preload, "torch") && alloc_->topology().source != "synthetic" &&
+      ::access("/dev/kfd", R_OK | W_OK) == 0 && alloc_->topology().size() > 0) {
+    std::vector<std::string> ids;
+    for (int i = 0; i < alloc_->topology().size(); ++i) ids.push_back(std::to_string(i));
+    argv.push_back("--warm-devices");
+    argv.push_back(join(ids, ","));
+  }
   std::string err;
-  z.pid = spawn({cfg_.python, "-m", "kubeflow_rm_amd.images.zygote", "--socket", z.sock, "--preload", z.preload}, env,
-                cfg_.root_dir, z.log, &err);
+  z.pid = spawn(argv, env, cfg_.root_dir, z.log, &err);
   z.started = now_seconds();
   return z.pid > 0;
 }
@@ -759,6 +773,72 @@ void Kubelet::supervise_zygotes() {
     static const auto restarts =
         Registry::global().counter("kubelet_zygote_restarts_total", "pre-imported interpreters restarted after an exit");
     if (z.quick_exits < 3 && spawn_zygote(z)) restarts->inc();
+  }
+}
+
+// Warm readiness ops (kfamd-readiness --warm-op): per node GPU, an op process with HIP, the device
+// context and a hardware queue already up, waiting on <root>/warm-readiness/gpu-<d>.sock for the
+// gpu-readiness sidecar of a 1-GPU pod on <d> (readiness.cc claim_warm_op). Each serves one pod and
+// exits; the next one starts kWarmOpRespawnS later (after the claiming pod's own GPU bring-up).
+namespace {
+constexpr double kWarmOpRespawnS = 0.3;
+}
+
+void Kubelet::start_warm_ops() {
+  const std::string bin = cfg_.bin_dir + "/kfamd-readiness";
+  if (!cfg_.pod_warm_gpus || alloc_->topology().source == "synthetic" || alloc_->topology().size() == 0 ||
+      ::access("/dev/kfd", R_OK | W_OK) != 0 || ::access(bin.c_str(), X_OK) != 0)
+    return;
+  warm_dir_ = cfg_.root_dir + "/warm-readiness";
+  make_dirs(warm_dir_);
+  ::chmod(warm_dir_.c_str(), 0700);
+  std::lock_guard<std::mutex> g(wo_mu_);
+  for (int d = 0; d < alloc_->topology().size(); ++d) {
+    WarmOp w;
+    w.dev = d;
+    warm_ops_.push_back(w);
+  }
+}
+
+void Kubelet::supervise_warm_ops() {
+  std::lock_guard<std::mutex> g(wo_mu_);
+  const double now = now_seconds();
+  for (auto& w : warm_ops_) {
+    if (w.pid > 0) {
+      int st = 0;
+      if (::waitpid(w.pid, &st, WNOHANG) != w.pid) continue;
+      // served a pod (exit after its verdict) or failed to warm up (exit 3 within seconds)
+      const bool quick = now - w.started < 5.0 && WIFEXITED(st) && WEXITSTATUS(st) == 3;
+      w.failures = quick ? w.failures + 1 : 0;
+      w.pid = -1;
+      w.next_start = now + kWarmOpRespawnS;
+    }
+    if (w.pid > 0 || w.failures >= 3 || now < w.next_start) continue;
+    std::vector<std::string> env;
+    for (char** e = environ; *e; ++e) {
+      const std::string kv = *e, k = kv.substr(0, kv.find('='));
+      if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || starts_with(k, "HSA_") ||
+          starts_with(k, "KFAMD_") || starts_with(k, "ROCM") || k == "HOME")
+        env.push_back(kv);
+    }
+    // the device plugin's view of a 1-GPU pod on this device (gpu_env_for)
+    env.push_back("ROCR_VISIBLE_DEVICES=" + std::to_string(w.dev));
+    env.push_back("HIP_VISIBLE_DEVICES=0");
+    const std::string sock = warm_dir_ + "/gpu-" + std::to_string(w.dev) + ".sock";
+    std::string err;
+    w.pid = spawn({cfg_.bin_dir + "/kfamd-readiness", "--warm-op", sock}, env, warm_dir_,
+                  warm_dir_ + "/gpu-" + std::to_string(w.dev) + ".log", &err);
+    w.started = now;
+  }
+}
+
+void Kubelet::stop_warm_ops() {
+  std::lock_guard<std::mutex> g(wo_mu_);
+  for (auto& w : warm_ops_) {
+    if (w.pid <= 0) continue;
+    ::kill(w.pid, SIGKILL);
+    ::waitpid(w.pid, nullptr, 0);
+    w.pid = -1;
   }
 }
 
@@ -1320,6 +1400,7 @@ void Kubelet::container_env(const PodSync& s, const Json& c, std::vector<std::st
   // a mesh-injected pod's apps listen on its private address, behind the inbound listeners
   if (rt.app_ip != rt.ip) set("KFAMD_BIND_IP", rt.app_ip);
   set("KFAMD_POD_DIR", rt.dir);
+  if (!warm_dir_.empty()) set("KFAMD_WARM_READINESS_DIR", warm_dir_);  // the gpu-readiness sidecar's warm ops
   set("KFAMD_ROOTFS", rootfs);
   set("KFAMD_TERMINATION_LOG", rt.dir + "/" + c["name"].as_string() + ".termination-log");
   Json mounts = Json::object();
@@ -1434,6 +1515,7 @@ void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
   // a recipe with a zygote forks from the pre-imported interpreter when one serves it ('python -m'
   // containers only); otherwise, or when it does not answer, a fresh interpreter as always
   Zygote zy;
+  bool warm = false;  // the process is a zygote's warm GPU child
   if (!zygote.empty()) {
     std::lock_guard<std::mutex> g(zy_mu_);
     auto it = zygotes_.find(zygote);
@@ -1441,10 +1523,14 @@ void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
   }
   if (zy.pid > 0 && argv.size() >= 3 && argv[0] == cfg_.python && argv[1] == "-m") {
     std::string zerr;
-    pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr, rt.netns ? rt.netns->path() : "");
+    // a 1-GPU container may take the zygote's warm child of its device (GPU already initialised)
+    const int warm_dev = rt.gpus.devices.size() == 1 && wants_pod_gpus(c) ? rt.gpus.devices[0] : -1;
+    pid = zygote_spawn(zy.sock, argv, envv, cwd, cr.log_path, cpus, &cr.zfd, &zerr, rt.netns ? rt.netns->path() : "",
+                       warm_dev, &warm);
     if (pid > 0) {
       std::ofstream lf(cr.log_path, std::ios::app);
-      lf << "# kflite: forked from zygote " << zy.pid << " (preloaded " << zygote << ")\n";
+      lf << "# kflite: " << (warm ? "warm child of zygote " : "forked from zygote ") << zy.pid << " (preloaded " << zygote
+         << (warm ? ", GPU " + std::to_string(warm_dev) + " initialised" : std::string()) << ")\n";
     } else if (!zerr.empty()) {
       std::ofstream lf(cr.log_path, std::ios::app);
       lf << "# kflite: " << zerr << "; starting a fresh interpreter\n";
@@ -1452,7 +1538,7 @@ void Kubelet::start_container(PodSync& s, ContainerRt& cr) {
   }
   static const auto starts = Registry::global().counter(
       "kubelet_container_starts_total", "container processes started, by how: zygote fork or fresh exec", {"mode"});
-  if (pid > 0) starts->inc({"zygote"});
+  if (pid > 0) starts->inc({warm ? "zygote-warm" : "zygote"});
   if (pid < 0) {
     pid = spawn(argv, envv, cwd, cr.log_path, &serr, cpus, rt.netns.get());
     if (pid > 0) starts->inc({"fresh"});

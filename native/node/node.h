@@ -96,6 +96,9 @@ struct KubeletConfig {
   // start a pre-imported interpreter (kubeflow_rm_amd/images/zygote.py) per image recipe that names
   // one, and fork Python containers from it instead of exec'ing a fresh interpreter
   bool pod_zygote = true;
+  // a torch zygote keeps one warm child per node GPU (HIP + device context up) that a 1-GPU
+  // container on that GPU takes over (kubeflow_rm_amd/images/zygote.py); real GPUs only
+  bool pod_warm_gpus = true;
   // per-pod network namespaces (node/netns.h): "auto" (when the node can create them and a policy
   // enforcer is wired), "on" (required: pods fail admission without one), "off" (private-address
   // convention only)
@@ -222,6 +225,19 @@ class Kubelet {
   std::mutex zy_mu_;
   void start_zygotes();
   void stop_zygotes();
+  // warm GPU readiness ops (kfamd-readiness --warm-op), one per node GPU
+  struct WarmOp {
+    int dev = 0;
+    pid_t pid = -1;
+    double started = 0, next_start = 0;
+    int failures = 0;  // warm-up failures in a row: 3 and the device gets none
+  };
+  std::vector<WarmOp> warm_ops_;
+  std::mutex wo_mu_;
+  std::string warm_dir_;  // set once in start() before any pod is admitted
+  void start_warm_ops();
+  void supervise_warm_ops();
+  void stop_warm_ops();
   void supervise_zygotes();  // heartbeat thread: restart a zygote that exited
   bool spawn_zygote(Zygote& z);
 };
@@ -246,7 +262,6 @@ struct GatewayOptions {
   // NetworkPolicy source of a connection made straight to a pod's inbound listener by a node process
   // (the culler, the API server's service proxy): the control plane's namespace
   std::string control_plane_namespace = "kubeflow";
-  bool pods_have_listeners = false;  // every pod has an inbound listener (kubelet --pod-netns)
 };
 
 class Gateway {
@@ -270,7 +285,7 @@ class Gateway {
   // evaluated with its own identity (ServiceAccount token in X-Kfamd-Peer-Token, else none). Then
   // proxied to the app (inside the pod's network namespace when it has one).
   void handle_inbound(const InboundTarget& t, HttpRequest& req, HttpResponse& resp);
-  void set_pods_have_listeners(bool v) { o_.pods_have_listeners = v; }
+  void set_pods_have_listeners(bool v) { pods_have_listeners_ = v; }
 
   struct Route {
     std::string prefix, rewrite, dest_host;
@@ -316,6 +331,7 @@ class Gateway {
   Result reconcile_mesh_policy(const Request& r, std::string* err);
   std::shared_ptr<Controller> mesh_np_;
   std::string hop_secret_;  // HMAC key of the hop proofs
+  std::atomic<bool> pods_have_listeners_{false};  // every pod has an inbound listener (kubelet --pod-netns)
   void forward(HttpRequest& req, HttpResponse& resp, const std::string& url, Headers h, int timeout_ms);
 
   std::shared_ptr<Client> c_;

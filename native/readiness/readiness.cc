@@ -38,6 +38,7 @@
 #include <netinet/in.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <execinfo.h>
 #include <signal.h>
 #include <spawn.h>
@@ -995,6 +996,210 @@ void signal_sidecar(bool ok) {
   g_report_fd = -1;
 }
 
+// ---- warm ops (--warm-op <socket>) ------------------------------------------------------------------
+// The kubelet keeps one op process per node GPU that has already brought up HIP, the device context
+// and a hardware queue (ROCR_VISIBLE_DEVICES=<d>, HIP_VISIBLE_DEVICES=0: a 1-GPU pod's view of <d>)
+// and waits on <dir>/gpu-<d>.sock. A sidecar whose pod holds exactly GPU <d> hands it the op (argv,
+// env, the verdict pipe and its stdout via SCM_RIGHTS) instead of forking a cold op: the ~90-120 ms of
+// HIP init + first queue leave the pod's cold-start path. Each warm op serves one pod, runs the
+// checks and exits (releasing its GPU state like a forked op); the kubelet starts the next. Ops that
+// need RCCL (dlopen'ed before HIP init) or the profiler still fork a cold op.
+namespace {
+bool send_with_fds(int sock, const std::string& data, const std::vector<int>& fds) {
+  msghdr mh{};
+  iovec iov{const_cast<char*>(data.data()), data.size()};
+  mh.msg_iov = &iov;
+  mh.msg_iovlen = 1;
+  std::vector<char> ctrl(CMSG_SPACE(sizeof(int) * fds.size()));
+  if (!fds.empty()) {
+    mh.msg_control = ctrl.data();
+    mh.msg_controllen = ctrl.size();
+    cmsghdr* cm = CMSG_FIRSTHDR(&mh);
+    cm->cmsg_level = SOL_SOCKET;
+    cm->cmsg_type = SCM_RIGHTS;
+    cm->cmsg_len = CMSG_LEN(sizeof(int) * fds.size());
+    std::memcpy(CMSG_DATA(cm), fds.data(), sizeof(int) * fds.size());
+  }
+  return ::sendmsg(sock, &mh, MSG_NOSIGNAL) == static_cast<ssize_t>(data.size());
+}
+
+// one JSON line (+ any passed fds) from a stream socket
+bool recv_line_with_fds(int sock, std::string& line, std::vector<int>& fds, int timeout_ms) {
+  line.clear();
+  while (line.empty() || line.back() != '\n') {
+    pollfd p{sock, POLLIN, 0};
+    if (::poll(&p, 1, timeout_ms) <= 0) return false;
+    char buf[65536];
+    char ctrl[CMSG_SPACE(sizeof(int) * 4)];
+    iovec iov{buf, sizeof buf};
+    msghdr mh{};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    mh.msg_control = ctrl;
+    mh.msg_controllen = sizeof ctrl;
+    const ssize_t n = ::recvmsg(sock, &mh, MSG_CMSG_CLOEXEC);
+    if (n <= 0) return false;
+    for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
+      if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) {
+        const size_t k = (cm->cmsg_len - CMSG_LEN(0)) / sizeof(int);
+        for (size_t i = 0; i < k; ++i) {
+          int fd;
+          std::memcpy(&fd, CMSG_DATA(cm) + i * sizeof(int), sizeof(int));
+          fds.push_back(fd);
+        }
+      }
+    line.append(buf, static_cast<size_t>(n));
+  }
+  return true;
+}
+
+// env read at HIP / ROCr init: a warm op serves only a pod whose values match its own
+bool hip_relevant(const std::string& k) {
+  for (const char* p : {"ROCR_", "HIP_", "HSA_", "GPU_", "CUDA_"})
+    if (k.rfind(p, 0) == 0) return true;
+  return false;
+}
+std::map<std::string, std::string> hip_env(const std::vector<std::string>& env) {
+  std::map<std::string, std::string> m;
+  for (const auto& kv : env) {
+    const size_t eq = kv.find('=');
+    if (eq != std::string::npos && hip_relevant(kv.substr(0, eq))) m[kv.substr(0, eq)] = kv.substr(eq + 1);
+  }
+  return m;
+}
+std::vector<std::string> own_env() {
+  std::vector<std::string> out;
+  for (char** e = environ; *e; ++e) out.push_back(*e);
+  return out;
+}
+
+// The sidecar's side: hand the op to this node's warm op for the pod's GPU. Returns the warm op's pid
+// (the verdict arrives on verdict_fd's pipe as from a forked op), or -1 to fork a cold op.
+pid_t claim_warm_op(const std::vector<char*>& op_argv, int verdict_fd) {
+  const char* dir = std::getenv("KFAMD_WARM_READINESS_DIR");
+  const char* rocr = std::getenv("ROCR_VISIBLE_DEVICES");
+  const char* prof = std::getenv("KFAMD_READINESS_PROFILE");
+  if (!dir || !*dir || !rocr || !*rocr || std::strchr(rocr, ',') || (prof && std::string(prof) == "1")) return -1;
+  for (char* a : op_argv)
+    if (a && (std::string(a) == "--rccl" || std::string(a) == "--rccl-single")) return -1;
+  const std::string path = std::string(dir) + "/gpu-" + rocr + ".sock";
+  const int s = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  if (s < 0 || path.size() >= sizeof sa.sun_path) {
+    if (s >= 0) ::close(s);
+    return -1;
+  }
+  std::memcpy(sa.sun_path, path.c_str(), path.size() + 1);
+  if (::connect(s, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
+    ::close(s);
+    return -1;
+  }
+  Json req{{"argv", Json::array()}, {"env", Json::array()}};
+  for (char* a : op_argv)
+    if (a) req["argv"].push_back(a);
+  for (const auto& kv : own_env()) req["env"].push_back(kv);
+  char cwd[4096];
+  if (::getcwd(cwd, sizeof cwd)) req["cwd"] = cwd;
+  std::string reply;
+  std::vector<int> none;
+  if (!send_with_fds(s, req.dump() + "\n", {verdict_fd, 1}) || !recv_line_with_fds(s, reply, none, 2000)) {
+    ::close(s);
+    return -1;
+  }
+  ::close(s);
+  Json r;
+  if (!Json::try_parse(reply, r) || !r["pid"].is_number()) {
+    std::fprintf(stderr, "kfamd-readiness: warm op for GPU %s declined: %s; forking one\n", rocr, reply.c_str());
+    return -1;
+  }
+  std::fprintf(stderr, "kfamd-readiness: op handed to the warm op of GPU %s (pid %lld)\n", rocr, (long long)r["pid"].as_int());
+  return static_cast<pid_t>(r["pid"].as_int());
+}
+}  // namespace
+
+int run_warm_op(const char* sock_path) {
+  ::signal(SIGPIPE, SIG_IGN);
+  const auto t0 = std::chrono::steady_clock::now();
+  int ndev = 0;
+  hipStream_t st = nullptr;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev != 1 || hipSetDevice(0) != hipSuccess || hipFree(nullptr) != hipSuccess ||
+      hipStreamCreate(&st) != hipSuccess) {
+    std::fprintf(stderr, "kfamd-readiness --warm-op: no single GPU to warm up (%d visible)\n", ndev);
+    return 3;
+  }
+  (void)hipStreamSynchronize(st);  // the device context and a hardware queue exist; the stream keeps the queue
+  const double warm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const std::string path = sock_path;
+  const int ls = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  if (ls < 0 || path.size() >= sizeof sa.sun_path) return 3;
+  std::memcpy(sa.sun_path, path.c_str(), path.size() + 1);
+  const std::string tmp = path + ".tmp";
+  sockaddr_un ta = sa;
+  std::memcpy(ta.sun_path, tmp.c_str(), std::min(tmp.size() + 1, sizeof ta.sun_path));
+  ::unlink(tmp.c_str());
+  if (::bind(ls, reinterpret_cast<sockaddr*>(&ta), sizeof ta) != 0 || ::chmod(tmp.c_str(), 0600) != 0 || ::listen(ls, 4) != 0 ||
+      ::rename(tmp.c_str(), path.c_str()) != 0) {
+    std::fprintf(stderr, "kfamd-readiness --warm-op: cannot listen on %s: %s\n", path.c_str(), std::strerror(errno));
+    return 3;
+  }
+  std::fprintf(stderr, "kfamd-readiness --warm-op: GPU %s warm in %.1f ms, serving %s\n",
+               std::getenv("ROCR_VISIBLE_DEVICES") ? std::getenv("ROCR_VISIBLE_DEVICES") : "?", warm_ms, path.c_str());
+  const auto mine = hip_env(own_env());
+  for (;;) {
+    const int cs = ::accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+    if (cs < 0) {
+      if (errno == EINTR) continue;
+      return 3;
+    }
+    std::string line;
+    std::vector<int> fds;
+    Json req;
+    if (!recv_line_with_fds(cs, line, fds, 2000) || !Json::try_parse(line, req) || fds.size() != 2) {
+      for (int fd : fds) ::close(fd);
+      ::close(cs);
+      continue;
+    }
+    std::vector<std::string> env;
+    for (const auto& e : req["env"].as_array()) env.push_back(e.as_string());
+    if (hip_env(env) != mine) {  // another GPU view: this warm op is not its to use
+      send_with_fds(cs, "{\"error\":\"GPU environment differs\"}\n", {});
+      for (int fd : fds) ::close(fd);
+      ::close(cs);
+      continue;
+    }
+    // claimed: become the pod's op (its env, output, cwd, verdict pipe); the socket goes away
+    ::close(ls);
+    ::unlink(path.c_str());
+    ::clearenv();
+    for (const auto& kv : env) {
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos) ::setenv(kv.substr(0, eq).c_str(), kv.substr(eq + 1).c_str(), 1);
+    }
+    std::fflush(nullptr);
+    ::dup2(fds[1], 1);
+    ::dup2(fds[1], 2);
+    ::close(fds[1]);
+    if (req["cwd"].is_string()) (void)!::chdir(req["cwd"].as_string().c_str());
+    g_report_fd = fds[0];
+    send_with_fds(cs, Json{{"pid", (long long)::getpid()}}.dump() + "\n", {});
+    ::close(cs);
+    std::vector<std::string> args;
+    for (const auto& a : req["argv"].as_array()) args.push_back(a.as_string());
+    std::vector<char*> av;
+    for (auto& a : args) av.push_back(a.data());
+    av.push_back(nullptr);
+    g_fast_exit = true;
+    g_result["warm_op"] = Json{{"warm_ms", warm_ms}};
+    const int rc = readiness_main(static_cast<int>(args.size()), av.data());
+    signal_sidecar(rc == 0);
+    std::fflush(nullptr);
+    _exit(rc);
+  }
+}
+
 int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
   int port = 8689;
   std::vector<char*> child_argv;
@@ -1010,7 +1215,10 @@ int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
   child_argv.push_back(nullptr);
   int fds[2];
   if (::pipe(fds) != 0) return 2;
-  const pid_t pid = ::fork();
+  // the node's warm op for this pod's GPU, else a cold op forked here (HIP lives only in the op)
+  pid_t pid = claim_warm_op(child_argv, fds[1]);
+  const bool own_child = pid < 0;
+  if (own_child) pid = ::fork();
   if (pid < 0) return 2;
   if (pid == 0) {  // the op: HIP lives only in this process
     ::close(fds[0]);
@@ -1045,6 +1253,7 @@ int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
       verdict = ::read(fds[0], &c, 1) == 1 && c == '1' ? 1 : 0;
       ::close(fds[0]);
     }
+    if (!own_child && !child_reaped && verdict >= 0) child_reaped = true;  // a warm op: the verdict is all we get
     if (!child_reaped) {
       int st = 0;
       if (::waitpid(pid, &st, verdict == 0 ? 0 : WNOHANG) == pid) {
@@ -1075,6 +1284,7 @@ int run_sidecar(int argc, char** argv, int (*op)(int, char**)) {
 
 int main(int argc, char** argv) {
   g_t_main_ms = realtime_ms();
+  if (argc == 3 && std::string(argv[1]) == "--warm-op") return run_warm_op(argv[2]);
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--sidecar")
       return run_sidecar(argc, argv, [](int ac, char** av) -> int {
@@ -1285,6 +1495,7 @@ int readiness_main(int argc, char** argv) {
       brief["gemm0_stages_ms"] = g_result["gemm"][0]["stages"];
     if (g_result.has("layernorm") && g_result["layernorm"].size()) brief["layernorm_GBps"] = g_result["layernorm"][0]["GBps"];
     if (g_result.has("devices_wall_ms")) brief["devices_wall_ms"] = g_result["devices_wall_ms"];
+    if (g_result.has("warm_op")) brief["warm_op_ms"] = g_result["warm_op"]["warm_ms"];  // HIP came up before the pod
     if (g_result.has("allreduce_oneshot") && g_result["allreduce_oneshot"].has("sweep")) {
       const Json& os = g_result["allreduce_oneshot"];
       const Json& sw = os["sweep"];
@@ -1293,8 +1504,18 @@ int readiness_main(int argc, char** argv) {
                               {"us_256KiB", sw.size() ? sw[sw.size() - 1]["us"] : Json()}};
     }
     if (g_result.has("allreduce")) {
-      const Json& sw = g_result["allreduce"]["sweep"];
+      // the in-pod RCCL smoke (BASELINE config 4): communicator, correctness and the sweep, compact
+      const Json& ar = g_result["allreduce"];
+      const Json& sw = ar["sweep"];
       if (sw.size()) brief["allreduce_busbw_GBps_max"] = sw[sw.size() - 1]["busbw_GBps"];
+      auto r2 = [](const Json& v) { return Json(std::round(v.as_double() * 100.0) / 100.0); };
+      Json pts = Json::array();
+      for (const auto& p : sw.as_array())
+        pts.push_back(Json{{"bytes", p["bytes"]}, {"us", r2(p["us"])}, {"algbw_GBps", r2(p["algbw_GBps"])},
+                           {"busbw_GBps", r2(p["busbw_GBps"])}});
+      brief["allreduce"] = Json{{"devices", ar["devices"]}, {"comm_init_ms", r2(ar["comm_init_ms"])}, {"correct", ar["correct"]},
+                                {"sweep", pts}};
+      if (g_result.has("rccl_load_ms")) brief["rccl_load_ms"] = r2(g_result["rccl_load_ms"]);
     }
     if (FILE* f = std::fopen(tl, "w")) {
       std::fputs(brief.dump().c_str(), f);

@@ -316,3 +316,63 @@ def test_cold_start_bench_zygote_path_on_cpu():
                            settle_s=0.0, timeout=60)
     assert len(r["runs"]) == 2 and r["zygote"] is True
     assert r["p50_s"] < 30 and "create_to_pod_ready_s" in r["phases_p50_s"]
+
+
+@pytest.mark.gpu
+def test_gpu_warm_child_takes_the_one_gpu_notebook():
+    """the product's default cold start. The torch zygote keeps a warm child per GPU
+    (HIP + torch's device context + the first GEMM's code object already up); each 1-GPU torch-ready
+    notebook takes the warm child of its GPU, so HIP bring-up is off the cold-start path, and the
+    server's own warmup (GEMM + fp32 spot check) still runs in the pod and passes."""
+    from kubeflow_rm_amd.bench_coldstart import measure_cold_start
+    r = measure_cold_start(runs=3, gpus_per_notebook=1, server="torch-ready", zygote=True, namespace="zy-warm",
+                           settle_s=1.0, timeout=60)
+    assert not r["failures"], r["failures"]
+    assert r["warm_children"] >= 2, [x.get("warm_child") for x in r["runs"]]
+    for run in r["runs"]:
+        w = run["server_warmup"] or {}
+        assert w.get("ok") is True, run
+    warm = [x for x in r["runs"] if x.get("warm_child")]
+    assert min(x["server_warmup"]["total_ms"] for x in warm) < 80, [x["server_warmup"] for x in warm]
+    # the gpu-readiness sidecar's op ran in the node's warm op of the GPU (kfamd-readiness --warm-op)
+    assert sum(x["readiness_stages"].get("warm_op", 0) for x in r["runs"]) >= 2, [x["readiness_stages"] for x in r["runs"]]
+
+
+def test_warm_children_fail_soft_without_a_gpu(tmp_path):
+    """On a host without a GPU a zygote asked for warm children reports each failure (at most 3 in a
+    row per device) and keeps serving plain forks."""
+    import socket
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    sock = str(tmp_path / "z.sock")
+    log = tmp_path / "z.log"
+    env = dict(os.environ, PYTHONPATH=str(root), HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    with open(log, "w") as lf:
+        z = subprocess.Popen([sys.executable, "-m", "kubeflow_rm_amd.images.zygote", "--socket", sock, "--preload", "torch",
+                              "--warm-devices", "0"], env=env, stdout=lf, stderr=subprocess.STDOUT)
+    try:
+        deadline = time.time() + 120
+        while not os.path.exists(sock):
+            assert z.poll() is None and time.time() < deadline, log.read_text()
+            time.sleep(0.05)
+        if "torch" in sys.modules and __import__("torch").cuda.is_available():
+            pytest.skip("a GPU is visible: warm children succeed here")
+        while log.read_text().count("for device 0 failed") < 3:
+            assert z.poll() is None and time.time() < deadline, log.read_text()
+            time.sleep(0.1)
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(sock)
+        out = tmp_path / "c.log"
+        s.sendall((json.dumps({"argv": ["-m", "tests.zygote_probe_mod"], "cwd": str(tmp_path), "log": str(out),
+                               "env": [f"PYTHONPATH={root}", "PROBE_EXIT=0"], "warm_device": 0}) + "\n").encode())
+        f = s.makefile("r")
+        rep = json.loads(f.readline())
+        assert "pid" in rep and not rep.get("warm")
+        assert json.loads(f.readline()) == {"exit": 0, "signal": 0}
+        s.close()
+        time.sleep(1.5)  # no fourth warm attempt
+        assert log.read_text().count("for device 0 failed") == 3
+    finally:
+        z.terminate()
+        z.wait(timeout=10)
