@@ -120,7 +120,9 @@ class Block(torch.nn.Module):
     def attention(self, x, residual=None):
         B, T, _ = x.shape
         h, hd = self.local_heads, self.cfg.head_dim
-        if x.is_cuda and ops.native_enabled() and ops.attention_supported(x, hd) and tpl._world(self.tp_group) == 1:
+        # the fused single-rank path whenever the TP layers would issue no collective; a forced-distributed
+        # run at world size 1 (KFAMD_FORCE_DIST) takes the TP layers and their RCCL all-reduces
+        if x.is_cuda and ops.native_enabled() and ops.attention_supported(x, hd) and not tpl._collective(self.tp_group):
             # one autograd node on the HIP path (ops.attn_block): its backward runs the QKV and
             # output-projection weight gradients as one GEMM launch
             return ops.attn_block(x, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias, h, hd,
@@ -136,7 +138,7 @@ class Block(torch.nn.Module):
     def mlp(self, h, residual):
         # without TP, fc1 + fc2 are one autograd node on the HIP path (ops.mlp): fc2's dgrad applies
         # fc1's gelu backward in its GEMM epilogue
-        if h.is_cuda and ops.native_enabled() and tpl._world(self.tp_group) == 1:
+        if h.is_cuda and ops.native_enabled() and not tpl._collective(self.tp_group):
             return ops.mlp(h, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, act=self.fc1.act,
                            residual=residual)
         return self.fc2(self.fc1(h), residual=residual)

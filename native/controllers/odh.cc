@@ -1,6 +1,11 @@
 // odh.cc — N8 OpenshiftNotebookReconciler + N9 ODH NotebookWebhook (see odh.h).
 #include "controllers/odh.h"
 
+#include <openssl/bio.h>
+#include <openssl/err.h>
+#include <openssl/pem.h>
+#include <openssl/x509.h>
+
 #include <algorithm>
 #include <cctype>
 
@@ -230,43 +235,20 @@ AdmissionFn make_odh_notebook_webhook(std::shared_ptr<Client> c, OdhOptions o) {
 }
 
 // ---- PEM / DER validation (pem.Decode + x509.ParseCertificate structure) -------------------------
-namespace {
-bool der_length(const std::string& d, size_t& i, size_t& len) {
-  if (i >= d.size()) return false;
-  unsigned char b = static_cast<unsigned char>(d[i++]);
-  if (b < 0x80) {
-    len = b;
-    return true;
-  }
-  int n = b & 0x7F;
-  if (n == 0 || n > 4 || i + static_cast<size_t>(n) > d.size()) return false;
-  len = 0;
-  for (int k = 0; k < n; ++k) len = (len << 8) | static_cast<unsigned char>(d[i++]);
-  return true;
-}
-}  // namespace
-
+// notebook_controller.go:301-307: pem.Decode of the first block, which must be a CERTIFICATE, then
+// x509.ParseCertificate of its DER — here OpenSSL's PEM reader + X.509 decoder (the whole
+// tbsCertificate is parsed, not only the outer framing)
 bool pem_certificate_valid(const std::string& pem) {
-  const std::string begin = "-----BEGIN CERTIFICATE-----", end = "-----END CERTIFICATE-----";
-  size_t b = pem.find(begin);
-  if (b == std::string::npos) return false;
-  size_t e = pem.find(end, b);
-  if (e == std::string::npos) return false;
-  std::string body;
-  for (size_t k = b + begin.size(); k < e; ++k)
-    if (!std::isspace(static_cast<unsigned char>(pem[k]))) body += pem[k];
-  const std::string der = base64_decode(body);
-  // Certificate ::= SEQUENCE { tbsCertificate SEQUENCE, signatureAlgorithm SEQUENCE, signature BIT STRING }
-  size_t i = 0, len = 0;
-  if (der.size() < 16 || static_cast<unsigned char>(der[i++]) != 0x30 || !der_length(der, i, len) || i + len != der.size()) return false;
-  size_t tbs_len = 0;
-  if (static_cast<unsigned char>(der[i++]) != 0x30 || !der_length(der, i, tbs_len) || i + tbs_len > der.size()) return false;
-  i += tbs_len;
-  size_t alg_len = 0;
-  if (i >= der.size() || static_cast<unsigned char>(der[i++]) != 0x30 || !der_length(der, i, alg_len)) return false;
-  i += alg_len;
-  size_t sig_len = 0;
-  return i < der.size() && static_cast<unsigned char>(der[i++]) == 0x03 && der_length(der, i, sig_len) && i + sig_len == der.size();
+  const size_t b = pem.find("-----BEGIN ");
+  if (b == std::string::npos || pem.compare(b, 27, "-----BEGIN CERTIFICATE-----") != 0) return false;
+  BIO* bio = BIO_new_mem_buf(pem.data() + b, static_cast<int>(pem.size() - b));
+  if (!bio) return false;
+  X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+  BIO_free(bio);
+  ERR_clear_error();
+  if (!x) return false;
+  X509_free(x);
+  return true;
 }
 
 // ---- generated objects ----------------------------------------------------------------------------

@@ -36,6 +36,31 @@ def test_pem_validation(native):
     assert native.call("pem_certificate_valid", pem="garbage") is False
 
 
+def test_pem_validation_parses_the_whole_certificate(native):
+    """a well-framed DER (SEQUENCE { SEQUENCE, SEQUENCE, BIT STRING }) with garbage
+    inside tbsCertificate is rejected, as x509.ParseCertificate rejects it
+    (odh-notebook-controller/controllers/notebook_controller.go:301-307); so is a first block of
+    another type."""
+    import base64
+    import textwrap
+
+    def der(tag, body):
+        n = len(body)
+        ln = bytes([n]) if n < 128 else bytes([0x81, n]) if n < 256 else bytes([0x82, n >> 8, n & 255])
+        return bytes([tag]) + ln + body
+    tbs = der(0x30, b"\x02\x01\x05" + b"\xde\xad\xbe\xef" * 20)  # not a TBSCertificate
+    alg = der(0x30, der(0x06, b"\x2a\x86\x48\x86\xf7\x0d\x01\x01\x0b") + b"\x05\x00")
+    sig = der(0x03, b"\x00" + b"\x11" * 64)
+    cert = der(0x30, tbs + alg + sig)
+    body = "\n".join(textwrap.wrap(base64.b64encode(cert).decode(), 64))
+    framed = f"-----BEGIN CERTIFICATE-----\n{body}\n-----END CERTIFICATE-----\n"
+    assert native.call("pem_certificate_valid", pem=framed) is False
+    good = (FIX / "test-ca.crt").read_text()
+    key_first = "-----BEGIN PRIVATE KEY-----\nAAAA\n-----END PRIVATE KEY-----\n" + good
+    assert native.call("pem_certificate_valid", pem=key_first) is False
+    assert native.call("pem_certificate_valid", pem=good + framed) is True  # the first block decides
+
+
 def _nb(name="nb", ns="ns", annotations=None, containers=None):
     return {"apiVersion": NB, "kind": "Notebook",
             "metadata": {"name": name, "namespace": ns, "annotations": annotations or {}},
