@@ -498,6 +498,294 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
 }
 
 // ------------------------------------------------------------------------------------------------
+// forward, 8 waves x 32 query rows = 256 rows per workgroup, one workgroup per CU (KFATT_FWD_PP,
+// profiles/r6d_attn_pp): two waves per SIMD share its matrix pipe, one K / V image per CU per tile
+// instead of two (half the LDS stores and global loads of attn_fwd's two 128-row workgroups), and the
+// hardware interleaves one wave's softmax VALU with the other's MFMAs. One barrier per tile.
+// The running max is a reference that moves only when a row's scores pass it by more than
+// KFATT_FWD_THR (log2 units; cdna_hip_programming.md T13): probabilities stay <= 2^THR (exact in the
+// fp32 l and O, bf16 keeps its relative precision), and the 64-register O rescale runs only on
+// those tiles instead of on nearly every early one (the tests force both branches: rule 26).
+// K / V are loaded two tiles ahead (KFATT_FWD_PF2: a four-slot ring, two staging register sets;
+// without it one tile ahead through a three-slot ring).
+// Measured and not taken (tools/attn_ab.py, profiles/r6d_attn_pp): staggering waves 4-7 half a tile
+// behind waves 0-3 (MI355X_MICROARCH.md "Two waves per SIMD" item 9): +7 % time; the QK^T of tile
+// j + 1 issued beside softmax(j), Q moved to LDS to pay for the second S tile (T15): +6 %.
+// ------------------------------------------------------------------------------------------------
+#ifndef KFATT_FWD_PP
+#define KFATT_FWD_PP 1  // forward by attn_fwd_pp (profiles/r6d_attn_pp)
+#endif
+#ifndef KFATT_FWD_THR
+#define KFATT_FWD_THR 8.0f
+#endif
+#ifndef KFATT_FWD_FENCE
+#define KFATT_FWD_FENCE 1  // scheduling fences between the QK^T / softmax / PV phases of attn_fwd_pp
+#endif
+#define FENCE() \
+  do {                                                   \
+    if (KFATT_FWD_FENCE) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+#ifndef KFATT_FWD_PF2
+#define KFATT_FWD_PF2 1  // K / V loads two tiles ahead (four-tile ring)
+#endif
+#ifndef KFATT_FWD_ABL
+#define KFATT_FWD_ABL 0  // timing ablations of attn_fwd_pp (tools/attn_ab.py; wrong results)
+#endif
+
+template <int D, bool CAUSAL, bool PAIR>
+__global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                      const __bf16* __restrict__ v, __bf16* __restrict__ o,
+                                                      float* __restrict__ lse, AttnShape a) {
+  constexpr int KS = D / 16, ND = D / 32, CH = D / 8;
+  constexpr int NT = 512, FQW = 256;
+  constexpr int NCH = FK * CH / NT;  // 16-B chunks per thread per K (and per V) tile
+  constexpr int TILE = FK * D * 2;
+  // K ring [NS][TILE] then V ring [NS][TILE]; the V ring's base VBASE rides in the V read offsets,
+  // so every slot / row offset of a read fits the 16-bit ds_read immediate
+  constexpr int NS = KFATT_FWD_PF2 ? 4 : 3, VBASE = NS * TILE;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NS * TILE];
+
+  const int T = a.T;
+  const int nq = (T + FQW - 1) / FQW, nta = (T + FK - 1) / FK;
+  const BlockId bo = block_order(blockIdx.x, PAIR ? nq / 2 : nq, a.H * a.B, 32);  // one workgroup per CU
+  const int bh = bo.bh, h = bh % a.H, b = bh / a.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the wave index as a uniform (scalar) value
+
+  const __bf16* qb = q + base_off(a, TQ, b, h);
+  const __bf16* kb = k + base_off(a, TK, b, h);
+  const __bf16* vb = v + base_off(a, TV, b, h);
+  const long long qt = a.s[TQ][2], kt = a.s[TK][2], vt = a.s[TV][2];
+  const auto rk = slice_rsrc(kb, 2LL * T * kt), rv = slice_rsrc(vb, 2LL * T * vt);
+  const float c = a.scale * kLog2e;
+  constexpr float THR = KFATT_FWD_THR;
+
+  // per-lane LDS offsets (as attn_fwd KFATT_FWD_OFFS): tile row parts ride in the ds_read immediates
+  int koff[KS], voff0[ND], voff1[ND];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) koff[kk] = img_off<D>(r, 2 * kk + hh);
+  {
+    const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+    const int r0 = 4 * hh + qq;
+#pragma unroll
+    for (int n = 0; n < ND; ++n) {
+      const int col = 32 * n + 16 * (g & 1) + 4 * pp;
+      voff0[n] = VBASE + img_off<D>(r0, col >> 3) + 8 * (pp & 1);
+      voff1[n] = VBASE + img_off<D>(r0 + 8, col >> 3) + 8 * (pp & 1);
+    }
+  }
+  u32x4 kreg[NCH], vreg[NCH];
+  auto stage_load = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + NT * i, row = cc / CH, ch = cc % CH;
+      kreg[i] = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * tile * FK * (int)kt);
+      vreg[i] = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * tile * FK * (int)vt);
+    }
+  };
+  auto stage_write = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + NT * i;
+      const int off = img_off<D>(cc / CH, cc % CH);
+      *reinterpret_cast<u32x4*>(smem + slot * TILE + off) = kreg[i];
+      *reinterpret_cast<u32x4*>(smem + VBASE + slot * TILE + off) = vreg[i];
+    }
+  };
+  auto qk = [&](const char* kimg, const bf16x8 (&qf)[KS], f32x16 (&s)[2]) __attribute__((always_inline)) {
+    s[0] = (f32x16){};
+    s[1] = (f32x16){};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) s[t] = mfma32(lds_row(kimg + 32 * t * D * 2, koff[kk]), qf[kk], s[t]);
+  };
+  auto pv = [&](const char* vimg, const uint32_t (&pf)[2][2][4], f32x16 (&oa)[ND]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 vf = join(tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff0[n]),
+                                 tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff1[n]));
+          const u32x4 pw = {pf[t][s2][0], pf[t][s2][1], pf[t][s2][2], pf[t][s2][3]};
+          oa[n] = mfma32(vf, __builtin_bit_cast(bf16x8, pw), oa[n]);
+        }
+  };
+  // causal / tail mask of the wave's S^T tile (keys from k0, rows from qw); a uniform branch
+  auto mask = [&](f32x16 (&s)[2], int k0, int qw) __attribute__((always_inline)) {
+    if ((CAUSAL && k0 + FK - 1 > qw) || k0 + FK > T) {
+      const int lim = (CAUSAL ? min(qw + r, T - 1) : T - 1) - k0 - 4 * hh;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if (32 * t + (e & 3) + 8 * (e >> 2) > lim) s[t][e] = -INFINITY;
+    }
+  };
+  // online softmax of one S^T tile into P (bf16 pairs: the PV B operand) and l; O is rescaled when
+  // some lane's reference max moved
+  auto softmax = [&](const f32x16 (&s)[2], float& m, float& l, uint32_t (&pf)[2][2][4], f32x16 (&oa)[ND])
+                     __attribute__((always_inline)) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[t][e]);
+    mx = kfw::max_halves(mx);
+    const bool move = (mx - m) * c > THR;  // m = -inf on the first tile: moves
+    const float mn = move ? mx : m;
+    const float alpha = move ? fast_exp2((m - mn) * c) : 1.f;
+    m = mn;
+    const float mc = mn * c;
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const float p0 = fast_exp2(fmaf(s[t][e], c, -mc));
+        const float p1 = fast_exp2(fmaf(s[t][e + 1], c, -mc));
+        rs += p0 + p1;
+        pf[t][e >> 3][(e & 7) >> 1] = pack2(p0, p1);
+      }
+    l = l * alpha + rs;
+    if (__builtin_amdgcn_ballot_w64(move) != 0) {
+#pragma unroll
+      for (int n = 0; n < ND; ++n) oa[n] *= alpha;
+    }
+  };
+
+#pragma unroll 1
+  for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
+    if (PAIR && pass) __syncthreads();  // the first block's last reads are done before the LDS is refilled
+    const int qblk = pass ? bo.rank : nq - 1 - bo.rank;  // the heaviest first
+    const int q0 = qblk * FQW, qw = q0 + 32 * wu, qrow = qw + r;
+    const int ntiles = CAUSAL ? min(nta, (q0 + FQW) / FK) : nta;
+    const int jl = CAUSAL ? min(ntiles - 1, (qw + 31) / FK) : ntiles - 1;  // this wave's last tile
+
+    bf16x8 qf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      u32x4 x = {0u, 0u, 0u, 0u};
+      if (qrow < T) x = gload16(qb + qrow * qt + kk * 16 + 8 * hh);
+      qf[kk] = __builtin_bit_cast(bf16x8, x);
+    }
+    f32x16 oacc[ND], S[2][2];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) oacc[n] = (f32x16){};
+    float m = -INFINITY, l = 0.f;
+    uint32_t pf[2][2][4];
+    // tile j sits in ring slot j % 3, compile-time in the unrolled loop (pv reads through
+    // smem + slot * TILE, the V ring base riding in voff)
+    if constexpr (KFATT_FWD_PF2) {
+      // K / V two tiles ahead: tile j + 2's loads are issued at tile j into the register set tile j
+      // used (written at tile j - 1), and tile j + 1's set is written at the end of tile j into the
+      // slot of tile j - 3 (a four-tile ring: slot and set compile-time in the 4x unrolled loop)
+      u32x4 kr2[NCH], vr2[NCH];
+      auto ld = [&](int tile, u32x4 (&kr)[NCH], u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          const int cc = tid + NT * i, row = cc / CH, ch = cc % CH;
+          kr[i] = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * tile * FK * (int)kt);
+          vr[i] = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * tile * FK * (int)vt);
+        }
+      };
+      auto st = [&](int slot, const u32x4 (&kr)[NCH], const u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          const int cc = tid + NT * i;
+          const int off = img_off<D>(cc / CH, cc % CH);
+          *reinterpret_cast<u32x4*>(smem + slot * TILE + off) = kr[i];
+          *reinterpret_cast<u32x4*>(smem + VBASE + slot * TILE + off) = vr[i];
+        }
+      };
+      ld(0, kreg, vreg);
+      st(0, kreg, vreg);
+      if (1 < ntiles) ld(1, kr2, vr2);
+      __syncthreads();
+      auto tile = [&](int j, auto SLC) __attribute__((always_inline)) {
+        constexpr int SL = decltype(SLC)::value;  // j % 4; register set j & 1
+        auto& kc = (SL & 1) ? kr2 : kreg;
+        auto& vc = (SL & 1) ? vr2 : vreg;
+        auto& kn = (SL & 1) ? kreg : kr2;
+        auto& vn = (SL & 1) ? vreg : vr2;
+        if ((KFATT_FWD_ABL & 1) == 0 && j + 2 < ntiles) ld(j + 2, kc, vc);
+        if (j <= jl) {
+          qk(smem + SL * TILE, qf, S[0]);
+          mask(S[0], j * FK, qw);
+          FENCE();
+          softmax(S[0], m, l, pf, oacc);
+          FENCE();
+          pv(smem + SL * TILE, pf, oacc);
+        }
+        if ((KFATT_FWD_ABL & 1) == 0 && j + 1 < ntiles) st((SL + 1) % 4, kn, vn);
+        if ((KFATT_FWD_ABL & 2) == 0) __syncthreads();
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      int j = 0;
+#pragma unroll 1
+      for (; j + 3 < ntiles; j += 4) {
+        tile(j, I0{});
+        tile(j + 1, I1{});
+        tile(j + 2, I2{});
+        tile(j + 3, I3{});
+      }
+      if (j < ntiles) tile(j, I0{});
+      if (j + 1 < ntiles) tile(j + 1, I1{});
+      if (j + 2 < ntiles) tile(j + 2, I2{});
+    } else {
+      stage_load(0);
+      stage_write(0);
+      __syncthreads();
+      auto tile = [&](int j, auto SLC) __attribute__((always_inline)) {
+        constexpr int SL = decltype(SLC)::value;
+        const bool more = (KFATT_FWD_ABL & 1) == 0 && j + 1 < ntiles;  // ABL 1: no staging (timing only)
+        if (more) stage_load(j + 1);
+        if (j <= jl) {
+          qk(smem + SL * TILE, qf, S[0]);
+          mask(S[0], j * FK, qw);
+          FENCE();
+          softmax(S[0], m, l, pf, oacc);
+          FENCE();
+          pv(smem + SL * TILE, pf, oacc);
+        }
+        if (more) stage_write((SL + 1) % 3);
+        if ((KFATT_FWD_ABL & 2) == 0) __syncthreads();  // ABL 2: no barrier (timing only)
+      };
+      int j = 0;
+#pragma unroll 1
+      for (; j + 2 < ntiles; j += 3) {
+        tile(j, std::integral_constant<int, 0>{});
+        tile(j + 1, std::integral_constant<int, 1>{});
+        tile(j + 2, std::integral_constant<int, 2>{});
+      }
+      if (j < ntiles) tile(j, std::integral_constant<int, 0>{});
+      if (j + 1 < ntiles) tile(j + 1, std::integral_constant<int, 1>{});
+    }
+
+    // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
+    const float lt = kfw::sum_halves(l);
+    const float inv = 1.f / lt;
+    if (qrow < T) {
+      __bf16* ob = o + base_off(a, TO, b, h) + qrow * a.s[TO][2];
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const u32x2 v2 = {pack2(oacc[n][4 * g] * inv, oacc[n][4 * g + 1] * inv),
+                            pack2(oacc[n][4 * g + 2] * inv, oacc[n][4 * g + 3] * inv)};
+          *reinterpret_cast<u32x2*>(ob + 32 * n + 8 * g + 4 * hh) = v2;
+        }
+      if (hh == 0) lse[((long long)b * a.H + h) * T + qrow] = m * a.scale + logf(lt);
+    }
+  }  // pass
+}
+
+// ------------------------------------------------------------------------------------------------
 // backward prologue, per row [b][h][t]: nd = -sum_d dO * O and nl = -lse / scale (fp32), the two
 // row constants of the backward in the form its products start from: S - lse / scale and dP - delta
 // are the MFMA accumulators initialised with nl and nd (no negate / scale per element and tile)
@@ -1319,6 +1607,17 @@ bool fill_shape(AttnShape& s, int B, int H, int T, int D, float scale, const lon
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// compute units of the current device, queried once (256 on MI355X)
+int device_cus() {
+  static const int n = [] {
+    int cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
 // a (b, h) slice of T rows read through a buffer descriptor (KFATT_BUF): 32-bit byte offsets
 bool slice_ok(int T, long long row_stride, int elem_bytes) {
   return row_stride > 0 && (long long)T * row_stride * elem_bytes < (1ll << 31);
@@ -1342,7 +1641,21 @@ extern "C" int kfamd_attn_fwd_bf16(const void* q, const void* k, const void* v, 
                        static_cast<float*>(lse), s);
   };
   const int nq = (T + FQ - 1) / FQ;
-  if constexpr (KFATT_FWD_NW == 8) {  // 8 waves x 32 rows per workgroup (A/B knob)
+  const int nq4 = (T + 255) / 256;
+  const bool pair4 = causal && nq4 % 2 == 0;
+  const long long g4 = (long long)(pair4 ? nq4 / 2 : nq4) * H * B;
+  // attn_fwd_pp where its grid fills the chip (one workgroup per CU); attn_fwd otherwise and at
+  // D = 64, where the two-workgroups-per-CU kernel measured faster (profiles/r6d_attn_pp)
+  if (KFATT_FWD_PP && D == 128 && g4 >= device_cus()) {
+    const bool pair = pair4;
+    auto go4 = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)g4), dim3(512), 0, st, static_cast<const __bf16*>(q),
+                         static_cast<const __bf16*>(k), static_cast<const __bf16*>(v), static_cast<__bf16*>(o),
+                         static_cast<float*>(lse), s);
+    };
+    pair ? go4(attn_fwd_pp<128, true, true>) : causal ? go4(attn_fwd_pp<128, true, false>)
+                                                   : go4(attn_fwd_pp<128, false, false>);
+  } else if constexpr (KFATT_FWD_NW == 8) {  // 8 waves x 32 rows per workgroup (A/B knob)
     const int nq8 = (T + 255) / 256;
     const bool pair = KFATT_FWD_PAIR && causal && nq8 % 2 == 0;
     const long long g8 = (long long)(pair ? nq8 / 2 : nq8) * H * B;

@@ -51,6 +51,10 @@ SHAPES = [
     (1, 2, 256, 64, False),
     (1, 2, 40, 128, True),   # shorter than one key tile and than one 128-row block
     (2, 1, 65, 64, False),   # one row / key past a tile
+    # grids of >= 256 workgroups of 256 query rows: the one-workgroup-per-CU forward (attn_fwd_pp)
+    (4, 32, 512, 128, True),  # paired query blocks
+    (2, 64, 700, 128, True),  # an odd number of 256-row blocks (unpaired), partial tiles
+    (4, 64, 1000, 128, False),
 ]
 
 
@@ -82,12 +86,13 @@ def test_flash_backward_matches_fp32(B, H, T, D, causal):
         assert _rel(got, want) < 2e-2, (name, _rel(got, want))
 
 
-def test_forward_lse_and_rescale_branch_forced():
+@pytest.mark.parametrize("H", [2, 256])  # 256 heads: the attn_fwd_pp grid
+def test_forward_lse_and_rescale_branch_forced(H):
     """Keys whose scores jump at a later tile force the online-softmax rescale of O and l (rule 26):
     one query row's max is set by a key far into the sequence, another row's max moves at every tile."""
     from kubeflow_rm_amd import ops
     from kubeflow_rm_amd.ops import attention as A
-    B, H, T, D = 1, 2, 1000, 128
+    B, T, D = 1, 1000, 128
     q, k, v = _inputs(B, H, T, D, seed=3)
     q[:, :, 900] = 0.5
     k[:, :, 700] = 4.0          # query 900 meets a far larger score at key 700 (tile 10)

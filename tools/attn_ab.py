@@ -40,7 +40,14 @@ def _variants():
         "nolpt": [*prod, "-DKFATT_LPT=0"],  # head-major block order (no longest-first across heads)
         "nofpair": [*prod, "-DKFATT_FWD_PAIR=0"],  # causal forward: one query block per workgroup
         "dqpair": [*prod, "-DKFATT_DQ_PAIR=1"],  # dQ kernel: heavy + light query block per workgroup
-        "fwd8": [*prod, "-DKFATT_FWD_NW=8"],  # forward: one 8-wave workgroup (256 query rows) per CU
+        "fwd8": [*prod, "-DKFATT_FWD_PP=0", "-DKFATT_FWD_NW=8"],  # forward: the unstaggered 8-wave attn_fwd
+        "fwdold": [*prod, "-DKFATT_FWD_PP=0"],  # forward: attn_fwd (4 waves, two workgroups per CU)
+        "fabl1": [*prod, "-DKFATT_FWD_ABL=1"],  # timing only: attn_fwd_pp without K / V staging
+        "fabl2": [*prod, "-DKFATT_FWD_ABL=2"],  # timing only: attn_fwd_pp without the per-tile barrier
+        "fabl3": [*prod, "-DKFATT_FWD_ABL=3"],  # timing only: neither
+        "pf1": [*prod, "-DKFATT_FWD_PF2=0"],  # attn_fwd_pp with K / V loads one tile ahead
+        "nofence": [*prod, "-DKFATT_FWD_FENCE=0"],  # attn_fwd_pp without the phase fences
+        "nopp": [*prod, "-DKFATT_FWD_PP=0"],  # forward by attn_fwd everywhere
     }
 
 
