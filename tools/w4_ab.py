@@ -46,6 +46,8 @@ VARIANTS = {
     "gm8": ["-DKFW4_GROUP_M=8"],
     "gm16": ["-DKFW4_GROUP_M=16"],
     "phase3": ["-DKFW4_DMA_PHASE=3"],
+    "gm32": ["-DKFW4_GROUP_M=32"],
+    "rg4gm16": ["-DKFW4_RG=4", "-DKFW4_GROUP_M=16"],
 }
 
 
