@@ -302,3 +302,36 @@ def test_pod_ip_traffic_is_checked_at_the_pod(cl):
         text = r.read().decode()
     deny = [ln for ln in text.splitlines() if ln.startswith('gateway_authz_decisions_total{listener="sidecar",result="deny"}')]
     assert deny and float(deny[0].split()[-1]) >= 4, deny
+
+
+def test_policy_on_a_pod_only_label_is_enforced_for_ingress_traffic(cl):
+    """the gateway decides ingress traffic on the Service's selector; a policy that selects
+    a label only the pod carries (notebook-name) is enforced where the pod's own labels are known —
+    its inbound listener re-evaluates the hopped request as the ingress gateway principal."""
+    c = cl.client
+    pod = c.get("v1", "Pod", "nb-0", "alice")
+    svc = c.get("v1", "Service", "nb", "alice")
+    assert pod["metadata"]["labels"].get("notebook-name") == "nb"
+    assert "notebook-name" not in (svc["spec"].get("selector") or {})
+    pol = {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy",
+           "metadata": {"name": "deny-files-pod-label", "namespace": "alice"},
+           "spec": {"selector": {"matchLabels": {"notebook-name": "nb"}}, "action": "DENY",
+                    "rules": [{"to": [{"operation": {"paths": ["/notebook/alice/nb/api/contents*"]}}]}]}}
+    c.create(pol)
+    try:
+        assert _eventually(lambda: _nb(cl, ALICE, path="api/contents"), 403) == 403
+        assert _nb(cl, ALICE) == 200
+    finally:
+        c.delete("security.istio.io/v1beta1", "AuthorizationPolicy", "deny-files-pod-label", "alice")
+    assert _eventually(lambda: _nb(cl, ALICE, path="api/contents") != 403, True)
+
+
+def test_plus_stays_a_plus_and_encoded_slashes_are_refused(cl):
+    """paths are decoded as paths, not as form data — a literal '+' (a file a+b.ipynb)
+    reaches the backend as '+', and an encoded '/' (%2F) is refused before routing or authorization
+    can read it as a segment separator (Istio's default for escaped slashes is to reject too)."""
+    code, body = _http(cl.gateway + "/notebook/alice/nb/files/a+b.ipynb", headers=cl.user_headers(ALICE))
+    assert code == 404 and "a+b.ipynb" in body and "a%20b" not in body, (code, body)
+    for p in ("files/a%2Fb", "files/a%2fb", "api/x%2F..%2Fterminals"):
+        code, _ = _http(cl.gateway + "/notebook/alice/nb/" + p, headers=cl.user_headers(ALICE))
+        assert code == 400, (p, code)
