@@ -367,6 +367,152 @@ ApiError ProfileReconciler::apply_plugins(const Json& profile, bool revoke) {
   return {};
 }
 
+namespace {
+bool has_finalizer(const Json& o, const char* fin) {
+  for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
+    if (f.as_string() == fin) return true;
+  return false;
+}
+}  // namespace
+
+ProfileReconciler::Failure ProfileReconciler::ensure_namespace(Json& profile, const std::map<std::string, std::string>& labels,
+                                                               bool* stop, Result* stop_result, std::string* err) {
+  const std::string name = profile.str_at({"metadata", "name"});
+  const std::string owner = profile.at_path({"spec", "owner", "name"}).as_string();
+  Json ns{{"apiVersion", "v1"}, {"kind", "Namespace"},
+          {"metadata", Json{{"name", name}, {"annotations", Json{{"owner", owner}}}, {"labels", Json{{"istio-injection", "enabled"}}}}}};
+  set_namespace_labels(ns, labels);
+  set_controller_reference(profile, ns);
+  Json found;
+  ApiError e = c_->get("v1", "Namespace", "", name, found);
+  if (e.code == 404) {
+    KF_INFO("profile-controller", "Creating Namespace: " + name);
+    Json n = ns;
+    e = c_->create(n);
+    if (e) return {e, "error creating namespace"};
+    // wait for completion (constant backoff, 5 x 3 s in the reference)
+    const double deadline = now_seconds() + o_.namespace_wait_s;
+    while (c_->get("v1", "Namespace", "", name, found)) {
+      if (now_seconds() > deadline) {
+        inc_request_error_counter("error namespace create completion", "major");
+        *stop = true;
+        *stop_result = fail_condition(profile, "Owning namespace failed to create within 15 seconds", err);
+        return {};
+      }
+      ::usleep(50000);
+    }
+    return {};
+  }
+  if (e) return {e, nullptr};
+  if (!(annotation(found, "owner") == owner && has_annotation(found, "owner"))) {
+    inc_request_counter("reject profile taking over existing namespace");
+    *stop = true;
+    *stop_result = fail_condition(profile, "namespace already exist, but not owned by profile creator " + owner, err);
+    return {};
+  }
+  Json updated = found;
+  set_namespace_labels(updated, labels);
+  if (updated.at_path({"metadata", "labels"}) != found.at_path({"metadata", "labels"})) return {c_->update(updated), nullptr};
+  return {};
+}
+
+ApiError ProfileReconciler::ensure_rolebinding(const Json& profile, const std::string& rb_name, const std::string& cluster_role,
+                                               const Json& subject, const Json& ann) {
+  const std::string ns = profile.str_at({"metadata", "name"});
+  Json rb{{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "RoleBinding"},
+          {"metadata", Json{{"name", rb_name}, {"namespace", ns}}},
+          {"roleRef", Json{{"apiGroup", "rbac.authorization.k8s.io"}, {"kind", "ClusterRole"}, {"name", cluster_role}}},
+          {"subjects", Json::array({subject})}};
+  if (ann.is_object()) rb["metadata"]["annotations"] = ann;
+  set_controller_reference(profile, rb);
+  Json cur;
+  ApiError ge = c_->get("rbac.authorization.k8s.io/v1", "RoleBinding", ns, rb_name, cur);
+  if (ge.code == 404) return c_->create(rb);
+  if (ge) return ge;
+  if (cur["roleRef"] == rb["roleRef"] && cur["subjects"] == rb["subjects"]) return ApiError{};
+  cur["roleRef"] = rb["roleRef"];
+  cur["subjects"] = rb["subjects"];
+  return c_->update(cur);
+}
+
+// default-editor / default-viewer ServiceAccounts, each bound to its kubeflow-edit / -view role
+ProfileReconciler::Failure ProfileReconciler::ensure_service_accounts(const Json& profile) {
+  const std::string ns = profile.str_at({"metadata", "name"});
+  for (auto sa_role : {std::make_pair(DEFAULT_EDITOR, "kubeflow-edit"), std::make_pair(DEFAULT_VIEWER, "kubeflow-view")}) {
+    Json sa{{"apiVersion", "v1"}, {"kind", "ServiceAccount"}, {"metadata", Json{{"name", sa_role.first}, {"namespace", ns}}}};
+    set_controller_reference(profile, sa);
+    Json cur;
+    ApiError ge = c_->get("v1", "ServiceAccount", ns, sa_role.first, cur);
+    if (ge.code == 404) ge = c_->create(sa);
+    if (ge) return {ge, "error updating ServiceAccount"};
+    ge = ensure_rolebinding(profile, sa_role.first, sa_role.second,
+                            Json{{"kind", "ServiceAccount"}, {"name", sa_role.first}, {"namespace", ns}}, Json());
+    if (ge) return {ge, nullptr};
+  }
+  return {};
+}
+
+// spec.resourceQuotaSpec as the namespace's kf-resource-quota (removed when the spec has none)
+ProfileReconciler::Failure ProfileReconciler::ensure_quota(const Json& profile) {
+  const std::string ns = profile.str_at({"metadata", "name"});
+  const Json& rq = profile.at_path({"spec", "resourceQuotaSpec"});
+  if (!(rq["hard"].is_object() && !rq["hard"].empty())) {
+    ApiError de = c_->remove("v1", "ResourceQuota", ns, KF_QUOTA);
+    if (de && de.code != 404) return {de, nullptr};
+    return {};
+  }
+  Json q{{"apiVersion", "v1"}, {"kind", "ResourceQuota"}, {"metadata", Json{{"name", KF_QUOTA}, {"namespace", ns}}}, {"spec", rq}};
+  set_controller_reference(profile, q);
+  Json cur;
+  ApiError ge = c_->get("v1", "ResourceQuota", ns, KF_QUOTA, cur);
+  if (ge.code == 404) {
+    ge = c_->create(q);
+  } else if (!ge && cur["spec"] != rq) {
+    cur["spec"] = rq;
+    ge = c_->update(cur);
+  }
+  if (ge) return {ge, "error updating resource quota"};
+  return {};
+}
+
+// the default WorkloadIdentity plugin (Q5 fix: the Profile is written only when one is added)
+ProfileReconciler::Failure ProfileReconciler::ensure_default_plugins(Json& profile) {
+  if (o_.workload_identity.empty()) return {};
+  for (const auto& p : profile.at_path({"spec", "plugins"}).as_array())
+    if (p["kind"].as_string() == KIND_WORKLOAD_IDENTITY) return {};
+  profile["spec"]["plugins"].push_back(Json{{"kind", KIND_WORKLOAD_IDENTITY}, {"spec", Json{{"gcpServiceAccount", o_.workload_identity}}}});
+  ApiError e = c_->update(profile);
+  if (e) return {e, "error patching DefaultPluginSpec"};
+  return {};
+}
+
+ProfileReconciler::Failure ProfileReconciler::ensure_finalizer(const Json& profile) {
+  if (has_finalizer(profile, PROFILE_FINALIZER)) return {};
+  ApiError e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", profile.str_at({"metadata", "name"}), [](Json& o) {
+    if (has_finalizer(o, PROFILE_FINALIZER)) return false;
+    o["metadata"]["finalizers"].push_back(PROFILE_FINALIZER);
+    return true;
+  });
+  if (e) return {e, "error updating finalizer"};
+  return {};
+}
+
+// deletion: revoke the plugins, then drop the finalizer (the namespace goes with its owner reference)
+ProfileReconciler::Failure ProfileReconciler::finalize(const Json& profile) {
+  if (!has_finalizer(profile, PROFILE_FINALIZER)) return {};
+  ApiError e = apply_plugins(profile, true);
+  if (e) return {e, "error revoking plugin"};
+  e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", profile.str_at({"metadata", "name"}), [](Json& o) {
+    Json fins = Json::array();
+    for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
+      if (f.as_string() != PROFILE_FINALIZER) fins.push_back(f);
+    o["metadata"]["finalizers"] = fins;
+    return true;
+  });
+  if (e) return {e, "error removing finalizer"};
+  return {};
+}
+
 Result ProfileReconciler::reconcile(const Request& r, std::string* err) {
   auto labels = read_labels();
   Json profile;
@@ -380,194 +526,39 @@ Result ProfileReconciler::reconcile(const Request& r, std::string* err) {
     *err = e.message;
     return {};
   }
+  auto failed = [&](const Failure& f) {
+    if (f.counter) inc_request_error_counter(f.counter, "major");
+    *err = f.error.message;
+    return Result{};
+  };
+  if (profile.at_path({"metadata", "deletionTimestamp"}).is_string()) {
+    if (Failure f = finalize(profile)) return failed(f);
+    inc_request_counter("reconcile");
+    return {};
+  }
+  // 1. namespace
+  bool stop = false;
+  Result stop_result;
+  if (Failure f = ensure_namespace(profile, labels, &stop, &stop_result, err)) return failed(f);
+  if (stop) return stop_result;
+  // 2. the owner's Istio AuthorizationPolicy
   const std::string name = profile.str_at({"metadata", "name"});
   const std::string owner = profile.at_path({"spec", "owner", "name"}).as_string();
-  const bool deleting = profile.at_path({"metadata", "deletionTimestamp"}).is_string();
-  if (!deleting) {
-    // ---- 1. namespace
-    Json ns{{"apiVersion", "v1"}, {"kind", "Namespace"},
-            {"metadata", Json{{"name", name}, {"annotations", Json{{"owner", owner}}}, {"labels", Json{{"istio-injection", "enabled"}}}}}};
-    set_namespace_labels(ns, labels);
-    set_controller_reference(profile, ns);
-    Json found;
-    e = c_->get("v1", "Namespace", "", name, found);
-    if (e.code == 404) {
-      KF_INFO("profile-controller", "Creating Namespace: " + name);
-      Json n = ns;
-      e = c_->create(n);
-      if (e) {
-        inc_request_error_counter("error creating namespace", "major");
-        *err = e.message;
-        return {};
-      }
-      // wait for completion (constant backoff, 5 x 3 s in the reference)
-      double deadline = now_seconds() + o_.namespace_wait_s;
-      while (c_->get("v1", "Namespace", "", name, found)) {
-        if (now_seconds() > deadline) {
-          inc_request_error_counter("error namespace create completion", "major");
-          return fail_condition(profile, "Owning namespace failed to create within 15 seconds", err);
-        }
-        ::usleep(50000);
-      }
-    } else if (e) {
-      *err = e.message;
-      return {};
-    } else {
-      if (annotation(found, "owner") == owner && has_annotation(found, "owner")) {
-        Json updated = found;
-        set_namespace_labels(updated, labels);
-        if (updated.at_path({"metadata", "labels"}) != found.at_path({"metadata", "labels"})) {
-          e = c_->update(updated);
-          if (e) {
-            *err = e.message;
-            return {};
-          }
-        }
-      } else {
-        inc_request_counter("reject profile taking over existing namespace");
-        return fail_condition(profile, "namespace already exist, but not owned by profile creator " + owner, err);
-      }
-    }
-    // ---- 2. Istio AuthorizationPolicy
-    Json ap{{"apiVersion", "security.istio.io/v1beta1"}, {"kind", "AuthorizationPolicy"},
-            {"metadata", Json{{"name", AUTHZ_POLICY_ISTIO}, {"namespace", name}, {"annotations", Json{{"user", owner}, {"role", "admin"}}}}},
-            {"spec", authorization_policy_spec(profile, o_)}};
-    set_controller_reference(profile, ap);
-    e = reconcile_owned(*c_, ap, CopyKind::Generic);
-    if (e) {
-      inc_request_error_counter("error updating Istio AuthorizationPolicy permission", "major");
-      *err = e.message;
-      return {};
-    }
-    // ---- 3. ServiceAccounts + their RoleBindings
-    auto rolebinding = [&](const std::string& rb_name, const std::string& cluster_role, const Json& subject, const Json& ann) {
-      Json rb{{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "RoleBinding"},
-              {"metadata", Json{{"name", rb_name}, {"namespace", name}}},
-              {"roleRef", Json{{"apiGroup", "rbac.authorization.k8s.io"}, {"kind", "ClusterRole"}, {"name", cluster_role}}},
-              {"subjects", Json::array({subject})}};
-      if (ann.is_object()) rb["metadata"]["annotations"] = ann;
-      set_controller_reference(profile, rb);
-      Json cur;
-      ApiError ge = c_->get("rbac.authorization.k8s.io/v1", "RoleBinding", name, rb_name, cur);
-      if (ge.code == 404) return c_->create(rb);
-      if (ge) return ge;
-      if (cur["roleRef"] == rb["roleRef"] && cur["subjects"] == rb["subjects"]) return ApiError{};
-      cur["roleRef"] = rb["roleRef"];
-      cur["subjects"] = rb["subjects"];
-      return c_->update(cur);
-    };
-    for (auto sa_role : {std::make_pair(DEFAULT_EDITOR, "kubeflow-edit"), std::make_pair(DEFAULT_VIEWER, "kubeflow-view")}) {
-      Json sa{{"apiVersion", "v1"}, {"kind", "ServiceAccount"}, {"metadata", Json{{"name", sa_role.first}, {"namespace", name}}}};
-      set_controller_reference(profile, sa);
-      Json cur;
-      ApiError ge = c_->get("v1", "ServiceAccount", name, sa_role.first, cur);
-      if (ge.code == 404) ge = c_->create(sa);
-      if (ge) {
-        inc_request_error_counter("error updating ServiceAccount", "major");
-        *err = ge.message;
-        return {};
-      }
-      ge = rolebinding(sa_role.first, sa_role.second,
-                       Json{{"kind", "ServiceAccount"}, {"name", sa_role.first}, {"namespace", name}}, Json());
-      if (ge) {
-        *err = ge.message;
-        return {};
-      }
-    }
-    // ---- 4. owner RoleBinding "namespaceAdmin"
-    Json owner_subject = profile.at_path({"spec", "owner"});
-    e = rolebinding("namespaceAdmin", "kubeflow-admin", owner_subject, Json{{"user", owner}, {"role", "admin"}});
-    if (e) {
-      inc_request_error_counter("error updating Owner Rolebinding", "major");
-      *err = e.message;
-      return {};
-    }
-    // ---- 5. ResourceQuota
-    const Json& rq = profile.at_path({"spec", "resourceQuotaSpec"});
-    if (rq["hard"].is_object() && !rq["hard"].empty()) {
-      Json q{{"apiVersion", "v1"}, {"kind", "ResourceQuota"}, {"metadata", Json{{"name", KF_QUOTA}, {"namespace", name}}}, {"spec", rq}};
-      set_controller_reference(profile, q);
-      Json cur;
-      ApiError ge = c_->get("v1", "ResourceQuota", name, KF_QUOTA, cur);
-      if (ge.code == 404) ge = c_->create(q);
-      else if (!ge && cur["spec"] != rq) {
-        cur["spec"] = rq;
-        ge = c_->update(cur);
-      }
-      if (ge) {
-        inc_request_error_counter("error updating resource quota", "major");
-        *err = ge.message;
-        return {};
-      }
-    } else {
-      ApiError de = c_->remove("v1", "ResourceQuota", name, KF_QUOTA);
-      if (de && de.code != 404) {
-        *err = de.message;
-        return {};
-      }
-    }
-    // ---- 6. default plugins (Q5 fix: only write when something is added)
-    if (!o_.workload_identity.empty()) {
-      bool have = false;
-      for (const auto& p : profile.at_path({"spec", "plugins"}).as_array()) have = have || p["kind"].as_string() == KIND_WORKLOAD_IDENTITY;
-      if (!have) {
-        profile["spec"]["plugins"].push_back(
-            Json{{"kind", KIND_WORKLOAD_IDENTITY}, {"spec", Json{{"gcpServiceAccount", o_.workload_identity}}}});
-        e = c_->update(profile);
-        if (e) {
-          inc_request_error_counter("error patching DefaultPluginSpec", "major");
-          *err = e.message;
-          return {};
-        }
-      }
-    }
-    // ---- 7. plugins
-    e = apply_plugins(profile, false);
-    if (e) {
-      inc_request_error_counter("error applying plugin", "major");
-      *err = e.message;
-      return {};
-    }
-    // ---- 8. finalizer
-    bool has_fin = false;
-    for (const auto& f : profile.at_path({"metadata", "finalizers"}).as_array()) has_fin = has_fin || f.as_string() == PROFILE_FINALIZER;
-    if (!has_fin) {
-      e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", name, [](Json& o) {
-        for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
-          if (f.as_string() == PROFILE_FINALIZER) return false;
-        o["metadata"]["finalizers"].push_back(PROFILE_FINALIZER);
-        return true;
-      });
-      if (e) {
-        inc_request_error_counter("error updating finalizer", "major");
-        *err = e.message;
-        return {};
-      }
-    }
-  } else {
-    bool has_fin = false;
-    for (const auto& f : profile.at_path({"metadata", "finalizers"}).as_array()) has_fin = has_fin || f.as_string() == PROFILE_FINALIZER;
-    if (has_fin) {
-      e = apply_plugins(profile, true);
-      if (e) {
-        inc_request_error_counter("error revoking plugin", "major");
-        *err = e.message;
-        return {};
-      }
-      e = c_->update_with_retry("kubeflow.org/v1", "Profile", "", name, [](Json& o) {
-        Json fins = Json::array();
-        for (const auto& f : o.at_path({"metadata", "finalizers"}).as_array())
-          if (f.as_string() != PROFILE_FINALIZER) fins.push_back(f);
-        o["metadata"]["finalizers"] = fins;
-        return true;
-      });
-      if (e) {
-        inc_request_error_counter("error removing finalizer", "major");
-        *err = e.message;
-        return {};
-      }
-    }
-  }
+  Json ap{{"apiVersion", "security.istio.io/v1beta1"}, {"kind", "AuthorizationPolicy"},
+          {"metadata", Json{{"name", AUTHZ_POLICY_ISTIO}, {"namespace", name}, {"annotations", Json{{"user", owner}, {"role", "admin"}}}}},
+          {"spec", authorization_policy_spec(profile, o_)}};
+  set_controller_reference(profile, ap);
+  if ((e = reconcile_owned(*c_, ap, CopyKind::Generic))) return failed({e, "error updating Istio AuthorizationPolicy permission"});
+  // 3. ServiceAccounts + their RoleBindings, 4. the owner's RoleBinding "namespaceAdmin"
+  if (Failure f = ensure_service_accounts(profile)) return failed(f);
+  if ((e = ensure_rolebinding(profile, "namespaceAdmin", "kubeflow-admin", profile.at_path({"spec", "owner"}),
+                              Json{{"user", owner}, {"role", "admin"}})))
+    return failed({e, "error updating Owner Rolebinding"});
+  // 5. ResourceQuota, 6. default plugins, 7. plugins, 8. finalizer
+  if (Failure f = ensure_quota(profile)) return failed(f);
+  if (Failure f = ensure_default_plugins(profile)) return failed(f);
+  if ((e = apply_plugins(profile, false))) return failed({e, "error applying plugin"});
+  if (Failure f = ensure_finalizer(profile)) return failed(f);
   inc_request_counter("reconcile");
   return {};
 }

@@ -97,6 +97,24 @@ class ProfileReconciler {
   std::map<std::string, std::string> read_labels();
   ApiError apply_plugins(const Json& profile, bool revoke);
   Result fail_condition(Json& profile, const std::string& msg, std::string* err);
+  // reconcile's steps (profile_controller.go Reconcile, in its order). A step that fails returns the
+  // error and names the request-error counter it bumps (nullptr: none)
+  struct Failure {
+    ApiError error;
+    const char* counter = nullptr;
+    explicit operator bool() const { return static_cast<bool>(error); }
+  };
+  // the owned namespace: created (and waited for) or relabelled; `stop` set when reconcile must
+  // return `stop_result` (a failed condition) instead of going on
+  Failure ensure_namespace(Json& profile, const std::map<std::string, std::string>& labels, bool* stop,
+                           Result* stop_result, std::string* err);
+  ApiError ensure_rolebinding(const Json& profile, const std::string& rb_name, const std::string& cluster_role,
+                              const Json& subject, const Json& ann);
+  Failure ensure_service_accounts(const Json& profile);
+  Failure ensure_quota(const Json& profile);
+  Failure ensure_default_plugins(Json& profile);
+  Failure ensure_finalizer(const Json& profile);
+  Failure finalize(const Json& profile);
   std::shared_ptr<Client> c_;
   ProfileOptions o_;
   std::shared_ptr<CloudIam> iam_;
