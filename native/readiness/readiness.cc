@@ -510,26 +510,30 @@ bool allreduce_check(int ndev, const Args& a, Json& out) {
   return ok;
 }
 
-// K3 fast path: one-shot peer all-reduce. sim_ranks > 0: that many ranks on device 0, one launch.
-bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<hipStream_t>& dev_streams, Json& out) {
-  g_stage = "allreduce-oneshot";
-  const bool sim = sim_ranks > 0;
-  const int nranks = sim ? sim_ranks : ndev;
-  if (nranks < 2 || nranks > 8) {
-    out = Json{{"skipped", "needs 2..8 ranks"}};
-    return true;
-  }
-  const size_t max_bytes = 256 << 10;
-  const int max_blocks = 64;
-  const long long fbytes = kfamd_allreduce_oneshot_flag_bytes(nranks, max_blocks);
-  Json stages = Json::object();
-  auto tp = std::chrono::steady_clock::now();
-  auto lap = [&](const char* name) {
-    const auto now = std::chrono::steady_clock::now();
-    stages[name] = std::chrono::duration<double, std::milli>(now - tp).count();
-    tp = now;
-  };
-  if (!sim) {
+double lap_ms(std::chrono::steady_clock::time_point& t) {
+  auto now = std::chrono::steady_clock::now();
+  double ms = std::chrono::duration<double, std::milli>(now - t).count();
+  t = now;
+  return ms;
+}
+
+// The one-shot / two-shot peer all-reduce rig (K3 fast path): per-rank buffers, cross-device flags
+// and timeout words, one stream per device (sim: nranks ranks on device 0, one launch)
+struct PeerRig {
+  int nranks = 0;
+  bool sim = false;
+  long long fbytes = 0;
+  unsigned epoch = 0;
+  std::vector<uint32_t*> flags;
+  std::vector<unsigned*> tmo;
+  std::vector<hipStream_t> st;
+  std::vector<bool> own;
+  int dev_of(int r) const { return sim ? 0 : r; }
+  hipStream_t stream_of(int r) const { return st[sim ? 0 : r]; }
+  int launchers() const { return sim ? 1 : nranks; }
+
+  bool enable_peers() {
+    if (sim) return true;
     for (int i = 0; i < nranks; ++i) {
       HIP_OK(hipSetDevice(i));
       for (int j = 0; j < nranks; ++j) {
@@ -541,64 +545,150 @@ bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<h
         }
       }
     }
+    return true;
   }
-  lap("peer_access_ms");
-  auto dev_of = [&](int r) { return sim ? 0 : r; };
-  std::vector<void*> in(8, nullptr), outb(8, nullptr);
-  std::vector<uint32_t*> flags(8, nullptr);
-  std::vector<unsigned*> tmo(nranks, nullptr);
   // each device's stream from the GEMM / LayerNorm stages: every new stream (and the null stream's
   // first use) brings up another HW queue, about 20 ms each on the cold-start path
-  std::vector<hipStream_t> st(sim ? 1 : nranks, nullptr);
-  std::vector<bool> own(st.size(), false);
-  for (size_t i = 0; i < st.size(); ++i) {
-    const int d = sim ? 0 : (int)i;
-    if (d < (int)dev_streams.size() && dev_streams[d]) {
-      st[i] = dev_streams[d];
-    } else {
-      HIP_OK(hipSetDevice(d));
-      HIP_OK(hipStreamCreate(&st[i]));
-      own[i] = true;
+  bool setup(const std::vector<hipStream_t>& dev_streams) {
+    flags.assign(8, nullptr);
+    tmo.assign(nranks, nullptr);
+    st.assign(sim ? 1 : nranks, nullptr);
+    own.assign(st.size(), false);
+    for (size_t i = 0; i < st.size(); ++i) {
+      const int d = sim ? 0 : (int)i;
+      if (d < (int)dev_streams.size() && dev_streams[d]) {
+        st[i] = dev_streams[d];
+      } else {
+        HIP_OK(hipSetDevice(d));
+        HIP_OK(hipStreamCreate(&st[i]));
+        own[i] = true;
+      }
+    }
+    for (int r = 0; r < nranks; ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      // flags are polled across devices: uncached so a peer's atomic store is seen without a flush
+      if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags[r]), fbytes, hipDeviceMallocUncached) != hipSuccess)
+        HIP_OK(hipMalloc(&flags[r], fbytes));
+      HIP_OK(hipMemsetAsync(flags[r], 0, fbytes, stream_of(r)));
+      HIP_OK(hipMalloc(&tmo[r], sizeof(unsigned)));
+      HIP_OK(hipMemsetAsync(tmo[r], 0, sizeof(unsigned), stream_of(r)));
+    }
+    for (size_t i = 0; i < st.size(); ++i) {
+      HIP_OK(hipSetDevice(sim ? 0 : (int)i));
+      HIP_OK(hipStreamSynchronize(st[i]));  // flags zeroed on every device before any rank launches
+    }
+    return true;
+  }
+  bool alloc(std::vector<void*>& in, std::vector<void*>& out, size_t bytes) {
+    in.assign(8, nullptr);
+    out.assign(8, nullptr);
+    for (int r = 0; r < nranks; ++r) {
+      HIP_OK(hipSetDevice(dev_of(r)));
+      HIP_OK(hipMalloc(&in[r], bytes));
+      HIP_OK(hipMalloc(&out[r], bytes));
+    }
+    return true;
+  }
+  void free_bufs(std::vector<void*>& in, std::vector<void*>& out) {
+    for (int r = 0; r < nranks; ++r) {
+      (void)hipSetDevice(dev_of(r));
+      (void)hipFree(in[r]);
+      (void)hipFree(out[r]);
     }
   }
-  auto stream_of = [&](int r) { return st[sim ? 0 : r]; };
-  for (int r = 0; r < nranks; ++r) {
-    HIP_OK(hipSetDevice(dev_of(r)));
-    HIP_OK(hipMalloc(&in[r], max_bytes));
-    HIP_OK(hipMalloc(&outb[r], max_bytes));
-    // flags are polled across devices: uncached so a peer's atomic store is seen without a flush
-    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags[r]), fbytes, hipDeviceMallocUncached) != hipSuccess)
-      HIP_OK(hipMalloc(&flags[r], fbytes));
-    HIP_OK(hipMemsetAsync(flags[r], 0, fbytes, stream_of(r)));
-    HIP_OK(hipMalloc(&tmo[r], sizeof(unsigned)));
-    HIP_OK(hipMemsetAsync(tmo[r], 0, sizeof(unsigned), stream_of(r)));
+  void teardown() {
+    for (int r = 0; r < nranks; ++r) {
+      (void)hipSetDevice(dev_of(r));
+      (void)hipFree(flags[r]);
+      (void)hipFree(tmo[r]);
+    }
+    for (size_t i = 0; i < st.size(); ++i)
+      if (own[i]) (void)hipStreamDestroy(st[i]);
   }
-  for (size_t i = 0; i < st.size(); ++i) {
-    HIP_OK(hipSetDevice(sim ? 0 : (int)i));
-    HIP_OK(hipStreamSynchronize(st[i]));  // flags zeroed on every device before any rank launches
-  }
-  lap("alloc_ms");
-  unsigned epoch = 0;
-  bool ok = true;
-  auto launch_all = [&](size_t n) -> bool {
+  // one all-reduce of n floats on every rank (twoshot: reduce-scatter + all-gather), all synced
+  bool launch(bool twoshot, std::vector<void*>& in, std::vector<void*>& out, size_t n) {
     ++epoch;
-    const int nb = kfamd_allreduce_oneshot_blocks((long long)n, KFAMD_DTYPE_F32);
-    for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+    const int nb = twoshot ? kfamd_allreduce_twoshot_blocks((long long)n, KFAMD_DTYPE_F32, nranks)
+                           : kfamd_allreduce_oneshot_blocks((long long)n, KFAMD_DTYPE_F32);
+    for (int r = 0; r < launchers(); ++r) {
       HIP_OK(hipSetDevice(dev_of(r)));
-      int rc = kfamd_allreduce_oneshot(in.data(), outb.data(), flags.data(), nranks, sim ? 0 : r, sim ? nranks : 1,
-                                       (long long)n, KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r]);
+      const int rank = sim ? 0 : r, local = sim ? nranks : 1;
+      const int rc = twoshot ? kfamd_allreduce_twoshot(in.data(), out.data(), flags.data(), nranks, rank, local, (long long)n,
+                                                       KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r])
+                             : kfamd_allreduce_oneshot(in.data(), out.data(), flags.data(), nranks, rank, local, (long long)n,
+                                                       KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r]);
       if (rc != 0) {
-        fail("kfamd_allreduce_oneshot rc=" + std::to_string(rc));
+        fail(std::string(twoshot ? "kfamd_allreduce_twoshot" : "kfamd_allreduce_oneshot") + " rc=" + std::to_string(rc));
         return false;
       }
     }
-    for (int r = 0; r < (sim ? 1 : nranks); ++r) {
+    for (int r = 0; r < launchers(); ++r) {
       HIP_OK(hipSetDevice(dev_of(r)));
       HIP_OK(hipStreamSynchronize(st[r]));
     }
     return true;
-  };
-  Json sweep = Json::array();
+  }
+  // each size: ranks fill r + 1, one checked all-reduce (every element = sum, no peer timeout),
+  // then `iters` timed ones; us = host wall per call incl. launch + stream sync
+  bool sweep(bool twoshot, std::vector<void*>& in, std::vector<void*>& out, const std::vector<size_t>& sizes, int iters,
+             bool* ok, Json& pts) {
+    for (size_t bytes : sizes) {
+      const size_t n = bytes / 4;
+      for (int r = 0; r < nranks; ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        hipLaunchKernelGGL(fill_const, dim3(64), dim3(256), 0, stream_of(r), static_cast<float*>(in[r]), n, (float)(r + 1));
+        HIP_OK(hipStreamSynchronize(stream_of(r)));
+      }
+      if (!launch(twoshot, in, out, n)) return false;
+      const float want = (float)nranks * (nranks + 1) / 2;
+      std::vector<float> h(n);
+      for (int r = 0; r < nranks; ++r) {
+        HIP_OK(hipSetDevice(dev_of(r)));
+        unsigned t = 0;
+        HIP_OK(hipMemcpyAsync(h.data(), out[r], bytes, hipMemcpyDeviceToHost, stream_of(r)));
+        HIP_OK(hipMemcpyAsync(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost, stream_of(r)));
+        HIP_OK(hipStreamSynchronize(stream_of(r)));
+        for (size_t i = 0; i < n; ++i)
+          if (h[i] != want) *ok = false;
+        if (t) *ok = false;
+      }
+      auto t1 = std::chrono::steady_clock::now();
+      for (int it = 0; it < iters; ++it)
+        if (!launch(twoshot, in, out, n)) return false;
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / iters;
+      Json p{{"bytes", (long long)bytes}, {"us", us}};
+      if (twoshot) {
+        const double algbw = bytes / (us * 1e-6) / 1e9;
+        p["algbw_GBps"] = algbw;
+        p["busbw_GBps"] = algbw * 2.0 * (nranks - 1) / nranks;
+      }
+      pts.push_back(p);
+    }
+    return true;
+  }
+};
+
+// K3 fast path: one-shot peer all-reduce. sim_ranks > 0: that many ranks on device 0, one launch.
+bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<hipStream_t>& dev_streams, Json& out) {
+  g_stage = "allreduce-oneshot";
+  PeerRig rig;
+  rig.sim = sim_ranks > 0;
+  rig.nranks = rig.sim ? sim_ranks : ndev;
+  if (rig.nranks < 2 || rig.nranks > 8) {
+    out = Json{{"skipped", "needs 2..8 ranks"}};
+    return true;
+  }
+  const size_t max_bytes = 256 << 10;
+  rig.fbytes = kfamd_allreduce_oneshot_flag_bytes(rig.nranks, 64);
+  Json stages = Json::object();
+  auto tp = std::chrono::steady_clock::now();
+  auto lap = [&](const char* name) { stages[name] = lap_ms(tp); };
+  if (!rig.enable_peers()) return false;
+  lap("peer_access_ms");
+  std::vector<void*> in, outb;
+  if (!rig.setup(dev_streams) || !rig.alloc(in, outb, max_bytes)) return false;
+  lap("alloc_ms");
+  bool ok = true;
   // on the cold-start path (an N-GPU pod's init container) three sizes verify the small, mid and
   // largest one-shot shapes; every launch syncs all N devices, so the full sweep costs tens of ms
   std::vector<size_t> sizes;
@@ -606,117 +696,30 @@ bool oneshot_check(int ndev, int sim_ranks, bool full_sweep, const std::vector<h
     for (size_t b = 16; b <= max_bytes; b *= 4) sizes.push_back(b);
   else
     sizes = {16, 16 << 10, max_bytes};
-  const int iters = full_sweep ? 50 : 10;
-  for (size_t bytes : sizes) {
-    const size_t n = bytes / 4;
-    for (int r = 0; r < nranks; ++r) {
-      HIP_OK(hipSetDevice(dev_of(r)));
-      hipLaunchKernelGGL(fill_const, dim3(64), dim3(256), 0, st[sim ? 0 : r], static_cast<float*>(in[r]), n, (float)(r + 1));
-      HIP_OK(hipStreamSynchronize(st[sim ? 0 : r]));
-    }
-    if (!launch_all(n)) return false;
-    const float want = (float)nranks * (nranks + 1) / 2;
-    std::vector<float> h(n);
-    for (int r = 0; r < nranks; ++r) {
-      HIP_OK(hipSetDevice(dev_of(r)));
-      unsigned t = 0;
-      HIP_OK(hipMemcpyAsync(h.data(), outb[r], bytes, hipMemcpyDeviceToHost, stream_of(r)));
-      HIP_OK(hipMemcpyAsync(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost, stream_of(r)));
-      HIP_OK(hipStreamSynchronize(stream_of(r)));
-      for (size_t i = 0; i < n; ++i)
-        if (h[i] != want) ok = false;
-      if (t) ok = false;
-    }
-    auto t1 = std::chrono::steady_clock::now();
-    for (int it = 0; it < iters; ++it)
-      if (!launch_all(n)) return false;
-    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / iters;
-    sweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}});
-  }
+  Json sweep = Json::array();
+  if (!rig.sweep(false, in, outb, sizes, full_sweep ? 50 : 10, &ok, sweep)) return false;
   lap("sweep_ms");
   // two-shot (reduce-scatter + all-gather over all peers at once) for the mid sizes: one size on the
   // cold-start path (correctness of the kernel on this hive), 256 KiB..64 MiB with --full-sweep
   Json tsweep = Json::array();
-  if (nranks > 2 || full_sweep) {
+  if (rig.nranks > 2 || full_sweep) {
     const size_t ts_max = full_sweep ? (64u << 20) : (1u << 20);
-    std::vector<void*> tin(8, nullptr), tout(8, nullptr);
-    for (int r = 0; r < nranks; ++r) {
-      HIP_OK(hipSetDevice(dev_of(r)));
-      HIP_OK(hipMalloc(&tin[r], ts_max));
-      HIP_OK(hipMalloc(&tout[r], ts_max));
-    }
-    auto launch_ts = [&](size_t n) -> bool {
-      ++epoch;
-      const int nb = kfamd_allreduce_twoshot_blocks((long long)n, KFAMD_DTYPE_F32, nranks);
-      for (int r = 0; r < (sim ? 1 : nranks); ++r) {
-        HIP_OK(hipSetDevice(dev_of(r)));
-        int rc = kfamd_allreduce_twoshot(tin.data(), tout.data(), flags.data(), nranks, sim ? 0 : r,
-                                         sim ? nranks : 1, (long long)n, KFAMD_DTYPE_F32, epoch, nb, tmo[r], st[r]);
-        if (rc != 0) {
-          fail("kfamd_allreduce_twoshot rc=" + std::to_string(rc));
-          return false;
-        }
-      }
-      for (int r = 0; r < (sim ? 1 : nranks); ++r) {
-        HIP_OK(hipSetDevice(dev_of(r)));
-        HIP_OK(hipStreamSynchronize(st[r]));
-      }
-      return true;
-    };
+    std::vector<void*> tin, tout;
+    if (!rig.alloc(tin, tout, ts_max)) return false;
     std::vector<size_t> tsizes;
     if (full_sweep)
       for (size_t b = 256u << 10; b <= ts_max; b *= 4) tsizes.push_back(b);
     else
       tsizes = {ts_max};
-    for (size_t bytes : tsizes) {
-      const size_t n = bytes / 4;
-      for (int r = 0; r < nranks; ++r) {
-        HIP_OK(hipSetDevice(dev_of(r)));
-        hipLaunchKernelGGL(fill_const, dim3(64), dim3(256), 0, st[sim ? 0 : r], static_cast<float*>(tin[r]), n,
-                           (float)(r + 1));
-        HIP_OK(hipStreamSynchronize(st[sim ? 0 : r]));
-      }
-      if (!launch_ts(n)) return false;
-      const float want = (float)nranks * (nranks + 1) / 2;
-      std::vector<float> h(n);
-      for (int r = 0; r < nranks; ++r) {
-        HIP_OK(hipSetDevice(dev_of(r)));
-        unsigned t = 0;
-        HIP_OK(hipMemcpyAsync(h.data(), tout[r], bytes, hipMemcpyDeviceToHost, stream_of(r)));
-        HIP_OK(hipMemcpyAsync(&t, tmo[r], sizeof t, hipMemcpyDeviceToHost, stream_of(r)));
-        HIP_OK(hipStreamSynchronize(stream_of(r)));
-        for (size_t i = 0; i < n; ++i)
-          if (h[i] != want) ok = false;
-        if (t) ok = false;
-      }
-      const int it = full_sweep ? 20 : 5;
-      auto t1 = std::chrono::steady_clock::now();
-      for (int k = 0; k < it; ++k)
-        if (!launch_ts(n)) return false;
-      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count() / it;
-      const double algbw = bytes / (us * 1e-6) / 1e9;
-      tsweep.push_back(Json{{"bytes", (long long)bytes}, {"us", us}, {"algbw_GBps", algbw},
-                            {"busbw_GBps", algbw * 2.0 * (nranks - 1) / nranks}});
-    }
-    for (int r = 0; r < nranks; ++r) {
-      (void)hipSetDevice(dev_of(r));
-      (void)hipFree(tin[r]);
-      (void)hipFree(tout[r]);
-    }
+    if (!rig.sweep(true, tin, tout, tsizes, full_sweep ? 20 : 5, &ok, tsweep)) return false;
+    rig.free_bufs(tin, tout);
     lap("twoshot_ms");
   }
-  for (int r = 0; r < nranks; ++r) {
-    (void)hipSetDevice(dev_of(r));
-    (void)hipFree(in[r]);
-    (void)hipFree(outb[r]);
-    (void)hipFree(flags[r]);
-    (void)hipFree(tmo[r]);
-  }
-  for (size_t i = 0; i < st.size(); ++i)
-    if (own[i]) (void)hipStreamDestroy(st[i]);
+  rig.free_bufs(in, outb);
+  rig.teardown();
   lap("free_ms");
-  out = Json{{"mode", sim ? "simulated-on-device-0" : "peer"}, {"ranks", nranks}, {"sweep", sweep}, {"correct", ok}, {"stages", stages},
-             {"note", "us = host wall per call incl. launch + stream sync"}};
+  out = Json{{"mode", rig.sim ? "simulated-on-device-0" : "peer"}, {"ranks", rig.nranks}, {"sweep", sweep}, {"correct", ok},
+             {"stages", stages}, {"note", "us = host wall per call incl. launch + stream sync"}};
   if (tsweep.size()) out["twoshot_sweep"] = tsweep;
   if (!ok) fail("one-shot all-reduce mismatch or peer timeout");
   return ok;
@@ -1315,11 +1318,7 @@ int main(int argc, char** argv) {
 }
 
 namespace {
-int readiness_main(int argc, char** argv) {
-  ::signal(SIGSEGV, on_fatal);
-  ::signal(SIGBUS, on_fatal);
-  ::signal(SIGABRT, on_fatal);
-  ::signal(SIGFPE, on_fatal);
+Args parse_args(int argc, char** argv) {
   Args a;
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
@@ -1348,132 +1347,151 @@ int readiness_main(int argc, char** argv) {
     else if (const char* v = val("--oneshot-sim")) a.oneshot_sim = std::atoi(v);
     else if (const char* v = val("--inject-fault")) a.inject_fault = v;
   }
-  {
-    // how many GPUs the pod was given, without touching the GPU (the device plugin's env)
-    int visible = -1;
-    for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"}) {
-      const char* v = std::getenv(var);
-      if (v && *v) {
-        visible = 1;
-        for (const char* c = v; *c; ++c) visible += *c == ',';
-        break;
-      }
-    }
-    if (!a.skip_ar && (a.force_rccl || (a.rccl && visible != 1))) {
-      auto tl = std::chrono::steady_clock::now();
-      g_rccl.load();
-      g_result["rccl_load_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count();
+  return a;
+}
+
+// librccl is loaded before HIP comes up when the pod will run the in-pod RCCL stage (the device
+// plugin's env says how many GPUs it has, without touching the GPU)
+void preload_rccl(const Args& a) {
+  int visible = -1;
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"}) {
+    const char* v = std::getenv(var);
+    if (v && *v) {
+      visible = 1;
+      for (const char* c = v; *c; ++c) visible += *c == ',';
+      break;
     }
   }
-  auto t0 = std::chrono::steady_clock::now();
-  g_stage = "hip-init";
-  int ndev = 0;
-  hipError_t e = hipGetDeviceCount(&ndev);
-  double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  g_result["hip_init_ms"] = init_ms;
-  if (!a.inject_fault.empty()) fail("injected fault at stage " + a.inject_fault + " (--inject-fault)");
-  const char* sim = std::getenv("KFAMD_SIMULATED_GPUS");
-  if (const char* vis = std::getenv("HIP_VISIBLE_DEVICES")) g_result["visible_devices"] = vis;
-  if ((e != hipSuccess || ndev == 0) && sim && std::string(sim) == "1") {
-    // node advertises synthetic GPUs (CPU CI): nothing to validate, report it as such
-    g_result["simulated"] = true;
-  } else if (e != hipSuccess || ndev == 0) {
-    fail(std::string("no GPU visible: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices"));
+  if (!a.skip_ar && (a.force_rccl || (a.rccl && visible != 1))) {
+    auto tl = std::chrono::steady_clock::now();
+    g_rccl.load();
+    g_result["rccl_load_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count();
+  }
+}
+
+// the per-device checks (one worker per device: query, GEMM, LayerNorm; per-device wall times
+// reported), then the multi-GPU stages on the same buffers and streams
+void check_devices(const Args& a, int ndev) {
+  struct DevResult {
+    Json dev = Json(), gemm = Json(), ln = Json();
+    double query_ms = 0, gemm_ms = 0, ln_ms = 0;
+  };
+  std::vector<DevResult> res(ndev);
+  // each device's buffers and stream live until the multi-GPU stages are done (they reuse the stream)
+  std::vector<DevBuffers> bufs(ndev);
+  auto check_device = [&](int d) {
+    DevResult& r = res[d];
+    g_stage = "device-query";
+    auto ts = std::chrono::steady_clock::now();
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess)
+      r.dev = Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
+                   {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}};
+    r.query_ms = lap_ms(ts);
+    DevBuffers& buf = bufs[d];
+    Json g;
+    if (gemm_check(d, a, buf, g)) r.gemm = g;
+    else r.gemm = Json{{"device", d}, {"error", first_error()}};
+    r.gemm_ms = lap_ms(ts);
+    if (!a.skip_ln) {
+      Json l;
+      if (ln_check(d, a, buf, l)) r.ln = l;
+      r.ln_ms = lap_ms(ts);
+    }
+  };
+  auto tw = std::chrono::steady_clock::now();
+  if (ndev == 1 || a.serial) {
+    for (int d = 0; d < ndev; ++d) check_device(d);
   } else {
-    // one worker per device: query, GEMM check, LayerNorm check (per-device wall times reported)
-    struct DevResult {
-      Json dev = Json(), gemm = Json(), ln = Json();
-      double query_ms = 0, gemm_ms = 0, ln_ms = 0;
-    };
-    std::vector<DevResult> res(ndev);
-    // each device's buffers and stream live until the multi-GPU stages are done (they reuse the stream)
-    std::vector<DevBuffers> bufs(ndev);
-    auto lap = [](std::chrono::steady_clock::time_point& t) {
-      auto now = std::chrono::steady_clock::now();
-      double ms = std::chrono::duration<double, std::milli>(now - t).count();
-      t = now;
-      return ms;
-    };
-    auto check_device = [&](int d) {
-      DevResult& r = res[d];
-      g_stage = "device-query";
-      auto ts = std::chrono::steady_clock::now();
-      hipDeviceProp_t p;
-      if (hipGetDeviceProperties(&p, d) == hipSuccess)
-        r.dev = Json{{"device", d}, {"name", p.name}, {"arch", p.gcnArchName}, {"cus", p.multiProcessorCount},
-                     {"hbm_GiB", (double)p.totalGlobalMem / (1ull << 30)}, {"clock_MHz", p.clockRate / 1000}};
-      r.query_ms = lap(ts);
-      DevBuffers& buf = bufs[d];
-      Json g;
-      if (gemm_check(d, a, buf, g)) r.gemm = g;
-      else r.gemm = Json{{"device", d}, {"error", first_error()}};
-      r.gemm_ms = lap(ts);
-      if (!a.skip_ln) {
-        Json l;
-        if (ln_check(d, a, buf, l)) r.ln = l;
-        r.ln_ms = lap(ts);
-      }
-    };
-    auto tw = std::chrono::steady_clock::now();
-    if (ndev == 1 || a.serial) {
-      for (int d = 0; d < ndev; ++d) check_device(d);
-    } else {
-      std::vector<std::thread> workers;
-      for (int d = 0; d < ndev; ++d) workers.emplace_back(check_device, d);
-      for (auto& w : workers) w.join();
-    }
-    g_result["devices_wall_ms"] = lap(tw);
-    g_result["devices_parallel"] = ndev > 1 && !a.serial;
-    Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
-    double st_query = 0, st_gemm = 0, st_ln = 0;  // summed over devices
-    for (int d = 0; d < ndev; ++d) {
-      if (!res[d].dev.is_null()) devs.push_back(res[d].dev);
-      gemms.push_back(res[d].gemm);
-      if (!res[d].ln.is_null()) lns.push_back(res[d].ln);
-      st_query += res[d].query_ms;
-      st_gemm += res[d].gemm_ms;
-      st_ln += res[d].ln_ms;
-    }
-    g_result["stages_ms"] = Json{{"device_query", st_query}, {"gemm", st_gemm}, {"layernorm", st_ln}};
-    g_result["devices"] = devs;
-    g_result["gemm"] = gemms;
-    if (!a.skip_ln) g_result["layernorm"] = lns;
-    double agg = 0;
-    for (const auto& gm : gemms.as_array())
-      if (gm.has("tflops")) agg += gm["tflops"].as_double();
-    g_result["gemm_tflops_aggregate"] = agg;
-    if (((ndev >= 2 && a.rccl) || a.force_rccl) && !a.skip_ar) {
-      Json ar;
-      auto ts = std::chrono::steady_clock::now();
-      allreduce_check(ndev, a, ar);
-      g_result["allreduce"] = ar;
-      g_result["stages_ms"]["allreduce"] = lap(ts);
-    }
-    if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
-      Json os;
-      auto ts = std::chrono::steady_clock::now();
-      std::vector<hipStream_t> streams;
-      for (const auto& b : bufs) streams.push_back(b.s);
-      oneshot_check(ndev, a.oneshot_sim, a.full_sweep, streams, os);
-      g_result["allreduce_oneshot"] = os;
-      g_result["stages_ms"]["allreduce_oneshot"] = lap(ts);
-    }
-    if (ndev >= 2 && (a.xgmi || a.full_sweep)) {
-      Json xg;
-      auto ts = std::chrono::steady_clock::now();
-      xgmi_probe(ndev, xg);
-      g_result["xgmi"] = xg;
-      g_result["stages_ms"]["xgmi"] = lap(ts);
-    }
+    std::vector<std::thread> workers;
+    for (int d = 0; d < ndev; ++d) workers.emplace_back(check_device, d);
+    for (auto& w : workers) w.join();
   }
-  g_stage = "report";
-  g_error = first_error();
-  g_result["ok"] = g_error.empty();
-  if (!g_error.empty()) g_result["error"] = g_error;
-  g_result["total_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  g_result["kernels"] = kfamd_build_info();
-  g_result["t_main_unix_ms"] = g_t_main_ms;
-  g_result["t_report_unix_ms"] = realtime_ms();
+  g_result["devices_wall_ms"] = lap_ms(tw);
+  g_result["devices_parallel"] = ndev > 1 && !a.serial;
+  Json devs = Json::array(), gemms = Json::array(), lns = Json::array();
+  double st_query = 0, st_gemm = 0, st_ln = 0;  // summed over devices
+  for (int d = 0; d < ndev; ++d) {
+    if (!res[d].dev.is_null()) devs.push_back(res[d].dev);
+    gemms.push_back(res[d].gemm);
+    if (!res[d].ln.is_null()) lns.push_back(res[d].ln);
+    st_query += res[d].query_ms;
+    st_gemm += res[d].gemm_ms;
+    st_ln += res[d].ln_ms;
+  }
+  g_result["stages_ms"] = Json{{"device_query", st_query}, {"gemm", st_gemm}, {"layernorm", st_ln}};
+  g_result["devices"] = devs;
+  g_result["gemm"] = gemms;
+  if (!a.skip_ln) g_result["layernorm"] = lns;
+  double agg = 0;
+  for (const auto& gm : gemms.as_array())
+    if (gm.has("tflops")) agg += gm["tflops"].as_double();
+  g_result["gemm_tflops_aggregate"] = agg;
+  if (((ndev >= 2 && a.rccl) || a.force_rccl) && !a.skip_ar) {
+    Json ar;
+    auto ts = std::chrono::steady_clock::now();
+    allreduce_check(ndev, a, ar);
+    g_result["allreduce"] = ar;
+    g_result["stages_ms"]["allreduce"] = lap_ms(ts);
+  }
+  if ((ndev >= 2 && !a.skip_ar) || a.oneshot_sim > 0) {
+    Json os;
+    auto ts = std::chrono::steady_clock::now();
+    std::vector<hipStream_t> streams;
+    for (const auto& b : bufs) streams.push_back(b.s);
+    oneshot_check(ndev, a.oneshot_sim, a.full_sweep, streams, os);
+    g_result["allreduce_oneshot"] = os;
+    g_result["stages_ms"]["allreduce_oneshot"] = lap_ms(ts);
+  }
+  if (ndev >= 2 && (a.xgmi || a.full_sweep)) {
+    Json xg;
+    auto ts = std::chrono::steady_clock::now();
+    xgmi_probe(ndev, xg);
+    g_result["xgmi"] = xg;
+    g_result["stages_ms"]["xgmi"] = lap_ms(ts);
+  }
+}
+
+// the termination message, capped at 4 KiB like Kubernetes': the summary fields first, the
+// multi-GPU stages compact
+Json termination_brief() {
+  Json brief = Json{{"ok", g_result["ok"]}, {"gemm_tflops_aggregate", g_result["gemm_tflops_aggregate"]},
+                    {"hip_init_ms", g_result["hip_init_ms"]}, {"total_ms", g_result["total_ms"]}};
+  if (g_result.has("error")) brief["error"] = g_result["error"];
+  if (g_result.has("devices")) brief["devices"] = (long long)g_result["devices"].size();
+  if (g_result.has("simulated")) brief["simulated"] = true;
+  if (g_result.has("stages_ms")) brief["stages_ms"] = g_result["stages_ms"];
+  if (g_result.has("gemm") && g_result["gemm"].size() && g_result["gemm"][0].has("stages"))
+    brief["gemm0_stages_ms"] = g_result["gemm"][0]["stages"];
+  if (g_result.has("layernorm") && g_result["layernorm"].size()) brief["layernorm_GBps"] = g_result["layernorm"][0]["GBps"];
+  if (g_result.has("devices_wall_ms")) brief["devices_wall_ms"] = g_result["devices_wall_ms"];
+  if (g_result.has("warm_op")) brief["warm_op_ms"] = g_result["warm_op"]["warm_ms"];  // HIP came up before the pod
+  if (g_result.has("allreduce_oneshot") && g_result["allreduce_oneshot"].has("sweep")) {
+    const Json& os = g_result["allreduce_oneshot"];
+    const Json& sw = os["sweep"];
+    brief["oneshot"] = Json{{"ranks", os["ranks"]}, {"mode", os["mode"]}, {"correct", os["correct"]},
+                            {"us_16B", sw.size() ? sw[0]["us"] : Json()},
+                            {"us_256KiB", sw.size() ? sw[sw.size() - 1]["us"] : Json()}};
+  }
+  if (g_result.has("allreduce")) {
+    // the in-pod RCCL smoke (BASELINE config 4): communicator, correctness and the sweep, compact
+    const Json& ar = g_result["allreduce"];
+    const Json& sw = ar["sweep"];
+    if (sw.size()) brief["allreduce_busbw_GBps_max"] = sw[sw.size() - 1]["busbw_GBps"];
+    auto r2 = [](const Json& v) { return Json(std::round(v.as_double() * 100.0) / 100.0); };
+    Json pts = Json::array();
+    for (const auto& p : sw.as_array())
+      pts.push_back(Json{{"bytes", p["bytes"]}, {"us", r2(p["us"])}, {"algbw_GBps", r2(p["algbw_GBps"])},
+                         {"busbw_GBps", r2(p["busbw_GBps"])}});
+    brief["allreduce"] = Json{{"devices", ar["devices"]}, {"comm_init_ms", r2(ar["comm_init_ms"])}, {"correct", ar["correct"]},
+                              {"sweep", pts}};
+    if (g_result.has("rccl_load_ms")) brief["rccl_load_ms"] = r2(g_result["rccl_load_ms"]);
+  }
+  return brief;
+}
+
+// the full report to stdout (or to the profile-mode parent's file), the brief to the termination log
+void write_report() {
   const std::string text = g_result.dump();
   const char* report_path = std::getenv("KFAMD_READINESS_REPORT");  // profile-mode child: to the parent
   FILE* rf = report_path ? std::fopen(report_path, "w") : nullptr;
@@ -1484,44 +1502,45 @@ int readiness_main(int argc, char** argv) {
     std::printf("%s\n", text.c_str());
   }
   if (const char* tl = std::getenv("KFAMD_TERMINATION_LOG")) {
-    // the termination message is capped at 4 KiB like Kubernetes'; keep the summary fields first
-    Json brief = Json{{"ok", g_result["ok"]}, {"gemm_tflops_aggregate", g_result["gemm_tflops_aggregate"]},
-                      {"hip_init_ms", g_result["hip_init_ms"]}, {"total_ms", g_result["total_ms"]}};
-    if (g_result.has("error")) brief["error"] = g_result["error"];
-    if (g_result.has("devices")) brief["devices"] = (long long)g_result["devices"].size();
-    if (g_result.has("simulated")) brief["simulated"] = true;
-    if (g_result.has("stages_ms")) brief["stages_ms"] = g_result["stages_ms"];
-    if (g_result.has("gemm") && g_result["gemm"].size() && g_result["gemm"][0].has("stages"))
-      brief["gemm0_stages_ms"] = g_result["gemm"][0]["stages"];
-    if (g_result.has("layernorm") && g_result["layernorm"].size()) brief["layernorm_GBps"] = g_result["layernorm"][0]["GBps"];
-    if (g_result.has("devices_wall_ms")) brief["devices_wall_ms"] = g_result["devices_wall_ms"];
-    if (g_result.has("warm_op")) brief["warm_op_ms"] = g_result["warm_op"]["warm_ms"];  // HIP came up before the pod
-    if (g_result.has("allreduce_oneshot") && g_result["allreduce_oneshot"].has("sweep")) {
-      const Json& os = g_result["allreduce_oneshot"];
-      const Json& sw = os["sweep"];
-      brief["oneshot"] = Json{{"ranks", os["ranks"]}, {"mode", os["mode"]}, {"correct", os["correct"]},
-                              {"us_16B", sw.size() ? sw[0]["us"] : Json()},
-                              {"us_256KiB", sw.size() ? sw[sw.size() - 1]["us"] : Json()}};
-    }
-    if (g_result.has("allreduce")) {
-      // the in-pod RCCL smoke (BASELINE config 4): communicator, correctness and the sweep, compact
-      const Json& ar = g_result["allreduce"];
-      const Json& sw = ar["sweep"];
-      if (sw.size()) brief["allreduce_busbw_GBps_max"] = sw[sw.size() - 1]["busbw_GBps"];
-      auto r2 = [](const Json& v) { return Json(std::round(v.as_double() * 100.0) / 100.0); };
-      Json pts = Json::array();
-      for (const auto& p : sw.as_array())
-        pts.push_back(Json{{"bytes", p["bytes"]}, {"us", r2(p["us"])}, {"algbw_GBps", r2(p["algbw_GBps"])},
-                           {"busbw_GBps", r2(p["busbw_GBps"])}});
-      brief["allreduce"] = Json{{"devices", ar["devices"]}, {"comm_init_ms", r2(ar["comm_init_ms"])}, {"correct", ar["correct"]},
-                                {"sweep", pts}};
-      if (g_result.has("rccl_load_ms")) brief["rccl_load_ms"] = r2(g_result["rccl_load_ms"]);
-    }
     if (FILE* f = std::fopen(tl, "w")) {
-      std::fputs(brief.dump().c_str(), f);
+      std::fputs(termination_brief().dump().c_str(), f);
       std::fclose(f);
     }
   }
+}
+
+int readiness_main(int argc, char** argv) {
+  ::signal(SIGSEGV, on_fatal);
+  ::signal(SIGBUS, on_fatal);
+  ::signal(SIGABRT, on_fatal);
+  ::signal(SIGFPE, on_fatal);
+  const Args a = parse_args(argc, argv);
+  preload_rccl(a);
+  auto t0 = std::chrono::steady_clock::now();
+  g_stage = "hip-init";
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  g_result["hip_init_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (!a.inject_fault.empty()) fail("injected fault at stage " + a.inject_fault + " (--inject-fault)");
+  const char* sim = std::getenv("KFAMD_SIMULATED_GPUS");
+  if (const char* vis = std::getenv("HIP_VISIBLE_DEVICES")) g_result["visible_devices"] = vis;
+  if ((e != hipSuccess || ndev == 0) && sim && std::string(sim) == "1") {
+    // node advertises synthetic GPUs (CPU CI): nothing to validate, report it as such
+    g_result["simulated"] = true;
+  } else if (e != hipSuccess || ndev == 0) {
+    fail(std::string("no GPU visible: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices"));
+  } else {
+    check_devices(a, ndev);
+  }
+  g_stage = "report";
+  g_error = first_error();
+  g_result["ok"] = g_error.empty();
+  if (!g_error.empty()) g_result["error"] = g_error;
+  g_result["total_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  g_result["kernels"] = kfamd_build_info();
+  g_result["t_main_unix_ms"] = g_t_main_ms;
+  g_result["t_report_unix_ms"] = realtime_ms();
+  write_report();
   const int rc = g_error.empty() ? 0 : 1;
   signal_sidecar(rc == 0);  // sidecar mode: the verdict goes out before the HIP / KFD teardown
   if (g_fast_exit) {
