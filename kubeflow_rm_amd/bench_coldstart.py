@@ -412,7 +412,9 @@ def measure_gpu_notebook_configs(gpus_per_notebook: int = 1, gpus: int | None = 
         rep = st.get("gpuReadiness") or {}
         ar = rep.get("allreduce") or {}
         sweep = ar.get("sweep") or []
-        out.update({"config4_readiness_args": rccl, "config4_gpus": st.get("gpus"), "config4_readiness_ok": rep.get("ok"),
+        ids = str(st.get("gpus") or "")
+        out.update({"config4_readiness_args": rccl, "config4_gpu_ids": ids, "config4_gpus": len([i for i in ids.split(",") if i]),
+                    "config4_readiness_ok": rep.get("ok"),
                     "config4_rccl_devices": ar.get("devices"), "config4_rccl_comm_init_ms": ar.get("comm_init_ms"),
                     "config4_rccl_correct": ar.get("correct"), "config4_rccl_load_ms": rep.get("rccl_load_ms"),
                     "config4_rccl_busbw_GBps": sweep[-1].get("busbw_GBps") if sweep else None,

@@ -11,7 +11,7 @@ def test_config4_and_5_on_one_eight_gpu_notebook():
     from kubeflow_rm_amd.bench_coldstart import measure_gpu_notebook_configs
     r = measure_gpu_notebook_configs(gpus_per_notebook=8, gpus=8, timeout=60)
     assert r["config4_readiness_args"] == "--rccl"
-    assert r["config4_gpus"] == "0,1,2,3,4,5,6,7" and r["config4_ready_s"] < 30
+    assert r["config4_gpu_ids"] == "0,1,2,3,4,5,6,7" and r["config4_gpus"] == 8 and r["config4_ready_s"] < 30
     assert r["config5_pvc"] == "cfg-nb-workspace"
     assert r["config5_coscheduled"] is True, r
     assert r["config5_tensorboard_ready_s"] < 30 and r["config5_pvcviewer_ready_s"] < 30
