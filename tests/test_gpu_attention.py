@@ -52,7 +52,7 @@ SHAPES = [
     (1, 2, 40, 128, True),   # shorter than one key tile and than one 128-row block
     (2, 1, 65, 64, False),   # one row / key past a tile
     # grids of >= 256 workgroups of 256 query rows: the one-workgroup-per-CU forward (attn_fwd_pp)
-    (4, 32, 512, 128, True),  # paired query blocks
+    (8, 32, 512, 128, True),  # paired query blocks
     (2, 64, 700, 128, True),  # an odd number of 256-row blocks (unpaired), partial tiles
     (4, 64, 1000, 128, False),
 ]
