@@ -191,6 +191,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_FWD_NW
 #define KFATT_FWD_NW 4  // forward workgroup: 4 waves (two workgroups per CU) or 8 (one; A/B runs)
 #endif
+#ifndef KFATT_DKDV_ABL
+#define KFATT_DKDV_ABL 0  // attn_bwd_dkdv8 timing ablations (tools/attn_ab.py builds; wrong results)
+#endif
 #ifndef KFATT_DQ_PAIR
 #define KFATT_DQ_PAIR 0  // the same for the dQ kernel (attn_bwd_dq_split PAIR)
 #endif
@@ -1138,7 +1141,7 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
   auto tile_body = [&](int it, auto BUFC) __attribute__((always_inline)) {
     constexpr int BUF = decltype(BUFC)::value;
     const int q0 = qstart + it * BQ;
-    if (it + 1 < ntiles) stage_dma(it + 1, 1 - BUF);
+    if ((KFATT_DKDV_ABL & 1) == 0 && it + 1 < ntiles) stage_dma(it + 1, 1 - BUF);  // ABL 1: no staging
     const char* qi = qtiles + BUF * 2 * QT + 32 * jh * D * 2;  // this wave's 32 query rows
     const char* oi = qi + QT;
     const float* nl_s = rowc + BUF * 2 * BQ + 32 * jh;
@@ -1161,8 +1164,9 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
       // S^T-free form as the 4-wave kernel: rows = this wave's queries, column = the lane's key
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        sacc = mfma32(lds_row(qi, koff[kk]), lds_row(kimg_w, koff[kk]), sacc);
-        dpacc = mfma32(lds_row(oi, koff[kk]), lds_row(vimg_w, koff[kk]), dpacc);
+        const int kr = (KFATT_DKDV_ABL & 4) ? 0 : kk;  // ABL 4: one K / V fragment read per tile (timing only)
+        sacc = mfma32(lds_row(qi, koff[kk]), lds_row(kimg_w, koff[kr]), sacc);
+        dpacc = mfma32(lds_row(oi, koff[kk]), lds_row(vimg_w, koff[kr]), dpacc);
       }
       uint32_t pf[2][4], sf[2][4];
 #pragma unroll
@@ -1191,7 +1195,7 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's pieces (the loop's only VMEM)
-    __syncthreads();
+    if ((KFATT_DKDV_ABL & 2) == 0) __syncthreads();       // ABL 2: no barrier (timing only)
   };
   for (int it = 0; it < ntiles; it += 2) {
     tile_body(it, std::integral_constant<int, 0>{});

@@ -47,6 +47,10 @@ def _variants():
         "fabl3": [*prod, "-DKFATT_FWD_ABL=3"],  # timing only: neither
         "pf1": [*prod, "-DKFATT_FWD_PF2=0"],  # attn_fwd_pp with K / V loads one tile ahead
         "nofence": [*prod, "-DKFATT_FWD_FENCE=0"],  # attn_fwd_pp without the phase fences
+        "babl1": [*prod, "-DKFATT_DKDV_ABL=1"],  # timing only: dK / dV kernel without Q / dO staging
+        "babl2": [*prod, "-DKFATT_DKDV_ABL=2"],  # timing only: ... without the per-tile barrier
+        "babl4": [*prod, "-DKFATT_DKDV_ABL=4"],  # timing only: ... one K / V fragment read per tile
+        "babl7": [*prod, "-DKFATT_DKDV_ABL=7"],  # timing only: all three
         "nopp": [*prod, "-DKFATT_FWD_PP=0"],  # forward by attn_fwd everywhere
     }
 
