@@ -15,7 +15,9 @@ bool starts(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
 std::optional<double> quantity_of(const Json& q) {
   if (q.is_number()) return q.as_double();
   if (!q.is_string()) return std::nullopt;
-  return parse_quantity(q.as_string());
+  const std::string& s = q.as_string();
+  if (s != trim(s)) return std::nullopt;  // resource.ParseQuantity takes no surrounding whitespace
+  return parse_quantity(s);
 }
 
 std::string field_invalid(const std::string& path, const std::string& value, const std::string& msg) {

@@ -62,9 +62,10 @@ def c(cluster):
     ({"amd.com/gpu": "2"}, {"amd.com/gpu": "1"}, 422, "must be equal to amd.com/gpu limit of 2"),
     (None, {"amd.com/gpu": "1"}, 422, "Limit must be set for non overcommitable resources"),
     ({"memory": "1 Gi"}, None, 400, "quantities must match"),
+    ({"amd.com/gpu": "1 "}, None, 400, "quantities must match"),
     ({"gpu": "1"}, None, 422, "must be a standard resource for containers"),
 ], ids=["two", "half", "one-and-half", "neg-gpu", "neg-cpu", "req-gt-lim", "ext-req-ne-lim", "ext-no-limit",
-        "space", "unqualified"])
+        "space", "trailing-space", "unqualified"])
 def test_invalid_pod_resources_are_rejected(c, limits, requests, status, msg):
     if not c.exists("v1", "Namespace", "val"):
         c.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "val"}})
