@@ -47,6 +47,9 @@ def _variants():
         "fabl3": [*prod, "-DKFATT_FWD_ABL=3"],  # timing only: neither
         "pf1": [*prod, "-DKFATT_FWD_PF2=0"],  # attn_fwd_pp with K / V loads one tile ahead
         "nofence": [*prod, "-DKFATT_FWD_FENCE=0"],  # attn_fwd_pp without the phase fences
+        "nowide": [*prod, "-DKFATT_FWD_WIDE=0"],  # attn_fwd_pp with 8-B O stores
+        "bnowide": [*prod, "-DKFATT_BWD_WIDE=0"],  # dQ / dK / dV with 8-B stores
+        "prio": [*prod, "-DKFATT_FWD_PRIO=1"],  # attn_fwd_pp with waves 4-7 at priority 1
         "babl1": [*prod, "-DKFATT_DKDV_ABL=1"],  # timing only: dK / dV kernel without Q / dO staging
         "babl2": [*prod, "-DKFATT_DKDV_ABL=2"],  # timing only: ... without the per-tile barrier
         "babl4": [*prod, "-DKFATT_DKDV_ABL=4"],  # timing only: ... one K / V fragment read per tile
