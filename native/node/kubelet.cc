@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
+#include <filesystem>
 #include <fstream>
 #include <functional>
 #include <optional>
@@ -783,38 +784,95 @@ void Kubelet::supervise_zygotes() {
 namespace {
 constexpr double kWarmOpRespawnS = 0.3;
 
-// librccl (~570 MB of fat binaries) read once into the page cache in the background: the first pod
-// that builds an RCCL communicator (kfamd-readiness --rccl, torch's nccl backend) then maps it from
-// memory instead of a cold disk (kfamd-readiness --rccl-single on a fresh box: communicator 5.7 s
-// cold, 1.7 s with the file cached; profiles/r6k_rccl_init)
-void prewarm_rccl_page_cache() {
-  std::thread([] {
-    const char* root = std::getenv("ROCM_PATH");
-    for (const std::string& path : {std::string(root ? root : "/opt/rocm") + "/lib/librccl.so.1",
-                                     std::string("/opt/rocm/lib/librccl.so.1")}) {
-      const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
-      if (fd < 0) continue;
-      ::posix_fadvise(fd, 0, 0, POSIX_FADV_WILLNEED);
-      std::vector<char> buf(1 << 20);
-      while (::read(fd, buf.data(), buf.size()) > 0) {
-      }
-      ::close(fd);
-      return;
-    }
-  }).detach();
+// The node's comgr seed: the first RCCL communicator in a process builds RCCL's device code through
+// comgr (~680 MB of cache entries, 3.8 s of the 5.5 s first `ncclCommInitAll` on MI355X; every later
+// process with that cache takes 1.7 s, profiles/r6k_rccl_init). Each namespace has its own cache
+// (container_env: tenants never share writable code objects), so each namespace's first RCCL pod
+// paid it. The kubelet builds the entries once per node with its own readiness op (a trusted binary,
+// a clean env, GPU 0, at low priority) into a node directory outside every pod, and a namespace's
+// cache starts as hard links to them (entries are content-hashed and only ever added or removed,
+// never rewritten in place).
+std::string comgr_seed_dir() {
+  if (const char* d = std::getenv("KFAMD_COMGR_SEED_DIR")) return d;
+  const char* xdg = std::getenv("XDG_CACHE_HOME");
+  const char* home = std::getenv("HOME");
+  const std::string base = xdg && *xdg ? xdg : std::string(home && *home ? home : "/tmp") + "/.cache";
+  return base + "/kfamd/comgr-seed";
 }
 }  // namespace
+
+void Kubelet::seed_comgr_cache() {
+  comgr_seed_ = comgr_seed_dir();
+  if (::access((comgr_seed_ + "/.complete").c_str(), F_OK) == 0) return;
+  // one build per host (several kubelets may share it, e.g. test clusters): a live kubelet's build
+  // in progress is left to finish; the leftovers of dead ones are removed
+  const std::filesystem::path seed(comgr_seed_);
+  const std::string prefix = seed.filename().string() + ".building-";
+  std::error_code ec;
+  for (const auto& e : std::filesystem::directory_iterator(seed.parent_path(), ec)) {
+    const std::string name = e.path().filename().string();
+    if (name.rfind(prefix, 0) != 0) continue;
+    const pid_t owner = static_cast<pid_t>(std::atol(name.c_str() + prefix.size()));
+    if (owner > 0 && (::kill(owner, 0) == 0 || errno == EPERM)) return;
+    std::filesystem::remove_all(e.path(), ec);
+  }
+  const std::string tmp = comgr_seed_ + ".building-" + std::to_string(::getpid());
+  std::filesystem::remove_all(tmp, ec);
+  make_dirs(tmp);
+  std::vector<std::string> env;
+  for (char** e = environ; *e; ++e) {
+    const std::string kv = *e, k = kv.substr(0, kv.find('='));
+    if (k == "PATH" || k == "LANG" || k == "LD_LIBRARY_PATH" || k == "TMPDIR" || k == "HOME" || starts_with(k, "HSA_") ||
+        starts_with(k, "ROCM"))
+      env.push_back(kv);
+  }
+  env.push_back("AMD_COMGR_CACHE_DIR=" + tmp);
+  env.push_back("ROCR_VISIBLE_DEVICES=0");
+  env.push_back("HIP_VISIBLE_DEVICES=0");
+  std::vector<std::string> argv = {cfg_.bin_dir + "/kfamd-readiness", "--rccl-single", "--skip-ln", "--iters", "1"};
+  if (::access("/usr/bin/nice", X_OK) == 0) argv.insert(argv.begin(), {"/usr/bin/nice", "-n", "10"});
+  std::string err;
+  seed_pid_ = spawn(argv, env, tmp, comgr_seed_ + ".log", &err);
+}
+
+// supervise tick: the seed build finished -> publish it (rename + marker); failures just leave none
+void Kubelet::finish_comgr_seed() {
+  if (seed_pid_ <= 0) return;
+  int st = 0;
+  if (::waitpid(seed_pid_, &st, WNOHANG) != seed_pid_) return;
+  seed_pid_ = -1;
+  const std::string tmp = comgr_seed_ + ".building-" + std::to_string(::getpid());
+  std::error_code ec;
+  if (WIFEXITED(st) && WEXITSTATUS(st) == 0 && ::access((comgr_seed_ + "/.complete").c_str(), F_OK) != 0) {
+    std::ofstream(tmp + "/.complete") << "1\n";
+    std::filesystem::remove_all(comgr_seed_, ec);  // an incomplete earlier attempt
+    std::filesystem::rename(tmp, comgr_seed_, ec);  // (another kubelet may have won: then ours goes)
+  }
+  std::filesystem::remove_all(tmp, ec);
+}
+
+// a namespace's new code-object cache starts as hard links to the node's seed entries
+void Kubelet::link_comgr_seed(const std::string& cache_dir) {
+  if (comgr_seed_.empty() || ::access((comgr_seed_ + "/.complete").c_str(), F_OK) != 0) return;
+  std::error_code ec;
+  for (const auto& e : std::filesystem::directory_iterator(comgr_seed_, ec)) {
+    const std::string name = e.path().filename().string();
+    if (name.rfind("llvmcache-", 0) != 0) continue;
+    ::chmod(e.path().c_str(), 0444);
+    (void)::link(e.path().c_str(), (cache_dir + "/" + name).c_str());
+  }
+}
 
 void Kubelet::start_warm_ops() {
   const std::string bin = cfg_.bin_dir + "/kfamd-readiness";
   if (!cfg_.pod_warm_gpus || alloc_->topology().source == "synthetic" || alloc_->topology().size() == 0 ||
       ::access("/dev/kfd", R_OK | W_OK) != 0 || ::access(bin.c_str(), X_OK) != 0)
     return;
-  prewarm_rccl_page_cache();
   warm_dir_ = cfg_.root_dir + "/warm-readiness";
   make_dirs(warm_dir_);
   ::chmod(warm_dir_.c_str(), 0700);
   std::lock_guard<std::mutex> g(wo_mu_);
+  seed_comgr_cache();
   for (int d = 0; d < alloc_->topology().size(); ++d) {
     WarmOp w;
     w.dev = d;
@@ -824,6 +882,7 @@ void Kubelet::start_warm_ops() {
 
 void Kubelet::supervise_warm_ops() {
   std::lock_guard<std::mutex> g(wo_mu_);
+  finish_comgr_seed();
   const double now = now_seconds();
   for (auto& w : warm_ops_) {
     if (w.pid > 0) {
@@ -1456,7 +1515,10 @@ void Kubelet::container_env(const PodSync& s, const Json& c, std::vector<std::st
     // Keyed per namespace: profiles are tenants, and a cache one tenant can write must never
     // feed code objects to another tenant's pods (a namespace's own pods share its warm cache).
     const std::string cache = cfg_.root_dir + "/gpu-cache/comgr/" + r.ns;
-    make_dirs(cache);
+    if (::access(cache.c_str(), F_OK) != 0) {
+      make_dirs(cache);
+      link_comgr_seed(cache);
+    }
     set("AMD_COMGR_CACHE_DIR", cache);
   }
   for (const auto& ef : c["envFrom"].as_array()) {

@@ -234,8 +234,15 @@ class Kubelet {
   };
   std::vector<WarmOp> warm_ops_;
   std::mutex wo_mu_;
+  // the node's trusted comgr seed (seed_comgr_cache): RCCL's device-code builds made once by the
+  // kubelet's own readiness op, hard-linked into each namespace's new code-object cache
+  std::string comgr_seed_;
+  pid_t seed_pid_ = -1;
   std::string warm_dir_;  // set once in start() before any pod is admitted
   void start_warm_ops();
+  void seed_comgr_cache();
+  void finish_comgr_seed();
+  void link_comgr_seed(const std::string& cache_dir);
   void supervise_warm_ops();
   void stop_warm_ops();
   void supervise_zygotes();  // heartbeat thread: restart a zygote that exited
