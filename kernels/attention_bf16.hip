@@ -197,6 +197,9 @@ __device__ __forceinline__ u32x4 gload16(const __bf16* p) { return *reinterpret_
 #ifndef KFATT_DQ_PAIR
 #define KFATT_DQ_PAIR 0  // the same for the dQ kernel (attn_bwd_dq_split PAIR)
 #endif
+#ifndef KFATT_FWD_WIDE
+#define KFATT_FWD_WIDE 1  // the forwards store O in whole 16-B rows per lane (store_rows16, T21)
+#endif
 #ifndef KFATT_FWD_DMA
 #define KFATT_FWD_DMA 0  // forward K / V tiles by LDS-DMA (attn_fwd stage_dma)
 #endif
@@ -510,8 +513,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
   // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh
   const float lt = kfw::sum_halves(l);
   const float inv = 1.f / lt;
-  if (qrow < T) {
-    __bf16* ob = o + base_off(a, TO, b, h) + qrow * a.s[TO][2];
+  __bf16* ob = o + base_off(a, TO, b, h) + qrow * a.s[TO][2];
+  if constexpr (KFATT_FWD_WIDE) {
+    store_rows16<ND>(ob, oacc, inv, qrow < T, hh);
+  } else if (qrow < T) {
 #pragma unroll
     for (int n = 0; n < ND; ++n) {
 #pragma unroll
@@ -521,8 +526,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
         *reinterpret_cast<u32x2*>(ob + 32 * n + 8 * g + 4 * hh) = v2;
       }
     }
-    if (hh == 0) lse[((long long)b * a.H + h) * T + qrow] = m * a.scale + logf(lt);
   }
+  if (qrow < T && hh == 0) lse[((long long)b * a.H + h) * T + qrow] = m * a.scale + logf(lt);
   }  // pass
 }
 
@@ -556,9 +561,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
   } while (0)
 #ifndef KFATT_FWD_PF2
 #define KFATT_FWD_PF2 1  // K / V loads two tiles ahead (four-tile ring)
-#endif
-#ifndef KFATT_FWD_WIDE
-#define KFATT_FWD_WIDE 1  // attn_fwd_pp stores O in whole 16-B rows per lane (T21)
 #endif
 #ifndef KFATT_BWD_WIDE
 #define KFATT_BWD_WIDE 1  // dQ / dK / dV in whole 16-B rows per lane (store_rows16)
