@@ -568,6 +568,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
 #ifndef KFATT_FWD_PRIO
 #define KFATT_FWD_PRIO 0  // attn_fwd_pp: static priority 1 for waves 4-7 (A/B knob)
 #endif
+#ifndef KFATT_FWD_PXP
+#define KFATT_FWD_PXP 1  // attn_fwd_pp pairs: the light block's prologue loads issued under the heavy block's epilogue
+#endif
 #ifndef KFATT_FWD_ABL
 #define KFATT_FWD_ABL 0  // timing ablations of attn_fwd_pp (tools/attn_ab.py; wrong results)
 #endif
@@ -699,6 +702,39 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
     }
   };
 
+  bf16x8 qf[KS];
+  auto load_q = [&](int qr) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      u32x4 x = {0u, 0u, 0u, 0u};
+      if (qr < T) x = gload16(qb + qr * qt + kk * 16 + 8 * hh);
+      qf[kk] = __builtin_bit_cast(bf16x8, x);
+    }
+  };
+  // KFATT_FWD_PF2 staging: two register sets, tile j + 2 issued at tile j (see the tile loop)
+  u32x4 kr2[NCH], vr2[NCH];
+  auto ld = [&](int tile, u32x4 (&kr)[NCH], u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + NT * i, row = cc / CH, ch = cc % CH;
+      kr[i] = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * tile * FK * (int)kt);
+      vr[i] = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * tile * FK * (int)vt);
+    }
+  };
+  auto st = [&](int slot, const u32x4 (&kr)[NCH], const u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int cc = tid + NT * i;
+      const int off = img_off<D>(cc / CH, cc % CH);
+      *reinterpret_cast<u32x4*>(smem + slot * TILE + off) = kr[i];
+      *reinterpret_cast<u32x4*>(smem + VBASE + slot * TILE + off) = vr[i];
+    }
+  };
+  // KFATT_FWD_PXP (pairs): the light block's Q and first two K / V tiles are issued when the heavy
+  // block's tile loop ends, so their latency hides under its epilogue instead of stalling a second
+  // prologue
+  constexpr bool PXP = KFATT_FWD_PXP && KFATT_FWD_PF2 && PAIR;
+
 #pragma unroll 1
   for (int pass = 0; pass < (PAIR ? 2 : 1); ++pass) {
     if (PAIR && pass) __syncthreads();  // the first block's last reads are done before the LDS is refilled
@@ -706,14 +742,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
     const int q0 = qblk * FQW, qw = q0 + 32 * wu, qrow = qw + r;
     const int ntiles = CAUSAL ? min(nta, (q0 + FQW) / FK) : nta;
     const int jl = CAUSAL ? min(ntiles - 1, (qw + 31) / FK) : ntiles - 1;  // this wave's last tile
+    const bool pre = PXP && pass == 1;  // Q and tiles 0 / 1 already in flight
 
-    bf16x8 qf[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      u32x4 x = {0u, 0u, 0u, 0u};
-      if (qrow < T) x = gload16(qb + qrow * qt + kk * 16 + 8 * hh);
-      qf[kk] = __builtin_bit_cast(bf16x8, x);
-    }
+    if (!pre) load_q(qrow);
     f32x16 oacc[ND], S[2][2];
 #pragma unroll
     for (int n = 0; n < ND; ++n) oacc[n] = (f32x16){};
@@ -725,27 +756,9 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
       // K / V two tiles ahead: tile j + 2's loads are issued at tile j into the register set tile j
       // used (written at tile j - 1), and tile j + 1's set is written at the end of tile j into the
       // slot of tile j - 3 (a four-tile ring: slot and set compile-time in the 4x unrolled loop)
-      u32x4 kr2[NCH], vr2[NCH];
-      auto ld = [&](int tile, u32x4 (&kr)[NCH], u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int cc = tid + NT * i, row = cc / CH, ch = cc % CH;
-          kr[i] = bload16(rk, 2 * (row * (int)kt + ch * 8), 2 * tile * FK * (int)kt);
-          vr[i] = bload16(rv, 2 * (row * (int)vt + ch * 8), 2 * tile * FK * (int)vt);
-        }
-      };
-      auto st = [&](int slot, const u32x4 (&kr)[NCH], const u32x4 (&vr)[NCH]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int cc = tid + NT * i;
-          const int off = img_off<D>(cc / CH, cc % CH);
-          *reinterpret_cast<u32x4*>(smem + slot * TILE + off) = kr[i];
-          *reinterpret_cast<u32x4*>(smem + VBASE + slot * TILE + off) = vr[i];
-        }
-      };
-      ld(0, kreg, vreg);
+      if (!pre) ld(0, kreg, vreg);
       st(0, kreg, vreg);
-      if (1 < ntiles) ld(1, kr2, vr2);
+      if (!pre && 1 < ntiles) ld(1, kr2, vr2);
       __syncthreads();
       auto tile = [&](int j, auto SLC) __attribute__((always_inline)) {
         constexpr int SL = decltype(SLC)::value;  // j % 4; register set j & 1
@@ -808,6 +821,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
       }
       if (j < ntiles) tile(j, std::integral_constant<int, 0>{});
       if (j + 1 < ntiles) tile(j + 1, std::integral_constant<int, 1>{});
+    }
+
+    if (PXP && pass == 0) {  // the light block's Q and first K / V tiles, under this epilogue
+      const int q0n = bo.rank * FQW;
+      load_q(q0n + 32 * wu + r);
+      ld(0, kreg, vreg);
+      if (1 < (CAUSAL ? min(nta, (q0n + FQW) / FK) : nta)) ld(1, kr2, vr2);
     }
 
     // epilogue: lane (r, hh) holds row qrow, d = 32 n + (e & 3) + 8 (e >> 2) + 4 hh

@@ -49,6 +49,7 @@ def _variants():
         "nofence": [*prod, "-DKFATT_FWD_FENCE=0"],  # attn_fwd_pp without the phase fences
         "nowide": [*prod, "-DKFATT_FWD_WIDE=0"],  # attn_fwd_pp with 8-B O stores
         "bnowide": [*prod, "-DKFATT_BWD_WIDE=0"],  # dQ / dK / dV with 8-B stores
+        "nopxp": [*prod, "-DKFATT_FWD_PXP=0"],  # attn_fwd_pp pairs without the cross-pass prefetch
         "prio": [*prod, "-DKFATT_FWD_PRIO=1"],  # attn_fwd_pp with waves 4-7 at priority 1
         "babl1": [*prod, "-DKFATT_DKDV_ABL=1"],  # timing only: dK / dV kernel without Q / dO staging
         "babl2": [*prod, "-DKFATT_DKDV_ABL=2"],  # timing only: ... without the per-tile barrier
