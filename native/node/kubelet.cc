@@ -809,13 +809,16 @@ void Kubelet::seed_comgr_cache() {
   const std::filesystem::path seed(comgr_seed_);
   const std::string prefix = seed.filename().string() + ".building-";
   std::error_code ec;
-  for (const auto& e : std::filesystem::directory_iterator(seed.parent_path(), ec)) {
-    const std::string name = e.path().filename().string();
+  std::vector<std::filesystem::path> stale;
+  for (std::filesystem::directory_iterator it(seed.parent_path(), ec), end; !ec && it != end; it.increment(ec)) {
+    const std::string name = it->path().filename().string();
     if (name.rfind(prefix, 0) != 0) continue;
     const pid_t owner = static_cast<pid_t>(std::atol(name.c_str() + prefix.size()));
     if (owner > 0 && (::kill(owner, 0) == 0 || errno == EPERM)) return;
-    std::filesystem::remove_all(e.path(), ec);
+    stale.push_back(it->path());
   }
+  for (const auto& d : stale) std::filesystem::remove_all(d, ec);
+  ec.clear();
   const std::string tmp = comgr_seed_ + ".building-" + std::to_string(::getpid());
   std::filesystem::remove_all(tmp, ec);
   make_dirs(tmp);
@@ -855,11 +858,11 @@ void Kubelet::finish_comgr_seed() {
 void Kubelet::link_comgr_seed(const std::string& cache_dir) {
   if (comgr_seed_.empty() || ::access((comgr_seed_ + "/.complete").c_str(), F_OK) != 0) return;
   std::error_code ec;
-  for (const auto& e : std::filesystem::directory_iterator(comgr_seed_, ec)) {
-    const std::string name = e.path().filename().string();
+  for (std::filesystem::directory_iterator it(comgr_seed_, ec), end; !ec && it != end; it.increment(ec)) {
+    const std::string name = it->path().filename().string();
     if (name.rfind("llvmcache-", 0) != 0) continue;
-    ::chmod(e.path().c_str(), 0444);
-    (void)::link(e.path().c_str(), (cache_dir + "/" + name).c_str());
+    ::chmod(it->path().c_str(), 0444);
+    (void)::link(it->path().c_str(), (cache_dir + "/" + name).c_str());
   }
 }
 
