@@ -802,7 +802,6 @@ std::string comgr_seed_dir() {
 }  // namespace
 
 void Kubelet::seed_comgr_cache() {
-  comgr_seed_ = comgr_seed_dir();
   if (::access((comgr_seed_ + "/.complete").c_str(), F_OK) == 0) return;
   // one build per host (several kubelets may share it, e.g. test clusters): a live kubelet's build
   // in progress is left to finish; the leftovers of dead ones are removed
@@ -867,6 +866,7 @@ void Kubelet::link_comgr_seed(const std::string& cache_dir) {
 }
 
 void Kubelet::start_warm_ops() {
+  comgr_seed_ = comgr_seed_dir();  // namespaces' new caches link a completed seed on any node
   const std::string bin = cfg_.bin_dir + "/kfamd-readiness";
   if (!cfg_.pod_warm_gpus || alloc_->topology().source == "synthetic" || alloc_->topology().size() == 0 ||
       ::access("/dev/kfd", R_OK | W_OK) != 0 || ::access(bin.c_str(), X_OK) != 0)
