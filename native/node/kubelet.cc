@@ -184,7 +184,12 @@ struct Kubelet::PodRuntime {
   std::mutex op_mu;
 };
 
+namespace {
+std::string comgr_seed_dir();
+}  // namespace
+
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)), cfg_(std::move(cfg)) {
+  comgr_seed_ = comgr_seed_dir();  // set before any thread: pod workers read it (link_comgr_seed)
   GpuTopology topo = cfg_.gpus >= 0            ? GpuTopology::synthetic(cfg_.gpus)
                      : !cfg_.sysfs_root.empty() ? GpuTopology::discover(SysfsRoots::under(cfg_.sysfs_root))
                                                 : GpuTopology::discover();
@@ -866,7 +871,6 @@ void Kubelet::link_comgr_seed(const std::string& cache_dir) {
 }
 
 void Kubelet::start_warm_ops() {
-  comgr_seed_ = comgr_seed_dir();  // namespaces' new caches link a completed seed on any node
   const std::string bin = cfg_.bin_dir + "/kfamd-readiness";
   if (!cfg_.pod_warm_gpus || alloc_->topology().source == "synthetic" || alloc_->topology().size() == 0 ||
       ::access("/dev/kfd", R_OK | W_OK) != 0 || ::access(bin.c_str(), X_OK) != 0)
