@@ -574,6 +574,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
 #ifndef KFATT_FWD_ABL
 #define KFATT_FWD_ABL 0  // timing ablations of attn_fwd_pp (tools/attn_ab.py; wrong results)
 #endif
+#ifndef KFATT_FWD_RA
+#define KFATT_FWD_RA 2  // attn_fwd_pp: LDS reads pinned this many MFMAs ahead of their use (0: compiler order)
+#endif
+#ifndef KFATT_DQ_RA
+#define KFATT_DQ_RA 0  // attn_bwd_dq_split (D = 128): LDS reads pinned this many MFMAs ahead (0: compiler order)
+#endif
+#ifndef KFATT_BWD_RA
+#define KFATT_BWD_RA 0  // attn_bwd_dkdv8: LDS reads pinned this many MFMAs ahead (0: compiler order)
+#endif
+#ifndef KFATT_FWD_SPLIT
+#define KFATT_FWD_SPLIT 0  // attn_fwd_pp softmax: row max and row sum as 4 independent chains
+#endif
 
 template <int D, bool CAUSAL, bool PAIR>
 __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -641,12 +653,60 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
   auto qk = [&](const char* kimg, const bf16x8 (&qf)[KS], f32x16 (&s)[2]) __attribute__((always_inline)) {
     s[0] = (f32x16){};
     s[1] = (f32x16){};
+    if constexpr (KFATT_FWD_RA > 0) {
+      // KFATT_FWD_RA: the K fragment of MFMA i + RA is read before MFMA i issues (RA b128 reads in
+      // flight), the order pinned by sched groups, so one LDS latency is paid per phase, not per k-step
+      constexpr int RA = KFATT_FWD_RA, NM = 2 * KS;
+      bf16x8 kf[NM];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
+      for (int i = 0; i < NM; ++i) {
+        if (i == 0)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) s[t] = mfma32(lds_row(kimg + 32 * t * D * 2, koff[kk]), qf[kk], s[t]);
+          for (int u = 0; u < RA; ++u) kf[u] = lds_row(kimg + 32 * (u & 1) * D * 2, koff[u >> 1]);
+        if (i + RA < NM) kf[i + RA] = lds_row(kimg + 32 * ((i + RA) & 1) * D * 2, koff[(i + RA) >> 1]);
+        s[i & 1] = mfma32(kf[i], qf[i >> 1], s[i & 1]);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) s[t] = mfma32(lds_row(kimg + 32 * t * D * 2, koff[kk]), qf[kk], s[t]);
+    }
   };
   auto pv = [&](const char* vimg, const uint32_t (&pf)[2][2][4], f32x16 (&oa)[ND]) __attribute__((always_inline)) {
+    if constexpr (KFATT_FWD_RA > 0) {
+      // as qk: the two transposed V reads of MFMA i + RA issued before MFMA i
+      constexpr int RA = KFATT_FWD_RA, NM = 4 * ND;  // MFMA i: n = i / 4, t = (i / 2) & 1, s2 = i & 1
+      auto rd = [&](int i) __attribute__((always_inline)) {
+        const int n = i >> 2, t = (i >> 1) & 1, s2 = i & 1;
+        return join(tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff0[n]),
+                    tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff1[n]));
+      };
+      bf16x8 vf[NM];
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i == 0)
+#pragma unroll
+          for (int u = 0; u < RA; ++u) vf[u] = rd(u);
+        if (i + RA < NM) vf[i + RA] = rd(i + RA);
+        const int t = (i >> 1) & 1, s2 = i & 1;
+        const u32x4 pw = {pf[t][s2][0], pf[t][s2][1], pf[t][s2][2], pf[t][s2][3]};
+        oa[i >> 2] = mfma32(vf[i], __builtin_bit_cast(bf16x8, pw), oa[i >> 2]);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int n = 0; n < ND; ++n)
 #pragma unroll
@@ -675,26 +735,36 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
   auto softmax = [&](const f32x16 (&s)[2], float& m, float& l, uint32_t (&pf)[2][2][4], f32x16 (&oa)[ND])
                      __attribute__((always_inline)) {
     float mx = -INFINITY;
+    if constexpr (KFATT_FWD_SPLIT) {
+      float mp[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[t][e]);
+        for (int e = 0; e < 16; ++e) mp[e & 3] = fmaxf(mp[e & 3], s[t][e]);
+      mx = fmaxf(fmaxf(mp[0], mp[1]), fmaxf(mp[2], mp[3]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, s[t][e]);
+    }
     mx = kfw::max_halves(mx);
     const bool move = (mx - m) * c > THR;  // m = -inf on the first tile: moves
     const float mn = move ? mx : m;
     const float alpha = move ? fast_exp2((m - mn) * c) : 1.f;
     m = mn;
     const float mc = mn * c;
-    float rs = 0.f;
+    float rp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; e += 2) {
         const float p0 = fast_exp2(fmaf(s[t][e], c, -mc));
         const float p1 = fast_exp2(fmaf(s[t][e + 1], c, -mc));
-        rs += p0 + p1;
+        rp[KFATT_FWD_SPLIT ? (e >> 1) & 3 : 0] += p0 + p1;
         pf[t][e >> 3][(e & 7) >> 1] = pack2(p0, p1);
       }
+    const float rs = KFATT_FWD_SPLIT ? (rp[0] + rp[1]) + (rp[2] + rp[3]) : rp[0];
     l = l * alpha + rs;
     if (__builtin_amdgcn_ballot_w64(move) != 0) {
 #pragma unroll
@@ -1014,6 +1084,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
     const char* vimg = kimg + TILE;
     if (!(CAUSAL && k0 > qw + 31)) {
       f32x16 sacc[2] = {(f32x16){}, (f32x16){}}, dpacc[2] = {(f32x16){}, (f32x16){}};
+      if constexpr (KFATT_DQ_RA > 0 && D == 128) {
+        // KFATT_DQ_RA: the K / V fragment of MFMA i + RA read before MFMA i issues (as attn_fwd_pp);
+        // MFMA i: k-step i / 4, t = (i / 2) & 1, S for even i, dP for odd
+        constexpr int RA = KFATT_DQ_RA, NM = 4 * KS;
+        bf16x8 fa[NM];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+          fa[i] = lds_row(((i & 1) ? vimg : kimg) + 32 * ((i >> 1) & 1) * D * 2, koff[i >> 2]);
+        };
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i == 0)
+#pragma unroll
+            for (int u = 0; u < RA; ++u) rd(u);
+          if (i + RA < NM) rd(i + RA);
+          const int t = (i >> 1) & 1;
+          if (i & 1) dpacc[t] = mfma32(fa[i], dof[i >> 2], dpacc[t]);
+          else sacc[t] = mfma32(fa[i], qf[i >> 2], sacc[t]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      } else
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
@@ -1037,6 +1132,30 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_split(const __bf16* __rest
           sf[t][e >> 3][(e & 7) >> 1] = pack2(p0 * (dpacc[t][e] + nd_q), p1 * (dpacc[t][e + 1] + nd_q));
         }
       }
+      if constexpr (KFATT_DQ_RA > 0 && D == 128) {
+        constexpr int RA = KFATT_DQ_RA, NM = 4 * ND;  // MFMA i: n = i / 4, t = (i / 2) & 1, s2 = i & 1
+        bf16x8 fk[NM];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+          const char* base = kimg + (32 * ((i >> 1) & 1) + 16 * (i & 1)) * D * 2;
+          fk[i] = join(tr_read(base, voff0[i >> 2]), tr_read(base, voff1[i >> 2]));
+        };
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i == 0)
+#pragma unroll
+            for (int u = 0; u < RA; ++u) rd(u);
+          if (i + RA < NM) rd(i + RA);
+          const int t = (i >> 1) & 1, s2 = i & 1;
+          const u32x4 sw = {sf[t][s2][0], sf[t][s2][1], sf[t][s2][2], sf[t][s2][3]};
+          dqacc[i >> 2] = mfma32(fk[i], __builtin_bit_cast(bf16x8, sw), dqacc[i >> 2]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      } else
 #pragma unroll
       for (int n = 0; n < ND; ++n) {
 #pragma unroll
@@ -1226,11 +1345,37 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
         }
       }
       // S^T-free form as the 4-wave kernel: rows = this wave's queries, column = the lane's key
+      if constexpr (KFATT_BWD_RA > 0 && D == 128) {
+        // KFATT_BWD_RA: both operands of MFMA i + RA read before MFMA i issues, pinned by sched
+        // groups (MFMA i: k-step i / 2, S for even i, dP for odd)
+        constexpr int RA = KFATT_BWD_RA, NM = 2 * KS;
+        bf16x8 fa[NM], fb[NM];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+          fa[i] = lds_row((i & 1) ? oi : qi, koff[i >> 1]);
+          fb[i] = lds_row((i & 1) ? vimg_w : kimg_w, koff[i >> 1]);
+        };
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int kr = (KFATT_DKDV_ABL & 4) ? 0 : kk;  // ABL 4: one K / V fragment read per tile (timing only)
-        sacc = mfma32(lds_row(qi, koff[kk]), lds_row(kimg_w, koff[kr]), sacc);
-        dpacc = mfma32(lds_row(oi, koff[kk]), lds_row(vimg_w, koff[kr]), dpacc);
+        for (int i = 0; i < NM; ++i) {
+          if (i == 0)
+#pragma unroll
+            for (int u = 0; u < RA; ++u) rd(u);
+          if (i + RA < NM) rd(i + RA);
+          if (i & 1) dpacc = mfma32(fa[i], fb[i], dpacc);
+          else sacc = mfma32(fa[i], fb[i], sacc);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int kr = (KFATT_DKDV_ABL & 4) ? 0 : kk;  // ABL 4: one K / V fragment read per tile (timing only)
+          sacc = mfma32(lds_row(qi, koff[kk]), lds_row(kimg_w, koff[kr]), sacc);
+          dpacc = mfma32(lds_row(oi, koff[kk]), lds_row(vimg_w, koff[kr]), dpacc);
+        }
       }
       uint32_t pf[2][4], sf[2][4];
 #pragma unroll
@@ -1245,6 +1390,35 @@ __global__ __launch_bounds__(512, D == 64 ? 2 : 1) void attn_bwd_dkdv8(const __b
         sf[e >> 3][(e & 7) >> 1] = pack2(p0 * dpacc[e], p1 * dpacc[e + 1]);
       }
       // dV^T += dO^T . P and dK^T += Q^T . dS over this half's rows (permuted k order)
+      if constexpr (KFATT_BWD_RA > 0 && D == 128) {
+        constexpr int RA = 2 * KFATT_BWD_RA, NM = 4 * ND;  // MFMA i: n = i / 4, sx = (i / 2) & 1, dV for even i
+        bf16x8 fa[NM];
+        auto rd = [&](int i) __attribute__((always_inline)) {
+          const char* base = ((i & 1) ? qi : oi) + 16 * ((i >> 1) & 1) * D * 2;
+          fa[i] = join(tr_read(base, voff0[i >> 2]), tr_read(base, voff1[i >> 2]));
+        };
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i == 0)
+#pragma unroll
+            for (int u = 0; u < RA; ++u) rd(u);
+          if (i + RA < NM) rd(i + RA);
+          const int sx = (i >> 1) & 1, n = i >> 2;
+          if (i & 1) {
+            const u32x4 sw = {sf[sx][0], sf[sx][1], sf[sx][2], sf[sx][3]};
+            dkacc[n] = mfma32(fa[i], __builtin_bit_cast(bf16x8, sw), dkacc[n]);
+          } else {
+            const u32x4 pw = {pf[sx][0], pf[sx][1], pf[sx][2], pf[sx][3]};
+            dvacc[n] = mfma32(fa[i], __builtin_bit_cast(bf16x8, pw), dvacc[n]);
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      } else
 #pragma unroll
       for (int n = 0; n < ND; ++n) {
 #pragma unroll

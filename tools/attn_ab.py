@@ -56,6 +56,15 @@ def _variants():
         "babl4": [*prod, "-DKFATT_DKDV_ABL=4"],  # timing only: ... one K / V fragment read per tile
         "babl7": [*prod, "-DKFATT_DKDV_ABL=7"],  # timing only: all three
         "nopp": [*prod, "-DKFATT_FWD_PP=0"],  # forward by attn_fwd everywhere
+        "ra4": [*prod, "-DKFATT_FWD_RA=4"],  # attn_fwd_pp: LDS reads pinned 4 MFMAs ahead (r6v_ra)
+        "split": [*prod, "-DKFATT_FWD_SPLIT=1"],  # attn_fwd_pp softmax max / sum as 4 chains
+        "fra0": [*prod, "-DKFATT_FWD_RA=0"],  # attn_fwd_pp reads in the compiler's order
+        "fra1": [*prod, "-DKFATT_FWD_RA=1"],
+        "fra3": [*prod, "-DKFATT_FWD_RA=3"],
+        "dra1": [*prod, "-DKFATT_DQ_RA=1"],  # attn_bwd_dq_split (D = 128): reads pinned 1 MFMA ahead
+        "dra2": [*prod, "-DKFATT_DQ_RA=2"],
+        "bra1": [*prod, "-DKFATT_BWD_RA=1"],  # attn_bwd_dkdv8 (D = 128): reads pinned 1 MFMA ahead
+        "bra2": [*prod, "-DKFATT_BWD_RA=2"],  # ... 2 MFMAs ahead
     }
 
 
