@@ -288,6 +288,64 @@ constexpr int FQ = 128, FK = 64;
 
 // PAIR (causal, an even number of query blocks, KFATT_FWD_PAIR): one workgroup runs query blocks
 // nq - 1 - i and i one after the other, nq + 1 key tiles for every workgroup, half the grid
+// The forwards' two MFMA phases with every LDS operand read RA MFMAs ahead of its use, the order
+// pinned by sched groups (KFATT_FWD_RA, profiles/r6v_ra): the compiler's own order read each
+// fragment one or two MFMAs early and waited on it there, so a wave paid an LDS round trip per
+// k-step. S^T = K Q^T: MFMA i is k-step i / 2, key half t = i & 1.
+template <int D, int RA>
+__device__ __forceinline__ void qk_ra(const char* kimg, const int (&koff)[D / 16], const bf16x8 (&qf)[D / 16],
+                                      f32x16 (&s)[2]) {
+  constexpr int NM = D / 8;
+  bf16x8 kf[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i == 0)
+#pragma unroll
+      for (int u = 0; u < RA; ++u) kf[u] = lds_row(kimg + 32 * (u & 1) * D * 2, koff[u >> 1]);
+    if (i + RA < NM) kf[i + RA] = lds_row(kimg + 32 * ((i + RA) & 1) * D * 2, koff[(i + RA) >> 1]);
+    s[i & 1] = mfma32(kf[i], qf[i >> 1], s[i & 1]);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);  // DS reads
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+  }
+}
+
+// O += P V: MFMA i is d tile n = i / 4, key half t = (i / 2) & 1, 16-key step s2 = i & 1, its A
+// operand two transposed V reads
+template <int D, int RA>
+__device__ __forceinline__ void pv_ra(const char* vimg, const int (&voff0)[D / 32], const int (&voff1)[D / 32],
+                                      const uint32_t (&pf)[2][2][4], f32x16 (&oa)[D / 32]) {
+  constexpr int NM = D / 8;
+  auto rd = [&](int i) __attribute__((always_inline)) {
+    const char* base = vimg + (32 * ((i >> 1) & 1) + 16 * (i & 1)) * D * 2;
+    return join(tr_read(base, voff0[i >> 2]), tr_read(base, voff1[i >> 2]));
+  };
+  bf16x8 vf[NM];
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i == 0)
+#pragma unroll
+      for (int u = 0; u < RA; ++u) vf[u] = rd(u);
+    if (i + RA < NM) vf[i + RA] = rd(i + RA);
+    const int t = (i >> 1) & 1, s2 = i & 1;
+    const u32x4 pw = {pf[t][s2][0], pf[t][s2][1], pf[t][s2][2], pf[t][s2][3]};
+    oa[i >> 2] = mfma32(vf[i], __builtin_bit_cast(bf16x8, pw), oa[i >> 2]);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  }
+}
+
+#ifndef KFATT_FWD4_RA
+#define KFATT_FWD4_RA 2  // attn_fwd (4 waves; D = 64 and small grids): KFATT_FWD_RA's pinned reads
+#endif
+
 template <int D, bool CAUSAL, bool PAIR = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                    const __bf16* __restrict__ v, __bf16* __restrict__ o,
@@ -431,6 +489,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
     // a wave whose 32 rows all precede the tile's first key has nothing to do (causal)
     if (!(CAUSAL && k0 > qw + 31)) {
       f32x16 sacc[2] = {(f32x16){}, (f32x16){}};
+      if constexpr (KFATT_FWD4_RA > 0 && KFATT_FWD_OFFS) qk_ra<D, KFATT_FWD4_RA>(kimg, koff, qf, sacc);
+      else
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
@@ -484,6 +544,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd(const __bf1
       } else {
         l += rs;
       }
+      if constexpr (KFATT_FWD4_RA > 0 && KFATT_FWD_OFFS) pv_ra<D, KFATT_FWD4_RA>(vimg, voff0, voff1, pf, oacc);
+      else
 #pragma unroll
       for (int n = 0; n < ND; ++n) {
 #pragma unroll
@@ -654,24 +716,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
     s[0] = (f32x16){};
     s[1] = (f32x16){};
     if constexpr (KFATT_FWD_RA > 0) {
-      // KFATT_FWD_RA: the K fragment of MFMA i + RA is read before MFMA i issues (RA b128 reads in
-      // flight), the order pinned by sched groups, so one LDS latency is paid per phase, not per k-step
-      constexpr int RA = KFATT_FWD_RA, NM = 2 * KS;
-      bf16x8 kf[NM];
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        if (i == 0)
-#pragma unroll
-          for (int u = 0; u < RA; ++u) kf[u] = lds_row(kimg + 32 * (u & 1) * D * 2, koff[u >> 1]);
-        if (i + RA < NM) kf[i + RA] = lds_row(kimg + 32 * ((i + RA) & 1) * D * 2, koff[(i + RA) >> 1]);
-        s[i & 1] = mfma32(kf[i], qf[i >> 1], s[i & 1]);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
+      qk_ra<D, KFATT_FWD_RA>(kimg, koff, qf, s);
     } else {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
@@ -681,30 +726,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp(const __bf16* __restrict__
   };
   auto pv = [&](const char* vimg, const uint32_t (&pf)[2][2][4], f32x16 (&oa)[ND]) __attribute__((always_inline)) {
     if constexpr (KFATT_FWD_RA > 0) {
-      // as qk: the two transposed V reads of MFMA i + RA issued before MFMA i
-      constexpr int RA = KFATT_FWD_RA, NM = 4 * ND;  // MFMA i: n = i / 4, t = (i / 2) & 1, s2 = i & 1
-      auto rd = [&](int i) __attribute__((always_inline)) {
-        const int n = i >> 2, t = (i >> 1) & 1, s2 = i & 1;
-        return join(tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff0[n]),
-                    tr_read(vimg + (32 * t + 16 * s2) * D * 2, voff1[n]));
-      };
-      bf16x8 vf[NM];
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        if (i == 0)
-#pragma unroll
-          for (int u = 0; u < RA; ++u) vf[u] = rd(u);
-        if (i + RA < NM) vf[i + RA] = rd(i + RA);
-        const int t = (i >> 1) & 1, s2 = i & 1;
-        const u32x4 pw = {pf[t][s2][0], pf[t][s2][1], pf[t][s2][2], pf[t][s2][3]};
-        oa[i >> 2] = mfma32(vf[i], __builtin_bit_cast(bf16x8, pw), oa[i >> 2]);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * RA, 0);
-#pragma unroll
-      for (int i = 0; i < NM; ++i) {
-        if (i + RA < NM) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
+      pv_ra<D, KFATT_FWD_RA>(vimg, voff0, voff1, pf, oa);
       return;
     }
 #pragma unroll

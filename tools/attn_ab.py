@@ -61,6 +61,8 @@ def _variants():
         "fra0": [*prod, "-DKFATT_FWD_RA=0"],  # attn_fwd_pp reads in the compiler's order
         "fra1": [*prod, "-DKFATT_FWD_RA=1"],
         "fra3": [*prod, "-DKFATT_FWD_RA=3"],
+        "f4ra1": [*prod, "-DKFATT_FWD4_RA=1"],  # attn_fwd (4 waves: D = 64, small grids) with pinned reads
+        "f4ra2": [*prod, "-DKFATT_FWD4_RA=2"],
         "dra1": [*prod, "-DKFATT_DQ_RA=1"],  # attn_bwd_dq_split (D = 128): reads pinned 1 MFMA ahead
         "dra2": [*prod, "-DKFATT_DQ_RA=2"],
         "bra1": [*prod, "-DKFATT_BWD_RA=1"],  # attn_bwd_dkdv8 (D = 128): reads pinned 1 MFMA ahead

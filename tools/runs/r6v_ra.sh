@@ -15,8 +15,8 @@ done
 set -- $VARS
 for r in 1 2 3; do
   for v in "$@"; do
-    KFAMD_KERNEL_LIB=$(lib $v) timeout -k 10 200 python -u tools/attn_bench.py --shapes 4x16x2048x128,2x32x4096x128 > $OUT/bench_${v}_$r.jsonl 2> $OUT/bench_${v}_$r.err || exit $?
-    KFAMD_KERNEL_LIB=$(lib $v) timeout -k 10 200 python -u tools/attn_bench.py --no-causal --shapes 4x16x2048x128 > $OUT/bench_nc${v}_$r.jsonl 2> $OUT/bench_nc${v}_$r.err || exit $?
+    KFAMD_KERNEL_LIB=$(lib $v) timeout -k 10 200 python -u tools/attn_bench.py --shapes ${SHAPES:-4x16x2048x128,2x32x4096x128} > $OUT/bench_${v}_$r.jsonl 2> $OUT/bench_${v}_$r.err || exit $?
+    KFAMD_KERNEL_LIB=$(lib $v) timeout -k 10 200 python -u tools/attn_bench.py --no-causal --shapes ${NCSHAPES:-4x16x2048x128} > $OUT/bench_nc${v}_$r.jsonl 2> $OUT/bench_nc${v}_$r.err || exit $?
   done
   set -- "${@:2}" "$1"   # rotate the order
 done
