@@ -10,11 +10,13 @@
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/epoll.h>
+#include <sys/ioctl.h>
 #include <sys/eventfd.h>
 #include <sys/syscall.h>
 #include <sys/un.h>
 #include <sys/wait.h>
 #include <unistd.h>
+#include <linux/fs.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -795,8 +797,10 @@ constexpr double kWarmOpRespawnS = 0.3;
 // (container_env: tenants never share writable code objects), so each namespace's first RCCL pod
 // paid it. The kubelet builds the entries once per node with its own readiness op (a trusted binary,
 // a clean env, GPU 0, at low priority) into a node directory outside every pod, and a namespace's
-// cache starts as hard links to them (entries are content-hashed and only ever added or removed,
-// never rewritten in place).
+// cache starts as reflink copies of them (copy-on-write: a tenant that rewrites an entry changes only
+// its own namespace's copy). Where the filesystem has no reflinks the entries are read-only hard
+// links instead. Process pods run under the kubelet's uid, so such a pod could still chmod and rewrite
+// a shared inode; comgr itself only adds and removes content-hashed entries, never rewrites them.
 std::string comgr_seed_dir() {
   if (const char* d = std::getenv("KFAMD_COMGR_SEED_DIR")) return d;
   const char* xdg = std::getenv("XDG_CACHE_HOME");
@@ -858,15 +862,36 @@ void Kubelet::finish_comgr_seed() {
   std::filesystem::remove_all(tmp, ec);
 }
 
-// a namespace's new code-object cache starts as hard links to the node's seed entries
+namespace {
+// dst as a copy-on-write clone of src (FICLONE); false where the filesystem cannot (ext4, tmpfs,
+// overlay, another device): the caller falls back
+bool reflink(const std::string& src, const std::string& dst) {
+  const int in = ::open(src.c_str(), O_RDONLY | O_CLOEXEC);
+  if (in < 0) return false;
+  const int out = ::open(dst.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+  bool ok = false;
+  if (out >= 0) {
+    ok = ::ioctl(out, FICLONE, in) == 0;
+    ::close(out);
+    if (!ok) ::unlink(dst.c_str());
+  }
+  ::close(in);
+  return ok;
+}
+}  // namespace
+
+// a namespace's new code-object cache starts as reflinks (else read-only hard links) of the node's
+// seed entries
 void Kubelet::link_comgr_seed(const std::string& cache_dir) {
   if (comgr_seed_.empty() || ::access((comgr_seed_ + "/.complete").c_str(), F_OK) != 0) return;
   std::error_code ec;
   for (std::filesystem::directory_iterator it(comgr_seed_, ec), end; !ec && it != end; it.increment(ec)) {
     const std::string name = it->path().filename().string();
     if (name.rfind("llvmcache-", 0) != 0) continue;
+    const std::string dst = cache_dir + "/" + name;
+    if (reflink(it->path().string(), dst)) continue;
     ::chmod(it->path().c_str(), 0444);
-    (void)::link(it->path().c_str(), (cache_dir + "/" + name).c_str());
+    (void)::link(it->path().c_str(), dst.c_str());
   }
 }
 

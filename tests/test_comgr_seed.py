@@ -2,8 +2,9 @@
 
 A GPU container's code-object cache is per namespace (AMD_COMGR_CACHE_DIR=<root>/gpu-cache/comgr/<ns>):
 tenants never share writable code objects. The kubelet builds RCCL's comgr entries once per host
-with its own readiness op (GPU nodes only) and a namespace's NEW cache starts as hard links to the
-completed seed's llvmcache-* entries (read-only), so the first RCCL communicator in a namespace does
+with its own readiness op (GPU nodes only) and a namespace's NEW cache starts as reflink (copy-on-write)
+copies of the completed seed's llvmcache-* entries, or read-only hard links where the filesystem has
+no reflinks, so the first RCCL communicator in a namespace does
 not pay the 3.8 s build (profiles/r6k_rccl_init). Here a completed seed is prepared by hand
 (KFAMD_COMGR_SEED_DIR) on a synthetic-GPU node; the build itself needs a GPU.
 """
@@ -60,11 +61,18 @@ def test_new_namespace_cache_starts_from_the_completed_seed(tmp_path):
         cache = got["CACHE"]
         assert cache.endswith("/gpu-cache/comgr/seed-a"), cache
         assert got["FILES"].split(",") == ["llvmcache-aaa", "llvmcache-bbb"], got
-        # hard links to the seed's entries, made read-only
-        for n in ("llvmcache-aaa", "llvmcache-bbb"):
-            st_seed, st_ns = os.stat(seed / n), os.stat(os.path.join(cache, n))
-            assert (st_seed.st_ino, st_seed.st_dev) == (st_ns.st_ino, st_ns.st_dev)
-            assert not st_ns.st_mode & 0o222
+        # reflink copies (own inode: a rewrite stays in this namespace) or, without reflinks,
+        # read-only hard links to the seed's entries
+        for n, body in (("llvmcache-aaa", b"entry-a"), ("llvmcache-bbb", b"entry-b")):
+            ns_path = os.path.join(cache, n)
+            st_seed, st_ns = os.stat(seed / n), os.stat(ns_path)
+            assert open(ns_path, "rb").read() == body
+            if (st_seed.st_ino, st_seed.st_dev) == (st_ns.st_ino, st_ns.st_dev):
+                assert not st_ns.st_mode & 0o222
+            else:
+                with open(ns_path, "wb") as f:
+                    f.write(b"rewritten-in-a")
+                assert (seed / n).read_bytes() == body
         # another tenant's namespace gets its own directory (same read-only entries, no shared dir)
         c.create(_pod("p2", "seed-b"))
         got_b = _wait_logs(c, "p2", "seed-b", "FILES")
