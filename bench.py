@@ -85,7 +85,7 @@ COLD_START_NOTE = ("process pods (no container runtime). cold_start_* = the prod
                    "= the torch server in a fresh interpreter (--pod-zygote=false); cold_start_odh_* = ODH path with "
                    "the OAuth proxy + reconciliation lock. The GPU readiness op runs as a native sidecar overlapping "
                    "the server start. *_failures = runs not Ready within the per-run timeout, with pod diagnostics "
-                   "in cold_start_failures")
+                   "in cold_start_failure_diagnostics")
 
 
 def _cs_keys(prefix: str, cs: dict) -> dict:
@@ -98,7 +98,8 @@ def _cs_keys(prefix: str, cs: dict) -> dict:
     if cs.get("truncated"):
         out[f"{prefix}_truncated"] = True
     if cs.get("failures"):
-        out.setdefault("cold_start_failures", {})[prefix] = cs["failures"]
+        # (not "<prefix>_failures": for the default path that is the count's own key)
+        out.setdefault("cold_start_failure_diagnostics", {})[prefix] = cs["failures"]
     return out
 
 
@@ -107,9 +108,9 @@ def run_cold_starts(ex, args, world: int) -> None:
     from kubeflow_rm_amd.bench_coldstart import measure_cold_start, measure_control_plane, measure_gpu_notebook_configs
 
     def merge_failures(e, out):
-        f = out.pop("cold_start_failures", None)
+        f = out.pop("cold_start_failure_diagnostics", None)
         if f:
-            e.data.setdefault("cold_start_failures", {}).update(f)
+            e.data.setdefault("cold_start_failure_diagnostics", {}).update(f)
         return out
 
     def default_path(e):

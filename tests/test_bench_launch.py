@@ -125,3 +125,17 @@ def test_bench_extras_skip_what_does_not_fit_the_budget():
     assert rep["x"] == 1 and "y" not in rep and "z" not in rep
     assert rep["extras_status"]["too_big"]["status"] == "skipped"
     assert rep["extras_status"]["peer_says_no"]["status"] == "skipped"
+
+
+def test_cold_start_failures_keep_their_count_and_diagnostics():
+    """The default path's prefix is ``cold_start``: its failure COUNT (``cold_start_failures``) must
+    not collide with the per-variant pod diagnostics (``cold_start_failure_diagnostics``)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    cs = {"runs": [0.1, 0.2], "p50_s": 0.1, "p90_s": 0.2, "failures": [{"pod": "bench/nb-3", "reason": "timeout"}]}
+    out = bench._cs_keys("cold_start", cs)
+    assert out["cold_start_failures"] == 1
+    assert out["cold_start_failure_diagnostics"] == {"cold_start": cs["failures"]}
+    out2 = bench._cs_keys("cold_start_odh", dict(cs, failures=[]))
+    assert out2["cold_start_odh_failures"] == 0 and "cold_start_failure_diagnostics" not in out2
