@@ -42,6 +42,7 @@ NetpolDecision evaluate_netpol(const std::vector<Json>& policies, const std::str
                                const std::string& port_name, const std::string& protocol, const NetpolSource& src);
 
 // "10.0.0.0/8" contains "10.1.2.3" (IPv4)
-bool cidr_contains(const std::string& cidr, const std::string& ip);
+bool cidr_contains(const std::string& cidr, const std::string& ip);  // false for a malformed CIDR
+bool cidr_valid(const std::string& cidr);
 
 }  // namespace kf

@@ -167,6 +167,21 @@ def test_netpol_evaluation_units(native):
     assert not d["allowed"] and d["isolated"] and d["policy"] == "p"
 
 
+def test_malformed_ip_blocks_fail_closed(native):
+    """A malformed ipBlock prefix matches nothing (it used to parse as /0 and admit every source),
+    and a malformed exception excludes its whole block."""
+    def ev(block, ip):
+        np_ = {"metadata": {"name": "p", "namespace": "a"},
+               "spec": {"podSelector": {}, "ingress": [{"from": [{"ipBlock": block}]}]}}
+        return native.call("evaluate_netpol", policies=[np_], namespace="a", pod_labels={"app": "nb"},
+                           port=80, port_name="", source={"ip": ip})["allowed"]
+    assert ev({"cidr": "10.0.0.0/8"}, "10.9.9.9") and ev({"cidr": "0.0.0.0/0"}, "192.168.1.1")
+    assert ev({"cidr": "10.1.2.3"}, "10.1.2.3") and not ev({"cidr": "10.1.2.3"}, "10.1.2.4")
+    for bad in ("10.0.0.0/x", "10.0.0.0/", "10.0.0.0/33", "10.0.0.0/-1", "nonsense/8", ""):
+        assert not ev({"cidr": bad}, "10.9.9.9"), bad
+    assert not ev({"cidr": "10.0.0.0/8", "except": ["10.1.0.0/zz"]}, "10.9.9.9")
+
+
 _ECHO = r"""
 import http.server, json
 class H(http.server.BaseHTTPRequestHandler):
