@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "core/util.h"
+#include "node/netpol.h"
 
 namespace kf {
 
@@ -19,16 +20,8 @@ bool istio_string_match(const std::string& pattern, const std::string& value) {
   return pattern == value;
 }
 
-bool ipv4_in_cidr(const std::string& ip, const std::string& cidr) {
-  const size_t slash = cidr.find('/');
-  const std::string net = cidr.substr(0, slash);
-  const int bits = slash == std::string::npos ? 32 : std::atoi(cidr.c_str() + slash + 1);
-  in_addr a{}, n{};
-  if (::inet_pton(AF_INET, ip.c_str(), &a) != 1 || ::inet_pton(AF_INET, net.c_str(), &n) != 1) return false;
-  if (bits <= 0) return true;
-  const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ~((1u << (32 - bits)) - 1);
-  return (ntohl(a.s_addr) & mask) == (ntohl(n.s_addr) & mask);
-}
+// one parser with the NetworkPolicy ipBlocks (netpol.cc): a malformed prefix matches nothing
+bool ipv4_in_cidr(const std::string& ip, const std::string& cidr) { return cidr_contains(cidr, ip); }
 
 std::string normalize_authz_path(const std::string& decoded_path) {
   std::string p = decoded_path;

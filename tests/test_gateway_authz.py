@@ -217,6 +217,29 @@ def test_policy_paths_are_normalized_like_istio_base():
     assert allowed("/public/admin")
 
 
+def test_policy_ip_blocks_parse_strictly():
+    """AuthorizationPolicy ipBlocks / notIpBlocks / source.ip conditions share the NetworkPolicy CIDR
+    parser: exact prefixes, bare addresses as /32, and a malformed prefix matching nothing (it used
+    to parse as /0 and match every source)."""
+    from kubeflow_rm_amd import native
+
+    def allowed(source, ip, when=None):
+        rule = {"from": [{"source": source}]} if source else {}
+        if when:
+            rule["when"] = when
+        pol = {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy",
+               "metadata": {"name": "ips", "namespace": "ns"}, "spec": {"action": "ALLOW", "rules": [rule]}}
+        return native.call("authz_evaluate", policies=[pol], namespace="ns", labels={},
+                           request={"path": "/", "method": "GET", "ip": ip})["allowed"]
+    assert allowed({"ipBlocks": ["10.0.0.0/8"]}, "10.2.3.4") and not allowed({"ipBlocks": ["10.0.0.0/8"]}, "11.2.3.4")
+    assert allowed({"ipBlocks": ["10.2.3.4"]}, "10.2.3.4") and not allowed({"ipBlocks": ["10.2.3.4"]}, "10.2.3.5")
+    assert allowed({"notIpBlocks": ["10.0.0.0/8"]}, "11.2.3.4") and not allowed({"notIpBlocks": ["10.0.0.0/8"]}, "10.2.3.4")
+    for bad in ("10.0.0.0/x", "10.0.0.0/40", "ten/8"):
+        assert not allowed({"ipBlocks": [bad]}, "10.2.3.4"), bad
+        assert not allowed(None, "10.2.3.4", when=[{"key": "source.ip", "values": [bad]}]), bad
+    assert allowed(None, "10.2.3.4", when=[{"key": "source.ip", "values": ["10.2.0.0/16"]}])
+
+
 def test_dot_segments_and_encoded_query_cannot_dodge_a_deny_rule(cl):
     c = cl.client
     pol = {"apiVersion": "security.istio.io/v1beta1", "kind": "AuthorizationPolicy",
