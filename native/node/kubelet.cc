@@ -25,6 +25,7 @@
 #include <fstream>
 #include <functional>
 #include <optional>
+#include <random>
 #include <regex>
 #include <set>
 
@@ -192,6 +193,14 @@ std::string comgr_seed_dir();
 
 Kubelet::Kubelet(std::shared_ptr<Client> c, KubeletConfig cfg) : c_(std::move(c)), cfg_(std::move(cfg)) {
   comgr_seed_ = comgr_seed_dir();  // set before any thread: pod workers read it (link_comgr_seed)
+  // pod addresses start at a random point of the 16-bit range: on a node without per-pod network
+  // namespaces, a process a previous kubelet on this host left behind (a test cluster stopped a
+  // moment ago) can still hold <addr>:<port>, and every instance counting from .0.2 would hand
+  // that address straight out again
+  {
+    std::random_device rd;
+    next_ip_ = 2 + rd() % 60000;
+  }
   GpuTopology topo = cfg_.gpus >= 0            ? GpuTopology::synthetic(cfg_.gpus)
                      : !cfg_.sysfs_root.empty() ? GpuTopology::discover(SysfsRoots::under(cfg_.sysfs_root))
                                                 : GpuTopology::discover();
@@ -1455,7 +1464,11 @@ std::shared_ptr<Kubelet::PodRuntime> Kubelet::admit(const Request& r, const Json
   make_dirs(rt->dir + "/rootfs");
   {
     std::lock_guard<std::mutex> g(mu_);
-    uint32_t n = next_ip_++;
+    uint32_t n;
+    do {  // (x.y.z.0 and .255 skipped; the range wraps)
+      n = next_ip_++;
+      if (next_ip_ >= 0xFFFF) next_ip_ = 2;
+    } while ((n & 0xFF) == 0 || (n & 0xFF) == 0xFF);
     rt->ip = cfg_.pod_ip_prefix + "." + std::to_string((n >> 8) & 0xFF) + "." + std::to_string(n & 0xFF);
     rt->app_ip = rt->ip;
   }
