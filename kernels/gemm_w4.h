@@ -383,8 +383,26 @@ void gemm_w4(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16*
   const int per_group = kGroupM * tiles_n;
   const int g = wg / per_group, first_m = g * kGroupM;
   const int gm = min(tiles_m - first_m, kGroupM);
-  const int tm = first_m + (wg % per_group) % gm;
-  const int tn = (wg % per_group) / gm;
+  int tm = first_m + (wg % per_group) % gm;
+  int tn = (wg % per_group) / gm;
+#ifndef KFW4_SUPER
+#define KFW4_SUPER 1  // 16 x 16-tile superblocks across the 8 XCDs for operands past the MALL (below)
+#endif
+  if constexpr (KFW4_SUPER && !GRP && BM == 256) {
+    // the chip's 256 resident tiles (one per CU) as ONE 16 x 16 block of the output: XCD x (block b
+    // runs on XCD b % 8) takes its 4 x 8 sub-block, rows 4 (x & 3), columns 8 (x >> 2); the waves walk
+    // the superblocks column-major. 16 A + 16 B panels are live at once instead of 32 A + 8 B with the
+    // per-XCD row groups (at 16384^3 a panel is 8 MiB: 256 vs 320 MiB against the 256 MiB MALL):
+    // 16384^3 0.987 -> 1.012 of hipBLASLt, 4096^3 / 8192^3 level (profiles/r6zm_super). Only where A
+    // and B together exceed the MALL; smaller problems keep the row groups.
+    if ((tiles_m & 15) == 0 && (tiles_n & 15) == 0 && gridDim.x == (unsigned)nwg &&  // (not the persistent grid)
+        (long long)(M + N) * K * 2 > (256LL << 20)) {
+      const int b = blockIdx.x, x = b & 7, i = b >> 3, wave = i >> 5, j = i & 31;
+      const int sbm = tiles_m >> 4, sr = wave % sbm, sc = wave / sbm;
+      tm = 16 * sr + 4 * (x & 3) + (j & 3);
+      tn = 16 * sc + 8 * (x >> 2) + (j >> 2);
+    }
+  }
   int m_lo = tm * BM, n_lo = tn * BN;                  // first output row / column this block stores
   int m0 = min(m_lo, M - BM), n0 = min(n_lo, N - BN);  // edge tiles shifted inside
 

@@ -48,6 +48,21 @@ def test_gemm_fast_path(M, N, K, variant):
     _assert_close(out, _ref_gemm(a, b), K)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 16448), (4096, 8192, 12288)])
+def test_gemm_superblock_raster_past_the_mall(M, N, K):
+    """Operands past 256 MiB take the 16 x 16-tile superblock raster (gemm_w4.h KFW4_SUPER): every
+    output tile written once, from the right A rows and B columns."""
+    from kubeflow_rm_amd.ops import gemm_nt
+    assert (M + N) * K * 2 > 256 << 20 and M % 4096 == 0 and N % 4096 == 0
+    a, b = _rand(M, K, seed=11), _rand(N, K, seed=12)
+    out = gemm_nt(a, b, variant="w4")
+    torch.cuda.synchronize()
+    rows = torch.arange(7, M, 61, device="cuda")  # rows in every 256-row tile row; all N columns
+    _assert_close(out.index_select(0, rows), _ref_gemm(a.index_select(0, rows), b), K)
+    cols = torch.arange(5, N, 53, device="cuda")
+    _assert_close(out.index_select(1, cols), _ref_gemm(a, b.index_select(0, cols)), K)
+
+
 def test_gemm_identity_asymmetric():
     """A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
     from kubeflow_rm_amd.ops import gemm_nt

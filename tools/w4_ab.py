@@ -48,6 +48,8 @@ VARIANTS = {
     "phase3": ["-DKFW4_DMA_PHASE=3"],
     "gm32": ["-DKFW4_GROUP_M=32"],
     "rg4gm16": ["-DKFW4_RG=4", "-DKFW4_GROUP_M=16"],
+    "nosuper": ["-DKFW4_SUPER=0"],  # the per-XCD row groups at every size (before r6zm_super)
+    "rg4super": ["-DKFW4_RG=4"],
 }
 
 
