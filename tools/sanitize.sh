@@ -11,7 +11,7 @@ OUT=${1:-profiles/r1_sanitizers}
 mkdir -p "$OUT"
 # every suite that drives the native control plane concurrently (the prober pool,
 # the TokenReview cache, the mesh listener, kubectl create/patch/apply and the split binaries too)
-SUITES="tests/test_comgr_seed.py tests/test_pod_network_isolation.py tests/test_resource_validation.py tests/test_crd_schemas.py tests/test_zygote.py tests/test_kubectl_cli.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py tests/test_kubelet_probes.py tests/test_gateway_authz.py tests/test_kubectl_mutate.py tests/test_kubectl_apply.py tests/test_split_binaries.py tests/test_tls.py"
+SUITES="tests/test_pod_addresses.py tests/test_comgr_seed.py tests/test_pod_network_isolation.py tests/test_resource_validation.py tests/test_crd_schemas.py tests/test_zygote.py tests/test_kubectl_cli.py tests/test_e2e_controlplane.py tests/test_odh.py tests/test_e2e_tensorboard_pvcviewer.py tests/test_loadtest.py tests/test_kfam.py tests/test_apiserver.py tests/test_e2e_telemetry.py tests/test_e2e_multigpu.py tests/test_resilience.py tests/test_kubelet_probes.py tests/test_gateway_authz.py tests/test_kubectl_mutate.py tests/test_kubectl_apply.py tests/test_split_binaries.py tests/test_tls.py"
 rc=0
 for san in thread address; do
   python -c "from kubeflow_rm_amd import _build; _build.build_native(sanitize='$san', build_type='RelWithDebInfo')" \
