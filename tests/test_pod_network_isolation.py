@@ -167,6 +167,31 @@ def test_netpol_evaluation_units(native):
     assert not d["allowed"] and d["isolated"] and d["policy"] == "p"
 
 
+def test_netpol_ports_policy_types_and_selectors(native):
+    """NetworkPolicy semantics beyond the ODH policies: port ranges (endPort), the protocol, an
+    Egress-only policy (does not isolate ingress), an empty ingress list (deny all), and an empty
+    namespaceSelector (every namespace, pods only)."""
+    def ev(spec, port, src, protocol="TCP"):
+        np_ = {"metadata": {"name": "p", "namespace": "a"}, "spec": {"podSelector": {}, **spec}}
+        return native.call("evaluate_netpol", policies=[np_], namespace="a", pod_labels={"app": "nb"},
+                           port=port, port_name="", protocol=protocol, source=src)
+    pod_b = {"pod": True, "ns": "b", "pod_labels": {}, "ns_labels": {}}
+    ranged = {"ingress": [{"ports": [{"port": 8000, "endPort": 8010}]}]}
+    assert ev(ranged, 8000, pod_b)["allowed"] and ev(ranged, 8010, pod_b)["allowed"]
+    assert not ev(ranged, 8011, pod_b)["allowed"] and not ev(ranged, 7999, pod_b)["allowed"]
+    udp = {"ingress": [{"ports": [{"port": 53, "protocol": "UDP"}]}]}
+    assert not ev(udp, 53, pod_b)["allowed"]  # a TCP connection is not a UDP rule's
+    egress_only = {"policyTypes": ["Egress"], "egress": []}
+    d = ev(egress_only, 8888, pod_b)
+    assert d["allowed"] and not d["isolated"]
+    deny_all = {"policyTypes": ["Ingress"], "ingress": []}
+    d = ev(deny_all, 8888, pod_b)
+    assert not d["allowed"] and d["isolated"]
+    any_ns = {"ingress": [{"from": [{"namespaceSelector": {}}]}]}
+    assert ev(any_ns, 8888, pod_b)["allowed"]
+    assert not ev(any_ns, 8888, {"ip": "10.0.0.1"})["allowed"]  # selectors never match a bare address
+
+
 def test_malformed_ip_blocks_fail_closed(native):
     """A malformed ipBlock prefix matches nothing (it used to parse as /0 and admit every source),
     and a malformed exception excludes its whole block."""
